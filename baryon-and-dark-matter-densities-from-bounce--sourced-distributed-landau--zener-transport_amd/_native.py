@@ -1,0 +1,109 @@
+"""ctypes binding of the lzq C ABI (include/lzq.h) -> `_build/liblzq.so`.
+
+There is no fallback: if the HIP library is missing or fails to load, every entry point
+raises.  Structures mirror include/lzq.h field for field (sizes are asserted).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import build as _build
+
+LIB_PATH = _build.LIB_PATH
+
+# ---- struct mirrors of include/lzq.h ---------------------------------------------------
+POINT_DOUBLE_FIELDS = (
+    "m_chi_GeV", "g_chi", "T_p_GeV", "beta_over_H", "v_w", "I_p", "g_star", "g_star_s",
+    "P_chi_to_B", "source_shape_sigma_y", "incident_flux_scale", "T_max_over_Tp",
+    "T_min_over_Tp", "Y_chi_init", "n_chi_at_Tp_GeV3")
+POINT_INT_FIELDS = ("stats", "regime", "has_Y_chi_init", "has_n_chi_at_Tp")
+YIELD_FIELDS = ("Y_B", "Y_chi", "rho_B_kg_m3", "rho_DM_kg_m3", "DM_over_B", "P_used")
+
+
+class LzqPoint(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in POINT_DOUBLE_FIELDS] + \
+               [(n, ctypes.c_int32) for n in POINT_INT_FIELDS]
+
+
+class LzqYield(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in YIELD_FIELDS]
+
+
+class LzqAxis(ctypes.Structure):
+    _fields_ = [("field", ctypes.c_int32), ("n", ctypes.c_int32), ("values", ctypes.c_void_p)]
+
+
+POINT_DTYPE = np.dtype([(n, "<f8") for n in POINT_DOUBLE_FIELDS] + [(n, "<i4") for n in POINT_INT_FIELDS])
+assert ctypes.sizeof(LzqPoint) == 136 == POINT_DTYPE.itemsize
+assert ctypes.sizeof(LzqYield) == 48
+
+# enum lzq_field
+FIELD = {n: i for i, n in enumerate(POINT_DOUBLE_FIELDS)}
+FIELD.update({"delta_LZ": 32, "m_mix": 33, "dprime": 34})
+FERMION, BOSON = 0, 1
+THERMAL, NONTHERMAL, REGIME_OTHER = 0, 1, 2
+LZQ_NZ = 1200
+LZQ_MAX_AXES = 8
+
+# Symbols declared in include/lzq.h (checked by tests/test_capi.py against the header).
+EXPORTS = ("lzq_abi_version", "lzq_last_error", "lzq_init", "lzq_ztables", "lzq_aov_batch",
+           "lzq_jchi_batch", "lzq_yields_batch", "lzq_sweep_grid", "lzq_p_closed_form",
+           "lzq_lz_propagate")
+
+
+class LzqError(RuntimeError):
+    """A negative status from the C ABI (message from lzq_last_error())."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"lzq error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def load(path: str | None = None):
+    """Load liblzq.so (does not touch the GPU).  Raises if the library is absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(f"lzq HIP library not built ({p}); run __graft_entry__.build() "
+                           "or python -m <package>.build")
+    L = ctypes.CDLL(p)
+    i32, i64, d, vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
+    P = ctypes.POINTER
+    L.lzq_abi_version.restype = ctypes.c_int
+    L.lzq_last_error.restype = ctypes.c_char_p
+    L.lzq_init.argtypes = [ctypes.c_int]
+    L.lzq_ztables.argtypes = [P(d), P(d), P(d)]
+    L.lzq_aov_batch.argtypes = [P(LzqPoint), vp, i64, vp, vp]
+    L.lzq_jchi_batch.argtypes = [P(LzqPoint), vp, i64, vp, vp]
+    L.lzq_yields_batch.argtypes = [vp, i64, i32, vp, vp, vp, vp, vp]
+    L.lzq_sweep_grid.argtypes = [P(LzqPoint), P(LzqAxis), i32, i64, i64, i32, vp, vp]
+    L.lzq_p_closed_form.argtypes = [vp, i64, vp, vp]
+    L.lzq_lz_propagate.argtypes = [vp, vp, vp, i64, i32, d, d, i32, vp, vp]
+    for name in EXPORTS:
+        if name not in ("lzq_abi_version", "lzq_last_error"):
+            getattr(L, name).restype = ctypes.c_int
+    if path is None:
+        _lib = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = load().lzq_last_error()
+        raise LzqError(rc, msg.decode() if msg else "")
+
+
+def ztables() -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Host copies of the z grid, gamma4 and the quadrature weights built by the library."""
+    z, g4, om = (np.empty(LZQ_NZ) for _ in range(3))
+    dp = ctypes.POINTER(ctypes.c_double)
+    check(load().lzq_ztables(z.ctypes.data_as(dp), g4.ctypes.data_as(dp), om.ctypes.data_as(dp)))
+    return z, g4, om

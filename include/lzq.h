@@ -1,0 +1,153 @@
+/*
+ * lzq.h -- C ABI of the MI355X-native bounce-sourced Landau-Zener yield engine.
+ *
+ * Drop-in boundary for the hot path of /root/reference/first_principles_yields.py ("fpy"):
+ *
+ *   fpy:141-165  AoverVKernel / A_over_V_y           -> lzq_aov_batch
+ *   fpy:231-267  integrate_YB_by_quadrature           -> lzq_yields_batch (out->Y_B), lzq_sweep_grid
+ *   fpy:372-384, fpy:413-417  Y_chi + densities        -> lzq_yields_batch / lzq_sweep_grid epilogue
+ *   fpy:170-187  LZ plug-in closed form (fpy:183-184)  -> lzq_p_closed_form
+ *   fpy:222-223 + fpy:122-123  J_chi (diagnostics)     -> lzq_jchi_batch
+ *   (no reference counterpart; north_star (1))        -> lzq_lz_propagate
+ *
+ * Conventions (all entry points):
+ *   - plain C types only; device buffers are raw device pointers, `stream` is a hipStream_t
+ *     passed as void* (NULL = the null stream) and must belong to the current HIP device;
+ *   - the caller owns every buffer; the library never frees caller memory; launches are
+ *     asynchronous on `stream` (no host synchronisation inside the launch functions once
+ *     lzq_init has run for the device);
+ *   - return 0 on success, a negative LZQ_E* code on failure; lzq_last_error() returns a
+ *     thread-local message for the last failure on the calling thread; no C++ exception
+ *     crosses the boundary;
+ *   - results are deterministic: each point is reduced by one wavefront in a fixed order, so
+ *     they do not depend on launch geometry, batch composition or the number of GPUs.
+ */
+#ifndef LZQ_H
+#define LZQ_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LZQ_ABI_VERSION 1
+#define LZQ_NZ 1200          /* fpy:142 nz default, used unchanged at fpy:197 */
+#define LZQ_Z_MAX 30.0       /* fpy:142 z_max default */
+#define LZQ_NY_MAIN 8000     /* fpy:374 */
+#define LZQ_NY_MIN 2000      /* fpy:246 */
+
+enum lzq_status {
+  LZQ_OK = 0,
+  LZQ_EINVAL = -1,       /* bad argument (null pointer, n < 0, unknown field, ...)        */
+  LZQ_EHIP = -2,         /* a HIP runtime call failed (message has the HIP error string)  */
+  LZQ_EUNSUPPORTED = -3, /* configuration outside the fast quadrature path (fpy:372)       */
+  LZQ_ENODEVICE = -4
+};
+
+/* chi statistics (fpy:96: str(stats).lower().startswith("ferm")) */
+enum lzq_stats { LZQ_FERMION = 0, LZQ_BOSON = 1 };
+/* regime (fpy:376-384); LZQ_REGIME_OTHER ("auto") has no branch in the reference, which
+ * raises UnboundLocalError; the engine returns NaN yields for such points. */
+enum lzq_regime { LZQ_THERMAL = 0, LZQ_NONTHERMAL = 1, LZQ_REGIME_OTHER = 2 };
+
+/* One parameter point: the fpy `Config` fields (fpy:44-79) read by the fast path.
+ * Optional[float] fields carry has_* flags.  136 bytes, 8-byte aligned. */
+typedef struct lzq_point {
+  double m_chi_GeV;            /* field  0 */
+  double g_chi;                /* field  1 (int in fpy; used as a float factor) */
+  double T_p_GeV;              /* field  2 */
+  double beta_over_H;          /* field  3 */
+  double v_w;                  /* field  4 */
+  double I_p;                  /* field  5 */
+  double g_star;               /* field  6 */
+  double g_star_s;             /* field  7 */
+  double P_chi_to_B;           /* field  8 */
+  double source_shape_sigma_y; /* field  9 */
+  double incident_flux_scale;  /* field 10 */
+  double T_max_over_Tp;        /* field 11 */
+  double T_min_over_Tp;        /* field 12 */
+  double Y_chi_init;           /* field 13 (valid iff has_Y_chi_init) */
+  double n_chi_at_Tp_GeV3;     /* field 14 (valid iff has_n_chi_at_Tp) */
+  int32_t stats;               /* enum lzq_stats  */
+  int32_t regime;              /* enum lzq_regime */
+  int32_t has_Y_chi_init;
+  int32_t has_n_chi_at_Tp;
+} lzq_point;
+
+/* Per-point yield record: the `final` block of yields_out.json (fpy:425-427) + P_used
+ * (fpy:424).  48 bytes; tables of these are what the multi-GPU all-gather moves. */
+typedef struct lzq_yield {
+  double Y_B, Y_chi, rho_B_kg_m3, rho_DM_kg_m3, DM_over_B, P_used;
+} lzq_yield;
+
+/* Sweep axis fields.  0..14 address the double fields of lzq_point in declaration order.
+ * Derived LZ fields set P_chi_to_B through the closed form (fpy:183-184, PAPER eq.(9)):
+ *   LZQ_F_DELTA_LZ           : P = clamp(1 - exp(-2 pi max(delta, 0)), 0, 1)
+ *   LZQ_F_M_MIX, LZQ_F_DPRIME: delta = m_mix^2 / (2 max(v_w,1e-12) |Delta'|) (PAPER eq.(8), F = 1)
+ * Axis values live in device memory. */
+enum lzq_field {
+  LZQ_F_M_CHI = 0, LZQ_F_G_CHI = 1, LZQ_F_T_P = 2, LZQ_F_BETA_OVER_H = 3, LZQ_F_V_W = 4,
+  LZQ_F_I_P = 5, LZQ_F_G_STAR = 6, LZQ_F_G_STAR_S = 7, LZQ_F_P = 8, LZQ_F_SIGMA_Y = 9,
+  LZQ_F_FLUX = 10, LZQ_F_T_MAX_OVER_TP = 11, LZQ_F_T_MIN_OVER_TP = 12, LZQ_F_Y_CHI_INIT = 13,
+  LZQ_F_N_CHI_AT_TP = 14,
+  LZQ_F_DELTA_LZ = 32, LZQ_F_M_MIX = 33, LZQ_F_DPRIME = 34
+};
+
+#define LZQ_MAX_AXES 8
+typedef struct lzq_axis {
+  int32_t field;          /* enum lzq_field */
+  int32_t n;              /* number of values (> 0) */
+  const double* values;   /* device pointer, n doubles */
+} lzq_axis;
+
+/* ---- library / device management ---------------------------------------------------- */
+int lzq_abi_version(void);
+const char* lzq_last_error(void);
+/* Builds and uploads the point-invariant z tables (fpy:154-156) for `device`.  Called
+ * lazily by every entry point; call it up front before capturing launches into a graph. */
+int lzq_init(int device);
+/* Host copies of the z tables: z (fpy:154), gamma4 (fpy:156) and the quadrature weights
+ * omega_k = z_k^2 e^{-z_k} * (trapezoid weight of node k).  Each array has LZQ_NZ entries. */
+int lzq_ztables(double* z, double* gamma4, double* omega);
+
+/* ---- hot path -------------------------------------------------------------------------- */
+/* fpy:158-165: out[i] = A_over_V_y(y[i]) for the kernel of point *pt (host struct). */
+int lzq_aov_batch(const lzq_point* pt, const double* d_y, int64_t n, double* d_out, void* stream);
+
+/* fpy:222-223: out[i] = BoltzmannSystem.J_chi(T[i]) for point *pt (diagnostics table). */
+int lzq_jchi_batch(const lzq_point* pt, const double* d_T, int64_t n, double* d_out, void* stream);
+
+/* fpy:231-267 + fpy:372-384 + fpy:413-417 for n explicit points (device AoS array).
+ * d_T_lo / d_T_hi: optional per-point integration range (NULL: main()'s
+ * T_lo = T_min_over_Tp*T_p, T_hi = T_max_over_Tp*T_p, fpy:367-369).
+ * d_P: optional per-point P override (NULL: point.P_chi_to_B), e.g. lzq_lz_propagate output.
+ * n_y: y-grid size as passed to integrate_YB_by_quadrature (fpy:374 uses 8000; raised to
+ * LZQ_NY_MIN as fpy:246). */
+int lzq_yields_batch(const lzq_point* d_points, int64_t n, int32_t n_y,
+                     const double* d_T_lo, const double* d_T_hi, const double* d_P,
+                     lzq_yield* d_out, void* stream);
+
+/* Cartesian sweep: points [start, start+count) of the grid base x axes[0] x ... x
+ * axes[n_axes-1] (C order: last axis fastest), generated on device from the flat index. */
+int lzq_sweep_grid(const lzq_point* base, const lzq_axis* axes, int32_t n_axes,
+                   int64_t start, int64_t count, int32_t n_y, lzq_yield* d_out, void* stream);
+
+/* fpy:183-184: P[i] = clamp(1 - exp(-2 pi max(lambda[i], 0)), 0, 1) (naive 1-exp kept). */
+int lzq_p_closed_form(const double* d_lambda, int64_t n, double* d_P, void* stream);
+
+/* ---- Landau-Zener propagator (north_star (1); no reference counterpart) --------------- */
+/* Coherent two-level propagation through n_cross sequential linear avoided crossings per
+ * point, i dpsi/dt = H(t) psi, H = [[D(t), m],[m, -D(t)]], D piecewise linear with slope
+ * v_w*Delta'_c near crossing c.  See DESIGN.md "LZ propagator" for the profile, the Magnus
+ * integrator and its stated tolerance.  d_m_mix / d_dprime: [n][n_cross] row-major;
+ * d_xi: [n][n_cross] crossing positions; out d_P[n] = conversion probability
+ * 1 - |<diabatic chi|psi(+inf)>|^2. */
+int lzq_lz_propagate(const double* d_m_mix, const double* d_dprime, const double* d_xi,
+                     int64_t n, int32_t n_cross, double v_w, double xi_half_window,
+                     int32_t steps_per_crossing, double* d_P, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LZQ_H */

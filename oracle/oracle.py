@@ -1,0 +1,129 @@
+"""ctypes front-end of the CPU oracle (oracle/lzq_oracle.c).
+
+TEST INFRASTRUCTURE ONLY.  Importable only from tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, and there only as the checker / the timed CPU baseline.
+The product (the HIP library + package host code) never imports this module.
+
+The C code restates /root/reference/first_principles_yields.py (fpy) verbatim; see the
+per-function citations in lzq_oracle.c.  Pinned by tests/test_oracle_golden.py.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liblzq_oracle.so")
+
+
+class OraclePoint(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in (
+        "m_chi_GeV", "g_chi", "T_p_GeV", "beta_over_H", "v_w", "I_p", "g_star", "g_star_s",
+        "P_chi_to_B", "source_shape_sigma_y", "incident_flux_scale",
+        "T_max_over_Tp", "T_min_over_Tp", "Y_chi_init", "n_chi_at_Tp_GeV3")] + [
+        (n, ctypes.c_int32) for n in ("stats", "regime", "has_Y_chi_init", "has_n_chi_at_Tp")]
+
+
+YIELD_FIELDS = ("Y_B", "Y_chi", "rho_B_kg_m3", "rho_DM_kg_m3", "DM_over_B", "P_used")
+
+
+class OracleYield(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in YIELD_FIELDS]
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        d, i32, i64 = ctypes.c_double, ctypes.c_int32, ctypes.c_int64
+        P = ctypes.POINTER
+        L.oracle_aov.restype = d
+        L.oracle_aov.argtypes = [d, d, d, d, d, d]
+        L.oracle_yb_quadrature.restype = d
+        L.oracle_yb_quadrature.argtypes = [P(OraclePoint), d, d, i32]
+        L.oracle_point_yields.restype = ctypes.c_int
+        L.oracle_point_yields.argtypes = [P(OraclePoint), P(OracleYield)]
+        L.oracle_points_batch.restype = i64
+        L.oracle_points_batch.argtypes = [P(OraclePoint), i64, P(OracleYield), i32]
+        L.oracle_p_closed_form.restype = d
+        L.oracle_p_closed_form.argtypes = [d]
+        L.oracle_j_chi.restype = d
+        L.oracle_j_chi.argtypes = [P(OraclePoint), d]
+        L.oracle_pairwise_sum.restype = d
+        L.oracle_pairwise_sum.argtypes = [P(d), i64]
+        L.oracle_linspace.restype = None
+        L.oracle_linspace.argtypes = [d, d, i64, P(d)]
+        _lib = L
+    return _lib
+
+
+def point_from_config(cfg: dict) -> OraclePoint:
+    """Config dict (fpy schema, defaults already applied) -> OraclePoint."""
+    p = OraclePoint()
+    for n in ("m_chi_GeV", "g_chi", "T_p_GeV", "beta_over_H", "v_w", "I_p", "g_star", "g_star_s",
+              "source_shape_sigma_y", "incident_flux_scale", "T_max_over_Tp", "T_min_over_Tp"):
+        setattr(p, n, float(cfg[n]))
+    p.P_chi_to_B = float(cfg["P_chi_to_B"])
+    p.stats = 0 if str(cfg["chi_stats"]).lower().startswith("ferm") else 1
+    r = str(cfg["regime"]).lower()
+    p.regime = 0 if r.startswith("therm") else (1 if r.startswith("non") else 2)
+    p.has_Y_chi_init = int(cfg["Y_chi_init"] is not None)
+    p.Y_chi_init = float(cfg["Y_chi_init"]) if cfg["Y_chi_init"] is not None else 0.0
+    p.has_n_chi_at_Tp = int(cfg["n_chi_at_Tp_GeV3"] is not None)
+    p.n_chi_at_Tp_GeV3 = float(cfg["n_chi_at_Tp_GeV3"]) if cfg["n_chi_at_Tp_GeV3"] is not None else 0.0
+    return p
+
+
+def point_yields(cfg: dict) -> dict:
+    p = point_from_config(cfg)
+    o = OracleYield()
+    rc = lib().oracle_point_yields(ctypes.byref(p), ctypes.byref(o))
+    if rc != 0:
+        raise UnboundLocalError("local variable 'Ychi_fin' referenced before assignment")
+    return {n: getattr(o, n) for n in YIELD_FIELDS}
+
+
+def points_batch(cfgs: list[dict], nthreads: int = 0) -> np.ndarray:
+    """Returns an (n, 6) float64 array in YIELD_FIELDS order (NaN rows for failed points)."""
+    n = len(cfgs)
+    arr = (OraclePoint * n)(*[point_from_config(c) for c in cfgs])
+    out = (OracleYield * n)()
+    lib().oracle_points_batch(arr, n, out, int(nthreads))
+    return np.frombuffer(out, dtype=np.float64).reshape(n, 6).copy()
+
+
+def aov(I_p, beta_over_H, T_p, v_w, g_star, y) -> float:
+    return lib().oracle_aov(I_p, beta_over_H, T_p, v_w, g_star, y)
+
+
+def p_closed_form(lam: float) -> float:
+    return lib().oracle_p_closed_form(lam)
+
+
+def j_chi(cfg: dict, T: float) -> float:
+    p = point_from_config(cfg)
+    return lib().oracle_j_chi(ctypes.byref(p), T)
+
+
+def pairwise_sum(a) -> float:
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    return lib().oracle_pairwise_sum(a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), a.size)
+
+
+def linspace(start, stop, num) -> np.ndarray:
+    out = np.empty(num, dtype=np.float64)
+    lib().oracle_linspace(start, stop, num, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    return out

@@ -1,0 +1,81 @@
+"""The C-ABI library loads, exports exactly what include/lzq.h declares, and validates
+arguments on the host (these calls return before any GPU work, so they run on CPU)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+
+from conftest import ROOT, pkg
+
+
+def header_symbols():
+    with open(os.path.join(ROOT, "include", "lzq.h")) as f:
+        src = f.read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(lzq_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_builds_and_exports_header_symbols():
+    path = pkg("build").build()
+    assert os.path.exists(path)
+    L = ctypes.CDLL(path)
+    syms = header_symbols()
+    assert len(syms) >= 10
+    for s in syms:
+        assert hasattr(L, s), s
+    assert sorted(pkg("_native").EXPORTS) == syms
+
+
+def test_abi_version_and_struct_layout():
+    n = pkg("_native")
+    L = n.load()
+    assert L.lzq_abi_version() == 1
+    assert ctypes.sizeof(n.LzqPoint) == 136 and ctypes.sizeof(n.LzqYield) == 48
+
+
+def test_ztables_match_reference_grid():
+    """fpy:154-156: z = linspace(0,30,1200), g4 verbatim; omega sums to int z^2 e^-z = 2."""
+    z, g4, om = pkg("_native").ztables()
+    assert np.array_equal(z, np.linspace(0.0, 30.0, 1200))
+    ez = np.exp(-z)
+    g4_np = 6.0 - ez * (z ** 3 + 3.0 * z ** 2 + 6.0 * z + 6.0)
+    # numpy's AVX-512 exp differs from libm by 1 ulp on a few nodes
+    assert np.max(np.abs(g4 - g4_np)) < 8 * np.finfo(float).eps
+    assert np.all(g4 >= 0.0)
+    assert abs(om.sum() - 2.0) < 1e-8
+
+
+def test_host_side_argument_validation():
+    n = pkg("_native")
+    L = n.load()
+    rc = L.lzq_yields_batch(None, -1, 8000, None, None, None, None, None)
+    assert rc == -1 and b"bad arguments" in L.lzq_last_error()
+    rc = L.lzq_p_closed_form(None, 0, None, None)  # n == 0 is a no-op
+    assert rc == 0
+    rc = L.lzq_lz_propagate(None, None, None, 4, 0, 0.3, 1.0, 10, None, None)
+    assert rc == -1
+    cfgm = pkg("config")
+    base = cfgm.to_ctypes_point(cfgm.to_point({**cfgm.default_config(), "P_chi_to_B": 0.1}))
+    ax = (n.LzqAxis * 1)()
+    ax[0].field, ax[0].n, ax[0].values = 99, 3, 8
+    rc = L.lzq_sweep_grid(ctypes.byref(base), ax, 1, 0, 1, 8000, 8, None)
+    assert rc == -1 and b"unknown field" in L.lzq_last_error()
+    ax[0].field = n.FIELD["m_mix"]
+    rc = L.lzq_sweep_grid(ctypes.byref(base), ax, 1, 0, 1, 8000, 8, None)
+    assert rc == -1 and b"swept together" in L.lzq_last_error()
+    ax[0].field = n.FIELD["I_p"]
+    rc = L.lzq_sweep_grid(ctypes.byref(base), ax, 1, 2, 5, 8000, 8, None)
+    assert rc == -1 and b"outside grid" in L.lzq_last_error()
+    base.regime = n.REGIME_OTHER
+    rc = L.lzq_sweep_grid(ctypes.byref(base), ax, 1, 0, 1, 8000, 8, None)
+    assert rc == -3
+
+
+def test_engine_refuses_without_gpu():
+    import pytest
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        pkg("engine").Engine()

@@ -1,0 +1,76 @@
+"""Grid sweeps on the GPU: on-device point generation vs explicit points, sharded launches
+bit-identical to one launch (the multi-GPU invariant), and the separability identities of
+SURVEY §8c at full grid sizes (size-independent properties)."""
+import numpy as np
+import pytest
+
+from conftest import BASE_CFG, full_cfg, pkg, rel_err
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def c2_axes(n_mix=1000, n_dp=1000):
+    return [("m_mix", np.logspace(-3, 0, n_mix)), ("dprime", np.logspace(-3, 1, n_dp))]
+
+
+def test_grid_matches_explicit_points(gpu_engine):
+    axes = [("m_chi_GeV", np.logspace(0, 3.5, 5)), ("I_p", np.linspace(0.05, 1, 3)),
+            ("delta_LZ", np.logspace(-4, 0, 4))]
+    t = gpu_engine.sweep(full_cfg(BASE_CFG), axes, 0, 60).cpu().numpy()
+    cfgm = pkg("config")
+    cfgs = []
+    for m in axes[0][1]:
+        for ip in axes[1][1]:
+            for dl in axes[2][1]:
+                P = O.p_closed_form(float(dl))
+                cfgs.append(full_cfg({**BASE_CFG, "m_chi_GeV": float(m), "I_p": float(ip), "P_chi_to_B": P}))
+    e = gpu_engine.yields(np.concatenate([cfgm.to_point(c) for c in cfgs])).cpu().numpy()
+    assert np.array_equal(t, e)
+    ref = O.points_batch(cfgs, nthreads=16)
+    assert max(rel_err(a, b) for a, b in zip(t.ravel(), ref.ravel())) < 1e-11
+
+
+def test_shards_bit_identical(gpu_engine):
+    axes = c2_axes(16, 16)
+    full = gpu_engine.sweep(full_cfg(BASE_CFG), axes, 0, 256).cpu().numpy()
+    for W in (2, 4, 8):
+        parts = [gpu_engine.sweep(full_cfg(BASE_CFG), axes, r * 256 // W, (r + 1) * 256 // W - r * 256 // W).cpu().numpy()
+                 for r in range(W)]
+        assert np.array_equal(np.concatenate(parts), full)
+
+
+def test_c2_full_grid_separability(gpu_engine):
+    """Full 1e6-point C2 grid: Y_B / P_used is the same quadrature for every point
+    (Y_B is linear in P, PAPER §8), and P_used follows eq.(8)-(9)."""
+    axes = c2_axes()
+    t = gpu_engine.sweep(full_cfg(BASE_CFG), axes, 0, 1_000_000).cpu().numpy()
+    P = t[:, 5]
+    ok = P > 1e-6
+    ratio = t[ok, 0] / P[ok]
+    assert np.max(np.abs(ratio / ratio[0] - 1)) < 1e-14
+    m, d = np.meshgrid(axes[0][1], axes[1][1], indexing="ij")
+    delta = (m * m / (2.0 * 0.3 * d)).ravel()
+    assert np.allclose(P, 1.0 - np.exp(-2.0 * np.pi * delta), rtol=1e-13, atol=1e-16)
+    YB1 = 8.720885362714675e-11 / 0.14925839040304145
+    assert rel_err(ratio[0], YB1) < 1e-11
+
+
+def test_known_answer_identities(gpu_engine):
+    """SURVEY §8c identities, exact to ~1e-15 in the reference."""
+    base = full_cfg(BASE_CFG)
+    variants = [base, {**base, "P_chi_to_B": 2 * base["P_chi_to_B"]},
+                {**base, "incident_flux_scale": 3 * base["incident_flux_scale"]}, {**base, "v_w": 0.15},
+                {**base, "T_p_GeV": 10.0}, {**base, "T_p_GeV": 1000.0}, {**base, "beta_over_H": 50.0},
+                {**base, "chi_stats": "boson"}, {**base, "m_chi_GeV": 50.0}, {**base, "T_min_over_Tp": 6.0}]
+    cfgm = pkg("config")
+    t = gpu_engine.yields(np.concatenate([cfgm.to_point(c) for c in variants])).cpu().numpy()[:, 0]
+    y0 = t[0]
+    assert rel_err(t[1], 2 * y0) < 1e-14
+    assert rel_err(t[2], 3 * y0) < 1e-14
+    assert rel_err(t[3], 2 * y0) < 1e-13
+    assert rel_err(t[4], y0) < 1e-12 and rel_err(t[5], y0) < 1e-12
+    assert rel_err(t[6], y0) < 1e-12
+    assert rel_err(t[7], 4.0 / 3.0 * y0) < 1e-14
+    assert rel_err(t[8], y0) < 1e-14
+    assert t[9] == 0.0

@@ -1,0 +1,275 @@
+"""Parameter-sweep driver (north_star (3); the reference has no sweep code).
+
+A sweep = a base config in the reference schema (fpy:44-79) x up to 8 Cartesian axes,
+flattened in C order (last axis fastest).  Points are generated ON DEVICE from the flat
+index (lzq_sweep_grid), so no parameter table ever crosses PCIe.
+
+Multi-GPU: one process per GPU; rank r owns the contiguous shard
+[r*N//W, (r+1)*N//W) and evaluates it with no communication; one all-gather of the 48-B
+per-point yield records (RCCL over xGMI on GPUs, gloo in CPU tests) assembles the table on
+every rank.  Each point is reduced by one wavefront, so the gathered table is bit-identical
+for W = 1, 2, 4, 8.  Grid-wide statistics are reduced on the host in index order.
+
+Checkpoint/resume: with --out, every evaluated chunk is written as
+`shard_<start>_<count>.npy` (allow_pickle=False); --resume reloads existing chunks instead
+of recomputing them, so a killed 1e8-point run restarts where it stopped.
+
+    python -m <package>.sweep --spec C2 --out sweep_c2          # 1 GPU
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m <package>.sweep --spec C4 --out c4
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+from dataclasses import dataclass, field
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _native
+
+YIELD_FIELDS = _native.YIELD_FIELDS
+
+EQUAL_MASS = {  # /root/reference/yields_config_equal_mass.json
+    "regime": "nonthermal", "m_chi_GeV": 0.95, "g_chi": 2, "chi_stats": "fermion",
+    "sigma_v_chi_GeV_m2": 0.0, "T_p_GeV": 100.0, "beta_over_H": 100.0, "v_w": 0.30, "I_p": 0.34,
+    "g_star": 106.75, "g_star_s": 106.75, "P_chi_to_B": 0.14925839040304145,
+    "source_shape_sigma_y": 9.0, "Gamma_wash_over_H": 0.0, "incident_flux_scale": 1.07e-9,
+    "deplete_DM_from_source": False, "T_max_over_Tp": 5.0, "T_min_over_Tp": 0.001,
+    "Y_chi_init": 4.90e-10, "n_chi_at_Tp_GeV3": None,
+}
+
+
+@dataclass
+class SweepSpec:
+    name: str
+    base: dict
+    axes: List[Tuple[str, np.ndarray]]
+    n_y: int = 8000
+    notes: str = ""
+
+    @property
+    def total(self) -> int:
+        n = 1
+        for _, v in self.axes:
+            n *= len(v)
+        return n
+
+    def point_params(self, idx: int) -> dict:
+        """Host-side decode of flat index -> axis values (for reporting / tests)."""
+        out = {}
+        for name, vals in reversed(self.axes):
+            out[name] = float(vals[idx % len(vals)])
+            idx //= len(vals)
+        return out
+
+    def to_json(self) -> dict:
+        return {"name": self.name, "base": self.base, "n_y": self.n_y, "notes": self.notes,
+                "axes": [{"field": n, "values": [float(x) for x in v]} for n, v in self.axes]}
+
+
+def _axis_from_json(a: dict) -> Tuple[str, np.ndarray]:
+    if "values" in a:
+        v = np.asarray(a["values"], dtype=np.float64)
+    elif "logspace" in a:
+        v = np.logspace(*a["logspace"][:2], int(a["logspace"][2]))
+    elif "linspace" in a:
+        v = np.linspace(*a["linspace"][:2], int(a["linspace"][2]))
+    else:
+        raise ValueError(f"axis {a!r} needs values / linspace / logspace")
+    if a["field"] not in _native.FIELD:
+        raise ValueError(f"unknown sweep field {a['field']!r}")
+    return a["field"], v
+
+
+def spec_from_json(d: dict) -> SweepSpec:
+    base = dict(EQUAL_MASS)
+    if "config" in d:
+        with open(d["config"]) as f:
+            base.update(json.load(f))
+    base.update(d.get("base", {}))
+    return SweepSpec(d.get("name", "custom"), base, [_axis_from_json(a) for a in d["axes"]], int(d.get("n_y", 8000)),
+                     d.get("notes", ""))
+
+
+def builtin_specs() -> dict:
+    """BASELINE.json configs C2-C4 with the grids of SURVEY §8d."""
+    ls, lin = np.logspace, np.linspace
+    return {
+        "C2": SweepSpec("C2", dict(EQUAL_MASS),
+                        [("m_mix", ls(-3, 0, 1000)), ("dprime", ls(-3, 1, 1000))],
+                        notes="equal-mass config, coupling x sweep-rate, v_w=0.30, F=1 -> delta -> P"),
+        "C3": SweepSpec("C3", dict(EQUAL_MASS),
+                        [("m_chi_GeV", ls(0, 3.5, 100)), ("I_p", lin(0.05, 1, 100)), ("delta_LZ", ls(-4, 0, 1000))],
+                        notes="m_chi crosses T=m/3 inside the window"),
+        "C4": SweepSpec("C4", dict(EQUAL_MASS),
+                        [("beta_over_H", ls(1, 3, 10)), ("I_p", lin(0.05, 1, 100)), ("v_w", lin(0.05, 0.95, 10)),
+                         ("source_shape_sigma_y", lin(3, 30, 10)), ("m_chi_GeV", ls(-1, 3.5, 10)),
+                         ("delta_LZ", ls(-4, 0, 100))],
+                        notes="full cosmological scan, 1e8 points"),
+    }
+
+
+def shard_range(total: int, rank: int, world: int) -> Tuple[int, int]:
+    """contiguous blocks [r*N/W, (r+1)*N/W)."""
+    return rank * total // world, (rank + 1) * total // world
+
+
+def _shard_file(out_dir: str, start: int, count: int) -> str:
+    return os.path.join(out_dir, f"shard_{start:012d}_{count}.npy")
+
+
+ComputeFn = Callable[[int, int, "object"], None]  # (start, count, out_tensor[count, 6]) -> None
+
+
+def run_local(compute: ComputeFn, start: int, end: int, make_out: Callable[[int], "object"], chunk: int,
+              out_dir: Optional[str] = None, resume: bool = False, sync: Callable[[], None] = lambda: None,
+              log: Callable[[str], None] = lambda s: None):
+    """Evaluate [start, end) in chunks into one (end-start, 6) tensor, with optional
+    per-chunk checkpoint files."""
+    import torch
+    local = make_out(end - start)
+    done = 0
+    for c0 in range(start, end, chunk):
+        n = min(chunk, end - c0)
+        view = local[c0 - start:c0 - start + n]
+        path = _shard_file(out_dir, c0, n) if out_dir else None
+        if path and resume and os.path.exists(path):
+            arr = np.load(path, allow_pickle=False)
+            if arr.shape != (n, 6):
+                raise RuntimeError(f"checkpoint {path} has shape {arr.shape}, expected {(n, 6)}")
+            view.copy_(torch.from_numpy(arr))
+            log(f"resumed {path}")
+            continue
+        compute(c0, n, view)
+        if path:
+            sync()
+            tmp = path + ".tmp.npy"
+            np.save(tmp, view.detach().cpu().numpy(), allow_pickle=False)
+            os.replace(tmp, path)
+        done += n
+    return local
+
+
+def gather_table(local, total: int, rank: int, world: int, group=None):
+    """All-gather the per-rank shards (sizes differ by <= 1) into the full (total, 6) table."""
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return local
+    sizes = [shard_range(total, r, world)[1] - shard_range(total, r, world)[0] for r in range(world)]
+    m = max(sizes)
+    pad = torch.zeros((m, 6), dtype=local.dtype, device=local.device)
+    pad[:local.shape[0]] = local
+    if dist.get_backend(group) == "nccl":
+        buf = torch.empty((world * m, 6), dtype=local.dtype, device=local.device)
+        dist.all_gather_into_tensor(buf, pad, group=group)  # RCCL over xGMI
+        parts = [buf[r * m:r * m + sizes[r]] for r in range(world)]
+    else:
+        lst = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(lst, pad, group=group)
+        parts = [lst[r][:sizes[r]] for r in range(world)]
+    return torch.cat(parts)
+
+
+def summarize(table: np.ndarray, spec: SweepSpec, elapsed: Optional[float] = None) -> dict:
+    """Grid-wide statistics, reduced on the host in flat-index order (deterministic); keys
+    match yields_out.json "final" (fpy:425-427) plus P_used."""
+    stats = {}
+    for j, k in enumerate(YIELD_FIELDS):
+        col = table[:, j]
+        fin = col[np.isfinite(col)]
+        stats[k] = {"min": float(fin.min()) if fin.size else None, "max": float(fin.max()) if fin.size else None,
+                    "mean": float(np.add.reduce(fin) / fin.size) if fin.size else None,
+                    "n_nonfinite": int(col.size - fin.size)}
+    best = int(np.nanargmin(np.abs(table[:, 4] - 5.357)))  # closest to the Planck ratio (PAPER eq.(22))
+    return {"spec": spec.name, "n_points": int(table.shape[0]), "fields": list(YIELD_FIELDS), "final": stats,
+            "closest_to_planck_ratio": {"index": best, "params": spec.point_params(best),
+                                        "final": dict(zip(YIELD_FIELDS, map(float, table[best])))},
+            "elapsed_s": elapsed}
+
+
+def run_sweep(spec: SweepSpec, engine=None, rank: int = 0, world: int = 1, chunk: int = 1 << 20,
+              out_dir: Optional[str] = None, resume: bool = False, group=None, log=print):
+    """Evaluate `spec` on this rank's shard, all-gather, return the full table (torch, on
+    the engine's device)."""
+    import torch
+    if engine is None:
+        from .engine import default_engine
+        engine = default_engine()
+    start, end = shard_range(spec.total, rank, world)
+    if out_dir:
+        os.makedirs(out_dir, exist_ok=True)
+
+    def compute(s, n, out):
+        engine.sweep(spec.base, spec.axes, s, n, n_y=spec.n_y, out=out)
+
+    local = run_local(compute, start, end,
+                      lambda n: torch.empty((n, 6), dtype=torch.float64, device=engine.device), chunk,
+                      out_dir, resume, sync=torch.cuda.synchronize, log=log)
+    return gather_table(local, spec.total, rank, world, group)
+
+
+def main(argv=None):
+    import torch
+    import torch.distributed as dist
+    ap = argparse.ArgumentParser(description="lzq parameter sweep (1..8 GPUs, RCCL all-gather)")
+    ap.add_argument("--spec", required=True, help="C2 | C3 | C4 | path to a sweep-spec JSON")
+    ap.add_argument("--out", default=None, help="directory for shard checkpoints, table.npy, summary.json")
+    ap.add_argument("--resume", action="store_true")
+    ap.add_argument("--chunk", type=int, default=1 << 20)
+    ap.add_argument("--limit", type=int, default=None, help="evaluate only the first N grid points")
+    args = ap.parse_args(argv)
+
+    specs = builtin_specs()
+    if args.spec in specs:
+        spec = specs[args.spec]
+    else:
+        with open(args.spec) as f:
+            spec = spec_from_json(json.load(f))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    if args.limit is not None:
+        spec = SweepSpec(spec.name, spec.base, spec.axes, spec.n_y, spec.notes)
+        total = min(args.limit, spec.total)
+        spec_total = total
+    else:
+        spec_total = spec.total
+
+    from .engine import Engine
+    eng = Engine(local_rank)
+    t0 = time.perf_counter()
+    start, end = shard_range(spec_total, rank, world)
+
+    def compute(s, n, out):
+        eng.sweep(spec.base, spec.axes, s, n, n_y=spec.n_y, out=out)
+
+    local = run_local(compute, start, end,
+                      lambda n: torch.empty((n, 6), dtype=torch.float64, device=eng.device), args.chunk,
+                      args.out, args.resume, sync=torch.cuda.synchronize,
+                      log=(print if rank == 0 else (lambda s: None)))
+    table = gather_table(local, spec_total, rank, world)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if rank == 0:
+        tab = table.cpu().numpy()
+        summ = summarize(tab, spec, elapsed)
+        summ["points_per_s"] = spec_total / elapsed
+        summ["n_gpus"] = world
+        if args.out:
+            np.save(os.path.join(args.out, "table.npy"), tab, allow_pickle=False)
+            with open(os.path.join(args.out, "summary.json"), "w") as f:
+                json.dump({**summ, "spec_def": spec.to_json()}, f, indent=2)
+        print(json.dumps({k: summ[k] for k in ("spec", "n_points", "points_per_s", "n_gpus", "elapsed_s")}))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -109,7 +109,10 @@ def test_quadrature_operator_api(gpu_engine):
         got = bs.integrate_YB_by_quadrature(tlo, thi, n_y=ny)
         ref = lib.oracle_yb_quadrature(ctypes.byref(p), tlo, thi, ny)
         assert rel_err(got, ref) < GUARD, (tlo, thi, ny, got, ref)
-    assert rel_err(bs.aov.A_over_V_y(15.975), 3.197927e-10) < 1e-6
+    # diagnostics row T/Tp = 0.871 prints A/V = 3.197927e-10 (%14.6e), fpy:430-438
+    T = np.geomspace(50.0, 200.0, 21)[8]
+    y = pkg("physics_host").y_of_T(T, 100.0, 100.0)
+    assert rel_err(bs.aov.A_over_V_y(y), 3.197927e-10) < 2e-7
 
 
 def test_deterministic_and_batch_independent(gpu_engine):

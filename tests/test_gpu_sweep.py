@@ -51,7 +51,7 @@ def test_c2_full_grid_separability(gpu_engine):
     assert np.max(np.abs(ratio / ratio[0] - 1)) < 1e-14
     m, d = np.meshgrid(axes[0][1], axes[1][1], indexing="ij")
     delta = (m * m / (2.0 * 0.3 * d)).ravel()
-    assert np.allclose(P, 1.0 - np.exp(-2.0 * np.pi * delta), rtol=1e-13, atol=1e-16)
+    assert np.allclose(P, 1.0 - np.exp(-2.0 * np.pi * delta), rtol=1e-13, atol=5e-16)  # GPU vs numpy exp: 1 ulp of 1.0
     YB1 = 8.720885362714675e-11 / 0.14925839040304145
     assert rel_err(ratio[0], YB1) < 1e-11
 

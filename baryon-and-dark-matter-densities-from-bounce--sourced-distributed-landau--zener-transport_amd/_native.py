@@ -46,10 +46,11 @@ FIELD.update({"delta_LZ": 32, "m_mix": 33, "dprime": 34})
 FERMION, BOSON = 0, 1
 THERMAL, NONTHERMAL, REGIME_OTHER = 0, 1, 2
 LZQ_NZ = 1200
+TUNE_EXP, EXP_POLY11, EXP_TABLE256 = 0, 0, 1  # enum lzq_tune_key / lzq_exp_variant
 LZQ_MAX_AXES = 8
 
 # Symbols declared in include/lzq.h (checked by tests/test_capi.py against the header).
-EXPORTS = ("lzq_abi_version", "lzq_last_error", "lzq_init", "lzq_ztables", "lzq_aov_batch",
+EXPORTS = ("lzq_abi_version", "lzq_last_error", "lzq_init", "lzq_ztables", "lzq_tune", "lzq_aov_batch",
            "lzq_jchi_batch", "lzq_yields_batch", "lzq_sweep_grid", "lzq_p_closed_form",
            "lzq_lz_propagate")
 
@@ -81,6 +82,7 @@ def load(path: str | None = None):
     L.lzq_last_error.restype = ctypes.c_char_p
     L.lzq_init.argtypes = [ctypes.c_int]
     L.lzq_ztables.argtypes = [P(d), P(d), P(d)]
+    L.lzq_tune.argtypes = [i32, i32]
     L.lzq_aov_batch.argtypes = [P(LzqPoint), vp, i64, vp, vp]
     L.lzq_jchi_batch.argtypes = [P(LzqPoint), vp, i64, vp, vp]
     L.lzq_yields_batch.argtypes = [vp, i64, i32, vp, vp, vp, vp, vp]

@@ -79,4 +79,32 @@ LZQ_HD double exp2_nonpos(double c2, double g) {
   return __builtin_ldexp(exp2_poly(r), k);
 }
 
+// ---------------------------------------------------------------------------------------
+// Table-driven variant (default): 2^u = 2^e * T[j] * 2^(r/256),  u*256 = 256 e + j + r,
+// T[j] = 2^(j/256) (2 KB, staged in LDS once per block), |r| <= 1/2 so r/256 <= 2^-9 and a
+// degree-4 Taylor polynomial is accurate to 3.8e-17 (0.17 ulp).  Per node: 11 FP64 VALU
+// (mul, rndne, fma, cvt, 3 fma + mul, fma, ldexp, + the caller's accumulate) + 3 integer
+// VALU (and, shift for the LDS address, arithmetic shift for e) + one ds_read_b64.  The LDS
+// table has 256 distinct 8-byte entries, so a wave64 read is at most 8-way bank-conflicted
+// and is usually far less (lanes of one wave hold neighbouring y-nodes).
+constexpr int kTabBits = 8;
+constexpr int kTabN = 1 << kTabBits;
+constexpr double kTabB1 = 0x1.62e42fefa39efp-9;   // (ln2/256)^1 / 1!
+constexpr double kTabB2 = 0x1.ebfbdff82c58fp-19;  // (ln2/256)^2 / 2!
+constexpr double kTabB3 = 0x1.c6b08d704a0c0p-29;  // (ln2/256)^3 / 3!
+constexpr double kTabB4 = 0x1.3b2ab6fba4e77p-39;  // (ln2/256)^4 / 4!
+
+// 2^(c2N*g / 256) for c2N*g <= 0 with c2N = 256*c2; tab[j] = 2^(j/256).
+LZQ_HD double exp2_nonpos_tab(double c2N, double g, const double* tab) {
+  double u = c2N * g;
+  double kd = __builtin_rint(u);
+  double r = __builtin_fma(c2N, g, -kd);
+  int32_t k = cvt_i32_sat(kd);
+  int32_t j = k & (kTabN - 1);
+  int32_t e = k >> kTabBits;  // arithmetic shift: floor(k / 256); INT_MIN -> -2^23 -> 0 result
+  double T = tab[j];
+  double q = r * __builtin_fma(r, __builtin_fma(r, __builtin_fma(r, kTabB4, kTabB3), kTabB2), kTabB1);
+  return __builtin_ldexp(__builtin_fma(T, q, T), e);
+}
+
 }  // namespace lzq

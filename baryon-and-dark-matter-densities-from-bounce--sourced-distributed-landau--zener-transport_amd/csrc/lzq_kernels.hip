@@ -118,9 +118,17 @@ __device__ __forceinline__ double y_weight(const QuadSetup& s, int64_t j, double
   return 0.5 * (dl + dr);
 }
 
+// exp variants of the inner loop (lzq_tune(LZQ_TUNE_EXP, ...))
+enum ExpVariant { kExpPoly11 = 0, kExpTable256 = 1 };
+
+// Scale of c2 expected by the variant (2^(c2*g) for poly11, 2^(c2N*g/256) for the table).
+template <int EXPV>
+__device__ __forceinline__ double c2_scale() { return EXPV == kExpTable256 ? (double)kTabN : 1.0; }
+
 // F(c2) = sum_k omega_k 2^(c2 g4_k) for YB independent y-nodes per lane.
-template <int YB>
-__device__ __forceinline__ void zsum(const ZNode* __restrict__ zt, const double (&c2)[YB], double (&F)[YB]) {
+template <int YB, int EXPV>
+__device__ __forceinline__ void zsum(const ZNode* __restrict__ zt, const double* tab, const double (&c2)[YB],
+                                     double (&F)[YB]) {
 #pragma unroll
   for (int b = 0; b < YB; ++b) F[b] = 0.0;
   for (int k = 0; k < kNZ; k += kKUnroll) {
@@ -129,9 +137,21 @@ __device__ __forceinline__ void zsum(const ZNode* __restrict__ zt, const double 
       const double g4 = zt[k + kk].g4;
       const double om = zt[k + kk].omega;
 #pragma unroll
-      for (int b = 0; b < YB; ++b) F[b] = __builtin_fma(om, exp2_nonpos(c2[b], g4), F[b]);
+      for (int b = 0; b < YB; ++b) {
+        const double e = EXPV == kExpTable256 ? exp2_nonpos_tab(c2[b], g4, tab) : exp2_nonpos(c2[b], g4);
+        F[b] = __builtin_fma(om, e, F[b]);
+      }
     }
   }
+}
+
+// Stage the 2 KB table T[j] = 2^(j/256) in LDS (every thread of the block must call this).
+template <int EXPV>
+__device__ __forceinline__ const double* stage_table(const double* __restrict__ gtab, double* lds) {
+  if (EXPV != kExpTable256) return nullptr;
+  for (int i = threadIdx.x; i < kTabN; i += blockDim.x) lds[i] = gtab[i];
+  __syncthreads();
+  return lds;
 }
 
 // Fixed-order xor butterfly over the 64 lanes (every lane ends with the same sum).
@@ -142,8 +162,8 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 // Y_B of one point by one wavefront.  fpy:231-267
-template <int YB>
-__device__ double yb_wave(const QuadSetup& s, const ZNode* __restrict__ zt, int lane) {
+template <int YB, int EXPV>
+__device__ double yb_wave(const QuadSetup& s, const ZNode* __restrict__ zt, const double* tab, int lane) {
   if (s.empty) return 0.0;
   double acc = 0.0;
   const int64_t n = s.n;
@@ -157,10 +177,10 @@ __device__ double yb_wave(const QuadSetup& s, const ZNode* __restrict__ zt, int 
       int64_t jj = j[b] < n ? j[b] : n - 1;  // tail lanes recompute the last node, weight 0
       y[b] = y_node(s, jj);
       expy[b] = exp(pymax(pymin(y[b], 50.0), -50.0));  // fpy:161
-      c2[b] = (s.cneg * expy[b]) * kLog2E;              // fpy:163 c, in log2 units
+      c2[b] = ((s.cneg * expy[b]) * kLog2E) * c2_scale<EXPV>();  // fpy:163 c, log2 units
     }
     double F[YB];
-    zsum<YB>(zt, c2, F);
+    zsum<YB, EXPV>(zt, tab, c2, F);
 #pragma unroll
     for (int b = 0; b < YB; ++b) {
       if (j[b] < n) {
@@ -256,13 +276,16 @@ __device__ __forceinline__ double grid_point(const lzq_point& base, const GridSp
 // ---------------------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------------------
-template <int YB>
+template <int YB, int EXPV>
 __global__ __launch_bounds__(kBlock) void yields_points_kernel(const lzq_point* __restrict__ pts, int64_t n,
                                                               int32_t n_y, const double* __restrict__ T_lo,
                                                               const double* __restrict__ T_hi,
                                                               const double* __restrict__ Pov,
                                                               const ZNode* __restrict__ zt,
+                                                              const double* __restrict__ gtab,
                                                               lzq_yield* __restrict__ out) {
+  __shared__ double lds_tab[kTabN];
+  const double* tab = stage_table<EXPV>(gtab, lds_tab);
   const int lane = threadIdx.x & (kWaveSize - 1);
   const int64_t idx = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (idx >= n) return;  // wave-uniform
@@ -271,35 +294,42 @@ __global__ __launch_bounds__(kBlock) void yields_points_kernel(const lzq_point* 
   const double tlo = T_lo ? T_lo[idx] : pt.T_min_over_Tp * pt.T_p_GeV;  // fpy:369
   const double thi = T_hi ? T_hi[idx] : pt.T_max_over_Tp * pt.T_p_GeV;  // fpy:368
   QuadSetup s = quad_setup(pt, P, tlo, thi, n_y);
-  const double Y_B = yb_wave<YB>(s, zt, lane);
+  const double Y_B = yb_wave<YB, EXPV>(s, zt, tab, lane);
   if (lane == 0) out[idx] = epilogue(pt, Y_B, P);
 }
 
-template <int YB>
+template <int YB, int EXPV>
 __global__ __launch_bounds__(kBlock) void yields_grid_kernel(lzq_point base, GridSpec grid, int64_t start,
                                                             int64_t count, int32_t n_y,
                                                             const ZNode* __restrict__ zt,
+                                                            const double* __restrict__ gtab,
                                                             lzq_yield* __restrict__ out) {
+  __shared__ double lds_tab[kTabN];
+  const double* tab = stage_table<EXPV>(gtab, lds_tab);
   const int lane = threadIdx.x & (kWaveSize - 1);
   const int64_t local = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (local >= count) return;
   lzq_point pt;
   const double P = grid_point(base, grid, start + local, pt);
   QuadSetup s = quad_setup(pt, P, pt.T_min_over_Tp * pt.T_p_GeV, pt.T_max_over_Tp * pt.T_p_GeV, n_y);
-  const double Y_B = yb_wave<YB>(s, zt, lane);
+  const double Y_B = yb_wave<YB, EXPV>(s, zt, tab, lane);
   if (lane == 0) out[local] = epilogue(pt, Y_B, P);
 }
 
 // fpy:158-165, one lane per y value
+template <int EXPV>
 __global__ __launch_bounds__(kBlock) void aov_kernel(lzq_point pt, const double* __restrict__ ys, int64_t n,
-                                                    const ZNode* __restrict__ zt, double* __restrict__ out) {
+                                                    const ZNode* __restrict__ zt, const double* __restrict__ gtab,
+                                                    double* __restrict__ out) {
+  __shared__ double lds_tab[kTabN];
+  const double* tab = stage_table<EXPV>(gtab, lds_tab);
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool live = i < n;
   const double y = live ? ys[i] : 0.0;
   QuadSetup s = quad_setup(pt, pt.P_chi_to_B, 1.0, 1.0, LZQ_NY_MIN);
   double expy = exp(pymax(pymin(y, 50.0), -50.0));
-  double c2[1] = {(s.cneg * expy) * kLog2E}, F[1];
-  zsum<1>(zt, c2, F);
+  double c2[1] = {((s.cneg * expy) * kLog2E) * c2_scale<EXPV>()}, F[1];
+  zsum<1, EXPV>(zt, tab, c2, F);
   if (live) out[i] = (y > 50.0) ? 0.0 : (s.pref0 * expy) * F[0];
 }
 
@@ -330,9 +360,12 @@ namespace {
 thread_local char g_err[512] = "";
 std::mutex g_mu;
 constexpr int kMaxDevices = 64;
-lzq::ZNode* g_dev_tab[kMaxDevices] = {nullptr};
+lzq::ZNode* g_dev_tab[kMaxDevices] = {nullptr};  // [LZQ_NZ] ZNode followed by kTabN doubles
 bool g_host_ready = false;
-double g_z[LZQ_NZ], g_g4[LZQ_NZ], g_omega[LZQ_NZ];
+double g_z[LZQ_NZ], g_g4[LZQ_NZ], g_omega[LZQ_NZ], g_exp2tab[lzq::kTabN];
+int g_exp_variant = lzq::kExpTable256;
+
+const double* exp_table(int dev) { return reinterpret_cast<const double*>(g_dev_tab[dev] + LZQ_NZ); }
 
 int fail(int code, const char* fmt, ...) {
   va_list ap;
@@ -368,6 +401,8 @@ int build_host_tables() {
     const double dr = k + 1 < n ? g_z[k + 1] - g_z[k] : 0.0;
     g_omega[k] = w[k] * (0.5 * (dl + dr));
   }
+  // T[j] = 2^(j/256): x87 long double exp2 (64-bit mantissa) rounded once to double
+  for (int j = 0; j < lzq::kTabN; ++j) g_exp2tab[j] = (double)exp2l((long double)j / (long double)lzq::kTabN);
   g_host_ready = true;
   return LZQ_OK;
 }
@@ -382,8 +417,10 @@ int ensure_device(int* dev_out) {
   if (g_dev_tab[dev]) return LZQ_OK;
   int rc = build_host_tables();
   if (rc) return rc;
-  lzq::ZNode host[LZQ_NZ];
+  static_assert(sizeof(lzq::ZNode) == 2 * sizeof(double), "ZNode layout");
+  lzq::ZNode host[LZQ_NZ + lzq::kTabN / 2];
   for (int k = 0; k < LZQ_NZ; ++k) host[k] = {g_g4[k], g_omega[k]};
+  memcpy(&host[LZQ_NZ], g_exp2tab, sizeof(g_exp2tab));
   lzq::ZNode* d = nullptr;
   LZQ_HIP(hipMalloc(&d, sizeof(host)));
   LZQ_HIP(hipMemcpy(d, host, sizeof(host), hipMemcpyHostToDevice));
@@ -417,6 +454,17 @@ int lzq_init(int device) {
   return rc;
 }
 
+int lzq_tune(int32_t key, int32_t value) {
+  if (key == LZQ_TUNE_EXP) {
+    if (value != LZQ_EXP_POLY11 && value != LZQ_EXP_TABLE256)
+      return fail(LZQ_EINVAL, "lzq_tune: unknown exp variant %d", value);
+    int prev = g_exp_variant;
+    g_exp_variant = value;
+    return prev;
+  }
+  return fail(LZQ_EINVAL, "lzq_tune: unknown key %d", key);
+}
+
 int lzq_ztables(double* z, double* gamma4, double* omega) {
   std::lock_guard<std::mutex> lk(g_mu);
   int rc = build_host_tables();
@@ -434,8 +482,12 @@ int lzq_aov_batch(const lzq_point* pt, const double* d_y, int64_t n, double* d_o
   if (rc) return rc;
   int64_t nb = blocks_for(n, lzq::kBlock);
   if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_aov_batch: n too large");
-  hipLaunchKernelGGL(lzq::aov_kernel, dim3((unsigned)nb), dim3(lzq::kBlock), 0, (hipStream_t)stream, *pt, d_y, n,
-                     g_dev_tab[dev], d_out);
+  if (g_exp_variant == lzq::kExpTable256)
+    hipLaunchKernelGGL(lzq::aov_kernel<lzq::kExpTable256>, dim3((unsigned)nb), dim3(lzq::kBlock), 0,
+                       (hipStream_t)stream, *pt, d_y, n, g_dev_tab[dev], exp_table(dev), d_out);
+  else
+    hipLaunchKernelGGL(lzq::aov_kernel<lzq::kExpPoly11>, dim3((unsigned)nb), dim3(lzq::kBlock), 0,
+                       (hipStream_t)stream, *pt, d_y, n, g_dev_tab[dev], exp_table(dev), d_out);
   LZQ_HIP(hipGetLastError());
   return LZQ_OK;
 }
@@ -461,8 +513,14 @@ int lzq_yields_batch(const lzq_point* d_points, int64_t n, int32_t n_y, const do
   if (rc) return rc;
   int64_t nb = blocks_for(n, lzq::kWavesPerBlock);
   if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_yields_batch: n too large");
-  hipLaunchKernelGGL(lzq::yields_points_kernel<1>, dim3((unsigned)nb), dim3(lzq::kBlock), 0, (hipStream_t)stream,
-                     d_points, n, n_y, d_T_lo, d_T_hi, d_P, g_dev_tab[dev], d_out);
+  if (g_exp_variant == lzq::kExpTable256)
+    hipLaunchKernelGGL((lzq::yields_points_kernel<1, lzq::kExpTable256>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
+                       (hipStream_t)stream, d_points, n, n_y, d_T_lo, d_T_hi, d_P, g_dev_tab[dev], exp_table(dev),
+                       d_out);
+  else
+    hipLaunchKernelGGL((lzq::yields_points_kernel<1, lzq::kExpPoly11>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
+                       (hipStream_t)stream, d_points, n, n_y, d_T_lo, d_T_hi, d_P, g_dev_tab[dev], exp_table(dev),
+                       d_out);
   LZQ_HIP(hipGetLastError());
   return LZQ_OK;
 }
@@ -502,8 +560,12 @@ int lzq_sweep_grid(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, 
   if (rc) return rc;
   int64_t nb = blocks_for(count, lzq::kWavesPerBlock);
   if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_sweep_grid: count too large for one launch");
-  hipLaunchKernelGGL(lzq::yields_grid_kernel<1>, dim3((unsigned)nb), dim3(lzq::kBlock), 0, (hipStream_t)stream,
-                     *base, g, start, count, n_y, g_dev_tab[dev], d_out);
+  if (g_exp_variant == lzq::kExpTable256)
+    hipLaunchKernelGGL((lzq::yields_grid_kernel<1, lzq::kExpTable256>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
+                       (hipStream_t)stream, *base, g, start, count, n_y, g_dev_tab[dev], exp_table(dev), d_out);
+  else
+    hipLaunchKernelGGL((lzq::yields_grid_kernel<1, lzq::kExpPoly11>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
+                       (hipStream_t)stream, *base, g, start, count, n_y, g_dev_tab[dev], exp_table(dev), d_out);
   LZQ_HIP(hipGetLastError());
   return LZQ_OK;
 }

@@ -33,6 +33,14 @@ class Engine:
         with torch.cuda.device(self.device):
             _native.check(self.lib.lzq_init(self.device.index))
 
+    def tune_exp(self, variant: str) -> str:
+        """Select the inner-loop exponential ('table256' default, 'poly11'); returns the previous."""
+        v = {"poly11": _native.EXP_POLY11, "table256": _native.EXP_TABLE256}[variant]
+        prev = self.lib.lzq_tune(_native.TUNE_EXP, v)
+        if prev < 0:
+            _native.check(prev)
+        return {_native.EXP_POLY11: "poly11", _native.EXP_TABLE256: "table256"}[prev]
+
     # -- helpers -------------------------------------------------------------------------
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)

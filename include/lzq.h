@@ -111,6 +111,14 @@ int lzq_init(int device);
  * omega_k = z_k^2 e^{-z_k} * (trapezoid weight of node k).  Each array has LZQ_NZ entries. */
 int lzq_ztables(double* z, double* gamma4, double* omega);
 
+/* Tuning knobs for ablations (process-wide, not thread-safe against concurrent launches).
+ * LZQ_TUNE_EXP selects the inner-loop exponential: LZQ_EXP_TABLE256 (default; 2^(j/256)
+ * LDS table + degree-4 polynomial) or LZQ_EXP_POLY11 (degree-11 minimax polynomial).
+ * Both are ~0.6 ulp; results agree to ~1e-15 relative.  Returns the previous value. */
+enum lzq_tune_key { LZQ_TUNE_EXP = 0 };
+enum lzq_exp_variant { LZQ_EXP_POLY11 = 0, LZQ_EXP_TABLE256 = 1 };
+int lzq_tune(int32_t key, int32_t value);
+
 /* ---- hot path -------------------------------------------------------------------------- */
 /* fpy:158-165: out[i] = A_over_V_y(y[i]) for the kernel of point *pt (host struct). */
 int lzq_aov_batch(const lzq_point* pt, const double* d_y, int64_t n, double* d_out, void* stream);

@@ -97,9 +97,9 @@ def load(path: str | None = None):
     return L
 
 
-def check(rc: int) -> None:
+def check(rc: int, lib=None) -> None:
     if rc != 0:
-        msg = load().lzq_last_error()
+        msg = (lib or load()).lzq_last_error()
         raise LzqError(rc, msg.decode() if msg else "")
 
 

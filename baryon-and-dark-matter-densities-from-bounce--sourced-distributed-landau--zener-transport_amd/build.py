@@ -43,17 +43,21 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found: the lzq HIP library cannot be built")
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
+def build(force: bool = False, verbose: bool = False, defines: dict | None = None,
+          out: str | None = None) -> str:
+    """Build liblzq.so (or a tuning variant with -D`defines` into `out`)."""
+    target = out or LIB_PATH
+    if not force and out is None and not defines and up_to_date():
         return LIB_PATH
-    os.makedirs(BUILD_DIR, exist_ok=True)
-    tmp = LIB_PATH + ".tmp"
-    cmd = [hipcc(), *FLAGS, "-I", INCLUDE, "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
+    os.makedirs(os.path.dirname(target), exist_ok=True)
+    tmp = target + ".tmp"
+    dflags = [f"-D{k}={v}" for k, v in (defines or {}).items()]
+    cmd = [hipcc(), *FLAGS, *dflags, "-I", INCLUDE, "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, target)
+    return target
 
 
 if __name__ == "__main__":

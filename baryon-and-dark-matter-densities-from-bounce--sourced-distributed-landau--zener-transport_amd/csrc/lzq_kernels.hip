@@ -34,7 +34,29 @@ constexpr int kNZ = LZQ_NZ;
 constexpr int kWaveSize = 64;
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWaveSize;
-constexpr int kKUnroll = 8;  // z-nodes per scalar-load batch (1200 % 8 == 0)
+#ifndef LZQ_KUNROLL
+#define LZQ_KUNROLL 8
+#endif
+#ifndef LZQ_YB
+#define LZQ_YB 1
+#endif
+// __launch_bounds__ second argument = minimum waves per SIMD (4: <= 128 VGPRs; +6.5% measured
+// over the compiler's own choice of 3 waves, tools/ablate_builds.py)
+#ifndef LZQ_MIN_WAVES
+#define LZQ_MIN_WAVES 4
+#endif
+// z-table source: 0 = wave-uniform scalar loads (SGPR operands), 1 = staged in LDS and read
+// with broadcast ds_read_b128 (keeps every LGKM operation of the loop in order, so the
+// compiler can use counted lgkmcnt waits instead of draining behind SMEM)
+#ifndef LZQ_ZLDS
+#define LZQ_ZLDS 0
+#endif
+// 1: magic-constant range reduction on waves whose lanes are all in int32 range or dead
+#ifndef LZQ_MAGIC
+#define LZQ_MAGIC 1
+#endif
+constexpr int kKUnroll = LZQ_KUNROLL;  // z-nodes per scalar-load batch (must divide 1200)
+constexpr int kYB = LZQ_YB;            // y-nodes per lane per pass (independent chains)
 static_assert(kNZ % kKUnroll == 0, "z unroll must divide nz");
 
 struct ZNode {
@@ -96,9 +118,22 @@ __device__ __forceinline__ double y_node(const QuadSetup& s, int64_t j) {
   return (double)j * s.step + s.y_lo;
 }
 
-// Integrand of fpy:264-265 at node y given F = trapz_z(...) of fpy:163-164.
-__device__ __forceinline__ double integrand(const QuadSetup& s, double y, double expy, double F) {
-  double Av = (y > 50.0) ? 0.0 : (s.pref0 * expy) * F;  // fpy:159-165
+// Per-y factors of the integrand of fpy:264-265 that do not depend on F, computed BEFORE the
+// z-loop so that only these 7 doubles (not the whole QuadSetup) stay live across it.  The
+// post-loop combination keeps the reference's rounding order:
+//   SB = ((P*J)*Av)*W,  integrand = SB/((s*H)*T)*|dT/dy|,  Av = (pref0*expy)*F.
+struct YFactors {
+  double PJ;     // P * J(T)                        fpy:260,264
+  double W;      // window                          fpy:262
+  double sHT;    // (s*H)*T                         fpy:258-259,265
+  double adTdy;  // |dT/dy|                         fpy:255,265
+  double pexp;   // pref0 * expy  (A/V prefactor)   fpy:162
+  double w;      // trapezoid weight of the node    fpy:267
+  double live;   // 1 if y <= 50 (fpy:159), else 0
+};
+
+__device__ __forceinline__ YFactors y_factors(const QuadSetup& s, double y, double expy, double wt) {
+  YFactors f;
   double denom = pymax(1.0 + 2.0 * y / s.Bc, 1e-12);     // fpy:252-253
   double T = s.Tp / sqrt(denom);                          // fpy:254
   double dTdy = s.dT0 * pow(denom, -1.5);                 // fpy:255
@@ -106,9 +141,20 @@ __device__ __forceinline__ double integrand(const QuadSetup& s, double y, double
   double sE = s_entropy(T, s.g_star_s);                   // fpy:259
   double J = s.flux * 0.25 * n_chi_eq(T, s.m, s.g, s.stats) * vbar_chi(T, s.m);  // fpy:260
   double q = y / s.sig;
-  double W = exp(-0.5 * (q * q));                         // fpy:262
-  double SB = s.P * J * Av * W;                           // fpy:264
-  return SB / (sE * H * T) * fabs(dTdy);                  // fpy:265
+  f.W = exp(-0.5 * (q * q));                              // fpy:262
+  f.PJ = s.P * J;
+  f.sHT = sE * H * T;
+  f.adTdy = fabs(dTdy);
+  f.pexp = s.pref0 * expy;
+  f.w = wt;
+  f.live = (y > 50.0) ? 0.0 : 1.0;
+  return f;
+}
+
+__device__ __forceinline__ double integrand_from(const YFactors& f, double F) {
+  double Av = f.live != 0.0 ? f.pexp * F : 0.0;           // fpy:159-165
+  double SB = f.PJ * Av * f.W;                            // fpy:264
+  return SB / f.sHT * f.adTdy;                            // fpy:265
 }
 
 // trapezoid weight of y-node j: (d_{j-1} + d_j)/2 with d = diff(ys)      fpy:267
@@ -126,23 +172,100 @@ template <int EXPV>
 __device__ __forceinline__ double c2_scale() { return EXPV == kExpTable256 ? (double)kTabN : 1.0; }
 
 // F(c2) = sum_k omega_k 2^(c2 g4_k) for YB independent y-nodes per lane.
-template <int YB, int EXPV>
+// The table variant is written in explicit phases per batch of kKUnroll z-nodes -- table
+// operands, range reduction, all LDS lookups, then polynomial + accumulate -- so the
+// lookups of a batch are in flight together and retire behind one wait.
+//
+// MAGIC selects the range reduction of the table variant:
+//   false: u = c2*g; kd = rint(u); r = fma(c2,g,-kd); k = cvt_i32_sat(kd)   (4 FP64 ops, any u)
+//   true : t = fma(c2,g,1.5*2^52); kd = t - 1.5*2^52; r = fma(c2,g,-kd); k = lo32(t)
+//          (3 FP64 ops; exact only while |c2*g| < 2^31 -- the caller guarantees it per wave)
+template <int YB, int EXPV, bool MAGIC = false>
 __device__ __forceinline__ void zsum(const ZNode* __restrict__ zt, const double* tab, const double (&c2)[YB],
                                      double (&F)[YB]) {
+  constexpr double kMagic = 0x1.8p52;
 #pragma unroll
   for (int b = 0; b < YB; ++b) F[b] = 0.0;
   for (int k = 0; k < kNZ; k += kKUnroll) {
+    double g4[kKUnroll], om[kKUnroll];
 #pragma unroll
     for (int kk = 0; kk < kKUnroll; ++kk) {
-      const double g4 = zt[k + kk].g4;
-      const double om = zt[k + kk].omega;
+      g4[kk] = zt[k + kk].g4;
+      om[kk] = zt[k + kk].omega;
+    }
+    if constexpr (EXPV == kExpTable256) {
+      double r[YB][kKUnroll], T[YB][kKUnroll];
+      int32_t e[YB][kKUnroll], j[YB][kKUnroll];
 #pragma unroll
-      for (int b = 0; b < YB; ++b) {
-        const double e = EXPV == kExpTable256 ? exp2_nonpos_tab(c2[b], g4, tab) : exp2_nonpos(c2[b], g4);
-        F[b] = __builtin_fma(om, e, F[b]);
-      }
+      for (int kk = 0; kk < kKUnroll; ++kk)
+#pragma unroll
+        for (int b = 0; b < YB; ++b) {
+          int32_t ki;
+          double kd;
+          if constexpr (MAGIC) {
+            const double t = __builtin_fma(c2[b], g4[kk], kMagic);
+            kd = t - kMagic;
+            ki = (int32_t)(uint32_t)__builtin_bit_cast(uint64_t, t);
+          } else {
+            kd = __builtin_rint(c2[b] * g4[kk]);
+            ki = cvt_i32_sat(kd);
+          }
+          r[b][kk] = __builtin_fma(c2[b], g4[kk], -kd);
+          j[b][kk] = ki & (kTabN - 1);
+          e[b][kk] = ki >> kTabBits;
+        }
+#pragma unroll
+      for (int kk = 0; kk < kKUnroll; ++kk)
+#pragma unroll
+        for (int b = 0; b < YB; ++b) T[b][kk] = tab[j[b][kk]];
+#pragma unroll
+      for (int kk = 0; kk < kKUnroll; ++kk)
+#pragma unroll
+        for (int b = 0; b < YB; ++b) {
+          const double rr = r[b][kk];
+          const double q =
+              rr * __builtin_fma(rr, __builtin_fma(rr, __builtin_fma(rr, kTabB4, kTabB3), kTabB2), kTabB1);
+          const double v = __builtin_ldexp(__builtin_fma(T[b][kk], q, T[b][kk]), e[b][kk]);
+          F[b] = __builtin_fma(om[kk], v, F[b]);
+        }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < kKUnroll; ++kk)
+#pragma unroll
+        for (int b = 0; b < YB; ++b) F[b] = __builtin_fma(om[kk], exp2_nonpos(c2[b], g4[kk]), F[b]);
     }
   }
+}
+
+// Pass-level dispatch of the z-sum (table variant).  A lane is
+//   * "in range" when |c2| * max_k g4_k < 2^31 - 2^20: the magic reduction is exact for all k;
+//   * "dead" when c2 * g4_1 <= -256*1077: every node k >= 1 underflows to exactly 0 in either
+//     reduction (g4 is increasing and k = 0 has omega_0 = 0), so F = 0 exactly.
+// If every lane of the wave is in range or dead, the pass runs the 3-op reduction (dead lanes
+// compute with c2 = 0 and are zeroed afterwards: same instruction stream, same exact zero);
+// otherwise the 4-op saturating reduction.  The choice is a function of the point only.
+template <int YB, int EXPV>
+__device__ __forceinline__ void zsum_dispatch(const ZNode* __restrict__ zt, const double* tab,
+                                              const double (&c2)[YB], double (&F)[YB]) {
+  if constexpr (EXPV == kExpTable256 && LZQ_MAGIC) {
+    const double g_max = zt[kNZ - 1].g4, g_1 = zt[1].g4;
+    bool dead[YB], ok = true;
+    double c2e[YB];
+#pragma unroll
+    for (int b = 0; b < YB; ++b) {
+      dead[b] = c2[b] * g_1 <= -256.0 * 1077.0;
+      const bool in_range = fabs(c2[b]) * g_max < 2147483648.0 - 1048576.0;
+      ok = ok && (dead[b] || in_range);
+      c2e[b] = dead[b] ? 0.0 : c2[b];
+    }
+    if (__all(ok)) {
+      zsum<YB, EXPV, true>(zt, tab, c2e, F);
+#pragma unroll
+      for (int b = 0; b < YB; ++b) F[b] = dead[b] ? 0.0 : F[b];
+      return;
+    }
+  }
+  zsum<YB, EXPV, false>(zt, tab, c2, F);
 }
 
 // Stage the 2 KB table T[j] = 2^(j/256) in LDS (every thread of the block must call this).
@@ -152,6 +275,22 @@ __device__ __forceinline__ const double* stage_table(const double* __restrict__ 
   for (int i = threadIdx.x; i < kTabN; i += blockDim.x) lds[i] = gtab[i];
   __syncthreads();
   return lds;
+}
+
+// LDS image of the per-block tables: z nodes (19.2 KB) followed by the exp2 table (2 KB).
+struct LdsTables {
+  ZNode z[kNZ];
+  double t[kTabN];
+};
+
+// Stage both tables (global layout: ZNode[kNZ] then double[kTabN], see ensure_device).
+template <int EXPV>
+__device__ __forceinline__ void stage_tables(const ZNode* __restrict__ gz, LdsTables* lds) {
+  const double* src = reinterpret_cast<const double*>(gz);
+  double* dst = reinterpret_cast<double*>(lds);
+  constexpr int n = 2 * kNZ + (EXPV == kExpTable256 ? kTabN : 0);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
 }
 
 // Fixed-order xor butterfly over the 64 lanes (every lane ends with the same sum).
@@ -169,25 +308,21 @@ __device__ double yb_wave(const QuadSetup& s, const ZNode* __restrict__ zt, cons
   const int64_t n = s.n;
   const int64_t per_pass = (int64_t)kWaveSize * YB;
   for (int64_t base = 0; base < n; base += per_pass) {
-    double c2[YB], expy[YB], y[YB];
-    int64_t j[YB];
+    double c2[YB];
+    YFactors fy[YB];
 #pragma unroll
     for (int b = 0; b < YB; ++b) {
-      j[b] = base + (int64_t)b * kWaveSize + lane;
-      int64_t jj = j[b] < n ? j[b] : n - 1;  // tail lanes recompute the last node, weight 0
-      y[b] = y_node(s, jj);
-      expy[b] = exp(pymax(pymin(y[b], 50.0), -50.0));  // fpy:161
-      c2[b] = ((s.cneg * expy[b]) * kLog2E) * c2_scale<EXPV>();  // fpy:163 c, log2 units
+      const int64_t j = base + (int64_t)b * kWaveSize + lane;
+      const int64_t jj = j < n ? j : n - 1;  // tail lanes recompute the last node with weight 0
+      const double y = y_node(s, jj);
+      const double expy = exp(pymax(pymin(y, 50.0), -50.0));               // fpy:161
+      c2[b] = ((s.cneg * expy) * kLog2E) * c2_scale<EXPV>();                // fpy:163 c, log2 units
+      fy[b] = y_factors(s, y, expy, j < n ? y_weight(s, jj, y) : 0.0);
     }
     double F[YB];
-    zsum<YB, EXPV>(zt, tab, c2, F);
+    zsum_dispatch<YB, EXPV>(zt, tab, c2, F);
 #pragma unroll
-    for (int b = 0; b < YB; ++b) {
-      if (j[b] < n) {
-        double I = integrand(s, y[b], expy[b], F[b]);
-        acc = __builtin_fma(y_weight(s, j[b], y[b]), I, acc);
-      }
-    }
+    for (int b = 0; b < YB; ++b) acc = __builtin_fma(fy[b].w, integrand_from(fy[b], F[b]), acc);
   }
   return wave_sum(acc);
 }
@@ -277,15 +412,22 @@ __device__ __forceinline__ double grid_point(const lzq_point& base, const GridSp
 // kernels
 // ---------------------------------------------------------------------------------------
 template <int YB, int EXPV>
-__global__ __launch_bounds__(kBlock) void yields_points_kernel(const lzq_point* __restrict__ pts, int64_t n,
+__global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void yields_points_kernel(const lzq_point* __restrict__ pts, int64_t n,
                                                               int32_t n_y, const double* __restrict__ T_lo,
                                                               const double* __restrict__ T_hi,
                                                               const double* __restrict__ Pov,
                                                               const ZNode* __restrict__ zt,
                                                               const double* __restrict__ gtab,
                                                               lzq_yield* __restrict__ out) {
+#if LZQ_ZLDS
+  __shared__ LdsTables lds;
+  stage_tables<EXPV>(zt, &lds);
+  const double* tab = lds.t;
+  zt = lds.z;
+#else
   __shared__ double lds_tab[kTabN];
   const double* tab = stage_table<EXPV>(gtab, lds_tab);
+#endif
   const int lane = threadIdx.x & (kWaveSize - 1);
   const int64_t idx = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (idx >= n) return;  // wave-uniform
@@ -299,13 +441,20 @@ __global__ __launch_bounds__(kBlock) void yields_points_kernel(const lzq_point* 
 }
 
 template <int YB, int EXPV>
-__global__ __launch_bounds__(kBlock) void yields_grid_kernel(lzq_point base, GridSpec grid, int64_t start,
+__global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void yields_grid_kernel(lzq_point base, GridSpec grid, int64_t start,
                                                             int64_t count, int32_t n_y,
                                                             const ZNode* __restrict__ zt,
                                                             const double* __restrict__ gtab,
                                                             lzq_yield* __restrict__ out) {
+#if LZQ_ZLDS
+  __shared__ LdsTables lds;
+  stage_tables<EXPV>(zt, &lds);
+  const double* tab = lds.t;
+  zt = lds.z;
+#else
   __shared__ double lds_tab[kTabN];
   const double* tab = stage_table<EXPV>(gtab, lds_tab);
+#endif
   const int lane = threadIdx.x & (kWaveSize - 1);
   const int64_t local = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (local >= count) return;
@@ -514,11 +663,11 @@ int lzq_yields_batch(const lzq_point* d_points, int64_t n, int32_t n_y, const do
   int64_t nb = blocks_for(n, lzq::kWavesPerBlock);
   if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_yields_batch: n too large");
   if (g_exp_variant == lzq::kExpTable256)
-    hipLaunchKernelGGL((lzq::yields_points_kernel<1, lzq::kExpTable256>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
+    hipLaunchKernelGGL((lzq::yields_points_kernel<lzq::kYB, lzq::kExpTable256>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
                        (hipStream_t)stream, d_points, n, n_y, d_T_lo, d_T_hi, d_P, g_dev_tab[dev], exp_table(dev),
                        d_out);
   else
-    hipLaunchKernelGGL((lzq::yields_points_kernel<1, lzq::kExpPoly11>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
+    hipLaunchKernelGGL((lzq::yields_points_kernel<lzq::kYB, lzq::kExpPoly11>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
                        (hipStream_t)stream, d_points, n, n_y, d_T_lo, d_T_hi, d_P, g_dev_tab[dev], exp_table(dev),
                        d_out);
   LZQ_HIP(hipGetLastError());
@@ -561,10 +710,10 @@ int lzq_sweep_grid(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, 
   int64_t nb = blocks_for(count, lzq::kWavesPerBlock);
   if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_sweep_grid: count too large for one launch");
   if (g_exp_variant == lzq::kExpTable256)
-    hipLaunchKernelGGL((lzq::yields_grid_kernel<1, lzq::kExpTable256>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
+    hipLaunchKernelGGL((lzq::yields_grid_kernel<lzq::kYB, lzq::kExpTable256>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
                        (hipStream_t)stream, *base, g, start, count, n_y, g_dev_tab[dev], exp_table(dev), d_out);
   else
-    hipLaunchKernelGGL((lzq::yields_grid_kernel<1, lzq::kExpPoly11>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
+    hipLaunchKernelGGL((lzq::yields_grid_kernel<lzq::kYB, lzq::kExpPoly11>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
                        (hipStream_t)stream, *base, g, start, count, n_y, g_dev_tab[dev], exp_table(dev), d_out);
   LZQ_HIP(hipGetLastError());
   return LZQ_OK;

@@ -24,24 +24,27 @@ def _vp(t: Optional[torch.Tensor]) -> Optional[int]:
 class Engine:
     """One engine per process/device (torch.cuda.current_device() unless given)."""
 
-    def __init__(self, device: Optional[int] = None):
+    def __init__(self, device: Optional[int] = None, lib_path: Optional[str] = None):
         if not torch.cuda.is_available():
             raise RuntimeError("lzq Engine needs a ROCm GPU (torch.cuda.is_available() is False); "
                                "there is no CPU fallback")
-        self.lib = _native.load()
+        self.lib = _native.load(lib_path)
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         with torch.cuda.device(self.device):
-            _native.check(self.lib.lzq_init(self.device.index))
+            self._check(self.lib.lzq_init(self.device.index))
 
     def tune_exp(self, variant: str) -> str:
         """Select the inner-loop exponential ('table256' default, 'poly11'); returns the previous."""
         v = {"poly11": _native.EXP_POLY11, "table256": _native.EXP_TABLE256}[variant]
         prev = self.lib.lzq_tune(_native.TUNE_EXP, v)
         if prev < 0:
-            _native.check(prev)
+            self._check(prev)
         return {_native.EXP_POLY11: "poly11", _native.EXP_TABLE256: "table256"}[prev]
 
     # -- helpers -------------------------------------------------------------------------
+    def _check(self, rc: int) -> None:
+        _native.check(rc, self.lib)
+
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
@@ -61,7 +64,7 @@ class Engine:
         out = torch.empty_like(y)
         p = to_ctypes_point(to_point(cfg, P=0.0))
         with torch.cuda.device(self.device):
-            _native.check(self.lib.lzq_aov_batch(ctypes.byref(p), _vp(y), y.numel(), _vp(out), self._stream()))
+            self._check(self.lib.lzq_aov_batch(ctypes.byref(p), _vp(y), y.numel(), _vp(out), self._stream()))
         return out
 
     # -- fpy:222-223 ------------------------------------------------------------------------
@@ -70,7 +73,7 @@ class Engine:
         out = torch.empty_like(T)
         p = to_ctypes_point(to_point(cfg, P=0.0))
         with torch.cuda.device(self.device):
-            _native.check(self.lib.lzq_jchi_batch(ctypes.byref(p), _vp(T), T.numel(), _vp(out), self._stream()))
+            self._check(self.lib.lzq_jchi_batch(ctypes.byref(p), _vp(T), T.numel(), _vp(out), self._stream()))
         return out
 
     # -- fpy:231-267 + epilogue ----------------------------------------------------------------
@@ -84,7 +87,7 @@ class Engine:
         th = None if T_hi is None else self._f64(T_hi)
         Pv = None if P is None else self._f64(P)
         with torch.cuda.device(self.device):
-            _native.check(self.lib.lzq_yields_batch(_vp(d_pts), n, int(n_y), _vp(tl), _vp(th), _vp(Pv), _vp(out),
+            self._check(self.lib.lzq_yields_batch(_vp(d_pts), n, int(n_y), _vp(tl), _vp(th), _vp(Pv), _vp(out),
                                                     self._stream()))
         return out
 
@@ -107,7 +110,7 @@ class Engine:
         if out is None:
             out = torch.empty((count, 6), dtype=torch.float64, device=self.device)
         with torch.cuda.device(self.device):
-            _native.check(self.lib.lzq_sweep_grid(ctypes.byref(base), arr, len(axes), int(start), int(count),
+            self._check(self.lib.lzq_sweep_grid(ctypes.byref(base), arr, len(axes), int(start), int(count),
                                                   int(n_y), _vp(out), self._stream()))
         self._keepalive = dev_vals  # axis buffers must outlive the async launch
         return out
@@ -117,7 +120,7 @@ class Engine:
         l = self._f64(lam).reshape(-1)
         out = torch.empty_like(l)
         with torch.cuda.device(self.device):
-            _native.check(self.lib.lzq_p_closed_form(_vp(l), l.numel(), _vp(out), self._stream()))
+            self._check(self.lib.lzq_p_closed_form(_vp(l), l.numel(), _vp(out), self._stream()))
         return out
 
     # -- LZ propagator (north_star (1)) ------------------------------------------------------
@@ -130,7 +133,7 @@ class Engine:
         x = self._f64(xi).reshape(m.shape)
         out = torch.empty(m.shape[0], dtype=torch.float64, device=self.device)
         with torch.cuda.device(self.device):
-            _native.check(self.lib.lzq_lz_propagate(_vp(m), _vp(d), _vp(x), m.shape[0], m.shape[1], float(v_w),
+            self._check(self.lib.lzq_lz_propagate(_vp(m), _vp(d), _vp(x), m.shape[0], m.shape[1], float(v_w),
                                                     float(xi_half_window), int(steps_per_crossing), _vp(out),
                                                     self._stream()))
         return out

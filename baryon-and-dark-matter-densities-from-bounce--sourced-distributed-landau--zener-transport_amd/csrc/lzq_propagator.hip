@@ -10,8 +10,9 @@
 //   i d psi/dt = H psi,   H(xi) = [[D(xi), m_c], [m_c, -D(xi)]]
 // with crossings c = 0..N-1 at xi_c (increasing).  On cell c, D(xi) = s_c |Delta'_c| (xi - xi_c),
 // s_c = (-1)^c, and the coupling is m_c.  Interior cell edges b_c are where neighbouring
-// linear pieces meet (D continuous, |D| maximal); the outer edges are xi_0 - W and
-// xi_{N-1} + W.  psi starts in the adiabatic state that is chi-like at the first edge; the
+// linear pieces meet (D continuous, |D| maximal); the outer edges are xi_0 - W_0 and
+// xi_{N-1} + W_{N-1} with W_c = K * L_c, L_c = sqrt(v_w/|Delta'_c|) * max(1, sqrt(delta_c))
+// the LZ length of crossing c (delta_c = m_c^2 / (2 v_w |Delta'_c|)) and K = window_lz.  psi starts in the adiabatic state that is chi-like at the first edge; the
 // result is the conversion probability 1 - |<chi-like adiabatic state | psi>|^2 at the last.
 //
 // Integrator: fourth-order Magnus (two Gauss-Legendre nodes) with the exact SU(2)
@@ -35,6 +36,12 @@ struct Cplx {
   double re, im;
 };
 
+// LZ length of a crossing in xi: sqrt(v_w/|Delta'|) * max(1, sqrt(delta)).
+__device__ __forceinline__ double lz_length(double m, double a, double v_w) {
+  const double delta = m * m / (2.0 * v_w * a);
+  return sqrt(v_w / a) * fmax(1.0, sqrt(delta));
+}
+
 // Adiabatic eigenvector of [[d, m],[m, -d]] with eigenvalue -sign * sqrt(d^2+m^2) ...
 // returns the eigenvector (u0, u1) (real) of the state that is chi-like (|u0| >= |u1|).
 __device__ __forceinline__ void chi_like_adiabatic(double d, double m, double& u0, double& u1) {
@@ -53,7 +60,7 @@ __device__ __forceinline__ void chi_like_adiabatic(double d, double m, double& u
 __global__ __launch_bounds__(kPropBlock) void lz_propagate_kernel(const double* __restrict__ m_mix,
                                                                   const double* __restrict__ dprime,
                                                                   const double* __restrict__ xi, int64_t n,
-                                                                  int32_t n_cross, double v_w, double W,
+                                                                  int32_t n_cross, double v_w, double K,
                                                                   int32_t S, double* __restrict__ P_out) {
   const int64_t p = (int64_t)blockIdx.x * kPropBlock + threadIdx.x;
   if (p >= n) return;
@@ -64,7 +71,7 @@ __global__ __launch_bounds__(kPropBlock) void lz_propagate_kernel(const double* 
 
   // left edge of cell 0
   double a0 = fabs(dp[0]);
-  double left = xc[0] - W;
+  double left = xc[0] - K * lz_length(mm[0], a0, v_w);
   double D_left = a0 * (left - xc[0]);  // s_0 = +1
   double u0, u1;
   chi_like_adiabatic(D_left, mm[0], u0, u1);
@@ -80,7 +87,7 @@ __global__ __launch_bounds__(kPropBlock) void lz_propagate_kernel(const double* 
       const double an = fabs(dp[c + 1]);
       right = (ac * xcc + an * xc[c + 1]) / (ac + an);  // D continuous at the turning point
     } else {
-      right = xcc + W;
+      right = xcc + K * lz_length(mc, ac, v_w);
     }
     const double h = (right - left) / (double)S;   // step in xi
     const double dt = h * inv_vw;                  // step in t
@@ -125,16 +132,16 @@ __global__ __launch_bounds__(kPropBlock) void lz_propagate_kernel(const double* 
 int lzq_set_error(int code, const char* msg);
 
 extern "C" int lzq_lz_propagate(const double* d_m_mix, const double* d_dprime, const double* d_xi, int64_t n,
-                                int32_t n_cross, double v_w, double xi_half_window, int32_t steps_per_crossing,
+                                int32_t n_cross, double v_w, double window_lz, int32_t steps_per_crossing,
                                 double* d_P, void* stream) {
-  if (n < 0 || n_cross <= 0 || steps_per_crossing <= 0 || !(v_w > 0.0) || !(xi_half_window > 0.0) ||
+  if (n < 0 || n_cross <= 0 || steps_per_crossing <= 0 || !(v_w > 0.0) || !(window_lz > 0.0) ||
       (n > 0 && (!d_m_mix || !d_dprime || !d_xi || !d_P)))
     return lzq_set_error(LZQ_EINVAL, "lzq_lz_propagate: bad arguments");
   if (n == 0) return LZQ_OK;
   const int64_t nb = (n + lzq::kPropBlock - 1) / lzq::kPropBlock;
   if (nb > 2147483647LL) return lzq_set_error(LZQ_EINVAL, "lzq_lz_propagate: n too large");
   hipLaunchKernelGGL(lzq::lz_propagate_kernel, dim3((unsigned)nb), dim3(lzq::kPropBlock), 0, (hipStream_t)stream,
-                     d_m_mix, d_dprime, d_xi, n, n_cross, v_w, xi_half_window, steps_per_crossing, d_P);
+                     d_m_mix, d_dprime, d_xi, n, n_cross, v_w, window_lz, steps_per_crossing, d_P);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return lzq_set_error(LZQ_EHIP, hipGetErrorString(e));
   return LZQ_OK;

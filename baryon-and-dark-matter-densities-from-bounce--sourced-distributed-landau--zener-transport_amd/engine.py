@@ -124,8 +124,9 @@ class Engine:
         return out
 
     # -- LZ propagator (north_star (1)) ------------------------------------------------------
-    def lz_propagate(self, m_mix, dprime, xi, v_w: float, xi_half_window: float,
+    def lz_propagate(self, m_mix, dprime, xi, v_w: float, window_lz: float,
                      steps_per_crossing: int) -> torch.Tensor:
+        """Coherent LZ conversion probability per point (arrays [n] or [n, n_cross])."""
         m = self._f64(m_mix)
         if m.dim() == 1:
             m = m.reshape(-1, 1)
@@ -134,7 +135,7 @@ class Engine:
         out = torch.empty(m.shape[0], dtype=torch.float64, device=self.device)
         with torch.cuda.device(self.device):
             self._check(self.lib.lzq_lz_propagate(_vp(m), _vp(d), _vp(x), m.shape[0], m.shape[1], float(v_w),
-                                                    float(xi_half_window), int(steps_per_crossing), _vp(out),
+                                                    float(window_lz), int(steps_per_crossing), _vp(out),
                                                     self._stream()))
         return out
 

@@ -92,6 +92,8 @@ def main():
     ap.add_argument("--points", type=int, default=1_000_000, help="points per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL over xGMI, default) | gloo (rehearsal of the N>1 path on one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -99,9 +101,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"[bench] WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE", file=sys.stderr)
+    local = local % max(1, torch.cuda.device_count())  # gloo rehearsal: several ranks may share a GPU
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
 
     eng = importlib.import_module(PKG + ".engine").Engine(local)
     axes = grid_axes(world)
@@ -124,7 +130,12 @@ def main():
             e1.record(stream)
             k_ev.append((e0, e1))
         if world > 1:
-            dist.all_gather_into_tensor(gathered, local_tab)  # RCCL over xGMI
+            if args.dist_backend == "nccl":
+                dist.all_gather_into_tensor(gathered, local_tab)  # RCCL over xGMI
+            else:
+                parts = [torch.empty((per, 6), dtype=torch.float64) for _ in range(world)]
+                dist.all_gather(parts, local_tab.cpu())
+                gathered.copy_(torch.cat(parts))
 
     for _ in range(args.warmup):
         step(False)
@@ -141,13 +152,16 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in k_ev]))
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=eng.device)
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64,
+                         device=eng.device if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
 
-    # sanity: the table is finite and the C1-equivalent ratio Y_B/P holds on this shard
-    tab = local_tab[:4096].cpu().numpy()
-    assert np.all(np.isfinite(tab)), "non-finite yields"
+    # sanity: every shard of the gathered table is finite and the gather put rank r's rows at
+    # [r*per, (r+1)*per)
+    assert bool(torch.isfinite(gathered).all()), "non-finite yields"
+    if world > 1:
+        assert torch.equal(gathered[start:start + per], local_tab), "all-gather misplaced a shard"
 
     if rank == 0:
         achieved = FLOP_PER_POINT * per / (kern_ms / 1e3) / 1e12
@@ -168,7 +182,8 @@ def main():
                                    "|Delta'|=logspace(-3,1,1000*N), v_w=0.30, delta->P->dense Y_B (n_y=8000, "
                                    "nz=1200) + epilogue; 1e6 points per GPU per step",
                        "points_per_gpu": per, "global_points_per_step": total, "n_y": 8000, "nz": 1200,
-                       "parallelism": f"grid-sharded x{world}, RCCL all-gather of 48 B/point yield tables"},
+                       "parallelism": f"grid-sharded x{world}, {'RCCL' if args.dist_backend == 'nccl' else args.dist_backend} "
+                                      f"all-gather of 48 B/point yield tables"},
             "roofline": {"bound": "fp64-valu", "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_FP64_TFLOPS, "traffic": None,
                          "kernel": "yields_grid_kernel", "kernel_ms": kern_ms,

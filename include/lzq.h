@@ -146,13 +146,17 @@ int lzq_p_closed_form(const double* d_lambda, int64_t n, double* d_P, void* stre
 
 /* ---- Landau-Zener propagator (north_star (1); no reference counterpart) --------------- */
 /* Coherent two-level propagation through n_cross sequential linear avoided crossings per
- * point, i dpsi/dt = H(t) psi, H = [[D(t), m],[m, -D(t)]], D piecewise linear with slope
- * v_w*Delta'_c near crossing c.  See DESIGN.md "LZ propagator" for the profile, the Magnus
- * integrator and its stated tolerance.  d_m_mix / d_dprime: [n][n_cross] row-major;
- * d_xi: [n][n_cross] crossing positions; out d_P[n] = conversion probability
- * 1 - |<diabatic chi|psi(+inf)>|^2. */
+ * point: i dpsi/dt = H(t) psi, H = [[D(xi), m_c],[m_c, -D(xi)]], xi = v_w t, D piecewise linear
+ * with slope (-1)^c |Delta'_c| through crossing c at xi_c (continuous at the turning points
+ * between crossings).  The outer half-windows are window_lz LZ lengths of the first/last
+ * crossing (L = sqrt(v_w/|Delta'|) max(1, sqrt(delta))); each cell gets steps_per_crossing
+ * fourth-order Magnus steps (exact SU(2) exponentials).  Arrays are [n][n_cross] row-major
+ * device buffers (xi increasing per point).  Output d_P[n]: conversion probability
+ * 1 - |<chi-like adiabatic state | psi_end>|^2, psi_start = chi-like adiabatic state.  For one
+ * crossing this tends to 1 - exp(-2 pi delta) (fpy:183-184, PAPER eq.(9)); DESIGN.md §6
+ * states the window / step tolerances. */
 int lzq_lz_propagate(const double* d_m_mix, const double* d_dprime, const double* d_xi,
-                     int64_t n, int32_t n_cross, double v_w, double xi_half_window,
+                     int64_t n, int32_t n_cross, double v_w, double window_lz,
                      int32_t steps_per_crossing, double* d_P, void* stream);
 
 #ifdef __cplusplus

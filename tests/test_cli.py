@@ -1,0 +1,108 @@
+"""Driver behaviour that needs no GPU, against the reference's own recorded CLI output
+(tests/golden/golden_cli.json): missing --config, --write-template bytes, regime 'auto',
+unknown keys, the config schema and the plug-in hook's module order."""
+import contextlib
+import io
+import json
+import os
+import sys
+import types
+
+import pytest
+
+from conftest import golden, pkg
+
+
+def cli_case(name):
+    return next(c for c in golden("golden_cli.json") if c["name"] == name)
+
+
+def run_cli(argv, cwd):
+    old = os.getcwd()
+    buf = io.StringIO()
+    try:
+        os.chdir(cwd)
+        with contextlib.redirect_stdout(buf):
+            pkg("cli").main(argv)
+    finally:
+        os.chdir(old)
+    return buf.getvalue()
+
+
+def test_no_config(tmp_path):
+    assert run_cli([], tmp_path) == cli_case("no_config")["stdout"]
+
+
+def test_write_template_bytes(tmp_path):
+    c = cli_case("write_template")
+    out = run_cli(["--write-template", "--config", "tmpl.json"], tmp_path)
+    assert out == c["stdout"]
+    assert (tmp_path / "tmpl.json").read_text() == c["template_text"]
+
+
+def test_regime_auto_raises_like_reference(tmp_path):
+    c = cli_case("regime_auto")
+    (tmp_path / "auto.json").write_text(c["config_text"])
+    with pytest.raises(UnboundLocalError) as ei:
+        run_cli(["--config", "auto.json"], tmp_path)
+    assert str(ei.value) in c["stderr_last_line"]
+
+
+def test_unknown_key_typeerror(tmp_path):
+    (tmp_path / "bad.json").write_text(json.dumps({"not_a_field": 1}))
+    with pytest.raises(TypeError):
+        pkg("config").load_config(str(tmp_path / "bad.json"))
+
+
+def test_ode_fallback_configs_refused(tmp_path):
+    (tmp_path / "ode.json").write_text(json.dumps({"P_chi_to_B": 0.1, "Gamma_wash_over_H": 1e-3}))
+    with pytest.raises(NotImplementedError):
+        run_cli(["--config", "ode.json"], tmp_path)
+
+
+def test_config_schema_order_matches_reference_dump():
+    """yields_out.json 'inputs' = cfg.__dict__ + P_used in dataclass order (fpy:424)."""
+    ref = json.loads(cli_case("equal_mass")["yields_out_json"])
+    cfgm = pkg("config")
+    path = os.path.join(os.path.dirname(__file__), "_tmp_cfg.json")
+    try:
+        with open(path, "w") as f:
+            f.write(cli_case("equal_mass")["config_text"])
+        cfg = cfgm.load_config(path)
+    finally:
+        os.remove(path)
+    ours = {**cfg.__dict__, "P_used": cfg.P_chi_to_B}
+    assert list(ours) == list(ref["inputs"]) and ours == ref["inputs"]
+
+
+def test_plugin_hook_order_and_swallowing(monkeypatch):
+    lz = pkg("lz")
+    a = types.ModuleType("extended_LZ_lambda")
+    a.compute_prob_from_profile = lambda path, v_w: 1.7       # clamped to 1.0
+    b = types.ModuleType("transport_from_profile")
+    b.compute_prob_from_profile = lambda path, v_w: 0.25
+    monkeypatch.setitem(sys.modules, "extended_LZ_lambda", a)
+    monkeypatch.setitem(sys.modules, "transport_from_profile", b)
+    assert lz.try_compute_P_from_profile("x.csv", 0.3) == 1.0    # earlier module wins
+    a.compute_prob_from_profile = lambda path, v_w: 1 / 0         # raises -> None
+    assert lz.try_compute_P_from_profile("x.csv", 0.3) is None
+    monkeypatch.delitem(sys.modules, "extended_LZ_lambda")
+    monkeypatch.setitem(sys.modules, "extended_LZ_lambda", None)  # import fails -> skipped
+    assert lz.try_compute_P_from_profile("x.csv", 0.3) == 0.25
+
+
+def test_maybe_P_messages(capsys):
+    lz = pkg("lz")
+    cfg = pkg("config").Config(P_chi_to_B=0.2)
+    assert lz.maybe_P(cfg, None) == 0.2
+    assert lz.maybe_P(cfg, "missing.csv") == 0.2
+    assert capsys.readouterr().out == "[warn] Could not compute P from profile automatically; falling back to config.\n"
+    with pytest.raises(RuntimeError, match="P_chi_to_B is not set"):
+        lz.maybe_P(pkg("config").Config(), None)
+
+
+def test_incoherent_composition():
+    lz = pkg("lz")
+    assert lz.p_incoherent([0.3]) == pytest.approx(0.3)
+    assert lz.p_incoherent([0.5, 0.2, 0.9]) == pytest.approx(0.5)
+    assert lz.p_incoherent([1.0, 1.0]) == pytest.approx(0.0)

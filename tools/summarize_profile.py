@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""Condense a gpurun_out/prof run (tools/gpu_profile.sh) into profiles/<tag>/:
+kernel_stats.csv (rocprofv3 --stats of the bench command), the PMC counter CSVs, and
+pmc_summary.json with per-point / per-wave-node figures for the quadrature kernel."""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NODES_PER_POINT = 8000 * 1200
+WAVE_NODES_PER_POINT = NODES_PER_POINT // 64
+
+
+def agg(path, key="grid"):
+    rows = list(csv.DictReader(open(path)))
+    tot = defaultdict(float)
+    disp = set()
+    dur = {}
+    meta = {}
+    for r in rows:
+        if key in r["Kernel_Name"]:
+            tot[r["Counter_Name"]] += float(r["Counter_Value"])
+            disp.add(r["Dispatch_Id"])
+            dur[r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            meta = {k: r[k] for k in ("VGPR_Count", "Accum_VGPR_Count", "SGPR_Count", "LDS_Block_Size",
+                                      "Scratch_Size", "Workgroup_Size", "Grid_Size")}
+    return dict(tot), len(disp), sum(dur.values()) / max(1, len(dur)), meta
+
+
+def main():
+    src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "prof")
+    tag = sys.argv[2] if len(sys.argv) > 2 else "round1"
+    dst = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    for f in ("bench_traced.json", "bench_plain.json"):
+        if os.path.exists(os.path.join(src, f)):
+            shutil.copy(os.path.join(src, f), os.path.join(dst, f))
+    points = 200000
+    out = {"pmc_points_per_launch": points, "counters": {}}
+    for g in ("fetch", "write", "sq", "inst"):
+        p = os.path.join(src, f"pmc_{g}", "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        shutil.copy(p, os.path.join(dst, f"pmc_{g}.csv"))
+        tot, nd, dur_ns, meta = agg(p)
+        assert nd == 1, (g, nd)
+        out["counters"].update(tot)
+        out["kernel_meta"] = meta
+        out.setdefault("pmc_kernel_ns", {})[g] = dur_ns
+    c = out["counters"]
+    # gfx950: FETCH_SIZE reads 1/2 of wide coalesced streaming reads (MI355X_MICROARCH.md §HBM);
+    # the kernel's reads are scalar/uniform loads, so we report both the raw and the x2 bound.
+    fetch_b = c.get("FETCH_SIZE", 0.0) * 1024
+    write_b = c.get("WRITE_SIZE", 0.0) * 1024
+    out["hbm_bytes_per_point"] = {"fetch_raw": fetch_b / points, "fetch_x2": 2 * fetch_b / points,
+                                  "write": write_b / points, "total_upper": (2 * fetch_b + write_b) / points}
+    if "SQ_INSTS_VALU" in c:
+        wn = points * WAVE_NODES_PER_POINT
+        ns = out["pmc_kernel_ns"]["inst"]
+        clk = c["GRBM_GUI_ACTIVE"] / 8 / (ns * 1e-9)  # summed over 8 XCDs
+        out["valu_insts_per_wave_node"] = c["SQ_INSTS_VALU"] / wn
+        out["lds_insts_per_wave_node"] = c["SQ_INSTS_LDS"] / wn
+        out["clock_ghz"] = clk / 1e9
+        out["cycles_per_wave_node_per_simd"] = 1024 * (ns * 1e-9) * clk / wn
+    if "SQ_WAVE_CYCLES" in c:
+        wc = c["SQ_WAVE_CYCLES"]
+        out["wave_time_split"] = {k: c[k] / wc for k in ("SQ_ACTIVE_INST_VALU", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY",
+                                                         "SQ_ACTIVE_INST_LDS")}
+        out["lds_bank_conflict_cycles_per_lds_inst"] = c["SQ_LDS_BANK_CONFLICT"] / max(1.0, c.get("SQ_INSTS_LDS", 0) or
+                                                                                        c["SQ_ACTIVE_INST_LDS"])
+    with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps({k: v for k, v in out.items() if k != "counters"}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -86,7 +86,7 @@ def load(path: str | None = None):
     L.lzq_aov_batch.argtypes = [P(LzqPoint), vp, i64, vp, vp]
     L.lzq_jchi_batch.argtypes = [P(LzqPoint), vp, i64, vp, vp]
     L.lzq_yields_batch.argtypes = [vp, i64, i32, vp, vp, vp, vp, vp]
-    L.lzq_sweep_grid.argtypes = [P(LzqPoint), P(LzqAxis), i32, i64, i64, i32, vp, vp]
+    L.lzq_sweep_grid.argtypes = [P(LzqPoint), P(LzqAxis), i32, i64, i64, i32, vp, vp, vp]
     L.lzq_p_closed_form.argtypes = [vp, i64, vp, vp]
     L.lzq_lz_propagate.argtypes = [vp, vp, vp, i64, i32, d, d, i32, vp, vp]
     for name in EXPORTS:

@@ -478,6 +478,7 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void yields_points_kernel(co
 template <int YB, int EXPV>
 __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void yields_grid_kernel(lzq_point base, GridSpec grid, int64_t start,
                                                             int64_t count, int32_t n_y,
+                                                            const double* __restrict__ Pov,
                                                             const ZNode* __restrict__ zt,
                                                             const double* __restrict__ gtab,
                                                             lzq_yield* __restrict__ out) {
@@ -494,7 +495,8 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void yields_grid_kernel(lzq_
   const int64_t local = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (local >= count) return;
   lzq_point pt;
-  const double P = grid_point(base, grid, start + local, pt);
+  const double Pg = grid_point(base, grid, start + local, pt);
+  const double P = Pov ? Pov[local] : Pg;
   QuadSetup s = quad_setup(pt, P, pt.T_min_over_Tp * pt.T_p_GeV, pt.T_max_over_Tp * pt.T_p_GeV, n_y);
   const double Y_B = yb_wave<YB, EXPV>(s, zt, tab, lane);
   if (lane == 0) out[local] = epilogue(pt, Y_B, P);
@@ -710,7 +712,7 @@ int lzq_yields_batch(const lzq_point* d_points, int64_t n, int32_t n_y, const do
 }
 
 int lzq_sweep_grid(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int64_t start, int64_t count,
-                   int32_t n_y, lzq_yield* d_out, void* stream) {
+                   int32_t n_y, const double* d_P, lzq_yield* d_out, void* stream) {
   if (!base || n_axes < 0 || n_axes > LZQ_MAX_AXES || (n_axes > 0 && !axes) || start < 0 || count < 0 ||
       (count > 0 && !d_out))
     return fail(LZQ_EINVAL, "lzq_sweep_grid: bad arguments");
@@ -746,10 +748,10 @@ int lzq_sweep_grid(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, 
   if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_sweep_grid: count too large for one launch");
   if (g_exp_variant == lzq::kExpTable256)
     hipLaunchKernelGGL((lzq::yields_grid_kernel<lzq::kYB, lzq::kExpTable256>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
-                       (hipStream_t)stream, *base, g, start, count, n_y, g_dev_tab[dev], exp_table(dev), d_out);
+                       (hipStream_t)stream, *base, g, start, count, n_y, d_P, g_dev_tab[dev], exp_table(dev), d_out);
   else
     hipLaunchKernelGGL((lzq::yields_grid_kernel<lzq::kYB, lzq::kExpPoly11>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
-                       (hipStream_t)stream, *base, g, start, count, n_y, g_dev_tab[dev], exp_table(dev), d_out);
+                       (hipStream_t)stream, *base, g, start, count, n_y, d_P, g_dev_tab[dev], exp_table(dev), d_out);
   LZQ_HIP(hipGetLastError());
   return LZQ_OK;
 }

@@ -93,9 +93,11 @@ class Engine:
 
     # -- grid sweep ----------------------------------------------------------------------------
     def sweep(self, base_cfg, axes: Sequence[tuple], start: int, count: int, n_y: int = 8000,
-              out: Optional[torch.Tensor] = None, P: Optional[float] = None) -> torch.Tensor:
+              out: Optional[torch.Tensor] = None, P: Optional[float] = None,
+              P_points: Optional[torch.Tensor] = None) -> torch.Tensor:
         """axes: sequence of (field_name, values) (C order, last fastest); field names are
-        the lzq_point double fields or 'delta_LZ' / 'm_mix' / 'dprime'."""
+        the lzq_point double fields or 'delta_LZ' / 'm_mix' / 'dprime'.  P_points: optional
+        per-point P override ([count], device), e.g. from lz_propagate (config C5)."""
         if len(axes) > _native.LZQ_MAX_AXES:
             raise ValueError(f"at most {_native.LZQ_MAX_AXES} sweep axes")
         dev_vals = [self._f64(v).reshape(-1) for _, v in axes]
@@ -110,8 +112,11 @@ class Engine:
         if out is None:
             out = torch.empty((count, 6), dtype=torch.float64, device=self.device)
         with torch.cuda.device(self.device):
+            Pp = None if P_points is None else self._f64(P_points).reshape(-1)
+            if Pp is not None and Pp.numel() != count:
+                raise ValueError("P_points must have `count` entries")
             self._check(self.lib.lzq_sweep_grid(ctypes.byref(base), arr, len(axes), int(start), int(count),
-                                                  int(n_y), _vp(out), self._stream()))
+                                                  int(n_y), _vp(Pp), _vp(out), self._stream()))
         self._keepalive = dev_vals  # axis buffers must outlive the async launch
         return out
 

@@ -43,12 +43,32 @@ EQUAL_MASS = {  # /root/reference/yields_config_equal_mass.json
 
 
 @dataclass
+class CrossingSpec:
+    """Multi-crossing bounce profile per grid point (BASELINE config C5; no reference
+    counterpart).  Crossing c of the point with grid values (m_mix, |Delta'|)
+    has m_c = m_mix (1 + jitter a_c), |Delta'_c| = |Delta'| (1 + jitter b_c) and position
+    xi_c = L (spacing_lz c + jitter d_c), L = sqrt(v_w/|Delta'|) max(1, sqrt(delta)), with
+    (a, b, d) ~ U(-1, 1) drawn once from numpy default_rng(seed).  P is the coherent
+    conversion probability through all crossings (lzq_lz_propagate)."""
+    n_cross: int = 8
+    spacing_lz: float = 40.0
+    jitter: float = 0.1
+    window_lz: float = 20.0
+    steps: int = 2000
+    seed: int = 5
+
+    def pattern(self) -> np.ndarray:
+        return np.random.default_rng(self.seed).uniform(-1.0, 1.0, (3, self.n_cross))
+
+
+@dataclass
 class SweepSpec:
     name: str
     base: dict
     axes: List[Tuple[str, np.ndarray]]
     n_y: int = 8000
     notes: str = ""
+    crossings: Optional[CrossingSpec] = None
 
     @property
     def total(self) -> int:
@@ -66,8 +86,36 @@ class SweepSpec:
         return out
 
     def to_json(self) -> dict:
-        return {"name": self.name, "base": self.base, "n_y": self.n_y, "notes": self.notes,
-                "axes": [{"field": n, "values": [float(x) for x in v]} for n, v in self.axes]}
+        d = {"name": self.name, "base": self.base, "n_y": self.n_y, "notes": self.notes,
+             "axes": [{"field": n, "values": [float(x) for x in v]} for n, v in self.axes]}
+        if self.crossings is not None:
+            d["crossings"] = dict(self.crossings.__dict__)
+        return d
+
+    def crossing_arrays(self, start: int, count: int, device):
+        """Per-point crossing parameters [count, n_cross] (torch, on `device`) for C5."""
+        import torch
+        cs = self.crossings
+        names = [n for n, _ in self.axes]
+        if "m_mix" not in names or "dprime" not in names:
+            raise ValueError("a multi-crossing spec needs m_mix and dprime axes")
+        idx = torch.arange(start, start + count, dtype=torch.int64, device=device)
+        vals = {}
+        stride = 1
+        for name, v in reversed(self.axes):
+            t = torch.as_tensor(np.asarray(v, dtype=np.float64), device=device)
+            vals[name] = t[(idx // stride) % len(v)]
+            stride *= len(v)
+        v_w = vals["v_w"] if "v_w" in vals else torch.full_like(vals["m_mix"], float(self.base["v_w"]))
+        m0, d0 = vals["m_mix"], vals["dprime"].abs()
+        delta0 = m0 * m0 / (2.0 * v_w * d0)
+        L = torch.sqrt(v_w / d0) * torch.clamp(torch.sqrt(delta0), min=1.0)
+        a, b, dd = (torch.as_tensor(r, device=device) for r in cs.pattern())
+        c = torch.arange(cs.n_cross, dtype=torch.float64, device=device)
+        m = m0[:, None] * (1.0 + cs.jitter * a[None, :])
+        dp = d0[:, None] * (1.0 + cs.jitter * b[None, :])
+        xi = L[:, None] * (cs.spacing_lz * c[None, :] + cs.jitter * dd[None, :])
+        return m.contiguous(), dp.contiguous(), xi.contiguous(), v_w
 
 
 def _axis_from_json(a: dict) -> Tuple[str, np.ndarray]:
@@ -90,8 +138,9 @@ def spec_from_json(d: dict) -> SweepSpec:
         with open(d["config"]) as f:
             base.update(json.load(f))
     base.update(d.get("base", {}))
+    cr = CrossingSpec(**d["crossings"]) if d.get("crossings") else None
     return SweepSpec(d.get("name", "custom"), base, [_axis_from_json(a) for a in d["axes"]], int(d.get("n_y", 8000)),
-                     d.get("notes", ""))
+                     d.get("notes", ""), cr)
 
 
 def builtin_specs() -> dict:
@@ -104,6 +153,10 @@ def builtin_specs() -> dict:
         "C3": SweepSpec("C3", dict(EQUAL_MASS),
                         [("m_chi_GeV", ls(0, 3.5, 100)), ("I_p", lin(0.05, 1, 100)), ("delta_LZ", ls(-4, 0, 1000))],
                         notes="m_chi crosses T=m/3 inside the window"),
+        "C5": SweepSpec("C5", dict(EQUAL_MASS),
+                        [("m_mix", ls(-3, 0, 1000)), ("dprime", ls(-3, 1, 1000))],
+                        notes="C2 grid, 8 jittered sequential crossings per point, coherent P (propagator)",
+                        crossings=CrossingSpec()),
         "C4": SweepSpec("C4", dict(EQUAL_MASS),
                         [("beta_over_H", ls(1, 3, 10)), ("I_p", lin(0.05, 1, 100)), ("v_w", lin(0.05, 0.95, 10)),
                          ("source_shape_sigma_y", lin(3, 30, 10)), ("m_chi_GeV", ls(-1, 3.5, 10)),
@@ -203,13 +256,24 @@ def run_sweep(spec: SweepSpec, engine=None, rank: int = 0, world: int = 1, chunk
     if out_dir:
         os.makedirs(out_dir, exist_ok=True)
 
-    def compute(s, n, out):
-        engine.sweep(spec.base, spec.axes, s, n, n_y=spec.n_y, out=out)
-
-    local = run_local(compute, start, end,
+    local = run_local(make_compute(spec, engine), start, end,
                       lambda n: torch.empty((n, 6), dtype=torch.float64, device=engine.device), chunk,
                       out_dir, resume, sync=torch.cuda.synchronize, log=log)
     return gather_table(local, spec.total, rank, world, group)
+
+
+def make_compute(spec: SweepSpec, engine) -> ComputeFn:
+    """(start, count, out) -> None on the GPU: [coherent multi-crossing P ->] quadrature."""
+    def compute(s, n, out):
+        P_points = None
+        if spec.crossings is not None:
+            m, dp, xi, v_w = spec.crossing_arrays(s, n, engine.device)
+            if not bool((v_w == v_w[0]).all()):
+                raise NotImplementedError("multi-crossing sweeps need a single v_w")
+            P_points = engine.lz_propagate(m, dp, xi, float(v_w[0]), spec.crossings.window_lz,
+                                           spec.crossings.steps)
+        engine.sweep(spec.base, spec.axes, s, n, n_y=spec.n_y, out=out, P_points=P_points)
+    return compute
 
 
 def main(argv=None):
@@ -235,22 +299,14 @@ def main(argv=None):
     torch.cuda.set_device(local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    if args.limit is not None:
-        spec = SweepSpec(spec.name, spec.base, spec.axes, spec.n_y, spec.notes)
-        total = min(args.limit, spec.total)
-        spec_total = total
-    else:
-        spec_total = spec.total
+    spec_total = spec.total if args.limit is None else min(args.limit, spec.total)
 
     from .engine import Engine
     eng = Engine(local_rank)
     t0 = time.perf_counter()
     start, end = shard_range(spec_total, rank, world)
 
-    def compute(s, n, out):
-        eng.sweep(spec.base, spec.axes, s, n, n_y=spec.n_y, out=out)
-
-    local = run_local(compute, start, end,
+    local = run_local(make_compute(spec, eng), start, end,
                       lambda n: torch.empty((n, 6), dtype=torch.float64, device=eng.device), args.chunk,
                       args.out, args.resume, sync=torch.cuda.synchronize,
                       log=(print if rank == 0 else (lambda s: None)))

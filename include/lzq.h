@@ -137,9 +137,12 @@ int lzq_yields_batch(const lzq_point* d_points, int64_t n, int32_t n_y,
                      lzq_yield* d_out, void* stream);
 
 /* Cartesian sweep: points [start, start+count) of the grid base x axes[0] x ... x
- * axes[n_axes-1] (C order: last axis fastest), generated on device from the flat index. */
+ * axes[n_axes-1] (C order: last axis fastest), generated on device from the flat index.
+ * d_P: optional [count] per-point P override (e.g. lzq_lz_propagate output for multi-crossing
+ * profiles, config C5); it takes precedence over P_chi_to_B and the LZ axes. */
 int lzq_sweep_grid(const lzq_point* base, const lzq_axis* axes, int32_t n_axes,
-                   int64_t start, int64_t count, int32_t n_y, lzq_yield* d_out, void* stream);
+                   int64_t start, int64_t count, int32_t n_y, const double* d_P,
+                   lzq_yield* d_out, void* stream);
 
 /* fpy:183-184: P[i] = clamp(1 - exp(-2 pi max(lambda[i], 0)), 0, 1) (naive 1-exp kept). */
 int lzq_p_closed_form(const double* d_lambda, int64_t n, double* d_P, void* stream);

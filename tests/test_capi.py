@@ -59,16 +59,16 @@ def test_host_side_argument_validation():
     base = cfgm.to_ctypes_point(cfgm.to_point({**cfgm.default_config(), "P_chi_to_B": 0.1}))
     ax = (n.LzqAxis * 1)()
     ax[0].field, ax[0].n, ax[0].values = 99, 3, 8
-    rc = L.lzq_sweep_grid(ctypes.byref(base), ax, 1, 0, 1, 8000, 8, None)
+    rc = L.lzq_sweep_grid(ctypes.byref(base), ax, 1, 0, 1, 8000, None, 8, None)
     assert rc == -1 and b"unknown field" in L.lzq_last_error()
     ax[0].field = n.FIELD["m_mix"]
-    rc = L.lzq_sweep_grid(ctypes.byref(base), ax, 1, 0, 1, 8000, 8, None)
+    rc = L.lzq_sweep_grid(ctypes.byref(base), ax, 1, 0, 1, 8000, None, 8, None)
     assert rc == -1 and b"swept together" in L.lzq_last_error()
     ax[0].field = n.FIELD["I_p"]
-    rc = L.lzq_sweep_grid(ctypes.byref(base), ax, 1, 2, 5, 8000, 8, None)
+    rc = L.lzq_sweep_grid(ctypes.byref(base), ax, 1, 2, 5, 8000, None, 8, None)
     assert rc == -1 and b"outside grid" in L.lzq_last_error()
     base.regime = n.REGIME_OTHER
-    rc = L.lzq_sweep_grid(ctypes.byref(base), ax, 1, 0, 1, 8000, 8, None)
+    rc = L.lzq_sweep_grid(ctypes.byref(base), ax, 1, 0, 1, 8000, None, 8, None)
     assert rc == -3
 
 

@@ -74,3 +74,41 @@ def test_known_answer_identities(gpu_engine):
     assert rel_err(t[7], 4.0 / 3.0 * y0) < 1e-14
     assert rel_err(t[8], y0) < 1e-14
     assert t[9] == 0.0
+
+
+def test_c5_multicrossing_pipeline(gpu_engine):
+    """C5: per-point 8-crossing profiles -> coherent P (propagator) -> quadrature.  P_used is
+    the propagator's output (checked against the numpy restatement) and Y_B = P_used x the
+    C1 quadrature (only P differs between C2-grid points)."""
+    from lz_ref import propagate
+    sw = pkg("sweep")
+    spec = sw.builtin_specs()["C5"]
+    start, n = 123_400, 96
+    t = gpu_engine.sweep(spec.base, spec.axes, start, n, P_points=None).cpu().numpy()  # closed-form P
+    comp = sw.make_compute(spec, gpu_engine)
+    import torch
+    out = torch.empty((n, 6), dtype=torch.float64, device=gpu_engine.device)
+    comp(start, n, out)
+    o = out.cpu().numpy()
+    m, dp, xi, v_w = (x.cpu().numpy() if hasattr(x, "cpu") else x for x in spec.crossing_arrays(start, n, "cpu"))
+    for i in (0, 17, 95):
+        ref = propagate(list(m[i]), list(dp[i]), list(xi[i]), float(v_w[i]), spec.crossings.window_lz,
+                        spec.crossings.steps)
+        assert abs(o[i, 5] - ref) <= 1e-10 * max(ref, 1e-3), (i, o[i, 5], ref)
+    YB1 = 8.720885362714675e-11 / 0.14925839040304145
+    ok = o[:, 5] > 1e-8
+    assert np.all(np.abs(o[ok, 0] / o[ok, 5] / YB1 - 1) < 1e-11)
+    assert not np.array_equal(o[:, 5], t[:, 5])  # coherent multi-crossing P differs from eq.(9)
+
+
+def test_sweep_cli_end_to_end(tmp_path, gpu_engine):
+    import json
+    sw = pkg("sweep")
+    sw.main(["--spec", "C2", "--limit", "2048", "--chunk", "700", "--out", str(tmp_path)])
+    tab = np.load(tmp_path / "table.npy")
+    summ = json.loads((tmp_path / "summary.json").read_text())
+    assert tab.shape == (2048, 6) and summ["n_points"] == 2048
+    ref = gpu_engine.sweep(sw.EQUAL_MASS, sw.builtin_specs()["C2"].axes, 0, 2048).cpu().numpy()
+    assert np.array_equal(tab, ref)
+    sw.main(["--spec", "C2", "--limit", "2048", "--chunk", "700", "--out", str(tmp_path), "--resume"])
+    assert np.array_equal(np.load(tmp_path / "table.npy"), ref)

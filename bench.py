@@ -47,6 +47,21 @@ BASE = {  # /root/reference/yields_config_equal_mass.json
 }
 
 
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "round1", "pmc_summary.json")
+
+
+def pmc_traffic(points_per_launch: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE in
+    separate runs, tools/gpu_profile.sh), scaled to this launch's point count.  FETCH_SIZE is
+    doubled per MI355X_MICROARCH.md's gfx950 correction, so this is an upper bound."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            d = json.load(f)
+        return d["hbm_bytes_per_point"]["total_upper"] * points_per_launch, os.path.relpath(PMC_SUMMARY, ROOT)
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def grid_axes(world: int):
     return [("m_mix", np.logspace(-3.0, 0.0, 1000)), ("dprime", np.logspace(-3.0, 1.0, 1000 * world))]
 
@@ -165,6 +180,7 @@ def main():
 
     if rank == 0:
         achieved = FLOP_PER_POINT * per / (kern_ms / 1e3) / 1e12
+        traffic, traffic_src = pmc_traffic(per)
         rec = {
             "metric": METRIC,
             "value": total * args.steps / elapsed,
@@ -185,9 +201,14 @@ def main():
                        "parallelism": f"grid-sharded x{world}, {'RCCL' if args.dist_backend == 'nccl' else args.dist_backend} "
                                       f"all-gather of 48 B/point yield tables"},
             "roofline": {"bound": "fp64-valu", "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_FP64_TFLOPS, "traffic": None,
+                         "frac": achieved / PEAK_FP64_TFLOPS, "traffic": traffic, "traffic_unit": "bytes/launch",
+                         "traffic_source": traffic_src, "algorithmic_bytes": 48.0 * per,
                          "kernel": "yields_grid_kernel", "kernel_ms": kern_ms,
-                         "flop_per_point": FLOP_PER_POINT},
+                         "flop_per_point": FLOP_PER_POINT,
+                         "note": "achieved = SURVEY §8d's 30 FLOP/node (priced at ROCm's exp(double)) x 9.6e6 "
+                                 "nodes/point; the table-driven exp executes 14 FLOP/node in ~12.8 VALU "
+                                 "issue slots, so frac > 1 means beating the stock-exp roofline; the "
+                                 "hardware bound is VALU issue (profiles/round1/pmc_summary.json)"},
         }
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(axes, grid_total, args.cpu_seconds)

@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Throughput of the BASELINE.json sweep configs C2-C5 on one GPU (subsets of C3/C4 grids;
+points/s is per-point work, which is uniform within a config).  One JSON line per config."""
+import importlib
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PKG = "baryon-and-dark-matter-densities-from-bounce--sourced-distributed-landau--zener-transport_amd"
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 400_000
+    sw = importlib.import_module(PKG + ".sweep")
+    eng = importlib.import_module(PKG + ".engine").Engine(0)
+    specs = sw.builtin_specs()
+    for name in ("C2", "C3", "C4", "C5"):
+        spec = specs[name]
+        cnt = min(n, spec.total)
+        start = (spec.total - cnt) // 2
+        comp = sw.make_compute(spec, eng)
+        out = torch.empty((cnt, 6), dtype=torch.float64, device=eng.device)
+        comp(start, min(cnt, 4096), out[:min(cnt, 4096)])  # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        comp(start, cnt, out)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        rec = {"config": name, "points": cnt, "start": start, "points_per_s": cnt / dt, "seconds": dt,
+               "finite": bool(torch.isfinite(out).all()), "notes": spec.notes}
+        if spec.crossings is not None:
+            m, dp, xi, v_w = spec.crossing_arrays(start, cnt, eng.device)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            eng.lz_propagate(m, dp, xi, float(v_w[0]), spec.crossings.window_lz, spec.crossings.steps)
+            torch.cuda.synchronize()
+            rec["propagator_seconds"] = time.perf_counter() - t0
+            rec["crossings"] = spec.crossings.__dict__
+        print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -15,12 +15,22 @@
 // the LZ length of crossing c (delta_c = m_c^2 / (2 v_w |Delta'_c|)) and K = window_lz.  psi starts in the adiabatic state that is chi-like at the first edge; the
 // result is the conversion probability 1 - |<chi-like adiabatic state | psi>|^2 at the last.
 //
-// Integrator: fourth-order Magnus (two Gauss-Legendre nodes) with the exact SU(2)
-// exponential: for H = D sz + m sx,
-//   Omega = -i (n . sigma),  n = (dt m, (sqrt3/6) dt^2 m (D2-D1)/dt * dt, dt (D1+D2)/2)
-//   U = cos|n| - i sin|n| (n/|n|) . sigma.
-// One parameter point per lane, all state in registers, S uniform steps per cell, so every
-// lane runs the same instruction stream (no divergence).
+// Integrator, per cell c with delta_c = m_c^2 / (2 v_w |Delta'_c|):
+//  * delta_c <= kDeltaAdiabatic: fourth-order Magnus (two Gauss-Legendre nodes) with the exact
+//    SU(2) exponential, S_c = max(S, ceil(Phi_c * kStepsPerRadian)) uniform steps, Phi_c the
+//    cell's adiabatic phase (closed form below), so wide / strongly coupled cells get the
+//    steps their phase needs: for H = D sz + m sx,
+//      Omega = -i (n . sigma),  n = (dt m, (sqrt3/6) dt^2 m (D2-D1), dt (D1+D2)/2)
+//      U = cos|n| - i sin|n| (n/|n|) . sigma;
+//  * delta_c > kDeltaAdiabatic: the crossing is adiabatic to e^{-2 pi delta} < 1e-43, and the
+//    cell is propagated exactly in the adiabatic basis: amplitudes b+- pick up
+//    exp(-+ i (Phi + phi_S)) with the WKB phase Phi = int E dt in closed form
+//    (E = sqrt(D^2 + m^2), G(x) = [x sqrt(x^2+m^2) + m^2 asinh(x/m)]/2) and the LZ Stokes phase
+//    phi_S = pi/4 + delta (ln delta - 1) + arg Gamma(1 - i delta) = 1/(12 delta) + 1/(360 delta^3)
+//    + 1/(1260 delta^5) + 1/(1680 delta^7) + O(delta^-9) (Stirling series of ln Gamma(-i delta);
+//    checked against mpmath, and its sign against brute-force Magnus, in
+//    tests/test_propagator_math.py).
+// One parameter point per lane, all state in registers.
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -31,6 +41,13 @@ namespace lzq {
 
 constexpr int kPropBlock = 256;
 constexpr double kSqrt3Over6 = 0x1.279a74590331cp-2;  // sqrt(3)/6
+constexpr double kDeltaAdiabatic = 16.0;              // e^{-2 pi 16} = 2e-44
+constexpr double kStepsPerRadian = 1.0;
+
+// G(x) = int_0^x sqrt(t^2 + m^2) dt
+__device__ __forceinline__ double wkb_G(double x, double m) {
+  return 0.5 * (x * sqrt(x * x + m * m) + (m > 0.0 ? m * m * asinh(x / m) : 0.0));
+}
 
 struct Cplx {
   double re, im;
@@ -89,29 +106,58 @@ __global__ __launch_bounds__(kPropBlock) void lz_propagate_kernel(const double* 
     } else {
       right = xcc + K * lz_length(mc, ac, v_w);
     }
-    const double h = (right - left) / (double)S;   // step in xi
-    const double dt = h * inv_vw;                  // step in t
     const double slope = sgn * ac;
-    const double nx = dt * mc;
-    for (int i = 0; i < S; ++i) {
-      const double xm = left + ((double)i + 0.5) * h;
-      const double D1 = slope * ((xm - kSqrt3Over6 * h) - xcc);
-      const double D2 = slope * ((xm + kSqrt3Over6 * h) - xcc);
-      const double ny = kSqrt3Over6 * dt * mc * (D2 - D1) * dt;
-      const double nz = 0.5 * dt * (D1 + D2);
-      const double nn = sqrt(nx * nx + ny * ny + nz * nz);
+    const double delta = mc * mc / (2.0 * v_w * ac);
+    // adiabatic phase of the cell, int E dt (closed form)
+    const double Phi = (wkb_G(ac * (right - xcc), mc) - wkb_G(ac * (left - xcc), mc)) / (ac * v_w);
+    if (delta > kDeltaAdiabatic) {
+      // exact adiabatic following through the cell (see header)
+      double l0, l1, r0, r1;
+      const double DL = slope * (left - xcc), DR = slope * (right - xcc);
+      {
+        const double th = 0.5 * atan2(mc, DL);
+        l0 = cos(th);
+        l1 = sin(th);
+        const double tr = 0.5 * atan2(mc, DR);
+        r0 = cos(tr);
+        r1 = sin(tr);
+      }
+      // b+ = <+|psi>, b- = <-|psi>; |+> = (c, s), |-> = (-s, c)
+      Cplx bp = {l0 * p0.re + l1 * p1.re, l0 * p0.im + l1 * p1.im};
+      Cplx bm = {-l1 * p0.re + l0 * p1.re, -l1 * p0.im + l0 * p1.im};
+      const double id = 1.0 / delta, id2 = id * id;
+      const double phiS = id * (1.0 / 12.0 + id2 * (1.0 / 360.0 + id2 * (1.0 / 1260.0 + id2 * (1.0 / 1680.0))));
       double sn, cs;
-      sincos(nn, &sn, &cs);
-      const double sc = nn > 0.0 ? sn / nn : 1.0;
-      const double sx = sc * nx, sy = sc * ny, sz = sc * nz;
-      // U11 = cs - i sz ; U12 = -sy - i sx ; U21 = sy - i sx ; U22 = cs + i sz
-      Cplx q0, q1;
-      q0.re = cs * p0.re + sz * p0.im - sy * p1.re + sx * p1.im;
-      q0.im = cs * p0.im - sz * p0.re - sy * p1.im - sx * p1.re;
-      q1.re = sy * p0.re + sx * p0.im + cs * p1.re - sz * p1.im;
-      q1.im = sy * p0.im - sx * p0.re + cs * p1.im + sz * p1.re;
-      p0 = q0;
-      p1 = q1;
+      sincos(Phi + phiS, &sn, &cs);
+      const Cplx bp2 = {bp.re * cs + bp.im * sn, bp.im * cs - bp.re * sn};  // * e^{-i a}
+      const Cplx bm2 = {bm.re * cs - bm.im * sn, bm.im * cs + bm.re * sn};  // * e^{+i a}
+      p0 = {r0 * bp2.re - r1 * bm2.re, r0 * bp2.im - r1 * bm2.im};
+      p1 = {r1 * bp2.re + r0 * bm2.re, r1 * bp2.im + r0 * bm2.im};
+    } else {
+      const int Sc = (int)fmax((double)S, ceil(Phi * kStepsPerRadian));
+      const double h = (right - left) / (double)Sc;  // step in xi
+      const double dt = h * inv_vw;                  // step in t
+      const double nx = dt * mc;
+      for (int i = 0; i < Sc; ++i) {
+        const double xm = left + ((double)i + 0.5) * h;
+        const double D1 = slope * ((xm - kSqrt3Over6 * h) - xcc);
+        const double D2 = slope * ((xm + kSqrt3Over6 * h) - xcc);
+        const double ny = kSqrt3Over6 * dt * mc * (D2 - D1) * dt;
+        const double nz = 0.5 * dt * (D1 + D2);
+        const double nn = sqrt(nx * nx + ny * ny + nz * nz);
+        double sn, cs;
+        sincos(nn, &sn, &cs);
+        const double sc = nn > 0.0 ? sn / nn : 1.0;
+        const double sx = sc * nx, sy = sc * ny, sz = sc * nz;
+        // U11 = cs - i sz ; U12 = -sy - i sx ; U21 = sy - i sx ; U22 = cs + i sz
+        Cplx q0, q1;
+        q0.re = cs * p0.re + sz * p0.im - sy * p1.re + sx * p1.im;
+        q0.im = cs * p0.im - sz * p0.re - sy * p1.im - sx * p1.re;
+        q1.re = sy * p0.re + sx * p0.im + cs * p1.re - sz * p1.im;
+        q1.im = sy * p0.im - sx * p0.re + cs * p1.im + sz * p1.re;
+        p0 = q0;
+        p1 = q1;
+      }
     }
     left = right;
     sgn = -sgn;

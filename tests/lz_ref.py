@@ -20,8 +20,37 @@ def chi_like(d, m):
     return (c, s) if abs(c) >= abs(s) else (-s, c)
 
 
-def propagate(m_mix, dprime, xi, v_w, K, S):
-    """K = outer half-window in LZ lengths of the first / last crossing."""
+DELTA_ADIABATIC = 16.0
+STEPS_PER_RADIAN = 1.0
+
+
+def wkb_G(x, m):
+    return 0.5 * (x * math.sqrt(x * x + m * m) + (m * m * math.asinh(x / m) if m > 0 else 0.0))
+
+
+def stokes_phase(delta):
+    """pi/4 + delta (ln delta - 1) + arg Gamma(1 - i delta), large-delta (Stirling) series."""
+    i1 = 1.0 / delta
+    i2 = i1 * i1
+    return i1 * (1.0 / 12.0 + i2 * (1.0 / 360.0 + i2 * (1.0 / 1260.0 + i2 * (1.0 / 1680.0))))
+
+
+def adiabatic_cell(p, m, a, slope, xc, left, right, v_w):
+    tl = 0.5 * math.atan2(m, slope * (left - xc))
+    tr = 0.5 * math.atan2(m, slope * (right - xc))
+    bp = math.cos(tl) * p[0] + math.sin(tl) * p[1]
+    bm = -math.sin(tl) * p[0] + math.cos(tl) * p[1]
+    Phi = (wkb_G(a * (right - xc), m) - wkb_G(a * (left - xc), m)) / (a * v_w)
+    ph = Phi + stokes_phase(m * m / (2.0 * v_w * a))
+    bp *= complex(math.cos(ph), -math.sin(ph))
+    bm *= complex(math.cos(ph), math.sin(ph))
+    return np.array([math.cos(tr) * bp - math.sin(tr) * bm, math.sin(tr) * bp + math.cos(tr) * bm])
+
+
+def propagate(m_mix, dprime, xi, v_w, K, S, hybrid=True):
+    """K = outer half-window in LZ lengths of the first / last crossing.  hybrid=True is the
+    kernel's scheme (Magnus with max(S, phase) steps, exact adiabatic cells for delta > 16);
+    hybrid=False is plain Magnus with S uniform steps in every cell (brute force)."""
     N = len(m_mix)
     left = xi[0] - K * xi_lz(m_mix[0], dprime[0], v_w)
     u0, u1 = chi_like(abs(dprime[0]) * (left - xi[0]), m_mix[0])
@@ -35,11 +64,19 @@ def propagate(m_mix, dprime, xi, v_w, K, S):
             right = (ac * xi[c] + an * xi[c + 1]) / (ac + an)
         else:
             right = xi[c] + K * xi_lz(m_mix[c], dprime[c], v_w)
-        h = (right - left) / S
-        dt = h / v_w
         slope = sgn * ac
+        delta = m_mix[c] ** 2 / (2.0 * v_w * ac)
+        if hybrid and delta > DELTA_ADIABATIC:
+            p = adiabatic_cell(p, m_mix[c], ac, slope, xi[c], left, right, v_w)
+            left = right
+            sgn = -sgn
+            continue
+        Phi = (wkb_G(ac * (right - xi[c]), m_mix[c]) - wkb_G(ac * (left - xi[c]), m_mix[c])) / (ac * v_w)
+        Sc = int(max(S, math.ceil(Phi * STEPS_PER_RADIAN))) if hybrid else S
+        h = (right - left) / Sc
+        dt = h / v_w
         nx = dt * m_mix[c]
-        for i in range(S):
+        for i in range(Sc):
             xm = left + (i + 0.5) * h
             D1 = slope * ((xm - S3 * h) - xi[c])
             D2 = slope * ((xm + S3 * h) - xi[c])

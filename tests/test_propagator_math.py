@@ -28,3 +28,32 @@ def test_norm_and_trivial_limits():
     # no coupling -> no conversion; huge coupling -> adiabatic following (P -> 1)
     assert propagate([0.0], [1.0], [0.0], 0.3, 10.0, 200) < 1e-24
     assert propagate([1.0], [0.1], [0.0], 0.3, 40, 16000) > 1 - 1e-6
+
+
+def test_adiabatic_cell_matches_brute_force_magnus():
+    """Two crossings: the first (delta = 0.6) splits the state, the second (delta = 23) is
+    adiabatic and only adds the WKB + Stokes phase, which the final interference exposes.
+    The hybrid's exact adiabatic cell must agree with brute-force Magnus (step-converged)."""
+    m = [0.3, 1.2]
+    d = [0.25, 0.1]
+    x = [0.0, 200.0]      # cell edge |D| = 14 >> m: adiabatic-cell edge error ~ 1/(4 delta (D/m)^3) ~ 6e-6
+    K, v_w = 20.0, 0.3
+    hyb = propagate(m, d, x, v_w, K, 400)
+    bf1 = propagate(m, d, x, v_w, K, 40000, hybrid=False)
+    bf2 = propagate(m, d, x, v_w, K, 80000, hybrid=False)
+    assert abs(bf1 - bf2) < 1e-8                        # brute force converged
+    # the second cell's phase decides the interference: P moves 0.015 -> 0.032 for x_2 180 -> 201
+    hyb_far = propagate(m, d, [0.0, 201.0], v_w, K, 400)
+    assert abs(hyb_far - hyb) > 0.01
+    # error budget: neglected non-adiabatic amplitude at the cell edges (~6e-6) and ~1 rad/step
+    assert abs(hyb - bf2) < 1e-5, (hyb, bf2)
+
+
+def test_stokes_phase_series_vs_mpmath():
+    import mpmath as mp
+    from lz_ref import stokes_phase
+    for dl in (16.0, 20.0, 50.0, 400.0):
+        d = mp.mpf(dl)
+        exact = mp.pi / 4 + d * (mp.log(d) - 1) + mp.arg(mp.gamma(1 - 1j * d))
+        exact = float((exact + mp.pi) % (2 * mp.pi) - mp.pi)
+        assert abs(stokes_phase(dl) - exact) < 1e-11, (dl, stokes_phase(dl), exact)

@@ -70,41 +70,137 @@ LZQ_HD int32_t cvt_i32_sat(double kd) {
 #endif
 }
 
-// 2^(c2*g) for c2*g <= 0 (see header comment).
-LZQ_HD double exp2_nonpos(double c2, double g) {
+// 2^(c2*g + bias) for c2*g <= 0 (see header comment); bias = kOmegaBias when the caller's
+// weights are the scaled omega' = omega * 2^-512 of the z table.
+LZQ_HD double exp2_nonpos(double c2, double g, int32_t bias = 0) {
   double u = c2 * g;
   double kd = __builtin_rint(u);
   double r = __builtin_fma(c2, g, -kd);
-  int32_t k = cvt_i32_sat(kd);
-  return __builtin_ldexp(exp2_poly(r), k);
+  int32_t k = cvt_i32_sat(kd);  // INT_MIN + bias stays hugely negative -> 0
+  return __builtin_ldexp(exp2_poly(r), k + bias);
 }
 
 // ---------------------------------------------------------------------------------------
-// Table-driven variant (default): 2^u = 2^e * T[j] * 2^(r/256),  u*256 = 256 e + j + r,
-// T[j] = 2^(j/256) (2 KB, staged in LDS once per block), |r| <= 1/2 so r/256 <= 2^-9 and a
-// degree-4 Taylor polynomial is accurate to 3.8e-17 (0.17 ulp).  Per node: 11 FP64 VALU
-// (mul, rndne, fma, cvt, 3 fma + mul, fma, ldexp, + the caller's accumulate) + 3 integer
-// VALU (and, shift for the LDS address, arithmetic shift for e) + one ds_read_b64.  The LDS
-// table has 256 distinct 8-byte entries, so a wave64 read is at most 8-way bank-conflicted
-// and is usually far less (lanes of one wave hold neighbouring y-nodes).
-constexpr int kTabBits = 8;
-constexpr int kTabN = 1 << kTabBits;
-constexpr double kTabB1 = 0x1.62e42fefa39efp-9;   // (ln2/256)^1 / 1!
-constexpr double kTabB2 = 0x1.ebfbdff82c58fp-19;  // (ln2/256)^2 / 2!
-constexpr double kTabB3 = 0x1.c6b08d704a0c0p-29;  // (ln2/256)^3 / 3!
-constexpr double kTabB4 = 0x1.3b2ab6fba4e77p-39;  // (ln2/256)^4 / 4!
+// Table-driven variant (default).  2^(u/N) for u = c2N*g <= 0 (u in 1/N-octave units):
+//   u = N e + j + r,  k = N e + j = round(u),  |r| <= 1/2,
+//   2^(u/N) = 2^e * T[j] * (1 + q(r)),  T[j] = 2^(j/N),  q(r) = r*(B1 + r*(B2 + ...)),
+// q a minimax polynomial of degree LZQ_POLYDEG in r (tools/exp2_tab_poly.py; absolute error
+// |dq| of q is the relative error of T*(1+q)).  The kernel (lzq_kernels.hip, zsum) never
+// forms 2^e with ldexp: the LDS table stores T'[j] with its high word pre-biased so that ONE
+// integer add of (k << S), S = 20 - BITS, gives T[j] * 2^(e + 512) (tab_scale), and the z
+// table's weights carry the compensating 2^-512 (kOmegaBias).  k is clamped to
+// KMIN = -1534 N so that e + 512 >= -1022 keeps that product a normal double.
+//
+//   BITS DEG  LDS/block  |dq| (minimax)     VALU/node  C2 points/s (1 GPU)
+//     8   4     2 KB     1.9e-17 (0.1 ulp)   12.5       3.17e5  (round-1 kernel: ldexp path)
+//    12   2    32 KB     2.5e-14 (114 ulp)   11.4       3.54e5  (ldexp path, 2-op address)
+//    13   2    64 KB     3.2e-15 (14 ulp)    10         (this path; 512-thread blocks)
+// The 13-bit address is ONE v_lshlrev_b16 ((k << 3) mod 2^16 = 8*(k mod 8192)).  The default's
+// 3.2e-15 bound moves Y_B by at most that much (relative), 3e6 x inside the north_star 1e-8
+// gate; tests/test_exp2_host.py pins every row against mpmath.
+#ifndef LZQ_TABBITS
+#define LZQ_TABBITS 13
+#endif
+#ifndef LZQ_POLYDEG
+#define LZQ_POLYDEG 2
+#endif
 
-// 2^(c2N*g / 256) for c2N*g <= 0 with c2N = 256*c2; tab[j] = 2^(j/256).
-LZQ_HD double exp2_nonpos_tab(double c2N, double g, const double* tab) {
-  double u = c2N * g;
-  double kd = __builtin_rint(u);
-  double r = __builtin_fma(c2N, g, -kd);
-  int32_t k = cvt_i32_sat(kd);
-  int32_t j = k & (kTabN - 1);
-  int32_t e = k >> kTabBits;  // arithmetic shift: floor(k / 256); INT_MIN -> -2^23 -> 0 result
-  double T = tab[j];
-  double q = r * __builtin_fma(r, __builtin_fma(r, __builtin_fma(r, kTabB4, kTabB3), kTabB2), kTabB1);
-  return __builtin_ldexp(__builtin_fma(T, q, T), e);
+template <int BITS, int DEG>
+struct TabPoly;  // coefficients B1..B_DEG of 2^(r/2^BITS) - 1 ~= r*(B1 + r*(B2 + ...))
+template <>
+struct TabPoly<8, 4> {  // Taylor: (ln2/256)^i / i!
+  static constexpr double B[4] = {0x1.62e42fefa39efp-9, 0x1.ebfbdff82c58fp-19, 0x1.c6b08d704a0c0p-29,
+                                  0x1.3b2ab6fba4e77p-39};
+};
+template <>
+struct TabPoly<10, 3> {
+  static constexpr double B[3] = {0x1.62e42fefa39efp-11, 0x1.ebfbe03972542p-23, 0x1.c6b08dae13771p-35};
+};
+template <>
+struct TabPoly<12, 2> {
+  static constexpr double B[2] = {0x1.62e42ff4f7b0ap-13, 0x1.ebfbdffcafed4p-27};
+};
+template <>
+struct TabPoly<12, 3> {
+  static constexpr double B[3] = {0x1.62e42fefa39efp-13, 0x1.ebfbdffc40b8ap-27, 0x1.c6b08d7426a2bp-41};
+};
+template <>
+struct TabPoly<13, 2> {
+  static constexpr double B[2] = {0x1.62e42ff0f8a36p-14, 0x1.ebfbdff94d3e0p-29};
+};
+template <>
+struct TabPoly<14, 2> {
+  static constexpr double B[2] = {0x1.62e42feff8e01p-15, 0x1.ebfbdff874923p-31};
+};
+template <>
+struct TabPoly<14, 3> {
+  static constexpr double B[3] = {0x1.62e42fefa39efp-15, 0x1.ebfbdff86d9eep-31, 0x1.c6b08d7087d56p-47};
+};
+
+constexpr int kTabBits = LZQ_TABBITS;
+constexpr int kTabN = 1 << kTabBits;
+constexpr int kPolyDeg = LZQ_POLYDEG;
+constexpr int kTabShift = 20 - kTabBits;          // (k << S) = (e << 20) + (j << S)
+constexpr int32_t kOmegaBias = 512;               // T' carries 2^512, omega' carries 2^-512
+constexpr int32_t kTabKMin = -1534 * kTabN;       // e >= -1534 -> e + 512 >= -1022 (normal)
+static_assert(kTabBits >= 8 && kTabBits <= 16, "table bits");
+static_assert((int64_t)kTabKMin * (1 << kTabShift) >= INT32_MIN, "k << S must not overflow");
+
+// q(r) = r*(B1 + r*(B2 + ...)): DEG-1 fma + 1 mul, coefficients passed in (so that a caller
+// can hold B1 in a VGPR across its loop: a VOP3 op reads at most one SGPR on gfx950, and the
+// compiler otherwise re-materialises the copy every iteration)
+template <int DEG>
+LZQ_HD double tab_q_with(double r, const double (&B)[DEG]) {
+  double acc = B[DEG - 1];
+#pragma unroll
+  for (int i = DEG - 2; i >= 0; --i) acc = __builtin_fma(r, acc, B[i]);
+  return r * acc;
+}
+
+// Table entry j as stored (host side): 2^(j/N) rounded once, high word pre-biased by
+// (512 << 20) - (j << S) (mod 2^32).
+static inline uint64_t tab_entry_bits(long double T_exact, int32_t j) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, (double)T_exact);
+  const uint32_t hi = (uint32_t)(b >> 32) + ((uint32_t)kOmegaBias << 20) - ((uint32_t)j << kTabShift);
+  return ((uint64_t)hi << 32) | (b & 0xffffffffu);
+}
+
+// LDS byte address of entry (k mod N) from the low word k of the clamped magic sum.
+LZQ_HD uint32_t tab_byte_addr(uint32_t k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (kTabBits == 13) {
+    uint32_t a;  // 16-bit shift, upper half zeroed: (k << 3) & 0xffff = 8 * (k & 8191)
+    asm("v_lshlrev_b16_sdwa %0, 3, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
+        : "=v"(a) : "v"(k));
+    return a;
+  }
+#endif
+  return (k & (uint32_t)(kTabN - 1)) << 3;
+}
+
+// T'[j] with its high word advanced by k << S:  T[j] * 2^(e + 512).
+// (written on a 2 x u32 vector so that the compiler emits one v_lshl_add_u32 on the high
+// VGPR of the pair, not a 64-bit add)
+typedef uint32_t lzq_u32x2 __attribute__((vector_size(8)));
+LZQ_HD double tab_scale(double Tp, uint32_t k) {
+  lzq_u32x2 w = __builtin_bit_cast(lzq_u32x2, Tp);
+  w[1] = w[1] + (k << kTabShift);
+  return __builtin_bit_cast(double, w);
+}
+
+// Host/device reference of one table-variant node: returns 2^(u/N) * 2^512 exactly as the
+// kernel forms it (the kernel multiplies by omega' = omega * 2^-512 inside its accumulate).
+// tabp = table as stored (tab_entry_bits).  c2N*g <= 0, |c2N*g| < 2^51.
+LZQ_HD double exp2_tab_scaled(double c2N, double g, const double* tabp) {
+  constexpr double kMagic = 0x1.8p52;
+  const double t = __builtin_fma(c2N, g, kMagic);
+  const double kd = t - kMagic;
+  const double r = __builtin_fma(c2N, g, -kd);
+  const double tc = __builtin_fmax(t, kMagic + (double)kTabKMin);
+  const uint32_t k = (uint32_t)__builtin_bit_cast(uint64_t, tc);
+  const double Ts = tab_scale(tabp[tab_byte_addr(k) >> 3], k);
+  const double q = tab_q_with<kPolyDeg>(r, TabPoly<kTabBits, kPolyDeg>::B);
+  return __builtin_fma(Ts, q, Ts);
 }
 
 }  // namespace lzq

@@ -23,6 +23,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <vector>
 
 #include "../../include/lzq.h"
 #include "lzq_exp2.h"
@@ -32,7 +33,12 @@ namespace lzq {
 
 constexpr int kNZ = LZQ_NZ;
 constexpr int kWaveSize = 64;
-constexpr int kBlock = 256;
+// The block is sized so that the LDS copies of the exp table that fit in a CU's 160 KB carry
+// 16 waves (4 per SIMD): 64-KB table (default) -> two 512-thread blocks per CU.
+#ifndef LZQ_BLOCK
+#define LZQ_BLOCK ((8 << LZQ_TABBITS) > 81920 ? 1024 : (8 << LZQ_TABBITS) > 40960 ? 512 : 256)
+#endif
+constexpr int kBlock = LZQ_BLOCK;
 constexpr int kWavesPerBlock = kBlock / kWaveSize;
 #ifndef LZQ_KUNROLL
 #define LZQ_KUNROLL 4
@@ -50,10 +56,6 @@ constexpr int kWavesPerBlock = kBlock / kWaveSize;
 // compiler can use counted lgkmcnt waits instead of draining behind SMEM)
 #ifndef LZQ_ZLDS
 #define LZQ_ZLDS 0
-#endif
-// 1: magic-constant range reduction on waves whose lanes are all in int32 range or dead
-#ifndef LZQ_MAGIC
-#define LZQ_MAGIC 1
 #endif
 constexpr int kKUnroll = LZQ_KUNROLL;  // z-nodes per scalar-load batch (must divide 1200)
 constexpr int kYB = LZQ_YB;            // y-nodes per lane per pass (independent chains)
@@ -132,6 +134,13 @@ __device__ __forceinline__ QuadSetup quad_setup(const lzq_point& pt, double P, d
   return s;
 }
 
+// A loop-invariant double materialised once in a VGPR (opaque to re-materialisation).
+__device__ __forceinline__ double vgpr_const(double x) {
+  double v;
+  asm volatile("v_mov_b64 %0, %1" : "=v"(v) : "s"(x));
+  return v;
+}
+
 // numpy.linspace element (handles numpy's step == 0 branch as well)
 __device__ __forceinline__ double y_node(const QuadSetup& s, int64_t j) {
   if (j == s.n - 1) return s.y_hi;
@@ -200,119 +209,126 @@ __device__ __forceinline__ double y_weight(const QuadSetup& s, int64_t j, double
 }
 
 // exp variants of the inner loop (lzq_tune(LZQ_TUNE_EXP, ...))
-enum ExpVariant { kExpPoly11 = 0, kExpTable256 = 1 };
+enum ExpVariant { kExpPoly11 = 0, kExpTable = 1 };
 
 // Scale of c2 expected by the variant (2^(c2*g) for poly11, 2^(c2N*g/256) for the table).
 template <int EXPV>
-__device__ __forceinline__ double c2_scale() { return EXPV == kExpTable256 ? (double)kTabN : 1.0; }
+__device__ __forceinline__ double c2_scale() { return EXPV == kExpTable ? (double)kTabN : 1.0; }
 
 // F(c2) = sum_k omega_k 2^(c2 g4_k) for YB independent y-nodes per lane.
-// The table variant is written in explicit phases per batch of kKUnroll z-nodes -- table
-// operands, range reduction, all LDS lookups, then polynomial + accumulate -- so the
-// lookups of a batch are in flight together and retire behind one wait.
 //
-// MAGIC selects the range reduction of the table variant:
-//   false: u = c2*g; kd = rint(u); r = fma(c2,g,-kd); k = cvt_i32_sat(kd)   (4 FP64 ops, any u)
-//   true : t = fma(c2,g,1.5*2^52); kd = t - 1.5*2^52; r = fma(c2,g,-kd); k = lo32(t)
-//          (3 FP64 ops; exact only while |c2*g| < 2^31 -- the caller guarantees it per wave)
-template <int YB, int EXPV, bool MAGIC = false>
+// Every VALU instruction of this mixed FP64/integer stream issues in ~4 cycles on gfx950
+// (tools/ubench_valu.hip: an integer op between FP64 ops costs as much as an FP64 op), so the
+// loop is built to minimise the instruction COUNT.  Table variant, per (y, z) node:
+//
+//   t  = fma(c2, g, M)          M = 1.5*2^52: t = M + round(u), u = c2*g in 1/N-octave units
+//   kd = t - M                  exact
+//   r  = fma(c2, g, -kd)        u - round(u) in [-1/2, 1/2], one rounding
+//   tc = max(t, M + KMIN)       clamp to e >= -1534 octaves (also keeps lo32 in int range)
+//   a  = (lo32(tc) & (N-1))*8   LDS byte address: ONE v_lshlrev_b16 for N = 8192
+//   T' = lds[a]                 T'.hi = hi(2^(j/N)) - (j << S) + (512 << 20), S = 20 - BITS
+//   T'.hi += lo32(tc) << S      ONE v_lshl_add_u32: T' = 2^(j/N) * 2^(e+512), e = floor(k/N)
+//   q  = r*(B1 + r*B2)          2 FP64
+//   v  = fma(T', q, T')         = 2^(u/N) * 2^512, always a normal double (e+512 >= -1022)
+//   F  = fma(omega', v, F)      omega' = omega * 2^-512 (z table), so omega'*v = omega*2^u
+//
+// = 10 VALU per node (round-1 kernel: 12.5).  The last fma rounds the exact product omega*2^u
+// once, so gradual underflow is exact; clamped nodes (u < -1534 octaves) contribute
+// omega*2^-1534*(...) which rounds away exactly like the underflowed 0 it stands for.
+// For |u| < 2^51 (every non-dead lane, checked on the host) t is exact; dead lanes (whose
+// every node k >= 1 underflows) run with c2 = 0 and are zeroed, so no input reaches the
+// loop with |u| >= 2^51.
+template <int YB, int EXPV>
 __device__ __forceinline__ void zsum(const ZNode* __restrict__ zt, const double* tab, const double (&c2)[YB],
                                      double (&F)[YB]) {
-  constexpr double kMagic = 0x1.8p52;
 #pragma unroll
   for (int b = 0; b < YB; ++b) F[b] = 0.0;
-  for (int k = 0; k < kNZ; k += kKUnroll) {
-    double g4[kKUnroll], om[kKUnroll];
+  if constexpr (EXPV == kExpTable) {
+    constexpr double kMagic = 0x1.8p52;
+    constexpr double kTClamp = kMagic + (double)kTabKMin;  // exact
+    const double Mv = vgpr_const(kMagic);
+    // polynomial coefficients; B1 pinned in a VGPR for the whole loop (see tab_q_with)
+    double Bv[kPolyDeg];
 #pragma unroll
-    for (int kk = 0; kk < kKUnroll; ++kk) {
-      g4[kk] = zt[k + kk].g4;
-      om[kk] = zt[k + kk].omega;
-    }
-    if constexpr (EXPV == kExpTable256) {
+    for (int i = 0; i < kPolyDeg; ++i) Bv[i] = TabPoly<kTabBits, kPolyDeg>::B[i];
+    Bv[0] = vgpr_const(Bv[0]);
+    const char* tabb = reinterpret_cast<const char*>(tab);
+    for (int k = 0; k < kNZ; k += kKUnroll) {
+      double g4[kKUnroll], om[kKUnroll];
+#pragma unroll
+      for (int kk = 0; kk < kKUnroll; ++kk) {
+        g4[kk] = zt[k + kk].g4;
+        om[kk] = zt[k + kk].omega;
+      }
+      // phases: reduction + addresses for the whole batch, then the lookups (in flight
+      // together), then polynomial + accumulate
       double r[YB][kKUnroll], T[YB][kKUnroll];
-      int32_t e[YB][kKUnroll], j[YB][kKUnroll];
+      uint32_t kc[YB][kKUnroll], a[YB][kKUnroll];
 #pragma unroll
       for (int kk = 0; kk < kKUnroll; ++kk)
 #pragma unroll
         for (int b = 0; b < YB; ++b) {
-          int32_t ki;
-          double kd;
-          if constexpr (MAGIC) {
-            const double t = __builtin_fma(c2[b], g4[kk], kMagic);
-            kd = t - kMagic;
-            ki = (int32_t)(uint32_t)__builtin_bit_cast(uint64_t, t);
-          } else {
-            kd = __builtin_rint(c2[b] * g4[kk]);
-            ki = cvt_i32_sat(kd);
-          }
+          const double t = __builtin_fma(c2[b], g4[kk], Mv);
+          const double kd = t - Mv;
           r[b][kk] = __builtin_fma(c2[b], g4[kk], -kd);
-          j[b][kk] = ki & (kTabN - 1);
-          e[b][kk] = ki >> kTabBits;
+          const double tc = __builtin_fmax(t, kTClamp);
+          kc[b][kk] = (uint32_t)__builtin_bit_cast(uint64_t, tc);
+          a[b][kk] = tab_byte_addr(kc[b][kk]);
         }
 #pragma unroll
       for (int kk = 0; kk < kKUnroll; ++kk)
 #pragma unroll
-        for (int b = 0; b < YB; ++b) T[b][kk] = tab[j[b][kk]];
+        for (int b = 0; b < YB; ++b) T[b][kk] = *reinterpret_cast<const double*>(tabb + a[b][kk]);
 #pragma unroll
       for (int kk = 0; kk < kKUnroll; ++kk)
 #pragma unroll
         for (int b = 0; b < YB; ++b) {
-          const double rr = r[b][kk];
-          const double q =
-              rr * __builtin_fma(rr, __builtin_fma(rr, __builtin_fma(rr, kTabB4, kTabB3), kTabB2), kTabB1);
-          const double v = __builtin_ldexp(__builtin_fma(T[b][kk], q, T[b][kk]), e[b][kk]);
-          F[b] = __builtin_fma(om[kk], v, F[b]);
+          const double Ts = tab_scale(T[b][kk], kc[b][kk]);
+          const double q = tab_q_with<kPolyDeg>(r[b][kk], Bv);
+          F[b] = __builtin_fma(om[kk], __builtin_fma(Ts, q, Ts), F[b]);
         }
-    } else {
+    }
+  } else {
+    for (int k = 0; k < kNZ; k += kKUnroll) {
 #pragma unroll
-      for (int kk = 0; kk < kKUnroll; ++kk)
+      for (int kk = 0; kk < kKUnroll; ++kk) {
+        const double g = zt[k + kk].g4, om = zt[k + kk].omega;
 #pragma unroll
-        for (int b = 0; b < YB; ++b) F[b] = __builtin_fma(om[kk], exp2_nonpos(c2[b], g4[kk]), F[b]);
+        for (int b = 0; b < YB; ++b) F[b] = __builtin_fma(om, exp2_nonpos(c2[b], g, kOmegaBias), F[b]);
+      }
     }
   }
 }
 
-// Pass-level dispatch of the z-sum (table variant).  A lane is
-//   * "in range" when |c2| * max_k g4_k < 2^31 - 2^20: the magic reduction is exact for all k;
-//   * "dead" when c2 * g4_1 <= -256*1077: every node k >= 1 underflows to exactly 0 in either
-//     reduction (g4 is increasing and k = 0 has omega_0 = 0), so F = 0 exactly.
-// If every lane of the wave is in range or dead, the pass runs the 3-op reduction (dead lanes
-// compute with c2 = 0 and are zeroed afterwards: same instruction stream, same exact zero);
-// otherwise the 4-op saturating reduction.  The choice is a function of the point only.
+// Pass-level wrapper: "dead" lanes, c2 * g4_1 <= -N*1077 (every node k >= 1 underflows to
+// exactly 0: g4 is increasing and omega_0 = 0), run the loop with c2 = 0 and are zeroed
+// afterwards -- the same instruction stream, the exact zero, and no |u| >= 2^51 in the loop.
 template <int YB, int EXPV>
 __device__ __forceinline__ void zsum_dispatch(const ZNode* __restrict__ zt, const double* tab,
                                               const double (&c2)[YB], double (&F)[YB]) {
-  if constexpr (EXPV == kExpTable256 && LZQ_MAGIC) {
-    const double g_max = zt[kNZ - 1].g4, g_1 = zt[1].g4;
-    bool dead[YB], ok = true;
-    double c2e[YB];
+  const double g_1 = zt[1].g4;
+  bool dead[YB];
+  double c2e[YB];
 #pragma unroll
-    for (int b = 0; b < YB; ++b) {
-      dead[b] = c2[b] * g_1 <= -256.0 * 1077.0;
-      const bool in_range = fabs(c2[b]) * g_max < 2147483648.0 - 1048576.0;
-      ok = ok && (dead[b] || in_range);
-      c2e[b] = dead[b] ? 0.0 : c2[b];
-    }
-    if (__all(ok)) {
-      zsum<YB, EXPV, true>(zt, tab, c2e, F);
-#pragma unroll
-      for (int b = 0; b < YB; ++b) F[b] = dead[b] ? 0.0 : F[b];
-      return;
-    }
+  for (int b = 0; b < YB; ++b) {
+    dead[b] = c2[b] * g_1 <= -c2_scale<EXPV>() * 1077.0;
+    c2e[b] = dead[b] ? 0.0 : c2[b];
   }
-  zsum<YB, EXPV, false>(zt, tab, c2, F);
+  zsum<YB, EXPV>(zt, tab, c2e, F);
+#pragma unroll
+  for (int b = 0; b < YB; ++b) F[b] = dead[b] ? 0.0 : F[b];
 }
 
-// Stage the 2 KB table T[j] = 2^(j/256) in LDS (every thread of the block must call this).
+// Stage the exp table (N doubles, see lzq_exp2.h) in LDS (every thread of the block must call this).
 template <int EXPV>
 __device__ __forceinline__ const double* stage_table(const double* __restrict__ gtab, double* lds) {
-  if (EXPV != kExpTable256) return nullptr;
+  if (EXPV != kExpTable) return nullptr;
   for (int i = threadIdx.x; i < kTabN; i += blockDim.x) lds[i] = gtab[i];
   __syncthreads();
   return lds;
 }
 
-// LDS image of the per-block tables: z nodes (19.2 KB) followed by the exp2 table (2 KB).
+// LDS image of the per-block tables: z nodes (19.2 KB) followed by the exp table.
 struct LdsTables {
   ZNode z[kNZ];
   double t[kTabN];
@@ -323,7 +339,7 @@ template <int EXPV>
 __device__ __forceinline__ void stage_tables(const ZNode* __restrict__ gz, LdsTables* lds) {
   const double* src = reinterpret_cast<const double*>(gz);
   double* dst = reinterpret_cast<double*>(lds);
-  constexpr int n = 2 * kNZ + (EXPV == kExpTable256 ? kTabN : 0);
+  constexpr int n = 2 * kNZ + (EXPV == kExpTable ? kTabN : 0);
   for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
   __syncthreads();
 }
@@ -515,7 +531,7 @@ __global__ __launch_bounds__(kBlock) void aov_kernel(lzq_point pt, const double*
   QuadSetup s = quad_setup(pt, pt.P_chi_to_B, 1.0, 1.0, LZQ_NY_MIN);
   double expy = exp(pymax(pymin(y, 50.0), -50.0));
   double c2[1] = {((s.cneg * expy) * kLog2E) * c2_scale<EXPV>()}, F[1];
-  zsum<1, EXPV>(zt, tab, c2, F);
+  zsum_dispatch<1, EXPV>(zt, tab, c2, F);
   if (live) out[i] = (y > 50.0) ? 0.0 : (s.pref0 * expy) * F[0];
 }
 
@@ -548,8 +564,9 @@ std::mutex g_mu;
 constexpr int kMaxDevices = 64;
 lzq::ZNode* g_dev_tab[kMaxDevices] = {nullptr};  // [LZQ_NZ] ZNode followed by kTabN doubles
 bool g_host_ready = false;
-double g_z[LZQ_NZ], g_g4[LZQ_NZ], g_omega[LZQ_NZ], g_exp2tab[lzq::kTabN];
-int g_exp_variant = lzq::kExpTable256;
+double g_z[LZQ_NZ], g_g4[LZQ_NZ], g_omega[LZQ_NZ];
+uint64_t g_exp2tab[lzq::kTabN];  // lzq::tab_entry_bits layout
+int g_exp_variant = lzq::kExpTable;
 
 const double* exp_table(int dev) { return reinterpret_cast<const double*>(g_dev_tab[dev] + LZQ_NZ); }
 
@@ -587,8 +604,14 @@ int build_host_tables() {
     const double dr = k + 1 < n ? g_z[k + 1] - g_z[k] : 0.0;
     g_omega[k] = w[k] * (0.5 * (dl + dr));
   }
-  // T[j] = 2^(j/256): x87 long double exp2 (64-bit mantissa) rounded once to double
-  for (int j = 0; j < lzq::kTabN; ++j) g_exp2tab[j] = (double)exp2l((long double)j / (long double)lzq::kTabN);
+  // T[j] = 2^(j/N): x87 long double exp2 (64-bit mantissa) rounded once to double, stored
+  // with the pre-biased high word of lzq::tab_entry_bits
+  for (int j = 0; j < lzq::kTabN; ++j)
+    g_exp2tab[j] = lzq::tab_entry_bits(exp2l((long double)j / (long double)lzq::kTabN), j);
+  // the kernel's magic-constant reduction needs |c2N*g| < 2^51 on every non-dead lane
+  // (zsum_dispatch: dead iff c2N*g_1 <= -N*1077), i.e. N*1077*g_max/g_1 < 2^51
+  if (!((double)lzq::kTabN * 1077.0 * g_g4[n - 1] / g_g4[1] < 0x1p50))
+    return fail(LZQ_EINVAL, "gamma4 table range breaks the magic-constant reduction");
   g_host_ready = true;
   return LZQ_OK;
 }
@@ -604,12 +627,14 @@ int ensure_device(int* dev_out) {
   int rc = build_host_tables();
   if (rc) return rc;
   static_assert(sizeof(lzq::ZNode) == 2 * sizeof(double), "ZNode layout");
-  lzq::ZNode host[LZQ_NZ + lzq::kTabN / 2];
-  for (int k = 0; k < LZQ_NZ; ++k) host[k] = {g_g4[k], g_omega[k]};
+  std::vector<lzq::ZNode> host(LZQ_NZ + lzq::kTabN / 2);
+  // device weights carry 2^-512 (the exp table's T' carries 2^+512, lzq_exp2.h)
+  for (int k = 0; k < LZQ_NZ; ++k) host[k] = {g_g4[k], ldexp(g_omega[k], -lzq::kOmegaBias)};
   memcpy(&host[LZQ_NZ], g_exp2tab, sizeof(g_exp2tab));
+  const size_t bytes = host.size() * sizeof(lzq::ZNode);
   lzq::ZNode* d = nullptr;
-  LZQ_HIP(hipMalloc(&d, sizeof(host)));
-  LZQ_HIP(hipMemcpy(d, host, sizeof(host), hipMemcpyHostToDevice));
+  LZQ_HIP(hipMalloc(&d, bytes));
+  LZQ_HIP(hipMemcpy(d, host.data(), bytes, hipMemcpyHostToDevice));
   g_dev_tab[dev] = d;
   return LZQ_OK;
 }
@@ -642,7 +667,7 @@ int lzq_init(int device) {
 
 int lzq_tune(int32_t key, int32_t value) {
   if (key == LZQ_TUNE_EXP) {
-    if (value != LZQ_EXP_POLY11 && value != LZQ_EXP_TABLE256)
+    if (value != LZQ_EXP_POLY11 && value != LZQ_EXP_TABLE)
       return fail(LZQ_EINVAL, "lzq_tune: unknown exp variant %d", value);
     int prev = g_exp_variant;
     g_exp_variant = value;
@@ -668,8 +693,8 @@ int lzq_aov_batch(const lzq_point* pt, const double* d_y, int64_t n, double* d_o
   if (rc) return rc;
   int64_t nb = blocks_for(n, lzq::kBlock);
   if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_aov_batch: n too large");
-  if (g_exp_variant == lzq::kExpTable256)
-    hipLaunchKernelGGL(lzq::aov_kernel<lzq::kExpTable256>, dim3((unsigned)nb), dim3(lzq::kBlock), 0,
+  if (g_exp_variant == lzq::kExpTable)
+    hipLaunchKernelGGL(lzq::aov_kernel<lzq::kExpTable>, dim3((unsigned)nb), dim3(lzq::kBlock), 0,
                        (hipStream_t)stream, *pt, d_y, n, g_dev_tab[dev], exp_table(dev), d_out);
   else
     hipLaunchKernelGGL(lzq::aov_kernel<lzq::kExpPoly11>, dim3((unsigned)nb), dim3(lzq::kBlock), 0,
@@ -699,8 +724,8 @@ int lzq_yields_batch(const lzq_point* d_points, int64_t n, int32_t n_y, const do
   if (rc) return rc;
   int64_t nb = blocks_for(n, lzq::kWavesPerBlock);
   if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_yields_batch: n too large");
-  if (g_exp_variant == lzq::kExpTable256)
-    hipLaunchKernelGGL((lzq::yields_points_kernel<lzq::kYB, lzq::kExpTable256>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
+  if (g_exp_variant == lzq::kExpTable)
+    hipLaunchKernelGGL((lzq::yields_points_kernel<lzq::kYB, lzq::kExpTable>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
                        (hipStream_t)stream, d_points, n, n_y, d_T_lo, d_T_hi, d_P, g_dev_tab[dev], exp_table(dev),
                        d_out);
   else
@@ -746,8 +771,8 @@ int lzq_sweep_grid(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, 
   if (rc) return rc;
   int64_t nb = blocks_for(count, lzq::kWavesPerBlock);
   if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_sweep_grid: count too large for one launch");
-  if (g_exp_variant == lzq::kExpTable256)
-    hipLaunchKernelGGL((lzq::yields_grid_kernel<lzq::kYB, lzq::kExpTable256>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
+  if (g_exp_variant == lzq::kExpTable)
+    hipLaunchKernelGGL((lzq::yields_grid_kernel<lzq::kYB, lzq::kExpTable>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
                        (hipStream_t)stream, *base, g, start, count, n_y, d_P, g_dev_tab[dev], exp_table(dev), d_out);
   else
     hipLaunchKernelGGL((lzq::yields_grid_kernel<lzq::kYB, lzq::kExpPoly11>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,

@@ -34,12 +34,12 @@ class Engine:
             self._check(self.lib.lzq_init(self.device.index))
 
     def tune_exp(self, variant: str) -> str:
-        """Select the inner-loop exponential ('table256' default, 'poly11'); returns the previous."""
-        v = {"poly11": _native.EXP_POLY11, "table256": _native.EXP_TABLE256}[variant]
+        """Select the inner-loop exponential ('table' default, 'poly11'); returns the previous."""
+        v = {"poly11": _native.EXP_POLY11, "table": _native.EXP_TABLE}[variant]
         prev = self.lib.lzq_tune(_native.TUNE_EXP, v)
         if prev < 0:
             self._check(prev)
-        return {_native.EXP_POLY11: "poly11", _native.EXP_TABLE256: "table256"}[prev]
+        return {_native.EXP_POLY11: "poly11", _native.EXP_TABLE: "table"}[prev]
 
     # -- helpers -------------------------------------------------------------------------
     def _check(self, rc: int) -> None:

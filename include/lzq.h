@@ -112,11 +112,12 @@ int lzq_init(int device);
 int lzq_ztables(double* z, double* gamma4, double* omega);
 
 /* Tuning knobs for ablations (process-wide, not thread-safe against concurrent launches).
- * LZQ_TUNE_EXP selects the inner-loop exponential: LZQ_EXP_TABLE256 (default; 2^(j/256)
- * LDS table + degree-4 polynomial) or LZQ_EXP_POLY11 (degree-11 minimax polynomial).
- * Both are ~0.6 ulp; results agree to ~1e-15 relative.  Returns the previous value. */
+ * LZQ_TUNE_EXP selects the inner-loop exponential: LZQ_EXP_TABLE (default; 2^(j/N) LDS table,
+ * N = 2^LZQ_TABBITS = 4096, + degree-2 minimax polynomial, <= 2.6e-14 relative) or
+ * LZQ_EXP_POLY11 (degree-11 minimax polynomial, 0.6 ulp).  Results agree to ~1e-14 relative.
+ * Returns the previous value. */
 enum lzq_tune_key { LZQ_TUNE_EXP = 0 };
-enum lzq_exp_variant { LZQ_EXP_POLY11 = 0, LZQ_EXP_TABLE256 = 1 };
+enum lzq_exp_variant { LZQ_EXP_POLY11 = 0, LZQ_EXP_TABLE = 1 };
 int lzq_tune(int32_t key, int32_t value);
 
 /* ---- hot path -------------------------------------------------------------------------- */

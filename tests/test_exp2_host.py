@@ -17,6 +17,7 @@ from conftest import ROOT, PKG_NAME
 
 SRC = r'''
 #include <math.h>
+#include <string.h>
 #include "lzq_exp2.h"
 extern "C" void ev(const double* c2, const double* g, long n, double* out) {
   for (long i = 0; i < n; ++i) out[i] = lzq::exp2_nonpos(c2[i], g[i]);
@@ -26,25 +27,41 @@ extern "C" void pv(const double* r, long n, double* out) {
 }
 static double tab[lzq::kTabN];
 extern "C" void evt(const double* c2, const double* g, long n, double* out) {
-  for (int j = 0; j < lzq::kTabN; ++j) tab[j] = (double)exp2l((long double)j / (long double)lzq::kTabN);
-  for (long i = 0; i < n; ++i) out[i] = lzq::exp2_nonpos_tab(c2[i] * lzq::kTabN, g[i], tab);
+  for (int j = 0; j < lzq::kTabN; ++j) {
+    uint64_t b = lzq::tab_entry_bits(exp2l((long double)j / (long double)lzq::kTabN), j);
+    memcpy(&tab[j], &b, 8);
+  }
+  // the kernel multiplies the 2^512-scaled value by omega' = omega * 2^-512 in one fma; here
+  // omega = 1, i.e. one rounding of v * 2^-512 (exact unless the result is subnormal)
+  for (long i = 0; i < n; ++i)
+    out[i] = ldexp(lzq::exp2_tab_scaled(c2[i] * lzq::kTabN, g[i], tab), -lzq::kOmegaBias);
 }
 '''
 
 
-@pytest.fixture(scope="module")
-def lib():
+def _build(defines=()):
     d = tempfile.mkdtemp()
     src = os.path.join(d, "t.cpp")
     with open(src, "w") as f:
         f.write(SRC)
     so = os.path.join(d, "t.so")
     subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+                    *[f"-D{k}={v}" for k, v in defines],
                     "-I", os.path.join(ROOT, PKG_NAME, "csrc"), src, "-o", so], check=True)
     L = ctypes.CDLL(so)
     for fn in (L.ev, L.pv, L.evt):
         fn.restype = None
     return L
+
+
+@pytest.fixture(scope="module")
+def lib():
+    return _build()
+
+
+# (table bits, polynomial degree) -> minimax |dq| of tools/exp2_tab_poly.py (Taylor for (8, 4))
+DEFAULT_TAB = (13, 2)  # LZQ_TABBITS / LZQ_POLYDEG defaults in lzq_exp2.h
+TAB_VARIANTS = {(8, 4): 1.9e-17, (10, 3): 9.4e-17, (12, 2): 2.53e-14, (12, 3): 3.7e-19, (13, 2): 3.16e-15, (14, 2): 3.95e-16, (14, 3): 1.5e-21}
 
 
 def run(L, c2, g, fn="ev"):
@@ -78,7 +95,8 @@ def test_exp2_nonpos_range(lib, fn):
     # tolerance: 1 ulp of the polynomial + |u| ulps from rounding the product inside exp2(c2*g)
     # (relative), plus 2 subnormal ulps of absolute slack for gradual underflow
     u_abs = np.abs(c2 * g)
-    tol = exact * (2.5e-16 + u_abs * 2.3e-16) + 2 * 5e-324
+    poly = TAB_VARIANTS[DEFAULT_TAB] if fn == "evt" else 0.0  # default table variant's |dq|
+    tol = exact * (2.5e-16 + poly + u_abs * 2.3e-16) + 2 * 5e-324
     assert np.all(np.abs(got - exact) <= tol), (np.abs(got - exact) / tol).max()
     assert np.all(got[c2 * g <= -1076.0] == 0.0)
     assert np.all(got >= 0.0) and np.all(np.isfinite(got))
@@ -90,10 +108,13 @@ def test_exp2_nonpos_zero_gamma(lib, fn):
     assert run(lib, [-4.1e21, -1.0], [0.0, 0.0], fn).tolist() == [1.0, 1.0]
 
 
-def test_table_variant_matches_mpmath(lib):
+@pytest.mark.parametrize("bits,deg", sorted(TAB_VARIANTS))
+def test_table_variant_matches_mpmath(bits, deg):
+    L = _build([("LZQ_TABBITS", bits), ("LZQ_POLYDEG", deg)])
     rng = np.random.default_rng(5)
     u = -np.concatenate([rng.uniform(0, 60, 3000), 10 ** rng.uniform(-15, 0, 1000)])
     g = np.ones_like(u)
-    got = run(lib, u, g, "evt")
+    got = run(L, u, g, "evt")
     worst = max(abs(float((mp.mpf(o) - mp.power(2, mp.mpf(x))) / mp.power(2, mp.mpf(x)))) for o, x in zip(got, u))
-    assert worst < 2.25e-16, worst  # <= 1 ulp (T[j] and the final fma each round once; measured 0.89)
+    # polynomial error + rounding of T[j] (1/2 ulp) + the final fma (1/2 ulp) + q's own rounding
+    assert worst < TAB_VARIANTS[(bits, deg)] + 2.3e-16, worst

@@ -23,7 +23,7 @@ def main():
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     eng = importlib.import_module(PKG + ".engine").Engine(0)
     axes = bench.grid_axes(1)
-    res = {"poly11": [], "table256": []}
+    res = {"poly11": [], "table": []}
     tabs = {}
     for v in res:
         eng.tune_exp(v)
@@ -37,12 +37,12 @@ def main():
             eng.sweep(bench.BASE, axes, 0, n)
             torch.cuda.synchronize()
             res[v].append(n / (time.perf_counter() - t0))
-    a, b = tabs["poly11"].cpu().numpy(), tabs["table256"].cpu().numpy()
+    a, b = tabs["poly11"].cpu().numpy(), tabs["table"].cpu().numpy()
     nz = a != 0
     out = {v: {"median": float(np.median(r)), "min": float(np.min(r))} for v, r in res.items()}
     out["max_rel_diff"] = float(np.max(np.abs(a[nz] - b[nz]) / np.abs(a[nz])))
-    out["speedup_table_vs_poly"] = out["table256"]["median"] / out["poly11"]["median"]
-    eng.tune_exp("table256")
+    out["speedup_table_vs_poly"] = out["table"]["median"] / out["poly11"]["median"]
+    eng.tune_exp("table")
     print(json.dumps(out))
 
 

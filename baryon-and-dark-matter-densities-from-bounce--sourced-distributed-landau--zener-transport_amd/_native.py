@@ -46,7 +46,8 @@ FIELD.update({"delta_LZ": 32, "m_mix": 33, "dprime": 34})
 FERMION, BOSON = 0, 1
 THERMAL, NONTHERMAL, REGIME_OTHER = 0, 1, 2
 LZQ_NZ = 1200
-TUNE_EXP, EXP_POLY11, EXP_TABLE = 0, 0, 1  # enum lzq_tune_key / lzq_exp_variant
+TUNE_EXP, TUNE_TRUNCATE = 0, 1  # enum lzq_tune_key
+EXP_POLY11, EXP_TABLE = 0, 1  # enum lzq_exp_variant
 LZQ_MAX_AXES = 8
 
 # Symbols declared in include/lzq.h (checked by tests/test_capi.py against the header).

@@ -41,7 +41,7 @@ constexpr int kWaveSize = 64;
 constexpr int kBlock = LZQ_BLOCK;
 constexpr int kWavesPerBlock = kBlock / kWaveSize;
 #ifndef LZQ_KUNROLL
-#define LZQ_KUNROLL 4
+#define LZQ_KUNROLL 8
 #endif
 #ifndef LZQ_YB
 #define LZQ_YB 1
@@ -56,6 +56,9 @@ constexpr int kWavesPerBlock = kBlock / kWaveSize;
 // compiler can use counted lgkmcnt waits instead of draining behind SMEM)
 #ifndef LZQ_ZLDS
 #define LZQ_ZLDS 0
+#endif
+#ifndef LZQ_YFACT_EARLY
+#define LZQ_YFACT_EARLY 0
 #endif
 constexpr int kKUnroll = LZQ_KUNROLL;  // z-nodes per scalar-load batch (must divide 1200)
 constexpr int kYB = LZQ_YB;            // y-nodes per lane per pass (independent chains)
@@ -238,9 +241,12 @@ __device__ __forceinline__ double c2_scale() { return EXPV == kExpTable ? (doubl
 // For |u| < 2^51 (every non-dead lane, checked on the host) t is exact; dead lanes (whose
 // every node k >= 1 underflows) run with c2 = 0 and are zeroed, so no input reaches the
 // loop with |u| >= 2^51.
-template <int YB, int EXPV>
+//
+// CLAMP = false drops the max (9 VALU/node) on passes whose lanes all satisfy |c2N|*g_max <=
+// N*1534 (no node can leave the clamp range); zsum_dispatch picks it per pass.
+template <int YB, int EXPV, bool CLAMP = true>
 __device__ __forceinline__ void zsum(const ZNode* __restrict__ zt, const double* tab, const double (&c2)[YB],
-                                     double (&F)[YB]) {
+                                     double (&F)[YB], int kend = kNZ) {
 #pragma unroll
   for (int b = 0; b < YB; ++b) F[b] = 0.0;
   if constexpr (EXPV == kExpTable) {
@@ -253,7 +259,7 @@ __device__ __forceinline__ void zsum(const ZNode* __restrict__ zt, const double*
     for (int i = 0; i < kPolyDeg; ++i) Bv[i] = TabPoly<kTabBits, kPolyDeg>::B[i];
     Bv[0] = vgpr_const(Bv[0]);
     const char* tabb = reinterpret_cast<const char*>(tab);
-    for (int k = 0; k < kNZ; k += kKUnroll) {
+    for (int k = 0; k < kend; k += kKUnroll) {
       double g4[kKUnroll], om[kKUnroll];
 #pragma unroll
       for (int kk = 0; kk < kKUnroll; ++kk) {
@@ -271,7 +277,7 @@ __device__ __forceinline__ void zsum(const ZNode* __restrict__ zt, const double*
           const double t = __builtin_fma(c2[b], g4[kk], Mv);
           const double kd = t - Mv;
           r[b][kk] = __builtin_fma(c2[b], g4[kk], -kd);
-          const double tc = __builtin_fmax(t, kTClamp);
+          const double tc = CLAMP ? __builtin_fmax(t, kTClamp) : t;
           kc[b][kk] = (uint32_t)__builtin_bit_cast(uint64_t, tc);
           a[b][kk] = tab_byte_addr(kc[b][kk]);
         }
@@ -289,7 +295,7 @@ __device__ __forceinline__ void zsum(const ZNode* __restrict__ zt, const double*
         }
     }
   } else {
-    for (int k = 0; k < kNZ; k += kKUnroll) {
+    for (int k = 0; k < kend; k += kKUnroll) {
 #pragma unroll
       for (int kk = 0; kk < kKUnroll; ++kk) {
         const double g = zt[k + kk].g4, om = zt[k + kk].omega;
@@ -303,18 +309,49 @@ __device__ __forceinline__ void zsum(const ZNode* __restrict__ zt, const double*
 // Pass-level wrapper: "dead" lanes, c2 * g4_1 <= -N*1077 (every node k >= 1 underflows to
 // exactly 0: g4 is increasing and omega_0 = 0), run the loop with c2 = 0 and are zeroed
 // afterwards -- the same instruction stream, the exact zero, and no |u| >= 2^51 in the loop.
+//
+// truncate != 0 (lzq_tune LZQ_TUNE_TRUNCATE; NOT used by the headline bench, which is dense
+// per SURVEY §8d): the pass stops at kend, the first z-node (rounded up to the unroll) beyond
+// which every live lane has c2*g4_k < -1080 octaves.  Those nodes add omega*2^u < 2^-1080 to
+// F, which the accumulate's rounding discards exactly, so F is bit-identical to the dense sum.
 template <int YB, int EXPV>
 __device__ __forceinline__ void zsum_dispatch(const ZNode* __restrict__ zt, const double* tab,
-                                              const double (&c2)[YB], double (&F)[YB]) {
-  const double g_1 = zt[1].g4;
-  bool dead[YB];
+                                              const double (&c2)[YB], double (&F)[YB], int truncate = 0) {
+  const double g_1 = zt[1].g4, g_max = zt[kNZ - 1].g4;
+  bool dead[YB], small = true;
   double c2e[YB];
 #pragma unroll
   for (int b = 0; b < YB; ++b) {
     dead[b] = c2[b] * g_1 <= -c2_scale<EXPV>() * 1077.0;
     c2e[b] = dead[b] ? 0.0 : c2[b];
+    small = small && c2e[b] * g_max >= (double)kTabKMin;  // every node stays >= KMIN
   }
-  zsum<YB, EXPV>(zt, tab, c2e, F);
+  int kend = kNZ;
+  if (truncate) {
+    // largest per-lane threshold g_thr = -1080 N / c2 (live lanes; dead lanes impose none,
+    // c2 = 0 lanes never underflow)
+    double thr = 0.0;
+#pragma unroll
+    for (int b = 0; b < YB; ++b) {
+      const double tb = dead[b] ? 0.0 : (c2e[b] < 0.0 ? (-1080.0 * c2_scale<EXPV>()) / c2e[b] : __builtin_inf());
+      thr = pymax(thr, tb);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) thr = pymax(thr, __shfl_xor(thr, off, kWaveSize));
+    thr = uniform(thr);
+    // first k with g4_k > thr (g4 increasing): scalar binary search over the z table
+    int lo = 0, hi = kNZ;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (zt[mid].g4 > thr) hi = mid;
+      else lo = mid + 1;
+    }
+    kend = (lo + kKUnroll - 1) / kKUnroll * kKUnroll;
+  }
+  if (EXPV == kExpTable && __all(small))
+    zsum<YB, EXPV, false>(zt, tab, c2e, F, kend);
+  else
+    zsum<YB, EXPV, true>(zt, tab, c2e, F, kend);
 #pragma unroll
   for (int b = 0; b < YB; ++b) F[b] = dead[b] ? 0.0 : F[b];
 }
@@ -353,27 +390,43 @@ __device__ __forceinline__ double wave_sum(double v) {
 
 // Y_B of one point by one wavefront.  fpy:231-267
 template <int YB, int EXPV>
-__device__ double yb_wave(const QuadSetup& s, const ZNode* __restrict__ zt, const double* tab, int lane) {
+__device__ double yb_wave(const QuadSetup& s, const ZNode* __restrict__ zt, const double* tab, int lane,
+                          int truncate) {
   if (s.empty) return 0.0;
   double acc = 0.0;
   const int64_t n = s.n;
   const int64_t per_pass = (int64_t)kWaveSize * YB;
   for (int64_t base = 0; base < n; base += per_pass) {
     double c2[YB];
+    // only y, e^y and the weight stay live across the z-loop (LZQ_YFACT_EARLY=1: the 7
+    // y-factors instead); the y-factors are formed after it
+    double yv[YB], ey[YB], wt[YB];
+#if LZQ_YFACT_EARLY
     YFactors fy[YB];
+#endif
 #pragma unroll
     for (int b = 0; b < YB; ++b) {
       const int64_t j = base + (int64_t)b * kWaveSize + lane;
       const int64_t jj = j < n ? j : n - 1;  // tail lanes recompute the last node with weight 0
-      const double y = y_node(s, jj);
-      const double expy = exp(pymax(pymin(y, 50.0), -50.0));               // fpy:161
-      c2[b] = ((s.cneg * expy) * kLog2E) * c2_scale<EXPV>();                // fpy:163 c, log2 units
-      fy[b] = y_factors(s, y, expy, j < n ? y_weight(s, jj, y) : 0.0);
+      yv[b] = y_node(s, jj);
+      ey[b] = exp(pymax(pymin(yv[b], 50.0), -50.0));                          // fpy:161
+      c2[b] = ((s.cneg * ey[b]) * kLog2E) * c2_scale<EXPV>();                 // fpy:163 c, log2 units
+      wt[b] = j < n ? y_weight(s, jj, yv[b]) : 0.0;
+#if LZQ_YFACT_EARLY
+      fy[b] = y_factors(s, yv[b], ey[b], wt[b]);
+#endif
     }
     double F[YB];
-    zsum_dispatch<YB, EXPV>(zt, tab, c2, F);
+    zsum_dispatch<YB, EXPV>(zt, tab, c2, F, truncate);
 #pragma unroll
-    for (int b = 0; b < YB; ++b) acc = __builtin_fma(fy[b].w, integrand_from(fy[b], F[b]), acc);
+    for (int b = 0; b < YB; ++b) {
+#if !LZQ_YFACT_EARLY
+      const YFactors f = y_factors(s, yv[b], ey[b], wt[b]);
+#else
+      const YFactors& f = fy[b];
+#endif
+      acc = __builtin_fma(f.w, integrand_from(f, F[b]), acc);
+    }
   }
   return wave_sum(acc);
 }
@@ -469,7 +522,7 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void yields_points_kernel(co
                                                               const double* __restrict__ Pov,
                                                               const ZNode* __restrict__ zt,
                                                               const double* __restrict__ gtab,
-                                                              lzq_yield* __restrict__ out) {
+                                                              lzq_yield* __restrict__ out, int truncate) {
 #if LZQ_ZLDS
   __shared__ LdsTables lds;
   stage_tables<EXPV>(zt, &lds);
@@ -487,7 +540,7 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void yields_points_kernel(co
   const double tlo = T_lo ? T_lo[idx] : pt.T_min_over_Tp * pt.T_p_GeV;  // fpy:369
   const double thi = T_hi ? T_hi[idx] : pt.T_max_over_Tp * pt.T_p_GeV;  // fpy:368
   QuadSetup s = quad_setup(pt, P, tlo, thi, n_y);
-  const double Y_B = yb_wave<YB, EXPV>(s, zt, tab, lane);
+  const double Y_B = yb_wave<YB, EXPV>(s, zt, tab, lane, truncate);
   if (lane == 0) out[idx] = epilogue(pt, Y_B, P);
 }
 
@@ -497,7 +550,7 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void yields_grid_kernel(lzq_
                                                             const double* __restrict__ Pov,
                                                             const ZNode* __restrict__ zt,
                                                             const double* __restrict__ gtab,
-                                                            lzq_yield* __restrict__ out) {
+                                                            lzq_yield* __restrict__ out, int truncate) {
 #if LZQ_ZLDS
   __shared__ LdsTables lds;
   stage_tables<EXPV>(zt, &lds);
@@ -514,7 +567,7 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void yields_grid_kernel(lzq_
   const double Pg = grid_point(base, grid, start + local, pt);
   const double P = Pov ? Pov[local] : Pg;
   QuadSetup s = quad_setup(pt, P, pt.T_min_over_Tp * pt.T_p_GeV, pt.T_max_over_Tp * pt.T_p_GeV, n_y);
-  const double Y_B = yb_wave<YB, EXPV>(s, zt, tab, lane);
+  const double Y_B = yb_wave<YB, EXPV>(s, zt, tab, lane, truncate);
   if (lane == 0) out[local] = epilogue(pt, Y_B, P);
 }
 
@@ -567,6 +620,7 @@ bool g_host_ready = false;
 double g_z[LZQ_NZ], g_g4[LZQ_NZ], g_omega[LZQ_NZ];
 uint64_t g_exp2tab[lzq::kTabN];  // lzq::tab_entry_bits layout
 int g_exp_variant = lzq::kExpTable;
+int g_truncate = 0;  // LZQ_TUNE_TRUNCATE
 
 const double* exp_table(int dev) { return reinterpret_cast<const double*>(g_dev_tab[dev] + LZQ_NZ); }
 
@@ -673,6 +727,12 @@ int lzq_tune(int32_t key, int32_t value) {
     g_exp_variant = value;
     return prev;
   }
+  if (key == LZQ_TUNE_TRUNCATE) {
+    if (value != 0 && value != 1) return fail(LZQ_EINVAL, "lzq_tune: truncate must be 0 or 1, got %d", value);
+    int prev = g_truncate;
+    g_truncate = value;
+    return prev;
+  }
   return fail(LZQ_EINVAL, "lzq_tune: unknown key %d", key);
 }
 
@@ -727,11 +787,11 @@ int lzq_yields_batch(const lzq_point* d_points, int64_t n, int32_t n_y, const do
   if (g_exp_variant == lzq::kExpTable)
     hipLaunchKernelGGL((lzq::yields_points_kernel<lzq::kYB, lzq::kExpTable>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
                        (hipStream_t)stream, d_points, n, n_y, d_T_lo, d_T_hi, d_P, g_dev_tab[dev], exp_table(dev),
-                       d_out);
+                       d_out, g_truncate);
   else
     hipLaunchKernelGGL((lzq::yields_points_kernel<lzq::kYB, lzq::kExpPoly11>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
                        (hipStream_t)stream, d_points, n, n_y, d_T_lo, d_T_hi, d_P, g_dev_tab[dev], exp_table(dev),
-                       d_out);
+                       d_out, g_truncate);
   LZQ_HIP(hipGetLastError());
   return LZQ_OK;
 }
@@ -773,10 +833,12 @@ int lzq_sweep_grid(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, 
   if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_sweep_grid: count too large for one launch");
   if (g_exp_variant == lzq::kExpTable)
     hipLaunchKernelGGL((lzq::yields_grid_kernel<lzq::kYB, lzq::kExpTable>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
-                       (hipStream_t)stream, *base, g, start, count, n_y, d_P, g_dev_tab[dev], exp_table(dev), d_out);
+                       (hipStream_t)stream, *base, g, start, count, n_y, d_P, g_dev_tab[dev], exp_table(dev), d_out,
+                       g_truncate);
   else
     hipLaunchKernelGGL((lzq::yields_grid_kernel<lzq::kYB, lzq::kExpPoly11>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
-                       (hipStream_t)stream, *base, g, start, count, n_y, d_P, g_dev_tab[dev], exp_table(dev), d_out);
+                       (hipStream_t)stream, *base, g, start, count, n_y, d_P, g_dev_tab[dev], exp_table(dev), d_out,
+                       g_truncate);
   LZQ_HIP(hipGetLastError());
   return LZQ_OK;
 }

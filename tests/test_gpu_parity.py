@@ -115,6 +115,25 @@ def test_quadrature_operator_api(gpu_engine):
     assert rel_err(bs.aov.A_over_V_y(y), 3.197927e-10) < 2e-7
 
 
+def test_truncation_is_bit_identical(gpu_engine):
+    """LZQ_TUNE_TRUNCATE stops each wave's z-sum where every remaining term is < 2^-1080:
+    the yields must be bit-identical to the dense sums (golden points + a C2 grid slice)."""
+    pts = golden("golden_points.json")["points"]
+    r = recs([full_cfg(p["config"]) for p in pts])
+    axes = [("m_mix", np.logspace(-3.0, 0.0, 40)), ("dprime", np.logspace(-3.0, 1.0, 50))]
+    assert gpu_engine.tune_truncate(False) is False  # dense is the default
+    dense = gpu_engine.yields(r).cpu().numpy()
+    dense_grid = gpu_engine.sweep(BASE_CFG, axes, 0, 2000).cpu().numpy()
+    try:
+        gpu_engine.tune_truncate(True)
+        trunc = gpu_engine.yields(r).cpu().numpy()
+        trunc_grid = gpu_engine.sweep(BASE_CFG, axes, 0, 2000).cpu().numpy()
+    finally:
+        gpu_engine.tune_truncate(False)
+    assert np.array_equal(dense, trunc, equal_nan=True)
+    assert np.array_equal(dense_grid, trunc_grid)
+
+
 def test_deterministic_and_batch_independent(gpu_engine):
     pts = golden("golden_points.json")["points"][:40]
     r = recs([full_cfg(p["config"]) for p in pts])

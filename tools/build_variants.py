@@ -13,9 +13,8 @@ B = importlib.import_module(PKG + ".build")
 
 GRID = {"LZQ_MAGIC": [0, 1], "LZQ_KUNROLL": [4, 8], "LZQ_YB": [1, 2]}
 # explicit list (overrides the full product when non-empty); keys omitted take the defaults
-CONFIGS = [dict(LZQ_TABBITS=b, LZQ_POLYDEG=d, LZQ_BLOCK=blk) for b, d, blk in
-           ((13, 2, 512), (13, 2, 1024), (12, 2, 256), (12, 2, 512), (14, 2, 1024))] + \
-          [dict(LZQ_TABBITS=13, LZQ_POLYDEG=2, LZQ_KUNROLL=8), dict(LZQ_TABBITS=13, LZQ_POLYDEG=2, LZQ_YB=2)]
+CONFIGS = [dict(LZQ_KUNROLL=4), dict(LZQ_KUNROLL=8), dict(LZQ_KUNROLL=8, LZQ_YFACT_EARLY=1),
+           dict(LZQ_KUNROLL=4, LZQ_YB=2), dict(LZQ_KUNROLL=8, LZQ_YB=2)]
 
 
 def main():

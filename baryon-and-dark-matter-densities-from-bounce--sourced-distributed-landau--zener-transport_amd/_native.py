@@ -36,6 +36,18 @@ class LzqAxis(ctypes.Structure):
     _fields_ = [("field", ctypes.c_int32), ("n", ctypes.c_int32), ("values", ctypes.c_void_p)]
 
 
+class LzqOdeParams(ctypes.Structure):
+    _fields_ = [("sigma_v_chi_GeV_m2", ctypes.c_double), ("Gamma_wash_over_H", ctypes.c_double),
+                ("deplete_DM_from_source", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+ODE_DTYPE = np.dtype([("sigma_v_chi_GeV_m2", "<f8"), ("Gamma_wash_over_H", "<f8"),
+                      ("deplete_DM_from_source", "<i4"), ("reserved", "<i4")])
+assert ctypes.sizeof(LzqOdeParams) == 24 == ODE_DTYPE.itemsize
+ODE_NT, ODE_WS_PER_POINT = 800, 3200  # LZQ_ODE_NT, LZQ_ODE_WS_PER_POINT
+ODE_STATUS = {0: "ok", 1: "`x` must be strictly increasing sequence.", 2: "`max_step` must be positive.",
+              3: "more than max_steps integration steps", 4: "Radau stage Newton iteration did not converge"}
+
 POINT_DTYPE = np.dtype([(n, "<f8") for n in POINT_DOUBLE_FIELDS] + [(n, "<i4") for n in POINT_INT_FIELDS])
 assert ctypes.sizeof(LzqPoint) == 136 == POINT_DTYPE.itemsize
 assert ctypes.sizeof(LzqYield) == 48
@@ -53,7 +65,8 @@ LZQ_MAX_AXES = 8
 # Symbols declared in include/lzq.h (checked by tests/test_capi.py against the header).
 EXPORTS = ("lzq_abi_version", "lzq_last_error", "lzq_init", "lzq_ztables", "lzq_tune", "lzq_aov_batch",
            "lzq_jchi_batch", "lzq_yields_batch", "lzq_sweep_grid", "lzq_p_closed_form",
-           "lzq_lz_propagate")
+           "lzq_lz_propagate", "lzq_ode_tables", "lzq_ode_integrate", "lzq_ode_batch", "lzq_ode_aov_T",
+           "lzq_ode_rhs")
 
 
 class LzqError(RuntimeError):
@@ -90,6 +103,11 @@ def load(path: str | None = None):
     L.lzq_sweep_grid.argtypes = [P(LzqPoint), P(LzqAxis), i32, i64, i64, i32, vp, vp, vp]
     L.lzq_p_closed_form.argtypes = [vp, i64, vp, vp]
     L.lzq_lz_propagate.argtypes = [vp, vp, vp, i64, i32, d, d, i32, vp, vp]
+    L.lzq_ode_tables.argtypes = [vp, i64, vp, vp, vp, i64, vp, vp]
+    L.lzq_ode_integrate.argtypes = [vp, vp, i64, vp, i64, i64, vp, vp, vp]
+    L.lzq_ode_batch.argtypes = [vp, vp, i64, vp, i64, i64, vp, vp, vp]
+    L.lzq_ode_aov_T.argtypes = [P(LzqPoint), d, d, vp, vp, i64, vp, vp]
+    L.lzq_ode_rhs.argtypes = [P(LzqPoint), P(LzqOdeParams), d, d, vp, vp, vp, i64, vp, vp]
     for name in EXPORTS:
         if name not in ("lzq_abi_version", "lzq_last_error"):
             getattr(L, name).restype = ctypes.c_int

@@ -3,7 +3,8 @@
 `AoverVKernel` and `BoltzmannSystem` keep the constructor signatures and method names of
 fpy:140-165 and fpy:192-267 so code written against the reference reads the same, but every
 evaluation runs on the GPU through the C ABI (engine.Engine).  Only the direct-quadrature
-path is provided; the Radau ODE fallback (fpy:207-219, 270-286) is out of scope and raises.
+path and the ODE fallback's operators (build_tables / A_over_V_T / rhs, fpy:207-219, 270-286)
+run on the GPU; the integration itself is engine.Engine.ode (lzq_ode_batch), used by cli.py.
 """
 from __future__ import annotations
 
@@ -11,7 +12,7 @@ import math
 
 import numpy as np
 
-from .config import Config, fast_path_ok, to_point
+from .config import Config, fast_path_ok, to_ode_params, to_point
 from .engine import default_engine
 
 LZQ_NZ, LZQ_ZMAX = 1200, 30.0
@@ -65,10 +66,42 @@ class BoltzmannSystem:
         out = default_engine().yields(rec, n_y=int(n_y), T_lo=[float(T_lo)], T_hi=[float(T_hi)], P=[self.P])
         return float(out[0, 0].item())
 
-    def build_tables(self, *a, **k):
-        raise NotImplementedError("ODE fallback (fpy:207-219, 270-286) is out of scope: use the fast path")
+    # ---- ODE fallback operators (fpy:207-219, 270-286) --------------------------------------
+    def build_tables(self, T_lo: float, T_hi: float, n: int = 800):
+        """fpy:207-212 on the GPU: A/V at linspace(T_lo, T_hi, 800) + not-a-knot cubic spline."""
+        if int(n) != 800:
+            raise NotImplementedError("the lzq ODE tables have n = 800 knots (fpy:207, fpy:386)")
+        if not (float(T_hi) > float(T_lo)):
+            raise ValueError("`x` must be strictly increasing sequence.")
+        eng = default_engine()
+        self._T_lo, self._T_hi = float(T_lo), float(T_hi)
+        self._rec = to_point(self.cfg, P=self.P)
+        self._work, status = eng.ode_tables(self._rec, [self._T_lo], [self._T_hi])
+        if int(status[0].item()) != 0:
+            raise ValueError("`x` must be strictly increasing sequence.")
 
-    rhs = A_over_V_T = build_tables
+    def _need_tables(self):
+        if getattr(self, "_work", None) is None:
+            raise RuntimeError("call build_tables(T_lo, T_hi) first (fpy:207)")
+
+    def A_over_V_Ts(self, Ts) -> np.ndarray:
+        """Batched fpy:214-218."""
+        self._need_tables()
+        return default_engine().ode_aov_T(self._rec, self._T_lo, self._T_hi, self._work, Ts).cpu().numpy()
+
+    def A_over_V_T(self, T: float) -> float:
+        """fpy:214-218 (needs build_tables, like the reference's spline path)."""
+        return float(self.A_over_V_Ts([T])[0])
+
+    def rhs_batch(self, xs, Ys) -> np.ndarray:
+        """Batched fpy:270-286: (n, 2) array of (dY_chi/dx, dY_B/dx)."""
+        self._need_tables()
+        return default_engine().ode_rhs(self._rec, to_ode_params(self.cfg), self._T_lo, self._T_hi, self._work, xs,
+                                        Ys).cpu().numpy()
+
+    def rhs(self, x: float, Y) -> np.ndarray:
+        """fpy:270-286."""
+        return self.rhs_batch([float(x)], [[float(Y[0]), float(Y[1])]])[0]
 
     def fast_path_ok(self) -> bool:
         return fast_path_ok(self.cfg)

@@ -4,8 +4,8 @@
 
 Flags, messages, exit behaviour and output bytes follow the reference (checked against
 the reference's own output in tests/golden/golden_cli.json).  Configurations outside the
-fast quadrature path (fpy:372) need the ODE fallback, which is out of scope: they raise
-NotImplementedError instead of silently computing something else.
+fast quadrature path (fpy:372) take the ODE fallback (fpy:385-410) on the GPU
+(engine.Engine.ode -> lzq_ode_batch), with the reference's error behaviour.
 """
 from __future__ import annotations
 
@@ -15,7 +15,8 @@ import math
 
 import numpy as np
 
-from .config import fast_path_ok, load_config, to_point, write_template
+from . import _native
+from .config import fast_path_ok, load_config, to_ode_params, to_point, write_template
 from .engine import default_engine
 from .lz import maybe_P
 from .physics_host import y_of_T
@@ -42,16 +43,22 @@ def main(argv=None):
 
     cfg = load_config(args.config)
     P_used = maybe_P(cfg, args.profile_csv)
-    if not fast_path_ok(cfg):
-        raise NotImplementedError("sigma_v / Gamma_wash / depletion need the Radau ODE fallback "
-                                  "(fpy:385-410), which this engine does not implement")
-    low = cfg.regime.lower()
-    if not (low.startswith("therm") or low.startswith("non")):
-        # fpy:376-384 has no else-branch on the fast path
-        raise UnboundLocalError("local variable 'Ychi_fin' referenced before assignment")
-
+    if fast_path_ok(cfg):
+        low = cfg.regime.lower()
+        if not (low.startswith("therm") or low.startswith("non")):
+            # fpy:376-384 has no else-branch on the fast path
+            raise UnboundLocalError("local variable 'Ychi_fin' referenced before assignment")
     eng = default_engine()
-    table = eng.yields(to_point(cfg, P=P_used), n_y=8000)  # fpy:374 + fpy:376-417 on the GPU
+    if fast_path_ok(cfg):
+        table = eng.yields(to_point(cfg, P=P_used), n_y=8000)  # fpy:374 + fpy:376-417 on the GPU
+    else:
+        # fpy:385-410: build_tables + Radau (lzq_ode_batch), then fpy:412-417
+        table, status = eng.ode(to_point(cfg, P=P_used), to_ode_params(cfg))
+        st = int(status[0].item())
+        if st in (1, 2):  # scipy's ValueError (CubicSpline knots / solve_ivp max_step)
+            raise ValueError(_native.ODE_STATUS[st])
+        if st != 0:
+            raise RuntimeError(f"lzq ODE fallback: {_native.ODE_STATUS[st]}")
     YB_fin, Ychi_fin, rhoB0, rhoDM0, ratio, _ = (float(v) for v in table[0].cpu().numpy())
 
     print("\n=== Results (today) ===")

@@ -118,6 +118,24 @@ def to_point(cfg, P: Optional[float] = None) -> np.ndarray:
     return rec
 
 
+def to_ode_params(cfg) -> np.ndarray:
+    """The three Config fields of the ODE fallback (fpy:279-284) -> one lzq_ode_params record."""
+    c = cfg if isinstance(cfg, dict) else cfg.__dict__
+    rec = np.zeros(1, dtype=_native.ODE_DTYPE)
+    rec["sigma_v_chi_GeV_m2"] = float(c["sigma_v_chi_GeV_m2"])
+    rec["Gamma_wash_over_H"] = float(c["Gamma_wash_over_H"])
+    rec["deplete_DM_from_source"] = int(bool(c["deplete_DM_from_source"]))
+    return rec
+
+
+def to_ctypes_ode(rec: np.ndarray) -> "_native.LzqOdeParams":
+    o = _native.LzqOdeParams()
+    o.sigma_v_chi_GeV_m2 = float(rec["sigma_v_chi_GeV_m2"].item())
+    o.Gamma_wash_over_H = float(rec["Gamma_wash_over_H"].item())
+    o.deplete_DM_from_source = int(rec["deplete_DM_from_source"].item())
+    return o
+
+
 def to_ctypes_point(rec: np.ndarray) -> "_native.LzqPoint":
     p = _native.LzqPoint()
     for n in _native.POINT_DOUBLE_FIELDS + _native.POINT_INT_FIELDS:

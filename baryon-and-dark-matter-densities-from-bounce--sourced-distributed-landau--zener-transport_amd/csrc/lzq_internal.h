@@ -1,0 +1,25 @@
+// lzq_internal.h -- declarations shared between the library's translation units (not ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/lzq.h"
+
+namespace lzq {
+
+constexpr int kOdeNT = LZQ_ODE_NT;           // fpy:207 build_tables(n=800)
+constexpr int kOdeWS = LZQ_ODE_WS_PER_POINT;  // workspace doubles per point
+
+// Per-point workspace layout (doubles): w[4k + 0..3] = PPoly c0..c3 of interval k < 799
+// (value c0 s^3 + c1 s^2 + c2 s + c3, s = T - T_k); w[kOdeWS - 1] holds A/V at the last knot
+// while the spline is built.
+
+// A/V at the 800 T-knots of every point into w[4k + 3] / w[kOdeWS - 1] (lzq_kernels.hip: the
+// quadrature kernels' z-sum, one wavefront per point).  Host-side launch; sets lzq_last_error.
+int launch_ode_aov_tables(const lzq_point* d_points, int64_t n, const double* d_T_lo, const double* d_T_hi,
+                          double* d_work, hipStream_t stream);
+
+}  // namespace lzq
+
+// lzq_kernels.hip's error plumbing (thread-local message behind lzq_last_error)
+int lzq_set_error(int code, const char* msg);

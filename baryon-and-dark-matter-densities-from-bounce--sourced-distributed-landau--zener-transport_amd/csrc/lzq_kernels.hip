@@ -27,6 +27,7 @@
 
 #include "../../include/lzq.h"
 #include "lzq_exp2.h"
+#include "lzq_internal.h"
 #include "lzq_physics.h"
 
 namespace lzq {
@@ -588,6 +589,40 @@ __global__ __launch_bounds__(kBlock) void aov_kernel(lzq_point pt, const double*
   if (live) out[i] = (y > 50.0) ? 0.0 : (s.pref0 * expy) * F[0];
 }
 
+// fpy:207-212 build_tables, first half: A/V at the 800 knots Ts = linspace(T_lo, T_hi, 800)
+// of main()'s window (fpy:368-369), np.maximum(Av, 0), one wavefront per point (lane i takes
+// knots i, i+64, ...).  The spline is fitted by lzq_ode.hip's ode_spline_kernel.
+template <int EXPV>
+__global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void ode_aov_table_kernel(const lzq_point* __restrict__ pts,
+                                                                               int64_t n, const ZNode* __restrict__ zt,
+                                                                               const double* __restrict__ gtab,
+                                                                               const double* __restrict__ Tlo,
+                                                                               const double* __restrict__ Thi,
+                                                                               double* __restrict__ ws, int truncate) {
+  __shared__ double lds_tab[kTabN];
+  const double* tab = stage_table<EXPV>(gtab, lds_tab);
+  const int lane = threadIdx.x & (kWaveSize - 1);
+  const int64_t idx = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  if (idx >= n) return;  // wave-uniform
+  const lzq_point pt = pts[idx];
+  const double Tp = pt.T_p_GeV, B = pt.beta_over_H;
+  const double T_lo = Tlo ? Tlo[idx] : pt.T_min_over_Tp * Tp, T_hi = Thi ? Thi[idx] : pt.T_max_over_Tp * Tp;
+  const double stepT = (T_hi - T_lo) / (double)(kOdeNT - 1);
+  const QuadSetup s = quad_setup(pt, 0.0, 1.0, 1.0, LZQ_NY_MIN);  // only pref0 / cneg are used
+  double* w = ws + idx * (int64_t)kOdeWS;
+  for (int base = 0; base < kOdeNT; base += kWaveSize) {
+    const int i = base + lane;
+    const int ii = i < kOdeNT ? i : kOdeNT - 1;
+    const double T = linspace_at(T_lo, T_hi, stepT, ii, kOdeNT);
+    const double y = y_of_T(T, Tp, B);
+    const double expy = exp(pymax(pymin(y, 50.0), -50.0));  // fpy:161
+    double c2[1] = {((s.cneg * expy) * kLog2E) * c2_scale<EXPV>()}, F[1];
+    zsum_dispatch<1, EXPV>(zt, tab, c2, F, truncate);
+    const double Av = (y > 50.0) ? 0.0 : (s.pref0 * expy) * F[0];  // fpy:159-165
+    if (i < kOdeNT) w[i < kOdeNT - 1 ? 4 * i + 3 : kOdeWS - 1] = pymax(Av, 0.0);
+  }
+}
+
 // fpy:222-223 (J_chi_flux fpy:122-123), one lane per T
 __global__ __launch_bounds__(kBlock) void jchi_kernel(lzq_point pt, const double* __restrict__ Ts, int64_t n,
                                                      double* __restrict__ out) {
@@ -700,6 +735,23 @@ constexpr int64_t kMaxGrid = 2147483647LL;
 }  // namespace
 
 int lzq_set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+
+int lzq::launch_ode_aov_tables(const lzq_point* d_points, int64_t n, const double* d_T_lo, const double* d_T_hi,
+                               double* d_work, hipStream_t stream) {
+  if (n == 0) return LZQ_OK;
+  int dev, rc = ensure_device(&dev);
+  if (rc) return rc;
+  const int64_t nb = blocks_for(n, lzq::kWavesPerBlock);
+  if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_ode_tables: n too large");
+  if (g_exp_variant == lzq::kExpTable)
+    hipLaunchKernelGGL(lzq::ode_aov_table_kernel<lzq::kExpTable>, dim3((unsigned)nb), dim3(lzq::kBlock), 0, stream,
+                       d_points, n, g_dev_tab[dev], exp_table(dev), d_T_lo, d_T_hi, d_work, g_truncate);
+  else
+    hipLaunchKernelGGL(lzq::ode_aov_table_kernel<lzq::kExpPoly11>, dim3((unsigned)nb), dim3(lzq::kBlock), 0, stream,
+                       d_points, n, g_dev_tab[dev], exp_table(dev), d_T_lo, d_T_hi, d_work, g_truncate);
+  LZQ_HIP(hipGetLastError());
+  return LZQ_OK;
+}
 
 extern "C" {
 

@@ -1,0 +1,519 @@
+// lzq_ode.hip -- the reference's ODE fallback (fpy = /root/reference/first_principles_yields.py,
+// lines 200-219 build_tables / A_over_V_T, 270-286 rhs, 385-417 main) for batches of points.
+//
+//   1. ode_aov_table_kernel (lzq_kernels.hip): A/V at the 800 T-knots, one wavefront per point;
+//   2. ode_spline_kernel: scipy CubicSpline(bc_type='not-a-knot') of those knots, one lane per
+//      point (Thomas elimination of the slope system, then the PPoly coefficients);
+//   3. ode_integrate_kernel: the reference's Radau IIA (3 stages, order 5) on uniform steps
+//      h <= max_step (fpy:404), one lane per point, state in registers.  The two equations
+//      decouple: Y_B is linear (each step is one 3x3 solve); Y_chi is a Riccati equation
+//      (Newton on the 3x3 stage system with its exact Jacobian; a linear update when
+//      sigma_v = 0).  tests/golden/golden_ode.json: the reference's own Radau output sits
+//      within ~1e-14 of its converged solution, so a fixed-step Radau reproduces it.
+//
+// The ingredients of rhs follow fpy:270-286 in the reference's operation order, with T**3 as
+// (T*T)*T and T**1.5 as T*sqrt(T) (<= 2 ulp from pow; the device pow is ~100 VALU).
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdio.h>
+
+#include "../../include/lzq.h"
+#include "lzq_internal.h"
+#include "lzq_physics.h"
+
+namespace lzq {
+
+constexpr int kOdeBlock = 256;
+
+// ---------------------------------------------------------------------------------------
+// per-point constants of rhs (one lane per point)
+// ---------------------------------------------------------------------------------------
+struct OdePoint {
+  double m, m3, Tp, B, sig, flux, P;
+  double H0;     // 1.66 sqrt(g*)                       fpy:85
+  double s0;     // (2 pi^2/45) g*s                      fpy:88
+  double c_rel;  // g 3 zeta3/(4 pi^2) | g zeta3/pi^2    fpy:96-99
+  double c_nr;   // g (m/2pi)^1.5                        fpy:104
+  double v0;     // pi max(m, 1e-20)                     fpy:117
+  double sigmav, gamma_w;
+  int deplete;
+  double T_lo, T_hi, stepT;
+};
+
+__device__ __forceinline__ OdePoint ode_point(const lzq_point& pt, const lzq_ode_params& od) {
+  OdePoint o;
+  o.m = pt.m_chi_GeV;
+  o.m3 = pt.m_chi_GeV / 3.0;
+  o.Tp = pt.T_p_GeV;
+  o.B = pt.beta_over_H;
+  o.sig = pymax(pt.source_shape_sigma_y, 1e-6);
+  o.flux = pt.incident_flux_scale;
+  o.P = pt.P_chi_to_B;
+  o.H0 = 1.66 * sqrt(pt.g_star);
+  o.s0 = (2.0 * (kPi * kPi) / 45.0) * pt.g_star_s;
+  o.c_rel = (pt.stats == 0) ? pt.g_chi * (3.0 * kZeta3 / (4.0 * (kPi * kPi))) : pt.g_chi * (kZeta3 / (kPi * kPi));
+  o.c_nr = pt.g_chi * pow(pt.m_chi_GeV / (2.0 * kPi), 1.5);
+  o.v0 = kPi * pymax(pt.m_chi_GeV, 1e-20);
+  o.sigmav = pymax(od.sigma_v_chi_GeV_m2, 0.0);  // fpy:279
+  o.gamma_w = pymax(od.Gamma_wash_over_H, 0.0);  // fpy:284
+  o.deplete = od.deplete_DM_from_source != 0;
+  o.T_lo = pt.T_min_over_Tp * pt.T_p_GeV;         // fpy:369
+  o.T_hi = pt.T_max_over_Tp * pt.T_p_GeV;         // fpy:368
+  o.stepT = (o.T_hi - o.T_lo) / (double)(kOdeNT - 1);
+  return o;
+}
+
+// fpy:214-218 A_over_V_T: min(max(T, T_lo), T_hi), then the PPoly of scipy (_ppoly.pyx:
+// interval k with T_k <= T < T_{k+1}, T == T_hi in the last one; c3 + c2 s + c1 s^2 + c0 s^3
+// accumulated in that order, powers by repeated multiplication).
+__device__ __forceinline__ double spline_eval(const OdePoint& o, const double* __restrict__ w, double T) {
+  const double Tq = pymin(pymax(T, o.T_lo), o.T_hi);
+  int k = (int)((Tq - o.T_lo) / o.stepT);
+  k = k < 0 ? 0 : (k > kOdeNT - 2 ? kOdeNT - 2 : k);
+  // the quotient can land one knot off after rounding: settle against the knots themselves
+  if (Tq < linspace_at(o.T_lo, o.T_hi, o.stepT, k, kOdeNT) && k > 0) --k;
+  else if (k < kOdeNT - 2 && Tq >= linspace_at(o.T_lo, o.T_hi, o.stepT, k + 1, kOdeNT)) ++k;
+  const double s = Tq - linspace_at(o.T_lo, o.T_hi, o.stepT, k, kOdeNT);
+  const double* c = w + 4 * k;
+  const double c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3];
+  double z = s, res = c3;
+  res = res + c2 * z;
+  z = z * s;
+  res = res + c1 * z;
+  z = z * s;
+  res = res + c0 * z;
+  return res;
+}
+
+// The ingredients of rhs(x, .) (fpy:270-286), which do not depend on Y:
+//   dY_chi/dx = -lam (Y_chi^2 - E2) - S        lam = sigmav s/(H x), E2 = (n_eq/s)^2,
+//                                               S = (deplete ? SB/s : 0)/(H x)
+//   dY_B/dx   = alpha - beta Y_B               alpha = (SB/s)/(H x), beta = (gamma_w H)/(H x)
+struct OdeStage {
+  double lam, E2, S, alpha, beta;
+};
+
+__device__ __forceinline__ OdeStage ode_stage(const OdePoint& o, const double* __restrict__ w, double x,
+                                              double* Av_out = nullptr) {
+  const double T = o.m / pymax(x, 1e-30);
+  const double H = pymax(o.H0 * T * T / kMplGeV, 1e-300);     // fpy:273 via fpy:85
+  const double T3 = (T * T) * T;
+  const double s = pymax(o.s0 * T3, 1e-300);                  // fpy:274 via fpy:88
+  const double y = y_of_T(T, o.Tp, o.B);                      // fpy:275
+  const double q = y / o.sig;
+  const double window = exp(-0.5 * (q * q));                  // fpy:276
+  double n_eq, vbar;                                          // fpy:90-120
+  if (T > o.m3) {
+    n_eq = o.c_rel * T3;
+    vbar = 1.0;
+  } else {
+    n_eq = o.c_nr * (T * sqrt(T)) * exp(-o.m / pymax(T, 1e-30));
+    vbar = sqrt(pymax(8.0 * T / o.v0, 0.0));
+  }
+  const double J = o.flux * (0.25 * n_eq * vbar);             // fpy:222-223
+  const double Av = spline_eval(o, w, T);                     // fpy:214-218
+  if (Av_out) *Av_out = Av;
+  const double SB = o.P * J * Av * window;                    // fpy:277
+  const double E = n_eq / s;                                  // fpy:280
+  const double SBs = SB / s;
+  const double Hx = H * x;
+  OdeStage st;
+  st.lam = (o.sigmav * s) / Hx;
+  st.E2 = E * E;
+  st.S = (o.deplete ? SBs : 0.0) / Hx;                        // fpy:282
+  st.alpha = SBs / Hx;                                        // fpy:285
+  st.beta = (o.gamma_w * H) / Hx;
+  return st;
+}
+
+// CubicSpline's check of the knots linspace(T_lo, T_hi, 800): strictly increasing.
+__device__ __forceinline__ bool ode_grid_ok(double T_lo, double T_hi, double stepT) {
+  bool ok = true;
+  double prev = linspace_at(T_lo, T_hi, stepT, 0, kOdeNT);
+  for (int k = 1; k < kOdeNT; ++k) {
+    const double xk = linspace_at(T_lo, T_hi, stepT, k, kOdeNT);
+    ok = ok && (xk > prev);
+    prev = xk;
+  }
+  return ok;
+}
+
+// Radau IIA, 3 stages (the method of scipy's Radau): nodes C, matrix A (row 3 = weights).
+struct Radau {
+  double c[3], a[3][3];
+};
+
+__device__ __forceinline__ Radau radau_tableau() {
+  Radau r;
+  const double s6 = sqrt(6.0);
+  r.c[0] = (4.0 - s6) / 10.0;
+  r.c[1] = (4.0 + s6) / 10.0;
+  r.c[2] = 1.0;
+  r.a[0][0] = (88.0 - 7.0 * s6) / 360.0;
+  r.a[0][1] = (296.0 - 169.0 * s6) / 1800.0;
+  r.a[0][2] = (-2.0 + 3.0 * s6) / 225.0;
+  r.a[1][0] = (296.0 + 169.0 * s6) / 1800.0;
+  r.a[1][1] = (88.0 + 7.0 * s6) / 360.0;
+  r.a[1][2] = (-2.0 - 3.0 * s6) / 225.0;
+  r.a[2][0] = (16.0 - s6) / 36.0;
+  r.a[2][1] = (16.0 + s6) / 36.0;
+  r.a[2][2] = 1.0 / 9.0;
+  return r;
+}
+
+// x = M^-1 b for the 3x3 stage matrices M = I + h A diag(d) (partial pivoting; branch-free
+// selects, so the lanes of a wave stay converged).
+__device__ __forceinline__ void solve3(double M[3][3], double b[3]) {
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+#pragma unroll
+    for (int r = c + 1; r < 3; ++r) {
+      const bool sw = fabs(M[r][c]) > fabs(M[c][c]);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const double t = M[c][k];
+        M[c][k] = sw ? M[r][k] : t;
+        M[r][k] = sw ? t : M[r][k];
+      }
+      const double t = b[c];
+      b[c] = sw ? b[r] : t;
+      b[r] = sw ? t : b[r];
+    }
+#pragma unroll
+    for (int r = c + 1; r < 3; ++r) {
+      const double f = M[r][c] / M[c][c];
+#pragma unroll
+      for (int k = c; k < 3; ++k) M[r][k] = M[r][k] - f * M[c][k];
+      b[r] = b[r] - f * b[c];
+    }
+  }
+#pragma unroll
+  for (int c = 2; c >= 0; --c) {
+    double acc = b[c];
+#pragma unroll
+    for (int k = c + 1; k < 3; ++k) acc = acc - M[c][k] * b[k];
+    b[c] = acc / M[c][c];
+  }
+}
+
+// One Radau step of size h for both equations; false when the Y_chi Newton iteration fails.
+__device__ __forceinline__ bool radau_step(const Radau& R, const OdeStage (&st)[3], double h, double& Ychi,
+                                           double& YB) {
+  // Y_B: (I + h A diag(beta)) Z = YB + h A alpha, exactly
+  {
+    double M[3][3], b[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      double acc = YB;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        acc = acc + h * R.a[i][j] * st[j].alpha;
+        M[i][j] = (i == j ? 1.0 : 0.0) + h * R.a[i][j] * st[j].beta;
+      }
+      b[i] = acc;
+    }
+    solve3(M, b);
+    YB = b[2];
+  }
+  // Y_chi: Z_i = Y + h sum_j a_ij f_j(Z_j), f_j(Z) = -lam_j (Z^2 - E2_j) - S_j
+  const bool nonlinear = st[0].lam != 0.0 || st[1].lam != 0.0 || st[2].lam != 0.0;
+  double Z[3] = {Ychi, Ychi, Ychi};
+  if (!nonlinear) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      double acc = Ychi;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc = acc - h * R.a[i][j] * st[j].S;
+      Z[i] = acc;
+    }
+    Ychi = Z[2];
+    return true;
+  }
+  for (int it = 0; it < 40; ++it) {
+    double M[3][3], g[3];
+    double f[3], jf[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      f[j] = -st[j].lam * (Z[j] * Z[j] - st[j].E2) - st[j].S;
+      jf[j] = -st[j].lam * (2.0 * Z[j]);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      double acc = Z[i] - Ychi;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        acc = acc - h * R.a[i][j] * f[j];
+        M[i][j] = (i == j ? 1.0 : 0.0) - h * R.a[i][j] * jf[j];
+      }
+      g[i] = -acc;
+    }
+    solve3(M, g);
+    double dmax = 0.0, zmax = 0.0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      Z[i] = Z[i] + g[i];
+      dmax = pymax(dmax, fabs(g[i]));
+      zmax = pymax(zmax, fabs(Z[i]));
+    }
+    if (!(dmax > 1e-15 * zmax)) {
+      Ychi = Z[2];
+      return true;
+    }
+  }
+  return false;
+}
+
+// ---------------------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------------------
+// fpy:207-212 build_tables, second half: scipy CubicSpline(Ts, Av, bc_type='not-a-knot')
+// (scipy/interpolate/_cubic.py), one lane per point.  The slope system is solved by Thomas
+// elimination (scipy: banded LU with partial pivoting; equal to rounding); the forward sweep
+// parks (c', d') in the c0/c1 slots of the point's workspace.
+__global__ __launch_bounds__(kOdeBlock) void ode_spline_kernel(const lzq_point* __restrict__ pts, int64_t n,
+                                                               const double* __restrict__ Tlo,
+                                                               const double* __restrict__ Thi,
+                                                               double* __restrict__ ws, int32_t* __restrict__ status) {
+  const int64_t i = (int64_t)blockIdx.x * kOdeBlock + threadIdx.x;
+  if (i >= n) return;
+  const lzq_point pt = pts[i];
+  const double T_lo = Tlo ? Tlo[i] : pt.T_min_over_Tp * pt.T_p_GeV;
+  const double T_hi = Thi ? Thi[i] : pt.T_max_over_Tp * pt.T_p_GeV;
+  const double stepT = (T_hi - T_lo) / (double)(kOdeNT - 1);
+  double* w = ws + i * (int64_t)kOdeWS;
+  constexpr int N = kOdeNT;
+  auto X = [&](int k) { return linspace_at(T_lo, T_hi, stepT, k, N); };
+  auto Yk = [&](int k) { return k < N - 1 ? w[4 * k + 3] : w[kOdeWS - 1]; };
+  if (!ode_grid_ok(T_lo, T_hi, stepT)) {
+    if (status) status[i] = LZQ_ODE_BAD_GRID;
+    return;
+  }
+  // forward sweep
+  double dxm1 = X(1) - X(0), slm1 = (Yk(1) - Yk(0)) / dxm1;  // dx[k-1], slope[k-1]
+  double cpm1, dpm1;
+  {
+    const double dx1 = X(2) - X(1), sl1 = (Yk(2) - Yk(1)) / dx1;
+    const double d = X(2) - X(0);
+    const double r = ((dxm1 + 2.0 * d) * dx1 * slm1 + (dxm1 * dxm1) * sl1) / d;
+    cpm1 = d / dx1;
+    dpm1 = r / dx1;
+    w[0] = cpm1;
+    w[1] = dpm1;
+  }
+  for (int k = 1; k < N - 1; ++k) {
+    const double dxk = X(k + 1) - X(k), slk = (Yk(k + 1) - Yk(k)) / dxk;
+    const double a = dxk, b = 2.0 * (dxm1 + dxk), c = dxm1;
+    const double r = 3.0 * (dxk * slm1 + dxm1 * slk);
+    const double den = b - a * cpm1;
+    cpm1 = c / den;
+    dpm1 = (r - a * dpm1) / den;
+    w[4 * k + 0] = cpm1;
+    w[4 * k + 1] = dpm1;
+    dxm1 = dxk;
+    slm1 = slk;
+  }
+  // last row (not-a-knot): (x[-1]-x[-3]) s[-2] + dx[-2] s[-1] = b[-1]
+  double s_next;
+  {
+    const double dx2 = X(N - 2) - X(N - 3), sl2 = (Yk(N - 2) - Yk(N - 3)) / dx2;  // dx[-2], slope[-2]
+    const double d = X(N - 1) - X(N - 3);
+    const double r = ((dxm1 * dxm1) * sl2 + (2.0 * d + dxm1) * dx2 * slm1) / d;
+    s_next = (r - d * dpm1) / (dx2 - d * cpm1);
+  }
+  // back substitution, forming the PPoly coefficients of interval k on the way
+  const double y_last = w[kOdeWS - 1];
+  for (int k = N - 2; k >= 0; --k) {
+    const double sk = w[4 * k + 1] - w[4 * k + 0] * s_next;
+    const double dxk = X(k + 1) - X(k);
+    const double yk = w[4 * k + 3], yk1 = (k + 1 < N - 1) ? w[4 * (k + 1) + 3] : y_last;
+    const double slk = (yk1 - yk) / dxk;
+    const double t = (sk + s_next - 2.0 * slk) / dxk;
+    w[4 * k + 0] = t / dxk;
+    w[4 * k + 1] = (slk - sk) / dxk - t;
+    w[4 * k + 2] = sk;
+    s_next = sk;
+  }
+  if (status) status[i] = LZQ_ODE_OK;
+}
+
+// fpy:385-417 on the ODE path, one lane per point.
+__global__ __launch_bounds__(kOdeBlock) void ode_integrate_kernel(const lzq_point* __restrict__ pts,
+                                                                  const lzq_ode_params* __restrict__ ode, int64_t n,
+                                                                  const double* __restrict__ ws, int64_t max_steps,
+                                                                  lzq_yield* __restrict__ out,
+                                                                  int32_t* __restrict__ status) {
+  const int64_t i = (int64_t)blockIdx.x * kOdeBlock + threadIdx.x;
+  if (i >= n) return;
+  const lzq_point pt = pts[i];
+  const OdePoint o = ode_point(pt, ode[i]);
+  const double* w = ws + i * (int64_t)kOdeWS;
+  const double nan = __builtin_nan("");
+  lzq_yield r = {nan, nan, nan, nan, nan, pt.P_chi_to_B};
+  int st = ode_grid_ok(o.T_lo, o.T_hi, o.stepT) ? LZQ_ODE_OK : LZQ_ODE_BAD_GRID;
+  const double m = o.m, T_p = o.Tp;
+  const double x0 = m / o.T_hi, x1 = m / pymax(o.T_lo, 1e-30);  // fpy:387-388
+  double Ychi;                                                   // fpy:389-399
+  if (pt.regime == LZQ_NONTHERMAL) {
+    if (pt.has_Y_chi_init) Ychi = pt.Y_chi_init;
+    else if (pt.has_n_chi_at_Tp) Ychi = pt.n_chi_at_Tp_GeV3 / pymax(s_entropy(T_p, pt.g_star_s), 1e-300);
+    else Ychi = 1.0e-12;
+  } else {  // thermal, and the fallback branch fpy:398-399 (no UnboundLocalError on this path)
+    Ychi = n_chi_eq(o.T_hi, m, pt.g_chi, pt.stats) / s_entropy(o.T_hi, pt.g_star_s);
+  }
+  double YB = 0.0;
+  const double x_p = m / pymax(T_p, 1e-30);
+  const double max_step = pymin(pymin(fabs(x1 - x0) / 20000.0, x_p / 1000.0), 5e-4);  // fpy:403-404
+  double steps = 0.0;
+  if (st == LZQ_ODE_OK) {
+    if (!(max_step > 0.0)) st = LZQ_ODE_BAD_STEP;
+    else {
+      steps = ceil(fabs(x1 - x0) / max_step);
+      if (!(steps <= (double)max_steps)) st = LZQ_ODE_TOO_MANY_STEPS;
+    }
+  }
+  if (st == LZQ_ODE_OK) {
+    const int64_t N = (int64_t)steps;
+    const double h = (x1 - x0) / (double)N;
+    const Radau R = radau_tableau();
+    for (int64_t k = 0; k < N; ++k) {
+      const double xk = x0 + (double)k * h;
+      OdeStage sg[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) sg[j] = ode_stage(o, w, xk + R.c[j] * h);
+      if (!radau_step(R, sg, h, Ychi, YB)) {
+        st = LZQ_ODE_NEWTON;
+        break;
+      }
+    }
+  }
+  if (st == LZQ_ODE_OK) {  // fpy:412-417
+    const double nB0 = YB * kS0M3, nDM0 = Ychi * kS0M3;
+    r.Y_B = YB;
+    r.Y_chi = Ychi;
+    r.rho_B_kg_m3 = nB0 * kMProtonKg;
+    r.rho_DM_kg_m3 = nDM0 * (m * kGeVToKg);
+    r.DM_over_B = r.rho_DM_kg_m3 / pymax(r.rho_B_kg_m3, 1e-300);
+  }
+  out[i] = r;
+  if (status) status[i] = st;
+}
+
+// BoltzmannSystem.A_over_V_T / .rhs of one point at n arguments (lane per argument).
+__global__ __launch_bounds__(kOdeBlock) void ode_eval_kernel(lzq_point pt, lzq_ode_params od, double T_lo,
+                                                             double T_hi, const double* __restrict__ w,
+                                                             const double* __restrict__ T, const double* __restrict__ x,
+                                                             const double* __restrict__ Y, int64_t n,
+                                                             double* __restrict__ out_Av, double* __restrict__ out_dY) {
+  const int64_t i = (int64_t)blockIdx.x * kOdeBlock + threadIdx.x;
+  if (i >= n) return;
+  OdePoint o = ode_point(pt, od);
+  o.T_lo = T_lo;
+  o.T_hi = T_hi;
+  o.stepT = (T_hi - T_lo) / (double)(kOdeNT - 1);
+  if (out_Av) out_Av[i] = spline_eval(o, w, T[i]);
+  if (out_dY) {
+    const OdeStage s = ode_stage(o, w, x[i]);
+    const double yc = Y[2 * i], yb = Y[2 * i + 1];
+    out_dY[2 * i] = -s.lam * (yc * yc - s.E2) - s.S;
+    out_dY[2 * i + 1] = s.alpha - s.beta * yb;
+  }
+}
+
+}  // namespace lzq
+
+// =========================================================================================
+// C ABI
+// =========================================================================================
+namespace {
+
+int64_t ode_blocks(int64_t n) { return (n + lzq::kOdeBlock - 1) / lzq::kOdeBlock; }
+
+int hip_check(hipError_t e, const char* what) {
+  if (e == hipSuccess) return LZQ_OK;
+  char buf[256];
+  snprintf(buf, sizeof(buf), "%s: %s", what, hipGetErrorString(e));
+  return lzq_set_error(LZQ_EHIP, buf);
+}
+
+int check_ws(int64_t n, const double* d_work, int64_t work_doubles, const char* fn) {
+  char buf[160];
+  if (n < 0 || (n > 0 && !d_work)) {
+    snprintf(buf, sizeof(buf), "%s: bad arguments", fn);
+    return lzq_set_error(LZQ_EINVAL, buf);
+  }
+  if (n > 0 && (work_doubles / LZQ_ODE_WS_PER_POINT) < n) {
+    snprintf(buf, sizeof(buf), "%s: workspace of %lld doubles < n * %d", fn, (long long)work_doubles,
+             LZQ_ODE_WS_PER_POINT);
+    return lzq_set_error(LZQ_EINVAL, buf);
+  }
+  if (ode_blocks(n) > 2147483647LL) {
+    snprintf(buf, sizeof(buf), "%s: n too large", fn);
+    return lzq_set_error(LZQ_EINVAL, buf);
+  }
+  return LZQ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lzq_ode_tables(const lzq_point* d_points, int64_t n, const double* d_T_lo, const double* d_T_hi, double* d_work,
+                   int64_t work_doubles, int32_t* d_status, void* stream) {
+  int rc = check_ws(n, d_work, work_doubles, "lzq_ode_tables");
+  if (rc) return rc;
+  if (n > 0 && !d_points) return lzq_set_error(LZQ_EINVAL, "lzq_ode_tables: bad arguments");
+  if ((d_T_lo == nullptr) != (d_T_hi == nullptr))
+    return lzq_set_error(LZQ_EINVAL, "lzq_ode_tables: T_lo and T_hi must both be given or both be NULL");
+  if (n == 0) return LZQ_OK;
+  hipStream_t s = (hipStream_t)stream;
+  rc = lzq::launch_ode_aov_tables(d_points, n, d_T_lo, d_T_hi, d_work, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(lzq::ode_spline_kernel, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, s, d_points, n,
+                     d_T_lo, d_T_hi, d_work, d_status);
+  return hip_check(hipGetLastError(), "lzq_ode_tables");
+}
+
+int lzq_ode_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, const double* d_work,
+                      int64_t work_doubles, int64_t max_steps, lzq_yield* d_out, int32_t* d_status, void* stream) {
+  int rc = check_ws(n, d_work, work_doubles, "lzq_ode_integrate");
+  if (rc) return rc;
+  if (n > 0 && (!d_points || !d_ode || !d_out)) return lzq_set_error(LZQ_EINVAL, "lzq_ode_integrate: bad arguments");
+  if (max_steps < 0) return lzq_set_error(LZQ_EINVAL, "lzq_ode_integrate: max_steps < 0");
+  if (n == 0) return LZQ_OK;
+  hipLaunchKernelGGL(lzq::ode_integrate_kernel, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0,
+                     (hipStream_t)stream, d_points, d_ode, n, d_work, max_steps, d_out, d_status);
+  return hip_check(hipGetLastError(), "lzq_ode_integrate");
+}
+
+int lzq_ode_batch(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, double* d_work,
+                  int64_t work_doubles, int64_t max_steps, lzq_yield* d_out, int32_t* d_status, void* stream) {
+  int rc = lzq_ode_tables(d_points, n, nullptr, nullptr, d_work, work_doubles, d_status, stream);
+  if (rc) return rc;
+  return lzq_ode_integrate(d_points, d_ode, n, d_work, work_doubles, max_steps, d_out, d_status, stream);
+}
+
+int lzq_ode_aov_T(const lzq_point* pt, double T_lo, double T_hi, const double* d_work_point, const double* d_T,
+                  int64_t n, double* d_out_Av, void* stream) {
+  if (!pt || n < 0 || (n > 0 && (!d_work_point || !d_T || !d_out_Av)))
+    return lzq_set_error(LZQ_EINVAL, "lzq_ode_aov_T: bad arguments");
+  if (n == 0) return LZQ_OK;
+  if (ode_blocks(n) > 2147483647LL) return lzq_set_error(LZQ_EINVAL, "lzq_ode_aov_T: n too large");
+  lzq_ode_params od = {0.0, 0.0, 0, 0};
+  hipLaunchKernelGGL(lzq::ode_eval_kernel, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, (hipStream_t)stream,
+                     *pt, od, T_lo, T_hi, d_work_point, d_T, nullptr, nullptr, n, d_out_Av, nullptr);
+  return hip_check(hipGetLastError(), "lzq_ode_aov_T");
+}
+
+int lzq_ode_rhs(const lzq_point* pt, const lzq_ode_params* ode, double T_lo, double T_hi, const double* d_work_point,
+                const double* d_x, const double* d_Y, int64_t n, double* d_out_dY, void* stream) {
+  if (!pt || !ode || n < 0 || (n > 0 && (!d_work_point || !d_x || !d_Y || !d_out_dY)))
+    return lzq_set_error(LZQ_EINVAL, "lzq_ode_rhs: bad arguments");
+  if (n == 0) return LZQ_OK;
+  if (ode_blocks(n) > 2147483647LL) return lzq_set_error(LZQ_EINVAL, "lzq_ode_rhs: n too large");
+  hipLaunchKernelGGL(lzq::ode_eval_kernel, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, (hipStream_t)stream,
+                     *pt, *ode, T_lo, T_hi, d_work_point, nullptr, d_x, d_Y, n, nullptr, d_out_dY);
+  return hip_check(hipGetLastError(), "lzq_ode_rhs");
+}
+
+}  // extern "C"

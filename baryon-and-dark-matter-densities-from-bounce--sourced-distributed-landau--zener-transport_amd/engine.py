@@ -12,7 +12,7 @@ import numpy as np
 import torch
 
 from . import _native
-from .config import to_ctypes_point, to_point
+from .config import to_ctypes_ode, to_ctypes_point, to_point
 
 YIELD_FIELDS = _native.YIELD_FIELDS
 
@@ -126,6 +126,71 @@ class Engine:
             self._check(self.lib.lzq_sweep_grid(ctypes.byref(base), arr, len(axes), int(start), int(count),
                                                   int(n_y), _vp(Pp), _vp(out), self._stream()))
         self._keepalive = dev_vals  # axis buffers must outlive the async launch
+        return out
+
+    # -- ODE fallback (fpy:200-219, 270-286, 385-417) ---------------------------------------
+    def ode_workspace(self, n: int) -> torch.Tensor:
+        return torch.empty(n * _native.ODE_WS_PER_POINT, dtype=torch.float64, device=self.device)
+
+    def ode_tables(self, points, T_lo=None, T_hi=None, work: Optional[torch.Tensor] = None) -> tuple:
+        """BoltzmannSystem.build_tables for each point (window T_lo/T_hi per point, or main()'s
+        window): returns the (n * LZQ_ODE_WS_PER_POINT) spline workspace and the int32 status."""
+        d_pts = points if isinstance(points, torch.Tensor) else self.points_to_device(points)
+        n = d_pts.numel() // _native.POINT_DTYPE.itemsize
+        work = self.ode_workspace(n) if work is None else work
+        tl = None if T_lo is None else self._f64(T_lo).reshape(-1)
+        th = None if T_hi is None else self._f64(T_hi).reshape(-1)
+        status = torch.zeros(n, dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            self._check(self.lib.lzq_ode_tables(_vp(d_pts), n, _vp(tl), _vp(th), _vp(work), work.numel(), _vp(status),
+                                                self._stream()))
+        return work, status
+
+    def ode(self, points, ode_params, max_steps: int = 1 << 26, chunk: int = 1 << 15) -> tuple:
+        """fpy:385-417 for n points (POINT_DTYPE records + ODE_DTYPE records): (n, 6) yields
+        table and (n,) int32 status (enum lzq_ode_status), both on the device.  Points are
+        processed in chunks so that the spline workspace stays <= chunk * 25.6 KB."""
+        pts = np.ascontiguousarray(points, dtype=_native.POINT_DTYPE).reshape(-1)
+        ods = np.ascontiguousarray(ode_params, dtype=_native.ODE_DTYPE).reshape(-1)
+        if pts.size != ods.size:
+            raise ValueError("points and ode_params must have the same length")
+        n = pts.size
+        out = torch.empty((n, 6), dtype=torch.float64, device=self.device)
+        status = torch.zeros(n, dtype=torch.int32, device=self.device)
+        work = self.ode_workspace(min(n, chunk)) if n else None
+        for c0 in range(0, n, chunk):
+            c1 = min(n, c0 + chunk)
+            d_pts = self.points_to_device(pts[c0:c1])
+            d_ode = torch.from_numpy(ods[c0:c1].view(np.uint8).copy()).to(self.device)
+            with torch.cuda.device(self.device):
+                self._check(self.lib.lzq_ode_batch(_vp(d_pts), _vp(d_ode), c1 - c0, _vp(work), work.numel(),
+                                                   int(max_steps), _vp(out[c0:c1]), _vp(status[c0:c1]),
+                                                   self._stream()))
+            self._keepalive = (d_pts, d_ode)
+        return out, status
+
+    def ode_aov_T(self, point, T_lo: float, T_hi: float, work_point: torch.Tensor, Ts) -> torch.Tensor:
+        """BoltzmannSystem.A_over_V_T (fpy:214-218) of one point at several T."""
+        T = self._f64(Ts).reshape(-1)
+        out = torch.empty_like(T)
+        p = to_ctypes_point(np.asarray(point, dtype=_native.POINT_DTYPE).reshape(1))
+        with torch.cuda.device(self.device):
+            self._check(self.lib.lzq_ode_aov_T(ctypes.byref(p), float(T_lo), float(T_hi), _vp(work_point), _vp(T),
+                                               T.numel(), _vp(out), self._stream()))
+        return out
+
+    def ode_rhs(self, point, ode_params, T_lo: float, T_hi: float, work_point: torch.Tensor, xs, Ys) -> torch.Tensor:
+        """BoltzmannSystem.rhs (fpy:270-286) of one point: (n, 2) dY/dx at (x[i], Y[i])."""
+        x = self._f64(xs).reshape(-1)
+        Y = self._f64(Ys).reshape(-1, 2).contiguous()
+        if Y.shape[0] != x.numel():
+            raise ValueError("need one (Y_chi, Y_B) pair per x")
+        out = torch.empty_like(Y)
+        p = to_ctypes_point(np.asarray(point, dtype=_native.POINT_DTYPE).reshape(1))
+        o = to_ctypes_ode(np.asarray(ode_params, dtype=_native.ODE_DTYPE).reshape(1))
+        with torch.cuda.device(self.device):
+            self._check(self.lib.lzq_ode_rhs(ctypes.byref(p), ctypes.byref(o), float(T_lo), float(T_hi),
+                                             _vp(work_point), _vp(x), _vp(Y), x.numel(), _vp(out), self._stream()))
         return out
 
     # -- fpy:183-184 -----------------------------------------------------------------------

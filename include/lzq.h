@@ -152,6 +152,59 @@ int lzq_sweep_grid(const lzq_point* base, const lzq_axis* axes, int32_t n_axes,
 /* fpy:183-184: P[i] = clamp(1 - exp(-2 pi max(lambda[i], 0)), 0, 1) (naive 1-exp kept). */
 int lzq_p_closed_form(const double* d_lambda, int64_t n, double* d_P, void* stream);
 
+/* ---- ODE fallback (fpy:200-219, 270-286, 385-417) -------------------------------------- */
+/* Configurations with sigma_v != 0, Gamma_wash != 0 or depletion leave the fast path
+ * (fpy:372) for the reference's Boltzmann ODE.  These three Config fields ride next to the
+ * lzq_point of each point. */
+typedef struct lzq_ode_params {
+  double sigma_v_chi_GeV_m2;       /* fpy:279 (max(., 0) applied) */
+  double Gamma_wash_over_H;        /* fpy:284 (max(., 0) applied) */
+  int32_t deplete_DM_from_source;  /* fpy:282 */
+  int32_t reserved;                /* 0 */
+} lzq_ode_params;                  /* 24 bytes */
+
+#define LZQ_ODE_NT 800             /* fpy:207 build_tables(n=800) */
+#define LZQ_ODE_WS_PER_POINT 3200  /* workspace doubles per point (spline coefficients) */
+enum lzq_ode_status {
+  LZQ_ODE_OK = 0,
+  LZQ_ODE_BAD_GRID = 1,       /* T grid not strictly increasing: CubicSpline raises ValueError */
+  LZQ_ODE_BAD_STEP = 2,       /* max_step <= 0 (zero-width x range): solve_ivp raises ValueError */
+  LZQ_ODE_TOO_MANY_STEPS = 3, /* more than max_steps integration steps: not attempted */
+  LZQ_ODE_NEWTON = 4          /* a Radau stage system did not converge */
+};
+
+/* BoltzmannSystem.build_tables(T_lo, T_hi, n=800) (fpy:207-212) for n points, at per-point
+ * windows d_T_lo/d_T_hi ([n] each) or, both NULL, main()'s window T_lo = T_min_over_Tp T_p,
+ * T_hi = T_max_over_Tp T_p (fpy:368-369, what lzq_ode_integrate needs): A/V at linspace(T_lo, T_hi, 800)
+ * (the quadrature kernels' z-sum) and its not-a-knot cubic spline (scipy CubicSpline), into
+ * d_work[i * LZQ_ODE_WS_PER_POINT ...] (work_doubles >= n * LZQ_ODE_WS_PER_POINT).
+ * d_status (optional, [n] int32): LZQ_ODE_BAD_GRID for a window CubicSpline rejects. */
+int lzq_ode_tables(const lzq_point* d_points, int64_t n, const double* d_T_lo, const double* d_T_hi,
+                   double* d_work, int64_t work_doubles, int32_t* d_status, void* stream);
+
+/* fpy:385-417 on built tables: Y_chi(x1), Y_B(x1) of rhs (fpy:270-286) from x0 = m/T_hi to
+ * x1 = m/max(T_lo, 1e-30), Y(x0) = (Y_chi0 of fpy:389-399, 0), by the reference's method
+ * (3-stage Radau IIA) on uniform steps h = (x1 - x0)/ceil(|x1 - x0|/max_step) <= max_step of
+ * fpy:404, one point per lane; then the densities epilogue.  Points needing more than
+ * max_steps steps are not integrated (status LZQ_ODE_TOO_MANY_STEPS, NaN yields); so are
+ * points whose T grid CubicSpline would reject (LZQ_ODE_BAD_GRID).  d_status: optional [n]
+ * int32 output (enum lzq_ode_status). */
+int lzq_ode_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, const double* d_work,
+                      int64_t work_doubles, int64_t max_steps, lzq_yield* d_out, int32_t* d_status,
+                      void* stream);
+
+/* lzq_ode_tables + lzq_ode_integrate (d_status may be NULL). */
+int lzq_ode_batch(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, double* d_work,
+                  int64_t work_doubles, int64_t max_steps, lzq_yield* d_out, int32_t* d_status, void* stream);
+
+/* BoltzmannSystem.A_over_V_T (fpy:214-218) and .rhs (fpy:270-286) of ONE point (host structs)
+ * whose tables for the window (T_lo, T_hi) are at d_work_point: out_Av[i] = A_over_V_T(T[i]);
+ * out_dY[2i..2i+1] = rhs(x[i], (Y[2i], Y[2i+1])). */
+int lzq_ode_aov_T(const lzq_point* pt, double T_lo, double T_hi, const double* d_work_point, const double* d_T,
+                  int64_t n, double* d_out_Av, void* stream);
+int lzq_ode_rhs(const lzq_point* pt, const lzq_ode_params* ode, double T_lo, double T_hi, const double* d_work_point,
+                const double* d_x, const double* d_Y, int64_t n, double* d_out_dY, void* stream);
+
 /* ---- Landau-Zener propagator (north_star (1); no reference counterpart) --------------- */
 /* Coherent two-level propagation through n_cross sequential linear avoided crossings per
  * point: i dpsi/dt = H(t) psi, H = [[D(xi), m_c],[m_c, -D(xi)]], xi = v_w t, D piecewise linear

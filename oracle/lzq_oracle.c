@@ -264,3 +264,287 @@ double oracle_p_closed_form(double lam) {
 double oracle_j_chi(const oracle_point* p, double T) {
   return p->incident_flux_scale * (0.25 * n_chi_eq(T, p->m_chi_GeV, p->g_chi, p->stats) * vbar_chi(T, p->m_chi_GeV));
 }
+
+/* =======================================================================================
+ * ODE fallback (fpy:200-219 build_tables / A_over_V_T, fpy:270-286 rhs, fpy:385-410 main).
+ * The reference integrates with scipy's adaptive Radau (rtol 1e-8, atol 1e-12, max_step of
+ * fpy:404).  Restated here as the same Radau IIA (3 stages, order 5) on uniform steps of
+ * h = (x1 - x0)/ceil(|x1 - x0|/max_step) <= max_step, each stage system solved by Newton with
+ * the rhs' analytic (diagonal) Jacobian to full precision.  tests/golden/golden_ode.json
+ * shows the reference's shipped solution within ~1e-14 of its own converged one, so the
+ * restatement is pinned against the shipped outputs at that level.
+ * ======================================================================================= */
+#define ODE_NT 800
+
+/* scipy.interpolate.CubicSpline(x, y, bc_type='not-a-knot') for n = ODE_NT points
+ * (scipy/interpolate/_cubic.py: banded system for the knot slopes s, then the PPoly
+ * coefficients of CubicHermiteSpline).  The tridiagonal solve is Thomas elimination
+ * (scipy: LAPACK gbsv with partial pivoting; the two agree to rounding).  coef[4k+0..3] =
+ * c[0..3][k], the PPoly coefficients of interval k (value c0 s^3 + c1 s^2 + c2 s + c3). */
+static void spline_notaknot(const double* x, const double* y, double* coef) {
+  const int n = ODE_NT;
+  double dx[ODE_NT], slope[ODE_NT], cp[ODE_NT], dp[ODE_NT], s[ODE_NT];
+  for (int k = 0; k + 1 < n; k++) {
+    dx[k] = x[k + 1] - x[k];
+    slope[k] = (y[k + 1] - y[k]) / dx[k];
+  }
+  /* row 0 (not-a-knot): dx1 s0 + (x2 - x0) s1 = ((dx0 + 2d) dx1 slope0 + dx0^2 slope1)/d */
+  {
+    double d = x[2] - x[0];
+    double b = dx[1], c = d;
+    double r = ((dx[0] + 2.0 * d) * dx[1] * slope[0] + (dx[0] * dx[0]) * slope[1]) / d;
+    cp[0] = c / b;
+    dp[0] = r / b;
+  }
+  for (int k = 1; k < n - 1; k++) {
+    double a = dx[k], b = 2.0 * (dx[k - 1] + dx[k]), c = dx[k - 1];
+    double r = 3.0 * (dx[k] * slope[k - 1] + dx[k - 1] * slope[k]);
+    double den = b - a * cp[k - 1];
+    cp[k] = c / den;
+    dp[k] = (r - a * dp[k - 1]) / den;
+  }
+  {
+    double d = x[n - 1] - x[n - 3];
+    double a = d, b = dx[n - 3];
+    double r = ((dx[n - 2] * dx[n - 2]) * slope[n - 3] + (2.0 * d + dx[n - 2]) * dx[n - 3] * slope[n - 2]) / d;
+    s[n - 1] = (r - a * dp[n - 2]) / (b - a * cp[n - 2]);
+  }
+  for (int k = n - 2; k >= 0; k--) s[k] = dp[k] - cp[k] * s[k + 1];
+  for (int k = 0; k + 1 < n; k++) {
+    double t = (s[k] + s[k + 1] - 2.0 * slope[k]) / dx[k];
+    coef[4 * k + 0] = t / dx[k];
+    coef[4 * k + 1] = (slope[k] - s[k]) / dx[k] - t;
+    coef[4 * k + 2] = s[k];
+    coef[4 * k + 3] = y[k];
+  }
+}
+
+int oracle_ode_tables(const oracle_point* p, double T_lo, double T_hi, double* coef) {
+  ztab_init();
+  double Ts[ODE_NT], Av[ODE_NT], f[ORACLE_NZ], scratch[ORACLE_NZ];
+  oracle_linspace(T_lo, T_hi, ODE_NT, Ts);
+  for (int k = 0; k + 1 < ODE_NT; k++)
+    if (!(Ts[k + 1] > Ts[k])) return -1; /* CubicSpline: `x` must be strictly increasing */
+  aov_t a = aov_make(p->I_p, p->beta_over_H, p->T_p_GeV, p->v_w, p->g_star);
+  for (int k = 0; k < ODE_NT; k++) {
+    double y = y_of_T(Ts[k], p->T_p_GeV, p->beta_over_H);
+    Av[k] = pymax(aov_eval(&a, y, f, scratch), 0.0); /* np.maximum(Av, 0.0) */
+  }
+  spline_notaknot(Ts, Av, coef);
+  return 0;
+}
+
+/* fpy:214-218 A_over_V_T: clamp T into [T_lo, T_hi], evaluate the PPoly (scipy _ppoly:
+ * interval k with x[k] <= T < x[k+1], T == x[-1] in the last one; value accumulated as
+ * c3 + c2 s + c1 s^2 + c0 s^3, powers by repeated multiplication). */
+double oracle_ode_aov_T(const double* coef, double T_lo, double T_hi, double T) {
+  double Ts[ODE_NT];
+  oracle_linspace(T_lo, T_hi, ODE_NT, Ts);
+  double Tq = pymin(pymax(T, T_lo), T_hi);
+  int lo = 0, hi = ODE_NT - 1; /* largest k <= n-2 with Ts[k] <= Tq */
+  while (hi - lo > 1) {
+    int mid = (lo + hi) / 2;
+    if (Ts[mid] <= Tq) lo = mid;
+    else hi = mid;
+  }
+  const double* c = coef + 4 * lo;
+  double s = Tq - Ts[lo];
+  double z = s, res = c[3];
+  res = res + c[2] * z;
+  z = z * s;
+  res = res + c[1] * z;
+  z = z * s;
+  res = res + c[0] * z;
+  return res;
+}
+
+typedef struct {
+  const oracle_point* p;
+  const oracle_ode* o;
+  const double* coef;
+  double T_lo, T_hi;
+} ode_ctx;
+
+/* fpy:270-286 rhs(x, Y), plus the diagonal of its Jacobian (the two equations decouple). */
+static void ode_rhs(const ode_ctx* c, double x, const double Y[2], double dY[2], double J[2]) {
+  const oracle_point* p = c->p;
+  double m = p->m_chi_GeV;
+  double T = m / pymax(x, 1e-30);
+  double H = pymax(H_std(T, p->g_star), 1e-300);
+  double s = pymax(s_entropy(T, p->g_star_s), 1e-300);
+  double y = y_of_T(T, p->T_p_GeV, p->beta_over_H);
+  double q = y / pymax(p->source_shape_sigma_y, 1e-6);
+  double window = exp(-0.5 * (q * q));
+  double J_chi = p->incident_flux_scale * (0.25 * n_chi_eq(T, m, p->g_chi, p->stats) * vbar_chi(T, m));
+  double SB = p->P_chi_to_B * J_chi * oracle_ode_aov_T(c->coef, c->T_lo, c->T_hi, T) * window;
+  double sigmav = pymax(c->o->sigma_v_chi_GeV_m2, 0.0);
+  double Yeq = n_chi_eq(T, m, p->g_chi, p->stats) / s;
+  double SB_term = c->o->deplete_DM_from_source ? (SB / s) : 0.0;
+  double Hx = H * x;
+  dY[0] = (-sigmav * s * (Y[0] * Y[0] - Yeq * Yeq) - SB_term) / Hx;
+  double gamma_w = pymax(c->o->Gamma_wash_over_H, 0.0);
+  dY[1] = (+SB / s - gamma_w * H * Y[1]) / Hx;
+  J[0] = (-sigmav * s * (2.0 * Y[0])) / Hx;
+  J[1] = (-gamma_w * H) / Hx;
+}
+
+void oracle_ode_rhs(const oracle_point* p, const oracle_ode* o, const double* coef, double T_lo, double T_hi,
+                    double x, const double* Y, double* dY) {
+  ode_ctx c = {p, o, coef, T_lo, T_hi};
+  double J[2];
+  ode_rhs(&c, x, Y, dY, J);
+}
+
+/* 3x3 solve with partial pivoting (M is overwritten). */
+static void solve3(double M[3][3], double b[3]) {
+  for (int c = 0; c < 3; c++) {
+    int piv = c;
+    for (int r = c + 1; r < 3; r++)
+      if (fabs(M[r][c]) > fabs(M[piv][c])) piv = r;
+    if (piv != c) {
+      for (int k = 0; k < 3; k++) {
+        double t = M[c][k];
+        M[c][k] = M[piv][k];
+        M[piv][k] = t;
+      }
+      double t = b[c];
+      b[c] = b[piv];
+      b[piv] = t;
+    }
+    for (int r = c + 1; r < 3; r++) {
+      double f = M[r][c] / M[c][c];
+      for (int k = c; k < 3; k++) M[r][k] -= f * M[c][k];
+      b[r] -= f * b[c];
+    }
+  }
+  for (int c = 2; c >= 0; c--) {
+    double acc = b[c];
+    for (int k = c + 1; k < 3; k++) acc -= M[c][k] * b[k];
+    b[c] = acc / M[c][c];
+  }
+}
+
+/* Radau IIA tableau (scipy/integrate/_ivp/radau.py uses the same method). */
+static void radau_tableau(double C[3], double A[3][3]) {
+  double s6 = sqrt(6.0);
+  C[0] = (4.0 - s6) / 10.0;
+  C[1] = (4.0 + s6) / 10.0;
+  C[2] = 1.0;
+  A[0][0] = (88.0 - 7.0 * s6) / 360.0;
+  A[0][1] = (296.0 - 169.0 * s6) / 1800.0;
+  A[0][2] = (-2.0 + 3.0 * s6) / 225.0;
+  A[1][0] = (296.0 + 169.0 * s6) / 1800.0;
+  A[1][1] = (88.0 + 7.0 * s6) / 360.0;
+  A[1][2] = (-2.0 - 3.0 * s6) / 225.0;
+  A[2][0] = (16.0 - s6) / 36.0;
+  A[2][1] = (16.0 + s6) / 36.0;
+  A[2][2] = 1.0 / 9.0;
+}
+
+/* One Radau IIA step of size h from (x, Y).  Returns 0, or 4 when Newton does not converge. */
+static int radau_step(const ode_ctx* c, const double C[3], const double A[3][3], double x, double h, double Y[2]) {
+  double Z[3][2], F[3][2], J[3][2];
+  for (int i = 0; i < 3; i++) Z[i][0] = Y[0], Z[i][1] = Y[1];
+  for (int it = 0; it < 40; it++) {
+    for (int i = 0; i < 3; i++) ode_rhs(c, x + C[i] * h, Z[i], F[i], J[i]);
+    double dmax = 0.0, zmax = 0.0;
+    for (int comp = 0; comp < 2; comp++) {
+      double M[3][3], g[3];
+      for (int i = 0; i < 3; i++) {
+        double acc = Z[i][comp] - Y[comp];
+        for (int j = 0; j < 3; j++) {
+          acc -= h * A[i][j] * F[j][comp];
+          M[i][j] = (i == j ? 1.0 : 0.0) - h * A[i][j] * J[j][comp];
+        }
+        g[i] = -acc;
+      }
+      solve3(M, g);
+      for (int i = 0; i < 3; i++) {
+        Z[i][comp] += g[i];
+        dmax = pymax(dmax, fabs(g[i]));
+        zmax = pymax(zmax, fabs(Z[i][comp]));
+      }
+    }
+    if (!(dmax > 1e-15 * zmax)) {
+      Y[0] = Z[2][0];
+      Y[1] = Z[2][1];
+      return 0;
+    }
+  }
+  return 4;
+}
+
+/* fpy:361-417 for a point on the ODE path; status 0 ok, 1 bad T grid (CubicSpline raises),
+ * 2 max_step <= 0 (solve_ivp raises), 3 more than max_steps steps, 4 Newton failure. */
+int oracle_ode_point(const oracle_point* p, const oracle_ode* o, int64_t max_steps, oracle_yield* out,
+                     int64_t* n_steps) {
+  double T_p = p->T_p_GeV, m = p->m_chi_GeV;
+  double T_hi = p->T_max_over_Tp * T_p, T_lo = p->T_min_over_Tp * T_p;
+  double* coef = (double*)malloc(sizeof(double) * 4 * ODE_NT);
+  int st = 0;
+  *n_steps = 0;
+  memset(out, 0xff, sizeof(*out)); /* NaN unless filled */
+  if (oracle_ode_tables(p, T_lo, T_hi, coef) != 0) {
+    free(coef);
+    return 1;
+  }
+  double x0 = m / T_hi, x1 = m / pymax(T_lo, 1e-30);
+  double Ychi0;
+  if (p->regime == 1) {
+    if (p->has_Y_chi_init) Ychi0 = p->Y_chi_init;
+    else if (p->has_n_chi_at_Tp) Ychi0 = p->n_chi_at_Tp_GeV3 / pymax(s_entropy(T_p, p->g_star_s), 1e-300);
+    else Ychi0 = 1.0e-12;
+  } else { /* thermal, and the else-branch of fpy:398-399 */
+    Ychi0 = n_chi_eq(T_hi, m, p->g_chi, p->stats) / s_entropy(T_hi, p->g_star_s);
+  }
+  double x_p = m / pymax(T_p, 1e-30);
+  double max_step = pymin(pymin(fabs(x1 - x0) / 20000.0, x_p / 1000.0), 5e-4);
+  if (!(max_step > 0.0)) {
+    free(coef);
+    return 2;
+  }
+  double steps = ceil(fabs(x1 - x0) / max_step);
+  if (!(steps <= (double)max_steps)) {
+    free(coef);
+    return 3;
+  }
+  int64_t N = (int64_t)steps;
+  double h = (x1 - x0) / (double)N;
+  double C[3], A[3][3];
+  radau_tableau(C, A);
+  ode_ctx c = {p, o, coef, T_lo, T_hi};
+  double Y[2] = {Ychi0, 0.0};
+  for (int64_t k = 0; k < N && st == 0; k++) st = radau_step(&c, C, A, x0 + (double)k * h, h, Y);
+  free(coef);
+  *n_steps = N;
+  if (st) return st;
+  double YB = Y[1], Ychi = Y[0];
+  double rhoB = YB * S0_M3 * M_PROTON_KG;
+  double rhoDM = Ychi * S0_M3 * (m * GEV_TO_KG);
+  out->Y_B = YB;
+  out->Y_chi = Ychi;
+  out->rho_B_kg_m3 = rhoB;
+  out->rho_DM_kg_m3 = rhoDM;
+  out->DM_over_B = rhoDM / pymax(rhoB, 1e-300);
+  out->P_used = p->P_chi_to_B;
+  return 0;
+}
+
+int64_t oracle_ode_batch(const oracle_point* p, const oracle_ode* o, int64_t n, int64_t max_steps, oracle_yield* out,
+                         int32_t* status, int32_t nthreads) {
+  ztab_init();
+  int64_t bad = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#else
+  (void)nthreads;
+#endif
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : bad)
+  for (int64_t i = 0; i < n; i++) {
+    int64_t ns;
+    int st = oracle_ode_point(&p[i], &o[i], max_steps, &out[i], &ns);
+    if (status) status[i] = st;
+    bad += st != 0;
+  }
+  return bad;
+}

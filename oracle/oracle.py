@@ -127,3 +127,100 @@ def linspace(start, stop, num) -> np.ndarray:
     out = np.empty(num, dtype=np.float64)
     lib().oracle_linspace(start, stop, num, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
     return out
+
+
+# ---- ODE fallback (fpy:200-219, 270-286, 385-417) -------------------------------------
+class OracleOde(ctypes.Structure):
+    _fields_ = [("sigma_v_chi_GeV_m2", ctypes.c_double), ("Gamma_wash_over_H", ctypes.c_double),
+                ("deplete_DM_from_source", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+ODE_NT = 800
+ODE_STATUS = {0: "ok", 1: "T grid not strictly increasing", 2: "max_step <= 0", 3: "too many steps",
+              4: "Newton failure"}
+
+
+def _ode_lib():
+    L = lib()
+    if not hasattr(L, "_ode_ready"):
+        d, i32, i64, P = ctypes.c_double, ctypes.c_int32, ctypes.c_int64, ctypes.POINTER
+        L.oracle_ode_tables.restype = ctypes.c_int
+        L.oracle_ode_tables.argtypes = [P(OraclePoint), d, d, P(d)]
+        L.oracle_ode_aov_T.restype = d
+        L.oracle_ode_aov_T.argtypes = [P(d), d, d, d]
+        L.oracle_ode_rhs.restype = None
+        L.oracle_ode_rhs.argtypes = [P(OraclePoint), P(OracleOde), P(d), d, d, d, P(d), P(d)]
+        L.oracle_ode_point.restype = ctypes.c_int
+        L.oracle_ode_point.argtypes = [P(OraclePoint), P(OracleOde), i64, P(OracleYield), P(i64)]
+        L.oracle_ode_batch.restype = i64
+        L.oracle_ode_batch.argtypes = [P(OraclePoint), P(OracleOde), i64, i64, P(OracleYield), P(i32), i32]
+        L._ode_ready = True
+    return L
+
+
+def ode_from_config(cfg: dict) -> OracleOde:
+    o = OracleOde()
+    o.sigma_v_chi_GeV_m2 = float(cfg["sigma_v_chi_GeV_m2"])
+    o.Gamma_wash_over_H = float(cfg["Gamma_wash_over_H"])
+    o.deplete_DM_from_source = int(bool(cfg["deplete_DM_from_source"]))
+    return o
+
+
+def _window(cfg):
+    T_p = float(cfg["T_p_GeV"])
+    return float(cfg["T_min_over_Tp"]) * T_p, float(cfg["T_max_over_Tp"]) * T_p
+
+
+def ode_tables(cfg: dict) -> np.ndarray:
+    """build_tables -> (799, 4) PPoly coefficients (rows = intervals, cols = c0..c3)."""
+    p = point_from_config(cfg)
+    T_lo, T_hi = _window(cfg)
+    coef = np.zeros(4 * ODE_NT)
+    rc = _ode_lib().oracle_ode_tables(ctypes.byref(p), T_lo, T_hi, coef.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    if rc != 0:
+        raise ValueError("`x` must be strictly increasing sequence.")
+    return coef[:4 * (ODE_NT - 1)].reshape(ODE_NT - 1, 4).copy()
+
+
+def ode_rhs(cfg: dict, x: float, Y) -> tuple:
+    p, o = point_from_config(cfg), ode_from_config(cfg)
+    T_lo, T_hi = _window(cfg)
+    coef = np.zeros(4 * ODE_NT)
+    dp = ctypes.POINTER(ctypes.c_double)
+    L = _ode_lib()
+    L.oracle_ode_tables(ctypes.byref(p), T_lo, T_hi, coef.ctypes.data_as(dp))
+    Yv = np.asarray(Y, dtype=np.float64)
+    dY = np.zeros(2)
+    L.oracle_ode_rhs(ctypes.byref(p), ctypes.byref(o), coef.ctypes.data_as(dp), T_lo, T_hi, float(x),
+                     Yv.ctypes.data_as(dp), dY.ctypes.data_as(dp))
+    return float(dY[0]), float(dY[1])
+
+
+def ode_aov_T(cfg: dict, T: float) -> float:
+    p = point_from_config(cfg)
+    T_lo, T_hi = _window(cfg)
+    coef = np.zeros(4 * ODE_NT)
+    dp = ctypes.POINTER(ctypes.c_double)
+    L = _ode_lib()
+    L.oracle_ode_tables(ctypes.byref(p), T_lo, T_hi, coef.ctypes.data_as(dp))
+    return L.oracle_ode_aov_T(coef.ctypes.data_as(dp), T_lo, T_hi, float(T))
+
+
+def ode_point(cfg: dict, max_steps: int = 1 << 26) -> dict:
+    p, o, out, ns = point_from_config(cfg), ode_from_config(cfg), OracleYield(), ctypes.c_int64()
+    st = _ode_lib().oracle_ode_point(ctypes.byref(p), ctypes.byref(o), int(max_steps), ctypes.byref(out),
+                                     ctypes.byref(ns))
+    r = {n: getattr(out, n) for n in YIELD_FIELDS}
+    r["status"], r["n_steps"] = st, ns.value
+    return r
+
+
+def ode_batch(cfgs: list[dict], max_steps: int = 1 << 26, nthreads: int = 0):
+    n = len(cfgs)
+    pts = (OraclePoint * n)(*[point_from_config(c) for c in cfgs])
+    ods = (OracleOde * n)(*[ode_from_config(c) for c in cfgs])
+    out = (OracleYield * n)()
+    st = np.zeros(n, dtype=np.int32)
+    _ode_lib().oracle_ode_batch(pts, ods, n, int(max_steps), out, st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                int(nthreads))
+    return np.frombuffer(out, dtype=np.float64).reshape(n, 6).copy(), st

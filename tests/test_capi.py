@@ -13,7 +13,7 @@ def header_symbols():
     with open(os.path.join(ROOT, "include", "lzq.h")) as f:
         src = f.read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(lzq_[a-z0-9_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(lzq_[A-Za-z0-9_]+)\s*\(", src)))
 
 
 def test_library_builds_and_exports_header_symbols():

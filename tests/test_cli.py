@@ -54,9 +54,13 @@ def test_unknown_key_typeerror(tmp_path):
         pkg("config").load_config(str(tmp_path / "bad.json"))
 
 
-def test_ode_fallback_configs_refused(tmp_path):
+def test_ode_fallback_configs_need_the_gpu(tmp_path):
+    """ODE configs (fpy:385-410) go to the GPU like the fast path: no CPU fallback."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present (covered by tests/test_gpu_cli.py)")
     (tmp_path / "ode.json").write_text(json.dumps({"P_chi_to_B": 0.1, "Gamma_wash_over_H": 1e-3}))
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
         run_cli(["--config", "ode.json"], tmp_path)
 
 

@@ -1,0 +1,126 @@
+"""ODE fallback on the GPU (lzq_ode_*): against the reference's own outputs
+(tests/golden/golden_ode.json) and against the CPU restatement (oracle), plus its operator API
+(build_tables / A_over_V_T / rhs) and error behaviour.  Needs an MI355X."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import BASE_CFG, GOLDEN, full_cfg, golden, pkg, rel_err
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+GOLDEN_ODE = os.path.join(GOLDEN, "golden_ode.json")
+needs_golden = pytest.mark.skipif(not os.path.exists(GOLDEN_ODE), reason="golden_ode.json not generated")
+NARROW = {"T_max_over_Tp": 1.6, "T_min_over_Tp": 0.6}
+
+
+def recs(cfgs):
+    cfgm = pkg("config")
+    return (np.concatenate([cfgm.to_point(c) for c in cfgs]), np.concatenate([cfgm.to_ode_params(c) for c in cfgs]))
+
+
+def seeded_cfgs(n, seed=11):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        c = full_cfg(BASE_CFG)
+        c.update(m_chi_GeV=float(10 ** rng.uniform(-1, 2.7)), I_p=float(rng.uniform(0.05, 1.0)),
+                 beta_over_H=float(10 ** rng.uniform(1.3, 2.5)), v_w=float(rng.uniform(0.1, 0.9)),
+                 source_shape_sigma_y=float(rng.uniform(3, 20)), P_chi_to_B=float(rng.uniform(0, 1)),
+                 chi_stats=str(rng.choice(["fermion", "boson"])), regime=str(rng.choice(["thermal", "nonthermal"])),
+                 T_max_over_Tp=float(rng.uniform(1.1, 2.5)), T_min_over_Tp=float(rng.uniform(0.3, 0.9)),
+                 Gamma_wash_over_H=float(rng.choice([0.0, 10 ** rng.uniform(-1, 1.5)])),
+                 sigma_v_chi_GeV_m2=float(rng.choice([0.0, 10 ** rng.uniform(-20, -10)])),
+                 deplete_DM_from_source=bool(rng.uniform() < 0.3))
+        if c["Gamma_wash_over_H"] == 0.0 and c["sigma_v_chi_GeV_m2"] == 0.0:
+            c["deplete_DM_from_source"] = True
+        out.append(c)
+    return out
+
+
+@needs_golden
+def test_ode_vs_reference_outputs(gpu_engine):
+    pts = golden("golden_ode.json")["points"]
+    cfgs = [full_cfg(r["config"]) for r in pts]
+    t, st = gpu_engine.ode(*recs(cfgs))
+    t, st = t.cpu().numpy(), st.cpu().numpy()
+    names = pkg("_native").YIELD_FIELDS
+    worst = 0.0
+    for row, s, r in zip(t, st, pts):
+        if "error" in r:
+            assert s == 1 and r["error"]["type"] == "ValueError" and np.isnan(row[0]), (r["error"], s)
+            continue
+        assert s == 0, (s, r["config"])
+        ref_acc = max(rel_err(r["final"]["Y_B"], r["tight"]["Y_B"]), rel_err(r["final"]["Y_chi"], r["tight"]["Y_chi"]))
+        for k, v in zip(names, row):
+            if k in r["final"]:
+                e = rel_err(v, r["final"][k])
+                assert e < 1e-8 + 10 * ref_acc, (k, v, r["final"][k], r["config"])
+                worst = max(worst, e)
+        assert row[5] == r["P_used"]
+    print(f"ODE GPU vs reference: worst rel err {worst:.3e}")
+
+
+def test_ode_vs_oracle_seeded(gpu_engine):
+    cfgs = seeded_cfgs(24)
+    t, st = gpu_engine.ode(*recs(cfgs))
+    t, st = t.cpu().numpy(), st.cpu().numpy()
+    ref, rst = O.ode_batch(cfgs, nthreads=16)
+    assert np.array_equal(st, rst)
+    for a, b in zip(t.ravel(), ref.ravel()):
+        assert rel_err(a, b) < 1e-11, (a, b)
+
+
+@needs_golden
+def test_ode_operator_api_vs_reference(gpu_engine):
+    """build_tables / A_over_V_T / rhs of BoltzmannSystem (fpy:207-218, 270-286)."""
+    B = pkg("boltzmann")
+    cfgm = pkg("config")
+    for r in golden("golden_ode.json")["points"][:8]:
+        if "error" in r:
+            continue
+        cfg = cfgm.Config(**full_cfg(r["config"]))
+        bs = B.BoltzmannSystem(cfg, r["P_used"])
+        T_p = cfg.T_p_GeV
+        bs.build_tables(cfg.T_min_over_Tp * T_p, cfg.T_max_over_Tp * T_p, n=800)
+        got = bs.A_over_V_Ts(r["A_over_V_T"]["T"])
+        amax = max(r["A_over_V_T"]["Av"])
+        for g, e in zip(got, r["A_over_V_T"]["Av"]):
+            assert abs(g - e) <= 1e-11 * abs(e) + 1e-14 * amax
+        xs = [s["x"] for s in r["rhs"]]
+        Ys = [s["Y"] for s in r["rhs"]]
+        dY = bs.rhs_batch(xs, Ys)
+        for g, s in zip(dY, r["rhs"]):
+            for a, e in zip(g, s["dY"]):
+                assert abs(a - e) <= 1e-11 * abs(e) + 1e-300, (s, g)
+        assert bs.rhs(xs[3], np.array(Ys[3])).tolist() == list(dY[3])
+
+
+def test_ode_status_and_step_cap(gpu_engine):
+    cfgs = [full_cfg({**BASE_CFG, "Gamma_wash_over_H": 1.0, **NARROW}),
+            full_cfg({**BASE_CFG, "Gamma_wash_over_H": 1.0, "T_max_over_Tp": 1.0, "T_min_over_Tp": 1.0}),
+            full_cfg({**BASE_CFG, "Gamma_wash_over_H": 1.0, "T_max_over_Tp": 0.5, "T_min_over_Tp": 0.9}),
+            full_cfg({**BASE_CFG, "Gamma_wash_over_H": 1.0})]                  # ~1e6 steps
+    t, st = gpu_engine.ode(*recs(cfgs), max_steps=100_000)
+    assert st.cpu().numpy().tolist() == [0, 1, 1, 3]
+    t = t.cpu().numpy()
+    assert np.isfinite(t[0]).all() and np.isnan(t[1:, :5]).all()
+
+
+def test_ode_deterministic_and_batch_independent(gpu_engine):
+    cfgs = seeded_cfgs(20, seed=3)
+    p, o = recs(cfgs)
+    a = gpu_engine.ode(p, o)[0].cpu().numpy()
+    b = gpu_engine.ode(p[::-1], o[::-1])[0].cpu().numpy()[::-1]
+    c = np.concatenate([gpu_engine.ode(p[i:i + 7], o[i:i + 7], chunk=3)[0].cpu().numpy() for i in range(0, 20, 7)])
+    assert np.array_equal(a, b) and np.array_equal(a, c)
+
+
+def test_ode_reduces_to_quadrature_without_sinks(gpu_engine):
+    """Depletion alone leaves dY_B/dx = S_B/(s H x): Y_B(ODE) equals the fast path's
+    quadrature of the same integrand up to the spline's interpolation of A/V."""
+    cfg = full_cfg({**BASE_CFG, "deplete_DM_from_source": True, "T_max_over_Tp": 1.3, "T_min_over_Tp": 0.7})
+    t, st = gpu_engine.ode(*recs([cfg]))
+    q = gpu_engine.yields(pkg("config").to_point(cfg)).cpu().numpy()[0, 0]
+    assert st.item() == 0 and rel_err(t.cpu().numpy()[0, 0], q) < 1e-2

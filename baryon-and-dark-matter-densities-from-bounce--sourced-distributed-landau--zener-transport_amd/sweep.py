@@ -29,6 +29,7 @@ from typing import Callable, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _native
+from .config import to_ode_params, to_point
 
 YIELD_FIELDS = _native.YIELD_FIELDS
 
@@ -118,6 +119,51 @@ class SweepSpec:
         return m.contiguous(), dp.contiguous(), xi.contiguous(), v_w
 
 
+ODE_FIELDS = ("sigma_v_chi_GeV_m2", "Gamma_wash_over_H", "deplete_DM_from_source")  # fpy:372 gate
+
+
+def is_ode_spec(spec: "SweepSpec") -> bool:
+    """Does any point of the sweep leave the fast path (fpy:372) for the ODE fallback?"""
+    b = spec.base
+    base_ode = bool(b.get("deplete_DM_from_source")) or float(b.get("sigma_v_chi_GeV_m2", 0.0)) != 0.0 or \
+        float(b.get("Gamma_wash_over_H", 0.0)) != 0.0
+    return base_ode or any(name in ODE_FIELDS and np.any(np.asarray(v) != 0) for name, v in spec.axes)
+
+
+def grid_records(spec: "SweepSpec", start: int, count: int, engine=None):
+    """Explicit point records of grid indices [start, start+count): (POINT_DTYPE, ODE_DTYPE)
+    numpy arrays, decoded in C order like lzq_sweep_grid.  The LZ axes set P through the
+    closed form evaluated on the GPU (lzq_p_closed_form, fpy:183-184)."""
+    pts = np.repeat(to_point(spec.base), count)
+    ods = np.repeat(to_ode_params(spec.base), count)
+    idx = np.arange(start, start + count, dtype=np.int64)
+    stride = 1
+    lz = {}
+    for name, vals in reversed(spec.axes):
+        v = np.asarray(vals, dtype=np.float64)[(idx // stride) % len(vals)]
+        stride *= len(vals)
+        if name in ("delta_LZ", "m_mix", "dprime"):
+            lz[name] = v
+        elif name in ODE_FIELDS:
+            ods[name] = v if name != "deplete_DM_from_source" else (v != 0).astype(np.int32)
+        elif name == "Y_chi_init":
+            pts["Y_chi_init"], pts["has_Y_chi_init"] = v, 1
+        elif name == "n_chi_at_Tp_GeV3":
+            pts["n_chi_at_Tp_GeV3"], pts["has_n_chi_at_Tp"] = v, 1
+        else:
+            pts[name] = v
+    if lz:
+        if "m_mix" in lz:  # PAPER eq.(8), F = 1
+            delta = lz["m_mix"] * lz["m_mix"] / (2.0 * np.maximum(pts["v_w"], 1e-12) * np.abs(lz["dprime"]))
+        else:
+            delta = lz["delta_LZ"]
+        if engine is None:
+            from .engine import default_engine
+            engine = default_engine()
+        pts["P_chi_to_B"] = engine.p_closed_form(delta).cpu().numpy()
+    return pts, ods
+
+
 def _axis_from_json(a: dict) -> Tuple[str, np.ndarray]:
     if "values" in a:
         v = np.asarray(a["values"], dtype=np.float64)
@@ -127,7 +173,7 @@ def _axis_from_json(a: dict) -> Tuple[str, np.ndarray]:
         v = np.linspace(*a["linspace"][:2], int(a["linspace"][2]))
     else:
         raise ValueError(f"axis {a!r} needs values / linspace / logspace")
-    if a["field"] not in _native.FIELD:
+    if a["field"] not in _native.FIELD and a["field"] not in ODE_FIELDS:
         raise ValueError(f"unknown sweep field {a['field']!r}")
     return a["field"], v
 
@@ -263,7 +309,27 @@ def run_sweep(spec: SweepSpec, engine=None, rank: int = 0, world: int = 1, chunk
 
 
 def make_compute(spec: SweepSpec, engine) -> ComputeFn:
-    """(start, count, out) -> None on the GPU: [coherent multi-crossing P ->] quadrature."""
+    """(start, count, out) -> None on the GPU: [coherent multi-crossing P ->] quadrature, or
+    the ODE fallback (lzq_ode_batch) for sweeps over sigma_v / Gamma_wash / depletion."""
+    if is_ode_spec(spec):
+        if spec.crossings is not None:
+            raise NotImplementedError("multi-crossing profiles with the ODE fallback")
+
+        def compute_ode(s, n, out):
+            import torch
+            pts, ods = grid_records(spec, s, n, engine)
+            # fpy:372 per point: points with no sink/depletion take the quadrature, the rest the ODE
+            ode = (ods["sigma_v_chi_GeV_m2"] != 0.0) | (ods["Gamma_wash_over_H"] != 0.0) | \
+                  (ods["deplete_DM_from_source"] != 0)
+            sel = np.nonzero(ode)[0]
+            if sel.size:
+                tab, _status = engine.ode(pts[sel], ods[sel])  # failed points: NaN rows (lzq_ode_status)
+                out[torch.as_tensor(sel, device=out.device)] = tab
+            sel = np.nonzero(~ode)[0]
+            if sel.size:
+                out[torch.as_tensor(sel, device=out.device)] = engine.yields(pts[sel], n_y=spec.n_y)
+        return compute_ode
+
     def compute(s, n, out):
         P_points = None
         if spec.crossings is not None:

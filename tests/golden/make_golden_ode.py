@@ -17,7 +17,8 @@ The fallback takes >= 20000 Radau steps per point (max_step <= |x1-x0|/20000, fp
 most cases use narrow integration windows; one case keeps the shipped window (~1e6 steps,
 several minutes).
 
-    python tests/golden/make_golden_ode.py       # ~10 min on 8 cores
+    python tests/golden/make_golden_ode.py             # ~25 min on 8 cores (one shipped-window case)
+    python tests/golden/make_golden_ode.py --cli-only  # golden_cli_ode.json, ~20 s
 """
 from __future__ import annotations
 
@@ -142,7 +143,33 @@ def _worker(cfg: dict) -> dict:
     return row
 
 
+def cli_ode_cases() -> list[dict]:
+    """Byte-exact stdout + yields_out.json of the reference CLI on ODE-path configs."""
+    import subprocess
+    out = []
+    for name, over in (("ode_wash", {"Gamma_wash_over_H": 0.5, "T_max_over_Tp": 1.6, "T_min_over_Tp": 0.6}),
+                       ("ode_deplete_annihilate", {"deplete_DM_from_source": True, "sigma_v_chi_GeV_m2": 1e-16,
+                                                   "T_max_over_Tp": 1.6, "T_min_over_Tp": 0.6})):
+        with tempfile.TemporaryDirectory() as d:
+            c = MG._base_cfg()
+            c.update(over)
+            cfg_text = json.dumps(c, indent=2)
+            with open(os.path.join(d, "cfg.json"), "w") as f:
+                f.write(cfg_text)
+            r = subprocess.run([sys.executable, "-B", os.path.join(MG.REF_DIR, "first_principles_yields.py"),
+                                "--config", "cfg.json"], cwd=d, capture_output=True, text=True)
+            with open(os.path.join(d, "yields_out.json")) as f:
+                yo = f.read()
+            out.append({"name": name, "flags": [], "config_text": cfg_text, "returncode": r.returncode,
+                        "stdout": r.stdout, "yields_out_json": yo})
+    return out
+
+
 def main():
+    if "--cli-only" in sys.argv:
+        with open(os.path.join(HERE, "golden_cli_ode.json"), "w") as f:
+            json.dump(cli_ode_cases(), f, indent=1)
+        return
     cases = ode_cases()
     order = sorted(range(len(cases)), key=lambda i: -("T_max_over_Tp" not in cases[i] or cases[i]["T_max_over_Tp"] == 5.0))
     with mp.get_context("fork").Pool(min(8, os.cpu_count() or 1)) as pool:

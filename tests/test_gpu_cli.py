@@ -30,3 +30,16 @@ def test_cli_matches_reference(case, tmp_path, gpu_engine):
     assert list(ours["final"]) == list(ref["final"])
     for k, v in ref["final"].items():
         assert rel_err(ours["final"][k], v) < 1e-11, (k, ours["final"][k], v)
+
+
+@pytest.mark.parametrize("case", golden("golden_cli_ode.json"), ids=lambda c: c["name"])
+def test_cli_ode_path_matches_reference(case, tmp_path, gpu_engine):
+    """sigma_v / Gamma_wash / depletion configs: the CLI takes the GPU ODE fallback (fpy:385-410);
+    stdout byte-identical, finals within 1e-10 of the reference's Radau."""
+    (tmp_path / "cfg.json").write_text(case["config_text"])
+    assert run_cli(["--config", "cfg.json"], tmp_path) == case["stdout"]
+    ref = json.loads(case["yields_out_json"])
+    ours = json.loads((tmp_path / "yields_out.json").read_text())
+    assert ours["inputs"] == ref["inputs"]
+    for k, v in ref["final"].items():
+        assert rel_err(ours["final"][k], v) < 1e-10, (k, ours["final"][k], v)

@@ -52,6 +52,9 @@ def test_ode_vs_reference_outputs(gpu_engine):
             assert s == 1 and r["error"]["type"] == "ValueError" and np.isnan(row[0]), (r["error"], s)
             continue
         assert s == 0, (s, r["config"])
+        if not r["tight"]["success"]:  # the reference's Radau gives up here (see test_ode_oracle.py)
+            assert np.isfinite(row).all()
+            continue
         ref_acc = max(rel_err(r["final"]["Y_B"], r["tight"]["Y_B"]), rel_err(r["final"]["Y_chi"], r["tight"]["Y_chi"]))
         for k, v in zip(names, row):
             if k in r["final"]:
@@ -91,9 +94,12 @@ def test_ode_operator_api_vs_reference(gpu_engine):
         xs = [s["x"] for s in r["rhs"]]
         Ys = [s["Y"] for s in r["rhs"]]
         dY = bs.rhs_batch(xs, Ys)
+        # per component: relative 1e-10, plus 1e-12 of the component's largest magnitude (the
+        # spline's absolute accuracy is relative to max A/V, not to a value deep in its tail)
+        scale = np.max(np.abs([s["dY"] for s in r["rhs"]]), axis=0)
         for g, s in zip(dY, r["rhs"]):
-            for a, e in zip(g, s["dY"]):
-                assert abs(a - e) <= 1e-11 * abs(e) + 1e-300, (s, g)
+            for a, e, sc in zip(g, s["dY"], scale):
+                assert abs(a - e) <= 1e-10 * abs(e) + 1e-12 * sc, (s, g)
         assert bs.rhs(xs[3], np.array(Ys[3])).tolist() == list(dY[3])
 
 
@@ -124,3 +130,24 @@ def test_ode_reduces_to_quadrature_without_sinks(gpu_engine):
     t, st = gpu_engine.ode(*recs([cfg]))
     q = gpu_engine.yields(pkg("config").to_point(cfg)).cpu().numpy()[0, 0]
     assert st.item() == 0 and rel_err(t.cpu().numpy()[0, 0], q) < 1e-2
+
+
+def test_ode_sweep_routes_per_point(gpu_engine, tmp_path):
+    """A sweep over Gamma_wash (0 -> fast path, > 0 -> ODE fallback, fpy:372) through the sweep
+    driver matches the oracle point by point."""
+    sw = pkg("sweep")
+    spec = sw.spec_from_json({"name": "ode", "base": {**NARROW},
+                              "axes": [{"field": "Gamma_wash_over_H", "values": [0.0, 0.5, 5.0]},
+                                       {"field": "delta_LZ", "values": [1e-3, 0.1]}]})
+    assert sw.is_ode_spec(spec)
+    import torch
+    out = torch.empty((6, 6), dtype=torch.float64, device=gpu_engine.device)
+    sw.make_compute(spec, gpu_engine)(0, 6, out)
+    t = out.cpu().numpy()
+    for i in range(6):
+        prm = spec.point_params(i)
+        cfg = full_cfg({**spec.base, "Gamma_wash_over_H": prm["Gamma_wash_over_H"],
+                        "P_chi_to_B": O.p_closed_form(prm["delta_LZ"])})
+        ref = O.ode_point(cfg) if prm["Gamma_wash_over_H"] else O.point_yields(cfg)
+        for j, k in enumerate(pkg("_native").YIELD_FIELDS):
+            assert rel_err(t[i, j], ref[k]) < 1e-11, (i, k, t[i, j], ref[k])

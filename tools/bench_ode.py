@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Throughput of the ODE fallback (fpy:385-417; lzq_ode_batch) on one GPU next to the C
+restatement on the host cores.  Configs: the equal-mass config with wash-out in a narrow
+window (20000 Radau steps/point), a stiff thermal annihilation case, and the shipped window
+(~1e6 steps/point).  Points differ in P and flux (uniform work).  One JSON line per config.
+
+    python tools/bench_ode.py [n_narrow] [n_full]
+"""
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PKG = "baryon-and-dark-matter-densities-from-bounce--sourced-distributed-landau--zener-transport_amd"
+import bench  # noqa: E402
+
+
+def cfgs_for(over: dict, n: int):
+    rng = np.random.default_rng(7)
+    out = []
+    for _ in range(n):
+        c = dict(bench.BASE)
+        c.update(over)
+        c["P_chi_to_B"] = float(rng.uniform(0.05, 1.0))
+        c["incident_flux_scale"] = float(10 ** rng.uniform(-10, -8))
+        out.append(c)
+    return out
+
+
+def main():
+    n_narrow = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    n_full = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
+    cfgm = importlib.import_module(PKG + ".config")
+    eng = importlib.import_module(PKG + ".engine").Engine(0)
+    from oracle import oracle as O
+    cases = [("narrow_wash", {"Gamma_wash_over_H": 1.0, "T_max_over_Tp": 1.6, "T_min_over_Tp": 0.6}, n_narrow),
+             ("stiff_thermal", {"sigma_v_chi_GeV_m2": 1e-9, "regime": "thermal", "m_chi_GeV": 300.0,
+                                "T_max_over_Tp": 1.3, "T_min_over_Tp": 0.2}, n_narrow),
+             ("full_window_wash", {"Gamma_wash_over_H": 1.0}, n_full)]
+    for name, over, n in cases:
+        cfgs = cfgs_for(over, n)
+        pts = np.concatenate([cfgm.to_point(c) for c in cfgs])
+        ods = np.concatenate([cfgm.to_ode_params(c) for c in cfgs])
+        eng.ode(pts[:64], ods[:64])  # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        tab, st = eng.ode(pts, ods, chunk=1 << 16)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        ok = bool((st == 0).all())
+        k = min(n, 32 if name != "full_window_wash" else 16)
+        t1 = time.perf_counter()
+        ref, rst = O.ode_batch(cfgs[:k], nthreads=16)
+        dtc = time.perf_counter() - t1
+        t = tab[:k].cpu().numpy()
+        err = float(np.max(np.abs(t - ref) / np.maximum(np.abs(ref), 1e-300)))
+        steps = O.ode_point(cfgs[0])["n_steps"]
+        print(json.dumps({"config": name, "points": n, "steps_per_point": steps, "gpu_points_per_s": n / dt,
+                          "gpu_seconds": dt, "all_ok": ok, "cpu_oracle_points_per_s": k / dtc, "cpu_threads": 16,
+                          "cpu_sample": k, "max_rel_diff_gpu_vs_oracle": err}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -5,13 +5,15 @@
 //   A/V(y) = pref(y) * trapz_z[ z^2 e^-z exp(c(y) g4(z)) ]          fpy:158-165
 // with 8000 y-nodes x 1200 z-nodes per parameter point.
 //
-// Mapping (DESIGN.md "Kernels"):
+// Mapping:
 //   * one 64-lane wavefront owns one parameter point; lane l takes y-nodes l, l+64, ...;
-//     no LDS, no barriers, no atomics; 4 independent wavefronts per 256-thread block;
-//   * the point-invariant z tables {g4_k, omega_k} (omega = z^2 e^-z x trapezoid weight)
-//     are read with wave-uniform addresses -> scalar loads into SGPRs, so every FP64 VALU
-//     op of the inner loop takes its table operand from an SGPR;
-//   * the inner exp is lzq::exp2_nonpos (17 VALU slots per node, see lzq_exp2.h);
+//     no barriers (besides staging the exp table) and no atomics; 8 independent wavefronts
+//     per 512-thread block, two blocks per CU;
+//   * the point-invariant z tables {g4_k, omega'_k} (omega = z^2 e^-z x trapezoid weight,
+//     scaled by 2^-512) are read with wave-uniform addresses -> scalar loads into SGPRs, so
+//     every FP64 VALU op of the inner loop takes its table operand from an SGPR;
+//   * the inner exp is the pre-biased 8192-entry LDS table of lzq_exp2.h: 9-10 VALU per
+//     (y, z) node including the accumulate (zsum below);
 //   * per-lane partial sums over its y-nodes are combined by a fixed xor-butterfly, so the
 //     result is a pure function of the point: independent of launch geometry, batch
 //     composition and GPU count (SURVEY §8e bit-identity across W = 1,2,4,8).

@@ -9,6 +9,8 @@
  *   fpy:170-187  LZ plug-in closed form (fpy:183-184)  -> lzq_p_closed_form
  *   fpy:222-223 + fpy:122-123  J_chi (diagnostics)     -> lzq_jchi_batch
  *   (no reference counterpart; north_star (1))        -> lzq_lz_propagate
+ *   fpy:200-219, 270-286, 385-417  ODE fallback        -> lzq_ode_tables / _integrate / _batch,
+ *                                                         lzq_ode_aov_T, lzq_ode_rhs
  *
  * Conventions (all entry points):
  *   - plain C types only; device buffers are raw device pointers, `stream` is a hipStream_t
@@ -113,7 +115,7 @@ int lzq_ztables(double* z, double* gamma4, double* omega);
 
 /* Tuning knobs for ablations (process-wide, not thread-safe against concurrent launches).
  * LZQ_TUNE_EXP selects the inner-loop exponential: LZQ_EXP_TABLE (default; 2^(j/N) LDS table,
- * N = 2^LZQ_TABBITS = 4096, + degree-2 minimax polynomial, <= 2.6e-14 relative) or
+ * N = 2^LZQ_TABBITS = 8192, + degree-2 minimax polynomial, <= 3.2e-15 relative) or
  * LZQ_EXP_POLY11 (degree-11 minimax polynomial, 0.6 ulp).  Results agree to ~1e-14 relative.
  * Returns the previous value. */
 /* LZQ_TUNE_TRUNCATE (0 = dense, the default; 1 = on): stop each wave's z-sum at the first

@@ -7,8 +7,8 @@
 //
 // Mapping:
 //   * one 64-lane wavefront owns one parameter point; lane l takes y-nodes l, l+64, ...;
-//     no barriers (besides staging the exp table) and no atomics; 8 independent wavefronts
-//     per 512-thread block, two blocks per CU;
+//     no barriers (besides staging the exp table) and no atomics; 16 independent wavefronts
+//     per 1024-thread block, two blocks per CU (8 waves per SIMD);
 //   * the point-invariant z tables {g4_k, omega'_k} (omega = z^2 e^-z x trapezoid weight,
 //     scaled by 2^-512) are read with wave-uniform addresses -> scalar loads into SGPRs, so
 //     every FP64 VALU op of the inner loop takes its table operand from an SGPR;
@@ -37,9 +37,11 @@ namespace lzq {
 constexpr int kNZ = LZQ_NZ;
 constexpr int kWaveSize = 64;
 // The block is sized so that the LDS copies of the exp table that fit in a CU's 160 KB carry
-// 16 waves (4 per SIMD): 64-KB table (default) -> two 512-thread blocks per CU.
+// the waves: 64-KB table (default) -> two 1024-thread blocks per CU = 8 waves per SIMD, with
+// LZQ_MIN_WAVES = 8 capping the kernel at 64 VGPRs (its few spills sit outside the z-loop;
+// +2.2% over 4 waves/SIMD, tools/ablate_builds.py).
 #ifndef LZQ_BLOCK
-#define LZQ_BLOCK ((8 << LZQ_TABBITS) > 81920 ? 1024 : (8 << LZQ_TABBITS) > 40960 ? 512 : 256)
+#define LZQ_BLOCK ((8 << LZQ_TABBITS) > 81920 ? 1024 : (8 << LZQ_TABBITS) > 40960 ? 1024 : 256)
 #endif
 constexpr int kBlock = LZQ_BLOCK;
 constexpr int kWavesPerBlock = kBlock / kWaveSize;
@@ -49,10 +51,9 @@ constexpr int kWavesPerBlock = kBlock / kWaveSize;
 #ifndef LZQ_YB
 #define LZQ_YB 1
 #endif
-// __launch_bounds__ second argument = minimum waves per SIMD (4: <= 128 VGPRs; +6.5% measured
-// over the compiler's own choice of 3 waves, tools/ablate_builds.py)
+// __launch_bounds__ second argument = minimum waves per SIMD (8: <= 64 VGPRs; see LZQ_BLOCK)
 #ifndef LZQ_MIN_WAVES
-#define LZQ_MIN_WAVES 4
+#define LZQ_MIN_WAVES 8
 #endif
 // z-table source: 0 = wave-uniform scalar loads (SGPR operands), 1 = staged in LDS and read
 // with broadcast ds_read_b128 (keeps every LGKM operation of the loop in order, so the

@@ -121,6 +121,12 @@ def test_ode_deterministic_and_batch_independent(gpu_engine):
     b = gpu_engine.ode(p[::-1], o[::-1])[0].cpu().numpy()[::-1]
     c = np.concatenate([gpu_engine.ode(p[i:i + 7], o[i:i + 7], chunk=3)[0].cpu().numpy() for i in range(0, 20, 7)])
     assert np.array_equal(a, b) and np.array_equal(a, c)
+    try:  # the A/V tables' z-sums under exact-underflow truncation: bit-identical
+        gpu_engine.tune_truncate(True)
+        d = gpu_engine.ode(p, o)[0].cpu().numpy()
+    finally:
+        gpu_engine.tune_truncate(False)
+    assert np.array_equal(a, d)
 
 
 def test_ode_reduces_to_quadrature_without_sinks(gpu_engine):

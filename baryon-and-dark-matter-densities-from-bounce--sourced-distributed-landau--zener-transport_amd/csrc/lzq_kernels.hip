@@ -64,6 +64,14 @@ constexpr int kWavesPerBlock = kBlock / kWaveSize;
 #ifndef LZQ_YFACT_EARLY
 #define LZQ_YFACT_EARLY 0
 #endif
+// re-form y / e^y / weight after the z-loop instead of keeping them live across it
+#ifndef LZQ_Y_RECOMPUTE
+#define LZQ_Y_RECOMPUTE 1
+#endif
+// keep yb_wave's per-lane running sum in the wave's LDS slot instead of a VGPR pair
+#ifndef LZQ_ACC_LDS
+#define LZQ_ACC_LDS 1
+#endif
 constexpr int kKUnroll = LZQ_KUNROLL;  // z-nodes per scalar-load batch (must divide 1200)
 constexpr int kYB = LZQ_YB;            // y-nodes per lane per pass (independent chains)
 static_assert(kNZ % kKUnroll == 0, "z unroll must divide nz");
@@ -99,6 +107,9 @@ __device__ __forceinline__ double uniform(double x) {
   return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
+// x**1.5 as x*sqrt(x) (<= 2 ulp from pow; the device pow is ~100 VALU and ~40 VGPRs)
+__device__ __forceinline__ double pow15(double x) { return x * sqrt(x); }
+
 __device__ __forceinline__ QuadSetup quad_setup(const lzq_point& pt, double P, double T_lo, double T_hi,
                                                 int32_t n_y) {
   QuadSetup s;
@@ -132,7 +143,7 @@ __device__ __forceinline__ QuadSetup quad_setup(const lzq_point& pt, double P, d
   s.H0 = 1.66 * sqrt(pt.g_star);
   s.s0 = (2.0 * (kPi * kPi) / 45.0) * pt.g_star_s;
   s.c_rel = (pt.stats == 0) ? pt.g_chi * (3.0 * kZeta3 / (4.0 * (kPi * kPi))) : pt.g_chi * (kZeta3 / (kPi * kPi));
-  s.c_nr = pt.g_chi * pow(pt.m_chi_GeV / (2.0 * kPi), 1.5);
+  s.c_nr = pt.g_chi * pow15(pt.m_chi_GeV / (2.0 * kPi));
   s.v0 = kPi * pymax(pt.m_chi_GeV, 1e-20);
   double* f[] = {&s.y_lo, &s.y_hi, &s.step, &s.delta, &s.pref0, &s.cneg, &s.Bc, &s.Tp, &s.dT0, &s.sig, &s.m,
                  &s.m3, &s.flux, &s.P, &s.g_star, &s.g_star_s, &s.H0, &s.s0, &s.c_rel, &s.c_nr, &s.v0};
@@ -146,6 +157,34 @@ __device__ __forceinline__ double vgpr_const(double x) {
   double v;
   asm volatile("v_mov_b64 %0, %1" : "=v"(v) : "s"(x));
   return v;
+}
+
+// e^x for the per-y factors (<= 1 ulp, like the device libm exp).  Cody-Waite reduction
+// x = k ln2 + r, |r| <= ln2/2, Taylor series to r^13 (truncation < 5e-18), ldexp.  The 15
+// constants are read from constant memory through an offset made opaque per call, so they
+// come in by scalar loads where needed: the libm exp's coefficients were hoisted out of the
+// y-loop into VGPRs and spilled to scratch across the z-loop (which needs ~60 of 64 VGPRs).
+__constant__ double kExpC[15] = {
+    0x1.6124613a86d09p-33, 0x1.1eed8eff8d898p-29, 0x1.ae64567f544e4p-26, 0x1.27e4fb7789f5cp-22,
+    0x1.71de3a556c734p-19, 0x1.a01a01a01a01ap-16, 0x1.a01a01a01a01ap-13, 0x1.6c16c16c16c17p-10,
+    0x1.1111111111111p-7,  0x1.5555555555555p-5,  0x1.5555555555555p-3,  0x1.0p-1,  // 1/13! .. 1/2!
+    0x1.71547652b82fep+0,                                                           // 1/ln2
+    0x1.62e42fefa39efp-1,  0x1.abc9e3b39803fp-56};                                  // ln2 hi, lo
+__device__ __forceinline__ double exp_sc(double x) {
+  int o = 0;
+  asm volatile("" : "+s"(o));
+  const double* c = kExpC + o;
+  x = x < -1100.0 ? -1100.0 : x;  // NaN passes through both
+  x = x > 710.0 ? 710.0 : x;
+  const double k = __builtin_rint(x * c[12]);
+  double r = __builtin_fma(-k, c[13], x);
+  r = __builtin_fma(-k, c[14], r);
+  double p = c[0];
+#pragma unroll
+  for (int i = 1; i < 12; ++i) p = __builtin_fma(p, r, c[i]);
+  p = __builtin_fma(p, r, 1.0);  // (e^r - 1) / r
+  p = __builtin_fma(p, r, 1.0);  // e^r
+  return __builtin_ldexp(p, (int)k);
 }
 
 // numpy.linspace element (handles numpy's step == 0 branch as well)
@@ -187,12 +226,12 @@ __device__ __forceinline__ YFactors y_factors(const QuadSetup& s, double y, doub
     n_eq = s.c_rel * T3;
     vbar = 1.0;
   } else {
-    n_eq = s.c_nr * (T * sqrt(T)) * exp(-s.m / pymax(T, 1e-30));
+    n_eq = s.c_nr * (T * sqrt(T)) * exp_sc(-s.m / pymax(T, 1e-30));
     vbar = sqrt(pymax(8.0 * T / s.v0, 0.0));
   }
   double J = s.flux * 0.25 * n_eq * vbar;                 // fpy:260
   double q = y / s.sig;
-  f.W = exp(-0.5 * (q * q));                              // fpy:262
+  f.W = exp_sc(-0.5 * (q * q));                              // fpy:262
   f.PJ = s.P * J;
   f.sHT = sE * H * T;
   f.adTdy = fabs(dTdy);
@@ -392,15 +431,38 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// Lane index 0..63, re-derived where it is used (v_mbcnt; volatile, so it is not kept live).
+__device__ __forceinline__ int lane_id() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 // Y_B of one point by one wavefront.  fpy:231-267
-template <int YB, int EXPV>
-__device__ double yb_wave(const QuadSetup& s, const ZNode* __restrict__ zt, const double* tab, int lane,
-                          int truncate) {
-  if (s.empty) return 0.0;
-  double acc = 0.0;
-  const int64_t n = s.n;
+//
+// Nothing but the z-loop's own state is held in registers across the z-loop (which needs ~60
+// of the 64 VGPRs at 8 waves/SIMD):
+//   * the point's QuadSetup lives in the wave's LDS slot (~44 SGPRs otherwise); each pass
+//     re-reads the fields it needs with broadcast ds_reads, through a slot index made opaque
+//     per pass so that the reads are not hoisted back out of the y-loop;
+//   * y, e^y and the weight are re-formed after the z-loop (same operations, same bits);
+//   * the lane's running sum over its y-nodes sits in the slot (LZQ_ACC_LDS).
+// Without this the kernel spilled ~200 B/lane to scratch around every z-loop.
+template <int YB, int EXPV, typename Slot>
+__device__ double yb_wave(Slot* slots, int w, const ZNode* __restrict__ zt, const double* tab, int truncate) {
+  if (slots[w].s.empty) return 0.0;
+  const int64_t n = __builtin_bit_cast(int64_t, uniform(__builtin_bit_cast(double, slots[w].s.n)));  // SGPR
   const int64_t per_pass = (int64_t)kWaveSize * YB;
+#if LZQ_ACC_LDS
+  slots[w].acc[lane_id()] = 0.0;
+#else
+  double acc = 0.0;
+#endif
   for (int64_t base = 0; base < n; base += per_pass) {
+    const int lane = lane_id();
+    int wo = w;
+    asm volatile("" : "+s"(wo));
+    const QuadSetup& s = slots[wo].s;
     double c2[YB];
     // only y, e^y and the weight stay live across the z-loop (LZQ_YFACT_EARLY=1: the 7
     // y-factors instead); the y-factors are formed after it
@@ -413,7 +475,7 @@ __device__ double yb_wave(const QuadSetup& s, const ZNode* __restrict__ zt, cons
       const int64_t j = base + (int64_t)b * kWaveSize + lane;
       const int64_t jj = j < n ? j : n - 1;  // tail lanes recompute the last node with weight 0
       yv[b] = y_node(s, jj);
-      ey[b] = exp(pymax(pymin(yv[b], 50.0), -50.0));                          // fpy:161
+      ey[b] = exp_sc(pymax(pymin(yv[b], 50.0), -50.0));                          // fpy:161
       c2[b] = ((s.cneg * ey[b]) * kLog2E) * c2_scale<EXPV>();                 // fpy:163 c, log2 units
       wt[b] = j < n ? y_weight(s, jj, yv[b]) : 0.0;
 #if LZQ_YFACT_EARLY
@@ -422,21 +484,54 @@ __device__ double yb_wave(const QuadSetup& s, const ZNode* __restrict__ zt, cons
     }
     double F[YB];
     zsum_dispatch<YB, EXPV>(zt, tab, c2, F, truncate);
+    int wr = w;
+    asm volatile("" : "+s"(wr));
+    const int lane2 = lane_id();
+#if LZQ_Y_RECOMPUTE && !LZQ_YFACT_EARLY
+    {
+      const QuadSetup& sr = slots[wr].s;
+#pragma unroll
+      for (int b = 0; b < YB; ++b) {
+        const int64_t j = base + (int64_t)b * kWaveSize + lane2;
+        const int64_t jj = j < n ? j : n - 1;
+        yv[b] = y_node(sr, jj);
+        ey[b] = exp_sc(pymax(pymin(yv[b], 50.0), -50.0));
+        wt[b] = j < n ? y_weight(sr, jj, yv[b]) : 0.0;
+      }
+    }
+#endif
+#if LZQ_ACC_LDS
+    double acc = slots[wr].acc[lane2];
+#endif
 #pragma unroll
     for (int b = 0; b < YB; ++b) {
 #if !LZQ_YFACT_EARLY
-      const YFactors f = y_factors(s, yv[b], ey[b], wt[b]);
+      const YFactors f = y_factors(slots[wr].s, yv[b], ey[b], wt[b]);
 #else
       const YFactors& f = fy[b];
 #endif
       acc = __builtin_fma(f.w, integrand_from(f, F[b]), acc);
     }
+#if LZQ_ACC_LDS
+    slots[wr].acc[lane2] = acc;
+#endif
   }
+#if LZQ_ACC_LDS
+  return wave_sum(slots[w].acc[lane_id()]);
+#else
   return wave_sum(acc);
+#endif
 }
 
-// fpy:372-384 (fast path) + fpy:413-417
-__device__ __forceinline__ lzq_yield epilogue(const lzq_point& pt, double YB, double P) {
+// fpy:372-384 (fast path) + fpy:413-417, split around the quadrature: epilogue_pre forms every
+// field that does not depend on Y_B before the z-loops (so the point record need not stay live
+// across them), epilogue_finish adds Y_B with the same operations and rounding order.
+struct EpiPre {
+  lzq_yield o;  // Y_chi, rho_DM_kg_m3, P_used set
+  int valid;    // regime is thermal / nonthermal
+};
+
+__device__ __forceinline__ EpiPre epilogue_pre(const lzq_point& pt, double P) {
   const double T_p = pt.T_p_GeV;
   const double T_hi = pt.T_max_over_Tp * T_p;
   double Ychi;
@@ -449,18 +544,54 @@ __device__ __forceinline__ lzq_yield epilogue(const lzq_point& pt, double YB, do
   } else {
     Ychi = __builtin_nan("");  // reference: UnboundLocalError
   }
-  lzq_yield o;
-  double nB0 = YB * kS0M3, nDM0 = Ychi * kS0M3;
+  EpiPre e;
+  const double nDM0 = Ychi * kS0M3;
+  e.o.Y_B = 0.0;
+  e.o.rho_B_kg_m3 = 0.0;
+  e.o.DM_over_B = 0.0;
+  e.o.Y_chi = Ychi;
+  e.o.rho_DM_kg_m3 = nDM0 * (pt.m_chi_GeV * kGeVToKg);
+  e.o.P_used = P;
+  e.valid = pt.regime == LZQ_THERMAL || pt.regime == LZQ_NONTHERMAL;
+  return e;
+}
+
+__device__ __forceinline__ lzq_yield epilogue_finish(const EpiPre& e, double YB) {
+  lzq_yield o = e.o;
+  const double nB0 = YB * kS0M3;
   o.Y_B = YB;
-  o.Y_chi = Ychi;
   o.rho_B_kg_m3 = nB0 * kMProtonKg;
-  o.rho_DM_kg_m3 = nDM0 * (pt.m_chi_GeV * kGeVToKg);
   o.DM_over_B = o.rho_DM_kg_m3 / pymax(o.rho_B_kg_m3, 1e-300);
-  o.P_used = P;
-  if (pt.regime != LZQ_THERMAL && pt.regime != LZQ_NONTHERMAL) {
-    o.Y_B = o.rho_B_kg_m3 = o.rho_DM_kg_m3 = o.DM_over_B = __builtin_nan("");
-  }
+  if (!e.valid) o.Y_B = o.rho_B_kg_m3 = o.rho_DM_kg_m3 = o.DM_over_B = __builtin_nan("");
   return o;
+}
+
+// Per-wave LDS slot of the quadrature kernels (one point per wavefront).
+struct WaveSlot {
+  QuadSetup s;
+  EpiPre e;
+#if LZQ_ACC_LDS
+  double acc[kWaveSize];  // per-lane running sums of yb_wave
+#endif
+};
+
+// Park the (wave-uniform) setup and epilogue inputs in the wave's slot.  Lane 0 writes; LDS
+// operations of one wavefront complete in order, the fence makes that formal for the compiler.
+__device__ __forceinline__ void park(WaveSlot& slot, const QuadSetup& s, const EpiPre& e, int lane) {
+  if (lane == 0) {
+    slot.s = s;
+    slot.e = e;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Quadrature of the parked point, then lane 0 stores its yields.
+template <int YB, int EXPV>
+__device__ __forceinline__ void point_yields(WaveSlot* slots, int w, const ZNode* __restrict__ zt,
+                                             const double* tab, int lane, int truncate, lzq_yield* out) {
+  const double Y_B = yb_wave<YB, EXPV>(slots, w, zt, tab, truncate);
+  if (lane == 0) *out = epilogue_finish(slots[w].e, Y_B);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -536,16 +667,19 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void yields_points_kernel(co
   __shared__ double lds_tab[kTabN];
   const double* tab = stage_table<EXPV>(gtab, lds_tab);
 #endif
+  __shared__ WaveSlot slots[kWavesPerBlock];
   const int lane = threadIdx.x & (kWaveSize - 1);
   const int64_t idx = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (idx >= n) return;  // wave-uniform
-  const lzq_point pt = pts[idx];
-  const double P = Pov ? Pov[idx] : pt.P_chi_to_B;
-  const double tlo = T_lo ? T_lo[idx] : pt.T_min_over_Tp * pt.T_p_GeV;  // fpy:369
-  const double thi = T_hi ? T_hi[idx] : pt.T_max_over_Tp * pt.T_p_GeV;  // fpy:368
-  QuadSetup s = quad_setup(pt, P, tlo, thi, n_y);
-  const double Y_B = yb_wave<YB, EXPV>(s, zt, tab, lane, truncate);
-  if (lane == 0) out[idx] = epilogue(pt, Y_B, P);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  {
+    const lzq_point pt = pts[idx];
+    const double P = Pov ? Pov[idx] : pt.P_chi_to_B;
+    const double tlo = T_lo ? T_lo[idx] : pt.T_min_over_Tp * pt.T_p_GeV;  // fpy:369
+    const double thi = T_hi ? T_hi[idx] : pt.T_max_over_Tp * pt.T_p_GeV;  // fpy:368
+    park(slots[w], quad_setup(pt, P, tlo, thi, n_y), epilogue_pre(pt, P), lane);
+  }
+  point_yields<YB, EXPV>(slots, w, zt, tab, lane, truncate, out + idx);
 }
 
 template <int YB, int EXPV>
@@ -564,15 +698,19 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void yields_grid_kernel(lzq_
   __shared__ double lds_tab[kTabN];
   const double* tab = stage_table<EXPV>(gtab, lds_tab);
 #endif
+  __shared__ WaveSlot slots[kWavesPerBlock];
   const int lane = threadIdx.x & (kWaveSize - 1);
   const int64_t local = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (local >= count) return;
-  lzq_point pt;
-  const double Pg = grid_point(base, grid, start + local, pt);
-  const double P = Pov ? Pov[local] : Pg;
-  QuadSetup s = quad_setup(pt, P, pt.T_min_over_Tp * pt.T_p_GeV, pt.T_max_over_Tp * pt.T_p_GeV, n_y);
-  const double Y_B = yb_wave<YB, EXPV>(s, zt, tab, lane, truncate);
-  if (lane == 0) out[local] = epilogue(pt, Y_B, P);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  {
+    lzq_point pt;
+    const double Pg = grid_point(base, grid, start + local, pt);
+    const double P = Pov ? Pov[local] : Pg;
+    park(slots[w], quad_setup(pt, P, pt.T_min_over_Tp * pt.T_p_GeV, pt.T_max_over_Tp * pt.T_p_GeV, n_y),
+         epilogue_pre(pt, P), lane);
+  }
+  point_yields<YB, EXPV>(slots, w, zt, tab, lane, truncate, out + local);
 }
 
 // fpy:158-165, one lane per y value
@@ -586,7 +724,7 @@ __global__ __launch_bounds__(kBlock) void aov_kernel(lzq_point pt, const double*
   const bool live = i < n;
   const double y = live ? ys[i] : 0.0;
   QuadSetup s = quad_setup(pt, pt.P_chi_to_B, 1.0, 1.0, LZQ_NY_MIN);
-  double expy = exp(pymax(pymin(y, 50.0), -50.0));
+  double expy = exp_sc(pymax(pymin(y, 50.0), -50.0));
   double c2[1] = {((s.cneg * expy) * kLog2E) * c2_scale<EXPV>()}, F[1];
   zsum_dispatch<1, EXPV>(zt, tab, c2, F);
   if (live) out[i] = (y > 50.0) ? 0.0 : (s.pref0 * expy) * F[0];
@@ -618,7 +756,7 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void ode_aov_table_kernel(co
     const int ii = i < kOdeNT ? i : kOdeNT - 1;
     const double T = linspace_at(T_lo, T_hi, stepT, ii, kOdeNT);
     const double y = y_of_T(T, Tp, B);
-    const double expy = exp(pymax(pymin(y, 50.0), -50.0));  // fpy:161
+    const double expy = exp_sc(pymax(pymin(y, 50.0), -50.0));  // fpy:161
     double c2[1] = {((s.cneg * expy) * kLog2E) * c2_scale<EXPV>()}, F[1];
     zsum_dispatch<1, EXPV>(zt, tab, c2, F, truncate);
     const double Av = (y > 50.0) ? 0.0 : (s.pref0 * expy) * F[0];  // fpy:159-165

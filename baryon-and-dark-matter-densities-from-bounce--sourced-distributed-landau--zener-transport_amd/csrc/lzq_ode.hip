@@ -24,7 +24,12 @@
 
 namespace lzq {
 
+// ode_integrate_kernel: minimum waves per SIMD (its VGPR cap = 512 / this)
+#ifndef LZQ_ODE_MIN_WAVES
+#define LZQ_ODE_MIN_WAVES 2
+#endif
 constexpr int kOdeBlock = 256;
+constexpr double kInvMplGeV = 1.0 / kMplGeV;
 
 // ---------------------------------------------------------------------------------------
 // per-point constants of rhs (one lane per point)
@@ -39,7 +44,15 @@ struct OdePoint {
   double sigmav, gamma_w;
   int deplete;
   double T_lo, T_hi, stepT;
+  double inv_m, inv_sig, inv_v0, inv_stepT;  // reciprocals: ode_stage multiplies instead of dividing
 };
+
+__device__ __forceinline__ void ode_point_recips(OdePoint& o) {
+  o.inv_m = 1.0 / o.m;
+  o.inv_sig = 1.0 / o.sig;
+  o.inv_v0 = 1.0 / o.v0;
+  o.inv_stepT = 1.0 / o.stepT;
+}
 
 __device__ __forceinline__ OdePoint ode_point(const lzq_point& pt, const lzq_ode_params& od) {
   OdePoint o;
@@ -61,6 +74,7 @@ __device__ __forceinline__ OdePoint ode_point(const lzq_point& pt, const lzq_ode
   o.T_lo = pt.T_min_over_Tp * pt.T_p_GeV;         // fpy:369
   o.T_hi = pt.T_max_over_Tp * pt.T_p_GeV;         // fpy:368
   o.stepT = (o.T_hi - o.T_lo) / (double)(kOdeNT - 1);
+  ode_point_recips(o);
   return o;
 }
 
@@ -69,7 +83,7 @@ __device__ __forceinline__ OdePoint ode_point(const lzq_point& pt, const lzq_ode
 // accumulated in that order, powers by repeated multiplication).
 __device__ __forceinline__ double spline_eval(const OdePoint& o, const double* __restrict__ w, double T) {
   const double Tq = pymin(pymax(T, o.T_lo), o.T_hi);
-  int k = (int)((Tq - o.T_lo) / o.stepT);
+  int k = (int)((Tq - o.T_lo) * o.inv_stepT);
   k = k < 0 ? 0 : (k > kOdeNT - 2 ? kOdeNT - 2 : k);
   // the quotient can land one knot off after rounding: settle against the knots themselves
   if (Tq < linspace_at(o.T_lo, o.T_hi, o.stepT, k, kOdeNT) && k > 0) --k;
@@ -96,34 +110,41 @@ struct OdeStage {
 
 __device__ __forceinline__ OdeStage ode_stage(const OdePoint& o, const double* __restrict__ w, double x,
                                               double* Av_out = nullptr) {
-  const double T = o.m / pymax(x, 1e-30);
-  const double H = pymax(o.H0 * T * T / kMplGeV, 1e-300);     // fpy:273 via fpy:85
+  // Three divisions per call (1/x, 1/s, 1/(H x)); every other quotient of fpy:270-286 is a
+  // product with a per-point reciprocal.  Each such product differs from the quotient by at
+  // most 1 ulp, far inside the 1e-11 oracle gate (tests/test_gpu_ode.py).
+  const double xc = pymax(x, 1e-30);
+  const double T = o.m * (1.0 / xc);                          // fpy:272  m / max(x, 1e-30)
+  const double iT = T >= 1e-30 ? xc * o.inv_m : 1e30;         // 1 / max(T, 1e-30)
+  const double H = pymax(o.H0 * T * T * kInvMplGeV, 1e-300);  // fpy:273 via fpy:85
   const double T3 = (T * T) * T;
   const double s = pymax(o.s0 * T3, 1e-300);                  // fpy:274 via fpy:88
-  const double y = y_of_T(T, o.Tp, o.B);                      // fpy:275
-  const double q = y / o.sig;
+  const double qT = o.Tp * iT;                                // fpy:275 y_of_T (fpy:126-128)
+  const double y = 0.5 * o.B * (qT * qT - 1.0);
+  const double q = y * o.inv_sig;
   const double window = exp(-0.5 * (q * q));                  // fpy:276
   double n_eq, vbar;                                          // fpy:90-120
   if (T > o.m3) {
     n_eq = o.c_rel * T3;
     vbar = 1.0;
   } else {
-    n_eq = o.c_nr * (T * sqrt(T)) * exp(-o.m / pymax(T, 1e-30));
-    vbar = sqrt(pymax(8.0 * T / o.v0, 0.0));
+    n_eq = o.c_nr * (T * sqrt(T)) * exp(-o.m * iT);
+    vbar = sqrt(pymax(8.0 * T * o.inv_v0, 0.0));
   }
   const double J = o.flux * (0.25 * n_eq * vbar);             // fpy:222-223
   const double Av = spline_eval(o, w, T);                     // fpy:214-218
   if (Av_out) *Av_out = Av;
   const double SB = o.P * J * Av * window;                    // fpy:277
-  const double E = n_eq / s;                                  // fpy:280
-  const double SBs = SB / s;
-  const double Hx = H * x;
+  const double is = 1.0 / s;
+  const double E = n_eq * is;                                 // fpy:280
+  const double SBs = SB * is;
+  const double iHx = 1.0 / (H * x);
   OdeStage st;
-  st.lam = (o.sigmav * s) / Hx;
+  st.lam = (o.sigmav * s) * iHx;
   st.E2 = E * E;
-  st.S = (o.deplete ? SBs : 0.0) / Hx;                        // fpy:282
-  st.alpha = SBs / Hx;                                        // fpy:285
-  st.beta = (o.gamma_w * H) / Hx;
+  st.S = (o.deplete ? SBs : 0.0) * iHx;                       // fpy:282
+  st.alpha = SBs * iHx;                                       // fpy:285
+  st.beta = (o.gamma_w * H) * iHx;
   return st;
 }
 
@@ -338,7 +359,7 @@ __global__ __launch_bounds__(kOdeBlock) void ode_spline_kernel(const lzq_point* 
 }
 
 // fpy:385-417 on the ODE path, one lane per point.
-__global__ __launch_bounds__(kOdeBlock) void ode_integrate_kernel(const lzq_point* __restrict__ pts,
+__global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_kernel(const lzq_point* __restrict__ pts,
                                                                   const lzq_ode_params* __restrict__ ode, int64_t n,
                                                                   const double* __restrict__ ws, int64_t max_steps,
                                                                   lzq_yield* __restrict__ out,
@@ -411,6 +432,7 @@ __global__ __launch_bounds__(kOdeBlock) void ode_eval_kernel(lzq_point pt, lzq_o
   o.T_lo = T_lo;
   o.T_hi = T_hi;
   o.stepT = (T_hi - T_lo) / (double)(kOdeNT - 1);
+  ode_point_recips(o);
   if (out_Av) out_Av[i] = spline_eval(o, w, T[i]);
   if (out_dY) {
     const OdeStage s = ode_stage(o, w, x[i]);

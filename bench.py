@@ -63,20 +63,26 @@ def pmc_traffic(points_per_launch: int):
 
 
 def valu_issue(points_per_launch: int, kern_ms: float):
-    """Utilisation of the SIMDs' VALU issue slots: the committed PMC pass's VALU instructions
-    per wave-node (each ~4 cycles in this mixed FP64/integer stream, tools/ubench_valu.hip)
-    and clock, over this run's measured kernel time.  1024 SIMDs = 256 CUs x 4."""
+    """Utilisation of the SIMDs' VALU issue slots: the committed PMC passes' VALU instructions
+    per wave-node and clock, over this run's measured kernel time.  Issue cost per wave64
+    instruction: FP64 4 cycles (16 FP64 lanes per SIMD: the 78.6 TFLOP/s peak), other VALU
+    2 cycles.  FP64 = the SQ_INSTS_VALU_{FMA,MUL,ADD}_F64 counters (v_max_f64 is in none of
+    them, so this floor is slightly low).  1024 SIMDs = 256 CUs x 4."""
     try:
         with open(PMC_SUMMARY) as f:
             d = json.load(f)
         ipn, ghz = d["valu_insts_per_wave_node"], d["clock_ghz"]
+        mix = d.get("valu_mix_per_wave_node")
     except (OSError, KeyError, ValueError):
         return None
+    fp64_pn = mix["fma_f64"] + mix["mul_f64"] + mix["add_f64"] if mix else ipn - 2.0  # DESIGN.md §5.1: 2 INT/node
+    cyc_pn = fp64_pn * 4.0 + (ipn - fp64_pn) * 2.0     # issue cycles per wave-node
     wave_nodes = 8000 * 1200 // 64 * points_per_launch
-    need = ipn * 4.0 * wave_nodes                      # SIMD-cycles of VALU issue
-    have = 1024 * ghz * 1e9 * (kern_ms / 1e3)          # SIMD-cycles available
-    return {"insts_per_wave_node": ipn, "cycles_per_inst": 4.0, "clock_ghz": ghz, "frac": need / have,
-            "source": os.path.relpath(PMC_SUMMARY, ROOT)}
+    need = cyc_pn * wave_nodes                         # SIMD-cycles of VALU issue
+    have = 1024 * ghz * 1e9 * (kern_ms / 1e3)          # SIMD-cycles available (PMC run's clock)
+    return {"insts_per_wave_node": ipn, "issue_cycles_per_wave_node": cyc_pn,
+            "model": "FP64 4 cycles, INT32 2 cycles per wave64 instruction", "clock_ghz": ghz,
+            "frac": need / have, "source": os.path.relpath(PMC_SUMMARY, ROOT)}
 
 
 def grid_axes(world: int):

@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Time the ODE fallback (lzq_ode_batch) of every library variant under
+<package>/_build/variants/ in ONE process, interleaved rounds, on tools/bench_ode.py's
+narrow-window and stiff cases.  Variants must agree with the first one to 1e-11.
+
+    python tools/ablate_ode.py [n_points] [rounds]
+"""
+import glob
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import bench  # noqa: E402
+from bench_ode import cfgs_for  # noqa: E402
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    cfgm = importlib.import_module(bench.PKG + ".config")
+    E = importlib.import_module(bench.PKG + ".engine").Engine
+    paths = sorted(glob.glob(os.path.join(ROOT, bench.PKG, "_build", "variants", "*.so")))
+    engs = {os.path.basename(p)[7:-3]: E(0, lib_path=p) for p in paths}
+    cases = {"narrow_wash": {"Gamma_wash_over_H": 1.0, "T_max_over_Tp": 1.6, "T_min_over_Tp": 0.6},
+             "stiff_thermal": {"sigma_v_chi_GeV_m2": 1e-9, "regime": "thermal", "m_chi_GeV": 300.0,
+                               "T_max_over_Tp": 1.3, "T_min_over_Tp": 0.2}}
+    out = {}
+    for cname, over in cases.items():
+        cfgs = cfgs_for(over, n)
+        pts = np.concatenate([cfgm.to_point(c) for c in cfgs])
+        ods = np.concatenate([cfgm.to_ode_params(c) for c in cfgs])
+        ref = None
+        for k, e in engs.items():  # warm-up + agreement
+            t = e.ode(pts[:256], ods[:256])[0].cpu().numpy()
+            if ref is None:
+                ref = t
+            assert np.max(np.abs(t - ref) / np.maximum(np.abs(ref), 1e-300)) < 1e-11, k
+        res = {k: [] for k in engs}
+        for _ in range(rounds):
+            for k, e in engs.items():
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                e.ode(pts, ods, chunk=1 << 16)
+                torch.cuda.synchronize()
+                res[k].append(n / (time.perf_counter() - t0))
+        out[cname] = {k: round(max(v)) for k, v in res.items()}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

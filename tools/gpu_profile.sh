@@ -14,6 +14,7 @@ pmc fetch FETCH_SIZE
 pmc write WRITE_SIZE
 pmc sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT
 pmc inst SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_SALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE GRBM_COUNT
+pmc mix SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_INT32
 timeout -k 10 300 python3 bench.py > $OUT/bench_plain.json 2> $OUT/bench_plain.err || exit 3
 cat $OUT/bench_plain.json
 echo done

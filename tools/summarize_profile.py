@@ -41,7 +41,7 @@ def main():
             shutil.copy(os.path.join(src, f), os.path.join(dst, f))
     points = 200000
     out = {"pmc_points_per_launch": points, "counters": {}}
-    for g in ("fetch", "write", "sq", "inst"):
+    for g in ("fetch", "write", "sq", "inst", "mix"):
         p = os.path.join(src, f"pmc_{g}", "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
@@ -66,6 +66,10 @@ def main():
         out["lds_insts_per_wave_node"] = c["SQ_INSTS_LDS"] / wn
         out["clock_ghz"] = clk / 1e9
         out["cycles_per_wave_node_per_simd"] = 1024 * (ns * 1e-9) * clk / wn
+    if "SQ_INSTS_VALU_FMA_F64" in c:
+        wn = points * WAVE_NODES_PER_POINT
+        out["valu_mix_per_wave_node"] = {k[14:].lower(): c[k] / wn for k in (
+            "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_INT32")}
     if "SQ_WAVE_CYCLES" in c:
         wc = c["SQ_WAVE_CYCLES"]
         out["wave_time_split"] = {k: c[k] / wc for k in ("SQ_ACTIVE_INST_VALU", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY",

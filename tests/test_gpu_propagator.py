@@ -6,6 +6,8 @@
   (m_mix, |Delta'|) grid (delta 1.7e-7 .. 1.7e3) at K = 80 LZ lengths, S = 6400: stated tolerance
   2e-6 relative (window-limited, ~K^-3, at small delta) and 5e-8 for delta > 1 (the phase-based
   step count and the exact adiabatic cells for delta > 16);
+* vs the EXACT finite-window solution (Weber functions, tests/golden/golden_weber.json):
+  stated tolerance 1e-7 at S = 2000, 1e-10 at S = 16000 (5e-7 with an adiabatic cell);
 * phase averaging: widely separated crossings averaged over position jitter reproduce the
   incoherent composition (1 - prod(1 - 2 P_c)) / 2.
 """
@@ -56,3 +58,29 @@ def test_phase_average_is_incoherent_composition(gpu_engine):
     inc = pkg("lz").p_incoherent([P1] * N)
     assert abs(got.mean() - inc) < 4 * got.std() / math.sqrt(n) + 1e-3, (got.mean(), inc)
     assert got.std() > 1e-3  # coherent (Stueckelberg) oscillations are present
+
+
+def test_kernel_vs_exact_weber_solution(gpu_engine):
+    """Kernel vs the EXACT finite-window solution of its model (cell-by-cell Weber functions,
+    tests/golden/golden_weber.json; tests/test_propagator_exact.py states the tolerances):
+    C5 settings S = 2000: <= 1e-7 (Magnus cells), <= 5e-7 with an exact adiabatic cell;
+    S = 16000: <= 1e-10 (Magnus cells, S^-4 convergence)."""
+    import json
+    import os
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden_weber.json")))
+    groups = {}
+    for c in g["cases"]:
+        groups.setdefault((len(c["m"]), c["K"]), []).append(c)
+    n = 0
+    for (N, K), cs in groups.items():
+        m = np.array([c["m"] for c in cs])
+        d = np.array([c["d"] for c in cs])
+        x = np.array([c["x"] for c in cs])
+        ex = np.array([c["P"] for c in cs])
+        adiabatic = np.any(m * m / (2 * g["v_w"] * d) > 16.0, axis=1)
+        for S, tol_m, tol_a in ((2000, 1e-7, 5e-7), (16000, 1e-10, 5e-7)):
+            got = gpu_engine.lz_propagate(m, d, x, g["v_w"], K, S).cpu().numpy()
+            tol = np.where(adiabatic, tol_a, tol_m)
+            assert np.all(np.abs(got - ex) <= tol), (N, K, S, np.abs(got - ex).max())
+        n += len(cs)
+    assert n == len(g["cases"]) == 50

@@ -1,0 +1,61 @@
+"""The LZ propagator's scheme (numpy restatement tests/lz_ref.py, the kernel's exact step
+sequence) against the EXACT finite-window solution of the same model: cell-by-cell Weber
+(parabolic-cylinder) functions, tests/weber_ref.py, committed as tests/golden/golden_weber.json
+by tests/golden/make_golden_weber.py.
+
+Stated accuracy of the kernel's scheme at the C5 production settings (K = 20 LZ lengths,
+S = 2000 Magnus steps per cell): |P - P_exact| <= 1e-7 with Magnus cells only, <= 5e-7 when an
+exact adiabatic cell (delta > 16) is used (its neglected edge amplitude); the Magnus error
+falls as S^-4.
+"""
+import json
+import os
+
+import pytest
+
+from lz_ref import propagate
+from weber_ref import propagate_exact
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = json.load(open(os.path.join(HERE, "golden", "golden_weber.json")))
+V_W = GOLD["v_w"]
+
+
+def _cases(kind):
+    return [c for c in GOLD["cases"] if c["kind"] == kind]
+
+
+def test_fixture_rederives():
+    for c in (_cases("single")[7], _cases("multi")[1], _cases("multi")[3], _cases("c5")[4]):
+        P = propagate_exact(c["m"], c["d"], c["x"], V_W, c["K"])
+        assert abs(P - c["P"]) <= 1e-14, (c, P)
+
+
+def test_exact_reduces_to_closed_form():
+    """Single crossing, K = 20: the window-limited exact P approaches eq.(9) (fpy:183-184)."""
+    import math
+    for c in _cases("single"):
+        delta = c["m"][0] ** 2 / (2 * V_W * c["d"][0])
+        P9 = 1.0 - math.exp(-2.0 * math.pi * delta)
+        assert abs(c["P"] - P9) <= 2e-3 * P9, (delta, c["P"], P9)
+
+
+@pytest.mark.parametrize("i", range(3))
+def test_brute_force_magnus_matches_exact(i):
+    c = _cases("multi")[i]
+    P = propagate(c["m"], c["d"], c["x"], V_W, c["K"], 6000, hybrid=False)
+    assert abs(P - c["P"]) <= 1e-10, (c, P)
+
+
+def test_hybrid_at_production_settings():
+    for c in _cases("c5")[:4] + _cases("multi"):
+        P = propagate(c["m"], c["d"], c["x"], V_W, c["K"], 2000)
+        adiabatic = any(m * m / (2 * V_W * d) > 16.0 for m, d in zip(c["m"], c["d"]))
+        assert abs(P - c["P"]) <= (5e-7 if adiabatic else 1e-7), (c, P)
+
+
+def test_magnus_fourth_order():
+    c = _cases("c5")[5]            # (m_mix, |Delta'|) = (1, 10): 8 crossings, delta ~ 0.17
+    e1 = abs(propagate(c["m"], c["d"], c["x"], V_W, c["K"], 1000) - c["P"])
+    e2 = abs(propagate(c["m"], c["d"], c["x"], V_W, c["K"], 2000) - c["P"])
+    assert 10.0 < e1 / e2 < 24.0, (e1, e2)

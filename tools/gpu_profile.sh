@@ -15,6 +15,9 @@ pmc write WRITE_SIZE
 pmc sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT
 pmc inst SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_SALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE GRBM_COUNT
 pmc mix SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_INT32
+# refresh profiles/round1/pmc_summary.json in the box's copy, so the plain bench's traffic /
+# valu_issue fields come from this build's counters (the host re-runs the summary on the merged output)
+python3 tools/summarize_profile.py $OUT round1 > $OUT/summary.log 2>&1 || echo "summary failed"
 timeout -k 10 300 python3 bench.py > $OUT/bench_plain.json 2> $OUT/bench_plain.err || exit 3
 cat $OUT/bench_plain.json
 echo done

@@ -12,8 +12,13 @@
 // s_c = (-1)^c, and the coupling is m_c.  Interior cell edges b_c are where neighbouring
 // linear pieces meet (D continuous, |D| maximal); the outer edges are xi_0 - W_0 and
 // xi_{N-1} + W_{N-1} with W_c = K * L_c, L_c = sqrt(v_w/|Delta'_c|) * max(1, sqrt(delta_c))
-// the LZ length of crossing c (delta_c = m_c^2 / (2 v_w |Delta'_c|)) and K = window_lz.  psi starts in the adiabatic state that is chi-like at the first edge; the
-// result is the conversion probability 1 - |<chi-like adiabatic state | psi>|^2 at the last.
+// the LZ length of crossing c (delta_c = m_c^2 / (2 v_w |Delta'_c|)) and K = window_lz.
+// psi starts in the chi-like DRESSED state of the first cell at its outer edge, and the result is
+// the conversion probability 1 - |<chi-like dressed state | psi>|^2 at the last cell's outer edge.
+// Dressed = second-order superadiabatic (dressed_basis below): the state that an adiabatic
+// state at t -> -inf has become, up to O(eps/(alpha tau^2)^2).  Projecting on it instead of the
+// plain adiabatic state removes the window's O(K^-3) error: a single crossing reproduces the
+// asymptotic eq.(9) to ~2e-9 at K = 20 (1/K^5), where the adiabatic projection was 7e-5 off.
 //
 // Integrator, per cell c with delta_c = m_c^2 / (2 v_w |Delta'_c|):
 //  * delta_c <= kDeltaAdiabatic: fourth-order Magnus (two Gauss-Legendre nodes) with the exact
@@ -23,13 +28,15 @@
 //      Omega = -i (n . sigma),  n = (dt m, (sqrt3/6) dt^2 m (D2-D1), dt (D1+D2)/2)
 //      U = cos|n| - i sin|n| (n/|n|) . sigma;
 //  * delta_c > kDeltaAdiabatic: the crossing is adiabatic to e^{-2 pi delta} < 1e-43, and the
-//    cell is propagated exactly in the adiabatic basis: amplitudes b+- pick up
-//    exp(-+ i (Phi + phi_S)) with the WKB phase Phi = int E dt in closed form
+//    cell is propagated exactly in its dressed basis: amplitudes b+- pick up
+//    exp(-+ i (Phi + phi_S - tails)) with the WKB phase Phi = int E dt in closed form
 //    (E = sqrt(D^2 + m^2), G(x) = [x sqrt(x^2+m^2) + m^2 asinh(x/m)]/2) and the LZ Stokes phase
 //    phi_S = pi/4 + delta (ln delta - 1) + arg Gamma(1 - i delta) = 1/(12 delta) + 1/(360 delta^3)
 //    + 1/(1260 delta^5) + 1/(1680 delta^7) + O(delta^-9) (Stirling series of ln Gamma(-i delta);
 //    checked against mpmath, and its sign against brute-force Magnus, in
-//    tests/test_propagator_math.py).
+//    tests/test_propagator_math.py).  phi_S is the whole line's dressed-energy correction; its
+//    leading part int theta'^2/(2E) dt = (m^2 alpha/8) int dD/E^5 (= 1/(12 delta) over the line)
+//    has the pieces beyond the cell's two edges removed ("tails", tail_T below).
 // One parameter point per lane, all state in registers.
 #include <hip/hip_runtime.h>
 
@@ -59,19 +66,62 @@ __device__ __forceinline__ double lz_length(double m, double a, double v_w) {
   return sqrt(v_w / a) * fmax(1.0, sqrt(delta));
 }
 
-// Adiabatic eigenvector of [[d, m],[m, -d]] with eigenvalue -sign * sqrt(d^2+m^2) ...
-// returns the eigenvector (u0, u1) (real) of the state that is chi-like (|u0| >= |u1|).
-__device__ __forceinline__ void chi_like_adiabatic(double d, double m, double& u0, double& u1) {
-  // theta = atan2(m, d)/2 ; |+> = (cos t, sin t) (eigenvalue +E), |-> = (-sin t, cos t)
-  double th = 0.5 * atan2(m, d);
-  double c = cos(th), s = sin(th);
-  if (fabs(c) >= fabs(s)) {  // |+> is chi-like
-    u0 = c;
-    u1 = s;
-  } else {                   // |-> is chi-like
-    u0 = -s;
-    u1 = c;
+// Second-order dressed (superadiabatic) basis of H = d sz + m sx with dd/dt = ddot (d linear in
+// t).  theta = atan2(m, d)/2, |+> = (cos, sin) (eigenvalue +E), |-> = (-sin, cos),
+// E = sqrt(d^2 + m^2).  Adiabatic elimination of the coupling theta' between the adiabatic
+// amplitudes, to second order in eps = theta'/(2E) = -m ddot/(4E^3):
+//   |+~> = N (|+> + beta |->),  |-~> = N (|-> - conj(beta) |+>),
+//   beta = -i eps - eps'/(2E),  eps' = 3 m ddot^2 d / (4 E^5),  N = (1 + |beta|^2)^-1/2
+// (orthonormal exactly).  tests/lz_ref.py dressed_basis restates it.
+struct Dressed {
+  Cplx p0, p1;  // |+~>
+  Cplx q0, q1;  // |-~>
+};
+
+__device__ __forceinline__ Dressed dressed_basis(double d, double ddot, double m) {
+  const double th = 0.5 * atan2(m, d);
+  double s, c;
+  sincos(th, &s, &c);
+  const double E = sqrt(d * d + m * m);
+  const double iE = 1.0 / E, iE2 = iE * iE;
+  const double eps = -m * ddot * 0.25 * iE2 * iE;
+  const double epsd = 0.75 * m * ddot * ddot * d * iE2 * iE2 * iE;
+  const double br = -0.5 * epsd * iE, bi = -eps;
+  const double nrm = 1.0 / sqrt(1.0 + br * br + bi * bi);
+  Dressed r;
+  r.p0 = {(c - s * br) * nrm, -s * bi * nrm};
+  r.p1 = {(s + c * br) * nrm, c * bi * nrm};
+  r.q0 = {(-s - c * br) * nrm, c * bi * nrm};
+  r.q1 = {(c - s * br) * nrm, s * bi * nrm};
+  return r;
+}
+
+// The chi-like dressed state (|<chi|.>| >= 1/sqrt2): start state and final projection.
+__device__ __forceinline__ void chi_like_dressed(double d, double ddot, double m, Cplx& u0, Cplx& u1) {
+  const Dressed b = dressed_basis(d, ddot, m);
+  const bool plus = b.p0.re * b.p0.re + b.p0.im * b.p0.im >= b.p1.re * b.p1.re + b.p1.im * b.p1.im;
+  u0 = plus ? b.p0 : b.q0;
+  u1 = plus ? b.p1 : b.q1;
+}
+
+// <u|psi> for u = (u0, u1)
+__device__ __forceinline__ Cplx inner(Cplx u0, Cplx u1, Cplx p0, Cplx p1) {
+  return {u0.re * p0.re + u0.im * p0.im + u1.re * p1.re + u1.im * p1.im,
+          u0.re * p0.im - u0.im * p0.re + u1.re * p1.im - u1.im * p1.re};
+}
+
+// T(x0) = int_{|x0|}^inf dx / (x^2 + m^2)^{5/2}: closed form, or its series in u = m^2/x0^2 where
+// the closed form cancels (u < 1e-3; truncation ~u^4).
+__device__ __forceinline__ double tail_T(double x0, double m) {
+  x0 = fabs(x0);
+  const double u = (m * m) / (x0 * x0);
+  if (u < 1e-3) {
+    const double ix2 = 1.0 / (x0 * x0);
+    return (0.25 - u * (5.0 / 12.0 - u * (35.0 / 64.0 - u * (21.0 / 32.0)))) * ix2 * ix2;
   }
+  const double E = sqrt(x0 * x0 + m * m);
+  const double m2 = m * m;
+  return (2.0 - x0 * (2.0 * x0 * x0 + 3.0 * m2) / (E * E * E)) / (3.0 * m2 * m2);
 }
 
 __global__ __launch_bounds__(kPropBlock) void lz_propagate_kernel(const double* __restrict__ m_mix,
@@ -90,9 +140,8 @@ __global__ __launch_bounds__(kPropBlock) void lz_propagate_kernel(const double* 
   double a0 = fabs(dp[0]);
   double left = xc[0] - K * lz_length(mm[0], a0, v_w);
   double D_left = a0 * (left - xc[0]);  // s_0 = +1
-  double u0, u1;
-  chi_like_adiabatic(D_left, mm[0], u0, u1);
-  Cplx p0 = {u0, 0.0}, p1 = {u1, 0.0};
+  Cplx p0, p1;
+  chi_like_dressed(D_left, a0 * v_w, mm[0], p0, p1);
 
   double sgn = 1.0;
   double right = left;
@@ -111,28 +160,22 @@ __global__ __launch_bounds__(kPropBlock) void lz_propagate_kernel(const double* 
     // adiabatic phase of the cell, int E dt (closed form)
     const double Phi = (wkb_G(ac * (right - xcc), mc) - wkb_G(ac * (left - xcc), mc)) / (ac * v_w);
     if (delta > kDeltaAdiabatic) {
-      // exact adiabatic following through the cell (see header)
-      double l0, l1, r0, r1;
+      // exact adiabatic following through the cell, in its dressed basis (see header)
       const double DL = slope * (left - xcc), DR = slope * (right - xcc);
-      {
-        const double th = 0.5 * atan2(mc, DL);
-        l0 = cos(th);
-        l1 = sin(th);
-        const double tr = 0.5 * atan2(mc, DR);
-        r0 = cos(tr);
-        r1 = sin(tr);
-      }
-      // b+ = <+|psi>, b- = <-|psi>; |+> = (c, s), |-> = (-s, c)
-      Cplx bp = {l0 * p0.re + l1 * p1.re, l0 * p0.im + l1 * p1.im};
-      Cplx bm = {-l1 * p0.re + l0 * p1.re, -l1 * p0.im + l0 * p1.im};
+      const double ddot = slope * v_w;
+      const Dressed L = dressed_basis(DL, ddot, mc), R = dressed_basis(DR, ddot, mc);
+      const Cplx bp = inner(L.p0, L.p1, p0, p1), bm = inner(L.q0, L.q1, p0, p1);
       const double id = 1.0 / delta, id2 = id * id;
       const double phiS = id * (1.0 / 12.0 + id2 * (1.0 / 360.0 + id2 * (1.0 / 1260.0 + id2 * (1.0 / 1680.0))));
+      const double tails = 0.125 * mc * mc * ac * v_w * (tail_T(DL, mc) + tail_T(DR, mc));
       double sn, cs;
-      sincos(Phi + phiS, &sn, &cs);
+      sincos(Phi + phiS - tails, &sn, &cs);
       const Cplx bp2 = {bp.re * cs + bp.im * sn, bp.im * cs - bp.re * sn};  // * e^{-i a}
       const Cplx bm2 = {bm.re * cs - bm.im * sn, bm.im * cs + bm.re * sn};  // * e^{+i a}
-      p0 = {r0 * bp2.re - r1 * bm2.re, r0 * bp2.im - r1 * bm2.im};
-      p1 = {r1 * bp2.re + r0 * bm2.re, r1 * bp2.im + r0 * bm2.im};
+      p0 = {bp2.re * R.p0.re - bp2.im * R.p0.im + bm2.re * R.q0.re - bm2.im * R.q0.im,
+            bp2.re * R.p0.im + bp2.im * R.p0.re + bm2.re * R.q0.im + bm2.im * R.q0.re};
+      p1 = {bp2.re * R.p1.re - bp2.im * R.p1.im + bm2.re * R.q1.re - bm2.im * R.q1.im,
+            bp2.re * R.p1.im + bp2.im * R.p1.re + bm2.re * R.q1.im + bm2.im * R.q1.re};
     } else {
       const int Sc = (int)fmax((double)S, ceil(Phi * kStepsPerRadian));
       const double h = (right - left) / (double)Sc;  // step in xi
@@ -162,12 +205,13 @@ __global__ __launch_bounds__(kPropBlock) void lz_propagate_kernel(const double* 
     left = right;
     sgn = -sgn;
   }
-  // project on the chi-like adiabatic state at the right edge of the last cell
+  // project on the chi-like dressed state at the right edge of the last cell
   const int last = n_cross - 1;
-  const double D_right = (sgn * -1.0) * fabs(dp[last]) * (right - xc[last]);  // sgn was flipped once more
-  chi_like_adiabatic(D_right, mm[last], u0, u1);
-  const double re = u0 * p0.re + u1 * p1.re;
-  const double im = u0 * p0.im + u1 * p1.im;
+  const double slope_last = -sgn * fabs(dp[last]);  // sgn was flipped once more
+  Cplx u0, u1;
+  chi_like_dressed(slope_last * (right - xc[last]), slope_last * v_w, mm[last], u0, u1);
+  const Cplx a = inner(u0, u1, p0, p1);
+  const double re = a.re, im = a.im;
   const double norm = p0.re * p0.re + p0.im * p0.im + p1.re * p1.re + p1.im * p1.im;
   P_out[p] = 1.0 - (re * re + im * im) / norm;
 }

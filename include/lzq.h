@@ -215,8 +215,10 @@ int lzq_ode_rhs(const lzq_point* pt, const lzq_ode_params* ode, double T_lo, dou
  * crossing (L = sqrt(v_w/|Delta'|) max(1, sqrt(delta))); each cell gets steps_per_crossing
  * fourth-order Magnus steps (exact SU(2) exponentials).  Arrays are [n][n_cross] row-major
  * device buffers (xi increasing per point).  Output d_P[n]: conversion probability
- * 1 - |<chi-like adiabatic state | psi_end>|^2, psi_start = chi-like adiabatic state.  For one
- * crossing this tends to 1 - exp(-2 pi delta) (fpy:183-184, PAPER eq.(9)); DESIGN.md §6
+ * 1 - |<chi-like dressed state | psi_end>|^2, psi_start = chi-like dressed state, where
+ * "dressed" = second-order superadiabatic state of the outer cell (the adiabatic state carried
+ * in from / out to infinity).  For one crossing this is 1 - exp(-2 pi delta) (fpy:183-184,
+ * PAPER eq.(9)) to <= 1e-8 relative at window_lz = 20, steps_per_crossing = 16000; DESIGN.md §6
  * states the window / step tolerances. */
 int lzq_lz_propagate(const double* d_m_mix, const double* d_dprime, const double* d_xi,
                      int64_t n, int32_t n_cross, double v_w, double window_lz,

@@ -5,7 +5,8 @@ The reference has no propagator, so parity is UNPINNED beyond the
 crossing limit, which must reproduce the reference's closed form P = 1 - exp(-2 pi delta)
 (fpy:183-184, PAPER eqs.(8)-(9)).  This module restates the same model with
 the same fourth-order Magnus scheme, step by step, so the GPU kernel can be checked against
-it to rounding, and the scheme itself against the closed form.
+it to rounding, and the scheme itself against the closed form.  Start state and final
+projection are the second-order dressed (superadiabatic) chi-like states of the outer cells.
 """
 import math
 
@@ -18,6 +19,43 @@ def chi_like(d, m):
     th = 0.5 * math.atan2(m, d)
     c, s = math.cos(th), math.sin(th)
     return (c, s) if abs(c) >= abs(s) else (-s, c)
+
+
+def dressed_basis(d, ddot, m):
+    """Second-order superadiabatic ("dressed") states of H = d sz + m sx with d' = ddot (d linear
+    in t), as the kernel's dressed_basis: returns (plus, minus), orthonormal complex 2-vectors.
+    With theta = atan2(m, d)/2, |+> = (cos, sin), |-> = (-sin, cos), E = sqrt(d^2 + m^2),
+    eps = theta'/(2E) = -m ddot/(4E^3) and eps' = 3 m ddot^2 d/(4E^5):
+        |+~> ~ |+> + beta |->,   beta  = -i eps - eps'/(2E)
+        |-~> ~ |-> + gamma |+>,  gamma = -i eps + eps'/(2E) = -conj(beta)
+    (adiabatic elimination of the non-adiabatic coupling to second order: a state prepared in
+    |+~> stays in it up to O(eps / (alpha tau^2)^2), so the window edges are K^-7 accurate)."""
+    th = 0.5 * math.atan2(m, d)
+    c, s = math.cos(th), math.sin(th)
+    E = math.hypot(d, m)
+    eps = -m * ddot / (4.0 * E ** 3)
+    epsd = 3.0 * m * ddot * ddot * d / (4.0 * E ** 5)
+    beta = complex(-epsd / (2.0 * E), -eps)
+    nrm = 1.0 / math.sqrt(1.0 + abs(beta) ** 2)
+    plus = np.array([c - s * beta, s + c * beta]) * nrm
+    minus = np.array([-s - c * beta.conjugate(), c - s * beta.conjugate()]) * nrm
+    return plus, minus
+
+
+def chi_like_dressed(d, ddot, m):
+    """The dressed state that is chi-like (|<chi|.>| >= 1/sqrt2): kernel's start / projection."""
+    plus, minus = dressed_basis(d, ddot, m)
+    return plus if abs(plus[0]) >= abs(plus[1]) else minus
+
+
+def tail_T(x0, m):
+    """int_{|x0|}^inf dx / (x^2 + m^2)^{5/2} (second-order dressed-energy tail, adiabatic cells)."""
+    x0 = abs(x0)
+    u = (m / x0) ** 2 if x0 > 0 else math.inf
+    if u < 1e-3:   # series in u = m^2/x0^2: (1/4 - 5u/12 + 35u^2/64 - 21u^3/32) / x0^4
+        return (0.25 - u * (5.0 / 12.0 - u * (35.0 / 64.0 - u * (21.0 / 32.0)))) / x0 ** 4
+    E = math.hypot(x0, m)
+    return (2.0 - x0 * (2.0 * x0 * x0 + 3.0 * m * m) / E ** 3) / (3.0 * m ** 4)
 
 
 DELTA_ADIABATIC = 16.0
@@ -36,15 +74,20 @@ def stokes_phase(delta):
 
 
 def adiabatic_cell(p, m, a, slope, xc, left, right, v_w):
-    tl = 0.5 * math.atan2(m, slope * (left - xc))
-    tr = 0.5 * math.atan2(m, slope * (right - xc))
-    bp = math.cos(tl) * p[0] + math.sin(tl) * p[1]
-    bm = -math.sin(tl) * p[0] + math.cos(tl) * p[1]
+    """Exact adiabatic following in the dressed basis of the cell: phase = WKB Phi + Stokes phase
+    (the whole line's dressed-energy correction) minus the part of that correction, (m^2 alpha/8)
+    int dx/E^5, that lies outside the cell."""
+    DL, DR = slope * (left - xc), slope * (right - xc)
+    ddot = slope * v_w
+    lp, lm = dressed_basis(DL, ddot, m)
+    rp, rm = dressed_basis(DR, ddot, m)
+    bp, bm = np.vdot(lp, p), np.vdot(lm, p)
     Phi = (wkb_G(a * (right - xc), m) - wkb_G(a * (left - xc), m)) / (a * v_w)
-    ph = Phi + stokes_phase(m * m / (2.0 * v_w * a))
+    tails = m * m * a * v_w / 8.0 * (tail_T(DL, m) + tail_T(DR, m))
+    ph = Phi + stokes_phase(m * m / (2.0 * v_w * a)) - tails
     bp *= complex(math.cos(ph), -math.sin(ph))
     bm *= complex(math.cos(ph), math.sin(ph))
-    return np.array([math.cos(tr) * bp - math.sin(tr) * bm, math.sin(tr) * bp + math.cos(tr) * bm])
+    return bp * rp + bm * rm
 
 
 def propagate(m_mix, dprime, xi, v_w, K, S, hybrid=True):
@@ -53,8 +96,8 @@ def propagate(m_mix, dprime, xi, v_w, K, S, hybrid=True):
     hybrid=False is plain Magnus with S uniform steps in every cell (brute force)."""
     N = len(m_mix)
     left = xi[0] - K * xi_lz(m_mix[0], dprime[0], v_w)
-    u0, u1 = chi_like(abs(dprime[0]) * (left - xi[0]), m_mix[0])
-    p = np.array([u0 + 0j, u1 + 0j])
+    a0 = abs(dprime[0])
+    p = chi_like_dressed(a0 * (left - xi[0]), a0 * v_w, m_mix[0])
     sgn = 1.0
     right = left
     for c in range(N):
@@ -90,8 +133,9 @@ def propagate(m_mix, dprime, xi, v_w, K, S, hybrid=True):
             p = U @ p
         left = right
         sgn = -sgn
-    u0, u1 = chi_like(-sgn * abs(dprime[-1]) * (right - xi[-1]), m_mix[-1])
-    a = u0 * p[0] + u1 * p[1]
+    slope = -sgn * abs(dprime[-1])
+    u = chi_like_dressed(slope * (right - xi[-1]), slope * v_w, m_mix[-1])
+    a = np.vdot(u, p)
     return 1.0 - abs(a) ** 2 / np.vdot(p, p).real
 
 

@@ -1,5 +1,7 @@
 """The Magnus scheme of the LZ propagator against the reference's closed form
-in the single-crossing limit, on CPU (numpy restatement tests/lz_ref.py)."""
+in the single-crossing limit, on CPU (numpy restatement tests/lz_ref.py).  With the
+second-order dressed edge states the finite window costs ~2e-9 relative at K = 20 LZ lengths
+(falling as ~K^-5), inside north_star's 1e-8 on P_LZ."""
 import math
 
 import pytest
@@ -12,16 +14,17 @@ def test_single_crossing_reduces_to_closed_form(m, dp):
     v_w = 0.3
     delta = m * m / (2 * v_w * dp)
     P_cf = 1.0 - math.exp(-2.0 * math.pi * delta)     # fpy:183-184
-    P = propagate([m], [dp], [0.0], v_w, 20, 400)
-    assert abs(P - P_cf) / P_cf < 1e-4                # finite window W = 20 xi_LZ, S = 400
+    P = propagate([m], [dp], [0.0], v_w, 20, 16000)
+    assert abs(P - P_cf) / P_cf < 5e-9                # window K = 20 LZ lengths (dressed edges), S = 16000
 
 
 def test_window_convergence_order():
     m, dp, v_w = 0.1, 1.0, 0.3
     P_cf = 1.0 - math.exp(-2.0 * math.pi * m * m / (2 * v_w * dp))
-    e20 = abs(propagate([m], [dp], [0.0], v_w, 20, 400) - P_cf)
-    e40 = abs(propagate([m], [dp], [0.0], v_w, 40, 1600) - P_cf)
-    assert e40 < e20 / 4                               # adiabatic-basis window error ~ W^-3
+    e20 = abs(propagate([m], [dp], [0.0], v_w, 20, 16000) - P_cf)
+    e40 = abs(propagate([m], [dp], [0.0], v_w, 40, 32000) - P_cf)
+    assert e40 < e20 / 25                              # dressed-edge window error ~ K^-5 (measured 52x)
+    assert e20 < 5e-9 * P_cf
 
 
 def test_norm_and_trivial_limits():
@@ -36,17 +39,17 @@ def test_adiabatic_cell_matches_brute_force_magnus():
     The hybrid's exact adiabatic cell must agree with brute-force Magnus (step-converged)."""
     m = [0.3, 1.2]
     d = [0.25, 0.1]
-    x = [0.0, 200.0]      # cell edge |D| = 14 >> m: adiabatic-cell edge error ~ 1/(4 delta (D/m)^3) ~ 6e-6
+    x = [0.0, 200.0]      # cell edge |D| = 14 m; dressed-basis edge error ~ eps (alpha/E^2)^2 ~ 1e-11
     K, v_w = 20.0, 0.3
-    hyb = propagate(m, d, x, v_w, K, 400)
+    hyb = propagate(m, d, x, v_w, K, 16000)
     bf1 = propagate(m, d, x, v_w, K, 40000, hybrid=False)
     bf2 = propagate(m, d, x, v_w, K, 80000, hybrid=False)
     assert abs(bf1 - bf2) < 1e-8                        # brute force converged
     # the second cell's phase decides the interference: P moves 0.015 -> 0.032 for x_2 180 -> 201
-    hyb_far = propagate(m, d, [0.0, 201.0], v_w, K, 400)
+    hyb_far = propagate(m, d, [0.0, 201.0], v_w, K, 2000)
     assert abs(hyb_far - hyb) > 0.01
-    # error budget: neglected non-adiabatic amplitude at the cell edges (~6e-6) and ~1 rad/step
-    assert abs(hyb - bf2) < 1e-5, (hyb, bf2)
+    # measured 1.8e-11 (the plain adiabatic basis at the edges cost 6e-6)
+    assert abs(hyb - bf2) < 1e-9, (hyb, bf2)
 
 
 def test_stokes_phase_series_vs_mpmath():

@@ -13,13 +13,14 @@ y'' + (nu + 1/2 - z^2/4) y = 0 with nu = -1 - i m^2/(2 alpha).  D_nu(z) and D_nu
 independent for non-integer nu, and c1 = (i c2' + alpha tau c2) / m.  Each cell is solved
 exactly in closed form (no time stepping), so this pins the kernel's Magnus / adiabatic-cell
 scheme and its window edges without sharing any of its numerics.  Cell edges, start state and
-final projection are the kernel's (tests/lz_ref.py).
+final projection (the second-order dressed chi-like states of the outer cells) are the
+kernel's (tests/lz_ref.py); inside the window the solution is exact.
 """
 import math
 
 import mpmath as mp
 
-from lz_ref import chi_like, xi_lz
+from lz_ref import chi_like_dressed, xi_lz
 
 
 def _cell(psi, m, alpha, tau0, tau1):
@@ -57,8 +58,9 @@ def propagate_exact(m_mix, dprime, xi, v_w, K, dps=40):
     with mp.workdps(dps):
         N = len(m_mix)
         left = xi[0] - K * xi_lz(m_mix[0], dprime[0], v_w)
-        u0, u1 = chi_like(abs(dprime[0]) * (left - xi[0]), m_mix[0])
-        psi = (mp.mpc(u0), mp.mpc(u1))
+        a0 = abs(dprime[0])
+        u = chi_like_dressed(a0 * (left - xi[0]), a0 * v_w, m_mix[0])
+        psi = (mp.mpc(u[0]), mp.mpc(u[1]))
         sgn = 1.0
         right = left
         for c in range(N):
@@ -74,8 +76,9 @@ def propagate_exact(m_mix, dprime, xi, v_w, K, dps=40):
             psi = _cell(psi, mp.mpf(m_mix[c]), alpha, t0, t1)
             left = right
             sgn = -sgn
-        u0, u1 = chi_like(-sgn * abs(dprime[-1]) * (right - xi[-1]), m_mix[-1])
-        a = u0 * psi[0] + u1 * psi[1]
+        slope = -sgn * abs(dprime[-1])
+        u = chi_like_dressed(slope * (right - xi[-1]), slope * v_w, m_mix[-1])
+        a = mp.conj(mp.mpc(u[0])) * psi[0] + mp.conj(mp.mpc(u[1])) * psi[1]
         nrm = abs(psi[0]) ** 2 + abs(psi[1]) ** 2
         return float(1 - abs(a) ** 2 / nrm)
 

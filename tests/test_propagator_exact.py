@@ -3,8 +3,8 @@ sequence) against the EXACT finite-window solution of the same model: cell-by-ce
 (parabolic-cylinder) functions, tests/weber_ref.py, committed as tests/golden/golden_weber.json
 by tests/golden/make_golden_weber.py.
 
-Stated accuracy of the kernel's scheme at the C5 production settings (K = 20 LZ lengths,
-S = 2000 Magnus steps per cell): |P - P_exact| <= 2e-7 (measured 1.1e-7); at S = 16000:
+Stated accuracy of the kernel's scheme at K = 20 LZ lengths: S = 2000 Magnus steps per cell
+|P - P_exact| <= 2e-7 (measured 1.1e-7); the C5 default S = 6000 <= 5e-9 (measured 2.5e-9); S = 16000:
 <= 1e-10 (measured 4.4e-11), exact adiabatic cells (delta > 16, dressed basis) included.  The
 Magnus error falls as S^-4.  The exact single-crossing P at K = 20 (dressed window edges) is
 within 5e-9 relative of eq.(9) (measured 1.95e-9).
@@ -53,6 +53,14 @@ def test_hybrid_at_production_settings():
     for c in _cases("c5")[:4] + _cases("multi"):
         P = propagate(c["m"], c["d"], c["x"], V_W, c["K"], 2000)
         assert abs(P - c["P"]) <= 2e-7, (c, P)
+
+
+def test_c5_default_steps():
+    from conftest import pkg
+    assert pkg("sweep").CrossingSpec().steps == 6000
+    for c in _cases("c5") + _cases("multi"):
+        P = propagate(c["m"], c["d"], c["x"], V_W, c["K"], 6000)
+        assert abs(P - c["P"]) <= 5e-9, (c, P)
 
 
 def test_hybrid_step_converged_with_adiabatic_cell():

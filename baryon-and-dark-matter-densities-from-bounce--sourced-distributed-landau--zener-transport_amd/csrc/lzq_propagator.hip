@@ -21,12 +21,18 @@
 // asymptotic eq.(9) to ~2e-9 at K = 20 (1/K^5), where the adiabatic projection was 7e-5 off.
 //
 // Integrator, per cell c with delta_c = m_c^2 / (2 v_w |Delta'_c|):
-//  * delta_c <= kDeltaAdiabatic: fourth-order Magnus (two Gauss-Legendre nodes) with the exact
-//    SU(2) exponential, S_c = max(S, ceil(Phi_c * kStepsPerRadian)) uniform steps, Phi_c the
-//    cell's adiabatic phase (closed form below), so wide / strongly coupled cells get the
-//    steps their phase needs: for H = D sz + m sx,
-//      Omega = -i (n . sigma),  n = (dt m, (sqrt3/6) dt^2 m (D2-D1), dt (D1+D2)/2)
-//      U = cos|n| - i sin|n| (n/|n|) . sigma;
+//  * delta_c <= kDeltaAdiabatic: eighth-order Magnus with the exact SU(2) exponential,
+//    S_c = max(S, ceil(Phi_c * kStepsPerRadian)) uniform steps, Phi_c the cell's adiabatic
+//    phase (closed form below), so wide / strongly coupled cells get the steps their phase
+//    needs.  H = D(t) sz + m sx is linear in t, so its Magnus series over a step of length dt
+//    centred on D is known in closed form (derived symbolically: Dyson series, then log):
+//      Omega = -i (n . sigma),  U = cos|n| - i sin|n| (n/|n|) . sigma,  D' = dD/dt, E2 = D^2 + m^2
+//      n_x = m dt [1 - D'^2 dt^4/60 - D'^2 dt^6 (3D^2 + 4m^2)/1890]
+//      n_y = D' m dt^3 [1/6 + dt^2 E2/90 + dt^4 (8 E2^2 - 9 D'^2)/7560]
+//      n_z = D dt [1 - D'^2 m^2 dt^6/1890]                                     + O(dt^9).
+//    The dt^3 terms alone are the two-node Gauss-Legendre (fourth-order) Magnus step; the dt^5
+//    and dt^7 terms carry the far-field E^2 growth of its error.  tests/lz_ref.py restates it;
+//    tests/test_propagator_exact.py checks it against the exact Weber solution;
 //  * delta_c > kDeltaAdiabatic: the crossing is adiabatic to e^{-2 pi delta} < 1e-43, and the
 //    cell is propagated exactly in its dressed basis: amplitudes b+- pick up
 //    exp(-+ i (Phi + phi_S - tails)) with the WKB phase Phi = int E dt in closed form
@@ -47,9 +53,8 @@
 namespace lzq {
 
 constexpr int kPropBlock = 256;
-constexpr double kSqrt3Over6 = 0x1.279a74590331cp-2;  // sqrt(3)/6
 constexpr double kDeltaAdiabatic = 16.0;              // e^{-2 pi 16} = 2e-44
-constexpr double kStepsPerRadian = 1.0;
+constexpr double kStepsPerRadian = 3.0;              // ~1/3 rad of adiabatic phase per step at most
 
 // G(x) = int_0^x sqrt(t^2 + m^2) dt
 __device__ __forceinline__ double wkb_G(double x, double m) {
@@ -180,13 +185,22 @@ __global__ __launch_bounds__(kPropBlock) void lz_propagate_kernel(const double* 
       const int Sc = (int)fmax((double)S, ceil(Phi * kStepsPerRadian));
       const double h = (right - left) / (double)Sc;  // step in xi
       const double dt = h * inv_vw;                  // step in t
-      const double nx = dt * mc;
+      // per-cell coefficients of the eighth-order Magnus vector (header)
+      const double ddot = slope * v_w, dd2 = ddot * ddot, m2 = mc * mc;
+      const double dt2 = dt * dt, dt4 = dt2 * dt2;
+      const double ax = 1.0 - dd2 * dt4 * (1.0 / 60.0);
+      const double bx = dd2 * dt4 * dt2 * (1.0 / 1890.0);
+      const double cxm = dt * mc, m2x4 = 4.0 * m2;
+      const double cy = ddot * mc * dt * dt2, ey1 = dt2 * (1.0 / 90.0), ey2 = dt4 * (1.0 / 7560.0);
+      const double dd2x9 = 9.0 * dd2;
+      const double cz = dt * (1.0 - bx * m2);
       for (int i = 0; i < Sc; ++i) {
         const double xm = left + ((double)i + 0.5) * h;
-        const double D1 = slope * ((xm - kSqrt3Over6 * h) - xcc);
-        const double D2 = slope * ((xm + kSqrt3Over6 * h) - xcc);
-        const double ny = kSqrt3Over6 * dt * mc * (D2 - D1) * dt;
-        const double nz = 0.5 * dt * (D1 + D2);
+        const double D = slope * (xm - xcc);
+        const double D2 = D * D, E2 = D2 + m2;
+        const double nx = cxm * (ax - bx * (3.0 * D2 + m2x4));
+        const double ny = cy * ((1.0 / 6.0) + ey1 * E2 + ey2 * (8.0 * E2 * E2 - dd2x9));
+        const double nz = cz * D;
         const double nn = sqrt(nx * nx + ny * ny + nz * nz);
         double sn, cs;
         sincos(nn, &sn, &cs);

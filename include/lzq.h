@@ -212,13 +212,14 @@ int lzq_ode_rhs(const lzq_point* pt, const lzq_ode_params* ode, double T_lo, dou
  * point: i dpsi/dt = H(t) psi, H = [[D(xi), m_c],[m_c, -D(xi)]], xi = v_w t, D piecewise linear
  * with slope (-1)^c |Delta'_c| through crossing c at xi_c (continuous at the turning points
  * between crossings).  The outer half-windows are window_lz LZ lengths of the first/last
- * crossing (L = sqrt(v_w/|Delta'|) max(1, sqrt(delta))); each cell gets steps_per_crossing
- * fourth-order Magnus steps (exact SU(2) exponentials).  Arrays are [n][n_cross] row-major
+ * crossing (L = sqrt(v_w/|Delta'|) max(1, sqrt(delta))); each cell gets
+ * max(steps_per_crossing, 3 x its adiabatic phase in radians) eighth-order Magnus steps (exact
+ * SU(2) exponentials; cells with delta > 16 are propagated in closed form).  Arrays are [n][n_cross] row-major
  * device buffers (xi increasing per point).  Output d_P[n]: conversion probability
  * 1 - |<chi-like dressed state | psi_end>|^2, psi_start = chi-like dressed state, where
  * "dressed" = second-order superadiabatic state of the outer cell (the adiabatic state carried
  * in from / out to infinity).  For one crossing this is 1 - exp(-2 pi delta) (fpy:183-184,
- * PAPER eq.(9)) to <= 1e-8 relative at window_lz = 20, steps_per_crossing = 16000; DESIGN.md §6
+ * PAPER eq.(9)) to <= 1e-8 relative at window_lz = 20, steps_per_crossing = 1000; DESIGN.md §6
  * states the window / step tolerances. */
 int lzq_lz_propagate(const double* d_m_mix, const double* d_dprime, const double* d_xi,
                      int64_t n, int32_t n_cross, double v_w, double window_lz,

@@ -4,7 +4,7 @@ csrc/lzq_propagator.hip (TEST INFRASTRUCTURE).
 The reference has no propagator, so parity is UNPINNED beyond the single-
 crossing limit, which must reproduce the reference's closed form P = 1 - exp(-2 pi delta)
 (fpy:183-184, PAPER eqs.(8)-(9)).  This module restates the same model with
-the same fourth-order Magnus scheme, step by step, so the GPU kernel can be checked against
+the same eighth-order Magnus scheme, step by step, so the GPU kernel can be checked against
 it to rounding, and the scheme itself against the closed form.  Start state and final
 projection are the second-order dressed (superadiabatic) chi-like states of the outer cells.
 """
@@ -12,7 +12,6 @@ import math
 
 import numpy as np
 
-S3 = math.sqrt(3.0) / 6.0
 
 
 def chi_like(d, m):
@@ -59,7 +58,7 @@ def tail_T(x0, m):
 
 
 DELTA_ADIABATIC = 16.0
-STEPS_PER_RADIAN = 1.0
+STEPS_PER_RADIAN = 3.0
 
 
 def wkb_G(x, m):
@@ -118,13 +117,27 @@ def propagate(m_mix, dprime, xi, v_w, K, S, hybrid=True):
         Sc = int(max(S, math.ceil(Phi * STEPS_PER_RADIAN))) if hybrid else S
         h = (right - left) / Sc
         dt = h / v_w
-        nx = dt * m_mix[c]
+        mc = m_mix[c]
+        # eighth-order Magnus vector of the linear-in-t Hamiltonian (kernel header), same
+        # operation order as the kernel
+        ddot = slope * v_w
+        dd2, m2 = ddot * ddot, mc * mc
+        dt2 = dt * dt
+        dt4 = dt2 * dt2
+        ax = 1.0 - dd2 * dt4 * (1.0 / 60.0)
+        bx = dd2 * dt4 * dt2 * (1.0 / 1890.0)
+        cxm, m2x4 = dt * mc, 4.0 * m2
+        cy, ey1, ey2 = ddot * mc * dt * dt2, dt2 * (1.0 / 90.0), dt4 * (1.0 / 7560.0)
+        dd2x9 = 9.0 * dd2
+        cz = dt * (1.0 - bx * m2)
         for i in range(Sc):
             xm = left + (i + 0.5) * h
-            D1 = slope * ((xm - S3 * h) - xi[c])
-            D2 = slope * ((xm + S3 * h) - xi[c])
-            ny = S3 * dt * m_mix[c] * (D2 - D1) * dt
-            nz = 0.5 * dt * (D1 + D2)
+            D = slope * (xm - xi[c])
+            D2 = D * D
+            E2 = D2 + m2
+            nx = cxm * (ax - bx * (3.0 * D2 + m2x4))
+            ny = cy * ((1.0 / 6.0) + ey1 * E2 + ey2 * (8.0 * E2 * E2 - dd2x9))
+            nz = cz * D
             nn = math.sqrt(nx * nx + ny * ny + nz * nz)
             sn, cs = math.sin(nn), math.cos(nn)
             sc = sn / nn if nn > 0 else 1.0

@@ -3,11 +3,11 @@
 * vs the numpy restatement tests/lz_ref.py (same scheme): agreement to rounding, for one and
   for several crossings (parity UNPINNED w.r.t. the reference, which has no propagator);
 * single crossing vs the reference's closed form (fpy:183-184, PAPER eq.(9)) over the C2
-  (m_mix, |Delta'|) grid (delta 1.7e-7 .. 1.7e3) at K = 20 LZ lengths, S = 16000: stated
+  (m_mix, |Delta'|) grid (delta 1.7e-7 .. 1.7e3) at K = 20 LZ lengths, S = 1000: stated
   tolerance 1e-8 relative (north_star's P_LZ gate; the dressed window edges leave ~2e-9);
 * vs the EXACT finite-window solution (Weber functions, tests/golden/golden_weber.json):
-  stated tolerance 2e-7 at S = 2000, 5e-9 at the C5 default S = 6000, 1e-10 at S = 16000
-  (exact adiabatic cells included);
+  stated tolerance 2e-9 at the C5 default S = 1000, 1e-11 at S = 16000 (exact adiabatic
+  cells included);
 * phase averaging: widely separated crossings averaged over position jitter reproduce the
   incoherent composition (1 - prod(1 - 2 P_c)) / 2.
 """
@@ -36,7 +36,7 @@ def test_matches_numpy_restatement(gpu_engine):
 def test_single_crossing_closed_form(gpu_engine):
     m, d = np.meshgrid(np.logspace(-3, 0, 12), np.logspace(-3, 1, 12), indexing="ij")
     m, d = m.ravel(), d.ravel()
-    got = gpu_engine.lz_propagate(m, d, np.zeros_like(m), V_W, 20.0, 16000).cpu().numpy()
+    got = gpu_engine.lz_propagate(m, d, np.zeros_like(m), V_W, 20.0, 1000).cpu().numpy()
     delta = m * m / (2 * V_W * d)
     P = -np.expm1(-2 * np.pi * delta)
     rel = np.abs(got - P) / np.maximum(P, 1e-300)
@@ -64,8 +64,8 @@ def test_phase_average_is_incoherent_composition(gpu_engine):
 def test_kernel_vs_exact_weber_solution(gpu_engine):
     """Kernel vs the EXACT finite-window solution of its model (cell-by-cell Weber functions,
     tests/golden/golden_weber.json; tests/test_propagator_exact.py states the tolerances):
-    S = 2000: <= 2e-7; C5 default S = 6000: <= 5e-9; S = 16000: <= 1e-10 (S^-4 convergence),
-    exact adiabatic cells (dressed basis) included."""
+    C5 default S = 1000: <= 2e-9; S = 16000: <= 1e-11 (eighth-order Magnus), exact adiabatic
+    cells (dressed basis) included."""
     import json
     import os
     g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden_weber.json")))
@@ -78,7 +78,7 @@ def test_kernel_vs_exact_weber_solution(gpu_engine):
         d = np.array([c["d"] for c in cs])
         x = np.array([c["x"] for c in cs])
         ex = np.array([c["P"] for c in cs])
-        for S, tol in ((2000, 2e-7), (6000, 5e-9), (16000, 1e-10)):
+        for S, tol in ((1000, 2e-9), (16000, 1e-11)):
             got = gpu_engine.lz_propagate(m, d, x, g["v_w"], K, S).cpu().numpy()
             assert np.all(np.abs(got - ex) <= tol), (N, K, S, np.abs(got - ex).max())
         n += len(cs)

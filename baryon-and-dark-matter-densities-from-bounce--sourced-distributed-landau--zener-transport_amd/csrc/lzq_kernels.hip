@@ -669,9 +669,11 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void yields_points_kernel(co
 #endif
   __shared__ WaveSlot slots[kWavesPerBlock];
   const int lane = threadIdx.x & (kWaveSize - 1);
-  const int64_t idx = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  if (idx >= n) return;  // wave-uniform
+  // wave index and point index formed from readfirstlane, so they live in SGPRs (a VGPR copy
+  // of the 64-bit index was the kernel's only scratch spill)
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t idx = (int64_t)blockIdx.x * kWavesPerBlock + w;
+  if (idx >= n) return;  // wave-uniform
   {
     const lzq_point pt = pts[idx];
     const double P = Pov ? Pov[idx] : pt.P_chi_to_B;
@@ -700,9 +702,9 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void yields_grid_kernel(lzq_
 #endif
   __shared__ WaveSlot slots[kWavesPerBlock];
   const int lane = threadIdx.x & (kWaveSize - 1);
-  const int64_t local = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // SGPR (see yields_points_kernel)
+  const int64_t local = (int64_t)blockIdx.x * kWavesPerBlock + w;
   if (local >= count) return;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   {
     lzq_point pt;
     const double Pg = grid_point(base, grid, start + local, pt);

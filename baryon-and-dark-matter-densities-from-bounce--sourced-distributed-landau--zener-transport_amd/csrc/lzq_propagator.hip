@@ -129,6 +129,28 @@ __device__ __forceinline__ double tail_T(double x0, double m) {
   return (2.0 - x0 * (2.0 * x0 * x0 + 3.0 * m2) / (E * E * E)) / (3.0 * m2 * m2);
 }
 
+// cos(x) and sin(x)/x as even Taylor polynomials in x2 = x^2 for x2 <= 1 (truncation < 1e-17;
+// the Magnus step's rotation angle |n| ~ E dt <= 1 at >= 3 steps per radian), else through
+// sincos.  Replaces sqrt + sincos + a division per step; tests/lz_ref.py uses libm sin/cos.
+__constant__ double kSincC[9] = {0x1.0000000000000p+0, -0x1.5555555555555p-3, 0x1.1111111111111p-7, -0x1.a01a01a01a01ap-13, 0x1.71de3a556c734p-19, -0x1.ae64567f544e4p-26, 0x1.6124613a86d09p-33, -0x1.ae7f3e733b81fp-41, 0x1.952c77030ad4ap-49};
+__constant__ double kCosC[10] = {0x1.0000000000000p+0, -0x1.0000000000000p-1, 0x1.5555555555555p-5, -0x1.6c16c16c16c17p-10, 0x1.a01a01a01a01ap-16, -0x1.27e4fb7789f5cp-22, 0x1.1eed8eff8d898p-29, -0x1.93974a8c07c9dp-37, 0x1.ae7f3e733b81fp-45, -0x1.6827863b97d97p-53};
+__device__ __forceinline__ void cos_sinc(double x2, double& cs, double& sc) {
+  if (x2 <= 1.0) {
+    double ps = kSincC[8], pc = kCosC[9];
+#pragma unroll
+    for (int k = 7; k >= 0; --k) ps = __builtin_fma(ps, x2, kSincC[k]);
+#pragma unroll
+    for (int k = 8; k >= 0; --k) pc = __builtin_fma(pc, x2, kCosC[k]);
+    sc = ps;
+    cs = pc;
+  } else {
+    const double x = sqrt(x2);
+    double sn;
+    sincos(x, &sn, &cs);
+    sc = sn / x;
+  }
+}
+
 __global__ __launch_bounds__(kPropBlock) void lz_propagate_kernel(const double* __restrict__ m_mix,
                                                                   const double* __restrict__ dprime,
                                                                   const double* __restrict__ xi, int64_t n,
@@ -201,10 +223,8 @@ __global__ __launch_bounds__(kPropBlock) void lz_propagate_kernel(const double* 
         const double nx = cxm * (ax - bx * (3.0 * D2 + m2x4));
         const double ny = cy * ((1.0 / 6.0) + ey1 * E2 + ey2 * (8.0 * E2 * E2 - dd2x9));
         const double nz = cz * D;
-        const double nn = sqrt(nx * nx + ny * ny + nz * nz);
-        double sn, cs;
-        sincos(nn, &sn, &cs);
-        const double sc = nn > 0.0 ? sn / nn : 1.0;
+        double cs, sc;  // cos|n| and sin|n|/|n|, both functions of |n|^2
+        cos_sinc(nx * nx + ny * ny + nz * nz, cs, sc);
         const double sx = sc * nx, sy = sc * ny, sz = sc * nz;
         // U11 = cs - i sz ; U12 = -sy - i sx ; U21 = sy - i sx ; U22 = cs + i sz
         Cplx q0, q1;

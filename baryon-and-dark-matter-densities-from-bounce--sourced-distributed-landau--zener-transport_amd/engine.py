@@ -146,10 +146,11 @@ class Engine:
                                                 self._stream()))
         return work, status
 
-    def ode(self, points, ode_params, max_steps: int = 1 << 26, chunk: int = 1 << 15) -> tuple:
+    def ode(self, points, ode_params, max_steps: int = 1 << 26, chunk: int = 1 << 18) -> tuple:
         """fpy:385-417 for n points (POINT_DTYPE records + ODE_DTYPE records): (n, 6) yields
         table and (n,) int32 status (enum lzq_ode_status), both on the device.  Points are
-        processed in chunks so that the spline workspace stays <= chunk * 25.6 KB."""
+        processed in chunks so that the spline workspace stays <= chunk * 25.6 KB (6.7 GB at the
+        default 2^18 points: 2 waves/SIMD on all 1024 SIMDs need >= 131072 points per launch)."""
         pts = np.ascontiguousarray(points, dtype=_native.POINT_DTYPE).reshape(-1)
         ods = np.ascontiguousarray(ode_params, dtype=_native.ODE_DTYPE).reshape(-1)
         if pts.size != ods.size:

@@ -4,7 +4,7 @@ restatement on the host cores.  Configs: the equal-mass config with wash-out in 
 window (20000 Radau steps/point), a stiff thermal annihilation case, and the shipped window
 (~1e6 steps/point).  Points differ in P and flux (uniform work).  One JSON line per config.
 
-    python tools/bench_ode.py [n_narrow] [n_full]
+    python tools/bench_ode.py [n_narrow] [n_full] [chunk]
 """
 import importlib
 import json
@@ -36,6 +36,7 @@ def cfgs_for(over: dict, n: int):
 def main():
     n_narrow = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
     n_full = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
+    chunk = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 18
     cfgm = importlib.import_module(PKG + ".config")
     eng = importlib.import_module(PKG + ".engine").Engine(0)
     from oracle import oracle as O
@@ -50,7 +51,7 @@ def main():
         eng.ode(pts[:64], ods[:64])  # warm-up
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        tab, st = eng.ode(pts, ods, chunk=1 << 16)
+        tab, st = eng.ode(pts, ods, chunk=chunk)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         ok = bool((st == 0).all())
@@ -61,7 +62,7 @@ def main():
         t = tab[:k].cpu().numpy()
         err = float(np.max(np.abs(t - ref) / np.maximum(np.abs(ref), 1e-300)))
         steps = O.ode_point(cfgs[0])["n_steps"]
-        print(json.dumps({"config": name, "points": n, "steps_per_point": steps, "gpu_points_per_s": n / dt,
+        print(json.dumps({"config": name, "points": n, "chunk": chunk, "steps_per_point": steps, "gpu_points_per_s": n / dt,
                           "gpu_seconds": dt, "all_ok": ok, "cpu_oracle_points_per_s": k / dtc, "cpu_threads": 16,
                           "cpu_sample": k, "max_rel_diff_gpu_vs_oracle": err}), flush=True)
 

@@ -116,10 +116,19 @@ def cpu_baseline(axes, n_points_total: int, seconds: float = 12.0) -> dict:
     t0 = time.perf_counter()
     O.points_batch(sample, nthreads=threads)
     dt = time.perf_counter() - t0
+    # the same restatement on one core (1 core and all cores), a short sample
+    one = cfgs(max(8, int(2.0 * len(sample) / dt / threads)))
+    t1 = time.perf_counter()
+    O.points_batch(one, nthreads=1)
+    dt1 = time.perf_counter() - t1
     return {"value": len(sample) / dt, "unit": "points/s", "cores": threads, "kind": "port",
             "sample": f"{len(sample)} uniformly sampled grid points (numpy default_rng(0)), full "
                       f"n_y=8000 x nz=1200 quadrature + epilogue each, C oracle (oracle/lzq_oracle.c) "
-                      f"with {threads} OpenMP threads, {dt:.1f} s"}
+                      f"with {threads} OpenMP threads, {dt:.1f} s",
+            "single_core": {"value": len(one) / dt1, "unit": "points/s", "cores": 1,
+                            "sample": f"{len(one)} further points of the same sample stream, 1 thread, {dt1:.1f} s"},
+            "reference_python_note": "the reference itself (numpy, fpy:231-267) ran 6.20 points/s on one core "
+                                     "of the build container (SURVEY §6); it cannot travel to the GPU box"}
 
 
 def main():

@@ -18,6 +18,7 @@
 // Accuracy vs the libm exp of the oracle: the rounding of c2 costs |u|*2^-53 relative,
 // i.e. < 1e-13 even where u ~ -1000 (and those nodes are ~1e-300 of the sum).
 #pragma once
+#include <math.h>
 #include <stdint.h>
 
 #if defined(__HIPCC__)
@@ -137,12 +138,32 @@ struct TabPoly<14, 3> {
   static constexpr double B[3] = {0x1.62e42fefa39efp-15, 0x1.ebfbdff86d9eep-31, 0x1.c6b08d7087d56p-47};
 };
 
+// Completed-square form of the degree-2 step (LZQ_SQFORM, default on for 13 bits / degree 2):
+//   2^(r/N) ~= C * ((r + A)^2 + beta),  A an INTEGER,
+// so that s = r + A comes out of the reduction at no extra cost (w = (M + A) - t is exact
+// because M + A is, then s = fma(c2N, g, w) rounds once), the polynomial is ONE fma
+// q = fma(s, s, beta), and C is folded into the table, T''[j] = C * 2^(j/N).  The node is then
+//   t, w, s, address, exponent insert, q, v = T'' * q, F += omega' * v  = 8 VALU (was 9).
+// A = N/ln2 would be Taylor's centre (11818.47); the nearest integers cost accuracy: the
+// minimax (C, beta) at A = 11819 leaves |2^(r/N) - p(r)| <= 1.73e-14 relative on [-1/2, 1/2]
+// (A = 11818: 2.16e-14) -- 6e5 x inside the north_star 1e-8 gate (tests/test_exp2_host.py
+// pins it against mpmath).  C ~ 2^-27.06 lowers the table's exponents by 28, so KMIN is
+// -1506 N (e + 512 - 28 >= -1022 keeps T''*2^(e+512) normal); those clamped nodes still
+// contribute omega*2^u with u < -1506 octaves, which rounds away exactly.
+#ifndef LZQ_SQFORM
+#define LZQ_SQFORM 1
+#endif
+
 constexpr int kTabBits = LZQ_TABBITS;
 constexpr int kTabN = 1 << kTabBits;
 constexpr int kPolyDeg = LZQ_POLYDEG;
+constexpr bool kSqForm = LZQ_SQFORM && kTabBits == 13 && kPolyDeg == 2;
+constexpr double kSqA = 11819.0;
+constexpr double kSqBeta = 139678307.60123383601;
+constexpr long double kSqC = 3.5795199663544010274e-9L;
 constexpr int kTabShift = 20 - kTabBits;          // (k << S) = (e << 20) + (j << S)
 constexpr int32_t kOmegaBias = 512;               // T' carries 2^512, omega' carries 2^-512
-constexpr int32_t kTabKMin = -1534 * kTabN;       // e >= -1534 -> e + 512 >= -1022 (normal)
+constexpr int32_t kTabKMin = (kSqForm ? -1506 : -1534) * kTabN;  // T'*2^(e+512) stays normal
 static_assert(kTabBits >= 8 && kTabBits <= 16, "table bits");
 static_assert((int64_t)kTabKMin * (1 << kTabShift) >= INT32_MIN, "k << S must not overflow");
 
@@ -157,7 +178,14 @@ LZQ_HD double tab_q_with(double r, const double (&B)[DEG]) {
   return r * acc;
 }
 
-// Table entry j as stored (host side): 2^(j/N) rounded once, high word pre-biased by
+// Exact value of table entry j before its one rounding (host side): 2^(j/N), times C in the
+// completed-square form.
+static inline long double tab_exact(int32_t j) {
+  const long double T = exp2l((long double)j / (long double)kTabN);
+  return kSqForm ? T * kSqC : T;
+}
+
+// Table entry j as stored (host side): tab_exact(j) rounded once, high word pre-biased by
 // (512 << 20) - (j << S) (mod 2^32).
 static inline uint64_t tab_entry_bits(long double T_exact, int32_t j) {
   const uint64_t b = __builtin_bit_cast(uint64_t, (double)T_exact);
@@ -194,11 +222,15 @@ LZQ_HD double tab_scale(double Tp, uint32_t k) {
 LZQ_HD double exp2_tab_scaled(double c2N, double g, const double* tabp) {
   constexpr double kMagic = 0x1.8p52;
   const double t = __builtin_fma(c2N, g, kMagic);
-  const double kd = t - kMagic;
-  const double r = __builtin_fma(c2N, g, -kd);
   const double tc = __builtin_fmax(t, kMagic + (double)kTabKMin);
   const uint32_t k = (uint32_t)__builtin_bit_cast(uint64_t, tc);
   const double Ts = tab_scale(tabp[tab_byte_addr(k) >> 3], k);
+  if constexpr (kSqForm) {
+    const double s = __builtin_fma(c2N, g, (kMagic + kSqA) - t);  // r + A, one rounding
+    return Ts * __builtin_fma(s, s, kSqBeta);
+  }
+  const double kd = t - kMagic;
+  const double r = __builtin_fma(c2N, g, -kd);
   const double q = tab_q_with<kPolyDeg>(r, TabPoly<kTabBits, kPolyDeg>::B);
   return __builtin_fma(Ts, q, Ts);
 }

@@ -296,6 +296,7 @@ __device__ __forceinline__ void zsum(const ZNode* __restrict__ zt, const double*
     constexpr double kMagic = 0x1.8p52;
     constexpr double kTClamp = kMagic + (double)kTabKMin;  // exact
     const double Mv = vgpr_const(kMagic);
+    const double MAv = kMagic + kSqA;  // exact (an integer below 2^53)
     // polynomial coefficients; B1 pinned in a VGPR for the whole loop (see tab_q_with)
     double Bv[kPolyDeg];
 #pragma unroll
@@ -318,8 +319,12 @@ __device__ __forceinline__ void zsum(const ZNode* __restrict__ zt, const double*
 #pragma unroll
         for (int b = 0; b < YB; ++b) {
           const double t = __builtin_fma(c2[b], g4[kk], Mv);
-          const double kd = t - Mv;
-          r[b][kk] = __builtin_fma(c2[b], g4[kk], -kd);
+          if constexpr (kSqForm) {
+            r[b][kk] = __builtin_fma(c2[b], g4[kk], MAv - t);  // s = r + A (lzq_exp2.h)
+          } else {
+            const double kd = t - Mv;
+            r[b][kk] = __builtin_fma(c2[b], g4[kk], -kd);
+          }
           const double tc = CLAMP ? __builtin_fmax(t, kTClamp) : t;
           kc[b][kk] = (uint32_t)__builtin_bit_cast(uint64_t, tc);
           a[b][kk] = tab_byte_addr(kc[b][kk]);
@@ -333,8 +338,12 @@ __device__ __forceinline__ void zsum(const ZNode* __restrict__ zt, const double*
 #pragma unroll
         for (int b = 0; b < YB; ++b) {
           const double Ts = tab_scale(T[b][kk], kc[b][kk]);
-          const double q = tab_q_with<kPolyDeg>(r[b][kk], Bv);
-          F[b] = __builtin_fma(om[kk], __builtin_fma(Ts, q, Ts), F[b]);
+          if constexpr (kSqForm) {
+            F[b] = __builtin_fma(om[kk], Ts * __builtin_fma(r[b][kk], r[b][kk], kSqBeta), F[b]);
+          } else {
+            const double q = tab_q_with<kPolyDeg>(r[b][kk], Bv);
+            F[b] = __builtin_fma(om[kk], __builtin_fma(Ts, q, Ts), F[b]);
+          }
         }
     }
   } else {
@@ -839,7 +848,7 @@ int build_host_tables() {
   // T[j] = 2^(j/N): x87 long double exp2 (64-bit mantissa) rounded once to double, stored
   // with the pre-biased high word of lzq::tab_entry_bits
   for (int j = 0; j < lzq::kTabN; ++j)
-    g_exp2tab[j] = lzq::tab_entry_bits(exp2l((long double)j / (long double)lzq::kTabN), j);
+    g_exp2tab[j] = lzq::tab_entry_bits(lzq::tab_exact(j), j);
   // the kernel's magic-constant reduction needs |c2N*g| < 2^51 on every non-dead lane
   // (zsum_dispatch: dead iff c2N*g_1 <= -N*1077), i.e. N*1077*g_max/g_1 < 2^51
   if (!((double)lzq::kTabN * 1077.0 * g_g4[n - 1] / g_g4[1] < 0x1p50))

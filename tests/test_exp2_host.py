@@ -28,7 +28,7 @@ extern "C" void pv(const double* r, long n, double* out) {
 static double tab[lzq::kTabN];
 extern "C" void evt(const double* c2, const double* g, long n, double* out) {
   for (int j = 0; j < lzq::kTabN; ++j) {
-    uint64_t b = lzq::tab_entry_bits(exp2l((long double)j / (long double)lzq::kTabN), j);
+    uint64_t b = lzq::tab_entry_bits(lzq::tab_exact(j), j);
     memcpy(&tab[j], &b, 8);
   }
   // the kernel multiplies the 2^512-scaled value by omega' = omega * 2^-512 in one fma; here
@@ -60,8 +60,11 @@ def lib():
 
 
 # (table bits, polynomial degree) -> minimax |dq| of tools/exp2_tab_poly.py (Taylor for (8, 4))
+# (13, 2) is the completed-square form C*((r + A)^2 + beta) with integer A (LZQ_SQFORM, the
+# default: one VALU fewer per node); (13, 2, 0) the plain r*(B1 + r*B2) form it replaced.
 DEFAULT_TAB = (13, 2)  # LZQ_TABBITS / LZQ_POLYDEG defaults in lzq_exp2.h
-TAB_VARIANTS = {(8, 4): 1.9e-17, (10, 3): 9.4e-17, (12, 2): 2.53e-14, (12, 3): 3.7e-19, (13, 2): 3.16e-15, (14, 2): 3.95e-16, (14, 3): 1.5e-21}
+TAB_VARIANTS = {(8, 4): 1.9e-17, (10, 3): 9.4e-17, (12, 2): 2.53e-14, (12, 3): 3.7e-19, (13, 2): 1.73e-14,
+                (13, 2, 0): 3.16e-15, (14, 2): 3.95e-16, (14, 3): 1.5e-21}
 
 
 def run(L, c2, g, fn="ev"):
@@ -104,17 +107,22 @@ def test_exp2_nonpos_range(lib, fn):
 
 @pytest.mark.parametrize("fn", ["ev", "evt"])
 def test_exp2_nonpos_zero_gamma(lib, fn):
-    # gamma4(z_0) = 0 and c2 from y = 50 (|c2| ~ 4e21): 2^(c2*0) = 1
-    assert run(lib, [-4.1e21, -1.0], [0.0, 0.0], fn).tolist() == [1.0, 1.0]
+    # gamma4(z_0) = 0 and c2 from y = 50 (|c2| ~ 4e21): 2^(c2*0) = 1 (exactly for the
+    # r*(B1 + r*B2) forms; within the minimax bound for the completed-square table form)
+    got = run(lib, [-4.1e21, -1.0], [0.0, 0.0], fn)
+    tol = TAB_VARIANTS[DEFAULT_TAB] + 2.3e-16 if fn == "evt" else 0.0
+    assert np.all(np.abs(got - 1.0) <= tol), got
 
 
-@pytest.mark.parametrize("bits,deg", sorted(TAB_VARIANTS))
-def test_table_variant_matches_mpmath(bits, deg):
-    L = _build([("LZQ_TABBITS", bits), ("LZQ_POLYDEG", deg)])
+@pytest.mark.parametrize("variant", sorted(TAB_VARIANTS))
+def test_table_variant_matches_mpmath(variant):
+    bits, deg = variant[:2]
+    sq = variant[2] if len(variant) > 2 else 1
+    L = _build([("LZQ_TABBITS", bits), ("LZQ_POLYDEG", deg), ("LZQ_SQFORM", sq)])
     rng = np.random.default_rng(5)
     u = -np.concatenate([rng.uniform(0, 60, 3000), 10 ** rng.uniform(-15, 0, 1000)])
     g = np.ones_like(u)
     got = run(L, u, g, "evt")
     worst = max(abs(float((mp.mpf(o) - mp.power(2, mp.mpf(x))) / mp.power(2, mp.mpf(x)))) for o, x in zip(got, u))
     # polynomial error + rounding of T[j] (1/2 ulp) + the final fma (1/2 ulp) + q's own rounding
-    assert worst < TAB_VARIANTS[(bits, deg)] + 2.3e-16, worst
+    assert worst < TAB_VARIANTS[variant] + 2.3e-16, worst

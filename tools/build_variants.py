@@ -13,8 +13,7 @@ B = importlib.import_module(PKG + ".build")
 
 GRID = {"LZQ_MAGIC": [0, 1], "LZQ_KUNROLL": [4, 8], "LZQ_YB": [1, 2]}
 # explicit list (overrides the full product when non-empty); keys omitted take the defaults
-CONFIGS = [dict(LZQ_KUNROLL=8), dict(LZQ_BLOCK=1024, LZQ_MIN_WAVES=8), dict(LZQ_BLOCK=1024, LZQ_MIN_WAVES=8, LZQ_KUNROLL=4),
-           dict(LZQ_BLOCK=512, LZQ_MIN_WAVES=6), dict(LZQ_BLOCK=768, LZQ_MIN_WAVES=6)]
+CONFIGS = [dict(LZQ_SQFORM=0), dict(LZQ_SQFORM=1)]
 
 
 def main():

@@ -188,9 +188,10 @@ __device__ __forceinline__ double exp_sc(double x) {
 }
 
 // numpy.linspace element (handles numpy's step == 0 branch as well)
-__device__ __forceinline__ double y_node(const QuadSetup& s, int64_t j) {
-  if (j == s.n - 1) return s.y_hi;
-  if (s.step == 0.0) return ((double)j / (double)(s.n - 1)) * s.delta + s.y_lo;
+__device__ __forceinline__ double y_node(const QuadSetup& s, int j) {  // n_y is int32
+  const int n = (int)s.n;
+  if (j == n - 1) return s.y_hi;
+  if (s.step == 0.0) return ((double)j / (double)(n - 1)) * s.delta + s.y_lo;
   return (double)j * s.step + s.y_lo;
 }
 
@@ -248,9 +249,9 @@ __device__ __forceinline__ double integrand_from(const YFactors& f, double F) {
 }
 
 // trapezoid weight of y-node j: (d_{j-1} + d_j)/2 with d = diff(ys)      fpy:267
-__device__ __forceinline__ double y_weight(const QuadSetup& s, int64_t j, double y) {
+__device__ __forceinline__ double y_weight(const QuadSetup& s, int j, double y) {
   double dl = (j > 0) ? y - y_node(s, j - 1) : 0.0;
-  double dr = (j + 1 < s.n) ? y_node(s, j + 1) - y : 0.0;
+  double dr = (j + 1 < (int)s.n) ? y_node(s, j + 1) - y : 0.0;
   return 0.5 * (dl + dr);
 }
 
@@ -460,14 +461,16 @@ __device__ __forceinline__ int lane_id() {
 template <int YB, int EXPV, typename Slot>
 __device__ double yb_wave(Slot* slots, int w, const ZNode* __restrict__ zt, const double* tab, int truncate) {
   if (slots[w].s.empty) return 0.0;
-  const int64_t n = __builtin_bit_cast(int64_t, uniform(__builtin_bit_cast(double, slots[w].s.n)));  // SGPR
-  const int64_t per_pass = (int64_t)kWaveSize * YB;
+  // y-node counts are int32 (n_y of the C ABI): 32-bit loop bounds save the SGPRs that
+  // would otherwise spill around the z-loop
+  const int n = (int)__builtin_bit_cast(int64_t, uniform(__builtin_bit_cast(double, slots[w].s.n)));  // SGPR
+  const int per_pass = kWaveSize * YB;
 #if LZQ_ACC_LDS
   slots[w].acc[lane_id()] = 0.0;
 #else
   double acc = 0.0;
 #endif
-  for (int64_t base = 0; base < n; base += per_pass) {
+  for (int base = 0; base < n; base += per_pass) {
     const int lane = lane_id();
     int wo = w;
     asm volatile("" : "+s"(wo));
@@ -481,8 +484,8 @@ __device__ double yb_wave(Slot* slots, int w, const ZNode* __restrict__ zt, cons
 #endif
 #pragma unroll
     for (int b = 0; b < YB; ++b) {
-      const int64_t j = base + (int64_t)b * kWaveSize + lane;
-      const int64_t jj = j < n ? j : n - 1;  // tail lanes recompute the last node with weight 0
+      const int j = base + b * kWaveSize + lane;
+      const int jj = j < n ? j : n - 1;  // tail lanes recompute the last node with weight 0
       yv[b] = y_node(s, jj);
       ey[b] = exp_sc(pymax(pymin(yv[b], 50.0), -50.0));                          // fpy:161
       c2[b] = ((s.cneg * ey[b]) * kLog2E) * c2_scale<EXPV>();                 // fpy:163 c, log2 units
@@ -501,8 +504,8 @@ __device__ double yb_wave(Slot* slots, int w, const ZNode* __restrict__ zt, cons
       const QuadSetup& sr = slots[wr].s;
 #pragma unroll
       for (int b = 0; b < YB; ++b) {
-        const int64_t j = base + (int64_t)b * kWaveSize + lane2;
-        const int64_t jj = j < n ? j : n - 1;
+        const int j = base + b * kWaveSize + lane2;
+        const int jj = j < n ? j : n - 1;
         yv[b] = y_node(sr, jj);
         ey[b] = exp_sc(pymax(pymin(yv[b], 50.0), -50.0));
         wt[b] = j < n ? y_weight(sr, jj, yv[b]) : 0.0;

@@ -265,7 +265,7 @@ def main():
                          "valu_issue": valu_issue(per, kern_ms),
                          "note": "achieved = SURVEY §8d's algorithmic 30 FLOP/node (the node priced at ROCm's "
                                  "exp(double), 27 FLOP) x 9.6e6 nodes/point over the kernel's HIP-event time. "
-                                 "The kernel's table-driven exp needs 12 FP64 FLOP/node in ~9.4 VALU issue "
+                                 "The kernel's table-driven exp needs 10 FP64 FLOP/node in ~8.5 VALU issue "
                                  "slots, so frac > 1 = beating the stock-exp FP64 roofline; the hardware bound "
                                  "is VALU issue, reported in valu_issue (DESIGN.md §5.1)"},
         }

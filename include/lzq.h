@@ -115,7 +115,7 @@ int lzq_ztables(double* z, double* gamma4, double* omega);
 
 /* Tuning knobs for ablations (process-wide, not thread-safe against concurrent launches).
  * LZQ_TUNE_EXP selects the inner-loop exponential: LZQ_EXP_TABLE (default; 2^(j/N) LDS table,
- * N = 2^LZQ_TABBITS = 8192, + degree-2 minimax polynomial, <= 3.2e-15 relative) or
+ * N = 2^LZQ_TABBITS = 8192, + degree-2 minimax polynomial in completed-square form, <= 1.73e-14 relative) or
  * LZQ_EXP_POLY11 (degree-11 minimax polynomial, 0.6 ulp).  Results agree to ~1e-14 relative.
  * Returns the previous value. */
 /* LZQ_TUNE_TRUNCATE (0 = dense, the default; 1 = on): stop each wave's z-sum at the first

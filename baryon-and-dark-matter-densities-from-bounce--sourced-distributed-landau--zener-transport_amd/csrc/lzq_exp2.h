@@ -159,7 +159,7 @@ constexpr int kTabN = 1 << kTabBits;
 constexpr int kPolyDeg = LZQ_POLYDEG;
 constexpr bool kSqForm = LZQ_SQFORM && kTabBits == 13 && kPolyDeg == 2;
 constexpr double kSqA = 11819.0;
-constexpr double kSqBeta = 139678307.60123383601;
+constexpr double kSqBeta = 139678307.60123383601;  // tools/exp2_tab_poly.py --sq 11819
 constexpr long double kSqC = 3.5795199663544010274e-9L;
 constexpr int kTabShift = 20 - kTabBits;          // (k << S) = (e << 20) + (j << S)
 constexpr int32_t kOmegaBias = 512;               // T' carries 2^512, omega' carries 2^-512

@@ -9,6 +9,11 @@ the result), then rounded to double.  Prints C hex-floats plus the fitted error 
 worst error of the double-precision evaluation against mpmath.
 
     python tools/exp2_tab_poly.py BITS DEG
+    python tools/exp2_tab_poly.py --sq [A]     (completed-square form, 13 bits)
+
+--sq fits the completed-square form of LZQ_SQFORM, 2^(r/N) ~= C*((r + A)^2 + beta) with A a
+fixed INTEGER (default 11819): a minimax of the RELATIVE error over (C, C*D), D = A^2 + beta,
+which is linear in those two unknowns (a linear program), and prints kSqC / kSqBeta.
 """
 import sys
 
@@ -48,7 +53,41 @@ def evaluate(Bd, r):
     return float(mp.mpf(r) * mp.mpf(acc))  # q = r * (...), one rounding
 
 
+def fit_sq(A, bits=13, npts=4001):
+    """Minimax by linear programming (scipy HiGHS) on a uniform grid of [-1/2, 1/2]: the
+    relative error is linear in (C, C*D); solved as corrections to Taylor's (C, C*D) scaled by
+    1e-14 so the LP sees O(1) numbers (the header's kSqC / kSqBeta come from this)."""
+    from scipy.optimize import linprog
+    mp.mp.dps = 40
+    N = mp.mpf(2) ** bits
+    h = mp.log(2) / N
+    A = mp.mpf(A)
+    xs = [mp.mpf(-0.5) + mp.mpf(i) / (npts - 1) for i in range(npts)]
+    fs = [mp.power(2, x / N) for x in xs]
+    x10 = h / (2 * A)
+    a1 = np.array([float(x10 * (x * x + 2 * A * x) / fv) for x, fv in zip(xs, fs)])
+    a2 = np.array([float(1 / fv) for fv in fs])
+    e0 = np.array([float(x10 * (x * x + 2 * A * x) / fv + 1 / fv - 1) for x, fv in zip(xs, fs)])
+    S = 1e-14
+    one = np.ones_like(a1)
+    res = linprog([0, 0, 1], A_ub=np.vstack([np.c_[a1, a2, -one], np.c_[-a1, -a2, -one]]),
+                  b_ub=np.r_[-e0 / S, e0 / S], bounds=[(None, None)] * 3, method="highs")
+    d1, d2, t = res.x
+    C = x10 * (1 + mp.mpf(d1) * S)
+    beta = (1 + mp.mpf(d2) * S) / C - A * A
+    return C, beta, t * S
+
+
+def main_sq(A):
+    C, beta, e = fit_sq(A)
+    print(f"A = {A}: minimax relative error ~ {mp.nstr(e, 5)}")
+    print(f"  kSqC    = {mp.nstr(C, 20)}L")
+    print(f"  kSqBeta = {mp.nstr(beta, 20)}")
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--sq":
+        return main_sq(int(sys.argv[2]) if len(sys.argv) > 2 else 11819)
     bits = int(sys.argv[1]) if len(sys.argv) > 1 else 14
     deg = int(sys.argv[2]) if len(sys.argv) > 2 else 2
     B, e = fit(bits, deg)

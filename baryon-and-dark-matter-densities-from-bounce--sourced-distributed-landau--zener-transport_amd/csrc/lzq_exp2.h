@@ -95,9 +95,10 @@ LZQ_HD double exp2_nonpos(double c2, double g, int32_t bias = 0) {
 //   BITS DEG  LDS/block  |dq| (minimax)     VALU/node  C2 points/s (1 GPU)
 //     8   4     2 KB     1.9e-17 (0.1 ulp)   12.5       3.17e5  (round-1 kernel: ldexp path)
 //    12   2    32 KB     2.5e-14 (114 ulp)   11.4       3.54e5  (ldexp path, 2-op address)
-//    13   2    64 KB     3.2e-15 (14 ulp)    10         (this path; 512-thread blocks)
+//    13   2    64 KB     3.2e-15 (14 ulp)    10         4.64e5  (LZQ_SQFORM=0)
+//    13   2sq  64 KB     1.73e-14 (78 ulp)   9          5.25e5  (default: completed square, below)
 // The 13-bit address is ONE v_lshlrev_b16 ((k << 3) mod 2^16 = 8*(k mod 8192)).  The default's
-// 3.2e-15 bound moves Y_B by at most that much (relative), 3e6 x inside the north_star 1e-8
+// 1.73e-14 bound moves Y_B by at most that much (relative), 6e5 x inside the north_star 1e-8
 // gate; tests/test_exp2_host.py pins every row against mpmath.
 #ifndef LZQ_TABBITS
 #define LZQ_TABBITS 13

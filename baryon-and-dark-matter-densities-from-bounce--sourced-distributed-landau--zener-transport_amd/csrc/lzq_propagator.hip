@@ -53,6 +53,9 @@
 namespace lzq {
 
 constexpr int kPropBlock = 256;
+#ifndef LZQ_PROP_MIN_WAVES
+#define LZQ_PROP_MIN_WAVES 3  // 167 VGPRs (4 spilled outside the step loop): 3 waves/SIMD, -13% time vs 2 (tools/ablate_prop.py)
+#endif
 constexpr double kDeltaAdiabatic = 16.0;              // e^{-2 pi 16} = 2e-44
 constexpr double kStepsPerRadian = 3.0;              // ~1/3 rad of adiabatic phase per step at most
 
@@ -151,7 +154,7 @@ __device__ __forceinline__ void cos_sinc(double x2, double& cs, double& sc) {
   }
 }
 
-__global__ __launch_bounds__(kPropBlock) void lz_propagate_kernel(const double* __restrict__ m_mix,
+__global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_kernel(const double* __restrict__ m_mix,
                                                                   const double* __restrict__ dprime,
                                                                   const double* __restrict__ xi, int64_t n,
                                                                   int32_t n_cross, double v_w, double K,

@@ -760,10 +760,14 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void ode_aov_table_kernel(co
   const int64_t idx = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (idx >= n) return;  // wave-uniform
   const lzq_point pt = pts[idx];
-  const double Tp = pt.T_p_GeV, B = pt.beta_over_H;
-  const double T_lo = Tlo ? Tlo[idx] : pt.T_min_over_Tp * Tp, T_hi = Thi ? Thi[idx] : pt.T_max_over_Tp * Tp;
-  const double stepT = (T_hi - T_lo) / (double)(kOdeNT - 1);
+  // every per-point value is wave-uniform: pinned in SGPRs (readfirstlane) so that the z-loop
+  // keeps its VGPRs (without this 12 VGPRs spilled around every z-loop)
+  const double Tp = uniform(pt.T_p_GeV), B = uniform(pt.beta_over_H);
+  const double T_lo = uniform(Tlo ? Tlo[idx] : pt.T_min_over_Tp * Tp);
+  const double T_hi = uniform(Thi ? Thi[idx] : pt.T_max_over_Tp * Tp);
+  const double stepT = uniform((T_hi - T_lo) / (double)(kOdeNT - 1));
   const QuadSetup s = quad_setup(pt, 0.0, 1.0, 1.0, LZQ_NY_MIN);  // only pref0 / cneg are used
+  const double pref0 = uniform(s.pref0), cneg = uniform(s.cneg);
   double* w = ws + idx * (int64_t)kOdeWS;
   for (int base = 0; base < kOdeNT; base += kWaveSize) {
     const int i = base + lane;
@@ -771,9 +775,9 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void ode_aov_table_kernel(co
     const double T = linspace_at(T_lo, T_hi, stepT, ii, kOdeNT);
     const double y = y_of_T(T, Tp, B);
     const double expy = exp_sc(pymax(pymin(y, 50.0), -50.0));  // fpy:161
-    double c2[1] = {((s.cneg * expy) * kLog2E) * c2_scale<EXPV>()}, F[1];
+    double c2[1] = {((cneg * expy) * kLog2E) * c2_scale<EXPV>()}, F[1];
     zsum_dispatch<1, EXPV>(zt, tab, c2, F, truncate);
-    const double Av = (y > 50.0) ? 0.0 : (s.pref0 * expy) * F[0];  // fpy:159-165
+    const double Av = (y > 50.0) ? 0.0 : (pref0 * expy) * F[0];  // fpy:159-165
     if (i < kOdeNT) w[i < kOdeNT - 1 ? 4 * i + 3 : kOdeWS - 1] = pymax(Av, 0.0);
   }
 }

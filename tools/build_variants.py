@@ -13,7 +13,7 @@ B = importlib.import_module(PKG + ".build")
 
 GRID = {"LZQ_MAGIC": [0, 1], "LZQ_KUNROLL": [4, 8], "LZQ_YB": [1, 2]}
 # explicit list (overrides the full product when non-empty); keys omitted take the defaults
-CONFIGS = [dict(LZQ_PROP_MIN_WAVES=1), dict(LZQ_PROP_MIN_WAVES=3)]
+CONFIGS = [dict(LZQ_KUNROLL=8), dict(LZQ_KUNROLL=10), dict(LZQ_KUNROLL=12)]
 
 
 def main():

@@ -279,7 +279,12 @@ __device__ __forceinline__ double c2_scale() { return EXPV == kExpTable ? (doubl
 //   v  = fma(T', q, T')         = 2^(u/N) * 2^512, always a normal double (e+512 >= -1022)
 //   F  = fma(omega', v, F)      omega' = omega * 2^-512 (z table), so omega'*v = omega*2^u
 //
-// = 10 VALU per node (round-1 kernel: 12.5).  The last fma rounds the exact product omega*2^u
+// = 10 VALU per node (round-1 kernel: 12.5).  The default completed-square form (kSqForm,
+// lzq_exp2.h) replaces kd, r, q and the T*(1+q) fma by
+//   w  = (M + A) - t            exact (M + A an integer below 2^53)
+//   s  = fma(c2, g, w)          r + A, one rounding
+//   v  = T'' * fma(s, s, beta)  T'' = C * 2^(j/N) * 2^(e+512) from the same lookup + insert
+// = 9 VALU per node, 8 on clamp-free passes.  The last fma rounds the exact product omega*2^u
 // once, so gradual underflow is exact; clamped nodes (u < -1534 octaves) contribute
 // omega*2^-1534*(...) which rounds away exactly like the underflowed 0 it stands for.
 // For |u| < 2^51 (every non-dead lane, checked on the host) t is exact; dead lanes (whose
@@ -298,11 +303,11 @@ __device__ __forceinline__ void zsum(const ZNode* __restrict__ zt, const double*
     constexpr double kTClamp = kMagic + (double)kTabKMin;  // exact
     const double Mv = vgpr_const(kMagic);
     const double MAv = kMagic + kSqA;  // exact (an integer below 2^53)
-    // polynomial coefficients; B1 pinned in a VGPR for the whole loop (see tab_q_with)
+    // plain form: polynomial coefficients, B1 pinned in a VGPR for the whole loop (see tab_q_with)
     double Bv[kPolyDeg];
 #pragma unroll
     for (int i = 0; i < kPolyDeg; ++i) Bv[i] = TabPoly<kTabBits, kPolyDeg>::B[i];
-    Bv[0] = vgpr_const(Bv[0]);
+    if constexpr (!kSqForm) Bv[0] = vgpr_const(Bv[0]);
     const char* tabb = reinterpret_cast<const char*>(tab);
     for (int k = 0; k < kend; k += kKUnroll) {
       double g4[kKUnroll], om[kKUnroll];

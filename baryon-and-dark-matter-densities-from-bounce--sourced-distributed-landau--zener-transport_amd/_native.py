@@ -61,6 +61,7 @@ LZQ_NZ = 1200
 TUNE_EXP, TUNE_TRUNCATE = 0, 1  # enum lzq_tune_key
 EXP_POLY11, EXP_TABLE = 0, 1  # enum lzq_exp_variant
 LZQ_MAX_AXES = 8
+ABI_VERSION = 1  # LZQ_ABI_VERSION (tests/test_capi.py checks it against the library)
 
 # Symbols declared in include/lzq.h (checked by tests/test_capi.py against the header).
 EXPORTS = ("lzq_abi_version", "lzq_last_error", "lzq_init", "lzq_ztables", "lzq_tune", "lzq_aov_batch",

@@ -57,7 +57,11 @@ def main(argv=None):
         st = int(status[0].item())
         if st in (1, 2):  # scipy's ValueError (CubicSpline knots / solve_ivp max_step)
             raise ValueError(_native.ODE_STATUS[st])
-        if st != 0:
+        if st == 4:  # fpy:408-410: warn, then report the state where the solver stopped
+            print("[warn] ODE solver reported failure:", _native.ODE_STATUS[st])
+        elif st != 0:
+            # LZQ_ODE_TOO_MANY_STEPS: a window needing > 2^26 fixed Radau steps (|x1-x0|/max_step,
+            # fpy:404) is deliberately unsupported (the reference would run for days); exit loudly
             raise RuntimeError(f"lzq ODE fallback: {_native.ODE_STATUS[st]}")
     YB_fin, Ychi_fin, rhoB0, rhoDM0, ratio, _ = (float(v) for v in table[0].cpu().numpy())
 

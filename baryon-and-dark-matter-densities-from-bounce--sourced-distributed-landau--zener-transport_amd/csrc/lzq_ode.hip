@@ -402,13 +402,15 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
       OdeStage sg[3];
 #pragma unroll
       for (int j = 0; j < 3; ++j) sg[j] = ode_stage(o, w, xk + R.c[j] * h);
+      const double YB_prev = YB;
       if (!radau_step(R, sg, h, Ychi, YB)) {
+        YB = YB_prev;  // report the state at the start of the failed step, like sol.y[:, -1] (fpy:408-410)
         st = LZQ_ODE_NEWTON;
         break;
       }
     }
   }
-  if (st == LZQ_ODE_OK) {  // fpy:412-417
+  if (st == LZQ_ODE_OK || st == LZQ_ODE_NEWTON) {  // fpy:412-417
     const double nB0 = YB * kS0M3, nDM0 = Ychi * kS0M3;
     r.Y_B = YB;
     r.Y_chi = Ychi;

@@ -21,10 +21,13 @@
 // asymptotic eq.(9) to ~2e-9 at K = 20 (1/K^5), where the adiabatic projection was 7e-5 off.
 //
 // Integrator, per cell c with delta_c = m_c^2 / (2 v_w |Delta'_c|):
-//  * delta_c <= kDeltaAdiabatic: eighth-order Magnus with the exact SU(2) exponential,
-//    S_c = max(S, ceil(Phi_c * kStepsPerRadian)) uniform steps, Phi_c the cell's adiabatic
-//    phase (closed form below), so wide / strongly coupled cells get the steps their phase
-//    needs.  H = D(t) sz + m sx is linear in t, so its Magnus series over a step of length dt
+//  * delta_c <= kDeltaAdiabatic: eighth-order Magnus with the exact SU(2) exponential on the
+//    cell's CORE [xi_c - W_c, xi_c + W_c] (core_halfwidth: 2K LZ lengths for delta <= 1, else
+//    out to where the adiabaticity eps = m|alpha|/(4E^3) falls to kCoreEps), with
+//    S_c = max(S, ceil(Phi_core * kStepsPerRadian)) uniform steps, Phi_core the core's adiabatic
+//    phase (closed form below); the parts of the cell outside the core are followed in the
+//    dressed basis with no stepping (dressed_follow).  The step count is thereby bounded by
+//    the core (<= 3 (2K)^2 max(1, delta) + S) whatever the crossing spacing.  H = D(t) sz + m sx is linear in t, so its Magnus series over a step of length dt
 //    centred on D is known in closed form (derived symbolically: Dyson series, then log):
 //      Omega = -i (n . sigma),  U = cos|n| - i sin|n| (n/|n|) . sigma,  D' = dD/dt, E2 = D^2 + m^2
 //      n_x = m dt [1 - D'^2 dt^4/60 - D'^2 dt^6 (3D^2 + 4m^2)/1890]
@@ -58,6 +61,8 @@ constexpr int kPropBlock = 256;
 #endif
 constexpr double kDeltaAdiabatic = 16.0;              // e^{-2 pi 16} = 2e-44
 constexpr double kStepsPerRadian = 3.0;              // ~1/3 rad of adiabatic phase per step at most
+constexpr double kCoreEps = 1e-5;                    // dressed following outside eps = m|alpha|/(4E^3) <= this
+constexpr double kMaxCellSteps = 16777216.0;         // per-cell Magnus steps beyond this: P = NaN (bad input)
 
 // G(x) = int_0^x sqrt(t^2 + m^2) dt
 __device__ __forceinline__ double wkb_G(double x, double m) {
@@ -154,6 +159,41 @@ __device__ __forceinline__ void cos_sinc(double x2, double& cs, double& sc) {
   }
 }
 
+// Half-width (in xi) of a Magnus cell's core (tests/lz_ref.py core_halfwidth): 2K LZ lengths
+// for delta <= 1 (there the transition builds up over the whole crossing region and the
+// dressed-following error is set by the distance in LZ lengths: ~1e-12 at 40); for delta > 1
+// out to |D| where eps = m|alpha|/(4E^3) = kCoreEps (following error ~eps^2), clamped to
+// [1, 2K] LZ lengths.
+__device__ __forceinline__ double core_halfwidth(double m, double a, double v_w, double K) {
+  const double L = lz_length(m, a, v_w);
+  if (m * m <= 2.0 * v_w * a) return 2.0 * K * L;
+  const double Ec = cbrt(m * a * v_w / (4.0 * kCoreEps));
+  const double Dc = sqrt(fmax(Ec * Ec - m * m, 0.0));
+  return fmin(2.0 * K * L, fmax(L, Dc / a));
+}
+
+// Dressed-basis following of psi from xa to xb on one side of crossing xc (tests/lz_ref.py
+// far_segment): the dressed amplitudes pick up exp(-+ i (Phi + (m^2 |alpha|/8) |int dD/E^5|)),
+// the WKB phase plus the second-order dressed energy over the segment (the adiabatic cells'
+// tail_T terms).
+__device__ __forceinline__ void dressed_follow(Cplx& p0, Cplx& p1, double m, double a, double slope, double xc,
+                                               double xa, double xb, double v_w) {
+  const double Da = slope * (xa - xc), Db = slope * (xb - xc);
+  const double ddot = slope * v_w;
+  const Dressed A = dressed_basis(Da, ddot, m), B = dressed_basis(Db, ddot, m);
+  const Cplx bp = inner(A.p0, A.p1, p0, p1), bm = inner(A.q0, A.q1, p0, p1);
+  const double Phi = (wkb_G(a * (xb - xc), m) - wkb_G(a * (xa - xc), m)) / (a * v_w);
+  const double corr = 0.125 * m * m * a * v_w * fabs(tail_T(Da, m) - tail_T(Db, m));
+  double sn, cs;
+  sincos(Phi + corr, &sn, &cs);
+  const Cplx bp2 = {bp.re * cs + bp.im * sn, bp.im * cs - bp.re * sn};  // * e^{-i ph}
+  const Cplx bm2 = {bm.re * cs - bm.im * sn, bm.im * cs + bm.re * sn};  // * e^{+i ph}
+  p0 = {bp2.re * B.p0.re - bp2.im * B.p0.im + bm2.re * B.q0.re - bm2.im * B.q0.im,
+        bp2.re * B.p0.im + bp2.im * B.p0.re + bm2.re * B.q0.im + bm2.im * B.q0.re};
+  p1 = {bp2.re * B.p1.re - bp2.im * B.p1.im + bm2.re * B.q1.re - bm2.im * B.q1.im,
+        bp2.re * B.p1.im + bp2.im * B.p1.re + bm2.re * B.q1.im + bm2.im * B.q1.re};
+}
+
 __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_kernel(const double* __restrict__ m_mix,
                                                                   const double* __restrict__ dprime,
                                                                   const double* __restrict__ xi, int64_t n,
@@ -187,9 +227,9 @@ __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_k
     }
     const double slope = sgn * ac;
     const double delta = mc * mc / (2.0 * v_w * ac);
-    // adiabatic phase of the cell, int E dt (closed form)
-    const double Phi = (wkb_G(ac * (right - xcc), mc) - wkb_G(ac * (left - xcc), mc)) / (ac * v_w);
     if (delta > kDeltaAdiabatic) {
+      // adiabatic phase of the cell, int E dt (closed form)
+      const double Phi = (wkb_G(ac * (right - xcc), mc) - wkb_G(ac * (left - xcc), mc)) / (ac * v_w);
       // exact adiabatic following through the cell, in its dressed basis (see header)
       const double DL = slope * (left - xcc), DR = slope * (right - xcc);
       const double ddot = slope * v_w;
@@ -207,8 +247,18 @@ __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_k
       p1 = {bp2.re * R.p1.re - bp2.im * R.p1.im + bm2.re * R.q1.re - bm2.im * R.q1.im,
             bp2.re * R.p1.im + bp2.im * R.p1.re + bm2.re * R.q1.im + bm2.im * R.q1.re};
     } else {
-      const int Sc = (int)fmax((double)S, ceil(Phi * kStepsPerRadian));
-      const double h = (right - left) / (double)Sc;  // step in xi
+      // Magnus on the core, dressed following on either side of it
+      const double W = core_halfwidth(mc, ac, v_w, K);
+      const double cl = fmax(left, xcc - W), cr = fmin(right, xcc + W);
+      if (left < cl) dressed_follow(p0, p1, mc, ac, slope, xcc, left, cl, v_w);
+      const double Phic = (wkb_G(ac * (cr - xcc), mc) - wkb_G(ac * (cl - xcc), mc)) / (ac * v_w);
+      const double Sd = fmax((double)S, ceil(Phic * kStepsPerRadian));
+      if (!(Sd <= kMaxCellSteps)) {  // non-finite or absurd input (bounded for any valid one)
+        P_out[p] = __builtin_nan("");
+        return;
+      }
+      const int Sc = (int)Sd;
+      const double h = (cr - cl) / (double)Sc;  // step in xi
       const double dt = h * inv_vw;                  // step in t
       // per-cell coefficients of the eighth-order Magnus vector (header)
       const double ddot = slope * v_w, dd2 = ddot * ddot, m2 = mc * mc;
@@ -220,7 +270,7 @@ __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_k
       const double dd2x9 = 9.0 * dd2;
       const double cz = dt * (1.0 - bx * m2);
       for (int i = 0; i < Sc; ++i) {
-        const double xm = left + ((double)i + 0.5) * h;
+        const double xm = cl + ((double)i + 0.5) * h;
         const double D = slope * (xm - xcc);
         const double D2 = D * D, E2 = D2 + m2;
         const double nx = cxm * (ax - bx * (3.0 * D2 + m2x4));
@@ -238,6 +288,7 @@ __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_k
         p0 = q0;
         p1 = q1;
       }
+      if (cr < right) dressed_follow(p0, p1, mc, ac, slope, xcc, cr, right, v_w);
     }
     left = right;
     sgn = -sgn;
@@ -261,9 +312,10 @@ int lzq_set_error(int code, const char* msg);
 extern "C" int lzq_lz_propagate(const double* d_m_mix, const double* d_dprime, const double* d_xi, int64_t n,
                                 int32_t n_cross, double v_w, double window_lz, int32_t steps_per_crossing,
                                 double* d_P, void* stream) {
-  if (n < 0 || n_cross <= 0 || steps_per_crossing <= 0 || !(v_w > 0.0) || !(window_lz > 0.0) ||
-      (n > 0 && (!d_m_mix || !d_dprime || !d_xi || !d_P)))
-    return lzq_set_error(LZQ_EINVAL, "lzq_lz_propagate: bad arguments");
+  if (n < 0 || n_cross <= 0 || steps_per_crossing <= 0 || steps_per_crossing > 1000000 || !(v_w > 0.0) ||
+      !(window_lz > 0.0) || !(window_lz <= 200.0) || (n > 0 && (!d_m_mix || !d_dprime || !d_xi || !d_P)))
+    return lzq_set_error(LZQ_EINVAL, "lzq_lz_propagate: bad arguments (need n >= 0, n_cross > 0, "
+                                     "0 < steps_per_crossing <= 1e6, v_w > 0, 0 < window_lz <= 200)");
   if (n == 0) return LZQ_OK;
   const int64_t nb = (n + lzq::kPropBlock - 1) / lzq::kPropBlock;
   if (nb > 2147483647LL) return lzq_set_error(LZQ_EINVAL, "lzq_lz_propagate: n too large");

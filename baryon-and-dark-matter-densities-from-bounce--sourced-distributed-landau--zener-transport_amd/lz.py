@@ -19,7 +19,10 @@ def p_closed_form(lam: float) -> float:
 
 
 def try_compute_P_from_profile(profile_csv_path: str, v_w: float) -> Optional[float]:
-    """fpy:170-187."""
+    """fpy:170-187: same module order, clamps and swallowing of the PLUG-IN's exceptions.
+    The closed form itself runs on the GPU (lzq_p_closed_form) outside the swallowing block:
+    a failure of the HIP library raises instead of silently falling back to the config P.
+    Plug-in modules are found on sys.path, as in the reference (lzq ships one in plugins/)."""
     try:
         for modname in PLUGIN_MODULES:
             try:
@@ -30,11 +33,13 @@ def try_compute_P_from_profile(profile_csv_path: str, v_w: float) -> Optional[fl
                 P = mod.compute_prob_from_profile(profile_csv_path, v_w)
                 return float(max(min(P, 1.0), 0.0))
             if hasattr(mod, "compute_lambda_eff_from_profile"):
-                lam_eff = mod.compute_lambda_eff_from_profile(profile_csv_path)
-                return p_closed_form(lam_eff)
-        return None
+                lam_eff = float(mod.compute_lambda_eff_from_profile(profile_csv_path))
+                break
+        else:
+            return None
     except Exception:
         return None
+    return p_closed_form(lam_eff)
 
 
 def maybe_P(cfg, profile_csv: Optional[str]) -> float:

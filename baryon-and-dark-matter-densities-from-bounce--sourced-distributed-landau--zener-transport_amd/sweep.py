@@ -11,8 +11,11 @@ every rank.  Each point is reduced by one wavefront, so the gathered table is bi
 for W = 1, 2, 4, 8.  Grid-wide statistics are reduced on the host in index order.
 
 Checkpoint/resume: with --out, every evaluated chunk is written as
-`shard_<start>_<count>.npy` (allow_pickle=False); --resume reloads existing chunks instead
-of recomputing them, so a killed 1e8-point run restarts where it stopped.
+`shard_<key>_<start>_<count>.npy` (allow_pickle=False), where <key> hashes the sweep
+definition (spec_key: axes, base config, n_y, crossings, library ABI); --resume reloads
+existing chunks of the SAME definition instead of recomputing them, so a killed 1e8-point
+run restarts where it stopped, and a directory written by another sweep is never mixed in
+(manifest.json records the definition; a mismatch refuses --resume).
 
     python -m <package>.sweep --spec C2 --out sweep_c2          # 1 GPU
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m <package>.sweep --spec C4 --out c4
@@ -20,6 +23,7 @@ of recomputing them, so a killed 1e8-point run restarts where it stopped.
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import time
@@ -216,8 +220,36 @@ def shard_range(total: int, rank: int, world: int) -> Tuple[int, int]:
     return rank * total // world, (rank + 1) * total // world
 
 
-def _shard_file(out_dir: str, start: int, count: int) -> str:
-    return os.path.join(out_dir, f"shard_{start:012d}_{count}.npy")
+def spec_key(spec: SweepSpec) -> str:
+    """Hash of everything a shard's contents depend on: the sweep definition (axes, base
+    config, n_y, crossings) and the library's ABI version."""
+    d = {"spec": spec.to_json(), "abi": _native.ABI_VERSION}
+    d["spec"].pop("notes", None)
+    return hashlib.sha256(json.dumps(d, sort_keys=True).encode()).hexdigest()[:16]
+
+
+def _shard_file(out_dir: str, start: int, count: int, key: str = "") -> str:
+    return os.path.join(out_dir, f"shard_{key + '_' if key else ''}{start:012d}_{count}.npy")
+
+
+def prepare_out_dir(out_dir: str, spec: SweepSpec, resume: bool, rank: int = 0) -> str:
+    """Create `out_dir`, check / write its manifest.json; returns the shard key.  --resume
+    into a directory whose manifest describes another sweep raises instead of mixing tables."""
+    os.makedirs(out_dir, exist_ok=True)
+    key = spec_key(spec)
+    man = os.path.join(out_dir, "manifest.json")
+    if resume and os.path.exists(man):
+        with open(man) as f:
+            old = json.load(f).get("key")
+        if old != key:
+            raise RuntimeError(f"--resume: {out_dir} holds shards of another sweep (manifest key {old}, this "
+                               f"sweep {key}); use a fresh --out directory")
+    if rank == 0:
+        tmp = man + f".tmp{os.getpid()}"
+        with open(tmp, "w") as f:
+            json.dump({"key": key, "abi": _native.ABI_VERSION, "spec_def": spec.to_json()}, f, indent=1)
+        os.replace(tmp, man)
+    return key
 
 
 ComputeFn = Callable[[int, int, "object"], None]  # (start, count, out_tensor[count, 6]) -> None
@@ -225,16 +257,16 @@ ComputeFn = Callable[[int, int, "object"], None]  # (start, count, out_tensor[co
 
 def run_local(compute: ComputeFn, start: int, end: int, make_out: Callable[[int], "object"], chunk: int,
               out_dir: Optional[str] = None, resume: bool = False, sync: Callable[[], None] = lambda: None,
-              log: Callable[[str], None] = lambda s: None):
+              log: Callable[[str], None] = lambda s: None, key: str = ""):
     """Evaluate [start, end) in chunks into one (end-start, 6) tensor, with optional
-    per-chunk checkpoint files."""
+    per-chunk checkpoint files (named by `key`, see spec_key)."""
     import torch
     local = make_out(end - start)
     done = 0
     for c0 in range(start, end, chunk):
         n = min(chunk, end - c0)
         view = local[c0 - start:c0 - start + n]
-        path = _shard_file(out_dir, c0, n) if out_dir else None
+        path = _shard_file(out_dir, c0, n, key) if out_dir else None
         if path and resume and os.path.exists(path):
             arr = np.load(path, allow_pickle=False)
             if arr.shape != (n, 6):
@@ -260,17 +292,19 @@ def gather_table(local, total: int, rank: int, world: int, group=None):
         return local
     sizes = [shard_range(total, r, world)[1] - shard_range(total, r, world)[0] for r in range(world)]
     m = max(sizes)
-    pad = torch.zeros((m, 6), dtype=local.dtype, device=local.device)
-    pad[:local.shape[0]] = local
     if dist.get_backend(group) == "nccl":
+        pad = torch.zeros((m, 6), dtype=local.dtype, device=local.device)
+        pad[:local.shape[0]] = local
         buf = torch.empty((world * m, 6), dtype=local.dtype, device=local.device)
         dist.all_gather_into_tensor(buf, pad, group=group)  # RCCL over xGMI
         parts = [buf[r * m:r * m + sizes[r]] for r in range(world)]
-    else:
-        lst = [torch.empty_like(pad) for _ in range(world)]
-        dist.all_gather(lst, pad, group=group)
-        parts = [lst[r][:sizes[r]] for r in range(world)]
-    return torch.cat(parts)
+        return torch.cat(parts)
+    # gloo (CPU tests, one-GPU rehearsals): stage through host memory
+    pad = torch.zeros((m, 6), dtype=local.dtype)
+    pad[:local.shape[0]] = local.cpu()
+    lst = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(lst, pad, group=group)
+    return torch.cat([lst[r][:sizes[r]] for r in range(world)]).to(local.device)
 
 
 def summarize(table: np.ndarray, spec: SweepSpec, elapsed: Optional[float] = None) -> dict:
@@ -299,12 +333,11 @@ def run_sweep(spec: SweepSpec, engine=None, rank: int = 0, world: int = 1, chunk
         from .engine import default_engine
         engine = default_engine()
     start, end = shard_range(spec.total, rank, world)
-    if out_dir:
-        os.makedirs(out_dir, exist_ok=True)
+    key = prepare_out_dir(out_dir, spec, resume, rank) if out_dir else ""
 
     local = run_local(make_compute(spec, engine), start, end,
                       lambda n: torch.empty((n, 6), dtype=torch.float64, device=engine.device), chunk,
-                      out_dir, resume, sync=torch.cuda.synchronize, log=log)
+                      out_dir, resume, sync=torch.cuda.synchronize, log=log, key=key)
     return gather_table(local, spec.total, rank, world, group)
 
 
@@ -351,6 +384,8 @@ def main(argv=None):
     ap.add_argument("--resume", action="store_true")
     ap.add_argument("--chunk", type=int, default=1 << 20)
     ap.add_argument("--limit", type=int, default=None, help="evaluate only the first N grid points")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL over xGMI, default) | gloo (rehearsal: several ranks on one GPU)")
     args = ap.parse_args(argv)
 
     specs = builtin_specs()
@@ -362,20 +397,25 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_rank %= max(1, torch.cuda.device_count())  # gloo rehearsal: several ranks may share a GPU
     torch.cuda.set_device(local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(args.dist_backend)
     spec_total = spec.total if args.limit is None else min(args.limit, spec.total)
 
     from .engine import Engine
     eng = Engine(local_rank)
     t0 = time.perf_counter()
     start, end = shard_range(spec_total, rank, world)
+    key = prepare_out_dir(args.out, spec, args.resume, rank) if args.out else ""
 
     local = run_local(make_compute(spec, eng), start, end,
                       lambda n: torch.empty((n, 6), dtype=torch.float64, device=eng.device), args.chunk,
                       args.out, args.resume, sync=torch.cuda.synchronize,
-                      log=(print if rank == 0 else (lambda s: None)))
+                      log=(print if rank == 0 else (lambda s: None)), key=key)
     table = gather_table(local, spec_total, rank, world)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0

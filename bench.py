@@ -89,11 +89,37 @@ def grid_axes(world: int):
     return [("m_mix", np.logspace(-3.0, 0.0, 1000)), ("dprime", np.logspace(-3.0, 1.0, 1000 * world))]
 
 
+def host_cpus() -> dict:
+    """The host cores this process may use: the affinity mask, capped by the cgroup CPU quota
+    (cpu.max; on the GPU pool a 1-GPU job gets a 16-CPU quota on a 256-CPU machine, so more
+    threads than the quota only time-slice the same 16 CPUs)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = int(f.read())
+            quota = q / per if q > 0 else None
+        except (OSError, ValueError):
+            pass
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
+    return {"affinity_cpus": aff, "cgroup_cpu_quota": quota, "usable": usable,
+            "os_cpu_count": os.cpu_count(), "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
+
+
 def cpu_baseline(axes, n_points_total: int, seconds: float = 12.0) -> dict:
-    """C oracle (CPU restatement of fpy, OpenMP) on a bounded uniform sample of the grid."""
+    """C oracle (CPU restatement of fpy, OpenMP) on a bounded uniform sample of the grid, on
+    every host core this job may use (host_cpus), and on one core."""
     from oracle import oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))
+    hc = host_cpus()
+    threads = hc["usable"]
     rng = np.random.default_rng(0)
     m_vals, d_vals = axes[0][1], axes[1][1]
 
@@ -122,9 +148,11 @@ def cpu_baseline(axes, n_points_total: int, seconds: float = 12.0) -> dict:
     O.points_batch(one, nthreads=1)
     dt1 = time.perf_counter() - t1
     return {"value": len(sample) / dt, "unit": "points/s", "cores": threads, "kind": "port",
+            "host": hc,
             "sample": f"{len(sample)} uniformly sampled grid points (numpy default_rng(0)), full "
                       f"n_y=8000 x nz=1200 quadrature + epilogue each, C oracle (oracle/lzq_oracle.c) "
-                      f"with {threads} OpenMP threads, {dt:.1f} s",
+                      f"with {threads} OpenMP threads = all CPUs of this job (affinity {hc['affinity_cpus']}, "
+                      f"cgroup quota {hc['cgroup_cpu_quota']}), {dt:.1f} s",
             "single_core": {"value": len(one) / dt1, "unit": "points/s", "cores": 1,
                             "sample": f"{len(one)} further points of the same sample stream, 1 thread, {dt1:.1f} s"},
             "reference_python_note": "the reference itself (numpy, fpy:231-267) ran 6.20 points/s on one core "

@@ -172,7 +172,9 @@ enum lzq_ode_status {
   LZQ_ODE_BAD_GRID = 1,       /* T grid not strictly increasing: CubicSpline raises ValueError */
   LZQ_ODE_BAD_STEP = 2,       /* max_step <= 0 (zero-width x range): solve_ivp raises ValueError */
   LZQ_ODE_TOO_MANY_STEPS = 3, /* more than max_steps integration steps: not attempted */
-  LZQ_ODE_NEWTON = 4          /* a Radau stage system did not converge */
+  LZQ_ODE_NEWTON = 4          /* a Radau stage system did not converge: the yields are the
+                                 state at the start of the failed step (fpy:408-410 reports
+                                 sol.y[:, -1] after a failed solve) */
 };
 
 /* BoltzmannSystem.build_tables(T_lo, T_hi, n=800) (fpy:207-212) for n points, at per-point
@@ -189,7 +191,8 @@ int lzq_ode_tables(const lzq_point* d_points, int64_t n, const double* d_T_lo, c
  * (3-stage Radau IIA) on uniform steps h = (x1 - x0)/ceil(|x1 - x0|/max_step) <= max_step of
  * fpy:404, one point per lane; then the densities epilogue.  Points needing more than
  * max_steps steps are not integrated (status LZQ_ODE_TOO_MANY_STEPS, NaN yields); so are
- * points whose T grid CubicSpline would reject (LZQ_ODE_BAD_GRID).  d_status: optional [n]
+ * points whose T grid CubicSpline would reject (LZQ_ODE_BAD_GRID).  A Newton failure
+ * (LZQ_ODE_NEWTON) stops the point and reports the state reached.  d_status: optional [n]
  * int32 output (enum lzq_ode_status). */
 int lzq_ode_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, const double* d_work,
                       int64_t work_doubles, int64_t max_steps, lzq_yield* d_out, int32_t* d_status,
@@ -212,10 +215,14 @@ int lzq_ode_rhs(const lzq_point* pt, const lzq_ode_params* ode, double T_lo, dou
  * point: i dpsi/dt = H(t) psi, H = [[D(xi), m_c],[m_c, -D(xi)]], xi = v_w t, D piecewise linear
  * with slope (-1)^c |Delta'_c| through crossing c at xi_c (continuous at the turning points
  * between crossings).  The outer half-windows are window_lz LZ lengths of the first/last
- * crossing (L = sqrt(v_w/|Delta'|) max(1, sqrt(delta))); each cell gets
- * max(steps_per_crossing, 3 x its adiabatic phase in radians) eighth-order Magnus steps (exact
- * SU(2) exponentials; cells with delta > 16 are propagated in closed form).  Arrays are [n][n_cross] row-major
- * device buffers (xi increasing per point).  Output d_P[n]: conversion probability
+ * crossing (L = sqrt(v_w/|Delta'|) max(1, sqrt(delta))).  Each cell with delta <= 16 takes
+ * max(steps_per_crossing, 3 x the adiabatic phase in radians of its core) eighth-order Magnus
+ * steps (exact SU(2) exponentials) on a core around its crossing (2 window_lz LZ lengths for
+ * delta <= 1, else out to adiabaticity 1e-5) and follows the state in the second-order dressed
+ * basis outside it, so the step count is bounded for any crossing spacing; cells with
+ * delta > 16 are propagated in closed form.  Arrays are [n][n_cross] row-major device buffers
+ * (xi increasing per point).  0 < window_lz <= 200, 0 < steps_per_crossing <= 1e6 (else
+ * LZQ_EINVAL); a point whose inputs are not finite gets P = NaN.  Output d_P[n]: conversion probability
  * 1 - |<chi-like dressed state | psi_end>|^2, psi_start = chi-like dressed state, where
  * "dressed" = second-order superadiabatic state of the outer cell (the adiabatic state carried
  * in from / out to infinity).  For one crossing this is 1 - exp(-2 pi delta) (fpy:183-184,

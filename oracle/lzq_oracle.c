@@ -517,7 +517,9 @@ int oracle_ode_point(const oracle_point* p, const oracle_ode* o, int64_t max_ste
   for (int64_t k = 0; k < N && st == 0; k++) st = radau_step(&c, C, A, x0 + (double)k * h, h, Y);
   free(coef);
   *n_steps = N;
-  if (st) return st;
+  if (st != 0 && st != 4) return st;
+  /* status 4 (Newton failure): the state at the start of the failed step, as the reference
+   * reports sol.y[:, -1] after a failed solve_ivp (fpy:408-410) */
   double YB = Y[1], Ychi = Y[0];
   double rhoB = YB * S0_M3 * M_PROTON_KG;
   double rhoDM = Ychi * S0_M3 * (m * GEV_TO_KG);
@@ -527,7 +529,7 @@ int oracle_ode_point(const oracle_point* p, const oracle_ode* o, int64_t max_ste
   out->rho_DM_kg_m3 = rhoDM;
   out->DM_over_B = rhoDM / pymax(rhoB, 1e-300);
   out->P_used = p->P_chi_to_B;
-  return 0;
+  return st;
 }
 
 int64_t oracle_ode_batch(const oracle_point* p, const oracle_ode* o, int64_t n, int64_t max_steps, oracle_yield* out,

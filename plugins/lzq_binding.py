@@ -1,0 +1,177 @@
+"""lzq_binding -- reference-side ctypes binding of the lzq C ABI (include/lzq.h).
+
+This is the file a maintainer of the reference drops next to first_principles_yields.py
+("fpy") to run its hot operator on the MI355X.  It needs neither torch nor numpy: device
+buffers come from hipMalloc through ctypes, and every number is computed by liblzq.so.
+
+    import lzq_binding
+    lzq_binding.install(first_principles_yields)   # BoltzmannSystem.integrate_YB_by_quadrature -> GPU
+
+Entry points (each cites the fpy code it replaces):
+  integrate_YB_by_quadrature(self, T_lo, T_hi, n_y=6000)  fpy:231-267 (method replacement)
+  yields(cfg, P, T_lo=None, T_hi=None, n_y=8000)          fpy:231-267 + fpy:372-384 + fpy:413-417
+  p_closed_form(lams)                                     fpy:183-184
+  lz_propagate(m_mix, dprime, xi, v_w, window_lz, steps)  no fpy counterpart (north_star (1))
+  install(fpy_module)                                     monkey-patches fpy's BoltzmannSystem
+
+The library is found at $LZQ_LIB, else at <repo>/<package>/_build/liblzq.so next to this
+file's directory.  Failures raise RuntimeError with lzq_last_error(); there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_PKG = "baryon-and-dark-matter-densities-from-bounce--sourced-distributed-landau--zener-transport_amd"
+DEFAULT_LIB = os.path.join(os.path.dirname(_HERE), _PKG, "_build", "liblzq.so")
+
+_H2D, _D2H = 1, 2  # hipMemcpyHostToDevice, hipMemcpyDeviceToHost
+
+
+class lzq_point(ctypes.Structure):  # include/lzq.h: struct lzq_point (136 B)
+    _fields_ = [(n, ctypes.c_double) for n in (
+        "m_chi_GeV", "g_chi", "T_p_GeV", "beta_over_H", "v_w", "I_p", "g_star", "g_star_s",
+        "P_chi_to_B", "source_shape_sigma_y", "incident_flux_scale", "T_max_over_Tp",
+        "T_min_over_Tp", "Y_chi_init", "n_chi_at_Tp_GeV3")] + \
+        [(n, ctypes.c_int32) for n in ("stats", "regime", "has_Y_chi_init", "has_n_chi_at_Tp")]
+
+
+class lzq_yield(ctypes.Structure):  # include/lzq.h: struct lzq_yield (48 B)
+    _fields_ = [(n, ctypes.c_double) for n in ("Y_B", "Y_chi", "rho_B_kg_m3", "rho_DM_kg_m3", "DM_over_B",
+                                                "P_used")]
+
+
+assert ctypes.sizeof(lzq_point) == 136 and ctypes.sizeof(lzq_yield) == 48
+
+_hip = None
+_lzq = None
+
+
+def _libs():
+    global _hip, _lzq
+    if _lzq is None:
+        hip = ctypes.CDLL("libamdhip64.so")
+        path = os.environ.get("LZQ_LIB", DEFAULT_LIB)
+        if not os.path.exists(path):
+            raise RuntimeError(f"liblzq.so not found at {path} (build it, or set LZQ_LIB)")
+        L = ctypes.CDLL(path)
+        vp, i64, i32, d = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_double
+        hip.hipMalloc.argtypes = [ctypes.POINTER(vp), ctypes.c_size_t]
+        hip.hipFree.argtypes = [vp]
+        hip.hipMemcpy.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int]
+        hip.hipGetDevice.argtypes = [ctypes.POINTER(ctypes.c_int)]
+        L.lzq_last_error.restype = ctypes.c_char_p
+        L.lzq_init.argtypes = [ctypes.c_int]
+        L.lzq_yields_batch.argtypes = [vp, i64, i32, vp, vp, vp, vp, vp]
+        L.lzq_p_closed_form.argtypes = [vp, i64, vp, vp]
+        L.lzq_lz_propagate.argtypes = [vp, vp, vp, i64, i32, d, d, i32, vp, vp]
+        dev = ctypes.c_int(0)
+        _ok(hip.hipGetDevice(ctypes.byref(dev)) == 0, "hipGetDevice failed (no GPU?)")
+        _hip = hip
+        _lzq = L
+        _check(L.lzq_init(dev.value))
+    return _hip, _lzq
+
+
+def _ok(cond, msg):
+    if not cond:
+        raise RuntimeError(msg)
+
+
+def _check(rc):
+    if rc != 0:
+        msg = _lzq.lzq_last_error() if _lzq is not None else b""
+        raise RuntimeError(f"lzq error {rc}: {(msg or b'').decode()}")
+
+
+class _Dev:
+    """A device buffer holding a copy of a host ctypes object (freed on exit)."""
+
+    def __init__(self, nbytes, host=None):
+        hip, _ = _libs()
+        self.p = ctypes.c_void_p()
+        self.n = nbytes
+        _ok(hip.hipMalloc(ctypes.byref(self.p), max(1, nbytes)) == 0, "hipMalloc failed")
+        if host is not None:
+            _ok(hip.hipMemcpy(self.p, ctypes.addressof(host), nbytes, _H2D) == 0, "hipMemcpy H2D failed")
+
+    def read(self, host):
+        # the null stream orders this after the launches on it (stream = NULL below)
+        _ok(_hip.hipMemcpy(ctypes.addressof(host), self.p, self.n, _D2H) == 0, "hipMemcpy D2H failed")
+        return host
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        _hip.hipFree(self.p)
+
+
+def _doubles(xs):
+    xs = [float(x) for x in xs]
+    return (ctypes.c_double * len(xs))(*xs)
+
+
+def point_from_cfg(c, P: float) -> lzq_point:
+    """A reference Config (fpy:44-79) + the P it runs with -> lzq_point."""
+    reg = str(c.regime).lower()
+    return lzq_point(c.m_chi_GeV, c.g_chi, c.T_p_GeV, c.beta_over_H, c.v_w, c.I_p, c.g_star, c.g_star_s,
+                     float(P), c.source_shape_sigma_y, c.incident_flux_scale, c.T_max_over_Tp, c.T_min_over_Tp,
+                     0.0 if c.Y_chi_init is None else float(c.Y_chi_init),
+                     0.0 if c.n_chi_at_Tp_GeV3 is None else float(c.n_chi_at_Tp_GeV3),
+                     0 if str(c.chi_stats).lower().startswith("ferm") else 1,
+                     0 if reg.startswith("therm") else (1 if reg.startswith("non") else 2),
+                     int(c.Y_chi_init is not None), int(c.n_chi_at_Tp_GeV3 is not None))
+
+
+def yields(cfg, P: float, T_lo=None, T_hi=None, n_y: int = 8000) -> dict:
+    """fpy:231-267 (Y_B) + fpy:372-384, 413-417 (Y_chi, densities) for one config on the GPU
+    (T_lo/T_hi default to main()'s window, fpy:367-369)."""
+    _, L = _libs()
+    pt = point_from_cfg(cfg, P)
+    out = lzq_yield()
+    tl, th = ctypes.c_double(T_lo or 0.0), ctypes.c_double(T_hi or 0.0)
+    with _Dev(136, pt) as d_pt, _Dev(8, tl) as d_tl, _Dev(8, th) as d_th, _Dev(48) as d_out:
+        _check(L.lzq_yields_batch(d_pt.p, 1, int(n_y), d_tl.p if T_lo is not None else None,
+                                  d_th.p if T_hi is not None else None, None, d_out.p, None))
+        d_out.read(out)
+    return {n: getattr(out, n) for n, _ in lzq_yield._fields_}
+
+
+def integrate_YB_by_quadrature(self, T_lo: float, T_hi: float, n_y: int = 6000) -> float:
+    """Drop-in for BoltzmannSystem.integrate_YB_by_quadrature (fpy:231-267): same arguments,
+    same result (north_star tolerance 1e-8; measured ~1e-13), computed by lzq_yields_batch."""
+    return yields(self.cfg, self.P, T_lo, T_hi, n_y)["Y_B"]
+
+
+def p_closed_form(lams) -> list:
+    """fpy:183-184 on the GPU: clamp(1 - exp(-2 pi max(lambda, 0)), 0, 1) per entry."""
+    _, L = _libs()
+    h = _doubles(lams)
+    n = len(h)
+    out = (ctypes.c_double * n)()
+    with _Dev(8 * n, h) as d_l, _Dev(8 * n) as d_p:
+        _check(L.lzq_p_closed_form(d_l.p, n, d_p.p, None))
+        d_p.read(out)
+    return list(out)
+
+
+def lz_propagate(m_mix, dprime, xi, v_w: float, window_lz: float = 20.0, steps: int = 1000) -> float:
+    """Coherent conversion probability through the crossings of ONE profile
+    (lzq_lz_propagate; xi increasing).  One crossing: 1 - exp(-2 pi delta) to <= 1e-8."""
+    _, L = _libs()
+    n_cross = len(m_mix)
+    _ok(n_cross > 0 and len(dprime) == n_cross and len(xi) == n_cross, "need equal-length crossing lists")
+    m, d, x = _doubles(m_mix), _doubles(dprime), _doubles(xi)
+    P = ctypes.c_double()
+    with _Dev(8 * n_cross, m) as d_m, _Dev(8 * n_cross, d) as d_d, _Dev(8 * n_cross, x) as d_x, _Dev(8) as d_P:
+        _check(L.lzq_lz_propagate(d_m.p, d_d.p, d_x.p, 1, n_cross, float(v_w), float(window_lz), int(steps),
+                                  d_P.p, None))
+        d_P.read(P)
+    return P.value
+
+
+def install(fpy_module) -> None:
+    """Route the reference's quadrature operator through the GPU."""
+    fpy_module.BoltzmannSystem.integrate_YB_by_quadrature = integrate_YB_by_quadrature

@@ -59,6 +59,39 @@ def tail_T(x0, m):
 
 DELTA_ADIABATIC = 16.0
 STEPS_PER_RADIAN = 3.0
+CORE_EPS = 1e-5   # Magnus core of a cell: where the adiabaticity eps = m|alpha|/(4E^3) exceeds this
+
+
+def core_halfwidth(m, a, v_w, K):
+    """Half-width (in xi) of the cell's Magnus core.  delta <= 1: 2K LZ lengths (the
+    transition builds up over the whole crossing region, so the dressed following error is set
+    by the distance in LZ lengths: ~1e-12 at 2K = 40, 2e-11 at K = 20).  delta > 1: out to
+    |D| where eps = m|alpha|/(4E^3) falls to CORE_EPS (beyond it the dressed basis follows the
+    state to ~eps^2), at least one and at most 2K LZ lengths.  Cells narrower than the core
+    (C5's are +-20 LZ lengths) are stepped end to end as before."""
+    L = xi_lz(m, a, v_w)
+    if m * m <= 2.0 * v_w * a:     # delta <= 1
+        return 2.0 * K * L
+    Ec = (m * a * v_w / (4.0 * CORE_EPS)) ** (1.0 / 3.0)
+    Dc = math.sqrt(max(Ec * Ec - m * m, 0.0))
+    return min(2.0 * K * L, max(L, Dc / a))
+
+
+def far_segment(p, m, a, slope, xc, xa, xb, v_w):
+    """Dressed-basis following from xa to xb on one side of crossing xc (no stepping): the
+    dressed amplitudes pick up exp(-+ i (Phi + (m^2 |alpha|/8) |int dD/E^5|)) over the segment
+    (the second-order dressed energy; the same terms as adiabatic_cell's tails)."""
+    Da, Db = slope * (xa - xc), slope * (xb - xc)
+    ddot = slope * v_w
+    lp, lm = dressed_basis(Da, ddot, m)
+    rp, rm = dressed_basis(Db, ddot, m)
+    bp, bm = np.vdot(lp, p), np.vdot(lm, p)
+    Phi = (wkb_G(a * (xb - xc), m) - wkb_G(a * (xa - xc), m)) / (a * v_w)
+    corr = m * m * a * v_w / 8.0 * abs(tail_T(Da, m) - tail_T(Db, m))
+    ph = Phi + corr
+    bp *= complex(math.cos(ph), -math.sin(ph))
+    bm *= complex(math.cos(ph), math.sin(ph))
+    return bp * rp + bm * rm
 
 
 def wkb_G(x, m):
@@ -113,6 +146,13 @@ def propagate(m_mix, dprime, xi, v_w, K, S, hybrid=True):
             left = right
             sgn = -sgn
             continue
+        cell_right = right
+        if hybrid:   # Magnus only on the cell's core; dressed following outside it
+            W = core_halfwidth(m_mix[c], ac, v_w, K)
+            cl, cr = max(left, xi[c] - W), min(right, xi[c] + W)
+            if left < cl:
+                p = far_segment(p, m_mix[c], ac, slope, xi[c], left, cl, v_w)
+            left, right = cl, cr
         Phi = (wkb_G(ac * (right - xi[c]), m_mix[c]) - wkb_G(ac * (left - xi[c]), m_mix[c])) / (ac * v_w)
         Sc = int(max(S, math.ceil(Phi * STEPS_PER_RADIAN))) if hybrid else S
         h = (right - left) / Sc
@@ -144,7 +184,9 @@ def propagate(m_mix, dprime, xi, v_w, K, S, hybrid=True):
             sx, sy, sz = sc * nx, sc * ny, sc * nz
             U = np.array([[cs - 1j * sz, -sy - 1j * sx], [sy - 1j * sx, cs + 1j * sz]])
             p = U @ p
-        left = right
+        if right < cell_right:
+            p = far_segment(p, m_mix[c], ac, slope, xi[c], right, cell_right, v_w)
+        left = right = cell_right
         sgn = -sgn
     slope = -sgn * abs(dprime[-1])
     u = chi_like_dressed(slope * (right - xi[-1]), slope * v_w, m_mix[-1])

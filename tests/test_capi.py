@@ -30,7 +30,7 @@ def test_library_builds_and_exports_header_symbols():
 def test_abi_version_and_struct_layout():
     n = pkg("_native")
     L = n.load()
-    assert L.lzq_abi_version() == 1
+    assert L.lzq_abi_version() == pkg("_native").ABI_VERSION == 1
     assert ctypes.sizeof(n.LzqPoint) == 136 and ctypes.sizeof(n.LzqYield) == 48
 
 

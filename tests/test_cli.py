@@ -110,3 +110,48 @@ def test_incoherent_composition():
     assert lz.p_incoherent([0.3]) == pytest.approx(0.3)
     assert lz.p_incoherent([0.5, 0.2, 0.9]) == pytest.approx(0.5)
     assert lz.p_incoherent([1.0, 1.0]) == pytest.approx(0.0)
+
+
+def test_plugin_profile_formats(tmp_path):
+    """plugins/transport_from_profile.py reads the two documented CSV formats (host logic;
+    the propagation itself is tests/test_gpu_plugin.py)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "tfp_cpu", os.path.join(os.path.dirname(os.path.dirname(__file__)), "plugins", "transport_from_profile.py"))
+    tfp = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(tfp)
+    (tmp_path / "a.csv").write_text("# window_lz = 30\n# v_w = 0.3\nxi,m_mix,dprime\n0,0.1,-1.0\n50,0.2,2.0\n")
+    xs, ms, ds, o = tfp.read_profile(str(tmp_path / "a.csv"))
+    assert xs == [0.0, 50.0] and ms == [0.1, 0.2] and ds == [1.0, 2.0]
+    assert o["window_lz"] == 30.0 and o["v_w"] == 0.3 and o["steps"] == 1000.0
+    # sampled profile: Delta = x - 1 on [0, 2] crosses once at x = 1, slope 1, m interpolated
+    rows = "".join(f"{x!r},{x - 1.0!r},{0.1 + 0.1 * x!r}\n" for x in (0.0, 0.5, 0.75, 1.25, 2.0))
+    (tmp_path / "b.csv").write_text("xi,Delta,m_mix\n" + rows)
+    xs, ms, ds, _ = tfp.read_profile(str(tmp_path / "b.csv"))
+    assert len(xs) == 1 and abs(xs[0] - 1.0) < 1e-15 and abs(ds[0] - 1.0) < 1e-15 and abs(ms[0] - 0.2) < 1e-15
+    # a sample exactly on the crossing, then a second crossing going down
+    (tmp_path / "c.csv").write_text("xi,Delta,m_mix\n-1,-1,0.1\n0,0,0.1\n1,1,0.1\n2,-1,0.3\n")
+    xs, ms, ds, _ = tfp.read_profile(str(tmp_path / "c.csv"))
+    assert xs == [0.0, 1.5] and ds == [1.0, 2.0] and ms == [0.1, 0.2]
+    for bad in ("xi,foo\n1,2\n", "xi,m_mix,dprime\n", "xi,m_mix,dprime\n1,0.1,1\n0,0.1,1\n",
+                "xi,Delta,m_mix\n0,1,0.1\n1,2,0.1\n"):
+        (tmp_path / "bad.csv").write_text(bad)
+        with pytest.raises(ValueError):
+            tfp.read_profile(str(tmp_path / "bad.csv"))
+
+
+def test_hook_does_not_mask_library_failures(monkeypatch, tmp_path):
+    """lz.py: a plug-in's own exception is swallowed (fpy:186-187), but a failure of lzq's
+    closed form (the HIP library) propagates instead of a silent fallback to the config P."""
+    lz = pkg("lz")
+    stub = types.ModuleType("lambda_local_LZ_from_profile")
+    stub.compute_lambda_eff_from_profile = lambda path: 0.01
+    monkeypatch.setitem(sys.modules, "lambda_local_LZ_from_profile", stub)
+
+    def broken(lam):
+        raise pkg("_native").LzqError(-2, "simulated HIP failure")
+    monkeypatch.setattr(lz, "p_closed_form", broken)
+    with pytest.raises(RuntimeError, match="simulated HIP failure"):
+        lz.try_compute_P_from_profile("x.csv", 0.3)
+    stub.compute_lambda_eff_from_profile = lambda path: 1 / 0
+    assert lz.try_compute_P_from_profile("x.csv", 0.3) is None

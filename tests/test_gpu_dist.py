@@ -1,0 +1,69 @@
+"""The real engine through the multi-rank path on one GPU: fresh child
+processes launched by torch.distributed.run, 2 ranks sharing cuda:0, gloo for the gather
+(RCCL refuses two ranks on one device; the 8-GPU RCCL run is the driver's).  Nothing in
+this module touches the GPU in the pytest process itself.
+
+- sweep.main over a 4096-point C3 slice at world_size 2 == the single-rank table, bit for
+  bit (each point is reduced by one wavefront, so sharding cannot change a result);
+- bench.py under torchrun with --dist-backend gloo emits one valid JSON line whose value
+  counts both ranks' points.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import PKG_NAME, ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def run(cmd, timeout):
+    env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, (cmd, r.stdout[-3000:], r.stderr[-3000:])
+    return r.stdout
+
+
+def torchrun(n):
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+            "--master-addr", "127.0.0.1", "--master-port", str(free_port())]
+
+
+def test_sweep_two_ranks_bit_identical_to_one(tmp_path):
+    args = ["--spec", "C3", "--limit", "4096", "--chunk", "1500"]
+    one, two = tmp_path / "w1", tmp_path / "w2"
+    run([sys.executable, "-m", PKG_NAME + ".sweep", *args, "--out", str(one)], 300)
+    out = run(torchrun(2) + ["-m", PKG_NAME + ".sweep", *args, "--out", str(two), "--dist-backend", "gloo"], 300)
+    t1, t2 = np.load(one / "table.npy"), np.load(two / "table.npy")
+    assert t1.shape == (4096, 6) and np.isfinite(t1).all()
+    assert np.array_equal(t1, t2)
+    line = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["n_points"] == 4096
+    # both ranks checkpointed their own chunks: rank 0 [0, 2048), rank 1 [2048, 4096)
+    starts = sorted(int(f.split("_")[2]) for f in os.listdir(two) if f.startswith("shard_"))
+    assert starts == [0, 1500, 2048, 3548]
+
+
+def test_bench_two_ranks_gloo():
+    out = run(torchrun(2) + ["bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1", "--points", "20000",
+                             "--dist-backend", "gloo"], 300)
+    recs = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+    assert len(recs) == 1
+    r = recs[0]
+    assert r["n_gpus"] == 2 and r["config"]["global_points_per_step"] == 40000
+    assert r["value"] > 0 and r["unit"] == "points/s" and r["scaling"] == "weak"
+    assert abs(r["value"] - 40000 / (r["ms_per_step"] / 1e3)) <= 1e-6 * r["value"]
+    assert "cpu_baseline" not in r   # rank 0 at N = 1 only

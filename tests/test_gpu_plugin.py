@@ -1,0 +1,157 @@
+"""The LZ plug-in path end to end on the GPU (fpy:170-187, 317-328):
+
+- lzq's driver with the reference's own stub-module cases (golden_cli_profile.json, made by
+  running the reference CLI with those stubs on PYTHONPATH): stdout byte-identical,
+  yields_out.json finals within 1e-11;
+- the shipped plug-in module plugins/transport_from_profile.py picked up by the hook in the
+  fpy:173 order: a one-crossing CSV reproduces P = 1 - exp(-2 pi delta) (eq.(9)) to 1e-8, a
+  multi-crossing list gives the propagator's coherent P, a sampled bounce profile
+  (xi, Delta, m_mix) is reduced to its crossings, and the CLI prints the reference's
+  `[info] Using P_chi_to_B from profile: ...` line byte-exactly for that P;
+- plugins/lzq_binding.py (the reference-side ctypes binding, no torch): the quadrature
+  operator on a stand-in with the reference BoltzmannSystem's attributes (self.cfg, self.P,
+  fpy:193-196) against the oracle, and its closed form against golden_lz.json.
+"""
+import importlib
+import json
+import math
+import os
+import sys
+import types
+
+import numpy as np
+import pytest
+
+from conftest import BASE_CFG, ROOT, full_cfg, golden, pkg, rel_err
+from oracle import oracle as O
+from test_cli import run_cli
+
+pytestmark = pytest.mark.gpu
+PLUGINS = os.path.join(ROOT, "plugins")
+V_W = 0.30
+
+
+@pytest.fixture
+def plugin_path(monkeypatch):
+    monkeypatch.syspath_prepend(PLUGINS)
+    for m in ("transport_from_profile", "extended_LZ_lambda", "lambda_local_LZ_from_profile"):
+        monkeypatch.delitem(sys.modules, m, raising=False)
+    yield PLUGINS
+    for m in ("transport_from_profile", "extended_LZ_lambda", "lambda_local_LZ_from_profile"):
+        sys.modules.pop(m, None)
+
+
+def equal_mass_cfg(tmp_path):
+    txt = next(c for c in golden("golden_cli.json") if c["name"] == "equal_mass")["config_text"]
+    (tmp_path / "cfg.json").write_text(txt)
+    return "cfg.json"
+
+
+@pytest.mark.parametrize("case", golden("golden_cli_profile.json"), ids=lambda c: c["name"])
+def test_cli_profile_stubs_match_reference(case, tmp_path, monkeypatch, gpu_engine):
+    plug = tmp_path / "plug"
+    plug.mkdir()
+    for mod, src in zip(case["modules"], case["module_sources"]):
+        (plug / (mod + ".py")).write_text(src)
+        monkeypatch.delitem(sys.modules, mod, raising=False)
+    monkeypatch.syspath_prepend(str(plug))
+    importlib.invalidate_caches()
+    (tmp_path / "bounce.csv").write_text("xi,m_mix,dprime\n0.0,0.1,1.0\n")
+    out = run_cli(["--config", equal_mass_cfg(tmp_path)] + case["flags"], tmp_path)
+    for mod in case["modules"]:
+        sys.modules.pop(mod, None)
+    assert out == case["stdout"]
+    ref = json.loads(case["yields_out_json"])
+    ours = json.loads((tmp_path / "yields_out.json").read_text())
+    assert ours["inputs"] == ref["inputs"]
+    for k, v in ref["final"].items():
+        assert rel_err(ours["final"][k], v) < 1e-11, (k, ours["final"][k], v)
+
+
+def test_shipped_module_single_crossing_closed_form(tmp_path, plugin_path, gpu_engine):
+    tfp = importlib.import_module("transport_from_profile")
+    assert tfp.__file__.startswith(PLUGINS)
+    worst = 0.0
+    for m, d in [(0.1, 1.0), (0.03, 0.01), (0.3, 0.5), (1e-3, 1e-3), (0.5, 10.0), (0.2, 0.05)]:
+        p = tmp_path / "one.csv"
+        p.write_text(f"# one crossing\nxi,m_mix,dprime\n1.5,{m!r},{-d!r}\n")
+        delta = m * m / (2 * V_W * d)
+        P9 = 1.0 - math.exp(-2.0 * math.pi * delta)           # fpy:183-184 / PAPER eq.(9)
+        P = tfp.compute_prob_from_profile(str(p), V_W)
+        worst = max(worst, abs(P - P9) / P9)
+        assert abs(P - P9) <= 1e-8 * P9, (m, d, P, P9)
+        (tmp_path / "lam.csv").write_text(f"# v_w = {V_W!r}\nxi,m_mix,dprime\n0.0,{m!r},{d!r}\n")
+        assert tfp.compute_lambda_eff_from_profile(str(tmp_path / "lam.csv")) == delta   # eq.(8) exactly
+    print(f"one-crossing CSV vs eq.(9): worst rel err {worst:.2e}")
+
+
+def test_shipped_module_multi_crossing_and_profile(tmp_path, plugin_path, gpu_engine):
+    from lz_ref import propagate
+    tfp = importlib.import_module("transport_from_profile")
+    m, d, x = [0.05, 0.08, 0.04], [0.5, 0.3, 0.7], [0.0, 60.0, 110.0]
+    (tmp_path / "list.csv").write_text("xi,m_mix,dprime\n" + "".join(f"{a!r},{b!r},{c!r}\n" for a, b, c in zip(x, m, d)))
+    P = tfp.compute_prob_from_profile(str(tmp_path / "list.csv"), V_W)
+    eng = gpu_engine.lz_propagate([m], [d], [x], V_W, 20.0, 1000).cpu().numpy()[0]
+    assert P == eng                                               # same kernel, same arrays
+    assert abs(P - propagate(m, d, x, V_W, 20.0, 1000)) <= 1e-10
+    # a sampled bounce profile with the same three crossings: Delta piecewise linear through
+    # them (slopes +0.5, -0.3, +0.7), m_mix constant per crossing neighbourhood
+    xs = np.linspace(-40.0, 150.0, 3801)
+    D = np.where(xs < 22.5, 0.5 * (xs - 0.0), np.where(xs < 95.0, -0.3 * (xs - 60.0), 0.7 * (xs - 110.0)))
+    # Delta is continuous at the joins, which are the model's turning points
+    assert abs(0.5 * 22.5 - (-0.3) * (22.5 - 60.0)) < 1e-12 and abs(-0.3 * (95.0 - 60.0) - 0.7 * (95.0 - 110.0)) < 1e-12
+    mm = np.where(xs < 22.5, 0.05, np.where(xs < 95.0, 0.08, 0.04))
+    (tmp_path / "prof.csv").write_text("xi,Delta,m_mix\n" + "".join(f"{float(a)!r},{float(b)!r},{float(c)!r}\n" for a, b, c in zip(xs, D, mm)))
+    xc, mc, dc, _ = tfp.read_profile(str(tmp_path / "prof.csv"))
+    assert np.allclose(xc, x, atol=1e-9) and np.allclose(mc, m) and np.allclose(dc, d, rtol=1e-9)
+    P2 = tfp.compute_prob_from_profile(str(tmp_path / "prof.csv"), V_W)
+    assert abs(P2 - P) <= 1e-9
+
+
+def test_cli_picks_up_shipped_module(tmp_path, plugin_path, gpu_engine):
+    """fpy:173 order with the shipped module: transport_from_profile is found on sys.path,
+    its P drives the run, and the info line is the reference's format (fpy:322)."""
+    m, d = 0.1, 1.0
+    (tmp_path / "bounce.csv").write_text(f"xi,m_mix,dprime\n0.0,{m!r},{d!r}\n")
+    tfp = importlib.import_module("transport_from_profile")
+    P = tfp.compute_prob_from_profile(str(tmp_path / "bounce.csv"), V_W)
+    out = run_cli(["--config", equal_mass_cfg(tmp_path), "--maybe-compute-P-from-profile", "bounce.csv"], tmp_path)
+    assert out.splitlines()[0] == f"[info] Using P_chi_to_B from profile: {P:.6g}"
+    yo = json.loads((tmp_path / "yields_out.json").read_text())
+    assert yo["inputs"]["P_used"] == P
+    ref = O.point_yields(full_cfg({**BASE_CFG, "P_chi_to_B": P}))
+    assert rel_err(yo["final"]["Y_B"], ref["Y_B"]) < 1e-11
+    # an earlier module in the search order wins over the shipped one
+    stub = types.ModuleType("extended_LZ_lambda")
+    stub.compute_prob_from_profile = lambda path, v_w: 0.125
+    sys.modules["extended_LZ_lambda"] = stub
+    try:
+        assert pkg("lz").try_compute_P_from_profile(str(tmp_path / "bounce.csv"), V_W) == 0.125
+    finally:
+        del sys.modules["extended_LZ_lambda"]
+
+
+def test_reference_side_binding(plugin_path, gpu_engine):
+    B = importlib.import_module("lzq_binding")
+    cfgm = pkg("config")
+
+    class StandIn:  # the attributes of the reference's BoltzmannSystem that the binding reads (fpy:193-196)
+        def __init__(self, cfg, P):
+            self.cfg, self.P = cfg, float(P)
+
+    ns = types.SimpleNamespace(BoltzmannSystem=StandIn)
+    B.install(ns)
+    cfg = cfgm.Config(**full_cfg(BASE_CFG))
+    bs = ns.BoltzmannSystem(cfg, cfg.P_chi_to_B)
+    p = O.point_from_config(full_cfg(BASE_CFG))
+    import ctypes
+    for (tlo, thi, ny) in ((0.1, 500.0, 8000), (60.0, 150.0, 2000), (90.0, 110.0, 6000)):
+        got = bs.integrate_YB_by_quadrature(tlo, thi, n_y=ny)
+        ref = O.lib().oracle_yb_quadrature(ctypes.byref(p), tlo, thi, ny)
+        assert rel_err(got, ref) < 1e-11, (tlo, thi, ny, got, ref)
+    y = B.yields(cfg, cfg.P_chi_to_B)
+    assert f"{y['Y_B']:.10e}" == "8.7208853627e-11"
+    d = golden("golden_lz.json")
+    lam = [float(s) for s in d["lambda"]]
+    for l, g, r in zip(lam, B.p_closed_form(lam), d["P"]):
+        assert abs(g - r) <= 1e-8 * abs(r) + 4.5e-16, (l, g, r)

@@ -104,11 +104,15 @@ def test_c5_multicrossing_pipeline(gpu_engine):
 def test_sweep_cli_end_to_end(tmp_path, gpu_engine):
     import json
     sw = pkg("sweep")
-    sw.main(["--spec", "C2", "--limit", "2048", "--chunk", "700", "--out", str(tmp_path)])
-    tab = np.load(tmp_path / "table.npy")
-    summ = json.loads((tmp_path / "summary.json").read_text())
+    out = tmp_path / "new_subdir"        # main() must create --out itself
+    sw.main(["--spec", "C2", "--limit", "2048", "--chunk", "700", "--out", str(out)])
+    tab = np.load(out / "table.npy")
+    summ = json.loads((out / "summary.json").read_text())
     assert tab.shape == (2048, 6) and summ["n_points"] == 2048
     ref = gpu_engine.sweep(sw.EQUAL_MASS, sw.builtin_specs()["C2"].axes, 0, 2048).cpu().numpy()
     assert np.array_equal(tab, ref)
-    sw.main(["--spec", "C2", "--limit", "2048", "--chunk", "700", "--out", str(tmp_path), "--resume"])
-    assert np.array_equal(np.load(tmp_path / "table.npy"), ref)
+    sw.main(["--spec", "C2", "--limit", "2048", "--chunk", "700", "--out", str(out), "--resume"])
+    assert np.array_equal(np.load(out / "table.npy"), ref)
+    # resuming another spec into the same directory is refused, not mixed
+    with pytest.raises(RuntimeError, match="another sweep"):
+        sw.main(["--spec", "C3", "--limit", "2048", "--chunk", "700", "--out", str(out), "--resume"])

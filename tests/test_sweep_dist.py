@@ -102,3 +102,34 @@ def test_summary_fixed_order():
     s1 = sw.summarize(t, spec)
     s2 = sw.summarize(t.copy(), spec)
     assert s1 == s2 and set(s1["final"]) == set(pkg("_native").YIELD_FIELDS)
+
+
+def test_out_dir_manifest_and_foreign_resume(tmp_path):
+    """--out is created if missing; shard names carry the sweep's key; --resume into a
+    directory written by another sweep definition refuses instead of mixing tables."""
+    sw = pkg("sweep")
+    specs = sw.builtin_specs()
+    out = tmp_path / "new" / "dir"
+    k2 = sw.prepare_out_dir(str(out), specs["C2"], resume=False)
+    assert (out / "manifest.json").exists() and len(k2) == 16
+    assert sw.prepare_out_dir(str(out), specs["C2"], resume=True) == k2   # same sweep: fine
+    with pytest.raises(RuntimeError, match="another sweep"):
+        sw.prepare_out_dir(str(out), specs["C3"], resume=True)
+    # the key depends on everything a shard's rows depend on
+    c2b = sw.SweepSpec("C2", dict(specs["C2"].base, I_p=0.5), specs["C2"].axes)
+    assert sw.spec_key(c2b) != k2 and sw.spec_key(specs["C5"]) != k2
+    assert sw.spec_key(sw.SweepSpec("C2", specs["C2"].base, specs["C2"].axes, notes="x")) == k2
+    # shards of one key are invisible to a run with another key
+    loc = sw.run_local(fake_compute, 0, 10, lambda n: torch.empty((n, 6), dtype=torch.float64), 4, str(out), key=k2)
+    names = sorted(os.listdir(out))
+    assert all(n.startswith(f"shard_{k2}_") for n in names if n.startswith("shard_"))
+
+    def boom(*a):
+        raise AssertionError("recomputed")
+    again = sw.run_local(boom, 0, 10, lambda n: torch.empty((n, 6), dtype=torch.float64), 4, str(out),
+                         resume=True, key=k2)
+    assert torch.equal(again, loc)
+    seen = []
+    sw.run_local(lambda s, n, o: (seen.append(s), fake_compute(s, n, o)), 0, 10,
+                 lambda n: torch.empty((n, 6), dtype=torch.float64), 4, str(out), resume=True, key="other")
+    assert seen == [0, 4, 8]

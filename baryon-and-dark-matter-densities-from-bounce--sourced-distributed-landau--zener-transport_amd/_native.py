@@ -66,8 +66,10 @@ ABI_VERSION = 1  # LZQ_ABI_VERSION (tests/test_capi.py checks it against the lib
 # Symbols declared in include/lzq.h (checked by tests/test_capi.py against the header).
 EXPORTS = ("lzq_abi_version", "lzq_last_error", "lzq_init", "lzq_ztables", "lzq_tune", "lzq_aov_batch",
            "lzq_jchi_batch", "lzq_yields_batch", "lzq_sweep_grid", "lzq_p_closed_form",
-           "lzq_lz_propagate", "lzq_ode_tables", "lzq_ode_integrate", "lzq_ode_batch", "lzq_ode_aov_T",
-           "lzq_ode_rhs")
+           "lzq_lz_propagate", "lzq_ode_tables", "lzq_ode_integrate", "lzq_ode_integrate_shared", "lzq_ode_batch",
+           "lzq_ode_aov_T", "lzq_ode_rhs")
+# the lzq_point fields an ODE spline table depends on (A/V kernel fpy:141-156 + window fpy:368-369)
+ODE_TABLE_KEY = ("I_p", "beta_over_H", "T_p_GeV", "v_w", "g_star", "T_min_over_Tp", "T_max_over_Tp")
 
 
 class LzqError(RuntimeError):
@@ -106,6 +108,7 @@ def load(path: str | None = None):
     L.lzq_lz_propagate.argtypes = [vp, vp, vp, i64, i32, d, d, i32, vp, vp]
     L.lzq_ode_tables.argtypes = [vp, i64, vp, vp, vp, i64, vp, vp]
     L.lzq_ode_integrate.argtypes = [vp, vp, i64, vp, i64, i64, vp, vp, vp]
+    L.lzq_ode_integrate_shared.argtypes = [vp, vp, i64, vp, i64, vp, i64, i64, vp, vp, vp]
     L.lzq_ode_batch.argtypes = [vp, vp, i64, vp, i64, i64, vp, vp, vp]
     L.lzq_ode_aov_T.argtypes = [P(LzqPoint), d, d, vp, vp, i64, vp, vp]
     L.lzq_ode_rhs.argtypes = [P(LzqPoint), P(LzqOdeParams), d, d, vp, vp, vp, i64, vp, vp]

@@ -45,6 +45,7 @@ struct OdePoint {
   int deplete;
   double T_lo, T_hi, stepT;
   double inv_m, inv_sig, inv_v0, inv_stepT;  // reciprocals: ode_stage multiplies instead of dividing
+  double inv_s0, mpl_over_h0;                // 1/s0, M_Pl/H0 (1/s and 1/(H x) as products)
 };
 
 __device__ __forceinline__ void ode_point_recips(OdePoint& o) {
@@ -52,6 +53,8 @@ __device__ __forceinline__ void ode_point_recips(OdePoint& o) {
   o.inv_sig = 1.0 / o.sig;
   o.inv_v0 = 1.0 / o.v0;
   o.inv_stepT = 1.0 / o.stepT;
+  o.inv_s0 = 1.0 / o.s0;
+  o.mpl_over_h0 = kMplGeV / o.H0;
 }
 
 __device__ __forceinline__ OdePoint ode_point(const lzq_point& pt, const lzq_ode_params& od) {
@@ -110,11 +113,15 @@ struct OdeStage {
 
 __device__ __forceinline__ OdeStage ode_stage(const OdePoint& o, const double* __restrict__ w, double x,
                                               double* Av_out = nullptr) {
-  // Three divisions per call (1/x, 1/s, 1/(H x)); every other quotient of fpy:270-286 is a
-  // product with a per-point reciprocal.  Each such product differs from the quotient by at
-  // most 1 ulp, far inside the 1e-11 oracle gate (tests/test_gpu_ode.py).
+  // One division per call (1/x); every other quotient of fpy:270-286 is a product with a
+  // per-point reciprocal or with powers of 1/T: 1/s = (1/T)^3 / s0 and 1/(H x) =
+  // (M_Pl/H0) (1/T)^2 / x, exact rewrites of s = s0 T^3 and H = H0 T^2 / M_Pl (fpy:85, 88)
+  // wherever the max(., 1e-300) guards are inactive (T > 1e-30 GeV: always on the ODE window;
+  // the guarded branch divides).  Each product differs from the quotient by a few ulp, far
+  // inside the 1e-11 oracle gate (tests/test_gpu_ode.py).
   const double xc = pymax(x, 1e-30);
-  const double T = o.m * (1.0 / xc);                          // fpy:272  m / max(x, 1e-30)
+  const double ixc = 1.0 / xc;
+  const double T = o.m * ixc;                                 // fpy:272  m / max(x, 1e-30)
   const double iT = T >= 1e-30 ? xc * o.inv_m : 1e30;         // 1 / max(T, 1e-30)
   const double H = pymax(o.H0 * T * T * kInvMplGeV, 1e-300);  // fpy:273 via fpy:85
   const double T3 = (T * T) * T;
@@ -135,10 +142,12 @@ __device__ __forceinline__ OdeStage ode_stage(const OdePoint& o, const double* _
   const double Av = spline_eval(o, w, T);                     // fpy:214-218
   if (Av_out) *Av_out = Av;
   const double SB = o.P * J * Av * window;                    // fpy:277
-  const double is = 1.0 / s;
+  const bool plain = H > 1e-290 && s > 1e-290 && x == xc;     // the max() guards are inactive
+  const double iT2 = iT * iT;
+  const double is = plain ? (iT2 * iT) * o.inv_s0 : 1.0 / s;
   const double E = n_eq * is;                                 // fpy:280
   const double SBs = SB * is;
-  const double iHx = 1.0 / (H * x);
+  const double iHx = plain ? (o.mpl_over_h0 * iT2) * ixc : 1.0 / (H * x);
   OdeStage st;
   st.lam = (o.sigmav * s) * iHx;
   st.E2 = E * E;
@@ -218,6 +227,19 @@ __device__ __forceinline__ void solve3(double M[3][3], double b[3]) {
   }
 }
 
+// z[2] of M z = b by Cramer's rule (one division): the Y_B stage system needs only the last
+// stage.  M = I + h A diag(beta), beta >= 0, is well conditioned for every h (A of Radau IIA
+// has eigenvalues in the right half plane), so the cofactor form loses nothing against the
+// pivoted elimination of solve3 (tests/test_gpu_ode.py: oracle at 1e-11).
+__device__ __forceinline__ double solve3_last(const double (&M)[3][3], const double (&b)[3]) {
+  const double c0 = M[1][0] * M[2][1] - M[1][1] * M[2][0];
+  const double det = M[0][0] * (M[1][1] * M[2][2] - M[1][2] * M[2][1]) -
+                     M[0][1] * (M[1][0] * M[2][2] - M[1][2] * M[2][0]) + M[0][2] * c0;
+  const double num = M[0][0] * (M[1][1] * b[2] - b[1] * M[2][1]) - M[0][1] * (M[1][0] * b[2] - b[1] * M[2][0]) +
+                     b[0] * c0;
+  return num / det;
+}
+
 // One Radau step of size h for both equations; false when the Y_chi Newton iteration fails.
 __device__ __forceinline__ bool radau_step(const Radau& R, const OdeStage (&st)[3], double h, double& Ychi,
                                            double& YB) {
@@ -234,8 +256,7 @@ __device__ __forceinline__ bool radau_step(const Radau& R, const OdeStage (&st)[
       }
       b[i] = acc;
     }
-    solve3(M, b);
-    YB = b[2];
+    YB = solve3_last(M, b);
   }
   // Y_chi: Z_i = Y + h sum_j a_ij f_j(Z_j), f_j(Z) = -lam_j (Z^2 - E2_j) - S_j
   const bool nonlinear = st[0].lam != 0.0 || st[1].lam != 0.0 || st[2].lam != 0.0;
@@ -359,8 +380,26 @@ __global__ __launch_bounds__(kOdeBlock) void ode_spline_kernel(const lzq_point* 
 }
 
 // fpy:385-417 on the ODE path, one lane per point.
+// The first x in (x0, x1) at which ode_stage's T = m * (1/x) is no longer > m/3 (the branch of
+// n_chi_eq / vbar_chi, fpy:100, 111), +inf if there is none: a few ulp steps from m/(m/3).
+__device__ __forceinline__ double branch_x(const OdePoint& o, double x0, double x1) {
+  auto rel = [&](double x) { return o.m * (1.0 / pymax(x, 1e-30)) > o.m3; };
+  double xg = o.m / o.m3;
+  if (!(xg > x0 && xg < x1 + 1.0)) return INFINITY;
+  int guard = 0;
+  if (rel(xg)) {
+    while (rel(xg) && ++guard < 64) xg = nextafter(xg, INFINITY);
+  } else {
+    while (!rel(nextafter(xg, -INFINITY)) && ++guard < 64) xg = nextafter(xg, -INFINITY);
+  }
+  return (x0 < xg && xg < x1) ? xg : INFINITY;
+}
+
+// tidx (optional): point i reads the spline table at ws[tidx[i] * kOdeWS] (tables shared by
+// points with the same A/V kernel and window, lzq_ode_integrate_shared); NULL: its own, ws[i].
 __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_kernel(const lzq_point* __restrict__ pts,
                                                                   const lzq_ode_params* __restrict__ ode, int64_t n,
+                                                                  const int32_t* __restrict__ tidx,
                                                                   const double* __restrict__ ws, int64_t max_steps,
                                                                   lzq_yield* __restrict__ out,
                                                                   int32_t* __restrict__ status) {
@@ -368,7 +407,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
   if (i >= n) return;
   const lzq_point pt = pts[i];
   const OdePoint o = ode_point(pt, ode[i]);
-  const double* w = ws + i * (int64_t)kOdeWS;
+  const double* w = ws + (tidx ? (int64_t)tidx[i] : i) * (int64_t)kOdeWS;
   const double nan = __builtin_nan("");
   lzq_yield r = {nan, nan, nan, nan, nan, pt.P_chi_to_B};
   int st = ode_grid_ok(o.T_lo, o.T_hi, o.stepT) ? LZQ_ODE_OK : LZQ_ODE_BAD_GRID;
@@ -397,13 +436,33 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
     const int64_t N = (int64_t)steps;
     const double h = (x1 - x0) / (double)N;
     const Radau R = radau_tableau();
+    // n_chi_eq / vbar_chi switch formula at the strict T > m/3 (fpy:100, 111): the rhs jumps at
+    // the first x whose T (ode_stage's m * (1/x)) is not > m/3.  The step that straddles it is
+    // split there, ending one ulp before it, so no stage sees both branches (the oracle does
+    // the same with its own T; tests/golden/golden_ode_stiff.json).
+    const double xb = branch_x(o, x0, x1);
     for (int64_t k = 0; k < N; ++k) {
       const double xk = x0 + (double)k * h;
-      OdeStage sg[3];
+      const bool split = xk < xb && xb <= xk + h;  // the last stage (x = xk + h) would see the other branch
+      const double xa = split ? nextafter(xb, -INFINITY) : xk + h;
+      double YB_prev = YB;
+      bool ok = true;
+      if (xa > xk) {
+        const double hs = xa - xk;
+        OdeStage sg[3];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) sg[j] = ode_stage(o, w, xk + R.c[j] * h);
-      const double YB_prev = YB;
-      if (!radau_step(R, sg, h, Ychi, YB)) {
+        for (int j = 0; j < 3; ++j) sg[j] = ode_stage(o, w, xk + R.c[j] * (split ? hs : h));
+        ok = radau_step(R, sg, split ? hs : h, Ychi, YB);
+      }
+      if (ok && split && xk + h > xb) {
+        const double hs = (xk + h) - xb;
+        OdeStage sg[3];
+        YB_prev = YB;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) sg[j] = ode_stage(o, w, xb + R.c[j] * hs);
+        ok = radau_step(R, sg, hs, Ychi, YB);
+      }
+      if (!ok) {
         YB = YB_prev;  // report the state at the start of the failed step, like sol.y[:, -1] (fpy:408-410)
         st = LZQ_ODE_NEWTON;
         break;
@@ -506,8 +565,25 @@ int lzq_ode_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, in
   if (max_steps < 0) return lzq_set_error(LZQ_EINVAL, "lzq_ode_integrate: max_steps < 0");
   if (n == 0) return LZQ_OK;
   hipLaunchKernelGGL(lzq::ode_integrate_kernel, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0,
-                     (hipStream_t)stream, d_points, d_ode, n, d_work, max_steps, d_out, d_status);
+                     (hipStream_t)stream, d_points, d_ode, n, (const int32_t*)nullptr, d_work, max_steps, d_out,
+                     d_status);
   return hip_check(hipGetLastError(), "lzq_ode_integrate");
+}
+
+int lzq_ode_integrate_shared(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n,
+                             const int32_t* d_table_index, int64_t n_tables, const double* d_work,
+                             int64_t work_doubles, int64_t max_steps, lzq_yield* d_out, int32_t* d_status,
+                             void* stream) {
+  if (n < 0 || n_tables < 0 || (n > 0 && (!d_points || !d_ode || !d_out || !d_table_index || n_tables == 0)))
+    return lzq_set_error(LZQ_EINVAL, "lzq_ode_integrate_shared: bad arguments");
+  int rc = check_ws(n_tables, d_work, work_doubles, "lzq_ode_integrate_shared");
+  if (rc) return rc;
+  if (max_steps < 0) return lzq_set_error(LZQ_EINVAL, "lzq_ode_integrate_shared: max_steps < 0");
+  if (ode_blocks(n) > 2147483647LL) return lzq_set_error(LZQ_EINVAL, "lzq_ode_integrate_shared: n too large");
+  if (n == 0) return LZQ_OK;
+  hipLaunchKernelGGL(lzq::ode_integrate_kernel, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0,
+                     (hipStream_t)stream, d_points, d_ode, n, d_table_index, d_work, max_steps, d_out, d_status);
+  return hip_check(hipGetLastError(), "lzq_ode_integrate_shared");
 }
 
 int lzq_ode_batch(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, double* d_work,

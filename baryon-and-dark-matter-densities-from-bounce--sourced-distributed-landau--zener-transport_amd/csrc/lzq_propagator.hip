@@ -164,7 +164,11 @@ __device__ __forceinline__ void cos_sinc(double x2, double& cs, double& sc) {
 // dressed-following error is set by the distance in LZ lengths: ~1e-12 at 40); for delta > 1
 // out to |D| where eps = m|alpha|/(4E^3) = kCoreEps (following error ~eps^2), clamped to
 // [1, 2K] LZ lengths.
+#ifndef LZQ_PROP_CORE
+#define LZQ_PROP_CORE 1  // 0: Magnus over every whole cell (round-1 scheme; tools/ablate_prop.py)
+#endif
 __device__ __forceinline__ double core_halfwidth(double m, double a, double v_w, double K) {
+  if (!LZQ_PROP_CORE) return INFINITY;
   const double L = lz_length(m, a, v_w);
   if (m * m <= 2.0 * v_w * a) return 2.0 * K * L;
   const double Ec = cbrt(m * a * v_w / (4.0 * kCoreEps));

@@ -146,11 +146,15 @@ class Engine:
                                                 self._stream()))
         return work, status
 
-    def ode(self, points, ode_params, max_steps: int = 1 << 26, chunk: int = 1 << 18) -> tuple:
+    def ode(self, points, ode_params, max_steps: int = 1 << 26, chunk: int = 1 << 18,
+            share_tables: bool = True) -> tuple:
         """fpy:385-417 for n points (POINT_DTYPE records + ODE_DTYPE records): (n, 6) yields
         table and (n,) int32 status (enum lzq_ode_status), both on the device.  Points are
         processed in chunks so that the spline workspace stays <= chunk * 25.6 KB (6.7 GB at the
-        default 2^18 points: 2 waves/SIMD on all 1024 SIMDs need >= 131072 points per launch)."""
+        default 2^18 points: 2 waves/SIMD on all 1024 SIMDs need >= 131072 points per launch).
+        share_tables: points equal in the fields the A/V spline depends on (ODE_TABLE_KEY) share
+        one table (lzq_ode_integrate_shared; bit-identical results, one A/V table per distinct
+        kernel instead of per point)."""
         pts = np.ascontiguousarray(points, dtype=_native.POINT_DTYPE).reshape(-1)
         ods = np.ascontiguousarray(ode_params, dtype=_native.ODE_DTYPE).reshape(-1)
         if pts.size != ods.size:
@@ -158,16 +162,37 @@ class Engine:
         n = pts.size
         out = torch.empty((n, 6), dtype=torch.float64, device=self.device)
         status = torch.zeros(n, dtype=torch.int32, device=self.device)
-        work = self.ode_workspace(min(n, chunk)) if n else None
+        work = None
+        keep = []
         for c0 in range(0, n, chunk):
             c1 = min(n, c0 + chunk)
-            d_pts = self.points_to_device(pts[c0:c1])
+            p = pts[c0:c1]
+            d_pts = self.points_to_device(p)
             d_ode = torch.from_numpy(ods[c0:c1].view(np.uint8).copy()).to(self.device)
+            rep = table_groups(d_pts, c1 - c0) if share_tables else None
+            if rep is not None:
+                rep, inv = rep
+            n_tab = (c1 - c0) if rep is None else rep.numel()
+            if work is None or work.numel() < n_tab * _native.ODE_WS_PER_POINT:
+                work = self.ode_workspace(max(n_tab, min(n, chunk) if rep is None else n_tab))
             with torch.cuda.device(self.device):
-                self._check(self.lib.lzq_ode_batch(_vp(d_pts), _vp(d_ode), c1 - c0, _vp(work), work.numel(),
-                                                   int(max_steps), _vp(out[c0:c1]), _vp(status[c0:c1]),
-                                                   self._stream()))
-            self._keepalive = (d_pts, d_ode)
+                if rep is None:
+                    self._check(self.lib.lzq_ode_batch(_vp(d_pts), _vp(d_ode), c1 - c0, _vp(work), work.numel(),
+                                                       int(max_steps), _vp(out[c0:c1]), _vp(status[c0:c1]),
+                                                       self._stream()))
+                else:
+                    rec = _native.POINT_DTYPE.itemsize
+                    d_rep = d_pts.view(c1 - c0, rec)[rep].contiguous()
+                    d_idx = inv.to(torch.int32)
+                    self._check(self.lib.lzq_ode_tables(_vp(d_rep), n_tab, None, None, _vp(work), work.numel(),
+                                                        None, self._stream()))
+                    self._check(self.lib.lzq_ode_integrate_shared(_vp(d_pts), _vp(d_ode), c1 - c0, _vp(d_idx),
+                                                                  n_tab, _vp(work), work.numel(), int(max_steps),
+                                                                  _vp(out[c0:c1]), _vp(status[c0:c1]),
+                                                                  self._stream()))
+                    keep.append((d_rep, d_idx))
+            keep.append((d_pts, d_ode))
+        self._keepalive = (keep, work)
         return out, status
 
     def ode_aov_T(self, point, T_lo: float, T_hi: float, work_point: torch.Tensor, Ts) -> torch.Tensor:
@@ -217,6 +242,36 @@ class Engine:
                                                     float(window_lz), int(steps_per_crossing), _vp(out),
                                                     self._stream()))
         return out
+
+
+_MIX = -7046029254386353131  # 0x9E3779B97F4A7C15 as int64 (torch multiplies wrap)
+_KEY_WORDS = [_native.POINT_DOUBLE_FIELDS.index(f) for f in _native.ODE_TABLE_KEY]  # 8-byte words of lzq_point
+
+
+def table_groups(d_pts: torch.Tensor, n: int):
+    """Points (device lzq_point records) that can share one ODE spline table: equal, bit for
+    bit, in _native.ODE_TABLE_KEY.  Returns (representative indices, per-point table index),
+    both int64 device tensors, or None when sharing would not pay (more than half the points
+    distinct).  Index bookkeeping on the device: a 64-bit mix of the key words is deduplicated
+    and every point's key is then compared with its representative's, so a hash collision only
+    costs the sharing, never a wrong table."""
+    if n < 2:
+        return None
+    key = d_pts.view(n, _native.POINT_DTYPE.itemsize).view(torch.int64)[:, _KEY_WORDS]
+    if bool((key == key[0]).all()):
+        z = torch.zeros(n, dtype=torch.int64, device=d_pts.device)
+        return z[:1], z
+    h = key[:, 0].clone()
+    for j in range(1, key.shape[1]):
+        h = (h * _MIX) ^ key[:, j]
+    u, inv = torch.unique(h, return_inverse=True)
+    if u.numel() * 2 > n:
+        return None
+    ar = torch.arange(n, dtype=torch.int64, device=d_pts.device)
+    first = torch.full((u.numel(),), n, dtype=torch.int64, device=d_pts.device).scatter_reduce_(0, inv, ar, "amin")
+    if not bool((key[first][inv] == key).all()):
+        return None
+    return first, inv
 
 
 _default: Optional[Engine] = None

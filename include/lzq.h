@@ -10,6 +10,7 @@
  *   fpy:222-223 + fpy:122-123  J_chi (diagnostics)     -> lzq_jchi_batch
  *   (no reference counterpart; north_star (1))        -> lzq_lz_propagate
  *   fpy:200-219, 270-286, 385-417  ODE fallback        -> lzq_ode_tables / _integrate / _batch,
+ *                                                         lzq_ode_integrate_shared,
  *                                                         lzq_ode_aov_T, lzq_ode_rhs
  *
  * Conventions (all entry points):
@@ -197,6 +198,18 @@ int lzq_ode_tables(const lzq_point* d_points, int64_t n, const double* d_T_lo, c
 int lzq_ode_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, const double* d_work,
                       int64_t work_doubles, int64_t max_steps, lzq_yield* d_out, int32_t* d_status,
                       void* stream);
+
+/* lzq_ode_integrate with tables shared between points: point i reads the spline table at
+ * d_work[d_table_index[i] * LZQ_ODE_WS_PER_POINT] (0 <= d_table_index[i] < n_tables, the
+ * caller's contract; work_doubles >= n_tables * LZQ_ODE_WS_PER_POINT).  A table depends only
+ * on the A/V kernel and the window of fpy:141-156, 207-212 -- (I_p, beta_over_H, T_p_GeV, v_w,
+ * g_star, T_min_over_Tp, T_max_over_Tp) -- so points equal in those fields (a sweep over P,
+ * flux, sigma_v, Gamma_wash, m_chi, ...) share one lzq_ode_tables row; the results are
+ * bit-identical to lzq_ode_integrate with per-point tables. */
+int lzq_ode_integrate_shared(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n,
+                             const int32_t* d_table_index, int64_t n_tables, const double* d_work,
+                             int64_t work_doubles, int64_t max_steps, lzq_yield* d_out, int32_t* d_status,
+                             void* stream);
 
 /* lzq_ode_tables + lzq_ode_integrate (d_status may be NULL). */
 int lzq_ode_batch(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, double* d_work,

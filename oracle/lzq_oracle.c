@@ -514,7 +514,31 @@ int oracle_ode_point(const oracle_point* p, const oracle_ode* o, int64_t max_ste
   radau_tableau(C, A);
   ode_ctx c = {p, o, coef, T_lo, T_hi};
   double Y[2] = {Ychi0, 0.0};
-  for (int64_t k = 0; k < N && st == 0; k++) st = radau_step(&c, C, A, x0 + (double)k * h, h, Y);
+  /* n_chi_eq / vbar_chi switch formula at the strict T > m/3 (fpy:100, 111): the rhs jumps at
+   * the first x whose T = m/max(x, 1e-30) is not > m/3.  A step that straddles that point is
+   * split there (ending one ulp before it), so no Radau stage sees both branches: the fixed
+   * step then stays 5th order across the jump (tests/golden/golden_ode_stiff.json). */
+  double xb = INFINITY;
+  {
+    const double m3 = m / 3.0;
+    double xg = 3.0;
+    if (m / xg > m3) {
+      while (m / xg > m3) xg = nextafter(xg, INFINITY);
+    } else {
+      while (m / nextafter(xg, -INFINITY) <= m3) xg = nextafter(xg, -INFINITY);
+    }
+    if (x0 < xg && xg < x1) xb = xg;
+  }
+  for (int64_t k = 0; k < N && st == 0; k++) {
+    const double xk = x0 + (double)k * h;
+    if (xk < xb && xb <= xk + h) { /* the step's last stage (x = xk + h) would see the other branch */
+      const double xa = nextafter(xb, -INFINITY);
+      if (xa > xk) st = radau_step(&c, C, A, xk, xa - xk, Y);
+      if (st == 0 && xk + h > xb) st = radau_step(&c, C, A, xb, (xk + h) - xb, Y);
+    } else {
+      st = radau_step(&c, C, A, xk, h, Y);
+    }
+  }
   free(coef);
   *n_steps = N;
   if (st != 0 && st != 4) return st;

@@ -79,3 +79,30 @@ def test_engine_refuses_without_gpu():
         pytest.skip("GPU present")
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         pkg("engine").Engine()
+
+
+def test_ode_table_groups_host_logic():
+    """Engine.ode's table sharing bookkeeping (engine.table_groups, device-agnostic torch):
+    groups = bitwise-equal ODE_TABLE_KEY fields; other fields never split a group."""
+    import torch
+    n_ = pkg("_native")
+    table_groups = pkg("engine").table_groups
+    rng = np.random.default_rng(0)
+    p = np.zeros(1000, dtype=n_.POINT_DTYPE)
+    for f in n_.ODE_TABLE_KEY:
+        p[f] = 1.25
+    p["P_chi_to_B"] = rng.uniform(size=p.size)
+    p["m_chi_GeV"] = rng.uniform(size=p.size)
+    t = torch.from_numpy(p.view(np.uint8).copy())
+    first, inv = table_groups(t, p.size)
+    assert first.tolist() == [0] and int(inv.max()) == 0
+    kinds = rng.integers(0, 7, p.size)
+    p["I_p"] = 0.1 * kinds
+    p["T_max_over_Tp"] = np.where(kinds == 3, 2.0, 1.6)
+    first, inv = table_groups(torch.from_numpy(p.view(np.uint8).copy()), p.size)
+    assert first.numel() == 7
+    key = np.stack([p[f] for f in n_.ODE_TABLE_KEY], axis=1)
+    assert np.array_equal(key[first.numpy()][inv.numpy()], key)
+    assert all(int(f) == int(np.argmax(kinds == kinds[int(f)])) for f in first)   # first occurrence
+    p["I_p"] = rng.uniform(size=p.size)                                           # all distinct: no sharing
+    assert table_groups(torch.from_numpy(p.view(np.uint8).copy()), p.size) is None

@@ -2,7 +2,10 @@
 """Throughput of the ODE fallback (fpy:385-417; lzq_ode_batch) on one GPU next to the C
 restatement on the host cores.  Configs: the equal-mass config with wash-out in a narrow
 window (20000 Radau steps/point), a stiff thermal annihilation case, and the shipped window
-(~1e6 steps/point).  Points differ in P and flux (uniform work).  One JSON line per config.
+(~1e6 steps/point).  Points differ in P and flux (uniform work), so they share one A/V spline
+table (Engine.ode share_tables); each case is also timed with a table per point
+(gpu_points_per_s_unshared, the cost for points that all differ in the A/V kernel).  One
+JSON line per config.
 
     python tools/bench_ode.py [n_narrow] [n_full] [chunk]
 """
@@ -49,21 +52,30 @@ def main():
         pts = np.concatenate([cfgm.to_point(c) for c in cfgs])
         ods = np.concatenate([cfgm.to_ode_params(c) for c in cfgs])
         eng.ode(pts[:64], ods[:64])  # warm-up
+        eng.ode(pts[:64], ods[:64], share_tables=False)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        tab, st = eng.ode(pts, ods, chunk=chunk)
+        tab, st = eng.ode(pts, ods, chunk=chunk)          # one shared A/V table (points differ in P, flux)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        ok = bool((st == 0).all())
+        t0 = time.perf_counter()
+        tab_u, st_u = eng.ode(pts, ods, chunk=chunk, share_tables=False)   # a table per point
+        torch.cuda.synchronize()
+        dt_u = time.perf_counter() - t0
+        ok = bool((st == 0).all()) and bool((st_u == 0).all())
+        same = bool(torch.equal(tab, tab_u))
         k = min(n, 32 if name != "full_window_wash" else 16)
+        threads = bench.host_cpus()["usable"]
         t1 = time.perf_counter()
-        ref, rst = O.ode_batch(cfgs[:k], nthreads=16)
+        ref, rst = O.ode_batch(cfgs[:k], nthreads=threads)
         dtc = time.perf_counter() - t1
         t = tab[:k].cpu().numpy()
         err = float(np.max(np.abs(t - ref) / np.maximum(np.abs(ref), 1e-300)))
         steps = O.ode_point(cfgs[0])["n_steps"]
-        print(json.dumps({"config": name, "points": n, "chunk": chunk, "steps_per_point": steps, "gpu_points_per_s": n / dt,
-                          "gpu_seconds": dt, "all_ok": ok, "cpu_oracle_points_per_s": k / dtc, "cpu_threads": 16,
+        print(json.dumps({"config": name, "points": n, "chunk": chunk, "steps_per_point": steps,
+                          "gpu_points_per_s": n / dt, "gpu_seconds": dt,
+                          "gpu_points_per_s_unshared": n / dt_u, "shared_bit_identical": same, "all_ok": ok,
+                          "cpu_oracle_points_per_s": k / dtc, "cpu_threads": threads,
                           "cpu_sample": k, "max_rel_diff_gpu_vs_oracle": err}), flush=True)
 
 

@@ -17,11 +17,14 @@ CONFIGS = [dict(LZQ_KUNROLL=8), dict(LZQ_KUNROLL=10), dict(LZQ_KUNROLL=12)]
 
 
 def main():
+    """argv: optional variant list, one 'KEY=VAL[,KEY=VAL...]' per variant (overrides CONFIGS)."""
     outdir = os.path.join(B.BUILD_DIR, "variants")
     import shutil
     shutil.rmtree(outdir, ignore_errors=True)
     keys = list(GRID)
     confs = CONFIGS or [dict(zip(keys, vals)) for vals in itertools.product(*(GRID[k] for k in keys))]
+    if len(sys.argv) > 1:
+        confs = [dict(kv.split("=", 1) for kv in arg.split(",")) for arg in sys.argv[1:]]
     for d in confs:
         name = "_".join(f"{k[4:].lower()}{v}" for k, v in d.items())
         B.build(defines=d, out=os.path.join(outdir, f"liblzq_{name}.so"))

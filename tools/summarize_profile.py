@@ -32,7 +32,7 @@ def agg(path, key="grid"):
 
 def main():
     src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "prof")
-    tag = sys.argv[2] if len(sys.argv) > 2 else "round1"
+    tag = sys.argv[2] if len(sys.argv) > 2 else "round2"
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
@@ -70,6 +70,11 @@ def main():
         wn = points * WAVE_NODES_PER_POINT
         out["valu_mix_per_wave_node"] = {k[14:].lower(): c[k] / wn for k in (
             "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_INT32")}
+    if "SQ_ACTIVE_INST_VALU" in c and "GRBM_GUI_ACTIVE" in c:
+        # rocprofv3's derived VALUBusy = 100 * sum(SQ_ACTIVE_INST_VALU) / CU_NUM / max(GRBM_GUI_ACTIVE);
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs here (all equal), so max = sum / 8.  It counts
+        # quad-cycles per VALU instruction, so 2-cycle integer ops inflate it past 100 %.
+        out["valubusy_rocprof"] = 100.0 * c["SQ_ACTIVE_INST_VALU"] / 256 / (c["GRBM_GUI_ACTIVE"] / 8)
     if "SQ_WAVE_CYCLES" in c:
         wc = c["SQ_WAVE_CYCLES"]
         out["wave_time_split"] = {k: c[k] / wc for k in ("SQ_ACTIVE_INST_VALU", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY",

@@ -907,12 +907,16 @@ int lzq::launch_ode_aov_tables(const lzq_point* d_points, int64_t n, const doubl
   if (rc) return rc;
   const int64_t nb = blocks_for(n, lzq::kWavesPerBlock);
   if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_ode_tables: n too large");
+  // The ODE tables always use the exact-underflow truncation of the z-sums: it is bit-identical
+  // to the dense sum (tests/test_gpu_parity.py::test_truncation_is_bit_identical) and this path
+  // is not the dense headline benchmark, so there is nothing to keep dense for.
+  const int truncate = 1;
   if (g_exp_variant == lzq::kExpTable)
     hipLaunchKernelGGL(lzq::ode_aov_table_kernel<lzq::kExpTable>, dim3((unsigned)nb), dim3(lzq::kBlock), 0, stream,
-                       d_points, n, g_dev_tab[dev], exp_table(dev), d_T_lo, d_T_hi, d_work, g_truncate);
+                       d_points, n, g_dev_tab[dev], exp_table(dev), d_T_lo, d_T_hi, d_work, truncate);
   else
     hipLaunchKernelGGL(lzq::ode_aov_table_kernel<lzq::kExpPoly11>, dim3((unsigned)nb), dim3(lzq::kBlock), 0, stream,
-                       d_points, n, g_dev_tab[dev], exp_table(dev), d_T_lo, d_T_hi, d_work, g_truncate);
+                       d_points, n, g_dev_tab[dev], exp_table(dev), d_T_lo, d_T_hi, d_work, truncate);
   LZQ_HIP(hipGetLastError());
   return LZQ_OK;
 }

@@ -19,6 +19,7 @@
 #include <stdio.h>
 
 #include "../../include/lzq.h"
+#include "lzq_exp2.h"
 #include "lzq_internal.h"
 #include "lzq_physics.h"
 
@@ -103,6 +104,29 @@ __device__ __forceinline__ double spline_eval(const OdePoint& o, const double* _
   return res;
 }
 
+#ifndef LZQ_ODE_FASTMATH
+#define LZQ_ODE_FASTMATH 1  // 0: IEEE division and ROCm exp in the stage function (tools/ablate_ode.py)
+#endif
+
+// 1/x for a positive normal x: v_rcp_f64 + two Newton steps (5 VALU; <= 1 ulp from the
+// correctly rounded quotient, which costs ~10).
+__device__ __forceinline__ double rcp_pos(double x) {
+  if (!LZQ_ODE_FASTMATH) return 1.0 / x;
+  double r = __builtin_amdgcn_rcp(x);
+  double e = __builtin_fma(-x, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-x, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+
+// exp(v) for v <= 0 as 2^(v log2 e) with the degree-11 exp2 of lzq_exp2.h (0.63 ulp on the
+// reduced argument; the one rounding of v log2 e costs |v| 2^-53 relative, < 1e-13 for
+// |v| < 700, where the factor is still > 1e-304).  ~16 VALU against ~22 for ROCm's exp.
+__device__ __forceinline__ double exp_nonpos(double v) {
+  if (!LZQ_ODE_FASTMATH) return exp(v);
+  return exp2_nonpos(v * kLog2E, 1.0);
+}
+
 // The ingredients of rhs(x, .) (fpy:270-286), which do not depend on Y:
 //   dY_chi/dx = -lam (Y_chi^2 - E2) - S        lam = sigmav s/(H x), E2 = (n_eq/s)^2,
 //                                               S = (deplete ? SB/s : 0)/(H x)
@@ -120,7 +144,7 @@ __device__ __forceinline__ OdeStage ode_stage(const OdePoint& o, const double* _
   // the guarded branch divides).  Each product differs from the quotient by a few ulp, far
   // inside the 1e-11 oracle gate (tests/test_gpu_ode.py).
   const double xc = pymax(x, 1e-30);
-  const double ixc = 1.0 / xc;
+  const double ixc = rcp_pos(xc);
   const double T = o.m * ixc;                                 // fpy:272  m / max(x, 1e-30)
   const double iT = T >= 1e-30 ? xc * o.inv_m : 1e30;         // 1 / max(T, 1e-30)
   const double H = pymax(o.H0 * T * T * kInvMplGeV, 1e-300);  // fpy:273 via fpy:85
@@ -129,13 +153,13 @@ __device__ __forceinline__ OdeStage ode_stage(const OdePoint& o, const double* _
   const double qT = o.Tp * iT;                                // fpy:275 y_of_T (fpy:126-128)
   const double y = 0.5 * o.B * (qT * qT - 1.0);
   const double q = y * o.inv_sig;
-  const double window = exp(-0.5 * (q * q));                  // fpy:276
+  const double window = exp_nonpos(-0.5 * (q * q));           // fpy:276
   double n_eq, vbar;                                          // fpy:90-120
   if (T > o.m3) {
     n_eq = o.c_rel * T3;
     vbar = 1.0;
   } else {
-    n_eq = o.c_nr * (T * sqrt(T)) * exp(-o.m * iT);
+    n_eq = o.c_nr * (T * sqrt(T)) * exp_nonpos(-o.m * iT);
     vbar = sqrt(pymax(8.0 * T * o.inv_v0, 0.0));
   }
   const double J = o.flux * (0.25 * n_eq * vbar);             // fpy:222-223
@@ -240,10 +264,25 @@ __device__ __forceinline__ double solve3_last(const double (&M)[3][3], const dou
   return num / det;
 }
 
-// One Radau step of size h for both equations; false when the Y_chi Newton iteration fails.
-__device__ __forceinline__ bool radau_step(const Radau& R, const OdeStage (&st)[3], double h, double& Ychi,
-                                           double& YB) {
-  // Y_B: (I + h A diag(beta)) Z = YB + h A alpha, exactly
+// h * a_ij of the Radau matrix for one step size (formed once per step size, not per step).
+struct RadauH {
+  double a[3][3];
+};
+
+__device__ __forceinline__ RadauH radau_h(const Radau& R, double h) {
+  RadauH r;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) r.a[i][j] = h * R.a[i][j];
+  return r;
+}
+
+// One Radau step for both equations (hA = h * A of the step); false when the Y_chi Newton
+// iteration fails.  The stage sums are explicit fmas (hA_ij * f_j + acc); only the last stage
+// of each equation is the step's result, so the linear cases form only what they need.
+__device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st)[3], double& Ychi, double& YB) {
+  // Y_B: (I + hA diag(beta)) Z = YB + hA alpha, exactly; Z_3 = Y_B(x + h)
   {
     double M[3][3], b[3];
 #pragma unroll
@@ -251,8 +290,8 @@ __device__ __forceinline__ bool radau_step(const Radau& R, const OdeStage (&st)[
       double acc = YB;
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        acc = acc + h * R.a[i][j] * st[j].alpha;
-        M[i][j] = (i == j ? 1.0 : 0.0) + h * R.a[i][j] * st[j].beta;
+        acc = __builtin_fma(hA.a[i][j], st[j].alpha, acc);
+        M[i][j] = __builtin_fma(hA.a[i][j], st[j].beta, i == j ? 1.0 : 0.0);
       }
       b[i] = acc;
     }
@@ -260,18 +299,14 @@ __device__ __forceinline__ bool radau_step(const Radau& R, const OdeStage (&st)[
   }
   // Y_chi: Z_i = Y + h sum_j a_ij f_j(Z_j), f_j(Z) = -lam_j (Z^2 - E2_j) - S_j
   const bool nonlinear = st[0].lam != 0.0 || st[1].lam != 0.0 || st[2].lam != 0.0;
-  double Z[3] = {Ychi, Ychi, Ychi};
-  if (!nonlinear) {
+  if (!nonlinear) {  // f_j = -S_j: Z_3 = Y - sum_j hA_3j S_j
+    double acc = Ychi;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      double acc = Ychi;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) acc = acc - h * R.a[i][j] * st[j].S;
-      Z[i] = acc;
-    }
-    Ychi = Z[2];
+    for (int j = 0; j < 3; ++j) acc = __builtin_fma(-hA.a[2][j], st[j].S, acc);
+    Ychi = acc;
     return true;
   }
+  double Z[3] = {Ychi, Ychi, Ychi};
   for (int it = 0; it < 40; ++it) {
     double M[3][3], g[3];
     double f[3], jf[3];
@@ -285,8 +320,8 @@ __device__ __forceinline__ bool radau_step(const Radau& R, const OdeStage (&st)[
       double acc = Z[i] - Ychi;
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        acc = acc - h * R.a[i][j] * f[j];
-        M[i][j] = (i == j ? 1.0 : 0.0) - h * R.a[i][j] * jf[j];
+        acc = __builtin_fma(-hA.a[i][j], f[j], acc);
+        M[i][j] = __builtin_fma(-hA.a[i][j], jf[j], i == j ? 1.0 : 0.0);
       }
       g[i] = -acc;
     }
@@ -441,6 +476,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
     // split there, ending one ulp before it, so no stage sees both branches (the oracle does
     // the same with its own T; tests/golden/golden_ode_stiff.json).
     const double xb = branch_x(o, x0, x1);
+    const RadauH hA = radau_h(R, h);
     for (int64_t k = 0; k < N; ++k) {
       const double xk = x0 + (double)k * h;
       const bool split = xk < xb && xb <= xk + h;  // the last stage (x = xk + h) would see the other branch
@@ -448,11 +484,11 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
       double YB_prev = YB;
       bool ok = true;
       if (xa > xk) {
-        const double hs = xa - xk;
+        const double hs = split ? xa - xk : h;
         OdeStage sg[3];
 #pragma unroll
-        for (int j = 0; j < 3; ++j) sg[j] = ode_stage(o, w, xk + R.c[j] * (split ? hs : h));
-        ok = radau_step(R, sg, split ? hs : h, Ychi, YB);
+        for (int j = 0; j < 3; ++j) sg[j] = ode_stage(o, w, xk + R.c[j] * hs);
+        ok = radau_step(split ? radau_h(R, hs) : hA, sg, Ychi, YB);
       }
       if (ok && split && xk + h > xb) {
         const double hs = (xk + h) - xb;
@@ -460,7 +496,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
         YB_prev = YB;
 #pragma unroll
         for (int j = 0; j < 3; ++j) sg[j] = ode_stage(o, w, xb + R.c[j] * hs);
-        ok = radau_step(R, sg, hs, Ychi, YB);
+        ok = radau_step(radau_h(R, hs), sg, Ychi, YB);
       }
       if (!ok) {
         YB = YB_prev;  // report the state at the start of the failed step, like sol.y[:, -1] (fpy:408-410)

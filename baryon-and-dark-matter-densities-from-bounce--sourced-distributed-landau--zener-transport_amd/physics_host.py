@@ -1,6 +1,6 @@
-"""Host-side scalar helpers the driver needs for input preparation and printing only
-(never on the hot path): y(T) for the diagnostics rows (fpy:126-128) and the scalar
-entropy/number density used nowhere in the timed path."""
+"""Host-side scalar helper for printing only (never on the hot path): y(T) for the
+diagnostics rows of the CLI (fpy:126-128, fpy:430-438).  Every other physics function runs on
+the GPU (csrc/lzq_physics.h)."""
 from __future__ import annotations
 
 

@@ -18,8 +18,13 @@ def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 400_000
     sw = importlib.import_module(PKG + ".sweep")
     eng = importlib.import_module(PKG + ".engine").Engine(0)
+    import dataclasses
     specs = sw.builtin_specs()
-    for name in ("C2", "C3", "C4", "C5"):
+    for nc in (16, 32):   # BASELINE C5: N >= 8 crossings per point; also 16 and 32
+        c5 = specs["C5"]
+        specs[f"C5_N{nc}"] = dataclasses.replace(c5, name=f"C5_N{nc}",
+                                                 crossings=dataclasses.replace(c5.crossings, n_cross=nc))
+    for name in ("C2", "C3", "C4", "C5", "C5_N16", "C5_N32"):
         spec = specs[name]
         cnt = min(n, spec.total)
         start = (spec.total - cnt) // 2

@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""profiles/<round>/ode_pmc.json from a tools/gpu_ode_pmc.sh run: per config, the
+ode_integrate_kernel's VALU and FP64 instructions per wave-step (PMC pass) and its duration
+(kernel-trace pass), hence executed FP64 TFLOP/s against the 78.6 TFLOP/s FP64 vector peak.
+bench_ode.py runs, per config, the shared-table and the per-point-table path: two
+integrate dispatches with the same work, in that order."""
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CONFIGS = [("narrow_wash", 262144, 20000), ("stiff_thermal", 262144, 25385), ("full_window_wash", 16384, 999800)]
+
+
+def main():
+    src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "odepmc")
+    tag = sys.argv[2] if len(sys.argv) > 2 else "round2"
+    rows = list(csv.DictReader(open(os.path.join(src, "pmc", "run_counter_collection.csv"))))
+    disp = defaultdict(dict)
+    for r in rows:
+        if "ode_integrate_kernel" in r["Kernel_Name"]:
+            disp[int(r["Dispatch_Id"])][r["Counter_Name"]] = disp[int(r["Dispatch_Id"])].get(r["Counter_Name"], 0.0) + \\
+                float(r["Counter_Value"])
+    tr = [r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv")))
+          if "ode_integrate_kernel" in r["Kernel_Name"]]
+    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9 for r in tr]
+    pmc = [disp[k] for k in sorted(disp)]
+    # skip the warm-up dispatches (64 points each, 2 per config): keep dispatches with the config's wave count
+    out = {"source": "tools/gpu_ode_pmc.sh + tools/summarize_ode_pmc.py", "kernel": "ode_integrate_kernel",
+           "peak_tflops": 78.6, "configs": {}}
+    big_p = [c for c in pmc if c.get("SQ_WAVES", 0) >= 256]
+    big_t = [d for d, r in zip(durs, tr) if int(r["Grid_Size"]) >= 256 * 64]
+    for i, (name, n, steps) in enumerate(CONFIGS):
+        c = big_p[2 * i]
+        waves = c["SQ_WAVES"]
+        ws = waves * steps
+        flop = 64.0 * (2.0 * c["SQ_INSTS_VALU_FMA_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + c["SQ_INSTS_VALU_ADD_F64"])
+        t_shared, t_unshared = big_t[2 * i], big_t[2 * i + 1]
+        out["configs"][name] = {
+            "points": n, "steps_per_point": steps, "waves": waves,
+            "valu_per_wave_step": c["SQ_INSTS_VALU"] / ws,
+            "fp64_fma_mul_add_per_wave_step": (c["SQ_INSTS_VALU_FMA_F64"] + c["SQ_INSTS_VALU_MUL_F64"] +
+                                               c["SQ_INSTS_VALU_ADD_F64"]) / ws,
+            "kernel_s_shared_tables": t_shared, "kernel_s_per_point_tables": t_unshared,
+            "executed_fp64_tflops": flop / t_shared / 1e12, "frac_of_fp64_peak": flop / t_shared / 1e12 / 78.6}
+    dst = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    with open(os.path.join(dst, "ode_pmc.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -21,7 +21,7 @@ def main():
     disp = defaultdict(dict)
     for r in rows:
         if "ode_integrate_kernel" in r["Kernel_Name"]:
-            disp[int(r["Dispatch_Id"])][r["Counter_Name"]] = disp[int(r["Dispatch_Id"])].get(r["Counter_Name"], 0.0) + \\
+            disp[int(r["Dispatch_Id"])][r["Counter_Name"]] = disp[int(r["Dispatch_Id"])].get(r["Counter_Name"], 0.0) + \
                 float(r["Counter_Value"])
     tr = [r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv")))
           if "ode_integrate_kernel" in r["Kernel_Name"]]
@@ -31,7 +31,7 @@ def main():
     out = {"source": "tools/gpu_ode_pmc.sh + tools/summarize_ode_pmc.py", "kernel": "ode_integrate_kernel",
            "peak_tflops": 78.6, "configs": {}}
     big_p = [c for c in pmc if c.get("SQ_WAVES", 0) >= 256]
-    big_t = [d for d, r in zip(durs, tr) if int(r["Grid_Size"]) >= 256 * 64]
+    big_t = [d for d, r in zip(durs, tr) if int(r["Grid_Size_X"]) >= 256 * 64]
     for i, (name, n, steps) in enumerate(CONFIGS):
         c = big_p[2 * i]
         waves = c["SQ_WAVES"]

@@ -46,7 +46,8 @@ ODE_DTYPE = np.dtype([("sigma_v_chi_GeV_m2", "<f8"), ("Gamma_wash_over_H", "<f8"
 assert ctypes.sizeof(LzqOdeParams) == 24 == ODE_DTYPE.itemsize
 ODE_NT, ODE_WS_PER_POINT = 800, 3200  # LZQ_ODE_NT, LZQ_ODE_WS_PER_POINT
 ODE_STATUS = {0: "ok", 1: "`x` must be strictly increasing sequence.", 2: "`max_step` must be positive.",
-              3: "more than max_steps integration steps", 4: "Radau stage Newton iteration did not converge"}
+              3: "more than max_steps integration steps", 4: "Radau stage Newton iteration did not converge",
+              5: "sigma_v != 0: the quadrature form needs a linear Y_chi equation"}
 
 POINT_DTYPE = np.dtype([(n, "<f8") for n in POINT_DOUBLE_FIELDS] + [(n, "<i4") for n in POINT_INT_FIELDS])
 assert ctypes.sizeof(LzqPoint) == 136 == POINT_DTYPE.itemsize
@@ -66,7 +67,7 @@ ABI_VERSION = 1  # LZQ_ABI_VERSION (tests/test_capi.py checks it against the lib
 # Symbols declared in include/lzq.h (checked by tests/test_capi.py against the header).
 EXPORTS = ("lzq_abi_version", "lzq_last_error", "lzq_init", "lzq_ztables", "lzq_tune", "lzq_aov_batch",
            "lzq_jchi_batch", "lzq_yields_batch", "lzq_sweep_grid", "lzq_p_closed_form",
-           "lzq_lz_propagate", "lzq_ode_tables", "lzq_ode_integrate", "lzq_ode_integrate_shared", "lzq_ode_batch",
+           "lzq_lz_propagate", "lzq_ode_tables", "lzq_ode_integrate", "lzq_ode_integrate_shared", "lzq_ode_quadrature", "lzq_ode_batch",
            "lzq_ode_aov_T", "lzq_ode_rhs")
 # the lzq_point fields an ODE spline table depends on (A/V kernel fpy:141-156 + window fpy:368-369)
 ODE_TABLE_KEY = ("I_p", "beta_over_H", "T_p_GeV", "v_w", "g_star", "T_min_over_Tp", "T_max_over_Tp")
@@ -109,6 +110,7 @@ def load(path: str | None = None):
     L.lzq_ode_tables.argtypes = [vp, i64, vp, vp, vp, i64, vp, vp]
     L.lzq_ode_integrate.argtypes = [vp, vp, i64, vp, i64, i64, vp, vp, vp]
     L.lzq_ode_integrate_shared.argtypes = [vp, vp, i64, vp, i64, vp, i64, i64, vp, vp, vp]
+    L.lzq_ode_quadrature.argtypes = [vp, vp, i64, vp, i64, vp, i64, vp, vp, vp]
     L.lzq_ode_batch.argtypes = [vp, vp, i64, vp, i64, i64, vp, vp, vp]
     L.lzq_ode_aov_T.argtypes = [P(LzqPoint), d, d, vp, vp, i64, vp, vp]
     L.lzq_ode_rhs.argtypes = [P(LzqPoint), P(LzqOdeParams), d, d, vp, vp, vp, i64, vp, vp]

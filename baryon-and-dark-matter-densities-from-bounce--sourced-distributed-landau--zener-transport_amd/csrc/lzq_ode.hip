@@ -517,6 +517,160 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
   if (status) status[i] = st;
 }
 
+// ---------------------------------------------------------------------------------------
+// Converged quadrature form of the sigma_v = 0 fallback (opt-in; lzq_ode_quadrature).
+// With sigma_v = 0 both equations of rhs (fpy:270-286) are linear with known integrating
+// factors: beta = gamma_w H / (H x) = gamma_w / x, so
+//   Y_B(x1)   = int_{x0}^{x1} alpha(x) (x / x1)^gamma_w dx,      alpha = (SB/s)/(H x),
+//   Y_chi(x1) = Y_chi(x0) - [deplete] int_{x0}^{x1} alpha(x) dx,
+// exactly.  In T = m/x (dx = m/T^2 dT) the integrand is the A/V spline's cubic on each knot
+// interval times smooth factors (power laws, the source window, the Boltzmann factor, the
+// integrating factor), with a jump at the strict T = m/3 branch (fpy:100-111): each knot
+// interval is split at that branch and into sub-intervals no wider than half the narrowest
+// local scale of those factors, and integrated by 8-point Gauss-Legendre.  This is the
+// converged solution of the reference's equations (tests/test_gpu_ode.py: within 1e-10 of the
+// reference's own rtol-1e-12 re-solve, golden_ode.json "tight"); the default Radau path
+// reproduces the reference's rtol-1e-8 integrator instead.
+// ---------------------------------------------------------------------------------------
+__constant__ double kGLx[8] = {-0x1.ebab1cb0acc66p-1, -0x1.97e4ab249f41ep-1, -0x1.0d129583284b4p-1,
+                               -0x1.77ac94f3c7344p-3, 0x1.77ac94f3c7344p-3,  0x1.0d129583284b4p-1,
+                               0x1.97e4ab249f41ep-1,  0x1.ebab1cb0acc66p-1};
+__constant__ double kGLw[8] = {0x1.9ea1d04ca0393p-4, 0x1.c76fb531d2b91p-3, 0x1.413c50a255611p-2, 0x1.736360b19933fp-2,
+                               0x1.736360b19933fp-2, 0x1.413c50a255611p-2, 0x1.c76fb531d2b91p-3, 0x1.9ea1d04ca0393p-4};
+constexpr int kQuadMaxSub = 256;
+#ifndef LZQ_QUAD_UNROLL
+#define LZQ_QUAD_UNROLL 1
+#endif
+#ifndef LZQ_QUAD_MIN_WAVES
+#define LZQ_QUAD_MIN_WAVES 3
+#endif
+
+// alpha(x) dx/dT = (SB/s)/(H x) * m/T^2 at T (inside knot interval k with PPoly coefficients c,
+// knot Tk), with the operations of ode_stage.
+__device__ __forceinline__ double ode_alpha_dT(const OdePoint& o, const double* c, double Tk, double T) {
+  const double iT = rcp_pos(T);
+  const double H = pymax(o.H0 * T * T * kInvMplGeV, 1e-300);
+  const double T3 = (T * T) * T;
+  const double s = pymax(o.s0 * T3, 1e-300);
+  const double qT = o.Tp * iT;
+  const double y = 0.5 * o.B * (qT * qT - 1.0);
+  const double q = y * o.inv_sig;
+  const double window = exp_nonpos(-0.5 * (q * q));
+  double n_eq, vbar;
+  if (T > o.m3) {
+    n_eq = o.c_rel * T3;
+    vbar = 1.0;
+  } else {
+    n_eq = o.c_nr * (T * sqrt(T)) * exp_nonpos(-o.m * iT);
+    vbar = sqrt(pymax(8.0 * T * o.inv_v0, 0.0));
+  }
+  const double J = o.flux * (0.25 * n_eq * vbar);
+  const double sT = T - Tk;
+  double z = sT, Av = c[3];
+  Av = Av + c[2] * z;
+  z = z * sT;
+  Av = Av + c[1] * z;
+  z = z * sT;
+  Av = Av + c[0] * z;
+  const double SB = o.P * J * Av * window;
+  const double x = o.m * iT;
+  return SB / (s * (H * x)) * (o.m * iT * iT);
+}
+
+// One wavefront per point; lane l takes knot intervals l, l+64, ...; a fixed xor-butterfly
+// reduces the lane sums (deterministic).  tidx: shared tables as in ode_integrate_kernel.
+__global__ __launch_bounds__(kOdeBlock, LZQ_QUAD_MIN_WAVES) void ode_quad_kernel(const lzq_point* __restrict__ pts,
+                                                             const lzq_ode_params* __restrict__ ode, int64_t n,
+                                                             const int32_t* __restrict__ tidx,
+                                                             const double* __restrict__ ws, lzq_yield* __restrict__ out,
+                                                             int32_t* __restrict__ status) {
+  constexpr int kW = 64;
+  const int lane = threadIdx.x & (kW - 1);
+  const int64_t i = (int64_t)blockIdx.x * (kOdeBlock / kW) + (threadIdx.x / kW);
+  if (i >= n) return;  // wave-uniform
+  const lzq_point pt = pts[i];
+  const OdePoint o = ode_point(pt, ode[i]);
+  const double* w = ws + (tidx ? (int64_t)tidx[i] : i) * (int64_t)kOdeWS;
+  const double nan = __builtin_nan("");
+  lzq_yield r = {nan, nan, nan, nan, nan, pt.P_chi_to_B};
+  int st = LZQ_OK;
+  if (o.sigmav != 0.0) st = LZQ_ODE_NOT_LINEAR;
+  // CubicSpline's strictly-increasing check, knots split over the lanes
+  bool ok = true;
+  for (int k = lane + 1; k < kOdeNT; k += kW)
+    ok = ok && linspace_at(o.T_lo, o.T_hi, o.stepT, k, kOdeNT) > linspace_at(o.T_lo, o.T_hi, o.stepT, k - 1, kOdeNT);
+  if (st == LZQ_OK && __any(!ok)) st = LZQ_ODE_BAD_GRID;
+  const double m = o.m, T_p = o.Tp;
+  const double x1 = m / pymax(o.T_lo, 1e-30);  // fpy:388
+  const double ix1 = 1.0 / x1;
+  double Ychi;  // fpy:389-399
+  if (pt.regime == LZQ_NONTHERMAL) {
+    if (pt.has_Y_chi_init) Ychi = pt.Y_chi_init;
+    else if (pt.has_n_chi_at_Tp) Ychi = pt.n_chi_at_Tp_GeV3 / pymax(s_entropy(T_p, pt.g_star_s), 1e-300);
+    else Ychi = 1.0e-12;
+  } else {
+    Ychi = n_chi_eq(o.T_hi, m, pt.g_chi, pt.stats) / s_entropy(o.T_hi, pt.g_star_s);
+  }
+  double accB = 0.0, accC = 0.0;
+  if (st == LZQ_OK) {
+    const double gam = o.gamma_w;
+    const double Bt = o.B * T_p * T_p;
+    for (int k = lane; k < kOdeNT - 1; k += kW) {
+      const double Tk = linspace_at(o.T_lo, o.T_hi, o.stepT, k, kOdeNT);
+      const double Tk1 = linspace_at(o.T_lo, o.T_hi, o.stepT, k + 1, kOdeNT);
+      const double c[4] = {w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]};
+      const bool split = Tk < o.m3 && o.m3 < Tk1;
+      for (int part = 0; part < (split ? 2 : 1); ++part) {
+        const double a = (split && part == 1) ? o.m3 : Tk;
+        const double b = (split && part == 0) ? o.m3 : Tk1;
+        // the window exp(-q^2/2), q = y(T)/sigma, y monotone in T: beyond |q| = 40 on the whole
+        // [a, b] it is below e^-800, i.e. exactly 0 in double -- skip (no sub-intervals wasted
+        // where the source is off)
+        const double qa = 0.5 * o.B * ((T_p / a) * (T_p / a) - 1.0) * o.inv_sig;
+        const double qb = 0.5 * o.B * ((T_p / b) * (T_p / b) - 1.0) * o.inv_sig;
+        if (qa * qb > 0.0 && pymin(fabs(qa), fabs(qb)) > 40.0) continue;
+        // narrowest local scale of the smooth factors on [a, b] (all shrink as T falls):
+        // window width in T, integrating factor / power laws, Boltzmann factor below m/3
+        double scale = o.sig * a * a * a / pymax(Bt, 1e-300);
+        scale = pymin(scale, a / (gam + 6.0));
+        if (a <= o.m3) scale = pymin(scale, a * a / m);
+        const double ns = ceil((b - a) / (0.5 * scale));
+        const int nsub = ns < 1.0 ? 1 : (ns > (double)kQuadMaxSub ? kQuadMaxSub : (int)ns);
+        const double hs = (b - a) / (double)nsub;
+        for (int j = 0; j < nsub; ++j) {
+          const double mid = a + ((double)j + 0.5) * hs;
+#pragma unroll LZQ_QUAD_UNROLL
+          for (int g = 0; g < 8; ++g) {
+            const double T = mid + (0.5 * hs) * kGLx[g];
+            const double f = (0.5 * hs * kGLw[g]) * ode_alpha_dT(o, c, Tk, T);
+            const double xr = (m * rcp_pos(T)) * ix1;                       // x / x1 <= 1
+            accB = __builtin_fma(f, gam == 0.0 ? 1.0 : exp_nonpos(gam * log(xr)), accB);
+            accC += f;
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int d = 1; d < kW; d <<= 1) {
+    accB += __shfl_xor(accB, d, kW);
+    accC += __shfl_xor(accC, d, kW);
+  }
+  if (lane != 0) return;
+  if (st == LZQ_OK) {  // fpy:412-417
+    const double YB = accB;
+    if (o.deplete) Ychi = Ychi - accC;
+    const double nB0 = YB * kS0M3, nDM0 = Ychi * kS0M3;
+    r.Y_B = YB;
+    r.Y_chi = Ychi;
+    r.rho_B_kg_m3 = nB0 * kMProtonKg;
+    r.rho_DM_kg_m3 = nDM0 * (m * kGeVToKg);
+    r.DM_over_B = r.rho_DM_kg_m3 / pymax(r.rho_B_kg_m3, 1e-300);
+  }
+  out[i] = r;
+  if (status) status[i] = st;
+}
+
 // BoltzmannSystem.A_over_V_T / .rhs of one point at n arguments (lane per argument).
 __global__ __launch_bounds__(kOdeBlock) void ode_eval_kernel(lzq_point pt, lzq_ode_params od, double T_lo,
                                                              double T_hi, const double* __restrict__ w,
@@ -620,6 +774,22 @@ int lzq_ode_integrate_shared(const lzq_point* d_points, const lzq_ode_params* d_
   hipLaunchKernelGGL(lzq::ode_integrate_kernel, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0,
                      (hipStream_t)stream, d_points, d_ode, n, d_table_index, d_work, max_steps, d_out, d_status);
   return hip_check(hipGetLastError(), "lzq_ode_integrate_shared");
+}
+
+int lzq_ode_quadrature(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n,
+                       const int32_t* d_table_index, int64_t n_tables, const double* d_work, int64_t work_doubles,
+                       lzq_yield* d_out, int32_t* d_status, void* stream) {
+  if (n < 0 || n_tables < 0 || (n > 0 && (!d_points || !d_ode || !d_out)) ||
+      (d_table_index && n > 0 && n_tables == 0))
+    return lzq_set_error(LZQ_EINVAL, "lzq_ode_quadrature: bad arguments");
+  int rc = check_ws(d_table_index ? n_tables : n, d_work, work_doubles, "lzq_ode_quadrature");
+  if (rc) return rc;
+  if (n == 0) return LZQ_OK;
+  const int64_t nb = (n + (lzq::kOdeBlock / 64) - 1) / (lzq::kOdeBlock / 64);
+  if (nb > 2147483647LL) return lzq_set_error(LZQ_EINVAL, "lzq_ode_quadrature: n too large");
+  hipLaunchKernelGGL(lzq::ode_quad_kernel, dim3((unsigned)nb), dim3(lzq::kOdeBlock), 0, (hipStream_t)stream, d_points,
+                     d_ode, n, d_table_index, d_work, d_out, d_status);
+  return hip_check(hipGetLastError(), "lzq_ode_quadrature");
 }
 
 int lzq_ode_batch(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, double* d_work,

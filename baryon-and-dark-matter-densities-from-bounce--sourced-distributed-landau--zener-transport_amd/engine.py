@@ -147,14 +147,19 @@ class Engine:
         return work, status
 
     def ode(self, points, ode_params, max_steps: int = 1 << 26, chunk: int = 1 << 18,
-            share_tables: bool = True) -> tuple:
+            share_tables: bool = True, method: str = "radau") -> tuple:
         """fpy:385-417 for n points (POINT_DTYPE records + ODE_DTYPE records): (n, 6) yields
         table and (n,) int32 status (enum lzq_ode_status), both on the device.  Points are
         processed in chunks so that the spline workspace stays <= chunk * 25.6 KB (6.7 GB at the
         default 2^18 points: 2 waves/SIMD on all 1024 SIMDs need >= 131072 points per launch).
         share_tables: points equal in the fields the A/V spline depends on (ODE_TABLE_KEY) share
         one table (lzq_ode_integrate_shared; bit-identical results, one A/V table per distinct
-        kernel instead of per point)."""
+        kernel instead of per point).
+        method: "radau" (default: the reference's integrator, fixed steps) or "quadrature"
+        (lzq_ode_quadrature: the converged solution of the sigma_v = 0 equations by quadrature,
+        opt-in; points with sigma_v != 0 are integrated by Radau)."""
+        if method not in ("radau", "quadrature"):
+            raise ValueError(f"method must be 'radau' or 'quadrature', got {method!r}")
         pts = np.ascontiguousarray(points, dtype=_native.POINT_DTYPE).reshape(-1)
         ods = np.ascontiguousarray(ode_params, dtype=_native.ODE_DTYPE).reshape(-1)
         if pts.size != ods.size:
@@ -176,7 +181,21 @@ class Engine:
             if work is None or work.numel() < n_tab * _native.ODE_WS_PER_POINT:
                 work = self.ode_workspace(max(n_tab, min(n, chunk) if rep is None else n_tab))
             with torch.cuda.device(self.device):
-                if rep is None:
+                if method == "quadrature":
+                    if rep is None:
+                        self._check(self.lib.lzq_ode_tables(_vp(d_pts), c1 - c0, None, None, _vp(work), work.numel(),
+                                                            None, self._stream()))
+                        d_idx = None
+                    else:
+                        d_rep = d_pts.view(c1 - c0, _native.POINT_DTYPE.itemsize)[rep].contiguous()
+                        d_idx = inv.to(torch.int32)
+                        self._check(self.lib.lzq_ode_tables(_vp(d_rep), n_tab, None, None, _vp(work), work.numel(),
+                                                            None, self._stream()))
+                        keep.append((d_rep, d_idx))
+                    self._check(self.lib.lzq_ode_quadrature(_vp(d_pts), _vp(d_ode), c1 - c0, _vp(d_idx), n_tab,
+                                                            _vp(work), work.numel(), _vp(out[c0:c1]),
+                                                            _vp(status[c0:c1]), self._stream()))
+                elif rep is None:
                     self._check(self.lib.lzq_ode_batch(_vp(d_pts), _vp(d_ode), c1 - c0, _vp(work), work.numel(),
                                                        int(max_steps), _vp(out[c0:c1]), _vp(status[c0:c1]),
                                                        self._stream()))
@@ -193,6 +212,13 @@ class Engine:
                     keep.append((d_rep, d_idx))
             keep.append((d_pts, d_ode))
         self._keepalive = (keep, work)
+        if method == "quadrature":   # sigma_v != 0 points: the Riccati equation needs Radau
+            sel = torch.nonzero(status == 5).reshape(-1).cpu().numpy()
+            if sel.size:
+                t, st = self.ode(pts[sel], ods[sel], max_steps, chunk, share_tables, "radau")
+                d_sel = torch.as_tensor(sel, device=self.device)
+                out[d_sel] = t
+                status[d_sel] = st
         return out, status
 
     def ode_aov_T(self, point, T_lo: float, T_hi: float, work_point: torch.Tensor, Ts) -> torch.Tensor:

@@ -206,3 +206,34 @@ def test_ode_shared_tables_bit_identical(gpu_engine):
 def torch_equal(a, b):
     import torch
     return bool(torch.equal(a, b)) or bool(np.array_equal(a.cpu().numpy(), b.cpu().numpy(), equal_nan=True))
+
+
+@needs_golden
+def test_ode_quadrature_vs_converged_reference(gpu_engine):
+    """lzq_ode_quadrature (opt-in, sigma_v = 0): the exact integrating-factor form of the
+    reference's equations, against the reference's own rtol-1e-12 re-solve (golden "tight"),
+    per case; sigma_v != 0 points fall back to Radau bit for bit."""
+    pts = [r for r in golden("golden_ode.json")["points"] if "error" not in r]
+    cfgs = [full_cfg(r["config"]) for r in pts]
+    p, o = recs(cfgs)
+    q, sq = gpu_engine.ode(p, o, method="quadrature")
+    rd, sr = gpu_engine.ode(p, o)
+    q, sq, rd, sr = q.cpu().numpy(), sq.cpu().numpy(), rd.cpu().numpy(), sr.cpu().numpy()
+    linear = [max(c["sigma_v_chi_GeV_m2"], 0.0) == 0.0 for c in cfgs]
+    assert sum(linear) >= 10
+    worst = 0.0
+    for r, c, lin, rq, rr, s in zip(pts, cfgs, linear, q, rd, sq):
+        assert s == 0
+        if not lin:
+            assert np.array_equal(rq, rr)          # routed to the Radau integrator
+            continue
+        t = r["tight"]
+        assert t["success"]
+        e_b, e_c = rel_err(rq[0], t["Y_B"]), rel_err(rq[1], t["Y_chi"])
+        ref_acc = rel_err(r["final"]["Y_B"], t["Y_B"])
+        print(f"  quadrature Gw={c['Gamma_wash_over_H']:g} T/Tp=[{c['T_min_over_Tp']:g},{c['T_max_over_Tp']:g}] "
+              f"deplete={c['deplete_DM_from_source']}: vs converged Y_B {e_b:.1e} Y_chi {e_c:.1e}; "
+              f"the reference's rtol-1e-8 Y_B is {ref_acc:.1e} from it")
+        assert e_b < 1e-10 and e_c < 1e-10, (c, rq, t)
+        worst = max(worst, e_b, e_c)
+    print(f"ODE quadrature vs converged reference: worst {worst:.2e}")

@@ -72,7 +72,18 @@ def main():
         t = tab[:k].cpu().numpy()
         err = float(np.max(np.abs(t - ref) / np.maximum(np.abs(ref), 1e-300)))
         steps = O.ode_point(cfgs[0])["n_steps"]
-        print(json.dumps({"config": name, "points": n, "chunk": chunk, "steps_per_point": steps,
+        quad = {}
+        if float(over.get("sigma_v_chi_GeV_m2", 0.0)) == 0.0:   # the opt-in quadrature form (sigma_v = 0)
+            eng.ode(pts[:64], ods[:64], method="quadrature")
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            tq, sq = eng.ode(pts, ods, chunk=chunk, method="quadrature")
+            torch.cuda.synchronize()
+            dq = time.perf_counter() - t0
+            rel = ((tq[:, :2] - tab[:, :2]).abs() / tab[:, :2].abs().clamp_min(1e-300)).max().item()
+            quad = {"gpu_points_per_s_quadrature": n / dq, "quadrature_max_rel_diff_vs_radau": rel,
+                    "quadrature_ok": bool((sq == 0).all())}
+        print(json.dumps({"config": name, "points": n, "chunk": chunk, "steps_per_point": steps, **quad,
                           "gpu_points_per_s": n / dt, "gpu_seconds": dt,
                           "gpu_points_per_s_unshared": n / dt_u, "shared_bit_identical": same, "all_ok": ok,
                           "cpu_oracle_points_per_s": k / dtc, "cpu_threads": threads,

@@ -74,6 +74,7 @@ class SweepSpec:
     n_y: int = 8000
     notes: str = ""
     crossings: Optional[CrossingSpec] = None
+    ode_method: str = "radau"   # ODE-path points: "radau" (the reference's integrator) | "quadrature" (opt-in)
 
     @property
     def total(self) -> int:
@@ -95,6 +96,8 @@ class SweepSpec:
              "axes": [{"field": n, "values": [float(x) for x in v]} for n, v in self.axes]}
         if self.crossings is not None:
             d["crossings"] = dict(self.crossings.__dict__)
+        if self.ode_method != "radau":
+            d["ode_method"] = self.ode_method
         return d
 
     def crossing_arrays(self, start: int, count: int, device):
@@ -189,8 +192,11 @@ def spec_from_json(d: dict) -> SweepSpec:
             base.update(json.load(f))
     base.update(d.get("base", {}))
     cr = CrossingSpec(**d["crossings"]) if d.get("crossings") else None
+    method = d.get("ode_method", "radau")
+    if method not in ("radau", "quadrature"):
+        raise ValueError(f"ode_method must be 'radau' or 'quadrature', got {method!r}")
     return SweepSpec(d.get("name", "custom"), base, [_axis_from_json(a) for a in d["axes"]], int(d.get("n_y", 8000)),
-                     d.get("notes", ""), cr)
+                     d.get("notes", ""), cr, method)
 
 
 def builtin_specs() -> dict:
@@ -356,7 +362,7 @@ def make_compute(spec: SweepSpec, engine) -> ComputeFn:
                   (ods["deplete_DM_from_source"] != 0)
             sel = np.nonzero(ode)[0]
             if sel.size:
-                tab, _status = engine.ode(pts[sel], ods[sel])  # failed points: NaN rows (lzq_ode_status)
+                tab, _status = engine.ode(pts[sel], ods[sel], method=spec.ode_method)  # failed points: NaN rows
                 out[torch.as_tensor(sel, device=out.device)] = tab
             sel = np.nonzero(~ode)[0]
             if sel.size:

@@ -133,3 +133,16 @@ def test_out_dir_manifest_and_foreign_resume(tmp_path):
     sw.run_local(lambda s, n, o: (seen.append(s), fake_compute(s, n, o)), 0, 10,
                  lambda n: torch.empty((n, 6), dtype=torch.float64), 4, str(out), resume=True, key="other")
     assert seen == [0, 4, 8]
+
+
+def test_spec_ode_method_roundtrip():
+    sw = pkg("sweep")
+    d = {"name": "w", "ode_method": "quadrature",
+         "axes": [{"field": "Gamma_wash_over_H", "values": [0.5, 1.0]}]}
+    spec = sw.spec_from_json(d)
+    assert spec.ode_method == "quadrature" and sw.is_ode_spec(spec)
+    again = sw.spec_from_json(spec.to_json())
+    assert again.ode_method == "quadrature"
+    assert sw.spec_key(again) != sw.spec_key(sw.spec_from_json({**d, "ode_method": "radau"}))
+    with pytest.raises(ValueError):
+        sw.spec_from_json({**d, "ode_method": "rk4"})

@@ -45,6 +45,7 @@ ODE_DTYPE = np.dtype([("sigma_v_chi_GeV_m2", "<f8"), ("Gamma_wash_over_H", "<f8"
                       ("deplete_DM_from_source", "<i4"), ("reserved", "<i4")])
 assert ctypes.sizeof(LzqOdeParams) == 24 == ODE_DTYPE.itemsize
 ODE_NT, ODE_WS_PER_POINT = 800, 3200  # LZQ_ODE_NT, LZQ_ODE_WS_PER_POINT
+ODE_OK, ODE_BAD_GRID, ODE_BAD_STEP, ODE_TOO_MANY_STEPS, ODE_NEWTON, ODE_NOT_LINEAR = range(6)  # enum lzq_ode_status
 ODE_STATUS = {0: "ok", 1: "`x` must be strictly increasing sequence.", 2: "`max_step` must be positive.",
               3: "more than max_steps integration steps", 4: "Radau stage Newton iteration did not converge",
               5: "sigma_v != 0: the quadrature form needs a linear Y_chi equation"}

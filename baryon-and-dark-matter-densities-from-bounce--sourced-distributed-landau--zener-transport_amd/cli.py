@@ -55,9 +55,9 @@ def main(argv=None):
         # fpy:385-410: build_tables + Radau (lzq_ode_batch), then fpy:412-417
         table, status = eng.ode(to_point(cfg, P=P_used), to_ode_params(cfg))
         st = int(status[0].item())
-        if st in (1, 2):  # scipy's ValueError (CubicSpline knots / solve_ivp max_step)
+        if st in (_native.ODE_BAD_GRID, _native.ODE_BAD_STEP):  # scipy's ValueError (CubicSpline / solve_ivp)
             raise ValueError(_native.ODE_STATUS[st])
-        if st == 4:  # fpy:408-410: warn, then report the state where the solver stopped
+        if st == _native.ODE_NEWTON:  # fpy:408-410: warn, then report the state where the solver stopped
             print("[warn] ODE solver reported failure:", _native.ODE_STATUS[st])
         elif st != 0:
             # LZQ_ODE_TOO_MANY_STEPS: a window needing > 2^26 fixed Radau steps (|x1-x0|/max_step,

@@ -213,7 +213,7 @@ class Engine:
             keep.append((d_pts, d_ode))
         self._keepalive = (keep, work)
         if method == "quadrature":   # sigma_v != 0 points: the Riccati equation needs Radau
-            sel = torch.nonzero(status == 5).reshape(-1).cpu().numpy()
+            sel = torch.nonzero(status == _native.ODE_NOT_LINEAR).reshape(-1).cpu().numpy()
             if sel.size:
                 t, st = self.ode(pts[sel], ods[sel], max_steps, chunk, share_tables, "radau")
                 d_sel = torch.as_tensor(sel, device=self.device)

@@ -34,7 +34,9 @@ import math
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+_HERE = os.path.dirname(os.path.abspath(__file__))
+if _HERE not in sys.path:   # lzq_binding lives next to this module
+    sys.path.insert(0, _HERE)
 import lzq_binding  # noqa: E402
 
 DEFAULTS = {"window_lz": 20.0, "steps": 1000.0}

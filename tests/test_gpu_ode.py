@@ -237,3 +237,31 @@ def test_ode_quadrature_vs_converged_reference(gpu_engine):
         assert e_b < 1e-10 and e_c < 1e-10, (c, rq, t)
         worst = max(worst, e_b, e_c)
     print(f"ODE quadrature vs converged reference: worst {worst:.2e}")
+
+
+def test_ode_quadrature_sweep_shared_and_deterministic(gpu_engine):
+    """The quadrature form through the sweep driver ("ode_method": "quadrature") equals
+    Engine.ode(method="quadrature"); shared vs per-point tables bit-identical; batch order and
+    splits do not change a result; agrees with the Radau path to the Radau path's own accuracy
+    on narrow windows (~1e-13)."""
+    import torch
+    sw = pkg("sweep")
+    spec = sw.spec_from_json({"name": "q", "base": {**NARROW}, "ode_method": "quadrature",
+                              "axes": [{"field": "Gamma_wash_over_H", "values": [0.0, 0.5, 5.0]},
+                                       {"field": "I_p", "values": [0.2, 0.6]},
+                                       {"field": "delta_LZ", "values": [1e-3, 0.1]}]})
+    out = torch.empty((12, 6), dtype=torch.float64, device=gpu_engine.device)
+    sw.make_compute(spec, gpu_engine)(0, 12, out)
+    t = out.cpu().numpy()
+    pts, ods = sw.grid_records(spec, 0, 12, gpu_engine)
+    ode = ods["Gamma_wash_over_H"] != 0
+    q, sq = gpu_engine.ode(pts[ode], ods[ode], method="quadrature")
+    assert np.array_equal(t[ode], q.cpu().numpy()) and bool((sq == 0).all())
+    q2, _ = gpu_engine.ode(pts[ode], ods[ode], method="quadrature", share_tables=False)
+    assert np.array_equal(q.cpu().numpy(), q2.cpu().numpy())
+    perm = np.random.default_rng(0).permutation(int(ode.sum()))
+    q3, _ = gpu_engine.ode(pts[ode][perm], ods[ode][perm], method="quadrature", chunk=3)
+    assert np.array_equal(q3.cpu().numpy(), q.cpu().numpy()[perm])
+    r, _ = gpu_engine.ode(pts[ode], ods[ode])
+    rr = r.cpu().numpy()
+    assert np.max(np.abs(q.cpu().numpy()[:, :2] - rr[:, :2]) / np.abs(rr[:, :2])) < 1e-11

@@ -264,9 +264,11 @@ __device__ __forceinline__ double c2_scale() { return EXPV == kExpTable ? (doubl
 
 // F(c2) = sum_k omega_k 2^(c2 g4_k) for YB independent y-nodes per lane.
 //
-// Every VALU instruction of this mixed FP64/integer stream issues in ~4 cycles on gfx950
-// (tools/ubench_valu.hip: an integer op between FP64 ops costs as much as an FP64 op), so the
-// loop is built to minimise the instruction COUNT.  Table variant, per (y, z) node:
+// The loop is VALU-issue bound: an FP64 instruction costs 4.4 cycles per wave64 on gfx950 and an
+// integer / FP32 one ~2.5 (tools/ubench_valu.hip, pure streams); in this kernel a node's 8.48
+// VALU instructions take 30.9 SIMD-cycles, 79% of them in the 6.1 FP64 FMA/MUL/ADD
+// (profiles/round2/pmc_summary.json).  So the loop is built to minimise the instruction count,
+// FP64 first.  Table variant, per (y, z) node:
 //
 //   t  = fma(c2, g, M)          M = 1.5*2^52: t = M + round(u), u = c2*g in 1/N-octave units
 //   kd = t - M                  exact

@@ -12,7 +12,9 @@ Cases:
   multi   - the 2- and 3-crossing cases of tests/test_gpu_propagator.py (K = 12) and the
             adiabatic-cell case of tests/test_propagator_math.py (K = 20);
   c5      - sweep.CrossingSpec's defaults (8 crossings 40 LZ lengths apart, jitter 0.1,
-            numpy default_rng(5), K = 20) at 8 (m_mix, |Delta'|) grid points, plus N = 16, 32.
+            numpy default_rng(5), K = 20) at 8 (m_mix, |Delta'|) grid points, plus N = 16, 32;
+  wide    - crossings hundreds of LZ lengths apart (K = 20): cells far wider than the kernel's
+            Magnus cores, so most of each cell is crossed by dressed following (round 2).
 """
 import json
 import os
@@ -58,6 +60,10 @@ def main():
         add("c5", *c5_case(m0, d0), 20.0)
     for n in (16, 32):
         add("c5", *c5_case(0.05, 0.1, n_cross=n), 20.0)
+    for m, d, x in [([0.1, 0.12], [1.0, 0.8], [0.0, 400.0]),                  # delta 0.017, 0.03
+                    ([0.6, 0.5, 0.7], [0.2, 0.25, 0.3], [0.0, 150.0, 260.0]),  # delta 3, 1.7, 2.7
+                    ([1.0, 0.9], [0.1, 0.12], [0.0, 300.0])]:                  # delta 16.7 (adiabatic), 11.25
+        add("wide", m, d, x, 20.0)
     with open(os.path.join(HERE, "golden_weber.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(len(out["cases"]), "cases")

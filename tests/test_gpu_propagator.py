@@ -82,4 +82,4 @@ def test_kernel_vs_exact_weber_solution(gpu_engine):
             got = gpu_engine.lz_propagate(m, d, x, g["v_w"], K, S).cpu().numpy()
             assert np.all(np.abs(got - ex) <= tol), (N, K, S, np.abs(got - ex).max())
         n += len(cs)
-    assert n == len(g["cases"]) == 50
+    assert n == len(g["cases"]) == 53

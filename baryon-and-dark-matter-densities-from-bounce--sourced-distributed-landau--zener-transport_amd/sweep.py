@@ -261,32 +261,74 @@ def prepare_out_dir(out_dir: str, spec: SweepSpec, resume: bool, rank: int = 0) 
 ComputeFn = Callable[[int, int, "object"], None]  # (start, count, out_tensor[count, 6]) -> None
 
 
+def _save_shard(path: str, arr: np.ndarray) -> None:
+    tmp = path + ".tmp.npy"
+    np.save(tmp, arr, allow_pickle=False)
+    os.replace(tmp, path)
+
+
 def run_local(compute: ComputeFn, start: int, end: int, make_out: Callable[[int], "object"], chunk: int,
               out_dir: Optional[str] = None, resume: bool = False, sync: Callable[[], None] = lambda: None,
               log: Callable[[str], None] = lambda s: None, key: str = ""):
     """Evaluate [start, end) in chunks into one (end-start, 6) tensor, with optional
-    per-chunk checkpoint files (named by `key`, see spec_key)."""
+    per-chunk checkpoint files (named by `key`, see spec_key).
+
+    On the GPU the checkpoint of chunk i is copied out on a side stream (device -> pinned host
+    memory, ordered after chunk i's kernels by an event) and written by a worker thread while
+    chunk i+1 computes, so checkpointing does not serialise the sweep.  On CPU tensors (tests)
+    it is written inline."""
     import torch
     local = make_out(end - start)
-    done = 0
-    for c0 in range(start, end, chunk):
-        n = min(chunk, end - c0)
-        view = local[c0 - start:c0 - start + n]
-        path = _shard_file(out_dir, c0, n, key) if out_dir else None
-        if path and resume and os.path.exists(path):
-            arr = np.load(path, allow_pickle=False)
-            if arr.shape != (n, 6):
-                raise RuntimeError(f"checkpoint {path} has shape {arr.shape}, expected {(n, 6)}")
-            view.copy_(torch.from_numpy(arr))
-            log(f"resumed {path}")
-            continue
-        compute(c0, n, view)
-        if path:
-            sync()
-            tmp = path + ".tmp.npy"
-            np.save(tmp, view.detach().cpu().numpy(), allow_pickle=False)
-            os.replace(tmp, path)
-        done += n
+    on_gpu = bool(getattr(local, "is_cuda", False)) and out_dir is not None
+    pending = []
+    if on_gpu:
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(max_workers=1)
+        copy_stream = torch.cuda.Stream(device=local.device)
+
+    def flush(block: bool):
+        while pending and (block or pending[0][0].done()):
+            fut, _ = pending.pop(0)
+            fut.result()   # re-raise a failed write here
+
+    try:
+        for c0 in range(start, end, chunk):
+            n = min(chunk, end - c0)
+            view = local[c0 - start:c0 - start + n]
+            path = _shard_file(out_dir, c0, n, key) if out_dir else None
+            if path and resume and os.path.exists(path):
+                arr = np.load(path, allow_pickle=False)
+                if arr.shape != (n, 6):
+                    raise RuntimeError(f"checkpoint {path} has shape {arr.shape}, expected {(n, 6)}")
+                view.copy_(torch.from_numpy(arr))
+                log(f"resumed {path}")
+                continue
+            compute(c0, n, view)
+            if not path:
+                continue
+            if not on_gpu:
+                sync()
+                _save_shard(path, view.detach().cpu().numpy())
+                continue
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(local.device))
+            host = torch.empty(view.shape, dtype=view.dtype, pin_memory=True)
+            with torch.cuda.stream(copy_stream):
+                copy_stream.wait_event(ev)
+                host.copy_(view, non_blocking=True)
+                done_ev = torch.cuda.Event()
+                done_ev.record(copy_stream)
+
+            def write(path=path, host=host, done_ev=done_ev):
+                done_ev.synchronize()
+                _save_shard(path, host.numpy())
+            pending.append((pool.submit(write), host))
+            flush(block=False)
+        if on_gpu:
+            flush(block=True)
+    finally:
+        if on_gpu:
+            pool.shutdown(wait=True)
     return local
 
 

@@ -71,3 +71,17 @@ def test_batch_matches_single():
 def test_regime_auto_is_an_error():
     with pytest.raises(UnboundLocalError):
         O.point_yields(full_cfg({**BASE_CFG, "regime": "auto"}))
+
+
+def test_oracle_under_asan_ubsan():
+    """The CPU restatement built with -fsanitize=address,undefined (oracle/asan_driver.c,
+    `make -C oracle asan-check`): quadrature, closed form, ODE paths run clean."""
+    import os
+    import subprocess
+    here = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")
+    subprocess.run(["make", "-s", "-C", here, "asan-check"], check=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([os.path.join(here, "_build", "asan_driver")], capture_output=True, text=True, env=env,
+                       timeout=300)
+    assert r.returncode == 0, (r.stdout, r.stderr[-3000:])
+    assert "ok (0 failures)" in r.stdout

@@ -304,6 +304,7 @@ def run_local(compute: ComputeFn, start: int, end: int, make_out: Callable[[int]
                 log(f"resumed {path}")
                 continue
             compute(c0, n, view)
+            log(f"chunk [{c0}, {c0 + n}) launched")
             if not path:
                 continue
             if not on_gpu:

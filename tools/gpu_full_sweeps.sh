@@ -1,0 +1,14 @@
+# GPU box: the full BASELINE C3 (1e7 points) and C4 (1e8 points) grids through the sweep CLI on
+# ONE GPU, checkpointing to local /tmp (not merged back); summaries -> gpurun_out/sweeps/.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
+mkdir -p gpurun_out/sweeps
+PKG=baryon-and-dark-matter-densities-from-bounce--sourced-distributed-landau--zener-transport_amd
+for S in C3 C4; do
+  rm -rf /tmp/sweep_$S
+  timeout -k 10 500 python -u -m $PKG.sweep --spec $S --out /tmp/sweep_$S > gpurun_out/sweeps/$S.log 2>&1 || { tail -5 gpurun_out/sweeps/$S.log; exit 1; }
+  tail -1 gpurun_out/sweeps/$S.log
+  python -c "import json,sys; d=json.load(open('/tmp/sweep_$S/summary.json')); d.pop('spec_def'); json.dump(d, open('gpurun_out/sweeps/${S}_summary.json','w'), indent=1)"
+  rm -rf /tmp/sweep_$S
+done
+echo all-done

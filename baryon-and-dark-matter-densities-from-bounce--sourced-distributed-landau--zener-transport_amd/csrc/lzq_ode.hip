@@ -278,6 +278,29 @@ __device__ __forceinline__ RadauH radau_h(const Radau& R, double h) {
   return r;
 }
 
+// x = M^-1 b by the adjugate (one division for all three components), for the Newton stage
+// systems M = I - hA diag(jf) of the Riccati equation: well conditioned like the Y_B system
+// (jf = -2 lam Z <= 0 near the solution), so the cofactor form loses nothing against pivoted
+// elimination (tests/test_gpu_ode.py: oracle at 1e-11, stiff cases at 1e-10 of converged).
+__device__ __forceinline__ void solve3_adj(const double (&M)[3][3], double (&b)[3]) {
+  const double a00 = M[1][1] * M[2][2] - M[1][2] * M[2][1];
+  const double a01 = M[0][2] * M[2][1] - M[0][1] * M[2][2];
+  const double a02 = M[0][1] * M[1][2] - M[0][2] * M[1][1];
+  const double a10 = M[1][2] * M[2][0] - M[1][0] * M[2][2];
+  const double a11 = M[0][0] * M[2][2] - M[0][2] * M[2][0];
+  const double a12 = M[0][2] * M[1][0] - M[0][0] * M[1][2];
+  const double a20 = M[1][0] * M[2][1] - M[1][1] * M[2][0];
+  const double a21 = M[0][1] * M[2][0] - M[0][0] * M[2][1];
+  const double a22 = M[0][0] * M[1][1] - M[0][1] * M[1][0];
+  const double id = 1.0 / (M[0][0] * a00 + M[0][1] * a10 + M[0][2] * a20);
+  const double x0 = (a00 * b[0] + a01 * b[1] + a02 * b[2]) * id;
+  const double x1 = (a10 * b[0] + a11 * b[1] + a12 * b[2]) * id;
+  const double x2 = (a20 * b[0] + a21 * b[1] + a22 * b[2]) * id;
+  b[0] = x0;
+  b[1] = x1;
+  b[2] = x2;
+}
+
 // One Radau step for both equations (hA = h * A of the step); false when the Y_chi Newton
 // iteration fails.  The stage sums are explicit fmas (hA_ij * f_j + acc); only the last stage
 // of each equation is the step's result, so the linear cases form only what they need.
@@ -325,7 +348,11 @@ __device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st
       }
       g[i] = -acc;
     }
+#if LZQ_ODE_FASTMATH
+    solve3_adj(M, g);
+#else
     solve3(M, g);
+#endif
     double dmax = 0.0, zmax = 0.0;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {

@@ -104,6 +104,9 @@ __device__ __forceinline__ double spline_eval(const OdePoint& o, const double* _
   return res;
 }
 
+#ifndef LZQ_ODE_PREDICT
+#define LZQ_ODE_PREDICT 1  // Radau5 collocation predictor for the Riccati Newton iteration
+#endif
 #ifndef LZQ_ODE_FASTMATH
 #define LZQ_ODE_FASTMATH 1  // 0: IEEE division and ROCm exp in the stage function (tools/ablate_ode.py)
 #endif
@@ -304,7 +307,19 @@ __device__ __forceinline__ void solve3_adj(const double (&M)[3][3], double (&b)[
 // One Radau step for both equations (hA = h * A of the step); false when the Y_chi Newton
 // iteration fails.  The stage sums are explicit fmas (hA_ij * f_j + acc); only the last stage
 // of each equation is the step's result, so the linear cases form only what they need.
-__device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st)[3], double& Ychi, double& YB) {
+// Newton starting values for the next step's Riccati stages: the previous step's collocation
+// polynomial (through Y at its start and its three stage values, nodes 0, c1, c2, 1) evaluated
+// at 1 + c_j (Lagrange weights, mpmath): the standard Radau5 predictor.
+__constant__ double kRadauPred[3][4] = {
+    {-0x1.94f343c8b1118p-1, 0x1.6c62e7ee47cd1p+0, -0x1.98b0a4fff4ae1p+0, 0x1.f6c75ef60569bp+0},
+    {-0x1.337d989041bbbp+3, 0x1.0879f93eee39dp+4, -0x1.c2e1b2531e4efp+3, 0x1.056b586583971p+3},
+    {-0x1.9000000000000p+4, 0x1.51cdd7dde1522p+5, -0x1.07232d3336a77p+5, 0x1.0aaaaaaaaaaabp+4}};
+
+// Zs: in, Newton starting stages when `guess` (else Ychi for all three); out, the converged
+// stages (the next predictor's data).  A predicted start that does not converge is retried
+// from Ychi, so the predictor can only save iterations, never lose a step.
+__device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st)[3], double& Ychi, double& YB,
+                                           double (&Zs)[3], bool guess) {
   // Y_B: (I + hA diag(beta)) Z = YB + hA alpha, exactly; Z_3 = Y_B(x + h)
   {
     double M[3][3], b[3];
@@ -329,7 +344,8 @@ __device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st
     Ychi = acc;
     return true;
   }
-  double Z[3] = {Ychi, Ychi, Ychi};
+  for (int attempt = guess ? 0 : 1; attempt < 2; ++attempt) {
+  double Z[3] = {attempt == 0 ? Zs[0] : Ychi, attempt == 0 ? Zs[1] : Ychi, attempt == 0 ? Zs[2] : Ychi};
   for (int it = 0; it < 40; ++it) {
     double M[3][3], g[3];
     double f[3], jf[3];
@@ -361,9 +377,13 @@ __device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st
       zmax = pymax(zmax, fabs(Z[i]));
     }
     if (!(dmax > 1e-15 * zmax)) {
+      Zs[0] = Z[0];
+      Zs[1] = Z[1];
+      Zs[2] = Z[2];
       Ychi = Z[2];
       return true;
     }
+  }
   }
   return false;
 }
@@ -504,18 +524,30 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
     // the same with its own T; tests/golden/golden_ode_stiff.json).
     const double xb = branch_x(o, x0, x1);
     const RadauH hA = radau_h(R, h);
+    const bool riccati = LZQ_ODE_PREDICT && o.sigmav != 0.0;
+    double Zs[3] = {Ychi, Ychi, Ychi}, Yp = Ychi;  // previous step's start and stages (predictor)
+    bool have = false;
     for (int64_t k = 0; k < N; ++k) {
       const double xk = x0 + (double)k * h;
       const bool split = xk < xb && xb <= xk + h;  // the last stage (x = xk + h) would see the other branch
       const double xa = split ? nextafter(xb, -INFINITY) : xk + h;
       double YB_prev = YB;
       bool ok = true;
+      const double Ystart = Ychi;
+      if (riccati && have && !split) {
+        double g[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          g[j] = kRadauPred[j][0] * Yp + kRadauPred[j][1] * Zs[0] + kRadauPred[j][2] * Zs[1] + kRadauPred[j][3] * Zs[2];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) Zs[j] = g[j];
+      }
       if (xa > xk) {
         const double hs = split ? xa - xk : h;
         OdeStage sg[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j) sg[j] = ode_stage(o, w, xk + R.c[j] * hs);
-        ok = radau_step(split ? radau_h(R, hs) : hA, sg, Ychi, YB);
+        ok = radau_step(split ? radau_h(R, hs) : hA, sg, Ychi, YB, Zs, riccati && have && !split);
       }
       if (ok && split && xk + h > xb) {
         const double hs = (xk + h) - xb;
@@ -523,8 +555,10 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
         YB_prev = YB;
 #pragma unroll
         for (int j = 0; j < 3; ++j) sg[j] = ode_stage(o, w, xb + R.c[j] * hs);
-        ok = radau_step(radau_h(R, hs), sg, Ychi, YB);
+        ok = radau_step(radau_h(R, hs), sg, Ychi, YB, Zs, false);
       }
+      have = !split;   // the predictor needs a full regular step behind it
+      Yp = Ystart;
       if (!ok) {
         YB = YB_prev;  // report the state at the start of the failed step, like sol.y[:, -1] (fpy:408-410)
         st = LZQ_ODE_NEWTON;

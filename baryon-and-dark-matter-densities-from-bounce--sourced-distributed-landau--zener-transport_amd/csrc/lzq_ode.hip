@@ -534,11 +534,18 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
       double YB_prev = YB;
       bool ok = true;
       const double Ystart = Ychi;
+      bool use_guess = false;
       if (riccati && have && !split) {
+        // the Riccati stage system has a second (unstable, other-sign) root: a predicted start
+        // is used only when it stays within 25% of Y_chi, where Newton converges to the same
+        // root as from Y_chi itself (an extrapolation across a fast transient can overshoot)
         double g[3];
+        use_guess = true;
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
+        for (int j = 0; j < 3; ++j) {
           g[j] = kRadauPred[j][0] * Yp + kRadauPred[j][1] * Zs[0] + kRadauPred[j][2] * Zs[1] + kRadauPred[j][3] * Zs[2];
+          use_guess = use_guess && fabs(g[j] - Ychi) <= 0.25 * fabs(Ychi);
+        }
 #pragma unroll
         for (int j = 0; j < 3; ++j) Zs[j] = g[j];
       }
@@ -547,7 +554,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
         OdeStage sg[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j) sg[j] = ode_stage(o, w, xk + R.c[j] * hs);
-        ok = radau_step(split ? radau_h(R, hs) : hA, sg, Ychi, YB, Zs, riccati && have && !split);
+        ok = radau_step(split ? radau_h(R, hs) : hA, sg, Ychi, YB, Zs, use_guess);
       }
       if (ok && split && xk + h > xb) {
         const double hs = (xk + h) - xb;

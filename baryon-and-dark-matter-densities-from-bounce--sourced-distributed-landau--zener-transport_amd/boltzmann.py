@@ -46,6 +46,15 @@ class BoltzmannSystem:
         self.m = float(cfg.m_chi_GeV)
         self.aov = AoverVKernel(cfg.I_p, cfg.beta_over_H, cfg.T_p_GeV, cfg.v_w, cfg.g_star)
 
+    # Cosmology/thermo wrappers (fpy:203-204; scalar host arithmetic, not on the hot path)
+    def H(self, T: float) -> float:
+        from .physics_host import H_std
+        return H_std(T, self.cfg.g_star)
+
+    def s(self, T: float) -> float:
+        from .physics_host import s_entropy
+        return s_entropy(T, self.cfg.g_star_s)
+
     def J_chi(self, T: float) -> float:
         """fpy:222-223."""
         return float(self.J_chi_T([T])[0])

@@ -155,3 +155,14 @@ def test_hook_does_not_mask_library_failures(monkeypatch, tmp_path):
         lz.try_compute_P_from_profile("x.csv", 0.3)
     stub.compute_lambda_eff_from_profile = lambda path: 1 / 0
     assert lz.try_compute_P_from_profile("x.csv", 0.3) is None
+
+
+def test_boltzmann_scalar_wrappers():
+    """BoltzmannSystem.H / .s (fpy:203-204) exist with the reference's formulas (fpy:84-88)."""
+    import math
+    B = pkg("boltzmann")
+    cfg = pkg("config").Config(P_chi_to_B=0.1)
+    bs = B.BoltzmannSystem.__new__(B.BoltzmannSystem)   # no GPU: only the scalar wrappers
+    bs.cfg = cfg
+    assert bs.H(100.0) == 1.66 * math.sqrt(cfg.g_star) * 100.0 * 100.0 / 1.220890e19
+    assert bs.s(100.0) == (2.0 * math.pi ** 2 / 45.0) * cfg.g_star_s * 100.0 ** 3

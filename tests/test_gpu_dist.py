@@ -67,3 +67,24 @@ def test_bench_two_ranks_gloo():
     assert r["value"] > 0 and r["unit"] == "points/s" and r["scaling"] == "weak"
     assert abs(r["value"] - 40000 / (r["ms_per_step"] / 1e3)) <= 1e-6 * r["value"]
     assert "cpu_baseline" not in r   # rank 0 at N = 1 only
+
+
+def test_bench_single_rank_line():
+    """bench.py at N = 1 (small): one JSON line with the contract's fields, a roofline fraction
+    in (0, 1] from executed FP64 FLOP, and the CPU baseline on every CPU of this job."""
+    out = run([sys.executable, "bench.py", "--steps", "1", "--warmup", "1", "--points", "50000",
+               "--cpu-seconds", "1"], 300)
+    recs = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+    assert len(recs) == 1
+    r = recs[0]
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in r, k
+    assert r["n_gpus"] == 1 and r["dtype"] == "f64" and r["config"]["points_per_gpu"] == 50000
+    rf = r["roofline"]
+    assert rf["unit"] == "TFLOP/s" and rf["peak"] == 78.6
+    assert rf["frac"] is not None and 0.0 < rf["frac"] <= 1.0, rf
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-12
+    assert rf["stock_exp_equivalent"]["achieved"] > rf["achieved"]
+    cb = r["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["cores"] == cb["host"]["usable"] and cb["value"] > 0

@@ -111,7 +111,7 @@ def load(path: str | None = None):
     L.lzq_ode_tables.argtypes = [vp, i64, vp, vp, vp, i64, vp, vp]
     L.lzq_ode_integrate.argtypes = [vp, vp, i64, vp, i64, i64, vp, vp, vp]
     L.lzq_ode_integrate_shared.argtypes = [vp, vp, i64, vp, i64, vp, i64, i64, vp, vp, vp]
-    L.lzq_ode_quadrature.argtypes = [vp, vp, i64, vp, i64, vp, i64, vp, vp, vp]
+    L.lzq_ode_quadrature.argtypes = [vp, vp, i64, vp, i64, vp, i64, i64, vp, vp, vp]
     L.lzq_ode_batch.argtypes = [vp, vp, i64, vp, i64, i64, vp, vp, vp]
     L.lzq_ode_aov_T.argtypes = [P(LzqPoint), d, d, vp, vp, i64, vp, vp]
     L.lzq_ode_rhs.argtypes = [P(LzqPoint), P(LzqOdeParams), d, d, vp, vp, vp, i64, vp, vp]

@@ -184,6 +184,34 @@ __device__ __forceinline__ OdeStage ode_stage(const OdePoint& o, const double* _
   return st;
 }
 
+// The Y_chi-only stage of the Riccati equation with no source term (deplete off):
+// lam = sigma_v s/(H x), E2 = (n_eq/s)^2, S = 0 -- no spline, no window (ode_stage's
+// operations otherwise).  alpha / beta are not formed (Y_B comes from the quadrature).
+__device__ __forceinline__ OdeStage ode_stage_chi(const OdePoint& o, double x) {
+  const double xc = pymax(x, 1e-30);
+  const double ixc = rcp_pos(xc);
+  const double T = o.m * ixc;
+  const double iT = T >= 1e-30 ? xc * o.inv_m : 1e30;
+  const double H = pymax(o.H0 * T * T * kInvMplGeV, 1e-300);
+  const double T3 = (T * T) * T;
+  const double s = pymax(o.s0 * T3, 1e-300);
+  double n_eq;
+  if (T > o.m3) n_eq = o.c_rel * T3;
+  else n_eq = o.c_nr * (T * sqrt(T)) * exp_nonpos(-o.m * iT);
+  const bool plain = H > 1e-290 && s > 1e-290 && x == xc;
+  const double iT2 = iT * iT;
+  const double is = plain ? (iT2 * iT) * o.inv_s0 : 1.0 / s;
+  const double E = n_eq * is;
+  const double iHx = plain ? (o.mpl_over_h0 * iT2) * ixc : 1.0 / (H * x);
+  OdeStage st;
+  st.lam = (o.sigmav * s) * iHx;
+  st.E2 = E * E;
+  st.S = 0.0;
+  st.alpha = 0.0;
+  st.beta = 0.0;
+  return st;
+}
+
 // CubicSpline's check of the knots linspace(T_lo, T_hi, 800): strictly increasing.
 __device__ __forceinline__ bool ode_grid_ok(double T_lo, double T_hi, double stepT) {
   bool ok = true;
@@ -318,10 +346,11 @@ __constant__ double kRadauPred[3][4] = {
 // Zs: in, Newton starting stages when `guess` (else Ychi for all three); out, the converged
 // stages (the next predictor's data).  A predicted start that does not converge is retried
 // from Ychi, so the predictor can only save iterations, never lose a step.
+template <bool kWithYB = true>
 __device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st)[3], double& Ychi, double& YB,
                                            double (&Zs)[3], bool guess) {
   // Y_B: (I + hA diag(beta)) Z = YB + hA alpha, exactly; Z_3 = Y_B(x + h)
-  {
+  if (kWithYB) {
     double M[3][3], b[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -479,6 +508,11 @@ __device__ __forceinline__ double branch_x(const OdePoint& o, double x0, double 
 
 // tidx (optional): point i reads the spline table at ws[tidx[i] * kOdeWS] (tables shared by
 // points with the same A/V kernel and window, lzq_ode_integrate_shared); NULL: its own, ws[i].
+// kChiOnly (lzq_ode_quadrature, sigma_v != 0 points): Y_B is already in out[i] from the
+// quadrature (exact for every sigma_v: its equation is linear); step only the Riccati equation
+// of Y_chi, with ode_stage_chi when there is no source term.  Points with sigma_v = 0 return
+// at once (the quadrature has done both).
+template <bool kChiOnly>
 __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_kernel(const lzq_point* __restrict__ pts,
                                                                   const lzq_ode_params* __restrict__ ode, int64_t n,
                                                                   const int32_t* __restrict__ tidx,
@@ -489,6 +523,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
   if (i >= n) return;
   const lzq_point pt = pts[i];
   const OdePoint o = ode_point(pt, ode[i]);
+  if (kChiOnly && (o.sigmav == 0.0 || (status && status[i] != LZQ_ODE_NOT_LINEAR))) return;
   const double* w = ws + (tidx ? (int64_t)tidx[i] : i) * (int64_t)kOdeWS;
   const double nan = __builtin_nan("");
   lzq_yield r = {nan, nan, nan, nan, nan, pt.P_chi_to_B};
@@ -503,7 +538,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
   } else {  // thermal, and the fallback branch fpy:398-399 (no UnboundLocalError on this path)
     Ychi = n_chi_eq(o.T_hi, m, pt.g_chi, pt.stats) / s_entropy(o.T_hi, pt.g_star_s);
   }
-  double YB = 0.0;
+  double YB = kChiOnly ? out[i].Y_B : 0.0;
   const double x_p = m / pymax(T_p, 1e-30);
   const double max_step = pymin(pymin(fabs(x1 - x0) / 20000.0, x_p / 1000.0), 5e-4);  // fpy:403-404
   double steps = 0.0;
@@ -553,16 +588,18 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
         const double hs = split ? xa - xk : h;
         OdeStage sg[3];
 #pragma unroll
-        for (int j = 0; j < 3; ++j) sg[j] = ode_stage(o, w, xk + R.c[j] * hs);
-        ok = radau_step(split ? radau_h(R, hs) : hA, sg, Ychi, YB, Zs, use_guess);
+        for (int j = 0; j < 3; ++j)
+          sg[j] = (kChiOnly && !o.deplete) ? ode_stage_chi(o, xk + R.c[j] * hs) : ode_stage(o, w, xk + R.c[j] * hs);
+        ok = radau_step<!kChiOnly>(split ? radau_h(R, hs) : hA, sg, Ychi, YB, Zs, use_guess);
       }
       if (ok && split && xk + h > xb) {
         const double hs = (xk + h) - xb;
         OdeStage sg[3];
         YB_prev = YB;
 #pragma unroll
-        for (int j = 0; j < 3; ++j) sg[j] = ode_stage(o, w, xb + R.c[j] * hs);
-        ok = radau_step(radau_h(R, hs), sg, Ychi, YB, Zs, false);
+        for (int j = 0; j < 3; ++j)
+          sg[j] = (kChiOnly && !o.deplete) ? ode_stage_chi(o, xb + R.c[j] * hs) : ode_stage(o, w, xb + R.c[j] * hs);
+        ok = radau_step<!kChiOnly>(radau_h(R, hs), sg, Ychi, YB, Zs, false);
       }
       have = !split;   // the predictor needs a full regular step behind it
       Yp = Ystart;
@@ -661,13 +698,11 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_QUAD_MIN_WAVES) void ode_quad_kernel
   const double* w = ws + (tidx ? (int64_t)tidx[i] : i) * (int64_t)kOdeWS;
   const double nan = __builtin_nan("");
   lzq_yield r = {nan, nan, nan, nan, nan, pt.P_chi_to_B};
-  int st = LZQ_OK;
-  if (o.sigmav != 0.0) st = LZQ_ODE_NOT_LINEAR;
   // CubicSpline's strictly-increasing check, knots split over the lanes
   bool ok = true;
   for (int k = lane + 1; k < kOdeNT; k += kW)
     ok = ok && linspace_at(o.T_lo, o.T_hi, o.stepT, k, kOdeNT) > linspace_at(o.T_lo, o.T_hi, o.stepT, k - 1, kOdeNT);
-  if (st == LZQ_OK && __any(!ok)) st = LZQ_ODE_BAD_GRID;
+  int st = __any(!ok) ? LZQ_ODE_BAD_GRID : (o.sigmav != 0.0 ? LZQ_ODE_NOT_LINEAR : LZQ_OK);
   const double m = o.m, T_p = o.Tp;
   const double x1 = m / pymax(o.T_lo, 1e-30);  // fpy:388
   const double ix1 = 1.0 / x1;
@@ -680,7 +715,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_QUAD_MIN_WAVES) void ode_quad_kernel
     Ychi = n_chi_eq(o.T_hi, m, pt.g_chi, pt.stats) / s_entropy(o.T_hi, pt.g_star_s);
   }
   double accB = 0.0, accC = 0.0;
-  if (st == LZQ_OK) {
+  if (st == LZQ_OK || st == LZQ_ODE_NOT_LINEAR) {  // Y_B's equation is linear for every sigma_v
     const double gam = o.gamma_w;
     const double Bt = o.B * T_p * T_p;
     for (int k = lane; k < kOdeNT - 1; k += kW) {
@@ -725,6 +760,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_QUAD_MIN_WAVES) void ode_quad_kernel
     accC += __shfl_xor(accC, d, kW);
   }
   if (lane != 0) return;
+  if (st == LZQ_ODE_NOT_LINEAR) r.Y_B = accB;  // Y_chi: the Riccati stepping (ode_integrate_kernel<true>)
   if (st == LZQ_OK) {  // fpy:412-417
     const double YB = accB;
     if (o.deplete) Ychi = Ychi - accC;
@@ -822,7 +858,7 @@ int lzq_ode_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, in
   if (n > 0 && (!d_points || !d_ode || !d_out)) return lzq_set_error(LZQ_EINVAL, "lzq_ode_integrate: bad arguments");
   if (max_steps < 0) return lzq_set_error(LZQ_EINVAL, "lzq_ode_integrate: max_steps < 0");
   if (n == 0) return LZQ_OK;
-  hipLaunchKernelGGL(lzq::ode_integrate_kernel, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0,
+  hipLaunchKernelGGL(lzq::ode_integrate_kernel<false>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0,
                      (hipStream_t)stream, d_points, d_ode, n, (const int32_t*)nullptr, d_work, max_steps, d_out,
                      d_status);
   return hip_check(hipGetLastError(), "lzq_ode_integrate");
@@ -839,15 +875,15 @@ int lzq_ode_integrate_shared(const lzq_point* d_points, const lzq_ode_params* d_
   if (max_steps < 0) return lzq_set_error(LZQ_EINVAL, "lzq_ode_integrate_shared: max_steps < 0");
   if (ode_blocks(n) > 2147483647LL) return lzq_set_error(LZQ_EINVAL, "lzq_ode_integrate_shared: n too large");
   if (n == 0) return LZQ_OK;
-  hipLaunchKernelGGL(lzq::ode_integrate_kernel, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0,
+  hipLaunchKernelGGL(lzq::ode_integrate_kernel<false>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0,
                      (hipStream_t)stream, d_points, d_ode, n, d_table_index, d_work, max_steps, d_out, d_status);
   return hip_check(hipGetLastError(), "lzq_ode_integrate_shared");
 }
 
 int lzq_ode_quadrature(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n,
                        const int32_t* d_table_index, int64_t n_tables, const double* d_work, int64_t work_doubles,
-                       lzq_yield* d_out, int32_t* d_status, void* stream) {
-  if (n < 0 || n_tables < 0 || (n > 0 && (!d_points || !d_ode || !d_out)) ||
+                       int64_t max_steps, lzq_yield* d_out, int32_t* d_status, void* stream) {
+  if (n < 0 || n_tables < 0 || max_steps < 0 || (n > 0 && (!d_points || !d_ode || !d_out)) ||
       (d_table_index && n > 0 && n_tables == 0))
     return lzq_set_error(LZQ_EINVAL, "lzq_ode_quadrature: bad arguments");
   int rc = check_ws(d_table_index ? n_tables : n, d_work, work_doubles, "lzq_ode_quadrature");
@@ -857,6 +893,11 @@ int lzq_ode_quadrature(const lzq_point* d_points, const lzq_ode_params* d_ode, i
   if (nb > 2147483647LL) return lzq_set_error(LZQ_EINVAL, "lzq_ode_quadrature: n too large");
   hipLaunchKernelGGL(lzq::ode_quad_kernel, dim3((unsigned)nb), dim3(lzq::kOdeBlock), 0, (hipStream_t)stream, d_points,
                      d_ode, n, d_table_index, d_work, d_out, d_status);
+  rc = hip_check(hipGetLastError(), "lzq_ode_quadrature");
+  if (rc) return rc;
+  // sigma_v != 0: Y_chi's Riccati equation by the Radau stepping (Y_B from the quadrature above)
+  hipLaunchKernelGGL(lzq::ode_integrate_kernel<true>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0,
+                     (hipStream_t)stream, d_points, d_ode, n, d_table_index, d_work, max_steps, d_out, d_status);
   return hip_check(hipGetLastError(), "lzq_ode_quadrature");
 }
 

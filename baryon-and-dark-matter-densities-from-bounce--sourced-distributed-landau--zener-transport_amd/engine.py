@@ -156,8 +156,9 @@ class Engine:
         one table (lzq_ode_integrate_shared; bit-identical results, one A/V table per distinct
         kernel instead of per point).
         method: "radau" (default: the reference's integrator, fixed steps) or "quadrature"
-        (lzq_ode_quadrature: the converged solution of the sigma_v = 0 equations by quadrature,
-        opt-in; points with sigma_v != 0 are integrated by Radau)."""
+        (lzq_ode_quadrature, opt-in: Y_B -- and Y_chi when sigma_v = 0 -- by the exact
+        integrating-factor quadrature; with sigma_v != 0, Y_chi's Riccati equation is stepped
+        alone by Radau)."""
         if method not in ("radau", "quadrature"):
             raise ValueError(f"method must be 'radau' or 'quadrature', got {method!r}")
         pts = np.ascontiguousarray(points, dtype=_native.POINT_DTYPE).reshape(-1)
@@ -193,7 +194,7 @@ class Engine:
                                                             None, self._stream()))
                         keep.append((d_rep, d_idx))
                     self._check(self.lib.lzq_ode_quadrature(_vp(d_pts), _vp(d_ode), c1 - c0, _vp(d_idx), n_tab,
-                                                            _vp(work), work.numel(), _vp(out[c0:c1]),
+                                                            _vp(work), work.numel(), int(max_steps), _vp(out[c0:c1]),
                                                             _vp(status[c0:c1]), self._stream()))
                 elif rep is None:
                     self._check(self.lib.lzq_ode_batch(_vp(d_pts), _vp(d_ode), c1 - c0, _vp(work), work.numel(),
@@ -212,13 +213,6 @@ class Engine:
                     keep.append((d_rep, d_idx))
             keep.append((d_pts, d_ode))
         self._keepalive = (keep, work)
-        if method == "quadrature":   # sigma_v != 0 points: the Riccati equation needs Radau
-            sel = torch.nonzero(status == _native.ODE_NOT_LINEAR).reshape(-1).cpu().numpy()
-            if sel.size:
-                t, st = self.ode(pts[sel], ods[sel], max_steps, chunk, share_tables, "radau")
-                d_sel = torch.as_tensor(sel, device=self.device)
-                out[d_sel] = t
-                status[d_sel] = st
         return out, status
 
     def ode_aov_T(self, point, T_lo: float, T_hi: float, work_point: torch.Tensor, Ts) -> torch.Tensor:

@@ -173,7 +173,7 @@ enum lzq_ode_status {
   LZQ_ODE_BAD_GRID = 1,       /* T grid not strictly increasing: CubicSpline raises ValueError */
   LZQ_ODE_BAD_STEP = 2,       /* max_step <= 0 (zero-width x range): solve_ivp raises ValueError */
   LZQ_ODE_TOO_MANY_STEPS = 3, /* more than max_steps integration steps: not attempted */
-  LZQ_ODE_NOT_LINEAR = 5,     /* lzq_ode_quadrature: sigma_v != 0 (Riccati in Y_chi): use Radau */
+  LZQ_ODE_NOT_LINEAR = 5,     /* internal to lzq_ode_quadrature: Y_chi still to be stepped */
   LZQ_ODE_NEWTON = 4          /* a Radau stage system did not converge: the yields are the
                                  state at the start of the failed step (fpy:408-410 reports
                                  sol.y[:, -1] after a failed solve) */
@@ -212,19 +212,21 @@ int lzq_ode_integrate_shared(const lzq_point* d_points, const lzq_ode_params* d_
                              int64_t work_doubles, int64_t max_steps, lzq_yield* d_out, int32_t* d_status,
                              void* stream);
 
-/* Converged quadrature form of the fallback for sigma_v = 0 points (opt-in; not the
- * reference's method).  With sigma_v = 0 both equations of fpy:270-286 are linear with known
- * integrating factors, so Y_B(x1) = int alpha(x) (x/x1)^Gamma_wash dx and
- * Y_chi(x1) = Y_chi(x0) - [deplete] int alpha(x) dx, alpha = (SB/s)/(H x), exactly; both are
+/* Quadrature form of the fallback (opt-in; not the reference's method).  Y_B's equation of
+ * fpy:270-286 is linear with integrating factor (x/x1)^Gamma_wash for every sigma_v, so
+ * Y_B(x1) = int alpha(x) (x/x1)^Gamma_wash dx, alpha = (SB/s)/(H x), exactly; with
+ * sigma_v = 0 so is Y_chi's: Y_chi(x1) = Y_chi(x0) - [deplete] int alpha(x) dx.  Both are
  * integrated over the built spline tables (knot intervals split at T = m/3 and into
  * sub-intervals below the window / integrating-factor / Boltzmann scales, 8-point
- * Gauss-Legendre), one wavefront per point.  The result is the converged solution of the
- * reference's equations (the reference's own rtol-1e-8 Radau sits up to ~2e-8 from it on wide
- * windows).  Points with sigma_v != 0 get LZQ_ODE_NOT_LINEAR and NaN yields.  d_table_index:
- * optional shared tables as in lzq_ode_integrate_shared (NULL: table i for point i). */
+ * Gauss-Legendre), one wavefront per point: the converged solution of the reference's
+ * equations (the reference's own rtol-1e-8 Radau sits up to ~2e-8 from it on wide windows).
+ * For sigma_v != 0 points Y_chi's Riccati equation is then stepped alone by the Radau
+ * integrator (max_steps as lzq_ode_integrate; without a source term its stages need neither
+ * the spline nor the window).  d_table_index: optional shared tables as in
+ * lzq_ode_integrate_shared (NULL: table i for point i). */
 int lzq_ode_quadrature(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n,
                        const int32_t* d_table_index, int64_t n_tables, const double* d_work, int64_t work_doubles,
-                       lzq_yield* d_out, int32_t* d_status, void* stream);
+                       int64_t max_steps, lzq_yield* d_out, int32_t* d_status, void* stream);
 
 /* lzq_ode_tables + lzq_ode_integrate (d_status may be NULL). */
 int lzq_ode_batch(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, double* d_work,

@@ -73,7 +73,7 @@ def main():
         err = float(np.max(np.abs(t - ref) / np.maximum(np.abs(ref), 1e-300)))
         steps = O.ode_point(cfgs[0])["n_steps"]
         quad = {}
-        if float(over.get("sigma_v_chi_GeV_m2", 0.0)) == 0.0:   # the opt-in quadrature form (sigma_v = 0)
+        if True:   # the opt-in quadrature form (Y_chi stepped alone when sigma_v != 0)
             eng.ode(pts[:64], ods[:64], method="quadrature")
             torch.cuda.synchronize()
             t0 = time.perf_counter()

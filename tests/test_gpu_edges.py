@@ -97,3 +97,25 @@ def test_propagator_limits(gpu_engine):
         part = gpu_engine.lz_propagate(mm[:k], dd[:k], xx[:k], V_W, 20.0, 300).cpu().numpy()
         assert np.array_equal(part, full[:k]), k
     assert np.all((full >= -1e-12) & (full <= 1.0 + 1e-12))
+
+
+def test_propagator_bounded_steps_and_bad_input(gpu_engine):
+    """Round 2: a cell's Magnus steps are bounded by its core whatever the crossing spacing
+    (round 1 computed max(S, 3 Phi_cell) with no bound: crossings 1e7 LZ lengths apart
+    overflowed int); non-finite input gives NaN, not a hang; out-of-range arguments are
+    rejected on the host."""
+    import time
+    import torch
+    m, d = [0.1, 0.12, 0.6], [1.0, 0.8, 0.2]
+    for gap in (60.0, 1e4, 1e7):
+        x = [0.0, gap, 2 * gap]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        P = gpu_engine.lz_propagate([m], [d], [x], V_W, 20.0, 1000).cpu().numpy()[0]
+        dt = time.perf_counter() - t0
+        assert np.isfinite(P) and -1e-12 <= P <= 1.0 + 1e-12, (gap, P)
+        assert dt < 2.0, (gap, dt)
+    P = gpu_engine.lz_propagate([[float("nan"), 0.1]], [[1.0, 1.0]], [[0.0, 50.0]], V_W, 20.0, 100).cpu().numpy()[0]
+    assert np.isnan(P)
+    with pytest.raises(pkg("_native").LzqError, match="window_lz <= 200"):
+        gpu_engine.lz_propagate([0.1], [1.0], [0.0], V_W, 500.0, 1000)

@@ -142,3 +142,41 @@ def test_deterministic_and_batch_independent(gpu_engine):
     c = gpu_engine.yields(r[::-1]).cpu().numpy()[::-1]
     d = np.concatenate([gpu_engine.yields(r[i:i + 7]).cpu().numpy() for i in range(0, 40, 7)])
     assert np.array_equal(a, b) and np.array_equal(a, c) and np.array_equal(a, d)
+
+
+def test_wide_random_fuzz_vs_oracle(gpu_engine):
+    """1024 seeded points far outside the BASELINE grids (every Config field the fast path
+    reads, over decades beyond the configs, both statistics and regimes, every initial-
+    abundance branch, narrow / inverted / clamped windows) against the oracle: 1e-11."""
+    rng = np.random.default_rng(77)
+    cfgs = []
+    for _ in range(1024):
+        c = full_cfg(BASE_CFG)
+        c.update(m_chi_GeV=float(10 ** rng.uniform(-3, 4)), g_chi=int(rng.choice([1, 2, 3, 4, 8])),
+                 chi_stats=str(rng.choice(["fermion", "boson"])), regime=str(rng.choice(["thermal", "nonthermal"])),
+                 T_p_GeV=float(10 ** rng.uniform(-2, 4)), beta_over_H=float(10 ** rng.uniform(0, 4)),
+                 v_w=float(rng.choice([10 ** rng.uniform(-3, 0), 0.0])), I_p=float(rng.uniform(0.0, 2.0)),
+                 g_star=float(rng.uniform(1, 200)), g_star_s=float(rng.uniform(1, 200)),
+                 P_chi_to_B=float(rng.uniform(0, 1)), source_shape_sigma_y=float(rng.choice([10 ** rng.uniform(-1, 2), 0.0])),
+                 incident_flux_scale=float(10 ** rng.uniform(-15, 2)),
+                 T_max_over_Tp=float(10 ** rng.uniform(-0.5, 1.5)), T_min_over_Tp=float(10 ** rng.uniform(-5, 0.5)))
+        u = rng.uniform()
+        if u < 0.4:
+            c["Y_chi_init"], c["n_chi_at_Tp_GeV3"] = float(10 ** rng.uniform(-14, -6)), None
+        elif u < 0.7:
+            c["Y_chi_init"], c["n_chi_at_Tp_GeV3"] = None, float(10 ** rng.uniform(-6, 2))
+        else:
+            c["Y_chi_init"], c["n_chi_at_Tp_GeV3"] = None, None
+        cfgs.append(c)
+    t = gpu_engine.yields(recs(cfgs)).cpu().numpy()
+    ref = O.points_batch(cfgs, nthreads=16)
+    worst = 0.0
+    for c, row, rr in zip(cfgs, t, ref):
+        for k, a, b in zip(O.YIELD_FIELDS, row, rr):
+            if np.isnan(b):
+                assert np.isnan(a), (k, a, b, c)
+                continue
+            e = rel_err(a, b)
+            assert e < GUARD, (k, a, b, c)
+            worst = max(worst, e)
+    print(f"wide fuzz: 1024 points vs oracle, worst rel err {worst:.3e}")

@@ -57,15 +57,18 @@ def test_sweep_two_ranks_bit_identical_to_one(tmp_path):
     assert starts == [0, 1500, 2048, 3548]
 
 
-def test_bench_two_ranks_gloo():
-    out = run(torchrun(2) + ["bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1", "--points", "20000",
-                             "--dist-backend", "gloo"], 300)
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_multi_rank_gloo(world):
+    """bench.py's N > 1 path (rank shards of the W-fold refined grid, the per-step gather,
+    barrier + max-over-ranks timing) with W ranks sharing the one GPU."""
+    out = run(torchrun(world) + ["bench.py", "--gpus", str(world), "--steps", "1", "--warmup", "1", "--points",
+                                 "20000", "--dist-backend", "gloo"], 300)
     recs = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
     assert len(recs) == 1
     r = recs[0]
-    assert r["n_gpus"] == 2 and r["config"]["global_points_per_step"] == 40000
+    assert r["n_gpus"] == world and r["config"]["global_points_per_step"] == 20000 * world
     assert r["value"] > 0 and r["unit"] == "points/s" and r["scaling"] == "weak"
-    assert abs(r["value"] - 40000 / (r["ms_per_step"] / 1e3)) <= 1e-6 * r["value"]
+    assert abs(r["value"] - 20000 * world / (r["ms_per_step"] / 1e3)) <= 1e-6 * r["value"]
     assert "cpu_baseline" not in r   # rank 0 at N = 1 only
 
 

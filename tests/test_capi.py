@@ -59,7 +59,7 @@ def test_host_side_argument_validation():
     for K, S in ((300.0, 1000), (20.0, 2_000_000), (float("nan"), 1000)):
         rc = L.lzq_lz_propagate(8, 8, 8, 1, 1, 0.3, K, S, 8, None)
         assert rc == -1 and b"window_lz <= 200" in L.lzq_last_error(), (K, S)
-    rc = L.lzq_ode_quadrature(8, 8, 4, 8, 0, 8, 1 << 20, 8, None, None)   # shared index but no tables
+    rc = L.lzq_ode_quadrature(8, 8, 4, 8, 0, 8, 1 << 20, 100, 8, None, None)   # shared index but no tables
     assert rc == -1
     rc = L.lzq_ode_integrate_shared(8, 8, 4, 8, 1, 8, 100, 1, 8, None, None)  # workspace < 1 table
     assert rc == -1 and b"workspace" in L.lzq_last_error()

@@ -96,6 +96,7 @@ struct QuadSetup {
   double c_rel;   // g * 3 zeta3/(4 pi^2) | g zeta3/pi^2   fpy:96-99
   double c_nr;    // g (m/2pi)^1.5                     fpy:104
   double v0;      // pi * max(m, 1e-20)                fpy:117
+  double two_iBc, isig;  // 2/Bc, 1/sig: y_factors multiplies instead of dividing
 };
 
 // Move a wave-uniform double into SGPRs (two v_readfirstlane_b32): the per-point constants
@@ -145,8 +146,11 @@ __device__ __forceinline__ QuadSetup quad_setup(const lzq_point& pt, double P, d
   s.c_rel = (pt.stats == 0) ? pt.g_chi * (3.0 * kZeta3 / (4.0 * (kPi * kPi))) : pt.g_chi * (kZeta3 / (kPi * kPi));
   s.c_nr = pt.g_chi * pow15(pt.m_chi_GeV / (2.0 * kPi));
   s.v0 = kPi * pymax(pt.m_chi_GeV, 1e-20);
+  s.two_iBc = 2.0 / s.Bc;
+  s.isig = 1.0 / s.sig;
   double* f[] = {&s.y_lo, &s.y_hi, &s.step, &s.delta, &s.pref0, &s.cneg, &s.Bc, &s.Tp, &s.dT0, &s.sig, &s.m,
-                 &s.m3, &s.flux, &s.P, &s.g_star, &s.g_star_s, &s.H0, &s.s0, &s.c_rel, &s.c_nr, &s.v0};
+                 &s.m3, &s.flux, &s.P, &s.g_star, &s.g_star_s, &s.H0, &s.s0, &s.c_rel, &s.c_nr, &s.v0,
+                 &s.two_iBc, &s.isig};
 #pragma unroll
   for (double* v : f) *v = uniform(*v);
   return s;
@@ -164,6 +168,19 @@ __device__ __forceinline__ double vgpr_const(double x) {
 // constants are read from constant memory through an offset made opaque per call, so they
 // come in by scalar loads where needed: the libm exp's coefficients were hoisted out of the
 // y-loop into VGPRs and spilled to scratch across the z-loop (which needs ~60 of 64 VGPRs).
+#ifndef LZQ_YFAST
+#define LZQ_YFAST 1  // 0: round-2 per-y work (divisions, sqrt, 3-VALU Horner steps) for A/B builds
+#endif
+
+// fma(a, b, c) with the addend c read straight from an SGPR pair: one VOP3 v_fma_f64.  Left
+// to itself the compiler emits v_fmac_f64 (addend = destination) and copies each SGPR
+// coefficient into the destination with two v_mov_b32 first -- 3 VALU per Horner step.
+__device__ __forceinline__ double fma_vvs(double a, double b, double c) {
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+  return r;
+}
+
 __constant__ double kExpC[15] = {
     0x1.6124613a86d09p-33, 0x1.1eed8eff8d898p-29, 0x1.ae64567f544e4p-26, 0x1.27e4fb7789f5cp-22,
     0x1.71de3a556c734p-19, 0x1.a01a01a01a01ap-16, 0x1.a01a01a01a01ap-13, 0x1.6c16c16c16c17p-10,
@@ -181,7 +198,7 @@ __device__ __forceinline__ double exp_sc(double x) {
   r = __builtin_fma(-k, c[14], r);
   double p = c[0];
 #pragma unroll
-  for (int i = 1; i < 12; ++i) p = __builtin_fma(p, r, c[i]);
+  for (int i = 1; i < 12; ++i) p = LZQ_YFAST ? fma_vvs(p, r, c[i]) : __builtin_fma(p, r, c[i]);
   p = __builtin_fma(p, r, 1.0);  // (e^r - 1) / r
   p = __builtin_fma(p, r, 1.0);  // e^r
   return __builtin_ldexp(p, (int)k);
@@ -209,17 +226,41 @@ struct YFactors {
   double live;   // 1 if y <= 50 (fpy:159), else 0
 };
 
-// The fixed-exponent powers of numpy's `**` (SVML pow, <= 1 ulp) are evaluated with sqrt
-// and products (<= 2 ulp): x**-1.5 = 1/(x sqrt x), T**3 = (T*T)*T, T**1.5 = T sqrt T.  This
-// keeps the per-y work small (the device pow(double) is ~100 VALU and ~40 VGPRs) and moves
-// results by ~1e-16 relative (tests: worst golden error unchanged at 1e-13).
+// 1/sqrt(d) for a positive normal d: v_rsq_f64, then the Goldschmidt iteration that the
+// compiler's correctly rounded sqrt uses (g -> sqrt(d), h -> 1/(2 sqrt(d))); <= 2 ulp.
+__device__ __forceinline__ double rsqrt_pos(double d) {
+  const double r = __builtin_amdgcn_rsq(d);
+  double g = d * r, h = 0.5 * r;
+  double e = __builtin_fma(-g, h, 0.5);
+  g = __builtin_fma(g, e, g);
+  h = __builtin_fma(h, e, h);
+  e = __builtin_fma(-g, h, 0.5);
+  h = __builtin_fma(h, e, h);
+  return 2.0 * h;
+}
+
+// The fixed-exponent powers of numpy's `**` (SVML pow, <= 1 ulp) are evaluated with products
+// (<= 3 ulp): denom**-0.5 and denom**-1.5 from one reciprocal square root, T**3 = (T*T)*T,
+// T**1.5 = T sqrt T; the quotients by per-point constants (2y/B, y/sigma, H's 1/M_Pl) are
+// products with their reciprocals.  This keeps the per-y work small (the device pow(double) is
+// ~100 VALU and ~40 VGPRs; a division or a sqrt ~10-16) and moves results by ~1e-16 relative
+// (tests: worst golden error unchanged at 1e-13).
 __device__ __forceinline__ YFactors y_factors(const QuadSetup& s, double y, double expy, double wt) {
   YFactors f;
-  double denom = pymax(1.0 + 2.0 * y / s.Bc, 1e-12);     // fpy:252-253
-  double sd = sqrt(denom);
-  double T = s.Tp / sd;                                   // fpy:254
-  double dTdy = s.dT0 * (1.0 / (denom * sd));             // fpy:255  denom**(-1.5)
-  double H = s.H0 * T * T / kMplGeV;                      // fpy:258 via fpy:85
+  double T, dTdy, H;
+  if (LZQ_YFAST) {
+    const double denom = pymax(1.0 + y * s.two_iBc, 1e-12);  // fpy:252-253
+    const double rs = rsqrt_pos(denom);
+    T = s.Tp * rs;                                           // fpy:254
+    dTdy = s.dT0 * ((rs * rs) * rs);                         // fpy:255  denom**(-1.5)
+    H = s.H0 * T * T * (1.0 / kMplGeV);                      // fpy:258 via fpy:85
+  } else {
+    const double denom = pymax(1.0 + 2.0 * y / s.Bc, 1e-12);
+    const double sd = sqrt(denom);
+    T = s.Tp / sd;
+    dTdy = s.dT0 * (1.0 / (denom * sd));
+    H = s.H0 * T * T / kMplGeV;
+  }
   double T3 = (T * T) * T;
   double sE = s.s0 * T3;                                  // fpy:259 via fpy:88
   double n_eq, vbar;                                      // fpy:90-120, strict T > m/3 branch
@@ -231,7 +272,7 @@ __device__ __forceinline__ YFactors y_factors(const QuadSetup& s, double y, doub
     vbar = sqrt(pymax(8.0 * T / s.v0, 0.0));
   }
   double J = s.flux * 0.25 * n_eq * vbar;                 // fpy:260
-  double q = y / s.sig;
+  double q = LZQ_YFAST ? y * s.isig : y / s.sig;
   f.W = exp_sc(-0.5 * (q * q));                              // fpy:262
   f.PJ = s.P * J;
   f.sHT = sE * H * T;

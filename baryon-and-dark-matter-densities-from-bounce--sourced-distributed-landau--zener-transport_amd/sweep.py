@@ -333,11 +333,19 @@ def run_local(compute: ComputeFn, start: int, end: int, make_out: Callable[[int]
     return local
 
 
+def launched_distributed(world: int) -> bool:
+    """True under torch.distributed.run (any world size, 1 included: its rendezvous sets
+    MASTER_ADDR / MASTER_PORT) or whenever WORLD_SIZE > 1."""
+    return world > 1 or ("MASTER_ADDR" in os.environ and "MASTER_PORT" in os.environ)
+
+
 def gather_table(local, total: int, rank: int, world: int, group=None):
-    """All-gather the per-rank shards (sizes differ by <= 1) into the full (total, 6) table."""
+    """All-gather the per-rank shards (sizes differ by <= 1) into the full (total, 6) table.
+    With no process group (a plain single-process run) the local shard is the table; under a
+    launcher the collective runs even for one rank, so a 1-rank torchrun exercises RCCL."""
     import torch
     import torch.distributed as dist
-    if world == 1:
+    if world == 1 and not (dist.is_available() and dist.is_initialized()):
         return local
     sizes = [shard_range(total, r, world)[1] - shard_range(total, r, world)[0] for r in range(world)]
     m = max(sizes)
@@ -448,7 +456,8 @@ def main(argv=None):
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     local_rank %= max(1, torch.cuda.device_count())  # gloo rehearsal: several ranks may share a GPU
     torch.cuda.set_device(local_rank)
-    if world > 1:
+    use_dist = launched_distributed(world)
+    if use_dist:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:
@@ -478,7 +487,7 @@ def main(argv=None):
             with open(os.path.join(args.out, "summary.json"), "w") as f:
                 json.dump({**summ, "spec_def": spec.to_json()}, f, indent=2)
         print(json.dumps({k: summ[k] for k in ("spec", "n_points", "points_per_s", "n_gpus", "elapsed_s")}))
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

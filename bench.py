@@ -200,7 +200,10 @@ def main():
         print(f"[bench] WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE", file=sys.stderr)
     local = local % max(1, torch.cuda.device_count())  # gloo rehearsal: several ranks may share a GPU
     torch.cuda.set_device(local)
-    if world > 1:
+    # a process group whenever a launcher started us (torchrun sets MASTER_ADDR/PORT), so a
+    # 1-rank torchrun runs the same RCCL all-gather as N ranks; plain `python bench.py` has none
+    use_dist = world > 1 or ("MASTER_ADDR" in os.environ and "MASTER_PORT" in os.environ)
+    if use_dist:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -214,7 +217,7 @@ def main():
     assert total <= grid_total
     start = rank * per
     local_tab = torch.empty((per, 6), dtype=torch.float64, device=eng.device)
-    gathered = torch.empty((total, 6), dtype=torch.float64, device=eng.device) if world > 1 else local_tab
+    gathered = torch.empty((total, 6), dtype=torch.float64, device=eng.device) if use_dist else local_tab
     stream = torch.cuda.current_stream()
     k_ev = []
 
@@ -226,7 +229,7 @@ def main():
         if record:
             e1.record(stream)
             k_ev.append((e0, e1))
-        if world > 1:
+        if use_dist:
             if args.dist_backend == "nccl":
                 dist.all_gather_into_tensor(gathered, local_tab)  # RCCL over xGMI
             else:
@@ -237,18 +240,18 @@ def main():
     for _ in range(args.warmup):
         step(False)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in k_ev]))
-    if world > 1:
+    if use_dist:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64,
                          device=eng.device if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -268,7 +271,7 @@ def main():
         t_tr = time.perf_counter() - t1
         eng.tune_truncate(False)
         same = bool(torch.equal(dense_tab, local_tab))
-        if world > 1:
+        if use_dist:
             t = torch.tensor([t_tr, 0.0 if same else 1.0], dtype=torch.float64,
                              device=eng.device if args.dist_backend == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -280,7 +283,7 @@ def main():
     # sanity: every shard of the gathered table is finite and the gather put rank r's rows at
     # [r*per, (r+1)*per)
     assert bool(torch.isfinite(gathered).all()), "non-finite yields"
-    if world > 1:
+    if use_dist:
         assert torch.equal(gathered[start:start + per], local_tab), "all-gather misplaced a shard"
 
     if rank == 0:
@@ -310,7 +313,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(axes, grid_total, args.cpu_seconds)
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

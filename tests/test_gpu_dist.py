@@ -6,7 +6,10 @@ this module touches the GPU in the pytest process itself.
 - sweep.main over a 4096-point C3 slice at world_size 2 == the single-rank table, bit for
   bit (each point is reduced by one wavefront, so sharding cannot change a result);
 - bench.py under torchrun with --dist-backend gloo emits one valid JSON line whose value
-  counts both ranks' points.
+  counts both ranks' points;
+- the RCCL code path itself (process group on the device, all_gather_into_tensor of the
+  device-resident yield tables) with ONE rank under torchrun: bench.py and sweep.main, the
+  sweep table bit-identical to the plain single-process run.
 """
 import json
 import os
@@ -91,3 +94,28 @@ def test_bench_single_rank_line():
     assert rf["stock_exp_equivalent"]["achieved"] > rf["achieved"]
     cb = r["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] == cb["host"]["usable"] and cb["value"] > 0
+
+
+def test_rccl_one_rank_sweep_bit_identical(tmp_path):
+    """sweep.main under a 1-rank torchrun: an RCCL process group on cuda:0 and the
+    all_gather_into_tensor of gather_table (padding, placement) over the real engine's table."""
+    args = ["--spec", "C4", "--limit", "3000", "--chunk", "1024"]
+    one, rccl = tmp_path / "plain", tmp_path / "rccl"
+    run([sys.executable, "-m", PKG_NAME + ".sweep", *args, "--out", str(one)], 300)
+    run(torchrun(1) + ["-m", PKG_NAME + ".sweep", *args, "--out", str(rccl), "--dist-backend", "nccl"], 300)
+    t1, t2 = np.load(one / "table.npy"), np.load(rccl / "table.npy")
+    assert t1.shape == (3000, 6) and np.isfinite(t1).all()
+    assert np.array_equal(t1, t2)
+
+
+def test_rccl_one_rank_bench_line():
+    """bench.py under a 1-rank torchrun takes the RCCL branch (process group, per-step
+    all_gather_into_tensor, barrier, max-over-ranks all_reduce on the device) and still emits
+    one valid line."""
+    out = run(torchrun(1) + ["bench.py", "--gpus", "1", "--steps", "1", "--warmup", "1", "--points", "20000",
+                             "--no-cpu-baseline"], 300)
+    recs = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+    assert len(recs) == 1
+    r = recs[0]
+    assert r["n_gpus"] == 1 and "RCCL" in r["config"]["parallelism"]
+    assert r["value"] > 0 and abs(r["value"] - 20000 / (r["ms_per_step"] / 1e3)) <= 1e-6 * r["value"]

@@ -198,13 +198,114 @@ __device__ __forceinline__ void dressed_follow(Cplx& p0, Cplx& p1, double m, dou
         bp2.re * B.p1.im + bp2.im * B.p1.re + bm2.re * B.q1.im + bm2.im * B.q1.re};
 }
 
+// ---------------------------------------------------------------------------------------
+// Launch order.  A lane's cost is its Magnus step count, which delta sets per cell: ~1000-1200
+// steps for delta <= 1, up to ~6e4 in core-limited cells with 1 < delta <= 16, none in the
+// closed-form cells (C5 slice: median 9.9e3 per point, 99th percentile 5.3e4).  In index order
+// a wave waits on its slowest lane in every cell and the launch ends on a few long waves.  So,
+// for large batches, the points are first binned by their step count (the kernel's own cell
+// geometry, point_steps), the bins laid out longest-first (a counting sort: LDS histograms, one
+// scan, a scatter), and the kernel reads its point index from that order.  Every point is still
+// computed by one lane from its own inputs, so P is bit-identical to index order; only the
+// order within a bin depends on the scatter's atomics.
+// ---------------------------------------------------------------------------------------
+#ifndef LZQ_PROP_SORT
+#define LZQ_PROP_SORT 1  // 0: index order (tools/ablate_prop.py)
+#endif
+constexpr int kCostBins = 128;           // 4 bins per octave of the step count
+constexpr int64_t kSortMinPoints = 16384;  // below this the three extra launches do not pay
+
+// Magnus steps of one point: the cell loop of lz_propagate_kernel without the propagation.
+__device__ double point_steps(const double* mm, const double* dp, const double* xc, int32_t n_cross, double v_w,
+                              double K, int32_t S) {
+  double left = xc[0] - K * lz_length(mm[0], fabs(dp[0]), v_w);
+  double total = 0.0;
+  for (int c = 0; c < n_cross; ++c) {
+    const double ac = fabs(dp[c]), mc = mm[c], xcc = xc[c];
+    double right;
+    if (c + 1 < n_cross) {
+      const double an = fabs(dp[c + 1]);
+      right = (ac * xcc + an * xc[c + 1]) / (ac + an);
+    } else {
+      right = xcc + K * lz_length(mc, ac, v_w);
+    }
+    const double delta = mc * mc / (2.0 * v_w * ac);
+    if (delta > kDeltaAdiabatic) {
+      total += 4.0;  // closed-form cell: a few steps' worth of work
+    } else {
+      const double W = core_halfwidth(mc, ac, v_w, K);
+      const double cl = fmax(left, xcc - W), cr = fmin(right, xcc + W);
+      const double Phic = (wkb_G(ac * (cr - xcc), mc) - wkb_G(ac * (cl - xcc), mc)) / (ac * v_w);
+      total += fmax((double)S, ceil(Phic * kStepsPerRadian));
+    }
+    left = right;
+  }
+  return total;
+}
+
+// bin (0 = costliest) of every point + the histogram of bins
+__global__ __launch_bounds__(kPropBlock) void lz_cost_kernel(const double* __restrict__ m_mix,
+                                                             const double* __restrict__ dprime,
+                                                             const double* __restrict__ xi, int64_t n, int32_t n_cross,
+                                                             double v_w, double K, int32_t S,
+                                                             int32_t* __restrict__ bins, int32_t* __restrict__ hist) {
+  __shared__ int32_t lh[kCostBins];
+  for (int t = threadIdx.x; t < kCostBins; t += kPropBlock) lh[t] = 0;
+  __syncthreads();
+  const int64_t p = (int64_t)blockIdx.x * kPropBlock + threadIdx.x;
+  if (p < n) {
+    const double st = point_steps(m_mix + p * n_cross, dprime + p * n_cross, xi + p * n_cross, n_cross, v_w, K, S);
+    // non-finite or absurd inputs (the kernel returns NaN at once) go with the cheapest
+    const double key = st == st ? fmin(fmax(4.0 * log2(1.0 + st), 0.0), (double)(kCostBins - 1)) : 0.0;
+    const int32_t b = (kCostBins - 1) - (int32_t)key;
+    bins[p] = b;
+    atomicAdd(&lh[b], 1);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < kCostBins; t += kPropBlock)
+    if (lh[t]) atomicAdd(&hist[t], lh[t]);
+}
+
+// exclusive prefix sum of the histogram (one block)
+__global__ void lz_bin_scan_kernel(const int32_t* __restrict__ hist, int32_t* __restrict__ offs) {
+  if (threadIdx.x == 0) {
+    int32_t acc = 0;
+    for (int b = 0; b < kCostBins; ++b) {
+      offs[b] = acc;
+      acc += hist[b];
+    }
+  }
+}
+
+// order[offs[bin] + rank] = p (rank within the bin from LDS counters + one global reservation
+// per bin and block)
+__global__ __launch_bounds__(kPropBlock) void lz_scatter_kernel(const int32_t* __restrict__ bins, int64_t n,
+                                                                int32_t* __restrict__ offs,
+                                                                int32_t* __restrict__ order) {
+  __shared__ int32_t cnt[kCostBins], base[kCostBins];
+  for (int t = threadIdx.x; t < kCostBins; t += kPropBlock) cnt[t] = 0;
+  __syncthreads();
+  const int64_t p = (int64_t)blockIdx.x * kPropBlock + threadIdx.x;
+  int32_t b = 0, r = 0;
+  if (p < n) {
+    b = bins[p];
+    r = atomicAdd(&cnt[b], 1);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < kCostBins; t += kPropBlock) base[t] = cnt[t] ? atomicAdd(&offs[t], cnt[t]) : 0;
+  __syncthreads();
+  if (p < n) order[base[b] + r] = (int32_t)p;
+}
+
 __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_kernel(const double* __restrict__ m_mix,
                                                                   const double* __restrict__ dprime,
                                                                   const double* __restrict__ xi, int64_t n,
                                                                   int32_t n_cross, double v_w, double K,
-                                                                  int32_t S, double* __restrict__ P_out) {
-  const int64_t p = (int64_t)blockIdx.x * kPropBlock + threadIdx.x;
-  if (p >= n) return;
+                                                                  int32_t S, const int32_t* __restrict__ order,
+                                                                  double* __restrict__ P_out) {
+  const int64_t tid = (int64_t)blockIdx.x * kPropBlock + threadIdx.x;
+  if (tid >= n) return;
+  const int64_t p = order ? (int64_t)order[tid] : tid;
   const double* mm = m_mix + p * n_cross;
   const double* dp = dprime + p * n_cross;
   const double* xc = xi + p * n_cross;
@@ -321,11 +422,36 @@ extern "C" int lzq_lz_propagate(const double* d_m_mix, const double* d_dprime, c
     return lzq_set_error(LZQ_EINVAL, "lzq_lz_propagate: bad arguments (need n >= 0, n_cross > 0, "
                                      "0 < steps_per_crossing <= 1e6, v_w > 0, 0 < window_lz <= 200)");
   if (n == 0) return LZQ_OK;
+  if (n > 2147483647LL) return lzq_set_error(LZQ_EINVAL, "lzq_lz_propagate: n too large (int32 point order)");
   const int64_t nb = (n + lzq::kPropBlock - 1) / lzq::kPropBlock;
-  if (nb > 2147483647LL) return lzq_set_error(LZQ_EINVAL, "lzq_lz_propagate: n too large");
-  hipLaunchKernelGGL(lzq::lz_propagate_kernel, dim3((unsigned)nb), dim3(lzq::kPropBlock), 0, (hipStream_t)stream,
-                     d_m_mix, d_dprime, d_xi, n, n_cross, v_w, window_lz, steps_per_crossing, d_P);
+  hipStream_t st = (hipStream_t)stream;
+  // longest-first launch order (see lz_cost_kernel); stream-ordered scratch, so calls on
+  // different streams stay independent
+  int32_t* ws = nullptr;
+  const int32_t* order = nullptr;
+  if (LZQ_PROP_SORT && n >= lzq::kSortMinPoints) {
+    const size_t bytes = (size_t)(2 * n + 2 * lzq::kCostBins) * sizeof(int32_t);
+    hipError_t e = hipMallocAsync((void**)&ws, bytes, st);
+    if (e != hipSuccess) return lzq_set_error(LZQ_EHIP, hipGetErrorString(e));
+    int32_t *bins = ws, *ord = ws + n, *hist = ws + 2 * n, *offs = hist + lzq::kCostBins;
+    e = hipMemsetAsync(hist, 0, lzq::kCostBins * sizeof(int32_t), st);
+    if (e != hipSuccess) {
+      (void)hipFreeAsync(ws, st);
+      return lzq_set_error(LZQ_EHIP, hipGetErrorString(e));
+    }
+    hipLaunchKernelGGL(lzq::lz_cost_kernel, dim3((unsigned)nb), dim3(lzq::kPropBlock), 0, st, d_m_mix, d_dprime, d_xi,
+                       n, n_cross, v_w, window_lz, steps_per_crossing, bins, hist);
+    hipLaunchKernelGGL(lzq::lz_bin_scan_kernel, dim3(1), dim3(64), 0, st, hist, offs);
+    hipLaunchKernelGGL(lzq::lz_scatter_kernel, dim3((unsigned)nb), dim3(lzq::kPropBlock), 0, st, bins, n, offs, ord);
+    order = ord;
+  }
+  hipLaunchKernelGGL(lzq::lz_propagate_kernel, dim3((unsigned)nb), dim3(lzq::kPropBlock), 0, st,
+                     d_m_mix, d_dprime, d_xi, n, n_cross, v_w, window_lz, steps_per_crossing, order, d_P);
   hipError_t e = hipGetLastError();
+  if (ws) {
+    const hipError_t ef = hipFreeAsync(ws, st);
+    if (e == hipSuccess) e = ef;
+  }
   if (e != hipSuccess) return lzq_set_error(LZQ_EHIP, hipGetErrorString(e));
   return LZQ_OK;
 }

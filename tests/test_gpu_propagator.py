@@ -83,3 +83,26 @@ def test_kernel_vs_exact_weber_solution(gpu_engine):
             assert np.all(np.abs(got - ex) <= tol), (N, K, S, np.abs(got - ex).max())
         n += len(cs)
     assert n == len(g["cases"]) == 53
+
+
+def test_longest_first_order_is_bit_identical(gpu_engine):
+    """Batches of >= 16384 points run in longest-first order (lz_cost_kernel + counting sort,
+    lzq_propagator.hip): P must be bit-identical to index order, which smaller batches use.
+    A C5 slice of 40000 points (8 jittered crossings) whose step counts span ~1e3..6e4, plus
+    NaN and adiabatic-only points mixed in."""
+    import torch
+    sw = pkg("sweep")
+    spec = sw.builtin_specs()["C5"]
+    n = 40000
+    m, dp, xi, v_w = spec.crossing_arrays((spec.total - n) // 2, n, gpu_engine.device)
+    m = m.clone()
+    m[7] = float("nan")            # the kernel's NaN exit
+    m[12345] *= 100.0              # every cell adiabatic (closed form only)
+    args = (float(v_w[0]), spec.crossings.window_lz, spec.crossings.steps)
+    whole = gpu_engine.lz_propagate(m, dp, xi, *args)
+    parts = torch.cat([gpu_engine.lz_propagate(m[i:i + 10000], dp[i:i + 10000], xi[i:i + 10000], *args)
+                       for i in range(0, n, 10000)])   # < 16384: index order
+    assert torch.isnan(whole[7]) and torch.isnan(parts[7])
+    ok = ~torch.isnan(parts)
+    assert int(ok.sum()) == n - 1
+    assert torch.equal(whole[ok], parts[ok])

@@ -374,25 +374,30 @@ __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_k
       const double cy = ddot * mc * dt * dt2, ey1 = dt2 * (1.0 / 90.0), ey2 = dt4 * (1.0 / 7560.0);
       const double dd2x9 = 9.0 * dd2;
       const double cz = dt * (1.0 - bx * m2);
+      // The step as fused multiply-adds (the file builds with -ffp-contract=off for the
+      // oracle-matching kernels, so contraction is spelled out): 63 VALU per step where the
+      // separate products and sums took 84.
+#define FMA __builtin_fma
       for (int i = 0; i < Sc; ++i) {
-        const double xm = cl + ((double)i + 0.5) * h;
+        const double xm = FMA((double)i + 0.5, h, cl);
         const double D = slope * (xm - xcc);
         const double D2 = D * D, E2 = D2 + m2;
-        const double nx = cxm * (ax - bx * (3.0 * D2 + m2x4));
-        const double ny = cy * ((1.0 / 6.0) + ey1 * E2 + ey2 * (8.0 * E2 * E2 - dd2x9));
+        const double nx = cxm * FMA(-bx, FMA(3.0, D2, m2x4), ax);
+        const double ny = cy * FMA(ey2, FMA(8.0 * E2, E2, -dd2x9), FMA(ey1, E2, 1.0 / 6.0));
         const double nz = cz * D;
         double cs, sc;  // cos|n| and sin|n|/|n|, both functions of |n|^2
-        cos_sinc(nx * nx + ny * ny + nz * nz, cs, sc);
+        cos_sinc(FMA(nx, nx, FMA(ny, ny, nz * nz)), cs, sc);
         const double sx = sc * nx, sy = sc * ny, sz = sc * nz;
         // U11 = cs - i sz ; U12 = -sy - i sx ; U21 = sy - i sx ; U22 = cs + i sz
         Cplx q0, q1;
-        q0.re = cs * p0.re + sz * p0.im - sy * p1.re + sx * p1.im;
-        q0.im = cs * p0.im - sz * p0.re - sy * p1.im - sx * p1.re;
-        q1.re = sy * p0.re + sx * p0.im + cs * p1.re - sz * p1.im;
-        q1.im = sy * p0.im - sx * p0.re + cs * p1.im + sz * p1.re;
+        q0.re = FMA(cs, p0.re, FMA(sz, p0.im, FMA(-sy, p1.re, sx * p1.im)));
+        q0.im = FMA(cs, p0.im, FMA(-sz, p0.re, FMA(-sy, p1.im, -(sx * p1.re))));
+        q1.re = FMA(sy, p0.re, FMA(sx, p0.im, FMA(cs, p1.re, -(sz * p1.im))));
+        q1.im = FMA(sy, p0.im, FMA(-sx, p0.re, FMA(cs, p1.im, sz * p1.re)));
         p0 = q0;
         p1 = q1;
       }
+#undef FMA
       if (cr < right) dressed_follow(p0, p1, mc, ac, slope, xcc, cr, right, v_w);
     }
     left = right;

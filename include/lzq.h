@@ -257,7 +257,10 @@ int lzq_ode_rhs(const lzq_point* pt, const lzq_ode_params* ode, double T_lo, dou
  * "dressed" = second-order superadiabatic state of the outer cell (the adiabatic state carried
  * in from / out to infinity).  For one crossing this is 1 - exp(-2 pi delta) (fpy:183-184,
  * PAPER eq.(9)) to <= 1e-8 relative at window_lz = 20, steps_per_crossing = 1000; DESIGN.md §6
- * states the window / step tolerances. */
+ * states the window / step tolerances.  Batches of n >= 16384 points run longest-first (points
+ * binned by their step count, a counting sort in three small kernels, scratch of 8n bytes from
+ * hipMallocAsync on `stream`, freed stream-ordered); d_P is bit-identical to index order.
+ * n < 2^31. */
 int lzq_lz_propagate(const double* d_m_mix, const double* d_dprime, const double* d_xi,
                      int64_t n, int32_t n_cross, double v_w, double window_lz,
                      int32_t steps_per_crossing, double* d_P, void* stream);

@@ -43,17 +43,30 @@ constexpr double kExp2A10 = 0x1.e61b4fc4ab239p-28;
 constexpr double kExp2A11 = 0x1.e79bb37875897p-32;
 constexpr double kLog2E = 0x1.71547652b82fep0;  // log2(e) rounded to nearest
 
+// fma(a, b, c) with the addend c in an SGPR pair: one VOP3 v_fma_f64 on the device.  Left to
+// itself the compiler keeps Horner coefficients in VGPRs (hoisted out of loops: 2 VGPRs each)
+// and emits v_mov_b64 + v_fmac_f64 (addend = destination) per step, 2 VALU instead of 1.
+LZQ_HD double fma_vvs(double a, double b, double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+  return r;
+#else
+  return __builtin_fma(a, b, c);
+#endif
+}
+
 LZQ_HD double exp2_poly(double r) {
-  double q = __builtin_fma(r, kExp2A11, kExp2A10);
-  q = __builtin_fma(r, q, kExp2A9);
-  q = __builtin_fma(r, q, kExp2A8);
-  q = __builtin_fma(r, q, kExp2A7);
-  q = __builtin_fma(r, q, kExp2A6);
-  q = __builtin_fma(r, q, kExp2A5);
-  q = __builtin_fma(r, q, kExp2A4);
-  q = __builtin_fma(r, q, kExp2A3);
-  q = __builtin_fma(r, q, kExp2A2);
-  q = __builtin_fma(r, q, kExp2A1);
+  double q = fma_vvs(r, kExp2A11, kExp2A10);
+  q = fma_vvs(r, q, kExp2A9);
+  q = fma_vvs(r, q, kExp2A8);
+  q = fma_vvs(r, q, kExp2A7);
+  q = fma_vvs(r, q, kExp2A6);
+  q = fma_vvs(r, q, kExp2A5);
+  q = fma_vvs(r, q, kExp2A4);
+  q = fma_vvs(r, q, kExp2A3);
+  q = fma_vvs(r, q, kExp2A2);
+  q = fma_vvs(r, q, kExp2A1);
   return __builtin_fma(r, q, 1.0);
 }
 

@@ -172,15 +172,6 @@ __device__ __forceinline__ double vgpr_const(double x) {
 #define LZQ_YFAST 1  // 0: round-2 per-y work (divisions, sqrt, 3-VALU Horner steps) for A/B builds
 #endif
 
-// fma(a, b, c) with the addend c read straight from an SGPR pair: one VOP3 v_fma_f64.  Left
-// to itself the compiler emits v_fmac_f64 (addend = destination) and copies each SGPR
-// coefficient into the destination with two v_mov_b32 first -- 3 VALU per Horner step.
-__device__ __forceinline__ double fma_vvs(double a, double b, double c) {
-  double r;
-  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
-  return r;
-}
-
 __constant__ double kExpC[15] = {
     0x1.6124613a86d09p-33, 0x1.1eed8eff8d898p-29, 0x1.ae64567f544e4p-26, 0x1.27e4fb7789f5cp-22,
     0x1.71de3a556c734p-19, 0x1.a01a01a01a01ap-16, 0x1.a01a01a01a01ap-13, 0x1.6c16c16c16c17p-10,

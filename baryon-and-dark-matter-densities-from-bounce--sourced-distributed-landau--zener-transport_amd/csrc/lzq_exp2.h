@@ -46,6 +46,9 @@ constexpr double kLog2E = 0x1.71547652b82fep0;  // log2(e) rounded to nearest
 // fma(a, b, c) with the addend c in an SGPR pair: one VOP3 v_fma_f64 on the device.  Left to
 // itself the compiler keeps Horner coefficients in VGPRs (hoisted out of loops: 2 VGPRs each)
 // and emits v_mov_b64 + v_fmac_f64 (addend = destination) per step, 2 VALU instead of 1.
+#ifndef LZQ_EXP2_VVS
+#define LZQ_EXP2_VVS 0  // 1: exp2_poly Horner steps through fma_vvs (ODE A/B: -3.5% narrow, +1% stiff; off)
+#endif
 LZQ_HD double fma_vvs(double a, double b, double c) {
 #if defined(__HIP_DEVICE_COMPILE__)
   double r;
@@ -57,6 +60,9 @@ LZQ_HD double fma_vvs(double a, double b, double c) {
 }
 
 LZQ_HD double exp2_poly(double r) {
+#if !LZQ_EXP2_VVS
+#define fma_vvs __builtin_fma
+#endif
   double q = fma_vvs(r, kExp2A11, kExp2A10);
   q = fma_vvs(r, q, kExp2A9);
   q = fma_vvs(r, q, kExp2A8);
@@ -67,6 +73,9 @@ LZQ_HD double exp2_poly(double r) {
   q = fma_vvs(r, q, kExp2A3);
   q = fma_vvs(r, q, kExp2A2);
   q = fma_vvs(r, q, kExp2A1);
+#if !LZQ_EXP2_VVS
+#undef fma_vvs
+#endif
   return __builtin_fma(r, q, 1.0);
 }
 

@@ -96,7 +96,7 @@ struct QuadSetup {
   double c_rel;   // g * 3 zeta3/(4 pi^2) | g zeta3/pi^2   fpy:96-99
   double c_nr;    // g (m/2pi)^1.5                     fpy:104
   double v0;      // pi * max(m, 1e-20)                fpy:117
-  double two_iBc, isig;  // 2/Bc, 1/sig: y_factors multiplies instead of dividing
+  double isig;    // 1/sig: y_factors multiplies instead of dividing
 };
 
 // Move a wave-uniform double into SGPRs (two v_readfirstlane_b32): the per-point constants
@@ -146,11 +146,10 @@ __device__ __forceinline__ QuadSetup quad_setup(const lzq_point& pt, double P, d
   s.c_rel = (pt.stats == 0) ? pt.g_chi * (3.0 * kZeta3 / (4.0 * (kPi * kPi))) : pt.g_chi * (kZeta3 / (kPi * kPi));
   s.c_nr = pt.g_chi * pow15(pt.m_chi_GeV / (2.0 * kPi));
   s.v0 = kPi * pymax(pt.m_chi_GeV, 1e-20);
-  s.two_iBc = 2.0 / s.Bc;
   s.isig = 1.0 / s.sig;
   double* f[] = {&s.y_lo, &s.y_hi, &s.step, &s.delta, &s.pref0, &s.cneg, &s.Bc, &s.Tp, &s.dT0, &s.sig, &s.m,
                  &s.m3, &s.flux, &s.P, &s.g_star, &s.g_star_s, &s.H0, &s.s0, &s.c_rel, &s.c_nr, &s.v0,
-                 &s.two_iBc, &s.isig};
+                 &s.isig};
 #pragma unroll
   for (double* v : f) *v = uniform(*v);
   return s;
@@ -169,7 +168,7 @@ __device__ __forceinline__ double vgpr_const(double x) {
 // come in by scalar loads where needed: the libm exp's coefficients were hoisted out of the
 // y-loop into VGPRs and spilled to scratch across the z-loop (which needs ~60 of 64 VGPRs).
 #ifndef LZQ_YFAST
-#define LZQ_YFAST 1  // 0: round-2 per-y work (divisions, sqrt, 3-VALU Horner steps) for A/B builds
+#define LZQ_YFAST 7  // bit mask (A/B builds): 1 SGPR Horner steps, 2 rsqrt, 4 1/sigma product
 #endif
 
 __constant__ double kExpC[15] = {
@@ -189,7 +188,7 @@ __device__ __forceinline__ double exp_sc(double x) {
   r = __builtin_fma(-k, c[14], r);
   double p = c[0];
 #pragma unroll
-  for (int i = 1; i < 12; ++i) p = LZQ_YFAST ? fma_vvs(p, r, c[i]) : __builtin_fma(p, r, c[i]);
+  for (int i = 1; i < 12; ++i) p = (LZQ_YFAST & 1) ? fma_vvs(p, r, c[i]) : __builtin_fma(p, r, c[i]);
   p = __builtin_fma(p, r, 1.0);  // (e^r - 1) / r
   p = __builtin_fma(p, r, 1.0);  // e^r
   return __builtin_ldexp(p, (int)k);
@@ -232,15 +231,17 @@ __device__ __forceinline__ double rsqrt_pos(double d) {
 
 // The fixed-exponent powers of numpy's `**` (SVML pow, <= 1 ulp) are evaluated with products
 // (<= 3 ulp): denom**-0.5 and denom**-1.5 from one reciprocal square root, T**3 = (T*T)*T,
-// T**1.5 = T sqrt T; the quotients by per-point constants (2y/B, y/sigma, H's 1/M_Pl) are
-// products with their reciprocals.  This keeps the per-y work small (the device pow(double) is
+// T**1.5 = T sqrt T; the quotients by per-point constants (y/sigma, H's 1/M_Pl) are products
+// with their reciprocals.  This keeps the per-y work small (the device pow(double) is
 // ~100 VALU and ~40 VGPRs; a division or a sqrt ~10-16) and moves results by ~1e-16 relative
 // (tests: worst golden error unchanged at 1e-13).
 __device__ __forceinline__ YFactors y_factors(const QuadSetup& s, double y, double expy, double wt) {
   YFactors f;
   double T, dTdy, H;
-  if (LZQ_YFAST) {
-    const double denom = pymax(1.0 + y * s.two_iBc, 1e-12);  // fpy:252-253
+  if (LZQ_YFAST & 2) {
+    // 2y/B stays a correctly rounded division: near y = -B/2 (T_max/T_p large) 1 + 2y/B cancels,
+    // and the product with a rounded 2/B moved Y_B by 6.7e-13 on a golden point (diag_golden.py)
+    const double denom = pymax(1.0 + 2.0 * y / s.Bc, 1e-12);  // fpy:252-253
     const double rs = rsqrt_pos(denom);
     T = s.Tp * rs;                                           // fpy:254
     dTdy = s.dT0 * ((rs * rs) * rs);                         // fpy:255  denom**(-1.5)
@@ -263,7 +264,7 @@ __device__ __forceinline__ YFactors y_factors(const QuadSetup& s, double y, doub
     vbar = sqrt(pymax(8.0 * T / s.v0, 0.0));
   }
   double J = s.flux * 0.25 * n_eq * vbar;                 // fpy:260
-  double q = LZQ_YFAST ? y * s.isig : y / s.sig;
+  double q = (LZQ_YFAST & 4) ? y * s.isig : y / s.sig;
   f.W = exp_sc(-0.5 * (q * q));                              // fpy:262
   f.PJ = s.P * J;
   f.sHT = sE * H * T;

@@ -87,7 +87,9 @@ __device__ __forceinline__ OdePoint ode_point(const lzq_point& pt, const lzq_ode
 #endif
 #ifndef LZQ_ODE_FASTMATH
 #define LZQ_ODE_FASTMATH 1  // 0: IEEE division and ROCm exp in the stage function (tools/ablate_ode.py);
-                            // also fused multiply-adds in the spline, the window exponent and Newton's f
+#endif
+#ifndef LZQ_ODE_FMA
+#define LZQ_ODE_FMA LZQ_ODE_FASTMATH  // fused multiply-adds in the spline, the window exponent, Newton's f
 #endif
 
 // fpy:214-218 A_over_V_T: min(max(T, T_lo), T_hi), then the PPoly of scipy (_ppoly.pyx:
@@ -103,7 +105,7 @@ __device__ __forceinline__ double spline_eval(const OdePoint& o, const double* _
   const double s = Tq - linspace_at(o.T_lo, o.T_hi, o.stepT, k, kOdeNT);
   const double* c = w + 4 * k;
   const double c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3];
-  if (LZQ_ODE_FASTMATH) return __builtin_fma(__builtin_fma(__builtin_fma(c0, s, c1), s, c2), s, c3);  // Horner, 3 fma
+  if (LZQ_ODE_FMA) return __builtin_fma(__builtin_fma(__builtin_fma(c0, s, c1), s, c2), s, c3);  // Horner, 3 fma
   double z = s, res = c3;
   res = res + c2 * z;
   z = z * s;
@@ -157,7 +159,7 @@ __device__ __forceinline__ OdeStage ode_stage(const OdePoint& o, const double* _
   const double T3 = (T * T) * T;
   const double s = pymax(o.s0 * T3, 1e-300);                  // fpy:274 via fpy:88
   const double qT = o.Tp * iT;                                // fpy:275 y_of_T (fpy:126-128)
-  const double y = 0.5 * o.B * (LZQ_ODE_FASTMATH ? __builtin_fma(qT, qT, -1.0) : qT * qT - 1.0);
+  const double y = 0.5 * o.B * (LZQ_ODE_FMA ? __builtin_fma(qT, qT, -1.0) : qT * qT - 1.0);
   const double q = y * o.inv_sig;
   const double window = exp_nonpos(-0.5 * (q * q));           // fpy:276
   double n_eq, vbar;                                          // fpy:90-120
@@ -383,7 +385,7 @@ __device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st
     double f[3], jf[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      f[j] = LZQ_ODE_FASTMATH ? __builtin_fma(-st[j].lam, __builtin_fma(Z[j], Z[j], -st[j].E2), -st[j].S)
+      f[j] = LZQ_ODE_FMA ? __builtin_fma(-st[j].lam, __builtin_fma(Z[j], Z[j], -st[j].E2), -st[j].S)
                               : -st[j].lam * (Z[j] * Z[j] - st[j].E2) - st[j].S;
       jf[j] = -st[j].lam * (2.0 * Z[j]);
     }
@@ -662,7 +664,7 @@ __device__ __forceinline__ double ode_alpha_dT(const OdePoint& o, const double* 
   const double T3 = (T * T) * T;
   const double s = pymax(o.s0 * T3, 1e-300);
   const double qT = o.Tp * iT;
-  const double y = 0.5 * o.B * (LZQ_ODE_FASTMATH ? __builtin_fma(qT, qT, -1.0) : qT * qT - 1.0);
+  const double y = 0.5 * o.B * (LZQ_ODE_FMA ? __builtin_fma(qT, qT, -1.0) : qT * qT - 1.0);
   const double q = y * o.inv_sig;
   const double window = exp_nonpos(-0.5 * (q * q));
   double n_eq, vbar;

@@ -47,6 +47,7 @@ struct OdePoint {
   double T_lo, T_hi, stepT;
   double inv_m, inv_sig, inv_v0, inv_stepT;  // reciprocals: ode_stage multiplies instead of dividing
   double inv_s0, mpl_over_h0;                // 1/s0, M_Pl/H0 (1/s and 1/(H x) as products)
+  double Pf;                                 // P * flux: the source term's per-point scale
 };
 
 __device__ __forceinline__ void ode_point_recips(OdePoint& o) {
@@ -67,6 +68,7 @@ __device__ __forceinline__ OdePoint ode_point(const lzq_point& pt, const lzq_ode
   o.sig = pymax(pt.source_shape_sigma_y, 1e-6);
   o.flux = pt.incident_flux_scale;
   o.P = pt.P_chi_to_B;
+  o.Pf = o.P * o.flux;
   o.H0 = 1.66 * sqrt(pt.g_star);
   o.s0 = (2.0 * (kPi * kPi) / 45.0) * pt.g_star_s;
   o.c_rel = (pt.stats == 0) ? pt.g_chi * (3.0 * kZeta3 / (4.0 * (kPi * kPi))) : pt.g_chi * (kZeta3 / (kPi * kPi));
@@ -87,6 +89,9 @@ __device__ __forceinline__ OdePoint ode_point(const lzq_point& pt, const lzq_ode
 #endif
 #ifndef LZQ_ODE_FASTMATH
 #define LZQ_ODE_FASTMATH 1  // 0: IEEE division and ROCm exp in the stage function (tools/ablate_ode.py);
+#endif
+#ifndef LZQ_ODE_COOP
+#define LZQ_ODE_COOP 1  // cooperative stage tables for group-uniform wavefronts (ode_integrate_kernel)
 #endif
 #ifndef LZQ_ODE_FMA
 #define LZQ_ODE_FMA LZQ_ODE_FASTMATH  // fused multiply-adds in the spline, the window exponent, Newton's f
@@ -143,8 +148,17 @@ struct OdeStage {
   double lam, E2, S, alpha, beta;
 };
 
-__device__ __forceinline__ OdeStage ode_stage(const OdePoint& o, const double* __restrict__ w, double x,
-                                              double* Av_out = nullptr) {
+// The same with the per-point scalars factored out: alpha (and S) per unit P * flux, lam per
+// unit sigma_v, beta per unit gamma_w.  Points that differ only in those scalars (and in their
+// initial state) share these values -- the cooperative mode of ode_integrate_kernel computes
+// them once per step for a whole wavefront.  Every stage goes through this split, so a point's
+// result does not depend on which mode its wavefront ran in.
+struct StageBase {
+  double a, lam, E2, beta;
+};
+
+__device__ __forceinline__ StageBase ode_stage_base(const OdePoint& o, const double* __restrict__ w, double x,
+                                                    double* Av_out = nullptr) {
   // One division per call (1/x); every other quotient of fpy:270-286 is a product with a
   // per-point reciprocal or with powers of 1/T: 1/s = (1/T)^3 / s0 and 1/(H x) =
   // (M_Pl/H0) (1/T)^2 / x, exact rewrites of s = s0 T^3 and H = H0 T^2 / M_Pl (fpy:85, 88)
@@ -170,23 +184,36 @@ __device__ __forceinline__ OdeStage ode_stage(const OdePoint& o, const double* _
     n_eq = o.c_nr * (T * sqrt(T)) * exp_nonpos(-o.m * iT);
     vbar = sqrt(pymax(8.0 * T * o.inv_v0, 0.0));
   }
-  const double J = o.flux * (0.25 * n_eq * vbar);             // fpy:222-223
+  const double Jb = 0.25 * n_eq * vbar;                       // fpy:222-223, J / flux
   const double Av = spline_eval(o, w, T);                     // fpy:214-218
   if (Av_out) *Av_out = Av;
-  const double SB = o.P * J * Av * window;                    // fpy:277
+  const double SBb = (Jb * Av) * window;                      // fpy:277, SB / (P flux)
   const bool plain = H > 1e-290 && s > 1e-290 && x == xc;     // the max() guards are inactive
   const double iT2 = iT * iT;
   const double is = plain ? (iT2 * iT) * o.inv_s0 : 1.0 / s;
   const double E = n_eq * is;                                 // fpy:280
-  const double SBs = SB * is;
   const double iHx = plain ? (o.mpl_over_h0 * iT2) * ixc : 1.0 / (H * x);
+  StageBase b;
+  b.a = (SBb * is) * iHx;                                     // fpy:282, 285
+  b.lam = s * iHx;                                            // fpy:279-281
+  b.E2 = E * E;
+  b.beta = H * iHx;                                           // fpy:284-285
+  return b;
+}
+
+__device__ __forceinline__ OdeStage stage_scale(const OdePoint& o, const StageBase& b) {
   OdeStage st;
-  st.lam = (o.sigmav * s) * iHx;
-  st.E2 = E * E;
-  st.S = (o.deplete ? SBs : 0.0) * iHx;                       // fpy:282
-  st.alpha = SBs * iHx;                                       // fpy:285
-  st.beta = (o.gamma_w * H) * iHx;
+  st.alpha = o.Pf * b.a;
+  st.S = o.deplete ? st.alpha : 0.0;
+  st.lam = o.sigmav * b.lam;
+  st.E2 = b.E2;
+  st.beta = o.gamma_w * b.beta;
   return st;
+}
+
+__device__ __forceinline__ OdeStage ode_stage(const OdePoint& o, const double* __restrict__ w, double x,
+                                              double* Av_out = nullptr) {
+  return stage_scale(o, ode_stage_base(o, w, x, Av_out));
 }
 
 // The Y_chi-only stage of the Riccati equation with no source term (deplete off):
@@ -525,6 +552,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
                                                                   const double* __restrict__ ws, int64_t max_steps,
                                                                   lzq_yield* __restrict__ out,
                                                                   int32_t* __restrict__ status) {
+  __shared__ StageBase s_base[kChiOnly ? 1 : kOdeBlock / 64][kChiOnly ? 1 : 64][3];  // cooperative mode
   const int64_t i = (int64_t)blockIdx.x * kOdeBlock + threadIdx.x;
   if (i >= n) return;
   const lzq_point pt = pts[i];
@@ -567,53 +595,95 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
     const RadauH hA = radau_h(R, h);
     const bool riccati = LZQ_ODE_PREDICT && o.sigmav != 0.0;
     double Zs[3] = {Ychi, Ychi, Ychi}, Yp = Ychi;  // previous step's start and stages (predictor)
-    bool have = false;
-    for (int64_t k = 0; k < N; ++k) {
-      const double xk = x0 + (double)k * h;
-      const bool split = xk < xb && xb <= xk + h;  // the last stage (x = xk + h) would see the other branch
-      const double xa = split ? nextafter(xb, -INFINITY) : xk + h;
-      double YB_prev = YB;
-      bool ok = true;
-      const double Ystart = Ychi;
-      bool use_guess = false;
-      if (riccati && have && !split) {
-        // the Riccati stage system has a second (unstable, other-sign) root: a predicted start
-        // is used only when it stays within 25% of Y_chi, where Newton converges to the same
-        // root as from Y_chi itself (an extrapolation across a fast transient can overshoot)
-        double g[3];
-        use_guess = true;
+    bool have = false, done = false;
+    // Cooperative mode (a full wavefront whose points agree in everything ode_stage_base reads:
+    // they differ at most in P, flux, sigma_v, Gamma_wash, deplete and the initial state, as in
+    // sweeps over those axes): lane l evaluates the stage ingredients of step kb + l for the
+    // whole wavefront into LDS, then every lane integrates those 64 steps of its own point from
+    // them.  The ingredients of a step are computed once instead of 64 times; the arithmetic is
+    // the same (ode_stage = stage_scale(ode_stage_base)), so results are bit-identical to the
+    // per-lane mode.  Split steps (the T = m/3 branch) always evaluate their own stages.
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    bool coop = false;
+    if (!kChiOnly && LZQ_ODE_COOP) {
+      auto same = [](double v) {  // bit-equal to the first active lane's value
+        const uint64_t b = __builtin_bit_cast(uint64_t, v);
+        const uint64_t u = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                           __builtin_amdgcn_readfirstlane((uint32_t)b);
+        return b == u;
+      };
+      const bool eq = same(o.m) && same(o.Tp) && same(o.B) && same(o.sig) && same(o.H0) && same(o.s0) &&
+                      same(o.c_rel) && same(o.c_nr) && same(o.v0) && same(o.T_lo) && same(o.T_hi) &&
+                      same(__builtin_bit_cast(double, w));
+      coop = __ballot(1) == ~0ull && __all(eq);
+    }
+    const int64_t block = coop ? 64 : N;
+    for (int64_t kb = 0; kb < N; kb += block) {
+      const int64_t kend = kb + block < N ? kb + block : N;
+      if (coop) {
+        const int64_t kl = kb + lane;
+        if (kl < N) {
+          const double xk = x0 + (double)kl * h;
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          g[j] = kRadauPred[j][0] * Yp + kRadauPred[j][1] * Zs[0] + kRadauPred[j][2] * Zs[1] + kRadauPred[j][3] * Zs[2];
-          use_guess = use_guess && fabs(g[j] - Ychi) <= 0.25 * fabs(Ychi);
+          for (int j = 0; j < 3; ++j) s_base[wv][lane][j] = ode_stage_base(o, w, xk + R.c[j] * h);
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      for (int64_t k = kb; k < kend && !done; ++k) {
+        const double xk = x0 + (double)k * h;
+        const bool split = xk < xb && xb <= xk + h;  // the last stage (x = xk + h) would see the other branch
+        const double xa = split ? nextafter(xb, -INFINITY) : xk + h;
+        double YB_prev = YB;
+        bool ok = true;
+        const double Ystart = Ychi;
+        bool use_guess = false;
+        if (riccati && have && !split) {
+          // the Riccati stage system has a second (unstable, other-sign) root: a predicted start
+          // is used only when it stays within 25% of Y_chi, where Newton converges to the same
+          // root as from Y_chi itself (an extrapolation across a fast transient can overshoot)
+          double g[3];
+          use_guess = true;
 #pragma unroll
-        for (int j = 0; j < 3; ++j) Zs[j] = g[j];
-      }
-      if (xa > xk) {
-        const double hs = split ? xa - xk : h;
-        OdeStage sg[3];
+          for (int j = 0; j < 3; ++j) {
+            g[j] = kRadauPred[j][0] * Yp + kRadauPred[j][1] * Zs[0] + kRadauPred[j][2] * Zs[1] + kRadauPred[j][3] * Zs[2];
+            use_guess = use_guess && fabs(g[j] - Ychi) <= 0.25 * fabs(Ychi);
+          }
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
-          sg[j] = (kChiOnly && !o.deplete) ? ode_stage_chi(o, xk + R.c[j] * hs) : ode_stage(o, w, xk + R.c[j] * hs);
-        ok = radau_step<!kChiOnly>(split ? radau_h(R, hs) : hA, sg, Ychi, YB, Zs, use_guess);
-      }
-      if (ok && split && xk + h > xb) {
-        const double hs = (xk + h) - xb;
-        OdeStage sg[3];
-        YB_prev = YB;
+          for (int j = 0; j < 3; ++j) Zs[j] = g[j];
+        }
+        if (xa > xk) {
+          const double hs = split ? xa - xk : h;
+          OdeStage sg[3];
+          if (coop && !split) {
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
-          sg[j] = (kChiOnly && !o.deplete) ? ode_stage_chi(o, xb + R.c[j] * hs) : ode_stage(o, w, xb + R.c[j] * hs);
-        ok = radau_step<!kChiOnly>(radau_h(R, hs), sg, Ychi, YB, Zs, false);
+            for (int j = 0; j < 3; ++j) sg[j] = stage_scale(o, s_base[wv][k - kb][j]);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+              sg[j] = (kChiOnly && !o.deplete) ? ode_stage_chi(o, xk + R.c[j] * hs) : ode_stage(o, w, xk + R.c[j] * hs);
+          }
+          ok = radau_step<!kChiOnly>(split ? radau_h(R, hs) : hA, sg, Ychi, YB, Zs, use_guess);
+        }
+        if (ok && split && xk + h > xb) {
+          const double hs = (xk + h) - xb;
+          OdeStage sg[3];
+          YB_prev = YB;
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+            sg[j] = (kChiOnly && !o.deplete) ? ode_stage_chi(o, xb + R.c[j] * hs) : ode_stage(o, w, xb + R.c[j] * hs);
+          ok = radau_step<!kChiOnly>(radau_h(R, hs), sg, Ychi, YB, Zs, false);
+        }
+        have = !split;   // the predictor needs a full regular step behind it
+        Yp = Ystart;
+        if (!ok) {
+          YB = YB_prev;  // report the state at the start of the failed step, like sol.y[:, -1] (fpy:408-410)
+          st = LZQ_ODE_NEWTON;
+          done = true;
+        }
       }
-      have = !split;   // the predictor needs a full regular step behind it
-      Yp = Ystart;
-      if (!ok) {
-        YB = YB_prev;  // report the state at the start of the failed step, like sol.y[:, -1] (fpy:408-410)
-        st = LZQ_ODE_NEWTON;
-        break;
-      }
+      if (coop) __builtin_amdgcn_wave_barrier();  // every lane is done with this block's table
     }
   }
   if (st == LZQ_ODE_OK || st == LZQ_ODE_NEWTON) {  // fpy:412-417

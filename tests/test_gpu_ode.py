@@ -266,3 +266,44 @@ def test_ode_quadrature_sweep_shared_and_deterministic(gpu_engine):
     r, _ = gpu_engine.ode(pts[ode], ods[ode])
     rr = r.cpu().numpy()
     assert np.max(np.abs(q.cpu().numpy()[:, :2] - rr[:, :2]) / np.abs(rr[:, :2])) < 1e-11
+
+
+def test_ode_cooperative_waves_bit_identical(gpu_engine):
+    """ode_integrate_kernel's cooperative mode (a full wavefront whose points differ only in P,
+    flux, sigma_v, Gamma_wash, deplete and the initial state computes each step's stage
+    ingredients once, into LDS) gives the same bits as the per-lane mode: the same 2 x 128
+    points run grouped (two uniform wavefronts per group) and interleaved (no uniform
+    wavefront), with wash-out, depletion, Riccati (sigma_v != 0) and thermal points mixed."""
+    rng = np.random.default_rng(31)
+    groups = []
+    for m_chi in (0.95, 40.0):           # the second crosses T = m/3 inside its window (split step)
+        g = []
+        for _ in range(128):
+            c = full_cfg(BASE_CFG)
+            c.update(NARROW, m_chi_GeV=m_chi, P_chi_to_B=float(rng.uniform(0.05, 1.0)),
+                     incident_flux_scale=float(10 ** rng.uniform(-10, -8)),
+                     Gamma_wash_over_H=float(rng.choice([0.0, 0.5, 2.0])),
+                     sigma_v_chi_GeV_m2=float(rng.choice([0.0, 1e-16, 1e-12])),
+                     deplete_DM_from_source=bool(rng.uniform() < 0.3),
+                     regime=str(rng.choice(["thermal", "nonthermal"])))
+            if c["Gamma_wash_over_H"] == 0.0 and c["sigma_v_chi_GeV_m2"] == 0.0:
+                c["deplete_DM_from_source"] = True
+            g.append(c)
+        groups.append(g)
+    grouped = groups[0] + groups[1]
+    inter = [c for pair in zip(groups[0], groups[1]) for c in pair]
+    p, o = recs(grouped)
+    a, sa = gpu_engine.ode(p, o, share_tables=True)
+    p2, o2 = recs(inter)
+    b, sb = gpu_engine.ode(p2, o2, share_tables=True)
+    order = np.concatenate([np.arange(0, 256, 2), np.arange(1, 256, 2)])   # interleaved -> grouped order
+    b, sb = b[order], sb[order]
+    assert torch_equal(sa, sb) and torch_equal(a, b)
+    # and against the C restatement (points both finished normally)
+    ref, sr = O.ode_batch(grouped, nthreads=16)
+    t, st = a.cpu().numpy(), sa.cpu().numpy()
+    assert int((st == 0).sum()) >= 200
+    for row, rr, s1, s2 in zip(t, ref, st, sr):
+        if s1 == 0 and s2 == 0:
+            for v, w in zip(row[:5], rr[:5]):
+                assert rel_err(v, w) < 1e-10, (v, w)

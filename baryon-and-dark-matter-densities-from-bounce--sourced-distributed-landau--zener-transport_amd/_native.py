@@ -60,7 +60,7 @@ FIELD.update({"delta_LZ": 32, "m_mix": 33, "dprime": 34})
 FERMION, BOSON = 0, 1
 THERMAL, NONTHERMAL, REGIME_OTHER = 0, 1, 2
 LZQ_NZ = 1200
-TUNE_EXP, TUNE_TRUNCATE = 0, 1  # enum lzq_tune_key
+TUNE_EXP, TUNE_TRUNCATE, TUNE_ODE_COOP = 0, 1, 2  # enum lzq_tune_key
 EXP_POLY11, EXP_TABLE = 0, 1  # enum lzq_exp_variant
 LZQ_MAX_AXES = 8
 ABI_VERSION = 1  # LZQ_ABI_VERSION (tests/test_capi.py checks it against the library)

@@ -988,6 +988,12 @@ int lzq_tune(int32_t key, int32_t value) {
     g_truncate = value;
     return prev;
   }
+  if (key == LZQ_TUNE_ODE_COOP) {
+    if (value != 0 && value != 1) return fail(LZQ_EINVAL, "lzq_tune: ode_coop must be 0 or 1, got %d", value);
+    int prev = lzq::g_ode_coop;
+    lzq::g_ode_coop = value;
+    return prev;
+  }
   return fail(LZQ_EINVAL, "lzq_tune: unknown key %d", key);
 }
 

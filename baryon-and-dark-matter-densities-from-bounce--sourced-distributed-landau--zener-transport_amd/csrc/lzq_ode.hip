@@ -30,6 +30,7 @@ namespace lzq {
 #define LZQ_ODE_MIN_WAVES 2
 #endif
 constexpr int kOdeBlock = 256;
+int g_ode_coop = 1;  // lzq_tune(LZQ_TUNE_ODE_COOP)
 constexpr double kInvMplGeV = 1.0 / kMplGeV;
 
 // ---------------------------------------------------------------------------------------
@@ -218,8 +219,9 @@ __device__ __forceinline__ OdeStage ode_stage(const OdePoint& o, const double* _
 
 // The Y_chi-only stage of the Riccati equation with no source term (deplete off):
 // lam = sigma_v s/(H x), E2 = (n_eq/s)^2, S = 0 -- no spline, no window (ode_stage's
-// operations otherwise).  alpha / beta are not formed (Y_B comes from the quadrature).
-__device__ __forceinline__ OdeStage ode_stage_chi(const OdePoint& o, double x) {
+// operations otherwise).  alpha / beta are not formed (Y_B comes from the quadrature).  Split
+// like ode_stage into a shared base (lam per unit sigma_v, E2) and the per-point product.
+__device__ __forceinline__ StageBase ode_stage_chi_base(const OdePoint& o, double x) {
   const double xc = pymax(x, 1e-30);
   const double ixc = rcp_pos(xc);
   const double T = o.m * ixc;
@@ -235,13 +237,26 @@ __device__ __forceinline__ OdeStage ode_stage_chi(const OdePoint& o, double x) {
   const double is = plain ? (iT2 * iT) * o.inv_s0 : 1.0 / s;
   const double E = n_eq * is;
   const double iHx = plain ? (o.mpl_over_h0 * iT2) * ixc : 1.0 / (H * x);
+  StageBase b;
+  b.a = 0.0;
+  b.lam = s * iHx;
+  b.E2 = E * E;
+  b.beta = 0.0;
+  return b;
+}
+
+__device__ __forceinline__ OdeStage chi_scale(const OdePoint& o, const StageBase& b) {
   OdeStage st;
-  st.lam = (o.sigmav * s) * iHx;
-  st.E2 = E * E;
+  st.lam = o.sigmav * b.lam;
+  st.E2 = b.E2;
   st.S = 0.0;
   st.alpha = 0.0;
   st.beta = 0.0;
   return st;
+}
+
+__device__ __forceinline__ OdeStage ode_stage_chi(const OdePoint& o, double x) {
+  return chi_scale(o, ode_stage_chi_base(o, x));
 }
 
 // CubicSpline's check of the knots linspace(T_lo, T_hi, 800): strictly increasing.
@@ -551,8 +566,8 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
                                                                   const int32_t* __restrict__ tidx,
                                                                   const double* __restrict__ ws, int64_t max_steps,
                                                                   lzq_yield* __restrict__ out,
-                                                                  int32_t* __restrict__ status) {
-  __shared__ StageBase s_base[kChiOnly ? 1 : kOdeBlock / 64][kChiOnly ? 1 : 64][3];  // cooperative mode
+                                                                  int32_t* __restrict__ status, int coop_on) {
+  __shared__ StageBase s_base[kOdeBlock / 64][64][3];  // cooperative mode
   const int64_t i = (int64_t)blockIdx.x * kOdeBlock + threadIdx.x;
   if (i >= n) return;
   const lzq_point pt = pts[i];
@@ -573,6 +588,9 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
     Ychi = n_chi_eq(o.T_hi, m, pt.g_chi, pt.stats) / s_entropy(o.T_hi, pt.g_star_s);
   }
   double YB = kChiOnly ? out[i].Y_B : 0.0;
+#ifdef LZQ_ODE_COOP_DEBUG
+  double dbg_coop = -1.0;
+#endif
   const double x_p = m / pymax(T_p, 1e-30);
   const double max_step = pymin(pymin(fabs(x1 - x0) / 20000.0, x_p / 1000.0), 5e-4);  // fpy:403-404
   double steps = 0.0;
@@ -596,7 +614,8 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
     const bool riccati = LZQ_ODE_PREDICT && o.sigmav != 0.0;
     double Zs[3] = {Ychi, Ychi, Ychi}, Yp = Ychi;  // previous step's start and stages (predictor)
     bool have = false, done = false;
-    // Cooperative mode (a full wavefront whose points agree in everything ode_stage_base reads:
+    // Cooperative mode (a full wavefront whose points agree in everything ode_stage_base (or
+    // ode_stage_chi_base: kChiOnly, the same deplete flag) reads:
     // they differ at most in P, flux, sigma_v, Gamma_wash, deplete and the initial state, as in
     // sweeps over those axes): lane l evaluates the stage ingredients of step kb + l for the
     // whole wavefront into LDS, then every lane integrates those 64 steps of its own point from
@@ -605,17 +624,18 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
     // per-lane mode.  Split steps (the T = m/3 branch) always evaluate their own stages.
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     bool coop = false;
-    if (!kChiOnly && LZQ_ODE_COOP) {
-      auto same = [](double v) {  // bit-equal to the first active lane's value
+    if (LZQ_ODE_COOP && coop_on) {
+      auto same = [](double v) {  // bit-equal to lane 0's value (the wave is full here)
         const uint64_t b = __builtin_bit_cast(uint64_t, v);
-        const uint64_t u = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
-                           __builtin_amdgcn_readfirstlane((uint32_t)b);
-        return b == u;
+        return b == __builtin_bit_cast(uint64_t, __shfl(v, 0, 64));
       };
       const bool eq = same(o.m) && same(o.Tp) && same(o.B) && same(o.sig) && same(o.H0) && same(o.s0) &&
                       same(o.c_rel) && same(o.c_nr) && same(o.v0) && same(o.T_lo) && same(o.T_hi) &&
-                      same(__builtin_bit_cast(double, w));
+                      same(__builtin_bit_cast(double, w)) && (!kChiOnly || same((double)o.deplete));
       coop = __ballot(1) == ~0ull && __all(eq);
+#ifdef LZQ_ODE_COOP_DEBUG
+      dbg_coop = coop ? 1.0 : 0.0;
+#endif
     }
     const int64_t block = coop ? 64 : N;
     for (int64_t kb = 0; kb < N; kb += block) {
@@ -625,7 +645,9 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
         if (kl < N) {
           const double xk = x0 + (double)kl * h;
 #pragma unroll
-          for (int j = 0; j < 3; ++j) s_base[wv][lane][j] = ode_stage_base(o, w, xk + R.c[j] * h);
+          for (int j = 0; j < 3; ++j)
+            s_base[wv][lane][j] = (kChiOnly && !o.deplete) ? ode_stage_chi_base(o, xk + R.c[j] * h)
+                                                           : ode_stage_base(o, w, xk + R.c[j] * h);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -658,7 +680,8 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
           OdeStage sg[3];
           if (coop && !split) {
 #pragma unroll
-            for (int j = 0; j < 3; ++j) sg[j] = stage_scale(o, s_base[wv][k - kb][j]);
+            for (int j = 0; j < 3; ++j)
+              sg[j] = (kChiOnly && !o.deplete) ? chi_scale(o, s_base[wv][k - kb][j]) : stage_scale(o, s_base[wv][k - kb][j]);
           } else {
 #pragma unroll
             for (int j = 0; j < 3; ++j)
@@ -694,6 +717,9 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
     r.rho_DM_kg_m3 = nDM0 * (m * kGeVToKg);
     r.DM_over_B = r.rho_DM_kg_m3 / pymax(r.rho_B_kg_m3, 1e-300);
   }
+#ifdef LZQ_ODE_COOP_DEBUG
+  r.P_used = dbg_coop;  // debug builds only: 1 = cooperative wavefront, 0 = per-lane
+#endif
   out[i] = r;
   if (status) status[i] = st;
 }
@@ -936,7 +962,7 @@ int lzq_ode_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, in
   if (n == 0) return LZQ_OK;
   hipLaunchKernelGGL(lzq::ode_integrate_kernel<false>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0,
                      (hipStream_t)stream, d_points, d_ode, n, (const int32_t*)nullptr, d_work, max_steps, d_out,
-                     d_status);
+                     d_status, lzq::g_ode_coop);
   return hip_check(hipGetLastError(), "lzq_ode_integrate");
 }
 
@@ -952,7 +978,8 @@ int lzq_ode_integrate_shared(const lzq_point* d_points, const lzq_ode_params* d_
   if (ode_blocks(n) > 2147483647LL) return lzq_set_error(LZQ_EINVAL, "lzq_ode_integrate_shared: n too large");
   if (n == 0) return LZQ_OK;
   hipLaunchKernelGGL(lzq::ode_integrate_kernel<false>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0,
-                     (hipStream_t)stream, d_points, d_ode, n, d_table_index, d_work, max_steps, d_out, d_status);
+                     (hipStream_t)stream, d_points, d_ode, n, d_table_index, d_work, max_steps, d_out, d_status,
+                     lzq::g_ode_coop);
   return hip_check(hipGetLastError(), "lzq_ode_integrate_shared");
 }
 
@@ -973,7 +1000,8 @@ int lzq_ode_quadrature(const lzq_point* d_points, const lzq_ode_params* d_ode, i
   if (rc) return rc;
   // sigma_v != 0: Y_chi's Riccati equation by the Radau stepping (Y_B from the quadrature above)
   hipLaunchKernelGGL(lzq::ode_integrate_kernel<true>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0,
-                     (hipStream_t)stream, d_points, d_ode, n, d_table_index, d_work, max_steps, d_out, d_status);
+                     (hipStream_t)stream, d_points, d_ode, n, d_table_index, d_work, max_steps, d_out, d_status,
+                     lzq::g_ode_coop);
   return hip_check(hipGetLastError(), "lzq_ode_quadrature");
 }
 

@@ -41,6 +41,14 @@ class Engine:
             self._check(prev)
         return {_native.EXP_POLY11: "poly11", _native.EXP_TABLE: "table"}[prev]
 
+    def tune_ode_coop(self, on: bool) -> bool:
+        """Cooperative stage tables in the ODE integrator (include/lzq.h LZQ_TUNE_ODE_COOP; on by
+        default, bit-identical results either way).  Returns the previous setting."""
+        prev = self.lib.lzq_tune(_native.TUNE_ODE_COOP, 1 if on else 0)
+        if prev < 0:
+            self._check(prev)
+        return bool(prev)
+
     def tune_truncate(self, on: bool) -> bool:
         """Exact-underflow truncation of the z-sums (bit-identical results, fewer nodes
         executed; include/lzq.h LZQ_TUNE_TRUNCATE).  Returns the previous setting."""

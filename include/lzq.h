@@ -123,7 +123,11 @@ int lzq_ztables(double* z, double* gamma4, double* omega);
  * node beyond which every lane's term is below 2^-1080, where it can no longer change the
  * FP64 accumulator.  Results are bit-identical to the dense sum; fewer nodes are executed.
  * The headline benchmark is dense and reports this mode separately. */
-enum lzq_tune_key { LZQ_TUNE_EXP = 0, LZQ_TUNE_TRUNCATE = 1 };
+/* LZQ_TUNE_ODE_COOP (1 = on, the default; 0 = off): the ODE integrator's cooperative mode,
+ * where a full wavefront of points that differ only in P, flux, sigma_v, Gamma_wash, deplete
+ * and the initial state evaluates each step's stage ingredients once for the whole wavefront.
+ * Results are bit-identical either way (tests/test_gpu_ode.py). */
+enum lzq_tune_key { LZQ_TUNE_EXP = 0, LZQ_TUNE_TRUNCATE = 1, LZQ_TUNE_ODE_COOP = 2 };
 enum lzq_exp_variant { LZQ_EXP_POLY11 = 0, LZQ_EXP_TABLE = 1 };
 int lzq_tune(int32_t key, int32_t value);
 

@@ -114,3 +114,12 @@ def test_ode_table_groups_host_logic():
     assert all(int(f) == int(np.argmax(kinds == kinds[int(f)])) for f in first)   # first occurrence
     p["I_p"] = rng.uniform(size=p.size)                                           # all distinct: no sharing
     assert table_groups(torch.from_numpy(p.view(np.uint8).copy()), p.size) is None
+
+
+def test_tune_ode_coop_knob():
+    """lzq_tune(LZQ_TUNE_ODE_COOP): on by default, 0/1 only, returns the previous value."""
+    n = pkg("_native")
+    L = n.load()
+    assert L.lzq_tune(n.TUNE_ODE_COOP, 0) == 1
+    assert L.lzq_tune(n.TUNE_ODE_COOP, 1) == 0
+    assert L.lzq_tune(n.TUNE_ODE_COOP, 2) < 0 and b"ode_coop" in L.lzq_last_error()

@@ -299,6 +299,20 @@ def test_ode_cooperative_waves_bit_identical(gpu_engine):
     order = np.concatenate([np.arange(0, 256, 2), np.arange(1, 256, 2)])   # interleaved -> grouped order
     b, sb = b[order], sb[order]
     assert torch_equal(sa, sb) and torch_equal(a, b)
+    prev = gpu_engine.tune_ode_coop(False)         # the grouped batch again, every wave per-lane
+    try:
+        c, sc = gpu_engine.ode(p, o, share_tables=True)
+    finally:
+        gpu_engine.tune_ode_coop(prev)
+    assert prev and torch_equal(sa, sc) and torch_equal(a, c)
+    # the quadrature method's Riccati stepping of Y_chi (sigma_v != 0) has the same mode
+    q1, sq1 = gpu_engine.ode(p, o, share_tables=True, method="quadrature")
+    gpu_engine.tune_ode_coop(False)
+    try:
+        q0, sq0 = gpu_engine.ode(p, o, share_tables=True, method="quadrature")
+    finally:
+        gpu_engine.tune_ode_coop(True)
+    assert torch_equal(sq1, sq0) and torch_equal(q1, q0)
     # and against the C restatement (points both finished normally)
     ref, sr = O.ode_batch(grouped, nthreads=16)
     t, st = a.cpu().numpy(), sa.cpu().numpy()

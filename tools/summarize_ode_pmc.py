@@ -3,7 +3,8 @@
 ode_integrate_kernel's VALU and FP64 instructions per wave-step (PMC pass) and its duration
 (kernel-trace pass), hence executed FP64 TFLOP/s against the 78.6 TFLOP/s FP64 vector peak.
 bench_ode.py runs, per config, the shared-table and the per-point-table path: two
-integrate dispatches with the same work, in that order."""
+ode_integrate_kernel<false> dispatches with the same work, in that order (the quadrature
+method's ode_integrate_kernel<true> dispatches are not counted)."""
 import csv
 import json
 import os
@@ -20,11 +21,11 @@ def main():
     rows = list(csv.DictReader(open(os.path.join(src, "pmc", "run_counter_collection.csv"))))
     disp = defaultdict(dict)
     for r in rows:
-        if "ode_integrate_kernel" in r["Kernel_Name"]:
+        if "ode_integrate_kernel<false>" in r["Kernel_Name"]:
             disp[int(r["Dispatch_Id"])][r["Counter_Name"]] = disp[int(r["Dispatch_Id"])].get(r["Counter_Name"], 0.0) + \
                 float(r["Counter_Value"])
     tr = [r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv")))
-          if "ode_integrate_kernel" in r["Kernel_Name"]]
+          if "ode_integrate_kernel<false>" in r["Kernel_Name"]]
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9 for r in tr]
     pmc = [disp[k] for k in sorted(disp)]
     # skip the warm-up dispatches (64 points each, 2 per config): keep dispatches with the config's wave count

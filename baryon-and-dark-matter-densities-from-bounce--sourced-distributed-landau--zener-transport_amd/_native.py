@@ -72,6 +72,10 @@ EXPORTS = ("lzq_abi_version", "lzq_last_error", "lzq_init", "lzq_ztables", "lzq_
            "lzq_ode_aov_T", "lzq_ode_rhs")
 # the lzq_point fields an ODE spline table depends on (A/V kernel fpy:141-156 + window fpy:368-369)
 ODE_TABLE_KEY = ("I_p", "beta_over_H", "T_p_GeV", "v_w", "g_star", "T_min_over_Tp", "T_max_over_Tp")
+# every point field the ODE integrator's stage ingredients read besides P, flux and the ODE
+# parameters (ode_stage_base / ode_stage_chi_base + the spline table): points equal in these can
+# share a cooperative wavefront (include/lzq.h LZQ_TUNE_ODE_COOP)
+ODE_STAGE_KEY = ODE_TABLE_KEY + ("m_chi_GeV", "g_chi", "g_star_s", "source_shape_sigma_y", "stats")
 
 
 class LzqError(RuntimeError):

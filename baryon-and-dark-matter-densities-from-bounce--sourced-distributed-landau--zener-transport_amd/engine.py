@@ -155,7 +155,7 @@ class Engine:
         return work, status
 
     def ode(self, points, ode_params, max_steps: int = 1 << 26, chunk: int = 1 << 18,
-            share_tables: bool = True, method: str = "radau") -> tuple:
+            share_tables: bool = True, method: str = "radau", group_waves: bool = True) -> tuple:
         """fpy:385-417 for n points (POINT_DTYPE records + ODE_DTYPE records): (n, 6) yields
         table and (n,) int32 status (enum lzq_ode_status), both on the device.  Points are
         processed in chunks so that the spline workspace stays <= chunk * 25.6 KB (6.7 GB at the
@@ -166,7 +166,11 @@ class Engine:
         method: "radau" (default: the reference's integrator, fixed steps) or "quadrature"
         (lzq_ode_quadrature, opt-in: Y_B -- and Y_chi when sigma_v = 0 -- by the exact
         integrating-factor quadrature; with sigma_v != 0, Y_chi's Riccati equation is stepped
-        alone by Radau)."""
+        alone by Radau).
+        group_waves: launch the points in an order that puts points with equal stage keys
+        (_native.ODE_STAGE_KEY, + deplete) next to each other, so that whole wavefronts qualify
+        for the integrator's cooperative mode; results are scattered back to the input order.
+        Each point's result is the same bits in either order."""
         if method not in ("radau", "quadrature"):
             raise ValueError(f"method must be 'radau' or 'quadrature', got {method!r}")
         pts = np.ascontiguousarray(points, dtype=_native.POINT_DTYPE).reshape(-1)
@@ -174,6 +178,9 @@ class Engine:
         if pts.size != ods.size:
             raise ValueError("points and ode_params must have the same length")
         n = pts.size
+        order = wave_order(pts, ods) if group_waves else None
+        if order is not None:
+            pts, ods = pts[order], ods[order]
         out = torch.empty((n, 6), dtype=torch.float64, device=self.device)
         status = torch.zeros(n, dtype=torch.int32, device=self.device)
         work = None
@@ -221,6 +228,11 @@ class Engine:
                     keep.append((d_rep, d_idx))
             keep.append((d_pts, d_ode))
         self._keepalive = (keep, work)
+        if order is not None:
+            idx = torch.from_numpy(order).to(self.device)
+            out_in, st_in = torch.empty_like(out), torch.empty_like(status)
+            out_in[idx], st_in[idx] = out, status
+            out, status = out_in, st_in
         return out, status
 
     def ode_aov_T(self, point, T_lo: float, T_hi: float, work_point: torch.Tensor, Ts) -> torch.Tensor:
@@ -273,6 +285,29 @@ class Engine:
 
 
 _MIX = -7046029254386353131  # 0x9E3779B97F4A7C15 as int64 (torch multiplies wrap)
+
+
+def wave_order(pts: np.ndarray, ods: np.ndarray):
+    """A launch order (int64 permutation) that makes points equal in _native.ODE_STAGE_KEY (and
+    deplete) contiguous, or None when the input is already grouped or has no repeated keys.
+    A 64-bit mix of the key fields' bits is sorted stably; a hash collision only puts unequal
+    points in one wavefront, which the kernel detects and runs per lane."""
+    n = pts.size
+    if n <= 64:
+        return None
+    h = np.zeros(n, dtype=np.uint64)
+    mix = np.uint64(0x9E3779B97F4A7C15)
+    with np.errstate(over="ignore"):
+        for f in _native.ODE_STAGE_KEY:
+            col = np.ascontiguousarray(pts[f])
+            bits = col.view(np.uint64) if col.dtype.itemsize == 8 else col.astype(np.uint64)
+            h = (h * mix) ^ bits
+        h = (h * mix) ^ ods["deplete_DM_from_source"].astype(np.uint64)
+    breaks = int(np.count_nonzero(h[1:] != h[:-1]))
+    distinct = int(np.unique(h).size)
+    if distinct == n or breaks <= 2 * (distinct - 1):
+        return None
+    return np.argsort(h, kind="stable")
 _KEY_WORDS = [_native.POINT_DOUBLE_FIELDS.index(f) for f in _native.ODE_TABLE_KEY]  # 8-byte words of lzq_point
 
 

@@ -295,7 +295,9 @@ def test_ode_cooperative_waves_bit_identical(gpu_engine):
     p, o = recs(grouped)
     a, sa = gpu_engine.ode(p, o, share_tables=True)
     p2, o2 = recs(inter)
-    b, sb = gpu_engine.ode(p2, o2, share_tables=True)
+    b, sb = gpu_engine.ode(p2, o2, share_tables=True, group_waves=False)   # every wave mixed: per-lane
+    g2, sg2 = gpu_engine.ode(p2, o2, share_tables=True)   # regrouped for the launch, scattered back
+    assert torch_equal(b, g2) and torch_equal(sb, sg2)
     order = np.concatenate([np.arange(0, 256, 2), np.arange(1, 256, 2)])   # interleaved -> grouped order
     b, sb = b[order], sb[order]
     assert torch_equal(sa, sb) and torch_equal(a, b)

@@ -89,6 +89,27 @@ def main():
                           "cpu_oracle_points_per_s": k / dtc, "cpu_threads": threads,
                           "cpu_sample": k, "max_rel_diff_gpu_vs_oracle": err}), flush=True)
 
+    # a sweep whose fastest axis is m_chi (4 values cycling): consecutive points differ in their
+    # stage key, so wavefronts are mixed unless Engine.ode regroups them (group_waves)
+    n = n_narrow
+    cfgs = cfgs_for({"Gamma_wash_over_H": 1.0, "T_max_over_Tp": 1.6, "T_min_over_Tp": 0.6}, n)
+    for i, c in enumerate(cfgs):
+        c["m_chi_GeV"] = (0.95, 3.0, 10.0, 30.0)[i % 4]
+    pts = np.concatenate([cfgm.to_point(c) for c in cfgs])
+    ods = np.concatenate([cfgm.to_ode_params(c) for c in cfgs])
+    res = {}
+    for g in (True, False):
+        eng.ode(pts[:256], ods[:256], group_waves=g)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        tab, st = eng.ode(pts, ods, chunk=chunk, group_waves=g)
+        torch.cuda.synchronize()
+        res[g] = (n / (time.perf_counter() - t0), tab, st)
+    print(json.dumps({"config": "narrow_wash_mchi_fastest", "points": n, "kernels": 4,
+                      "gpu_points_per_s_grouped": res[True][0], "gpu_points_per_s_input_order": res[False][0],
+                      "bit_identical": bool(torch.equal(res[True][1], res[False][1])),
+                      "all_ok": bool((res[True][2] == 0).all())}), flush=True)
+
 
 if __name__ == "__main__":
     main()

@@ -178,18 +178,21 @@ class Engine:
         if pts.size != ods.size:
             raise ValueError("points and ode_params must have the same length")
         n = pts.size
-        order = wave_order(pts, ods) if group_waves else None
+        d_pts_all = self.points_to_device(pts)
+        d_ode_all = torch.from_numpy(ods.view(np.uint8).copy()).to(self.device)
+        order = wave_order(d_pts_all, d_ode_all, n) if group_waves else None
         if order is not None:
-            pts, ods = pts[order], ods[order]
+            d_pts_all = d_pts_all.view(n, -1)[order].contiguous().view(-1)
+            d_ode_all = d_ode_all.view(n, -1)[order].contiguous().view(-1)
+        rp, ro = _native.POINT_DTYPE.itemsize, _native.ODE_DTYPE.itemsize
         out = torch.empty((n, 6), dtype=torch.float64, device=self.device)
         status = torch.zeros(n, dtype=torch.int32, device=self.device)
         work = None
         keep = []
         for c0 in range(0, n, chunk):
             c1 = min(n, c0 + chunk)
-            p = pts[c0:c1]
-            d_pts = self.points_to_device(p)
-            d_ode = torch.from_numpy(ods[c0:c1].view(np.uint8).copy()).to(self.device)
+            d_pts = d_pts_all[c0 * rp:c1 * rp]
+            d_ode = d_ode_all[c0 * ro:c1 * ro]
             rep = table_groups(d_pts, c1 - c0) if share_tables else None
             if rep is not None:
                 rep, inv = rep
@@ -227,11 +230,11 @@ class Engine:
                                                                   self._stream()))
                     keep.append((d_rep, d_idx))
             keep.append((d_pts, d_ode))
+        keep.append((d_pts_all, d_ode_all))
         self._keepalive = (keep, work)
         if order is not None:
-            idx = torch.from_numpy(order).to(self.device)
             out_in, st_in = torch.empty_like(out), torch.empty_like(status)
-            out_in[idx], st_in[idx] = out, status
+            out_in[order], st_in[order] = out, status
             out, status = out_in, st_in
         return out, status
 
@@ -287,27 +290,32 @@ class Engine:
 _MIX = -7046029254386353131  # 0x9E3779B97F4A7C15 as int64 (torch multiplies wrap)
 
 
-def wave_order(pts: np.ndarray, ods: np.ndarray):
-    """A launch order (int64 permutation) that makes points equal in _native.ODE_STAGE_KEY (and
-    deplete) contiguous, or None when the input is already grouped or has no repeated keys.
-    A 64-bit mix of the key fields' bits is sorted stably; a hash collision only puts unequal
-    points in one wavefront, which the kernel detects and runs per lane."""
-    n = pts.size
+def wave_order(d_pts: torch.Tensor, d_ode: torch.Tensor, n: int):
+    """A launch order (int64 permutation tensor, on the points' device) that makes points equal
+    in _native.ODE_STAGE_KEY (and deplete) contiguous, or None when the input is already grouped
+    or has no repeated keys.  d_pts / d_ode: the lzq_point / lzq_ode_params records as byte
+    tensors.  A 64-bit mix of the key fields' bits is sorted stably; a hash collision only puts
+    unequal points in one wavefront, which the kernel detects and runs per lane."""
     if n <= 64:
         return None
-    h = np.zeros(n, dtype=np.uint64)
-    mix = np.uint64(0x9E3779B97F4A7C15)
-    with np.errstate(over="ignore"):
-        for f in _native.ODE_STAGE_KEY:
-            col = np.ascontiguousarray(pts[f])
-            bits = col.view(np.uint64) if col.dtype.itemsize == 8 else col.astype(np.uint64)
-            h = (h * mix) ^ bits
-        h = (h * mix) ^ ods["deplete_DM_from_source"].astype(np.uint64)
-    breaks = int(np.count_nonzero(h[1:] != h[:-1]))
-    distinct = int(np.unique(h).size)
+    w64 = d_pts.view(n, _native.POINT_DTYPE.itemsize).view(torch.int64)
+    w32 = d_pts.view(n, _native.POINT_DTYPE.itemsize).view(torch.int32)
+    o32 = d_ode.view(n, _native.ODE_DTYPE.itemsize).view(torch.int32)
+    h = torch.zeros(n, dtype=torch.int64, device=d_pts.device)
+    for f in _native.ODE_STAGE_KEY:
+        off = _native.POINT_DTYPE.fields[f][1]
+        col = w64[:, off // 8] if _native.POINT_DTYPE.fields[f][0].itemsize == 8 else w32[:, off // 4].to(torch.int64)
+        h = (h * _MIX) ^ col
+    h = (h * _MIX) ^ o32[:, _native.ODE_DTYPE.fields["deplete_DM_from_source"][1] // 4].to(torch.int64)
+    breaks = int((h[1:] != h[:-1]).sum())
+    if breaks == 0:
+        return None
+    distinct = int(torch.unique(h).numel())
     if distinct == n or breaks <= 2 * (distinct - 1):
         return None
-    return np.argsort(h, kind="stable")
+    return torch.argsort(h, stable=True)
+
+
 _KEY_WORDS = [_native.POINT_DOUBLE_FIELDS.index(f) for f in _native.ODE_TABLE_KEY]  # 8-byte words of lzq_point
 
 

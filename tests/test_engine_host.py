@@ -2,6 +2,7 @@
 puts points with equal stage keys next to each other so that whole wavefronts qualify for the
 integrator's cooperative mode."""
 import numpy as np
+import torch
 
 from conftest import BASE_CFG, full_cfg, pkg
 
@@ -9,6 +10,14 @@ from conftest import BASE_CFG, full_cfg, pkg
 def _recs(cfgs):
     cfgm = pkg("config")
     return (np.concatenate([cfgm.to_point(c) for c in cfgs]), np.concatenate([cfgm.to_ode_params(c) for c in cfgs]))
+
+
+def _order(p, o):
+    """engine.wave_order on CPU byte tensors of the records, as a numpy permutation (or None)."""
+    tp = torch.from_numpy(np.ascontiguousarray(p).view(np.uint8).copy())
+    to = torch.from_numpy(np.ascontiguousarray(o).view(np.uint8).copy())
+    r = pkg("engine").wave_order(tp, to, p.size)
+    return None if r is None else r.numpy()
 
 
 def _cfgs(m_values, reps, rng):
@@ -23,13 +32,12 @@ def _cfgs(m_values, reps, rng):
 
 
 def test_wave_order_groups_interleaved_points():
-    wave_order = pkg("engine").wave_order
     rng = np.random.default_rng(3)
     grouped = _cfgs([0.95, 40.0, 300.0], 100, rng)
     p, o = _recs(grouped)
-    assert wave_order(p, o) is None                      # already contiguous
+    assert _order(p, o) is None                      # already contiguous
     perm = rng.permutation(len(grouped))
-    order = wave_order(p[perm], o[perm])
+    order = _order(p[perm], o[perm])
     assert order is not None and sorted(order.tolist()) == list(range(len(grouped)))
     m = p[perm]["m_chi_GeV"][order]
     assert int(np.count_nonzero(m[1:] != m[:-1])) == 2  # three contiguous groups
@@ -40,19 +48,18 @@ def test_wave_order_groups_interleaved_points():
 
 
 def test_wave_order_no_repeats_or_small():
-    wave_order = pkg("engine").wave_order
     rng = np.random.default_rng(4)
     distinct = _cfgs(np.linspace(1.0, 2.0, 200), 1, rng)
     p, o = _recs(distinct)
-    assert wave_order(p, o) is None                      # nothing to group
+    assert _order(p, o) is None                      # nothing to group
     small = _cfgs([0.95, 40.0], 20, rng)
     p, o = _recs(small)
-    assert wave_order(p[::-1], o[::-1]) is None          # <= 64 points: one wavefront anyway
+    assert _order(p[::-1], o[::-1]) is None          # <= 64 points: one wavefront anyway
     # the deplete flag is part of the key (it selects the Y_chi-only stage function)
     cfgs = _cfgs([0.95], 200, rng)
     for i, c in enumerate(cfgs):
         c["deplete_DM_from_source"] = bool(i % 2)
     p, o = _recs(cfgs)
-    order = wave_order(p, o)
+    order = _order(p, o)
     d = o["deplete_DM_from_source"][order]
     assert int(np.count_nonzero(d[1:] != d[:-1])) == 1

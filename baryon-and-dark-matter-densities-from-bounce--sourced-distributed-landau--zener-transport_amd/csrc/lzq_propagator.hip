@@ -56,8 +56,11 @@
 namespace lzq {
 
 constexpr int kPropBlock = 256;
+#ifndef LZQ_PROP_UNROLL
+#define LZQ_PROP_UNROLL 3  // step-loop unroll: ILP across steps (A/B: 1 -> 3 = -12%, tools/ablate_prop.py)
+#endif
 #ifndef LZQ_PROP_MIN_WAVES
-#define LZQ_PROP_MIN_WAVES 3  // 167 VGPRs (4 spilled outside the step loop): 3 waves/SIMD, -13% time vs 2 (tools/ablate_prop.py)
+#define LZQ_PROP_MIN_WAVES 2  // 217 VGPRs with the 3-step unroll, no spills (3 waves/SIMD: 168 VGPRs, spills; same time)
 #endif
 constexpr double kDeltaAdiabatic = 16.0;              // e^{-2 pi 16} = 2e-44
 constexpr double kStepsPerRadian = 3.0;              // ~1/3 rad of adiabatic phase per step at most
@@ -378,6 +381,7 @@ __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_k
       // oracle-matching kernels, so contraction is spelled out): 63 VALU per step where the
       // separate products and sums took 84.
 #define FMA __builtin_fma
+#pragma unroll LZQ_PROP_UNROLL
       for (int i = 0; i < Sc; ++i) {
         const double xm = FMA((double)i + 0.5, h, cl);
         const double D = slope * (xm - xcc);

@@ -568,8 +568,14 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
                                                                   lzq_yield* __restrict__ out,
                                                                   int32_t* __restrict__ status, int coop_on) {
   __shared__ StageBase s_base[kOdeBlock / 64][64][3];  // cooperative mode
-  const int64_t i = (int64_t)blockIdx.x * kOdeBlock + threadIdx.x;
-  if (i >= n) return;
+  // Lanes past the end of the batch are clones of their wavefront's first point (they compute
+  // it again and write nothing), so a partial wavefront -- a single CLI point included -- is
+  // still full and can run cooperatively.
+  const int64_t wave0 = (int64_t)blockIdx.x * kOdeBlock + (threadIdx.x & ~63);
+  if (wave0 >= n) return;
+  const int64_t i_self = (int64_t)blockIdx.x * kOdeBlock + threadIdx.x;
+  const bool real = i_self < n;
+  const int64_t i = real ? i_self : wave0;
   const lzq_point pt = pts[i];
   const OdePoint o = ode_point(pt, ode[i]);
   if (kChiOnly && (o.sigmav == 0.0 || (status && status[i] != LZQ_ODE_NOT_LINEAR))) return;
@@ -720,6 +726,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
 #ifdef LZQ_ODE_COOP_DEBUG
   r.P_used = dbg_coop;  // debug builds only: 1 = cooperative wavefront, 0 = per-lane
 #endif
+  if (!real) return;
   out[i] = r;
   if (status) status[i] = st;
 }

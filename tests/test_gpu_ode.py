@@ -307,6 +307,11 @@ def test_ode_cooperative_waves_bit_identical(gpu_engine):
     finally:
         gpu_engine.tune_ode_coop(prev)
     assert prev and torch_equal(sa, sc) and torch_equal(a, c)
+    # partial wavefronts (here: single points) are filled with clones of their first point, so
+    # they run cooperatively too; each must match the batch result bit for bit
+    for j in (0, 5, 131, 200):
+        one, s1 = gpu_engine.ode(p[j:j + 1], o[j:j + 1], share_tables=True)
+        assert torch_equal(one[0], a[j]) and torch_equal(s1[0], sa[j])
     # the quadrature method's Riccati stepping of Y_chi (sigma_v != 0) has the same mode
     q1, sq1 = gpu_engine.ode(p, o, share_tables=True, method="quadrature")
     gpu_engine.tune_ode_coop(False)

@@ -47,6 +47,20 @@ def main():
             for g in (True, False):
                 t, _ = e2.ode(pts, ods, group_waves=g)
                 out[f"{name}_group{int(g)}_coop_points"] = int((t[:, 5] == 1.0).sum())
+    # one point alone (the CLI's case): a wavefront of 1 real lane + 63 clones
+    for name, over in (("single_narrow", {"Gamma_wash_over_H": 1.0, "T_max_over_Tp": 1.6, "T_min_over_Tp": 0.6}),
+                       ("single_full_window", {"Gamma_wash_over_H": 1.0})):
+        c = cfgs_for(over, 1)
+        pts, ods = cfgm.to_point(c[0]), cfgm.to_ode_params(c[0])
+        for coop in (True, False):
+            eng.tune_ode_coop(coop)
+            eng.ode(pts, ods)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            eng.ode(pts, ods)
+            torch.cuda.synchronize()
+            out[f"{name}_coop{int(coop)}_seconds"] = round(time.perf_counter() - t0, 4)
+        eng.tune_ode_coop(True)
     print(json.dumps(out, indent=1))
 
 

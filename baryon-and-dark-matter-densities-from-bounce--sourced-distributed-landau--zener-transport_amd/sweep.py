@@ -398,16 +398,26 @@ def run_sweep(spec: SweepSpec, engine=None, rank: int = 0, world: int = 1, chunk
     return gather_table(local, spec.total, rank, world, group)
 
 
+def coherent_P(spec: SweepSpec, s: int, n: int, engine):
+    """Coherent conversion probability of grid points [s, s+n) through their crossings
+    (spec.crossings; lzq_lz_propagate), a device tensor."""
+    m, dp, xi, v_w = spec.crossing_arrays(s, n, engine.device)
+    if not bool((v_w == v_w[0]).all()):
+        raise NotImplementedError("multi-crossing sweeps need a single v_w")
+    return engine.lz_propagate(m, dp, xi, float(v_w[0]), spec.crossings.window_lz, spec.crossings.steps)
+
+
 def make_compute(spec: SweepSpec, engine) -> ComputeFn:
     """(start, count, out) -> None on the GPU: [coherent multi-crossing P ->] quadrature, or
-    the ODE fallback (lzq_ode_batch) for sweeps over sigma_v / Gamma_wash / depletion."""
+    the ODE fallback (lzq_ode_batch) for sweeps over sigma_v / Gamma_wash / depletion (with or
+    without crossings)."""
     if is_ode_spec(spec):
-        if spec.crossings is not None:
-            raise NotImplementedError("multi-crossing profiles with the ODE fallback")
 
         def compute_ode(s, n, out):
             import torch
             pts, ods = grid_records(spec, s, n, engine)
+            if spec.crossings is not None:   # coherent multi-crossing P (propagator) for every point
+                pts["P_chi_to_B"] = coherent_P(spec, s, n, engine).cpu().numpy()
             # fpy:372 per point: points with no sink/depletion take the quadrature, the rest the ODE
             ode = (ods["sigma_v_chi_GeV_m2"] != 0.0) | (ods["Gamma_wash_over_H"] != 0.0) | \
                   (ods["deplete_DM_from_source"] != 0)
@@ -421,13 +431,7 @@ def make_compute(spec: SweepSpec, engine) -> ComputeFn:
         return compute_ode
 
     def compute(s, n, out):
-        P_points = None
-        if spec.crossings is not None:
-            m, dp, xi, v_w = spec.crossing_arrays(s, n, engine.device)
-            if not bool((v_w == v_w[0]).all()):
-                raise NotImplementedError("multi-crossing sweeps need a single v_w")
-            P_points = engine.lz_propagate(m, dp, xi, float(v_w[0]), spec.crossings.window_lz,
-                                           spec.crossings.steps)
+        P_points = coherent_P(spec, s, n, engine) if spec.crossings is not None else None
         engine.sweep(spec.base, spec.axes, s, n, n_y=spec.n_y, out=out, P_points=P_points)
     return compute
 

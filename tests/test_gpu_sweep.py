@@ -116,3 +116,31 @@ def test_sweep_cli_end_to_end(tmp_path, gpu_engine):
     # resuming another spec into the same directory is refused, not mixed
     with pytest.raises(RuntimeError, match="another sweep"):
         sw.main(["--spec", "C3", "--limit", "2048", "--chunk", "700", "--out", str(out), "--resume"])
+
+
+def test_multicrossing_with_ode_fallback(gpu_engine):
+    """A multi-crossing sweep (C5-style crossings) over Gamma_wash: every point's P is the
+    coherent propagator output, and the points route per fpy:372 -- Gamma_wash = 0 to the
+    quadrature, > 0 to the ODE fallback -- bit-identical to calling those directly."""
+    import dataclasses
+
+    import torch
+    sw = pkg("sweep")
+    c5 = sw.builtin_specs()["C5"]
+    spec = dataclasses.replace(c5, name="C5_ode", base={**c5.base, "T_max_over_Tp": 1.6, "T_min_over_Tp": 0.6},
+                               axes=[("m_mix", np.logspace(-3, 0, 6)), ("dprime", np.logspace(-3, 1, 5)),
+                                     ("Gamma_wash_over_H", np.array([0.0, 0.5]))])
+    assert sw.is_ode_spec(spec)
+    n = spec.total
+    out = torch.empty((n, 6), dtype=torch.float64, device=gpu_engine.device)
+    sw.make_compute(spec, gpu_engine)(0, n, out)
+    P = sw.coherent_P(spec, 0, n, gpu_engine).cpu().numpy()
+    pts, ods = sw.grid_records(spec, 0, n, gpu_engine)
+    pts["P_chi_to_B"] = P
+    ode = ods["Gamma_wash_over_H"] != 0.0
+    want = torch.empty_like(out)
+    want[torch.as_tensor(np.nonzero(ode)[0], device=out.device)] = gpu_engine.ode(pts[ode], ods[ode])[0]
+    want[torch.as_tensor(np.nonzero(~ode)[0], device=out.device)] = gpu_engine.yields(pts[~ode], n_y=spec.n_y)
+    assert torch.equal(out, want)
+    t = out.cpu().numpy()
+    assert np.isfinite(t).all() and np.array_equal(t[:, 5], P)

@@ -38,6 +38,7 @@ PKG = "baryon-and-dark-matter-densities-from-bounce--sourced-distributed-landau-
 METRIC = "LZ param points/sec (node) at 1/2/4/8 MI355X; % FP64 VALU peak"
 FLOP_PER_POINT = 30.0 * 8000 * 1200   # 30 FLOP per (y, z) node
 PEAK_FP64_TFLOPS = 78.6               # MI355X FP64 vector: 256 CU x 2.4 GHz x 128 FLOP/clk
+HBM_PEAK_BPS = 8.0e12                 # MI355X HBM3E (MI355X_MICROARCH.md)
 BASE = {  # /root/reference/yields_config_equal_mass.json
     "regime": "nonthermal", "m_chi_GeV": 0.95, "g_chi": 2, "chi_stats": "fermion",
     "sigma_v_chi_GeV_m2": 0.0, "T_p_GeV": 100.0, "beta_over_H": 100.0, "v_w": 0.30, "I_p": 0.34,
@@ -93,6 +94,10 @@ def roofline(points_per_launch: int, kern_ms: float) -> dict:
         "achieved": achieved, "frac": achieved / PEAK_FP64_TFLOPS,
         "flop_per_point_executed": flop_pt,
         "traffic": d["hbm_bytes_per_point"]["total_upper"] * points_per_launch, "traffic_unit": "bytes/launch",
+        # north_star: "achieved HBM GB/s for the grid I/O" -- the path is FP64-bound, so this is small
+        "grid_io": {"GB_per_s": d["hbm_bytes_per_point"]["total_upper"] * points_per_launch / (kern_ms / 1e3) / 1e9,
+                    "frac_of_hbm_peak": d["hbm_bytes_per_point"]["total_upper"] * points_per_launch /
+                    (kern_ms / 1e3) / HBM_PEAK_BPS, "hbm_peak_TB_per_s": HBM_PEAK_BPS / 1e12},
         "issue": {"valu_insts_per_wave_node": d["valu_insts_per_wave_node"], "fp64_insts_per_wave_node": fp64_wn,
                   "simd_cycles_per_wave_node": cyc_wn, "clock_ghz": ghz,
                   "fp64_pipe_busy_frac": 4.0 * fp64_wn / cyc_wn,

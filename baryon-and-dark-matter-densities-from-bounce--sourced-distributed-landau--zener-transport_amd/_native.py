@@ -67,7 +67,8 @@ ABI_VERSION = 1  # LZQ_ABI_VERSION (tests/test_capi.py checks it against the lib
 
 # Symbols declared in include/lzq.h (checked by tests/test_capi.py against the header).
 EXPORTS = ("lzq_abi_version", "lzq_last_error", "lzq_init", "lzq_ztables", "lzq_tune", "lzq_aov_batch",
-           "lzq_jchi_batch", "lzq_yields_batch", "lzq_sweep_grid", "lzq_p_closed_form",
+           "lzq_jchi_batch", "lzq_yields_batch", "lzq_sweep_grid", "lzq_sweep_grid_reuse_workspace",
+           "lzq_sweep_grid_reuse", "lzq_p_closed_form",
            "lzq_lz_propagate", "lzq_ode_tables", "lzq_ode_integrate", "lzq_ode_integrate_shared", "lzq_ode_quadrature", "lzq_ode_batch",
            "lzq_ode_aov_T", "lzq_ode_rhs")
 # the lzq_point fields an ODE spline table depends on (A/V kernel fpy:141-156 + window fpy:368-369)
@@ -110,6 +111,8 @@ def load(path: str | None = None):
     L.lzq_jchi_batch.argtypes = [P(LzqPoint), vp, i64, vp, vp]
     L.lzq_yields_batch.argtypes = [vp, i64, i32, vp, vp, vp, vp, vp]
     L.lzq_sweep_grid.argtypes = [P(LzqPoint), P(LzqAxis), i32, i64, i64, i32, vp, vp, vp]
+    L.lzq_sweep_grid_reuse_workspace.argtypes = [P(LzqAxis), i32, i32]
+    L.lzq_sweep_grid_reuse.argtypes = [P(LzqPoint), P(LzqAxis), i32, i64, i64, i32, vp, vp, i64, vp, vp]
     L.lzq_p_closed_form.argtypes = [vp, i64, vp, vp]
     L.lzq_lz_propagate.argtypes = [vp, vp, vp, i64, i32, d, d, i32, vp, vp]
     L.lzq_ode_tables.argtypes = [vp, i64, vp, vp, vp, i64, vp, vp]
@@ -122,6 +125,7 @@ def load(path: str | None = None):
     for name in EXPORTS:
         if name not in ("lzq_abi_version", "lzq_last_error"):
             getattr(L, name).restype = ctypes.c_int
+    L.lzq_sweep_grid_reuse_workspace.restype = ctypes.c_int64
     if path is None:
         _lib = L
     return L

@@ -498,8 +498,17 @@ __device__ __forceinline__ int lane_id() {
 //   * y, e^y and the weight are re-formed after the z-loop (same operations, same bits);
 //   * the lane's running sum over its y-nodes sits in the slot (LZQ_ACC_LDS).
 // Without this the kernel spilled ~200 B/lane to scratch around every z-loop.
-template <int YB, int EXPV, typename Slot>
-__device__ double yb_wave(Slot* slots, int w, const ZNode* __restrict__ zt, const double* tab, int truncate) {
+// MODE (see lzq_sweep_grid_reuse): kYbDense computes every F(y_j) = sum_k omega_k 2^(c2_j g_k)
+// itself (the headline); kYbTable computes them the same way and stores them to Fout instead of
+// integrating; kYbReuse reads them from Fin (a table written by kYbTable for a point with the
+// same y-grid and A/V kernel) and integrates.  The F values and the integration are the same
+// operations in the same lane order in every mode, so Y_B is bit-identical.
+enum YbMode { kYbDense = 0, kYbReuse = 1, kYbTable = 2 };
+
+template <int YB, int EXPV, int MODE = kYbDense, typename Slot>
+__device__ double yb_wave(Slot* slots, int w, const ZNode* __restrict__ zt, const double* tab, int truncate,
+                          const double* __restrict__ Fin = nullptr, double* __restrict__ Fout = nullptr) {
+  static_assert(MODE == kYbDense || !LZQ_YFACT_EARLY, "table modes re-form the y-factors after the z-loop");
   if (slots[w].s.empty) return 0.0;
   // y-node counts are int32 (n_y of the C ABI): 32-bit loop bounds save the SGPRs that
   // would otherwise spill around the z-loop
@@ -511,36 +520,52 @@ __device__ double yb_wave(Slot* slots, int w, const ZNode* __restrict__ zt, cons
   double acc = 0.0;
 #endif
   for (int base = 0; base < n; base += per_pass) {
-    const int lane = lane_id();
-    int wo = w;
-    asm volatile("" : "+s"(wo));
-    const QuadSetup& s = slots[wo].s;
-    double c2[YB];
     // only y, e^y and the weight stay live across the z-loop (LZQ_YFACT_EARLY=1: the 7
     // y-factors instead); the y-factors are formed after it
     double yv[YB], ey[YB], wt[YB];
 #if LZQ_YFACT_EARLY
     YFactors fy[YB];
 #endif
-#pragma unroll
-    for (int b = 0; b < YB; ++b) {
-      const int j = base + b * kWaveSize + lane;
-      const int jj = j < n ? j : n - 1;  // tail lanes recompute the last node with weight 0
-      yv[b] = y_node(s, jj);
-      ey[b] = exp_sc(pymax(pymin(yv[b], 50.0), -50.0));                          // fpy:161
-      c2[b] = ((s.cneg * ey[b]) * kLog2E) * c2_scale<EXPV>();                 // fpy:163 c, log2 units
-      wt[b] = j < n ? y_weight(s, jj, yv[b]) : 0.0;
-#if LZQ_YFACT_EARLY
-      fy[b] = y_factors(s, yv[b], ey[b], wt[b]);
-#endif
-    }
     double F[YB];
-    zsum_dispatch<YB, EXPV>(zt, tab, c2, F, truncate);
+    if constexpr (MODE == kYbReuse) {
+      const int lane = lane_id();
+#pragma unroll
+      for (int b = 0; b < YB; ++b) {
+        const int j = base + b * kWaveSize + lane;
+        F[b] = Fin[j < n ? j : n - 1];
+      }
+    } else {
+      const int lane = lane_id();
+      int wo = w;
+      asm volatile("" : "+s"(wo));
+      const QuadSetup& s = slots[wo].s;
+      double c2[YB];
+#pragma unroll
+      for (int b = 0; b < YB; ++b) {
+        const int j = base + b * kWaveSize + lane;
+        const int jj = j < n ? j : n - 1;  // tail lanes recompute the last node with weight 0
+        yv[b] = y_node(s, jj);
+        ey[b] = exp_sc(pymax(pymin(yv[b], 50.0), -50.0));                          // fpy:161
+        c2[b] = ((s.cneg * ey[b]) * kLog2E) * c2_scale<EXPV>();                 // fpy:163 c, log2 units
+        wt[b] = j < n ? y_weight(s, jj, yv[b]) : 0.0;
+#if LZQ_YFACT_EARLY
+        fy[b] = y_factors(s, yv[b], ey[b], wt[b]);
+#endif
+      }
+      zsum_dispatch<YB, EXPV>(zt, tab, c2, F, truncate);
+      if constexpr (MODE == kYbTable) {
+#pragma unroll
+        for (int b = 0; b < YB; ++b) {
+          const int j = base + b * kWaveSize + lane;
+          if (j < n) Fout[j] = F[b];
+        }
+        continue;
+      }
+    }
     int wr = w;
     asm volatile("" : "+s"(wr));
     const int lane2 = lane_id();
-#if LZQ_Y_RECOMPUTE && !LZQ_YFACT_EARLY
-    {
+    if (MODE == kYbReuse || (LZQ_Y_RECOMPUTE && !LZQ_YFACT_EARLY)) {
       const QuadSetup& sr = slots[wr].s;
 #pragma unroll
       for (int b = 0; b < YB; ++b) {
@@ -551,7 +576,6 @@ __device__ double yb_wave(Slot* slots, int w, const ZNode* __restrict__ zt, cons
         wt[b] = j < n ? y_weight(sr, jj, yv[b]) : 0.0;
       }
     }
-#endif
 #if LZQ_ACC_LDS
     double acc = slots[wr].acc[lane2];
 #endif
@@ -655,6 +679,7 @@ struct GridSpec {
   int64_t n[LZQ_MAX_AXES];
   int64_t stride[LZQ_MAX_AXES];
   const double* values[LZQ_MAX_AXES];
+  int64_t tstride[LZQ_MAX_AXES];  // lzq_sweep_grid_reuse: stride in the z-sum table index (0: axis not in it)
 };
 
 __device__ __forceinline__ void set_field(lzq_point& p, int32_t f, double v, double& delta, double& m_mix,
@@ -765,6 +790,84 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void yields_grid_kernel(lzq_
          epilogue_pre(pt, P), lane);
   }
   point_yields<YB, EXPV>(slots, w, zt, tab, lane, truncate, out + local);
+}
+
+// ---------------------------------------------------------------------------------------
+// lzq_sweep_grid_reuse: the z-sums F(y_j) depend on a grid point only through the fields of
+// quad_setup's y-grid and c (I_p, beta/H, T_p, T_min/T_p, T_max/T_p, n_y).  The table kernel
+// computes them once per combination of the grid's values of those fields (one wavefront per
+// table, kYbTable: the dense kernel's passes, F stored instead of integrated); the reuse kernel
+// then integrates every point from its table (kYbReuse).  Same operations, same lane order: Y_B
+// is bit-identical to lzq_sweep_grid.  Table t: kTabHdr header doubles (the y-grid and c of the
+// QuadSetup it was made for; a point whose own setup differs gets NaN yields, never a wrong
+// table), then its F values.
+constexpr int kTabHdr = 4;
+
+__device__ __forceinline__ int64_t table_of(const GridSpec& g, int64_t idx) {
+  int64_t t = 0;
+  for (int a = 0; a < g.n_axes; ++a) t += ((idx / g.stride[a]) % g.n[a]) * g.tstride[a];
+  return t;
+}
+
+// flat grid index of table t's representative (every other axis at its first value)
+__device__ __forceinline__ int64_t table_rep(const GridSpec& g, int64_t t) {
+  int64_t idx = 0;
+  for (int a = 0; a < g.n_axes; ++a)
+    if (g.tstride[a]) idx += ((t / g.tstride[a]) % g.n[a]) * g.stride[a];
+  return idx;
+}
+
+template <int EXPV>
+__global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void grid_ztable_kernel(lzq_point base, GridSpec grid,
+                                                                          int64_t n_tab, int32_t n_y, int64_t tstride,
+                                                                          const ZNode* __restrict__ zt,
+                                                                          const double* __restrict__ gtab,
+                                                                          double* __restrict__ Fw, int truncate) {
+  __shared__ double lds_tab[kTabN];
+  const double* tab = stage_table<EXPV>(gtab, lds_tab);
+  __shared__ WaveSlot slots[kWavesPerBlock];
+  const int lane = threadIdx.x & (kWaveSize - 1);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t t = (int64_t)blockIdx.x * kWavesPerBlock + w;
+  if (t >= n_tab) return;
+  lzq_point pt;
+  const double P = grid_point(base, grid, table_rep(grid, t), pt);
+  const QuadSetup qs = quad_setup(pt, P, pt.T_min_over_Tp * pt.T_p_GeV, pt.T_max_over_Tp * pt.T_p_GeV, n_y);
+  double* F = Fw + t * tstride;
+  if (lane == 0) {
+    F[0] = qs.y_lo;
+    F[1] = qs.y_hi;
+    F[2] = (double)qs.n;
+    F[3] = qs.cneg;
+  }
+  park(slots[w], qs, epilogue_pre(pt, P), lane);
+  yb_wave<kYB, EXPV, kYbTable>(slots, w, zt, tab, truncate, nullptr, F + kTabHdr);
+}
+
+__global__ __launch_bounds__(kBlock) void grid_reuse_kernel(lzq_point base, GridSpec grid, int64_t start,
+                                                           int64_t count, int32_t n_y,
+                                                           const double* __restrict__ Pov,
+                                                           const double* __restrict__ Fw, int64_t tstride,
+                                                           lzq_yield* __restrict__ out) {
+  __shared__ WaveSlot slots[kWavesPerBlock];
+  const int lane = threadIdx.x & (kWaveSize - 1);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t local = (int64_t)blockIdx.x * kWavesPerBlock + w;
+  if (local >= count) return;
+  lzq_point pt;
+  const double Pg = grid_point(base, grid, start + local, pt);
+  const double P = Pov ? Pov[local] : Pg;
+  const QuadSetup qs = quad_setup(pt, P, pt.T_min_over_Tp * pt.T_p_GeV, pt.T_max_over_Tp * pt.T_p_GeV, n_y);
+  const double* F = Fw + table_of(grid, start + local) * tstride;
+  const bool match = qs.empty || (F[0] == qs.y_lo && F[1] == qs.y_hi && F[2] == (double)qs.n && F[3] == qs.cneg);
+  park(slots[w], qs, epilogue_pre(pt, P), lane);
+  // (match is wave-uniform: every lane formed the same setup)
+  const double Y_B = match ? yb_wave<kYB, kExpTable, kYbReuse>(slots, w, nullptr, nullptr, 0, F + kTabHdr) : 0.0;
+  if (lane == 0) {
+    lzq_yield o = epilogue_finish(slots[w].e, Y_B);
+    if (!match) o.Y_B = o.rho_B_kg_m3 = o.DM_over_B = __builtin_nan("");
+    out[local] = o;
+  }
 }
 
 // fpy:158-165, one lane per y value
@@ -1057,12 +1160,13 @@ int lzq_yields_batch(const lzq_point* d_points, int64_t n, int32_t n_y, const do
   return LZQ_OK;
 }
 
-int lzq_sweep_grid(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int64_t start, int64_t count,
-                   int32_t n_y, const double* d_P, lzq_yield* d_out, void* stream) {
+namespace {
+// lzq_sweep_grid's argument checks and GridSpec (shared with lzq_sweep_grid_reuse)
+int make_grid(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int64_t start, int64_t count,
+              const lzq_yield* d_out, const char* who, lzq::GridSpec& g) {
   if (!base || n_axes < 0 || n_axes > LZQ_MAX_AXES || (n_axes > 0 && !axes) || start < 0 || count < 0 ||
       (count > 0 && !d_out))
-    return fail(LZQ_EINVAL, "lzq_sweep_grid: bad arguments");
-  lzq::GridSpec g;
+    return fail(LZQ_EINVAL, "%s: bad arguments", who);
   memset(&g, 0, sizeof(g));
   g.n_axes = n_axes;
   int64_t total = 1;
@@ -1070,25 +1174,48 @@ int lzq_sweep_grid(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, 
   for (int a = n_axes - 1; a >= 0; --a) {
     const int32_t f = axes[a].field;
     if (!((f >= 0 && f <= 14) || f == LZQ_F_DELTA_LZ || f == LZQ_F_M_MIX || f == LZQ_F_DPRIME))
-      return fail(LZQ_EINVAL, "lzq_sweep_grid: axis %d has unknown field %d", a, f);
-    if (axes[a].n <= 0 || !axes[a].values) return fail(LZQ_EINVAL, "lzq_sweep_grid: axis %d is empty", a);
+      return fail(LZQ_EINVAL, "%s: axis %d has unknown field %d", who, a, f);
+    if (axes[a].n <= 0 || !axes[a].values) return fail(LZQ_EINVAL, "%s: axis %d is empty", who, a);
     mix |= f == LZQ_F_M_MIX;
     dpr |= f == LZQ_F_DPRIME;
     g.field[a] = f;
     g.n[a] = axes[a].n;
     g.values[a] = axes[a].values;
     g.stride[a] = total;
-    if (total > INT64_MAX / axes[a].n) return fail(LZQ_EINVAL, "lzq_sweep_grid: grid too large");
+    if (total > INT64_MAX / axes[a].n) return fail(LZQ_EINVAL, "%s: grid too large", who);
     total *= axes[a].n;
   }
-  if (mix != dpr) return fail(LZQ_EINVAL, "lzq_sweep_grid: LZQ_F_M_MIX and LZQ_F_DPRIME must be swept together");
+  if (mix != dpr) return fail(LZQ_EINVAL, "%s: LZQ_F_M_MIX and LZQ_F_DPRIME must be swept together", who);
   if (start > total || count > total - start)
-    return fail(LZQ_EINVAL, "lzq_sweep_grid: range [%lld, %lld) outside grid of %lld points", (long long)start,
+    return fail(LZQ_EINVAL, "%s: range [%lld, %lld) outside grid of %lld points", who, (long long)start,
                 (long long)(start + count), (long long)total);
   if (base->regime != LZQ_THERMAL && base->regime != LZQ_NONTHERMAL)
-    return fail(LZQ_EUNSUPPORTED, "lzq_sweep_grid: regime must be thermal or nonthermal (fpy:376-384)");
+    return fail(LZQ_EUNSUPPORTED, "%s: regime must be thermal or nonthermal (fpy:376-384)", who);
+  return LZQ_OK;
+}
+
+// the fields quad_setup's y-grid and c depend on (lzq_sweep_grid_reuse's table axes)
+bool ztable_field(int32_t f) {
+  return f == LZQ_F_I_P || f == LZQ_F_BETA_OVER_H || f == LZQ_F_T_P || f == LZQ_F_T_MIN_OVER_TP ||
+         f == LZQ_F_T_MAX_OVER_TP;
+}
+
+int64_t ztable_count(const lzq::GridSpec& g) {
+  int64_t n = 1;
+  for (int a = 0; a < g.n_axes; ++a)
+    if (ztable_field(g.field[a])) n *= g.n[a];
+  return n;
+}
+}  // namespace
+
+int lzq_sweep_grid(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int64_t start, int64_t count,
+                   int32_t n_y, const double* d_P, lzq_yield* d_out, void* stream) {
+  lzq::GridSpec g;
+  int rc = make_grid(base, axes, n_axes, start, count, d_out, "lzq_sweep_grid", g);
+  if (rc) return rc;
   if (count == 0) return LZQ_OK;
-  int dev, rc = ensure_device(&dev);
+  int dev;
+  rc = ensure_device(&dev);
   if (rc) return rc;
   int64_t nb = blocks_for(count, lzq::kWavesPerBlock);
   if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_sweep_grid: count too large for one launch");
@@ -1100,6 +1227,60 @@ int lzq_sweep_grid(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, 
     hipLaunchKernelGGL((lzq::yields_grid_kernel<lzq::kYB, lzq::kExpPoly11>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
                        (hipStream_t)stream, *base, g, start, count, n_y, d_P, g_dev_tab[dev], exp_table(dev), d_out,
                        g_truncate);
+  LZQ_HIP(hipGetLastError());
+  return LZQ_OK;
+}
+
+int64_t lzq_sweep_grid_reuse_workspace(const lzq_axis* axes, int32_t n_axes, int32_t n_y) {
+  if (n_axes < 0 || n_axes > LZQ_MAX_AXES || (n_axes > 0 && !axes)) return fail(LZQ_EINVAL, "lzq_sweep_grid_reuse_workspace: bad arguments");
+  int64_t n = 1;
+  for (int a = 0; a < n_axes; ++a) {
+    if (axes[a].n <= 0) return fail(LZQ_EINVAL, "lzq_sweep_grid_reuse_workspace: axis %d is empty", a);
+    if (ztable_field(axes[a].field)) {
+      if (n > INT64_MAX / 16 / axes[a].n) return fail(LZQ_EINVAL, "lzq_sweep_grid_reuse_workspace: too many tables");
+      n *= axes[a].n;
+    }
+  }
+  const int64_t ny = n_y > LZQ_NY_MIN ? n_y : LZQ_NY_MIN;
+  if (n > INT64_MAX / (ny + lzq::kTabHdr)) return fail(LZQ_EINVAL, "lzq_sweep_grid_reuse_workspace: too many tables");
+  return n * (ny + lzq::kTabHdr);
+}
+
+int lzq_sweep_grid_reuse(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int64_t start, int64_t count,
+                         int32_t n_y, const double* d_P, double* d_work, int64_t work_doubles, lzq_yield* d_out,
+                         void* stream) {
+  lzq::GridSpec g;
+  int rc = make_grid(base, axes, n_axes, start, count, d_out, "lzq_sweep_grid_reuse", g);
+  if (rc) return rc;
+  const int64_t need = lzq_sweep_grid_reuse_workspace(axes, n_axes, n_y);
+  if (need < 0) return (int)need;
+  if (count > 0 && (!d_work || work_doubles < need))
+    return fail(LZQ_EINVAL, "lzq_sweep_grid_reuse: workspace of %lld doubles < %lld needed", (long long)work_doubles,
+                (long long)need);
+  if (count == 0) return LZQ_OK;
+  int dev;
+  rc = ensure_device(&dev);
+  if (rc) return rc;
+  const int64_t n_tab = ztable_count(g);
+  int64_t ts = 1;
+  for (int a = g.n_axes - 1; a >= 0; --a)
+    if (ztable_field(g.field[a])) {
+      g.tstride[a] = ts;
+      ts *= g.n[a];
+    }
+  const int64_t stride = (n_y > LZQ_NY_MIN ? n_y : LZQ_NY_MIN) + lzq::kTabHdr;
+  const int64_t nbt = blocks_for(n_tab, lzq::kWavesPerBlock), nb = blocks_for(count, lzq::kWavesPerBlock);
+  if (nbt > kMaxGrid || nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_sweep_grid_reuse: too large for one launch");
+  // the tables always use the exact-underflow truncation: bit-identical to the dense sums
+  if (g_exp_variant == lzq::kExpTable)
+    hipLaunchKernelGGL((lzq::grid_ztable_kernel<lzq::kExpTable>), dim3((unsigned)nbt), dim3(lzq::kBlock), 0,
+                       (hipStream_t)stream, *base, g, n_tab, n_y, stride, g_dev_tab[dev], exp_table(dev), d_work, 1);
+  else
+    hipLaunchKernelGGL((lzq::grid_ztable_kernel<lzq::kExpPoly11>), dim3((unsigned)nbt), dim3(lzq::kBlock), 0,
+                       (hipStream_t)stream, *base, g, n_tab, n_y, stride, g_dev_tab[dev], exp_table(dev), d_work, 1);
+  LZQ_HIP(hipGetLastError());
+  hipLaunchKernelGGL(lzq::grid_reuse_kernel, dim3((unsigned)nb), dim3(lzq::kBlock), 0, (hipStream_t)stream, *base, g,
+                     start, count, n_y, d_P, d_work, stride, d_out);
   LZQ_HIP(hipGetLastError());
   return LZQ_OK;
 }

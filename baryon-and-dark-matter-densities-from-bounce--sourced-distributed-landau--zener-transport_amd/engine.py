@@ -30,6 +30,7 @@ class Engine:
                                "there is no CPU fallback")
         self.lib = _native.load(lib_path)
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        self._zwork = None  # lzq_sweep_grid_reuse's z-sum tables (grown on demand)
         with torch.cuda.device(self.device):
             self._check(self.lib.lzq_init(self.device.index))
 
@@ -110,10 +111,13 @@ class Engine:
     # -- grid sweep ----------------------------------------------------------------------------
     def sweep(self, base_cfg, axes: Sequence[tuple], start: int, count: int, n_y: int = 8000,
               out: Optional[torch.Tensor] = None, P: Optional[float] = None,
-              P_points: Optional[torch.Tensor] = None) -> torch.Tensor:
+              P_points: Optional[torch.Tensor] = None, reuse: bool = False) -> torch.Tensor:
         """axes: sequence of (field_name, values) (C order, last fastest); field names are
         the lzq_point double fields or 'delta_LZ' / 'm_mix' / 'dprime'.  P_points: optional
-        per-point P override ([count], device), e.g. from lz_propagate (config C5)."""
+        per-point P override ([count], device), e.g. from lz_propagate (config C5).
+        reuse: lzq_sweep_grid_reuse -- the z-sums computed once per combination of the grid's
+        I_p / beta_over_H / T_p_GeV / T_min_over_Tp / T_max_over_Tp values and shared by the
+        points (bit-identical results; NOT the dense headline path)."""
         if len(axes) > _native.LZQ_MAX_AXES:
             raise ValueError(f"at most {_native.LZQ_MAX_AXES} sweep axes")
         dev_vals = [self._f64(v).reshape(-1) for _, v in axes]
@@ -131,8 +135,18 @@ class Engine:
             Pp = None if P_points is None else self._f64(P_points).reshape(-1)
             if Pp is not None and Pp.numel() != count:
                 raise ValueError("P_points must have `count` entries")
-            self._check(self.lib.lzq_sweep_grid(ctypes.byref(base), arr, len(axes), int(start), int(count),
-                                                  int(n_y), _vp(Pp), _vp(out), self._stream()))
+            if reuse:
+                need = self.lib.lzq_sweep_grid_reuse_workspace(arr, len(axes), int(n_y))
+                if need < 0:
+                    self._check(int(need))
+                if self._zwork is None or self._zwork.numel() < need:
+                    self._zwork = torch.empty(max(int(need), 1), dtype=torch.float64, device=self.device)
+                self._check(self.lib.lzq_sweep_grid_reuse(ctypes.byref(base), arr, len(axes), int(start), int(count),
+                                                          int(n_y), _vp(Pp), _vp(self._zwork), self._zwork.numel(),
+                                                          _vp(out), self._stream()))
+            else:
+                self._check(self.lib.lzq_sweep_grid(ctypes.byref(base), arr, len(axes), int(start), int(count),
+                                                      int(n_y), _vp(Pp), _vp(out), self._stream()))
         self._keepalive = dev_vals  # axis buffers must outlive the async launch
         return out
 

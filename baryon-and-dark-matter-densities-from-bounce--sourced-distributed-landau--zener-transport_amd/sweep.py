@@ -382,7 +382,7 @@ def summarize(table: np.ndarray, spec: SweepSpec, elapsed: Optional[float] = Non
 
 
 def run_sweep(spec: SweepSpec, engine=None, rank: int = 0, world: int = 1, chunk: int = 1 << 20,
-              out_dir: Optional[str] = None, resume: bool = False, group=None, log=print):
+              out_dir: Optional[str] = None, resume: bool = False, group=None, log=print, reuse: bool = False):
     """Evaluate `spec` on this rank's shard, all-gather, return the full table (torch, on
     the engine's device)."""
     import torch
@@ -392,7 +392,7 @@ def run_sweep(spec: SweepSpec, engine=None, rank: int = 0, world: int = 1, chunk
     start, end = shard_range(spec.total, rank, world)
     key = prepare_out_dir(out_dir, spec, resume, rank) if out_dir else ""
 
-    local = run_local(make_compute(spec, engine), start, end,
+    local = run_local(make_compute(spec, engine, reuse=reuse), start, end,
                       lambda n: torch.empty((n, 6), dtype=torch.float64, device=engine.device), chunk,
                       out_dir, resume, sync=torch.cuda.synchronize, log=log, key=key)
     return gather_table(local, spec.total, rank, world, group)
@@ -407,10 +407,11 @@ def coherent_P(spec: SweepSpec, s: int, n: int, engine):
     return engine.lz_propagate(m, dp, xi, float(v_w[0]), spec.crossings.window_lz, spec.crossings.steps)
 
 
-def make_compute(spec: SweepSpec, engine) -> ComputeFn:
+def make_compute(spec: SweepSpec, engine, reuse: bool = False) -> ComputeFn:
     """(start, count, out) -> None on the GPU: [coherent multi-crossing P ->] quadrature, or
     the ODE fallback (lzq_ode_batch) for sweeps over sigma_v / Gamma_wash / depletion (with or
-    without crossings)."""
+    without crossings).  reuse: the quadrature's z-sums shared across points with the same
+    y-grid and A/V kernel (lzq_sweep_grid_reuse; bit-identical, not the dense headline path)."""
     if is_ode_spec(spec):
 
         def compute_ode(s, n, out):
@@ -432,7 +433,7 @@ def make_compute(spec: SweepSpec, engine) -> ComputeFn:
 
     def compute(s, n, out):
         P_points = coherent_P(spec, s, n, engine) if spec.crossings is not None else None
-        engine.sweep(spec.base, spec.axes, s, n, n_y=spec.n_y, out=out, P_points=P_points)
+        engine.sweep(spec.base, spec.axes, s, n, n_y=spec.n_y, out=out, P_points=P_points, reuse=reuse)
     return compute
 
 
@@ -445,6 +446,9 @@ def main(argv=None):
     ap.add_argument("--resume", action="store_true")
     ap.add_argument("--chunk", type=int, default=1 << 20)
     ap.add_argument("--limit", type=int, default=None, help="evaluate only the first N grid points")
+    ap.add_argument("--reuse-zsums", action="store_true",
+                    help="share the quadrature's z-sums between points with the same y-grid and A/V kernel "
+                         "(lzq_sweep_grid_reuse: bit-identical, much faster; not the dense headline mode)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI, default) | gloo (rehearsal: several ranks on one GPU)")
     args = ap.parse_args(argv)
@@ -474,7 +478,7 @@ def main(argv=None):
     start, end = shard_range(spec_total, rank, world)
     key = prepare_out_dir(args.out, spec, args.resume, rank) if args.out else ""
 
-    local = run_local(make_compute(spec, eng), start, end,
+    local = run_local(make_compute(spec, eng, reuse=args.reuse_zsums), start, end,
                       lambda n: torch.empty((n, 6), dtype=torch.float64, device=eng.device), args.chunk,
                       args.out, args.resume, sync=torch.cuda.synchronize,
                       log=(print if rank == 0 else (lambda s: None)), key=key)

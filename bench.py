@@ -206,6 +206,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--truncated", action="store_true",
                     help="also time one step with exact-underflow truncation (secondary field, not the headline)")
+    ap.add_argument("--reuse", action="store_true",
+                    help="also time one step with the z-sums shared between points (lzq_sweep_grid_reuse; "
+                         "secondary field, not the headline: SURVEY §8d keeps the headline dense)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI, default) | gloo (rehearsal of the N>1 path on one GPU)")
@@ -298,6 +301,27 @@ def main():
                  "note": "exact-underflow truncation (include/lzq.h LZQ_TUNE_TRUNCATE): nodes whose "
                          "terms are < 2^-1080 are skipped; one step, not the headline"}
 
+    # Secondary (NOT the headline): the z-sums computed once per y-grid / A/V kernel and shared
+    # by the points (lzq_sweep_grid_reuse); the table must be bit-identical to the dense one.
+    reuse = None
+    if args.reuse:
+        dense_tab = local_tab.clone()
+        eng.sweep(BASE, axes, start, per, out=local_tab, reuse=True)   # warm-up (table workspace)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        eng.sweep(BASE, axes, start, per, out=local_tab, reuse=True)
+        torch.cuda.synchronize()
+        t_re = time.perf_counter() - t1
+        same = bool(torch.equal(dense_tab, local_tab))
+        if use_dist:
+            t = torch.tensor([t_re, 0.0 if same else 1.0], dtype=torch.float64,
+                             device=eng.device if args.dist_backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            t_re, same = float(t[0]), float(t[1]) == 0.0
+        reuse = {"value": total / t_re, "unit": "points/s", "bit_identical_to_dense": same,
+                 "note": "z-sums shared by the points of one y-grid / A/V kernel (include/lzq.h "
+                         "lzq_sweep_grid_reuse; the C2 grid has one); one step, not the headline"}
+
     # sanity: every shard of the gathered table is finite and the gather put rank r's rows at
     # [r*per, (r+1)*per)
     assert bool(torch.isfinite(gathered).all()), "non-finite yields"
@@ -328,6 +352,8 @@ def main():
         }
         if trunc is not None:
             rec["truncated"] = trunc
+        if reuse is not None:
+            rec["reuse_zsums"] = reuse
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(axes, grid_total, args.cpu_seconds)
         print(json.dumps(rec), flush=True)

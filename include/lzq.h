@@ -156,6 +156,20 @@ int lzq_sweep_grid(const lzq_point* base, const lzq_axis* axes, int32_t n_axes,
                    int64_t start, int64_t count, int32_t n_y, const double* d_P,
                    lzq_yield* d_out, void* stream);
 
+/* lzq_sweep_grid with the z-sums shared -- a separate mode, NOT the dense headline path
+ * (SURVEY §8d allows separable reuse only as such).  The z-sums F(y_j) = sum_k omega_k
+ * exp(c(y_j) gamma4_k) of fpy:160-165 depend on a point only through I_p, beta_over_H, T_p_GeV,
+ * T_min_over_Tp, T_max_over_Tp (its y-grid and c, fpy:141-156, 234-247) and n_y: they are
+ * computed once per combination of the grid's values of those fields (each table = the dense
+ * kernel's passes for the combination's first grid point, into d_work), then every point of
+ * [start, start+count) is integrated from its table.  Yields are bit-identical to
+ * lzq_sweep_grid (same operations, same lane order).  d_work: >= lzq_sweep_grid_reuse_workspace
+ * doubles (tables x (max(n_y, LZQ_NY_MIN) + 4)); a negative return is an error code. */
+int64_t lzq_sweep_grid_reuse_workspace(const lzq_axis* axes, int32_t n_axes, int32_t n_y);
+int lzq_sweep_grid_reuse(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int64_t start, int64_t count,
+                         int32_t n_y, const double* d_P, double* d_work, int64_t work_doubles, lzq_yield* d_out,
+                         void* stream);
+
 /* fpy:183-184: P[i] = clamp(1 - exp(-2 pi max(lambda[i], 0)), 0, 1) (naive 1-exp kept). */
 int lzq_p_closed_form(const double* d_lambda, int64_t n, double* d_P, void* stream);
 

@@ -123,3 +123,33 @@ def test_tune_ode_coop_knob():
     assert L.lzq_tune(n.TUNE_ODE_COOP, 0) == 1
     assert L.lzq_tune(n.TUNE_ODE_COOP, 1) == 0
     assert L.lzq_tune(n.TUNE_ODE_COOP, 2) < 0 and b"ode_coop" in L.lzq_last_error()
+
+
+def test_sweep_grid_reuse_workspace_and_validation():
+    """lzq_sweep_grid_reuse_workspace: one table of max(n_y, 2000) + 4 doubles per combination of
+    the grid's I_p / beta_over_H / T_p / T_min / T_max values; lzq_sweep_grid_reuse refuses a
+    smaller workspace (no GPU work is launched on these paths)."""
+    n = pkg("_native")
+    L = n.load()
+    sw = pkg("sweep")
+    cfgm = pkg("config")
+    vals = {}
+    def axes_of(spec):
+        arr = (n.LzqAxis * len(spec.axes))()
+        for a, (name, v) in enumerate(spec.axes):
+            buf = (ctypes.c_double * len(v))(*[float(x) for x in v])
+            vals[(spec.name, a)] = buf
+            arr[a].field, arr[a].n, arr[a].values = n.FIELD[name], len(v), ctypes.cast(buf, ctypes.c_void_p).value
+        return arr
+    specs = sw.builtin_specs()
+    for name, tables in (("C2", 1), ("C3", 100), ("C4", 1000)):
+        spec = specs[name]
+        assert L.lzq_sweep_grid_reuse_workspace(axes_of(spec), len(spec.axes), 8000) == tables * 8004, name
+        assert L.lzq_sweep_grid_reuse_workspace(axes_of(spec), len(spec.axes), 100) == tables * 2004, name
+    spec = specs["C3"]
+    base = cfgm.to_ctypes_point(cfgm.to_point({**cfgm.default_config(), "P_chi_to_B": 0.1}))
+    rc = L.lzq_sweep_grid_reuse(ctypes.byref(base), axes_of(spec), len(spec.axes), 0, 10, 8000, None, 8, 100 * 8004 - 1,
+                                8, None)
+    assert rc < 0 and b"workspace" in L.lzq_last_error()
+    rc = L.lzq_sweep_grid_reuse(ctypes.byref(base), axes_of(spec), len(spec.axes), 0, 0, 8000, None, None, 0, None, None)
+    assert rc == 0   # empty range: nothing to do

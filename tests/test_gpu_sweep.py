@@ -144,3 +144,37 @@ def test_multicrossing_with_ode_fallback(gpu_engine):
     assert torch.equal(out, want)
     t = out.cpu().numpy()
     assert np.isfinite(t).all() and np.array_equal(t[:, 5], P)
+
+
+@pytest.mark.parametrize("name", ["C2", "C3", "C4"])
+def test_reuse_zsums_bit_identical(gpu_engine, name):
+    """lzq_sweep_grid_reuse (z-sums shared per y-grid + A/V kernel; not the headline mode) gives
+    the same bits as the dense lzq_sweep_grid: 3000-point slices of each config grid at two
+    offsets (C3 crosses m_chi's T = m/3 branch, C4 sweeps beta/H, I_p, v_w, sigma_y, m_chi)."""
+    import torch
+    spec = pkg("sweep").builtin_specs()[name]
+    for start in (0, spec.total // 2 - 1500):
+        dense = gpu_engine.sweep(spec.base, spec.axes, start, 3000, n_y=spec.n_y)
+        reuse = gpu_engine.sweep(spec.base, spec.axes, start, 3000, n_y=spec.n_y, reuse=True)
+        assert torch.equal(dense, reuse), (name, start)
+        assert bool(torch.isfinite(reuse).all())
+
+
+def test_reuse_zsums_table_axes_and_overrides(gpu_engine):
+    """Every field the z-sums depend on as an axis (I_p, beta/H, T_p, T_min/T_p, T_max/T_p,
+    including an empty window), fields they do not (m_chi, v_w, delta) in between, a P override,
+    and n_y below the 2000 floor: reuse == dense bit for bit."""
+    import torch
+    axes = [("T_p_GeV", np.array([10.0, 100.0])), ("m_chi_GeV", np.array([0.95, 40.0])),
+            ("T_max_over_Tp", np.array([1.6, 5.0])), ("I_p", np.array([0.1, 0.34, 0.9])),
+            ("v_w", np.array([0.2, 0.8])), ("T_min_over_Tp", np.array([0.001, 0.5, 8.0])),
+            ("beta_over_H", np.array([30.0, 300.0])), ("delta_LZ", np.array([1e-3, 0.2]))]
+    base = {**BASE_CFG, "regime": "thermal"}
+    total = int(np.prod([len(v) for _, v in axes]))
+    P = torch.rand(total, dtype=torch.float64, device=gpu_engine.device)
+    for n_y in (8000, 500):
+        dense = gpu_engine.sweep(base, axes, 0, total, n_y=n_y, P_points=P)
+        reuse = gpu_engine.sweep(base, axes, 0, total, n_y=n_y, P_points=P, reuse=True)
+        assert torch.equal(dense, reuse)
+    t = reuse.cpu().numpy()
+    assert (t[:, 0] == 0.0).any() and np.isfinite(t[:, 1]).all()   # T_min/T_p = 8: empty window, Y_B = 0

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Throughput of the BASELINE.json sweep configs C2-C5 on one GPU (subsets of C3/C4 grids;
-points/s is per-point work, which is uniform within a config).  One JSON line per config."""
+points/s is per-point work, which is uniform within a config).  One JSON line per config, with
+the dense path (the headline's) and, as a secondary field, the z-sum reuse mode
+(lzq_sweep_grid_reuse) and its bit-identity to the dense table."""
 import importlib
 import json
 import os
@@ -46,6 +48,16 @@ def main():
             torch.cuda.synchronize()
             rec["propagator_seconds"] = time.perf_counter() - t0
             rec["crossings"] = spec.crossings.__dict__
+        # secondary (not the headline): z-sums shared per y-grid / A/V kernel, bit-identical
+        comp_r = sw.make_compute(spec, eng, reuse=True)
+        out_r = torch.empty_like(out)
+        comp_r(start, min(cnt, 4096), out_r[:min(cnt, 4096)])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        comp_r(start, cnt, out_r)
+        torch.cuda.synchronize()
+        dtr = time.perf_counter() - t0
+        rec["reuse_zsums"] = {"points_per_s": cnt / dtr, "bit_identical": bool(torch.equal(out, out_r))}
         print(json.dumps(rec), flush=True)
 
 

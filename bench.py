@@ -206,9 +206,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--truncated", action="store_true",
                     help="also time one step with exact-underflow truncation (secondary field, not the headline)")
-    ap.add_argument("--reuse", action="store_true",
-                    help="also time one step with the z-sums shared between points (lzq_sweep_grid_reuse; "
-                         "secondary field, not the headline: SURVEY §8d keeps the headline dense)")
+    ap.add_argument("--no-reuse", dest="reuse", action="store_false",
+                    help="skip the secondary reuse_zsums field (one step with the z-sums shared between points, "
+                         "lzq_sweep_grid_reuse; not the headline: SURVEY §8d keeps the headline dense)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI, default) | gloo (rehearsal of the N>1 path on one GPU)")

@@ -19,6 +19,7 @@ import bench  # noqa: E402
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    reuse = len(sys.argv) > 3 and sys.argv[3] == "reuse"   # time lzq_sweep_grid_reuse instead of the dense sweep
     E = importlib.import_module(bench.PKG + ".engine").Engine
     paths = sorted(glob.glob(os.path.join(ROOT, bench.PKG, "_build", "variants", "*.so")))
     engs = {os.path.basename(p)[7:-3]: E(0, lib_path=p) for p in paths}
@@ -26,7 +27,7 @@ def main():
     ref = None
     res = {k: [] for k in engs}
     for k, e in engs.items():  # warm-up + cross-variant agreement
-        t = e.sweep(bench.BASE, axes, 0, n).cpu().numpy()
+        t = e.sweep(bench.BASE, axes, 0, n, reuse=reuse).cpu().numpy()
         if ref is None:
             ref = t
         nz = ref != 0
@@ -35,7 +36,7 @@ def main():
         for k, e in engs.items():
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            e.sweep(bench.BASE, axes, 0, n)
+            e.sweep(bench.BASE, axes, 0, n, reuse=reuse)
             torch.cuda.synchronize()
             res[k].append(n / (time.perf_counter() - t0))
     out = {k: round(float(np.median(v))) for k, v in sorted(res.items(), key=lambda kv: -np.median(kv[1]))}

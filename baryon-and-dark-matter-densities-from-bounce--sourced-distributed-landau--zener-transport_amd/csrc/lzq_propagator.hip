@@ -249,14 +249,16 @@ __device__ double point_steps(const double* mm, const double* dp, const double* 
 // bin (0 = costliest) of every point + the histogram of bins
 __global__ __launch_bounds__(kPropBlock) void lz_cost_kernel(const double* __restrict__ m_mix,
                                                              const double* __restrict__ dprime,
-                                                             const double* __restrict__ xi, int64_t n, int32_t n_cross,
-                                                             double v_w, double K, int32_t S,
+                                                             const double* __restrict__ xi,
+                                                             const double* __restrict__ vw, int64_t n, int32_t n_cross,
+                                                             double v_w0, double K, int32_t S,
                                                              int32_t* __restrict__ bins, int32_t* __restrict__ hist) {
   __shared__ int32_t lh[kCostBins];
   for (int t = threadIdx.x; t < kCostBins; t += kPropBlock) lh[t] = 0;
   __syncthreads();
   const int64_t p = (int64_t)blockIdx.x * kPropBlock + threadIdx.x;
   if (p < n) {
+    const double v_w = vw ? vw[p] : v_w0;
     const double st = point_steps(m_mix + p * n_cross, dprime + p * n_cross, xi + p * n_cross, n_cross, v_w, K, S);
     // non-finite or absurd inputs (the kernel returns NaN at once) go with the cheapest
     const double key = st == st ? fmin(fmax(4.0 * log2(1.0 + st), 0.0), (double)(kCostBins - 1)) : 0.0;
@@ -302,13 +304,19 @@ __global__ __launch_bounds__(kPropBlock) void lz_scatter_kernel(const int32_t* _
 
 __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_kernel(const double* __restrict__ m_mix,
                                                                   const double* __restrict__ dprime,
-                                                                  const double* __restrict__ xi, int64_t n,
-                                                                  int32_t n_cross, double v_w, double K,
+                                                                  const double* __restrict__ xi,
+                                                                  const double* __restrict__ vw, int64_t n,
+                                                                  int32_t n_cross, double v_w0, double K,
                                                                   int32_t S, const int32_t* __restrict__ order,
                                                                   double* __restrict__ P_out) {
   const int64_t tid = (int64_t)blockIdx.x * kPropBlock + threadIdx.x;
   if (tid >= n) return;
   const int64_t p = order ? (int64_t)order[tid] : tid;
+  const double v_w = vw ? vw[p] : v_w0;  // per-point wall speed (lzq_lz_propagate_v) or the batch's
+  if (!(v_w > 0.0)) {
+    P_out[p] = __builtin_nan("");
+    return;
+  }
   const double* mm = m_mix + p * n_cross;
   const double* dp = dprime + p * n_cross;
   const double* xc = xi + p * n_cross;
@@ -423,13 +431,10 @@ __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_k
 // error plumbing shared with lzq_kernels.hip (C++ linkage, not part of the C ABI)
 int lzq_set_error(int code, const char* msg);
 
-extern "C" int lzq_lz_propagate(const double* d_m_mix, const double* d_dprime, const double* d_xi, int64_t n,
-                                int32_t n_cross, double v_w, double window_lz, int32_t steps_per_crossing,
-                                double* d_P, void* stream) {
-  if (n < 0 || n_cross <= 0 || steps_per_crossing <= 0 || steps_per_crossing > 1000000 || !(v_w > 0.0) ||
-      !(window_lz > 0.0) || !(window_lz <= 200.0) || (n > 0 && (!d_m_mix || !d_dprime || !d_xi || !d_P)))
-    return lzq_set_error(LZQ_EINVAL, "lzq_lz_propagate: bad arguments (need n >= 0, n_cross > 0, "
-                                     "0 < steps_per_crossing <= 1e6, v_w > 0, 0 < window_lz <= 200)");
+namespace {
+int propagate_launch(const double* d_m_mix, const double* d_dprime, const double* d_xi, const double* d_v_w, int64_t n,
+                     int32_t n_cross, double v_w, double window_lz, int32_t steps_per_crossing, double* d_P,
+                     void* stream) {
   if (n == 0) return LZQ_OK;
   if (n > 2147483647LL) return lzq_set_error(LZQ_EINVAL, "lzq_lz_propagate: n too large (int32 point order)");
   const int64_t nb = (n + lzq::kPropBlock - 1) / lzq::kPropBlock;
@@ -449,13 +454,13 @@ extern "C" int lzq_lz_propagate(const double* d_m_mix, const double* d_dprime, c
       return lzq_set_error(LZQ_EHIP, hipGetErrorString(e));
     }
     hipLaunchKernelGGL(lzq::lz_cost_kernel, dim3((unsigned)nb), dim3(lzq::kPropBlock), 0, st, d_m_mix, d_dprime, d_xi,
-                       n, n_cross, v_w, window_lz, steps_per_crossing, bins, hist);
+                       d_v_w, n, n_cross, v_w, window_lz, steps_per_crossing, bins, hist);
     hipLaunchKernelGGL(lzq::lz_bin_scan_kernel, dim3(1), dim3(64), 0, st, hist, offs);
     hipLaunchKernelGGL(lzq::lz_scatter_kernel, dim3((unsigned)nb), dim3(lzq::kPropBlock), 0, st, bins, n, offs, ord);
     order = ord;
   }
   hipLaunchKernelGGL(lzq::lz_propagate_kernel, dim3((unsigned)nb), dim3(lzq::kPropBlock), 0, st,
-                     d_m_mix, d_dprime, d_xi, n, n_cross, v_w, window_lz, steps_per_crossing, order, d_P);
+                     d_m_mix, d_dprime, d_xi, d_v_w, n, n_cross, v_w, window_lz, steps_per_crossing, order, d_P);
   hipError_t e = hipGetLastError();
   if (ws) {
     const hipError_t ef = hipFreeAsync(ws, st);
@@ -463,4 +468,32 @@ extern "C" int lzq_lz_propagate(const double* d_m_mix, const double* d_dprime, c
   }
   if (e != hipSuccess) return lzq_set_error(LZQ_EHIP, hipGetErrorString(e));
   return LZQ_OK;
+}
+
+bool propagate_args_ok(int64_t n, int32_t n_cross, double window_lz, int32_t steps_per_crossing) {
+  return n >= 0 && n_cross > 0 && steps_per_crossing > 0 && steps_per_crossing <= 1000000 && window_lz > 0.0 &&
+         window_lz <= 200.0;
+}
+}  // namespace
+
+extern "C" int lzq_lz_propagate(const double* d_m_mix, const double* d_dprime, const double* d_xi, int64_t n,
+                                int32_t n_cross, double v_w, double window_lz, int32_t steps_per_crossing,
+                                double* d_P, void* stream) {
+  if (!propagate_args_ok(n, n_cross, window_lz, steps_per_crossing) || !(v_w > 0.0) ||
+      (n > 0 && (!d_m_mix || !d_dprime || !d_xi || !d_P)))
+    return lzq_set_error(LZQ_EINVAL, "lzq_lz_propagate: bad arguments (need n >= 0, n_cross > 0, "
+                                     "0 < steps_per_crossing <= 1e6, v_w > 0, 0 < window_lz <= 200)");
+  return propagate_launch(d_m_mix, d_dprime, d_xi, nullptr, n, n_cross, v_w, window_lz, steps_per_crossing, d_P,
+                          stream);
+}
+
+extern "C" int lzq_lz_propagate_v(const double* d_m_mix, const double* d_dprime, const double* d_xi,
+                                  const double* d_v_w, int64_t n, int32_t n_cross, double window_lz,
+                                  int32_t steps_per_crossing, double* d_P, void* stream) {
+  if (!propagate_args_ok(n, n_cross, window_lz, steps_per_crossing) ||
+      (n > 0 && (!d_m_mix || !d_dprime || !d_xi || !d_v_w || !d_P)))
+    return lzq_set_error(LZQ_EINVAL, "lzq_lz_propagate_v: bad arguments (need n >= 0, n_cross > 0, "
+                                     "0 < steps_per_crossing <= 1e6, 0 < window_lz <= 200, d_v_w)");
+  return propagate_launch(d_m_mix, d_dprime, d_xi, d_v_w, n, n_cross, 1.0, window_lz, steps_per_crossing, d_P,
+                          stream);
 }

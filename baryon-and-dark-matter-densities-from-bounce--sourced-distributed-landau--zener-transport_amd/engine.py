@@ -285,19 +285,30 @@ class Engine:
         return out
 
     # -- LZ propagator (north_star (1)) ------------------------------------------------------
-    def lz_propagate(self, m_mix, dprime, xi, v_w: float, window_lz: float,
+    def lz_propagate(self, m_mix, dprime, xi, v_w, window_lz: float,
                      steps_per_crossing: int) -> torch.Tensor:
-        """Coherent LZ conversion probability per point (arrays [n] or [n, n_cross])."""
+        """Coherent LZ conversion probability per point (arrays [n] or [n, n_cross]).  v_w: one
+        wall speed for the batch, or one per point ([n]: lzq_lz_propagate_v)."""
         m = self._f64(m_mix)
         if m.dim() == 1:
             m = m.reshape(-1, 1)
         d = self._f64(dprime).reshape(m.shape)
         x = self._f64(xi).reshape(m.shape)
         out = torch.empty(m.shape[0], dtype=torch.float64, device=self.device)
+        per_point = isinstance(v_w, (torch.Tensor, np.ndarray, list, tuple))
         with torch.cuda.device(self.device):
-            self._check(self.lib.lzq_lz_propagate(_vp(m), _vp(d), _vp(x), m.shape[0], m.shape[1], float(v_w),
-                                                    float(window_lz), int(steps_per_crossing), _vp(out),
-                                                    self._stream()))
+            if per_point:
+                vw = self._f64(v_w).reshape(-1)
+                if vw.numel() != m.shape[0]:
+                    raise ValueError("v_w must be a scalar or have one entry per point")
+                self._check(self.lib.lzq_lz_propagate_v(_vp(m), _vp(d), _vp(x), _vp(vw), m.shape[0], m.shape[1],
+                                                          float(window_lz), int(steps_per_crossing), _vp(out),
+                                                          self._stream()))
+                self._keepalive_vw = vw
+            else:
+                self._check(self.lib.lzq_lz_propagate(_vp(m), _vp(d), _vp(x), m.shape[0], m.shape[1], float(v_w),
+                                                        float(window_lz), int(steps_per_crossing), _vp(out),
+                                                        self._stream()))
         return out
 
 

@@ -402,9 +402,8 @@ def coherent_P(spec: SweepSpec, s: int, n: int, engine):
     """Coherent conversion probability of grid points [s, s+n) through their crossings
     (spec.crossings; lzq_lz_propagate), a device tensor."""
     m, dp, xi, v_w = spec.crossing_arrays(s, n, engine.device)
-    if not bool((v_w == v_w[0]).all()):
-        raise NotImplementedError("multi-crossing sweeps need a single v_w")
-    return engine.lz_propagate(m, dp, xi, float(v_w[0]), spec.crossings.window_lz, spec.crossings.steps)
+    vw = float(v_w[0]) if bool((v_w == v_w[0]).all()) else v_w   # a v_w axis: per-point wall speeds
+    return engine.lz_propagate(m, dp, xi, vw, spec.crossings.window_lz, spec.crossings.steps)
 
 
 def make_compute(spec: SweepSpec, engine, reuse: bool = False) -> ComputeFn:

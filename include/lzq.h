@@ -283,6 +283,12 @@ int lzq_lz_propagate(const double* d_m_mix, const double* d_dprime, const double
                      int64_t n, int32_t n_cross, double v_w, double window_lz,
                      int32_t steps_per_crossing, double* d_P, void* stream);
 
+/* lzq_lz_propagate with a per-point wall speed d_v_w[n] (sweeps over v_w with crossings); a
+ * point whose v_w is not > 0 gets P = NaN. */
+int lzq_lz_propagate_v(const double* d_m_mix, const double* d_dprime, const double* d_xi, const double* d_v_w,
+                       int64_t n, int32_t n_cross, double window_lz, int32_t steps_per_crossing, double* d_P,
+                       void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -106,3 +106,45 @@ def test_longest_first_order_is_bit_identical(gpu_engine):
     ok = ~torch.isnan(parts)
     assert int(ok.sum()) == n - 1
     assert torch.equal(whole[ok], parts[ok])
+
+
+def test_per_point_wall_speed(gpu_engine):
+    """lzq_lz_propagate_v (a wall speed per point, for sweeps over v_w with crossings): equal bit
+    for bit to lzq_lz_propagate called per v_w value, in both launch orders (>= 16384 points:
+    longest-first), and NaN for a non-positive v_w."""
+    import torch
+    sw = pkg("sweep")
+    spec = sw.builtin_specs()["C5"]
+    n = 20000
+    m, dp, xi, _ = spec.crossing_arrays((spec.total - n) // 2, n, gpu_engine.device)
+    speeds = torch.tensor([0.1, 0.3, 0.9], dtype=torch.float64, device=gpu_engine.device)
+    vw = speeds[torch.arange(n, device=gpu_engine.device) % 3].clone()
+    K, S = spec.crossings.window_lz, spec.crossings.steps
+    got = gpu_engine.lz_propagate(m, dp, xi, vw, K, S)
+    for k in range(3):
+        sel = torch.arange(k, n, 3, device=gpu_engine.device)
+        want = gpu_engine.lz_propagate(m[sel], dp[sel], xi[sel], float(speeds[k]), K, S)
+        assert torch.equal(got[sel], want)
+    small = gpu_engine.lz_propagate(m[:500], dp[:500], xi[:500], vw[:500], K, S)   # index order
+    assert torch.equal(small, got[:500])
+    vw[3] = 0.0
+    bad = gpu_engine.lz_propagate(m[:8], dp[:8], xi[:8], vw[:8], K, S)
+    assert torch.isnan(bad[3]) and bool(torch.isfinite(bad[torch.arange(8) != 3]).all())
+
+
+def test_multicrossing_sweep_over_wall_speed(gpu_engine):
+    """A C5-style sweep with a v_w axis (the C4 scan's v_w values) runs through the sweep driver
+    (it used to refuse): every point's P is the per-point-v_w propagator output."""
+    import dataclasses
+
+    import torch
+    sw = pkg("sweep")
+    c5 = sw.builtin_specs()["C5"]
+    spec = dataclasses.replace(c5, name="C5_vw", axes=[("v_w", np.linspace(0.05, 0.95, 10)),
+                                                       ("m_mix", np.logspace(-3, 0, 8)), ("dprime", np.logspace(-3, 1, 8))])
+    n = spec.total
+    out = torch.empty((n, 6), dtype=torch.float64, device=gpu_engine.device)
+    sw.make_compute(spec, gpu_engine)(0, n, out)
+    m, dp, xi, vw = spec.crossing_arrays(0, n, gpu_engine.device)
+    P = gpu_engine.lz_propagate(m, dp, xi, vw, spec.crossings.window_lz, spec.crossings.steps)
+    assert torch.equal(out[:, 5], P) and bool(torch.isfinite(out).all())

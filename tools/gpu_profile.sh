@@ -8,7 +8,7 @@ OUT=gpurun_out/prof
 rm -rf $OUT; mkdir -p $OUT
 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_traced.json 2> $OUT/bench_traced.err || { tail -5 $OUT/bench_traced.err; exit 2; }
 cat $OUT/bench_traced.json
-P="--points 200000 --steps 1 --warmup 0 --no-cpu-baseline"
+P="--points 200000 --steps 1 --warmup 0 --no-cpu-baseline --no-reuse"
 pmc() { tag=$1; shift; timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d $OUT/pmc_$tag -o run -- python3 bench.py $P > $OUT/pmc_$tag.json 2> $OUT/pmc_$tag.err || echo "pmc $tag failed"; }
 pmc fetch FETCH_SIZE
 pmc write WRITE_SIZE

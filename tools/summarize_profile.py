@@ -14,7 +14,7 @@ NODES_PER_POINT = 8000 * 1200
 WAVE_NODES_PER_POINT = NODES_PER_POINT // 64
 
 
-def agg(path, key="grid"):
+def agg(path, key="yields_grid_kernel"):
     rows = list(csv.DictReader(open(path)))
     tot = defaultdict(float)
     disp = set()

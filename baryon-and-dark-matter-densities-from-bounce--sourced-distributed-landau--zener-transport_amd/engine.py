@@ -135,10 +135,15 @@ class Engine:
             Pp = None if P_points is None else self._f64(P_points).reshape(-1)
             if Pp is not None and Pp.numel() != count:
                 raise ValueError("P_points must have `count` entries")
+            need = self.lib.lzq_sweep_grid_reuse_workspace(arr, len(axes), int(n_y)) if reuse else 0
+            if need < 0:
+                self._check(int(need))
+            n_tables = need // (max(int(n_y), 2000) + 4)
+            # every table costs one dense point, so they pay only with at least as many points as
+            # tables; and their workspace stays bounded (REUSE_MAX_BYTES): otherwise the dense path,
+            # which gives the same bits
+            reuse = reuse and 0 < n_tables <= count and need * 8 <= REUSE_MAX_BYTES
             if reuse:
-                need = self.lib.lzq_sweep_grid_reuse_workspace(arr, len(axes), int(n_y))
-                if need < 0:
-                    self._check(int(need))
                 if self._zwork is None or self._zwork.numel() < need:
                     self._zwork = torch.empty(max(int(need), 1), dtype=torch.float64, device=self.device)
                 self._check(self.lib.lzq_sweep_grid_reuse(ctypes.byref(base), arr, len(axes), int(start), int(count),
@@ -313,6 +318,7 @@ class Engine:
 
 
 _MIX = -7046029254386353131  # 0x9E3779B97F4A7C15 as int64 (torch multiplies wrap)
+REUSE_MAX_BYTES = 16 << 30     # Engine.sweep(reuse=True): z-sum tables beyond this run dense
 
 
 def wave_order(d_pts: torch.Tensor, d_ode: torch.Tensor, n: int):

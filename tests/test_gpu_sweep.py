@@ -178,3 +178,10 @@ def test_reuse_zsums_table_axes_and_overrides(gpu_engine):
         assert torch.equal(dense, reuse)
     t = reuse.cpu().numpy()
     assert (t[:, 0] == 0.0).any() and np.isfinite(t[:, 1]).all()   # T_min/T_p = 8: empty window, Y_B = 0
+    prev = gpu_engine.tune_exp("poly11")            # the tables follow the exponential variant too
+    try:
+        dense = gpu_engine.sweep(base, axes, 0, total, P_points=P)
+        reuse = gpu_engine.sweep(base, axes, 0, total, P_points=P, reuse=True)
+    finally:
+        gpu_engine.tune_exp(prev)
+    assert torch.equal(dense, reuse)

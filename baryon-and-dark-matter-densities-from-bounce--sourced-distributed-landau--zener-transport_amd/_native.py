@@ -68,11 +68,13 @@ ABI_VERSION = 1  # LZQ_ABI_VERSION (tests/test_capi.py checks it against the lib
 # Symbols declared in include/lzq.h (checked by tests/test_capi.py against the header).
 EXPORTS = ("lzq_abi_version", "lzq_last_error", "lzq_init", "lzq_ztables", "lzq_tune", "lzq_aov_batch",
            "lzq_jchi_batch", "lzq_yields_batch", "lzq_sweep_grid", "lzq_sweep_grid_reuse_workspace",
-           "lzq_sweep_grid_reuse", "lzq_p_closed_form",
+           "lzq_sweep_grid_reuse", "lzq_yields_batch_reuse", "lzq_p_closed_form",
            "lzq_lz_propagate", "lzq_lz_propagate_v", "lzq_ode_tables", "lzq_ode_integrate", "lzq_ode_integrate_shared", "lzq_ode_quadrature", "lzq_ode_batch",
            "lzq_ode_aov_T", "lzq_ode_rhs")
 # the lzq_point fields an ODE spline table depends on (A/V kernel fpy:141-156 + window fpy:368-369)
 ODE_TABLE_KEY = ("I_p", "beta_over_H", "T_p_GeV", "v_w", "g_star", "T_min_over_Tp", "T_max_over_Tp")
+# the lzq_point fields the quadrature's z-sums depend on (its y-grid and c; lzq_yields_batch_reuse)
+ZSUM_KEY = ("I_p", "beta_over_H", "T_p_GeV", "T_min_over_Tp", "T_max_over_Tp")
 # every point field the ODE integrator's stage ingredients read besides P, flux and the ODE
 # parameters (ode_stage_base / ode_stage_chi_base + the spline table): points equal in these can
 # share a cooperative wavefront (include/lzq.h LZQ_TUNE_ODE_COOP)
@@ -113,6 +115,7 @@ def load(path: str | None = None):
     L.lzq_sweep_grid.argtypes = [P(LzqPoint), P(LzqAxis), i32, i64, i64, i32, vp, vp, vp]
     L.lzq_sweep_grid_reuse_workspace.argtypes = [P(LzqAxis), i32, i32]
     L.lzq_sweep_grid_reuse.argtypes = [P(LzqPoint), P(LzqAxis), i32, i64, i64, i32, vp, vp, i64, vp, vp]
+    L.lzq_yields_batch_reuse.argtypes = [vp, i64, i32, vp, vp, vp, i64, vp, i64, vp, vp]
     L.lzq_p_closed_form.argtypes = [vp, i64, vp, vp]
     L.lzq_lz_propagate.argtypes = [vp, vp, vp, i64, i32, d, d, i32, vp, vp]
     L.lzq_lz_propagate_v.argtypes = [vp, vp, vp, vp, i64, i32, d, i32, vp, vp]

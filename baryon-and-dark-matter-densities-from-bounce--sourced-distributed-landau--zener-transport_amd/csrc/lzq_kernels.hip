@@ -870,6 +870,60 @@ __global__ __launch_bounds__(kBlock) void grid_reuse_kernel(lzq_point base, Grid
   }
 }
 
+// The same for explicit points (lzq_yields_batch_reuse): table t is made for point reps[t];
+// point i integrates from table tidx[i].
+template <int EXPV>
+__global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void points_ztable_kernel(const lzq_point* __restrict__ pts,
+                                                                            const int64_t* __restrict__ reps,
+                                                                            int64_t n_tab, int32_t n_y, int64_t tstride,
+                                                                            const ZNode* __restrict__ zt,
+                                                                            const double* __restrict__ gtab,
+                                                                            double* __restrict__ Fw, int truncate) {
+  __shared__ double lds_tab[kTabN];
+  const double* tab = stage_table<EXPV>(gtab, lds_tab);
+  __shared__ WaveSlot slots[kWavesPerBlock];
+  const int lane = threadIdx.x & (kWaveSize - 1);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t t = (int64_t)blockIdx.x * kWavesPerBlock + w;
+  if (t >= n_tab) return;
+  const lzq_point pt = pts[reps[t]];
+  const double P = pt.P_chi_to_B;
+  const QuadSetup qs = quad_setup(pt, P, pt.T_min_over_Tp * pt.T_p_GeV, pt.T_max_over_Tp * pt.T_p_GeV, n_y);
+  double* F = Fw + t * tstride;
+  if (lane == 0) {
+    F[0] = qs.y_lo;
+    F[1] = qs.y_hi;
+    F[2] = (double)qs.n;
+    F[3] = qs.cneg;
+  }
+  park(slots[w], qs, epilogue_pre(pt, P), lane);
+  yb_wave<kYB, EXPV, kYbTable>(slots, w, zt, tab, truncate, nullptr, F + kTabHdr);
+}
+
+__global__ __launch_bounds__(kBlock) void points_reuse_kernel(const lzq_point* __restrict__ pts, int64_t n,
+                                                             int32_t n_y, const double* __restrict__ Pov,
+                                                             const int32_t* __restrict__ tidx,
+                                                             const double* __restrict__ Fw, int64_t tstride,
+                                                             lzq_yield* __restrict__ out) {
+  __shared__ WaveSlot slots[kWavesPerBlock];
+  const int lane = threadIdx.x & (kWaveSize - 1);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t idx = (int64_t)blockIdx.x * kWavesPerBlock + w;
+  if (idx >= n) return;
+  const lzq_point pt = pts[idx];
+  const double P = Pov ? Pov[idx] : pt.P_chi_to_B;
+  const QuadSetup qs = quad_setup(pt, P, pt.T_min_over_Tp * pt.T_p_GeV, pt.T_max_over_Tp * pt.T_p_GeV, n_y);
+  const double* F = Fw + (int64_t)tidx[idx] * tstride;
+  const bool match = qs.empty || (F[0] == qs.y_lo && F[1] == qs.y_hi && F[2] == (double)qs.n && F[3] == qs.cneg);
+  park(slots[w], qs, epilogue_pre(pt, P), lane);
+  const double Y_B = match ? yb_wave<kYB, kExpTable, kYbReuse>(slots, w, nullptr, nullptr, 0, F + kTabHdr) : 0.0;
+  if (lane == 0) {
+    lzq_yield o = epilogue_finish(slots[w].e, Y_B);
+    if (!match) o.Y_B = o.rho_B_kg_m3 = o.DM_over_B = __builtin_nan("");
+    out[idx] = o;
+  }
+}
+
 // fpy:158-165, one lane per y value
 template <int EXPV>
 __global__ __launch_bounds__(kBlock) void aov_kernel(lzq_point pt, const double* __restrict__ ys, int64_t n,
@@ -1227,6 +1281,36 @@ int lzq_sweep_grid(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, 
     hipLaunchKernelGGL((lzq::yields_grid_kernel<lzq::kYB, lzq::kExpPoly11>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
                        (hipStream_t)stream, *base, g, start, count, n_y, d_P, g_dev_tab[dev], exp_table(dev), d_out,
                        g_truncate);
+  LZQ_HIP(hipGetLastError());
+  return LZQ_OK;
+}
+
+int lzq_yields_batch_reuse(const lzq_point* d_points, int64_t n, int32_t n_y, const double* d_P,
+                           const int64_t* d_rep, const int32_t* d_table_index, int64_t n_tables, double* d_work,
+                           int64_t work_doubles, lzq_yield* d_out, void* stream) {
+  if (n < 0 || n_tables < 0 || (n > 0 && (!d_points || !d_out || !d_rep || !d_table_index || n_tables == 0)))
+    return fail(LZQ_EINVAL, "lzq_yields_batch_reuse: bad arguments");
+  const int64_t stride = (n_y > LZQ_NY_MIN ? n_y : LZQ_NY_MIN) + lzq::kTabHdr;
+  if (n_tables > INT64_MAX / stride) return fail(LZQ_EINVAL, "lzq_yields_batch_reuse: too many tables");
+  if (n > 0 && (!d_work || work_doubles < n_tables * stride))
+    return fail(LZQ_EINVAL, "lzq_yields_batch_reuse: workspace of %lld doubles < %lld needed", (long long)work_doubles,
+                (long long)(n_tables * stride));
+  if (n == 0) return LZQ_OK;
+  int dev, rc = ensure_device(&dev);
+  if (rc) return rc;
+  const int64_t nbt = blocks_for(n_tables, lzq::kWavesPerBlock), nb = blocks_for(n, lzq::kWavesPerBlock);
+  if (nbt > kMaxGrid || nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_yields_batch_reuse: too large for one launch");
+  if (g_exp_variant == lzq::kExpTable)
+    hipLaunchKernelGGL((lzq::points_ztable_kernel<lzq::kExpTable>), dim3((unsigned)nbt), dim3(lzq::kBlock), 0,
+                       (hipStream_t)stream, d_points, d_rep, n_tables, n_y, stride, g_dev_tab[dev], exp_table(dev),
+                       d_work, 1);
+  else
+    hipLaunchKernelGGL((lzq::points_ztable_kernel<lzq::kExpPoly11>), dim3((unsigned)nbt), dim3(lzq::kBlock), 0,
+                       (hipStream_t)stream, d_points, d_rep, n_tables, n_y, stride, g_dev_tab[dev], exp_table(dev),
+                       d_work, 1);
+  LZQ_HIP(hipGetLastError());
+  hipLaunchKernelGGL(lzq::points_reuse_kernel, dim3((unsigned)nb), dim3(lzq::kBlock), 0, (hipStream_t)stream, d_points,
+                     n, n_y, d_P, d_table_index, d_work, stride, d_out);
   LZQ_HIP(hipGetLastError());
   return LZQ_OK;
 }

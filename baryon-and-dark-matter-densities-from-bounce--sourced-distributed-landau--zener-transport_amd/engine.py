@@ -94,9 +94,12 @@ class Engine:
         return out
 
     # -- fpy:231-267 + epilogue ----------------------------------------------------------------
-    def yields(self, points, n_y: int = 8000, T_lo=None, T_hi=None, P=None) -> torch.Tensor:
+    def yields(self, points, n_y: int = 8000, T_lo=None, T_hi=None, P=None, reuse: bool = False) -> torch.Tensor:
         """points: POINT_DTYPE numpy array or a device byte tensor from points_to_device.
-        Returns (n, 6) float64 device tensor in YIELD_FIELDS order."""
+        Returns (n, 6) float64 device tensor in YIELD_FIELDS order.
+        reuse: lzq_yields_batch_reuse -- points equal in _native.ZSUM_KEY share one table of
+        z-sums (bit-identical; not the dense headline path).  Used only with main()'s window
+        and when points do share; otherwise the dense path."""
         d_pts = points if isinstance(points, torch.Tensor) else self.points_to_device(points)
         n = d_pts.numel() // _native.POINT_DTYPE.itemsize
         out = torch.empty((n, 6), dtype=torch.float64, device=self.device)
@@ -104,8 +107,21 @@ class Engine:
         th = None if T_hi is None else self._f64(T_hi)
         Pv = None if P is None else self._f64(P)
         with torch.cuda.device(self.device):
-            self._check(self.lib.lzq_yields_batch(_vp(d_pts), n, int(n_y), _vp(tl), _vp(th), _vp(Pv), _vp(out),
-                                                    self._stream()))
+            groups = table_groups(d_pts, n, _ZSUM_WORDS) if reuse and tl is None and th is None else None
+            stride = max(int(n_y), 2000) + 4
+            if groups is not None and groups[0].numel() * stride * 8 <= REUSE_MAX_BYTES:
+                rep, inv = groups
+                need = rep.numel() * stride
+                if self._zwork is None or self._zwork.numel() < need:
+                    self._zwork = torch.empty(need, dtype=torch.float64, device=self.device)
+                idx = inv.to(torch.int32)
+                self._check(self.lib.lzq_yields_batch_reuse(_vp(d_pts), n, int(n_y), _vp(Pv), _vp(rep), _vp(idx),
+                                                              rep.numel(), _vp(self._zwork), self._zwork.numel(),
+                                                              _vp(out), self._stream()))
+                self._keepalive_reuse = (rep, idx, d_pts)
+            else:
+                self._check(self.lib.lzq_yields_batch(_vp(d_pts), n, int(n_y), _vp(tl), _vp(th), _vp(Pv), _vp(out),
+                                                        self._stream()))
         return out
 
     # -- grid sweep ----------------------------------------------------------------------------
@@ -348,18 +364,20 @@ def wave_order(d_pts: torch.Tensor, d_ode: torch.Tensor, n: int):
 
 
 _KEY_WORDS = [_native.POINT_DOUBLE_FIELDS.index(f) for f in _native.ODE_TABLE_KEY]  # 8-byte words of lzq_point
+_ZSUM_WORDS = [_native.POINT_DOUBLE_FIELDS.index(f) for f in _native.ZSUM_KEY]
 
 
-def table_groups(d_pts: torch.Tensor, n: int):
+def table_groups(d_pts: torch.Tensor, n: int, words=None):
     """Points (device lzq_point records) that can share one ODE spline table: equal, bit for
-    bit, in _native.ODE_TABLE_KEY.  Returns (representative indices, per-point table index),
+    bit, in _native.ODE_TABLE_KEY (or in the lzq_point words `words`: _ZSUM_WORDS for the
+    quadrature's z-sum tables).  Returns (representative indices, per-point table index),
     both int64 device tensors, or None when sharing would not pay (more than half the points
     distinct).  Index bookkeeping on the device: a 64-bit mix of the key words is deduplicated
     and every point's key is then compared with its representative's, so a hash collision only
     costs the sharing, never a wrong table."""
     if n < 2:
         return None
-    key = d_pts.view(n, _native.POINT_DTYPE.itemsize).view(torch.int64)[:, _KEY_WORDS]
+    key = d_pts.view(n, _native.POINT_DTYPE.itemsize).view(torch.int64)[:, _KEY_WORDS if words is None else words]
     if bool((key == key[0]).all()):
         z = torch.zeros(n, dtype=torch.int64, device=d_pts.device)
         return z[:1], z

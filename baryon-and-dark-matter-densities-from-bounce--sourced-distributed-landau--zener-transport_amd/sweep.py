@@ -427,7 +427,7 @@ def make_compute(spec: SweepSpec, engine, reuse: bool = False) -> ComputeFn:
                 out[torch.as_tensor(sel, device=out.device)] = tab
             sel = np.nonzero(~ode)[0]
             if sel.size:
-                out[torch.as_tensor(sel, device=out.device)] = engine.yields(pts[sel], n_y=spec.n_y)
+                out[torch.as_tensor(sel, device=out.device)] = engine.yields(pts[sel], n_y=spec.n_y, reuse=reuse)
         return compute_ode
 
     def compute(s, n, out):

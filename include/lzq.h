@@ -166,6 +166,14 @@ int lzq_sweep_grid(const lzq_point* base, const lzq_axis* axes, int32_t n_axes,
  * lzq_sweep_grid (same operations, same lane order).  d_work: >= lzq_sweep_grid_reuse_workspace
  * doubles (tables x (max(n_y, LZQ_NY_MIN) + 4)); a negative return is an error code. */
 int64_t lzq_sweep_grid_reuse_workspace(const lzq_axis* axes, int32_t n_axes, int32_t n_y);
+/* The same for n explicit points: d_rep[n_tables] (int64) names one point per table, whose
+ * I_p, beta_over_H, T_p_GeV, T_min_over_Tp, T_max_over_Tp the table is made for;
+ * d_table_index[n] (int32) gives each point's table.  main()'s window only (no T_lo/T_hi
+ * overrides).  d_work >= n_tables * (max(n_y, LZQ_NY_MIN) + 4) doubles.  A point whose y-grid or
+ * c differs from its table's gets NaN yields.  Bit-identical to lzq_yields_batch. */
+int lzq_yields_batch_reuse(const lzq_point* d_points, int64_t n, int32_t n_y, const double* d_P,
+                           const int64_t* d_rep, const int32_t* d_table_index, int64_t n_tables, double* d_work,
+                           int64_t work_doubles, lzq_yield* d_out, void* stream);
 int lzq_sweep_grid_reuse(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int64_t start, int64_t count,
                          int32_t n_y, const double* d_P, double* d_work, int64_t work_doubles, lzq_yield* d_out,
                          void* stream);

@@ -180,3 +180,26 @@ def test_wide_random_fuzz_vs_oracle(gpu_engine):
             assert e < GUARD, (k, a, b, c)
             worst = max(worst, e)
     print(f"wide fuzz: 1024 points vs oracle, worst rel err {worst:.3e}")
+
+
+def test_points_reuse_bit_identical(gpu_engine):
+    """lzq_yields_batch_reuse (Engine.yields(reuse=True); z-sums shared by points equal in I_p,
+    beta/H, T_p, T_min/T_p, T_max/T_p; not the headline mode): the golden points' configs, each
+    repeated with other P / m_chi / sigma_y / flux / statistics, in shuffled order, give the
+    same bits as the dense batch."""
+    import torch
+    pts = golden("golden_points.json")["points"]
+    rng = np.random.default_rng(17)
+    cfgs = []
+    for r in pts[:120]:
+        for _ in range(4):
+            c = full_cfg(r["config"])
+            c.update(P_chi_to_B=float(rng.uniform(0, 1)), m_chi_GeV=float(10 ** rng.uniform(-1, 3)),
+                     source_shape_sigma_y=float(rng.uniform(3, 30)), chi_stats=str(rng.choice(["fermion", "boson"])))
+            cfgs.append(c)
+    perm = rng.permutation(len(cfgs))
+    rec = recs([cfgs[i] for i in perm])
+    dense = gpu_engine.yields(rec)
+    reuse = gpu_engine.yields(rec, reuse=True)
+    ok = torch.isfinite(dense) | torch.isnan(dense)
+    assert bool(ok.all()) and torch.equal(torch.nan_to_num(dense, nan=7.0), torch.nan_to_num(reuse, nan=7.0))

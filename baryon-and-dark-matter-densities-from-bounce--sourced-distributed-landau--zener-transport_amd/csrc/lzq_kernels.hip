@@ -817,6 +817,34 @@ __device__ __forceinline__ int64_t table_rep(const GridSpec& g, int64_t t) {
   return idx;
 }
 
+// Table t of one wavefront: header + the F values of the point parked in the wave's slot.
+template <int EXPV>
+__device__ __forceinline__ void ztable_wave(WaveSlot* slots, int w, int lane, const QuadSetup& qs, const EpiPre& e,
+                                            const ZNode* __restrict__ zt, const double* tab, int truncate, double* F) {
+  if (lane == 0) {
+    F[0] = qs.y_lo;
+    F[1] = qs.y_hi;
+    F[2] = (double)qs.n;
+    F[3] = qs.cneg;
+  }
+  park(slots[w], qs, e, lane);
+  yb_wave<kYB, EXPV, kYbTable>(slots, w, zt, tab, truncate, nullptr, F + kTabHdr);
+}
+
+// One point integrated from its table F (NaN yields if the table was made for another y-grid).
+__device__ __forceinline__ void reuse_wave(WaveSlot* slots, int w, int lane, const QuadSetup& qs, const EpiPre& e,
+                                           const double* __restrict__ F, lzq_yield* out) {
+  // match is wave-uniform: every lane formed the same setup
+  const bool match = qs.empty || (F[0] == qs.y_lo && F[1] == qs.y_hi && F[2] == (double)qs.n && F[3] == qs.cneg);
+  park(slots[w], qs, e, lane);
+  const double Y_B = match ? yb_wave<kYB, kExpTable, kYbReuse>(slots, w, nullptr, nullptr, 0, F + kTabHdr) : 0.0;
+  if (lane == 0) {
+    lzq_yield o = epilogue_finish(slots[w].e, Y_B);
+    if (!match) o.Y_B = o.rho_B_kg_m3 = o.DM_over_B = __builtin_nan("");
+    *out = o;
+  }
+}
+
 template <int EXPV>
 __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void grid_ztable_kernel(lzq_point base, GridSpec grid,
                                                                           int64_t n_tab, int32_t n_y, int64_t tstride,
@@ -833,15 +861,7 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void grid_ztable_kernel(lzq_
   lzq_point pt;
   const double P = grid_point(base, grid, table_rep(grid, t), pt);
   const QuadSetup qs = quad_setup(pt, P, pt.T_min_over_Tp * pt.T_p_GeV, pt.T_max_over_Tp * pt.T_p_GeV, n_y);
-  double* F = Fw + t * tstride;
-  if (lane == 0) {
-    F[0] = qs.y_lo;
-    F[1] = qs.y_hi;
-    F[2] = (double)qs.n;
-    F[3] = qs.cneg;
-  }
-  park(slots[w], qs, epilogue_pre(pt, P), lane);
-  yb_wave<kYB, EXPV, kYbTable>(slots, w, zt, tab, truncate, nullptr, F + kTabHdr);
+  ztable_wave<EXPV>(slots, w, lane, qs, epilogue_pre(pt, P), zt, tab, truncate, Fw + t * tstride);
 }
 
 __global__ __launch_bounds__(kBlock) void grid_reuse_kernel(lzq_point base, GridSpec grid, int64_t start,
@@ -858,16 +878,7 @@ __global__ __launch_bounds__(kBlock) void grid_reuse_kernel(lzq_point base, Grid
   const double Pg = grid_point(base, grid, start + local, pt);
   const double P = Pov ? Pov[local] : Pg;
   const QuadSetup qs = quad_setup(pt, P, pt.T_min_over_Tp * pt.T_p_GeV, pt.T_max_over_Tp * pt.T_p_GeV, n_y);
-  const double* F = Fw + table_of(grid, start + local) * tstride;
-  const bool match = qs.empty || (F[0] == qs.y_lo && F[1] == qs.y_hi && F[2] == (double)qs.n && F[3] == qs.cneg);
-  park(slots[w], qs, epilogue_pre(pt, P), lane);
-  // (match is wave-uniform: every lane formed the same setup)
-  const double Y_B = match ? yb_wave<kYB, kExpTable, kYbReuse>(slots, w, nullptr, nullptr, 0, F + kTabHdr) : 0.0;
-  if (lane == 0) {
-    lzq_yield o = epilogue_finish(slots[w].e, Y_B);
-    if (!match) o.Y_B = o.rho_B_kg_m3 = o.DM_over_B = __builtin_nan("");
-    out[local] = o;
-  }
+  reuse_wave(slots, w, lane, qs, epilogue_pre(pt, P), Fw + table_of(grid, start + local) * tstride, out + local);
 }
 
 // The same for explicit points (lzq_yields_batch_reuse): table t is made for point reps[t];
@@ -889,15 +900,7 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void points_ztable_kernel(co
   const lzq_point pt = pts[reps[t]];
   const double P = pt.P_chi_to_B;
   const QuadSetup qs = quad_setup(pt, P, pt.T_min_over_Tp * pt.T_p_GeV, pt.T_max_over_Tp * pt.T_p_GeV, n_y);
-  double* F = Fw + t * tstride;
-  if (lane == 0) {
-    F[0] = qs.y_lo;
-    F[1] = qs.y_hi;
-    F[2] = (double)qs.n;
-    F[3] = qs.cneg;
-  }
-  park(slots[w], qs, epilogue_pre(pt, P), lane);
-  yb_wave<kYB, EXPV, kYbTable>(slots, w, zt, tab, truncate, nullptr, F + kTabHdr);
+  ztable_wave<EXPV>(slots, w, lane, qs, epilogue_pre(pt, P), zt, tab, truncate, Fw + t * tstride);
 }
 
 __global__ __launch_bounds__(kBlock) void points_reuse_kernel(const lzq_point* __restrict__ pts, int64_t n,
@@ -913,15 +916,7 @@ __global__ __launch_bounds__(kBlock) void points_reuse_kernel(const lzq_point* _
   const lzq_point pt = pts[idx];
   const double P = Pov ? Pov[idx] : pt.P_chi_to_B;
   const QuadSetup qs = quad_setup(pt, P, pt.T_min_over_Tp * pt.T_p_GeV, pt.T_max_over_Tp * pt.T_p_GeV, n_y);
-  const double* F = Fw + (int64_t)tidx[idx] * tstride;
-  const bool match = qs.empty || (F[0] == qs.y_lo && F[1] == qs.y_hi && F[2] == (double)qs.n && F[3] == qs.cneg);
-  park(slots[w], qs, epilogue_pre(pt, P), lane);
-  const double Y_B = match ? yb_wave<kYB, kExpTable, kYbReuse>(slots, w, nullptr, nullptr, 0, F + kTabHdr) : 0.0;
-  if (lane == 0) {
-    lzq_yield o = epilogue_finish(slots[w].e, Y_B);
-    if (!match) o.Y_B = o.rho_B_kg_m3 = o.DM_over_B = __builtin_nan("");
-    out[idx] = o;
-  }
+  reuse_wave(slots, w, lane, qs, epilogue_pre(pt, P), Fw + (int64_t)tidx[idx] * tstride, out + idx);
 }
 
 // fpy:158-165, one lane per y value

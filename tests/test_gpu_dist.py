@@ -119,3 +119,14 @@ def test_rccl_one_rank_bench_line():
     r = recs[0]
     assert r["n_gpus"] == 1 and "RCCL" in r["config"]["parallelism"]
     assert r["value"] > 0 and abs(r["value"] - 20000 / (r["ms_per_step"] / 1e3)) <= 1e-6 * r["value"]
+
+
+def test_sweep_two_ranks_reuse_equals_dense(tmp_path):
+    """--reuse-zsums through the multi-rank path: 2 ranks (gloo) on a 4096-point C4 slice give the
+    dense single-rank table bit for bit (each rank builds the tables it needs itself)."""
+    args = ["--spec", "C4", "--limit", "4096", "--chunk", "1500"]
+    one, two = tmp_path / "dense", tmp_path / "reuse2"
+    run([sys.executable, "-m", PKG_NAME + ".sweep", *args, "--out", str(one)], 300)
+    run(torchrun(2) + ["-m", PKG_NAME + ".sweep", *args, "--out", str(two), "--dist-backend", "gloo",
+                       "--reuse-zsums"], 300)
+    assert np.array_equal(np.load(one / "table.npy"), np.load(two / "table.npy"))

@@ -864,7 +864,10 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void grid_ztable_kernel(lzq_
   ztable_wave<EXPV>(slots, w, lane, qs, epilogue_pre(pt, P), zt, tab, truncate, Fw + t * tstride);
 }
 
-__global__ __launch_bounds__(kBlock) void grid_reuse_kernel(lzq_point base, GridSpec grid, int64_t start,
+#ifndef LZQ_REUSE_MIN_WAVES
+#define LZQ_REUSE_MIN_WAVES 8  // 8 waves/SIMD (SGPRs capped, a few spilled to VGPR lanes): +12% over 7 (tools/ablate_builds.py ... reuse)
+#endif
+__global__ __launch_bounds__(kBlock, LZQ_REUSE_MIN_WAVES) void grid_reuse_kernel(lzq_point base, GridSpec grid, int64_t start,
                                                            int64_t count, int32_t n_y,
                                                            const double* __restrict__ Pov,
                                                            const double* __restrict__ Fw, int64_t tstride,
@@ -903,7 +906,7 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void points_ztable_kernel(co
   ztable_wave<EXPV>(slots, w, lane, qs, epilogue_pre(pt, P), zt, tab, truncate, Fw + t * tstride);
 }
 
-__global__ __launch_bounds__(kBlock) void points_reuse_kernel(const lzq_point* __restrict__ pts, int64_t n,
+__global__ __launch_bounds__(kBlock, LZQ_REUSE_MIN_WAVES) void points_reuse_kernel(const lzq_point* __restrict__ pts, int64_t n,
                                                              int32_t n_y, const double* __restrict__ Pov,
                                                              const int32_t* __restrict__ tidx,
                                                              const double* __restrict__ Fw, int64_t tstride,

@@ -3,7 +3,7 @@
 <package>/_build/variants/ in ONE process, interleaved rounds, on tools/bench_ode.py's
 narrow-window and stiff cases.  Variants must agree with the first one to 1e-11.
 
-    python tools/ablate_ode.py [n_points] [rounds]
+    python tools/ablate_ode.py [n_points] [rounds] [radau|quadrature]
 """
 import glob
 import importlib
@@ -25,6 +25,7 @@ from bench_ode import cfgs_for  # noqa: E402
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    method = sys.argv[3] if len(sys.argv) > 3 else "radau"   # or "quadrature" (the opt-in form)
     cfgm = importlib.import_module(bench.PKG + ".config")
     E = importlib.import_module(bench.PKG + ".engine").Engine
     paths = sorted(glob.glob(os.path.join(ROOT, bench.PKG, "_build", "variants", "*.so")))
@@ -39,7 +40,7 @@ def main():
         ods = np.concatenate([cfgm.to_ode_params(c) for c in cfgs])
         ref = None
         for k, e in engs.items():  # warm-up + agreement
-            t = e.ode(pts[:256], ods[:256])[0].cpu().numpy()
+            t = e.ode(pts[:256], ods[:256], method=method)[0].cpu().numpy()
             if ref is None:
                 ref = t
             assert np.max(np.abs(t - ref) / np.maximum(np.abs(ref), 1e-300)) < 1e-11, k
@@ -48,7 +49,7 @@ def main():
             for k, e in engs.items():
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
-                e.ode(pts, ods, chunk=1 << 16)
+                e.ode(pts, ods, chunk=1 << 16, method=method)
                 torch.cuda.synchronize()
                 res[k].append(n / (time.perf_counter() - t0))
         out[cname] = {k: round(max(v)) for k, v in res.items()}

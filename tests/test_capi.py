@@ -153,3 +153,20 @@ def test_sweep_grid_reuse_workspace_and_validation():
     assert rc < 0 and b"workspace" in L.lzq_last_error()
     rc = L.lzq_sweep_grid_reuse(ctypes.byref(base), axes_of(spec), len(spec.axes), 0, 0, 8000, None, None, 0, None, None)
     assert rc == 0   # empty range: nothing to do
+
+
+def test_new_entry_points_validate_arguments():
+    """lzq_lz_propagate_v and lzq_yields_batch_reuse refuse bad arguments on the host (no GPU
+    work is launched on these paths); empty batches are no-ops."""
+    n = pkg("_native")
+    L = n.load()
+    rc = L.lzq_lz_propagate_v(8, 8, 8, None, 4, 1, 20.0, 1000, 8, None)        # no v_w array
+    assert rc < 0 and b"lzq_lz_propagate_v" in L.lzq_last_error()
+    rc = L.lzq_lz_propagate_v(8, 8, 8, 8, 4, 1, 300.0, 1000, 8, None)          # window too wide
+    assert rc < 0 and b"window_lz <= 200" in L.lzq_last_error()
+    assert L.lzq_lz_propagate_v(None, None, None, None, 0, 1, 20.0, 1000, None, None) == 0
+    rc = L.lzq_yields_batch_reuse(8, 4, 8000, None, None, 8, 1, 8, 10 ** 6, 8, None)   # no rep array
+    assert rc < 0 and b"lzq_yields_batch_reuse" in L.lzq_last_error()
+    rc = L.lzq_yields_batch_reuse(8, 4, 8000, None, 8, 8, 2, 8, 2 * 8004 - 1, 8, None)  # workspace short
+    assert rc < 0 and b"workspace" in L.lzq_last_error()
+    assert L.lzq_yields_batch_reuse(None, 0, 8000, None, None, None, 0, None, 0, None, None) == 0

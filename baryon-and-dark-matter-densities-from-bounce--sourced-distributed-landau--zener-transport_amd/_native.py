@@ -50,6 +50,12 @@ ODE_STATUS = {0: "ok", 1: "`x` must be strictly increasing sequence.", 2: "`max_
               3: "more than max_steps integration steps", 4: "Radau stage Newton iteration did not converge",
               5: "sigma_v != 0: the quadrature form needs a linear Y_chi equation"}
 
+# struct lzq_profile_point (40 B): a bounce-profile shape + the couplings of PAPER eqs.(5)-(8)
+PROFILE_POINT_DTYPE = np.dtype([("y_B", "<f8"), ("y_chi", "<f8"), ("lambda_tr_eff", "<f8"), ("v_w", "<f8"),
+                                ("shape", "<i4"), ("reserved", "<i4")])
+assert PROFILE_POINT_DTYPE.itemsize == 40
+PROFILE_COEF = 8  # doubles per knot-interval row: (phi c0..c3, Phi c0..c3)
+
 POINT_DTYPE = np.dtype([(n, "<f8") for n in POINT_DOUBLE_FIELDS] + [(n, "<i4") for n in POINT_INT_FIELDS])
 assert ctypes.sizeof(LzqPoint) == 136 == POINT_DTYPE.itemsize
 assert ctypes.sizeof(LzqYield) == 48
@@ -70,7 +76,8 @@ EXPORTS = ("lzq_abi_version", "lzq_last_error", "lzq_init", "lzq_ztables", "lzq_
            "lzq_jchi_batch", "lzq_yields_batch", "lzq_sweep_grid", "lzq_sweep_grid_reuse_workspace",
            "lzq_sweep_grid_reuse", "lzq_yields_batch_reuse", "lzq_p_closed_form",
            "lzq_lz_propagate", "lzq_lz_propagate_v", "lzq_ode_tables", "lzq_ode_integrate", "lzq_ode_integrate_shared", "lzq_ode_quadrature", "lzq_ode_batch",
-           "lzq_ode_aov_T", "lzq_ode_rhs")
+           "lzq_ode_aov_T", "lzq_ode_rhs", "lzq_profile_splines", "lzq_profile_crossings",
+           "lzq_lz_propagate_profile")
 # the lzq_point fields an ODE spline table depends on (A/V kernel fpy:141-156 + window fpy:368-369)
 ODE_TABLE_KEY = ("I_p", "beta_over_H", "T_p_GeV", "v_w", "g_star", "T_min_over_Tp", "T_max_over_Tp")
 # the lzq_point fields the quadrature's z-sums depend on (its y-grid and c; lzq_yields_batch_reuse)
@@ -126,6 +133,9 @@ def load(path: str | None = None):
     L.lzq_ode_batch.argtypes = [vp, vp, i64, vp, i64, i64, vp, vp, vp]
     L.lzq_ode_aov_T.argtypes = [P(LzqPoint), d, d, vp, vp, i64, vp, vp]
     L.lzq_ode_rhs.argtypes = [P(LzqPoint), P(LzqOdeParams), d, d, vp, vp, vp, i64, vp, vp]
+    L.lzq_profile_splines.argtypes = [vp, vp, vp, i32, i32, vp, vp, vp]
+    L.lzq_profile_crossings.argtypes = [vp, vp, i32, i32, vp, i64, i32, vp, vp, vp, vp, vp, vp]
+    L.lzq_lz_propagate_profile.argtypes = [vp, vp, i32, i32, vp, i64, d, i32, vp, vp]
     for name in EXPORTS:
         if name not in ("lzq_abi_version", "lzq_last_error"):
             getattr(L, name).restype = ctypes.c_int

@@ -14,8 +14,8 @@ CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.normpath(os.path.join(HERE, "..", "include"))
 BUILD_DIR = os.path.join(HERE, "_build")
 LIB_PATH = os.path.join(BUILD_DIR, "liblzq.so")
-SOURCES = ["lzq_kernels.hip", "lzq_propagator.hip", "lzq_ode.hip"]
-HEADERS = ["lzq_exp2.h", "lzq_physics.h", "lzq_internal.h"]
+SOURCES = ["lzq_kernels.hip", "lzq_propagator.hip", "lzq_ode.hip", "lzq_profile.hip"]
+HEADERS = ["lzq_exp2.h", "lzq_physics.h", "lzq_internal.h", "lzq_su2.h"]
 ARCH = os.environ.get("LZQ_OFFLOAD_ARCH", "gfx950")
 # -ffp-contract=off: every a*b+c rounds twice exactly like numpy; fused ops are explicit
 # __builtin_fma in the hot loops.

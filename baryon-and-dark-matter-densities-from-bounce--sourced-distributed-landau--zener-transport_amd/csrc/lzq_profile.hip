@@ -1,0 +1,463 @@
+// lzq_profile.hip -- the bounce-profile LZ path (PAPER p.3 §3, eqs.(5)-(9); the reference's
+// plug-in hook fpy:170-187 imports the absent `transport_from_profile` for it, fpy:173).
+//
+// A profile SHAPE is the bounce solution's two background fields phi(xi), Phi(xi) sampled on
+// knots xi_0 < ... < xi_{K-1} (xi = r - R_0, PAPER §3.1), "interpolated as smooth functions":
+// here not-a-knot cubic splines, the interpolant scipy's CubicSpline builds and fpy:212 uses
+// for its own tables.  A POINT is a shape plus the couplings of eqs.(5)-(8):
+//   Delta(xi) = y_B phi(xi) - y_chi Phi(xi)      eq.(5)   crossings xi*: Delta(xi*) = 0
+//   Delta'*   = y_B phi'(xi*) - y_chi Phi'(xi*)  eq.(6)
+//   m_mix(xi) = lambda_tr_eff phi(xi)            eq.(7)
+//   delta_LZ  = m_mix(xi*)^2 / (2 v_w |Delta'*|) eq.(8), F(k) = 1;  P = 1 - exp(-2 pi delta) eq.(9)
+//
+// Kernels (one lane per point or per spline; every lane computes from its own inputs, so the
+// results do not depend on launch geometry or batch composition):
+//  * profile_spline_kernel   -- the two not-a-knot splines of a shape (scipy's banded system,
+//                               Thomas elimination), coefficients [shape][interval][8] =
+//                               (phi c0..c3, Phi c0..c3), ascending powers of t = xi - xi_j;
+//  * profile_crossings_kernel-- eqs.(5)-(8): every sign change of the cubic Delta on every knot
+//                               interval (split at its stationary points into monotone pieces,
+//                               each root by safeguarded Newton to full precision);
+//  * profile_propagate_kernel-- the time-ordered propagation i dpsi/dt = H psi,
+//                               H = Delta(xi) sigma_z + m_mix(xi) sigma_x, xi = v_w t, through the
+//                               whole profile [xi_0, xi_{K-1}], started in and projected on the
+//                               chi-like second-order dressed state at the two ends (several
+//                               crossings interfere coherently; for one linear crossing in a wide
+//                               window this is eq.(9)).  Sixth-order Magnus: three Gauss-Legendre
+//                               nodes per step, the Blanes-Casas-Ros commutator form, exact SU(2)
+//                               exponential; on knot interval j, S_j = max(min_steps,
+//                               ceil(steps_per_radian * (len_j / v_w) * omega_j)) uniform steps,
+//                               omega_j = the largest of E = sqrt(Delta^2 + m^2) and
+//                               4 sqrt(|dH/dt|) (4 / the LZ time) at 5 points of the interval.  The shape's knots and
+//                               coefficients are staged in LDS once per block (lanes whose point
+//                               has another shape read them from HBM through the same pointer);
+//                               a lane keeps its interval's Delta and m coefficients, the state
+//                               and the step in registers.
+// tests/profile_ref.py restates all three in numpy; tests/test_gpu_profile.py checks them.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+
+#include "../../include/lzq.h"
+#include "lzq_su2.h"
+
+int lzq_set_error(int code, const char* msg);
+
+namespace lzq {
+
+constexpr int kProfBlock = 256;
+#ifndef LZQ_PROF_LDS_KNOTS
+#define LZQ_PROF_LDS_KNOTS 512  // shapes up to this many knots are staged in LDS (36.9 KB per block)
+#endif
+#ifndef LZQ_PROF_MIN_WAVES
+#define LZQ_PROF_MIN_WAVES 2
+#endif
+constexpr double kMaxIntervalSteps = 16777216.0;  // per knot interval; beyond: P = NaN (absurd input)
+constexpr int kProfCoef = 8;                      // doubles per interval row
+constexpr double kHdotRate = 4.0;  // crossing-region rate: kHdotRate / (LZ time), LZ time = |dH/dt|^-1/2
+
+struct ProfPt {
+  double yB, ychi, lam, vw;
+  int32_t shape;
+};
+
+__device__ __forceinline__ ProfPt load_point(const lzq_profile_point* p) {
+  return {p->y_B, p->y_chi, p->lambda_tr_eff, p->v_w, p->shape};
+}
+
+// c0 + t (c1 + t (c2 + t c3)) and derivatives (numpy order of operations, no contraction)
+__device__ __forceinline__ double pp0(const double* c, double t) { return c[0] + t * (c[1] + t * (c[2] + t * c[3])); }
+__device__ __forceinline__ double pp1(const double* c, double t) { return c[1] + t * (2.0 * c[2] + t * 3.0 * c[3]); }
+__device__ __forceinline__ double pp2(const double* c, double t) { return 2.0 * c[2] + 6.0 * c[3] * t; }
+
+// Delta (eq.5) and m_mix (eq.7) coefficients of interval j of the point's shape
+__device__ __forceinline__ void interval_coefs(const double* __restrict__ row, const ProfPt& p, double* cD,
+                                               double* cM) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const double a = row[k], b = row[4 + k];
+    cD[k] = p.yB * a - p.ychi * b;
+    cM[k] = p.lam * a;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Splines: scipy.interpolate.CubicSpline(x, y) (bc_type='not-a-knot', n >= 4): the slope
+// system of scipy/_cubic.py by Thomas elimination (scipy: banded LU; equal to rounding), then
+// c0 = y_j, c1 = s_j, c2 = (slope_j - s_j)/dx_j - t, c3 = t/dx_j, t = (s_j + s_{j+1} - 2 slope_j)/dx_j.
+// One lane per (shape, field); the forward sweep parks (c', d') in the row's c2/c3 slots.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kProfBlock) void profile_spline_kernel(const double* __restrict__ knots,
+                                                                    const double* __restrict__ phi,
+                                                                    const double* __restrict__ Phi, int32_t n_shapes,
+                                                                    int32_t K, double* __restrict__ coef,
+                                                                    int32_t* __restrict__ bad) {
+  const int64_t lane = (int64_t)blockIdx.x * kProfBlock + threadIdx.x;
+  if (lane >= 2 * (int64_t)n_shapes) return;
+  const int64_t s = lane >> 1;
+  const int f = (int)(lane & 1);  // 0: phi, 1: Phi
+  const double* x = knots + s * K;
+  const double* y = (f ? Phi : phi) + s * K;
+  double* w = coef + s * (int64_t)(K - 1) * kProfCoef + 4 * f;  // row j: w[j * 8 + 0..3]
+  for (int j = 0; j + 1 < K; ++j)
+    if (!(x[j + 1] > x[j])) {  // CubicSpline: "x must be strictly increasing"
+      if (f == 0) bad[s] = 1;
+      return;
+    }
+  auto DX = [&](int j) { return x[j + 1] - x[j]; };
+  auto SL = [&](int j) { return (y[j + 1] - y[j]) / DX(j); };
+  // row 0 (not-a-knot): dx1 s0 + (x2 - x0) s1 = ((dx0 + 2d) dx1 sl0 + dx0^2 sl1) / d
+  double dxm1 = DX(0), slm1 = SL(0), cp, dp;
+  {
+    const double dx1 = DX(1), sl1 = SL(1), d = x[2] - x[0];
+    const double r = ((dxm1 + 2.0 * d) * dx1 * slm1 + (dxm1 * dxm1) * sl1) / d;
+    cp = d / dx1;
+    dp = r / dx1;
+    w[2] = cp;
+    w[3] = dp;
+  }
+  // rows 1..K-2: dx_k s_{k-1} + 2 (dx_{k-1} + dx_k) s_k + dx_{k-1} s_{k+1} = 3 (dx_k sl_{k-1} + dx_{k-1} sl_k)
+  for (int k = 1; k < K - 1; ++k) {
+    const double dxk = DX(k), slk = SL(k);
+    const double a = dxk, b = 2.0 * (dxm1 + dxk), c = dxm1;
+    const double r = 3.0 * (dxk * slm1 + dxm1 * slk);
+    const double den = b - a * cp;
+    cp = c / den;
+    dp = (r - a * dp) / den;
+    w[k * kProfCoef + 2] = cp;
+    w[k * kProfCoef + 3] = dp;
+    dxm1 = dxk;
+    slm1 = slk;
+  }
+  // last row (not-a-knot): (x[-1] - x[-3]) s[-2] + dx[-2] s[-1] = b[-1]
+  double s_next;
+  {
+    const double dx2 = DX(K - 3), sl2 = SL(K - 3), d = x[K - 1] - x[K - 3];
+    const double r = ((dxm1 * dxm1) * sl2 + (2.0 * d + dxm1) * dx2 * slm1) / d;
+    s_next = (r - d * dp) / (dx2 - d * cp);
+  }
+  for (int k = K - 2; k >= 0; --k) {
+    double* rk = w + (int64_t)k * kProfCoef;
+    const double sk = rk[3] - rk[2] * s_next;
+    const double dxk = DX(k), slk = SL(k);
+    const double t = (sk + s_next - 2.0 * slk) / dxk;
+    rk[0] = y[k];
+    rk[1] = sk;
+    rk[2] = (slk - sk) / dxk - t;
+    rk[3] = t / dxk;
+    s_next = sk;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Crossings, eqs.(5)-(8)
+// ---------------------------------------------------------------------------------------
+// root of the cubic c on [a, b], where it is monotone and changes sign: secant start, Newton
+// steps kept inside the shrinking bracket (bisection otherwise), to full precision
+__device__ double cubic_root(const double* c, double a, double b) {
+  const double fa = pp0(c, a);
+  double lo = a, hi = b;
+  double x = a - fa * (b - a) / (pp0(c, b) - fa);
+  for (int it = 0; it < 100; ++it) {
+    const double f = pp0(c, x);
+    if (f == 0.0) return x;
+    if ((f < 0.0) == (fa < 0.0))
+      lo = x;
+    else
+      hi = x;
+    const double d = pp1(c, x);
+    double xn = d != 0.0 ? x - f / d : 0.5 * (lo + hi);
+    if (!(lo < xn && xn < hi)) xn = 0.5 * (lo + hi);
+    if (xn == x || hi - lo <= 4e-16 * fmax(fmax(fabs(lo), fabs(hi)), 1e-300)) return xn;
+    x = xn;
+  }
+  return x;
+}
+
+__global__ __launch_bounds__(kProfBlock) void profile_crossings_kernel(
+    const double* __restrict__ knots, const double* __restrict__ coef, int32_t n_shapes, int32_t K,
+    const lzq_profile_point* __restrict__ pts, int64_t n, int32_t max_cross, double* __restrict__ o_xi, double* __restrict__ o_dp, double* __restrict__ o_m,
+    double* __restrict__ o_delta, int32_t* __restrict__ o_count) {
+  const int64_t i = (int64_t)blockIdx.x * kProfBlock + threadIdx.x;
+  if (i >= n) return;
+  const ProfPt p = load_point(pts + i);
+  if (p.shape < 0 || p.shape >= n_shapes) {  // bad shape index: no crossings, count -1
+    o_count[i] = -1;
+    return;
+  }
+  const double* x = knots + (int64_t)p.shape * K;
+  const double* cf = coef + (int64_t)p.shape * (K - 1) * kProfCoef;
+  const double vw = fmax(p.vw, 1e-12);
+  int32_t cnt = 0;
+  double last = 0.0;            // sign of the last nonzero boundary value (0: none yet)
+  int pj = -1;                  // a boundary zero awaiting the next sign: interval pj, local pt
+  double pt = 0.0;
+  double cD[4], cM[4];
+  auto emit = [&](int j, double t) {
+    if (cnt < max_cross) {
+      double rD[4], rM[4];  // the interval's Delta / m_mix rows (j may be a pending earlier one)
+      interval_coefs(cf + (int64_t)j * kProfCoef, p, rD, rM);
+      const double dprime = pp1(rD, t), m = pp0(rM, t);
+      const int64_t o = i * max_cross + cnt;
+      o_xi[o] = x[j] + t;
+      o_dp[o] = dprime;
+      o_m[o] = m;
+      o_delta[o] = m * m / (2.0 * vw * fabs(dprime));
+    }
+    ++cnt;
+  };
+  // a zero exactly on a piece boundary is a crossing when the last nonzero value before it and
+  // the first after it differ in sign (tests/profile_ref.py crossings)
+  auto boundary = [&](double v, int j, double t) {
+    if (v == 0.0) {
+      if (pj < 0 && last != 0.0) {
+        pj = j;
+        pt = t;
+      }
+      return;
+    }
+    const double sg = v > 0.0 ? 1.0 : -1.0;
+    if (pj >= 0 && sg != last) emit(pj, pt);
+    pj = -1;
+    last = sg;
+  };
+  for (int j = 0; j + 1 < K; ++j) {
+    interval_coefs(cf + (int64_t)j * kProfCoef, p, cD, cM);
+    const double L = x[j + 1] - x[j];
+    // monotone pieces: cut at the stationary points of the cubic inside (0, L)
+    double cuts[4];
+    int nc = 0;
+    cuts[nc++] = 0.0;
+    const double A = 3.0 * cD[3], B = 2.0 * cD[2], C = cD[1];
+    if (A != 0.0) {
+      const double disc = B * B - 4.0 * A * C;
+      if (disc > 0.0) {
+        const double sq = sqrt(disc);
+        const double q = -0.5 * (B + copysign(sq, B));
+        double r1 = q / A, r2 = C / q;
+        if (r2 < r1) {
+          const double tt = r1;
+          r1 = r2;
+          r2 = tt;
+        }
+        if (0.0 < r1 && r1 < L) cuts[nc++] = r1;
+        if (0.0 < r2 && r2 < L) cuts[nc++] = r2;
+      }
+    } else if (B != 0.0) {
+      const double r = -C / B;
+      if (0.0 < r && r < L) cuts[nc++] = r;
+    }
+    cuts[nc++] = L;
+    for (int k = 0; k + 1 < nc; ++k) {
+      const double a = cuts[k], b = cuts[k + 1];
+      const double fa = pp0(cD, a), fb = pp0(cD, b);
+      boundary(fa, j, a);
+      if (fa * fb < 0.0) emit(j, cubic_root(cD, a, b));
+      boundary(fb, j, b);
+    }
+  }
+  o_count[i] = cnt;
+}
+
+// ---------------------------------------------------------------------------------------
+// Propagation through the profile
+// ---------------------------------------------------------------------------------------
+// chi-like second-order dressed state of H = D sz + m sx with time derivatives (Dd, Ddd),
+// (md, mdd) (lzq_propagator.hip dressed_basis with m(t) varying; tests/profile_ref.py
+// dressed_chi_like): theta = atan2(m, D)/2, theta' = (m' D - m D')/(2 E^2), eps = theta'/(2E),
+// eps' = theta''/(2E) - theta' E'/(2E^2), beta = -i eps - eps'/(2E).
+__device__ void dressed_chi_like(double D, double Dd, double Ddd, double m, double md, double mdd, Cplx& u0,
+                                 Cplx& u1) {
+  const double E2 = D * D + m * m;
+  const double E = sqrt(E2);
+  const double th = 0.5 * atan2(m, D);
+  double s, c;
+  sincos(th, &s, &c);
+  const double w = md * D - m * Dd;
+  const double thd = w / (2.0 * E2);
+  const double Ed = (D * Dd + m * md) / E;
+  const double thdd = (mdd * D - m * Ddd) / (2.0 * E2) - w * Ed / (E2 * E);
+  const double eps = thd / (2.0 * E);
+  const double epsd = thdd / (2.0 * E) - thd * Ed / (2.0 * E2);
+  const double br = -epsd / (2.0 * E), bi = -eps;
+  const double nrm = 1.0 / sqrt(1.0 + (br * br + bi * bi));
+  const Cplx p0 = {(c - s * br) * nrm, -s * bi * nrm}, p1 = {(s + c * br) * nrm, c * bi * nrm};
+  const bool plus = p0.re * p0.re + p0.im * p0.im >= p1.re * p1.re + p1.im * p1.im;
+  if (plus) {
+    u0 = p0;
+    u1 = p1;
+  } else {
+    u0 = {(-s - c * br) * nrm, c * bi * nrm};
+    u1 = {(c - s * br) * nrm, s * bi * nrm};
+  }
+}
+
+__device__ __forceinline__ void edge_state(const double* cD, const double* cM, double t, double vw, Cplx& u0,
+                                           Cplx& u1) {
+  const double v2 = vw * vw;
+  dressed_chi_like(pp0(cD, t), vw * pp1(cD, t), v2 * pp2(cD, t), pp0(cM, t), vw * pp1(cM, t), v2 * pp2(cM, t), u0,
+                   u1);
+}
+
+// uniform Magnus steps on one interval (tests/profile_ref.py interval_steps, same operations)
+__device__ __forceinline__ double interval_steps(const double* cD, const double* cM, double L, double vw, double spr,
+                                                 int32_t n_min) {
+  double w = 0.0;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const double t = (0.25 * q) * L;
+    const double D = pp0(cD, t), m = pp0(cM, t);
+    const double Dd = pp1(cD, t), md = pp1(cM, t);
+    w = fmax(w, fmax(sqrt(D * D + m * m), kHdotRate * sqrt(vw * sqrt(Dd * Dd + md * md))));
+  }
+  return fmax((double)n_min, ceil(spr * (L / vw) * w));
+}
+
+__global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_propagate_kernel(
+    const double* __restrict__ knots, const double* __restrict__ coef, int32_t n_shapes, int32_t K,
+    const lzq_profile_point* __restrict__ pts, int64_t n, double spr, int32_t n_min, const int32_t* __restrict__ order,
+    double* __restrict__ P_out) {
+  __shared__ double s_knots[LZQ_PROF_LDS_KNOTS];
+  __shared__ double s_coef[(LZQ_PROF_LDS_KNOTS - 1) * kProfCoef];
+  const int64_t tid = (int64_t)blockIdx.x * kProfBlock + threadIdx.x;
+  // stage the shape of the block's first point (block-uniform)
+  const int64_t first = (int64_t)blockIdx.x * kProfBlock;
+  const int32_t s0 = pts[order ? (int64_t)order[first] : first].shape;
+  const bool staged = K <= LZQ_PROF_LDS_KNOTS && s0 >= 0 && s0 < n_shapes;
+  if (staged) {
+    const double* gk = knots + (int64_t)s0 * K;
+    const double* gc = coef + (int64_t)s0 * (K - 1) * kProfCoef;
+    for (int q = threadIdx.x; q < K; q += kProfBlock) s_knots[q] = gk[q];
+    for (int q = threadIdx.x; q < (K - 1) * kProfCoef; q += kProfBlock) s_coef[q] = gc[q];
+  }
+  __syncthreads();
+  if (tid >= n) return;
+  const int64_t i = order ? (int64_t)order[tid] : tid;
+  const ProfPt p = load_point(pts + i);
+  if (!(p.vw > 0.0) || p.shape < 0 || p.shape >= n_shapes) {  // bad wall speed or shape index
+    P_out[i] = __builtin_nan("");
+    return;
+  }
+  const bool mine = staged && p.shape == s0;
+  const double* x = mine ? s_knots : knots + (int64_t)p.shape * K;
+  const double* cf = mine ? s_coef : coef + (int64_t)p.shape * (K - 1) * kProfCoef;
+  const double ivw = 1.0 / p.vw;
+  constexpr double kSq15 = 3.872983346207416885;  // sqrt(15)
+  constexpr double g1 = 0.5 - kSq15 / 10.0, g3 = 0.5 + kSq15 / 10.0;
+
+  double cD[4], cM[4];
+  interval_coefs(cf, p, cD, cM);
+  Cplx p0, p1;
+  edge_state(cD, cM, 0.0, p.vw, p0, p1);
+  double L = 0.0;
+  for (int j = 0; j + 1 < K; ++j) {
+    if (j > 0) interval_coefs(cf + j * kProfCoef, p, cD, cM);
+    L = x[j + 1] - x[j];
+    const double Sd = interval_steps(cD, cM, L, p.vw, spr, n_min);
+    if (!(Sd <= kMaxIntervalSteps)) {  // non-finite or absurd input
+      P_out[i] = __builtin_nan("");
+      return;
+    }
+    const int S = (int)Sd;
+    const double h = L / Sd;
+    const double dt = h * ivw;
+    const double k2 = (kSq15 / 3.0) * dt, k3 = (10.0 / 3.0) * dt;
+    const double gh1 = g1 * h, gh2 = 0.5 * h, gh3 = g3 * h;
+#define FMA __builtin_fma
+#pragma unroll 2
+    for (int st = 0; st < S; ++st) {
+      const double t0 = (double)st * h;
+      const double t1 = t0 + gh1, t2 = t0 + gh2, t3 = t0 + gh3;
+      // H at the three Gauss nodes: (x, z) = (m, Delta)
+      const double X1 = FMA(FMA(FMA(cM[3], t1, cM[2]), t1, cM[1]), t1, cM[0]);
+      const double X2 = FMA(FMA(FMA(cM[3], t2, cM[2]), t2, cM[1]), t2, cM[0]);
+      const double X3 = FMA(FMA(FMA(cM[3], t3, cM[2]), t3, cM[1]), t3, cM[0]);
+      const double Z1 = FMA(FMA(FMA(cD[3], t1, cD[2]), t1, cD[1]), t1, cD[0]);
+      const double Z2 = FMA(FMA(FMA(cD[3], t2, cD[2]), t2, cD[1]), t2, cD[0]);
+      const double Z3 = FMA(FMA(FMA(cD[3], t3, cD[2]), t3, cD[1]), t3, cD[0]);
+      // alpha1 = dt A2, alpha2 = sqrt15/3 dt (A3 - A1), alpha3 = 10/3 dt (A3 - 2 A2 + A1)
+      const double x1 = dt * X2, z1 = dt * Z2;
+      const double x2 = k2 * (X3 - X1), z2 = k2 * (Z3 - Z1);
+      const double x3 = k3 * FMA(-2.0, X2, X1 + X3), z3 = k3 * FMA(-2.0, Z2, Z1 + Z3);
+      // Lie bracket of -i a.sigma, -i b.sigma is -i (2 a x b).sigma; the alphas lie in the x-z plane
+      const double c = 2.0 * FMA(z1, x2, -(x1 * z2));                 // C1 = [alpha1, alpha2]  (y only)
+      const double C2x = z1 * c * (1.0 / 30.0);                         // C2 = -[alpha1, 2 alpha3 + C1]/60
+      const double C2y = FMA(x1, z3, -(z1 * x3)) * (1.0 / 15.0);
+      const double C2z = -(x1 * c) * (1.0 / 30.0);
+      const double Lx = FMA(-20.0, x1, -x3), Lz = FMA(-20.0, z1, -z3);  // -20 alpha1 - alpha3 + C1
+      const double Rx = x2 + C2x, Rz = z2 + C2z;                        // alpha2 + C2  (Ry = C2y)
+      const double nx = FMA(FMA(c, Rz, -(Lz * C2y)), 1.0 / 120.0, FMA(x3, 1.0 / 12.0, x1));
+      const double ny = FMA(Lz, Rx, -(Lx * Rz)) * (1.0 / 120.0);
+      const double nz = FMA(FMA(Lx, C2y, -(c * Rx)), 1.0 / 120.0, FMA(z3, 1.0 / 12.0, z1));
+      double cs, sc;
+      cos_sinc(FMA(nx, nx, FMA(ny, ny, nz * nz)), cs, sc);
+      su2_apply(cs, sc * nx, sc * ny, sc * nz, p0, p1);
+    }
+#undef FMA
+  }
+  Cplx u0, u1;
+  edge_state(cD, cM, L, p.vw, u0, u1);
+  const Cplx a = inner(u0, u1, p0, p1);
+  const double norm = p0.re * p0.re + p0.im * p0.im + p1.re * p1.re + p1.im * p1.im;
+  P_out[i] = 1.0 - (a.re * a.re + a.im * a.im) / norm;
+}
+
+}  // namespace lzq
+
+namespace {
+bool shape_args_ok(const double* knots, const double* coef, int32_t n_shapes, int32_t K) {
+  return knots && coef && n_shapes > 0 && K >= 4;
+}
+}  // namespace
+
+extern "C" int lzq_profile_splines(const double* d_knots, const double* d_phi, const double* d_Phi, int32_t n_shapes,
+                                   int32_t n_knots, double* d_coef, int32_t* d_bad, void* stream) {
+  if (!d_knots || !d_phi || !d_Phi || !d_coef || !d_bad || n_shapes <= 0 || n_knots < 4)
+    return lzq_set_error(LZQ_EINVAL, "lzq_profile_splines: bad arguments (need n_shapes > 0, n_knots >= 4, "
+                                     "non-null buffers)");
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t e = hipMemsetAsync(d_bad, 0, sizeof(int32_t) * (size_t)n_shapes, st);
+  if (e != hipSuccess) return lzq_set_error(LZQ_EHIP, hipGetErrorString(e));
+  const int64_t lanes = 2 * (int64_t)n_shapes;
+  hipLaunchKernelGGL(lzq::profile_spline_kernel, dim3((unsigned)((lanes + lzq::kProfBlock - 1) / lzq::kProfBlock)),
+                     dim3(lzq::kProfBlock), 0, st, d_knots, d_phi, d_Phi, n_shapes, n_knots, d_coef, d_bad);
+  e = hipGetLastError();
+  if (e != hipSuccess) return lzq_set_error(LZQ_EHIP, hipGetErrorString(e));
+  return LZQ_OK;
+}
+
+extern "C" int lzq_profile_crossings(const double* d_knots, const double* d_coef, int32_t n_shapes, int32_t n_knots,
+                                     const lzq_profile_point* d_points, int64_t n, int32_t max_cross, double* d_xi,
+                                     double* d_dprime, double* d_m_mix, double* d_delta, int32_t* d_count,
+                                     void* stream) {
+  if (!shape_args_ok(d_knots, d_coef, n_shapes, n_knots) || n < 0 || max_cross < 0 ||
+      (n > 0 && (!d_points || !d_count || (max_cross > 0 && (!d_xi || !d_dprime || !d_m_mix || !d_delta)))))
+    return lzq_set_error(LZQ_EINVAL, "lzq_profile_crossings: bad arguments (need n_shapes > 0, n_knots >= 4, "
+                                     "n >= 0, max_cross >= 0, non-null buffers)");
+  if (n == 0) return LZQ_OK;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(lzq::profile_crossings_kernel, dim3((unsigned)((n + lzq::kProfBlock - 1) / lzq::kProfBlock)),
+                     dim3(lzq::kProfBlock), 0, st, d_knots, d_coef, n_shapes, n_knots, d_points, n, max_cross, d_xi, d_dprime,
+                     d_m_mix, d_delta, d_count);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return lzq_set_error(LZQ_EHIP, hipGetErrorString(e));
+  return LZQ_OK;
+}
+
+extern "C" int lzq_lz_propagate_profile(const double* d_knots, const double* d_coef, int32_t n_shapes,
+                                        int32_t n_knots, const lzq_profile_point* d_points, int64_t n,
+                                        double steps_per_radian, int32_t min_steps, double* d_P, void* stream) {
+  if (!shape_args_ok(d_knots, d_coef, n_shapes, n_knots) || n < 0 || !(steps_per_radian >= 0.5) ||
+      !(steps_per_radian <= 1000.0) || min_steps < 1 || min_steps > 1000000 || (n > 0 && (!d_points || !d_P)))
+    return lzq_set_error(LZQ_EINVAL, "lzq_lz_propagate_profile: bad arguments (need n_shapes > 0, n_knots >= 4, "
+                                     "n >= 0, 0.5 <= steps_per_radian <= 1000, 1 <= min_steps <= 1e6)");
+  if (n == 0) return LZQ_OK;
+  if (n > 2147483647LL) return lzq_set_error(LZQ_EINVAL, "lzq_lz_propagate_profile: n too large");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(lzq::profile_propagate_kernel, dim3((unsigned)((n + lzq::kProfBlock - 1) / lzq::kProfBlock)),
+                     dim3(lzq::kProfBlock), 0, st, d_knots, d_coef, n_shapes, n_knots, d_points, n, steps_per_radian, min_steps,
+                     (const int32_t*)nullptr, d_P);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return lzq_set_error(LZQ_EHIP, hipGetErrorString(e));
+  return LZQ_OK;
+}

@@ -52,6 +52,7 @@
 #include <math.h>
 
 #include "../../include/lzq.h"
+#include "lzq_su2.h"
 
 namespace lzq {
 
@@ -71,10 +72,6 @@ constexpr double kMaxCellSteps = 16777216.0;         // per-cell Magnus steps be
 __device__ __forceinline__ double wkb_G(double x, double m) {
   return 0.5 * (x * sqrt(x * x + m * m) + (m > 0.0 ? m * m * asinh(x / m) : 0.0));
 }
-
-struct Cplx {
-  double re, im;
-};
 
 // LZ length of a crossing in xi: sqrt(v_w/|Delta'|) * max(1, sqrt(delta)).
 __device__ __forceinline__ double lz_length(double m, double a, double v_w) {
@@ -120,12 +117,6 @@ __device__ __forceinline__ void chi_like_dressed(double d, double ddot, double m
   u1 = plus ? b.p1 : b.q1;
 }
 
-// <u|psi> for u = (u0, u1)
-__device__ __forceinline__ Cplx inner(Cplx u0, Cplx u1, Cplx p0, Cplx p1) {
-  return {u0.re * p0.re + u0.im * p0.im + u1.re * p1.re + u1.im * p1.im,
-          u0.re * p0.im - u0.im * p0.re + u1.re * p1.im - u1.im * p1.re};
-}
-
 // T(x0) = int_{|x0|}^inf dx / (x^2 + m^2)^{5/2}: closed form, or its series in u = m^2/x0^2 where
 // the closed form cancels (u < 1e-3; truncation ~u^4).
 __device__ __forceinline__ double tail_T(double x0, double m) {
@@ -138,28 +129,6 @@ __device__ __forceinline__ double tail_T(double x0, double m) {
   const double E = sqrt(x0 * x0 + m * m);
   const double m2 = m * m;
   return (2.0 - x0 * (2.0 * x0 * x0 + 3.0 * m2) / (E * E * E)) / (3.0 * m2 * m2);
-}
-
-// cos(x) and sin(x)/x as even Taylor polynomials in x2 = x^2 for x2 <= 1 (truncation < 1e-17;
-// the Magnus step's rotation angle |n| ~ E dt <= 1 at >= 3 steps per radian), else through
-// sincos.  Replaces sqrt + sincos + a division per step; tests/lz_ref.py uses libm sin/cos.
-__constant__ double kSincC[9] = {0x1.0000000000000p+0, -0x1.5555555555555p-3, 0x1.1111111111111p-7, -0x1.a01a01a01a01ap-13, 0x1.71de3a556c734p-19, -0x1.ae64567f544e4p-26, 0x1.6124613a86d09p-33, -0x1.ae7f3e733b81fp-41, 0x1.952c77030ad4ap-49};
-__constant__ double kCosC[10] = {0x1.0000000000000p+0, -0x1.0000000000000p-1, 0x1.5555555555555p-5, -0x1.6c16c16c16c17p-10, 0x1.a01a01a01a01ap-16, -0x1.27e4fb7789f5cp-22, 0x1.1eed8eff8d898p-29, -0x1.93974a8c07c9dp-37, 0x1.ae7f3e733b81fp-45, -0x1.6827863b97d97p-53};
-__device__ __forceinline__ void cos_sinc(double x2, double& cs, double& sc) {
-  if (x2 <= 1.0) {
-    double ps = kSincC[8], pc = kCosC[9];
-#pragma unroll
-    for (int k = 7; k >= 0; --k) ps = __builtin_fma(ps, x2, kSincC[k]);
-#pragma unroll
-    for (int k = 8; k >= 0; --k) pc = __builtin_fma(pc, x2, kCosC[k]);
-    sc = ps;
-    cs = pc;
-  } else {
-    const double x = sqrt(x2);
-    double sn;
-    sincos(x, &sn, &cs);
-    sc = sn / x;
-  }
 }
 
 // Half-width (in xi) of a Magnus cell's core (tests/lz_ref.py core_halfwidth): 2K LZ lengths
@@ -399,15 +368,7 @@ __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_k
         const double nz = cz * D;
         double cs, sc;  // cos|n| and sin|n|/|n|, both functions of |n|^2
         cos_sinc(FMA(nx, nx, FMA(ny, ny, nz * nz)), cs, sc);
-        const double sx = sc * nx, sy = sc * ny, sz = sc * nz;
-        // U11 = cs - i sz ; U12 = -sy - i sx ; U21 = sy - i sx ; U22 = cs + i sz
-        Cplx q0, q1;
-        q0.re = FMA(cs, p0.re, FMA(sz, p0.im, FMA(-sy, p1.re, sx * p1.im)));
-        q0.im = FMA(cs, p0.im, FMA(-sz, p0.re, FMA(-sy, p1.im, -(sx * p1.re))));
-        q1.re = FMA(sy, p0.re, FMA(sx, p0.im, FMA(cs, p1.re, -(sz * p1.im))));
-        q1.im = FMA(sy, p0.im, FMA(-sx, p0.re, FMA(cs, p1.im, sz * p1.re)));
-        p0 = q0;
-        p1 = q1;
+        su2_apply(cs, sc * nx, sc * ny, sc * nz, p0, p1);
       }
 #undef FMA
       if (cr < right) dressed_follow(p0, p1, mc, ac, slope, xcc, cr, right, v_w);

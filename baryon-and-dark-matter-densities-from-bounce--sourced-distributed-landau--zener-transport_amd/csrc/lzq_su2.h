@@ -1,0 +1,59 @@
+// lzq_su2.h -- two-level (SU(2)) helpers shared by the LZ propagators (lzq_propagator.hip,
+// lzq_profile.hip).  Not ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace lzq {
+
+struct Cplx {
+  double re, im;
+};
+
+// <u|psi> for u = (u0, u1)
+__device__ __forceinline__ Cplx inner(Cplx u0, Cplx u1, Cplx p0, Cplx p1) {
+  return {u0.re * p0.re + u0.im * p0.im + u1.re * p1.re + u1.im * p1.im,
+          u0.re * p0.im - u0.im * p0.re + u1.re * p1.im - u1.im * p1.re};
+}
+
+// cos(x) and sin(x)/x as even Taylor polynomials in x2 = x^2 for x2 <= 1 (truncation < 1e-17;
+// a Magnus step's rotation angle |n| ~ E dt <= 1 at >= 3 steps per radian), else through
+// sincos.  Replaces sqrt + sincos + a division per step; the numpy restatements use libm.
+static __constant__ double kSincC[9] = {0x1.0000000000000p+0,  -0x1.5555555555555p-3, 0x1.1111111111111p-7,
+                                        -0x1.a01a01a01a01ap-13, 0x1.71de3a556c734p-19, -0x1.ae64567f544e4p-26,
+                                        0x1.6124613a86d09p-33,  -0x1.ae7f3e733b81fp-41, 0x1.952c77030ad4ap-49};
+static __constant__ double kCosC[10] = {0x1.0000000000000p+0,  -0x1.0000000000000p-1, 0x1.5555555555555p-5,
+                                        -0x1.6c16c16c16c17p-10, 0x1.a01a01a01a01ap-16, -0x1.27e4fb7789f5cp-22,
+                                        0x1.1eed8eff8d898p-29,  -0x1.93974a8c07c9dp-37, 0x1.ae7f3e733b81fp-45,
+                                        -0x1.6827863b97d97p-53};
+__device__ __forceinline__ void cos_sinc(double x2, double& cs, double& sc) {
+  if (x2 <= 1.0) {
+    double ps = kSincC[8], pc = kCosC[9];
+#pragma unroll
+    for (int k = 7; k >= 0; --k) ps = __builtin_fma(ps, x2, kSincC[k]);
+#pragma unroll
+    for (int k = 8; k >= 0; --k) pc = __builtin_fma(pc, x2, kCosC[k]);
+    sc = ps;
+    cs = pc;
+  } else {
+    const double x = sqrt(x2);
+    double sn;
+    sincos(x, &sn, &cs);
+    sc = sn / x;
+  }
+}
+
+// psi <- exp(-i n.sigma) psi, with cs = cos|n| and (sx, sy, sz) = sin|n|/|n| * n:
+// U11 = cs - i sz ; U12 = -sy - i sx ; U21 = sy - i sx ; U22 = cs + i sz
+__device__ __forceinline__ void su2_apply(double cs, double sx, double sy, double sz, Cplx& p0, Cplx& p1) {
+#define FMA __builtin_fma
+  Cplx q0, q1;
+  q0.re = FMA(cs, p0.re, FMA(sz, p0.im, FMA(-sy, p1.re, sx * p1.im)));
+  q0.im = FMA(cs, p0.im, FMA(-sz, p0.re, FMA(-sy, p1.im, -(sx * p1.re))));
+  q1.re = FMA(sy, p0.re, FMA(sx, p0.im, FMA(cs, p1.re, -(sz * p1.im))));
+  q1.im = FMA(sy, p0.im, FMA(-sx, p0.re, FMA(cs, p1.im, sz * p1.re)));
+#undef FMA
+  p0 = q0;
+  p1 = q1;
+}
+
+}  // namespace lzq

@@ -332,6 +332,71 @@ class Engine:
                                                         self._stream()))
         return out
 
+    # -- bounce profiles (PAPER eqs.(5)-(9); the absent modules of fpy:173) ------------------
+    def profile_shapes(self, knots, phi, Phi) -> "ProfileShapes":
+        """Not-a-knot cubic splines (scipy CubicSpline) of phi(xi), Phi(xi) for n_shapes profiles
+        sampled on their own knots: arrays [n_knots] or [n_shapes, n_knots] (lzq_profile_splines).
+        Raises ValueError for knots that are not strictly increasing, as CubicSpline does."""
+        x = self._f64(knots)
+        x = x.reshape(1, -1) if x.dim() == 1 else x
+        a, b = self._f64(phi).reshape(x.shape), self._f64(Phi).reshape(x.shape)
+        ns, nk = x.shape
+        if nk < 4:
+            raise ValueError("a profile needs at least 4 knots")
+        coef = torch.empty((ns, nk - 1, _native.PROFILE_COEF), dtype=torch.float64, device=self.device)
+        bad = torch.empty(ns, dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            self._check(self.lib.lzq_profile_splines(_vp(x), _vp(a), _vp(b), ns, nk, _vp(coef), _vp(bad),
+                                                     self._stream()))
+        nbad = int(bad.sum().item())
+        if nbad:
+            raise ValueError(f"{nbad} profile(s) with knots that are not strictly increasing")
+        return ProfileShapes(x, coef)
+
+    def profile_points(self, y_B, y_chi, lambda_tr_eff, v_w, shape=0) -> torch.Tensor:
+        """lzq_profile_point records (broadcast arrays) -> device byte tensor [n * 40]."""
+        cols = np.broadcast_arrays(*(np.asarray(v, dtype=np.float64) for v in (y_B, y_chi, lambda_tr_eff, v_w)),
+                                   np.asarray(shape, dtype=np.int32))
+        rec = np.zeros(cols[0].size, dtype=_native.PROFILE_POINT_DTYPE)
+        for name, c in zip(("y_B", "y_chi", "lambda_tr_eff", "v_w", "shape"), cols):
+            rec[name] = c.reshape(-1)
+        return torch.from_numpy(rec.view(np.uint8).copy()).to(self.device)
+
+    def profile_crossings(self, shapes: "ProfileShapes", points: torch.Tensor, max_cross: int = 8) -> dict:
+        """eqs.(5)-(8) per point: {'xi', 'dprime', 'm_mix', 'delta_lz'} [n, max_cross] and
+        'count' [n] (lzq_profile_crossings; entries past count are unspecified)."""
+        n = points.numel() // _native.PROFILE_POINT_DTYPE.itemsize
+        out = {k: torch.empty((n, max_cross), dtype=torch.float64, device=self.device)
+               for k in ("xi", "dprime", "m_mix", "delta_lz")}
+        out["count"] = torch.empty(n, dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            self._check(self.lib.lzq_profile_crossings(
+                _vp(shapes.knots), _vp(shapes.coef), shapes.n_shapes, shapes.n_knots, _vp(points), n, int(max_cross),
+                _vp(out["xi"]), _vp(out["dprime"]), _vp(out["m_mix"]), _vp(out["delta_lz"]), _vp(out["count"]),
+                self._stream()))
+        return out
+
+    def lz_propagate_profile(self, shapes: "ProfileShapes", points: torch.Tensor, steps_per_radian: float = 3.0,
+                             min_steps: int = 8) -> torch.Tensor:
+        """Coherent conversion probability through each point's whole profile
+        (lzq_lz_propagate_profile)."""
+        n = points.numel() // _native.PROFILE_POINT_DTYPE.itemsize
+        out = torch.empty(n, dtype=torch.float64, device=self.device)
+        with torch.cuda.device(self.device):
+            self._check(self.lib.lzq_lz_propagate_profile(
+                _vp(shapes.knots), _vp(shapes.coef), shapes.n_shapes, shapes.n_knots, _vp(points), n,
+                float(steps_per_radian), int(min_steps), _vp(out), self._stream()))
+        return out
+
+
+class ProfileShapes:
+    """Device knots [n_shapes, n_knots] and spline rows [n_shapes, n_knots - 1, 8] of bounce
+    profiles (include/lzq.h lzq_profile_splines)."""
+
+    def __init__(self, knots: torch.Tensor, coef: torch.Tensor):
+        self.knots, self.coef = knots.contiguous(), coef.contiguous()
+        self.n_shapes, self.n_knots = int(knots.shape[0]), int(knots.shape[1])
+
 
 _MIX = -7046029254386353131  # 0x9E3779B97F4A7C15 as int64 (torch multiplies wrap)
 REUSE_MAX_BYTES = 16 << 30     # Engine.sweep(reuse=True): z-sum tables beyond this run dense

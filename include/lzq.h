@@ -297,6 +297,58 @@ int lzq_lz_propagate_v(const double* d_m_mix, const double* d_dprime, const doub
                        int64_t n, int32_t n_cross, double window_lz, int32_t steps_per_crossing, double* d_P,
                        void* stream);
 
+/* ---- bounce-profile LZ path (PAPER p.3 §3 eqs.(5)-(9); the absent modules of fpy:173) ---- */
+/* The reference's hook (fpy:170-187) imports `transport_from_profile` and calls
+ * compute_prob_from_profile(csv, v_w) / compute_lambda_eff_from_profile(csv) (fpy:178-184);
+ * that module is absent from the reference, so these entry points implement the paper's
+ * definition of it.  A profile SHAPE is the bounce's two background fields phi(xi), Phi(xi)
+ * on n_knots knots xi_0 < ... < xi_{n_knots-1} (xi = r - R_0), each a not-a-knot cubic spline
+ * (scipy CubicSpline, the interpolant fpy:212 uses).  Coefficient rows: d_coef[shape][j][8] =
+ * (phi c0..c3, Phi c0..c3) with value c0 + c1 t + c2 t^2 + c3 t^3, t = xi - xi_j on
+ * [xi_j, xi_{j+1}].  A POINT is a shape plus the couplings of eqs.(5)-(8):
+ *   Delta = y_B phi - y_chi Phi (eq.5), Delta'* (eq.6), m_mix = lambda_tr_eff phi (eq.7),
+ *   delta_LZ = m_mix(xi*)^2 / (2 v_w |Delta'*|) (eq.8, F = 1), P = 1 - exp(-2 pi delta) (eq.9). */
+typedef struct lzq_profile_point {
+  double y_B;            /* eq.(5) */
+  double y_chi;          /* eq.(5) */
+  double lambda_tr_eff;  /* eq.(7) */
+  double v_w;            /* eq.(8); the propagation's xi = v_w t */
+  int32_t shape;         /* 0 <= shape < n_shapes (else: NaN P / count -1) */
+  int32_t reserved;      /* 0 */
+} lzq_profile_point;     /* 40 bytes */
+
+/* The not-a-knot splines of n_shapes shapes: d_knots/d_phi/d_Phi [n_shapes][n_knots] (device),
+ * n_knots >= 4, into d_coef [n_shapes][n_knots-1][8].  d_bad[n_shapes] (int32): 1 for a shape
+ * whose knots are not strictly increasing (CubicSpline raises ValueError; its rows are not
+ * written), else 0. */
+int lzq_profile_splines(const double* d_knots, const double* d_phi, const double* d_Phi, int32_t n_shapes,
+                        int32_t n_knots, double* d_coef, int32_t* d_bad, void* stream);
+
+/* eqs.(5)-(8) per point: every sign change of Delta in [xi_0, xi_{n_knots-1}) (a cubic per knot
+ * interval, split at its stationary points; each root by safeguarded Newton to full precision).
+ * Up to max_cross crossings per point, in increasing xi, into d_xi / d_dprime (signed Delta'*) /
+ * d_m_mix / d_delta_lz [n][max_cross]; d_count[n] = the number found (which may exceed
+ * max_cross: the rest are not written; -1 for a bad shape index). */
+int lzq_profile_crossings(const double* d_knots, const double* d_coef, int32_t n_shapes, int32_t n_knots,
+                          const lzq_profile_point* d_points, int64_t n, int32_t max_cross, double* d_xi,
+                          double* d_dprime, double* d_m_mix, double* d_delta_lz, int32_t* d_count, void* stream);
+
+/* Time-ordered propagation through the whole profile (beyond the minimal estimator of eq.(8):
+ * the crossings' energy dependence and their interference are kept): i dpsi/dt = H psi,
+ * H = Delta(xi) sigma_z + m_mix(xi) sigma_x, xi = v_w t, from xi_0 to xi_{n_knots-1}.  psi starts
+ * in the chi-like second-order dressed (superadiabatic) state of H at xi_0; d_P[n] =
+ * 1 - |<chi-like dressed state at the far end | psi>|^2.  Sixth-order Magnus (three
+ * Gauss-Legendre nodes, exact SU(2) exponentials), on knot interval j
+ * max(min_steps, ceil(steps_per_radian x duration x max(E, 4 sqrt|dH/dt|))) uniform steps.
+ * 0.5 <= steps_per_radian <= 1000 and 1 <= min_steps <= 1e6 (else LZQ_EINVAL); a point with
+ * v_w <= 0, a bad shape index or more than 2^24 steps in one interval gets P = NaN.  For one
+ * linear crossing in a wide window P -> eq.(9); at steps_per_radian = 3 it is within ~2e-10 of
+ * the exact (Weber) solution of lzq_lz_propagate's piecewise-linear model.
+ * n < 2^31. */
+int lzq_lz_propagate_profile(const double* d_knots, const double* d_coef, int32_t n_shapes, int32_t n_knots,
+                             const lzq_profile_point* d_points, int64_t n, double steps_per_radian,
+                             int32_t min_steps, double* d_P, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

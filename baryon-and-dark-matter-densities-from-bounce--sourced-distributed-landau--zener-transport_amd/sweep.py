@@ -259,6 +259,7 @@ def prepare_out_dir(out_dir: str, spec: SweepSpec, resume: bool, rank: int = 0) 
 
 
 ComputeFn = Callable[[int, int, "object"], None]  # (start, count, out_tensor[count, 6]) -> None
+MAX_INFLIGHT_WRITES = 3   # checkpoint chunks copied out and waiting for the disk (pinned ring of <= 4)
 
 
 def _save_shard(path: str, arr: np.ndarray) -> None:
@@ -275,12 +276,15 @@ def run_local(compute: ComputeFn, start: int, end: int, make_out: Callable[[int]
 
     On the GPU the checkpoint of chunk i is copied out on a side stream (device -> pinned host
     memory, ordered after chunk i's kernels by an event) and written by a worker thread while
-    chunk i+1 computes, so checkpointing does not serialise the sweep.  On CPU tensors (tests)
-    it is written inline."""
+    chunk i+1 computes, so checkpointing does not serialise the sweep.  The pinned buffers are a
+    small ring reused chunk after chunk, and at most MAX_INFLIGHT_WRITES writes wait for the disk
+    (a slow disk throttles the sweep rather than pinning the whole shard).  On CPU tensors
+    (tests) it is written inline."""
     import torch
     local = make_out(end - start)
     on_gpu = bool(getattr(local, "is_cuda", False)) and out_dir is not None
-    pending = []
+    pending = []    # (future, pinned buffer) of the writes in flight, oldest first
+    ring = []       # pinned host buffers free for reuse
     if on_gpu:
         from concurrent.futures import ThreadPoolExecutor
         pool = ThreadPoolExecutor(max_workers=1)
@@ -288,8 +292,9 @@ def run_local(compute: ComputeFn, start: int, end: int, make_out: Callable[[int]
 
     def flush(block: bool):
         while pending and (block or pending[0][0].done()):
-            fut, _ = pending.pop(0)
+            fut, buf = pending.pop(0)
             fut.result()   # re-raise a failed write here
+            ring.append(buf)
 
     try:
         for c0 in range(start, end, chunk):
@@ -313,7 +318,19 @@ def run_local(compute: ComputeFn, start: int, end: int, make_out: Callable[[int]
                 continue
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(local.device))
-            host = torch.empty(view.shape, dtype=view.dtype, pin_memory=True)
+            # at most MAX_INFLIGHT_WRITES chunks wait for the disk: when the disk is slower than the
+            # GPU the sweep waits here instead of pinning the whole shard in host memory
+            flush(block=False)
+            while len(pending) >= MAX_INFLIGHT_WRITES:
+                fut, buf = pending.pop(0)
+                fut.result()
+                ring.append(buf)
+            full = next((b for b in ring if b.shape[0] >= n), None)
+            if full is not None:
+                ring.remove(full)
+            else:
+                full = torch.empty((chunk, 6), dtype=view.dtype, pin_memory=True)
+            host = full[:n]
             with torch.cuda.stream(copy_stream):
                 copy_stream.wait_event(ev)
                 host.copy_(view, non_blocking=True)
@@ -323,7 +340,7 @@ def run_local(compute: ComputeFn, start: int, end: int, make_out: Callable[[int]
             def write(path=path, host=host, done_ev=done_ev):
                 done_ev.synchronize()
                 _save_shard(path, host.numpy())
-            pending.append((pool.submit(write), host))
+            pending.append((pool.submit(write), full))
             flush(block=False)
         if on_gpu:
             flush(block=True)
@@ -339,29 +356,54 @@ def launched_distributed(world: int) -> bool:
     return world > 1 or ("MASTER_ADDR" in os.environ and "MASTER_PORT" in os.environ)
 
 
-def gather_table(local, total: int, rank: int, world: int, group=None):
-    """All-gather the per-rank shards (sizes differ by <= 1) into the full (total, 6) table.
-    With no process group (a plain single-process run) the local shard is the table; under a
-    launcher the collective runs even for one rank, so a 1-rank torchrun exercises RCCL."""
+GATHER_ROWS = 1 << 18   # rows per rank per collective when the shards differ in size
+
+
+def gather_table(local, total: int, rank: int, world: int, group=None, rows_per_round: int = GATHER_ROWS):
+    """All-gather the per-rank shards (sizes differ by <= 1) into the full (total, 6) table on
+    every rank (the one collective of north_star (3); every rank keeps the table, 1.7% of a
+    288-GB HBM at C4, so any rank can post-process the grid without a second collective).
+
+    Equal shards (C4 at W = 2, 4, 8): one all_gather_into_tensor straight into the output --
+    rank-major order IS flat-index order -- with no padding and no concatenation: the transient
+    is nothing beyond the table and the rank's own shard.  Unequal shards: the common m0 rows of
+    every shard in rounds of <= rows_per_round rows per rank (transient world x rows_per_round
+    x 48 B), each round's rank-major block scattered to the shards' places, then one round for
+    the last row of the shards that have m0 + 1.  RCCL moves device tensors over xGMI; gloo (CPU
+    tests, one-GPU rehearsals) stages through host memory.  With no process group (a plain
+    single-process run) the local shard is the table; under a launcher the collective runs even
+    for one rank, so a 1-rank torchrun exercises RCCL."""
     import torch
     import torch.distributed as dist
     if world == 1 and not (dist.is_available() and dist.is_initialized()):
         return local
-    sizes = [shard_range(total, r, world)[1] - shard_range(total, r, world)[0] for r in range(world)]
-    m = max(sizes)
-    if dist.get_backend(group) == "nccl":
-        pad = torch.zeros((m, 6), dtype=local.dtype, device=local.device)
-        pad[:local.shape[0]] = local
-        buf = torch.empty((world * m, 6), dtype=local.dtype, device=local.device)
-        dist.all_gather_into_tensor(buf, pad, group=group)  # RCCL over xGMI
-        parts = [buf[r * m:r * m + sizes[r]] for r in range(world)]
-        return torch.cat(parts)
-    # gloo (CPU tests, one-GPU rehearsals): stage through host memory
-    pad = torch.zeros((m, 6), dtype=local.dtype)
-    pad[:local.shape[0]] = local.cpu()
-    lst = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(lst, pad, group=group)
-    return torch.cat([lst[r][:sizes[r]] for r in range(world)]).to(local.device)
+    rng = [shard_range(total, r, world) for r in range(world)]
+    sizes = [e - s for s, e in rng]
+    nccl = dist.get_backend(group) == "nccl"
+    src = local if nccl else local.cpu()
+    src = src.contiguous()
+    out = torch.empty((total, 6), dtype=local.dtype, device=src.device)
+    if len(set(sizes)) == 1:
+        dist.all_gather_into_tensor(out, src, group=group)
+        return out if nccl else out.to(local.device)
+    m0 = min(sizes)
+    c = max(1, min(rows_per_round, m0))
+    tmp = torch.empty((world * c, 6), dtype=local.dtype, device=src.device)
+    for k in range(0, m0, c):
+        cc = min(c, m0 - k)
+        buf = tmp[:world * cc]
+        dist.all_gather_into_tensor(buf, src[k:k + cc], group=group)
+        for r in range(world):
+            out[rng[r][0] + k:rng[r][0] + k + cc] = buf[r * cc:(r + 1) * cc]
+    last = torch.zeros((1, 6), dtype=local.dtype, device=src.device)
+    if sizes[rank] > m0:
+        last[0] = src[m0]
+    lb = torch.empty((world, 6), dtype=local.dtype, device=src.device)
+    dist.all_gather_into_tensor(lb, last, group=group)
+    for r in range(world):
+        if sizes[r] > m0:
+            out[rng[r][0] + m0] = lb[r]
+    return out if nccl else out.to(local.device)
 
 
 def summarize(table: np.ndarray, spec: SweepSpec, elapsed: Optional[float] = None) -> dict:

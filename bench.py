@@ -14,9 +14,12 @@ all-gathered over RCCL at the end of every step (north_star (3)).
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 Prints one JSON line (rank 0).  `roofline` = the kernel's executed FP64 FLOP (PMC
-instruction mix of profiles/round2) over its HIP-event time in this run, against the 78.6
-TFLOP/s FP64 vector peak; `cpu_baseline` times the C oracle (the CPU restatement, OpenMP) on
-a bounded random sample of the same grid on every CPU of this job, and on one core.
+instruction mix of profiles/round3, used only if that profile's code-object sha256 is the timed
+library's) over its HIP-event time in this run, against the 78.6 TFLOP/s FP64 vector peak, with
+the FP64-pipe and VALU issue fractions beside it; `parity_spot` checks 64 rows of the timed table
+against the C oracle after the timed region; `cpu_baseline` times the C oracle (the CPU
+restatement, OpenMP) on a bounded random sample of the same grid on every CPU of this job, and
+on one core.
 """
 from __future__ import annotations
 
@@ -49,7 +52,7 @@ BASE = {  # /root/reference/yields_config_equal_mass.json
 }
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "round2", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "round3", "pmc_summary.json")
 WAVE_NODES_PER_POINT = 8000 * 1200 // 64
 
 
@@ -59,6 +62,13 @@ def _pmc():
             return json.load(f)
     except (OSError, ValueError):
         return None
+
+
+def timed_code_object() -> str | None:
+    """sha256 of the gfx950 code object holding yields_grid_kernel in the library this process
+    loaded (the one being timed)."""
+    native = importlib.import_module(PKG + "._native")
+    return importlib.import_module(PKG + ".codeobj").kernel_object_sha256(native.LIB_PATH)
 
 
 def roofline(points_per_launch: int, kern_ms: float) -> dict:
@@ -72,6 +82,7 @@ def roofline(points_per_launch: int, kern_ms: float) -> dict:
     cycles each -- the issue rate the peak is defined by -- over the SIMD cycles of this run at
     the profile's clock), and SURVEY §8d's 30-FLOP stock-exp pricing as a secondary figure."""
     d = _pmc()
+    sha = timed_code_object()
     stock = FLOP_PER_POINT * points_per_launch / (kern_ms / 1e3) / 1e12
     out = {"bound": "fp64-valu", "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s", "kernel": "yields_grid_kernel",
            "kernel_ms": kern_ms, "algorithmic_bytes": 48.0 * points_per_launch,
@@ -79,9 +90,17 @@ def roofline(points_per_launch: int, kern_ms: float) -> dict:
                                     "note": "SURVEY §8d prices a node at ROCm exp(double) (27 FLOP) + 3: 30 FLOP/node; "
                                             "the table exponential does the node in ~10 executed FLOP, so this "
                                             "figure exceeds the peak and is NOT a roofline fraction"}}
+    out["code_object_sha256"] = sha
     if d is None or "valu_mix_per_wave_node" not in d:
         out.update(achieved=None, frac=None, traffic=None,
                    note=f"no PMC summary at {os.path.relpath(PMC_SUMMARY, ROOT)}: executed FLOP unknown")
+        return out
+    if d.get("code_object_sha256") != sha:
+        # the counters describe another build of the kernel: no fraction rather than a stale one
+        out.update(achieved=None, frac=None, fp64_pipe_busy_frac=None, traffic=None,
+                   profile_code_object_sha256=d.get("code_object_sha256"),
+                   note=f"stale profile: {os.path.relpath(PMC_SUMMARY, ROOT)} was measured on code object "
+                        f"{d.get('code_object_sha256')}, this run timed {sha}; re-run tools/gpu_profile.sh")
         return out
     mix = d["valu_mix_per_wave_node"]
     flop_wn = 64.0 * (2.0 * mix["fma_f64"] + mix["mul_f64"] + mix["add_f64"])
@@ -90,8 +109,14 @@ def roofline(points_per_launch: int, kern_ms: float) -> dict:
     fp64_wn = mix["fma_f64"] + mix["mul_f64"] + mix["add_f64"]
     ghz = d["clock_ghz"]
     cyc_wn = 1024 * ghz * 1e9 * (kern_ms / 1e3) / (WAVE_NODES_PER_POINT * points_per_launch)
+    other_wn = d["valu_insts_per_wave_node"] - fp64_wn
     out.update({
         "achieved": achieved, "frac": achieved / PEAK_FP64_TFLOPS,
+        # the same run as issue utilisation: every FP64 instruction a full 4-cycle slot (the rate
+        # the peak is defined by), and with the non-FP64 VALU instructions at 2 cycles each
+        "fp64_pipe_busy_frac": 4.0 * fp64_wn / cyc_wn,
+        "valu_issue_busy_frac": (4.0 * fp64_wn + 2.0 * other_wn) / cyc_wn,
+        "profile_code_object_sha256": d["code_object_sha256"],
         "flop_per_point_executed": flop_pt,
         "traffic": d["hbm_bytes_per_point"]["total_upper"] * points_per_launch, "traffic_unit": "bytes/launch",
         # north_star: "achieved HBM GB/s for the grid I/O" -- the path is FP64-bound, so this is small
@@ -106,7 +131,10 @@ def roofline(points_per_launch: int, kern_ms: float) -> dict:
         "note": "frac = executed FP64 FLOP (PMC instruction mix, FMA = 2) / kernel time / FP64 vector peak. "
                 "It is below 1 because MUL/ADD fill a 2-FLOP slot with 1 FLOP and the per-node integer "
                 "table address / exponent insert (and the range clamp) take VALU issue slots "
-                "(DESIGN.md §5.1)"})
+                "(DESIGN.md §5.1). fp64_pipe_busy_frac counts every FP64 instruction as a full slot; "
+                "valu_issue_busy_frac adds the other VALU instructions at 2 cycles: the kernel is at its "
+                "formulation's issue ceiling, so the lever left is instruction count. The counters are "
+                "used only when their profile's code-object hash equals the timed library's"})
     return out
 
 
@@ -146,17 +174,8 @@ def cpu_baseline(axes, n_points_total: int, seconds: float = 12.0) -> dict:
     hc = host_cpus()
     threads = hc["usable"]
     rng = np.random.default_rng(0)
-    m_vals, d_vals = axes[0][1], axes[1][1]
-
     def cfgs(n):
-        idx = rng.integers(0, n_points_total, n)
-        out = []
-        for i in idx:
-            m, d = m_vals[i // len(d_vals)], d_vals[i % len(d_vals)]
-            c = dict(BASE)
-            c["P_chi_to_B"] = O.p_closed_form(m * m / (2.0 * max(c["v_w"], 1e-12) * abs(d)))
-            out.append(c)
-        return out
+        return [grid_config(axes, int(i), O) for i in rng.integers(0, n_points_total, n)]
 
     calib = cfgs(threads)
     t0 = time.perf_counter()
@@ -197,6 +216,32 @@ def cpu_baseline(axes, n_points_total: int, seconds: float = 12.0) -> dict:
                                      "of the build container (SURVEY §6); it cannot travel to the GPU box"}
 
 
+def grid_config(axes, i: int, O) -> dict:
+    """The fpy Config of flat grid index i (last axis fastest), P by eqs.(8)-(9) as on the device."""
+    m_vals, d_vals = axes[0][1], axes[1][1]
+    m, d = m_vals[i // len(d_vals)], d_vals[i % len(d_vals)]
+    c = dict(BASE)
+    c["P_chi_to_B"] = O.p_closed_form(m * m / (2.0 * max(c["v_w"], 1e-12) * abs(d)))
+    return c
+
+
+def parity_spot(axes, start: int, table: torch.Tensor, n: int = 64) -> dict:
+    """Outside the timed region: n default_rng(0)-sampled rows of this rank's timed table against
+    the C oracle (the checker the cpu_baseline leg loads anyway), all 6 fields."""
+    from oracle import oracle as O
+    per = table.shape[0]
+    idx = np.sort(np.random.default_rng(0).choice(per, size=min(n, per), replace=False))
+    tab = table[torch.as_tensor(idx, device=table.device)].cpu().numpy()
+    ref = O.points_batch([grid_config(axes, start + int(i), O) for i in idx], nthreads=host_cpus()["usable"])
+    fields = importlib.import_module(PKG + "._native").YIELD_FIELDS
+    err = np.where(ref != 0.0, np.abs(tab - ref) / np.where(ref != 0.0, np.abs(ref), 1.0), np.abs(tab))
+    worst = float(np.nanmax(err)) if np.isfinite(ref).all() else float("nan")
+    return {"n": int(len(idx)), "worst_rel": worst, "fields": list(fields), "gate": 1e-8, "guard_band": 1e-11,
+            "ok": bool(worst < 1e-11),
+            "sample": f"{len(idx)} rows of the last timed step's table (rank 0 shard), numpy default_rng(0), "
+                      f"vs oracle/lzq_oracle.c (pinned to the reference's golden outputs)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -204,6 +249,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--points", type=int, default=1_000_000, help="points per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity-spot", action="store_true", help="skip the oracle check of 64 timed rows")
     ap.add_argument("--truncated", action="store_true",
                     help="also time one step with exact-underflow truncation (secondary field, not the headline)")
     ap.add_argument("--no-reuse", dest="reuse", action="store_false",
@@ -327,6 +373,7 @@ def main():
     assert bool(torch.isfinite(gathered).all()), "non-finite yields"
     if use_dist:
         assert torch.equal(gathered[start:start + per], local_tab), "all-gather misplaced a shard"
+    spot = parity_spot(axes, start, local_tab) if rank == 0 and not args.no_parity_spot else None
 
     if rank == 0:
         rec = {
@@ -350,6 +397,8 @@ def main():
                                       f"all-gather of 48 B/point yield tables"},
             "roofline": roofline(per, kern_ms),
         }
+        if spot is not None:
+            rec["parity_spot"] = spot
         if trunc is not None:
             rec["truncated"] = trunc
         if reuse is not None:

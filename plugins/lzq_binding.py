@@ -12,6 +12,8 @@ Entry points (each cites the fpy code it replaces):
   yields(cfg, P, T_lo=None, T_hi=None, n_y=8000)          fpy:231-267 + fpy:372-384 + fpy:413-417
   p_closed_form(lams)                                     fpy:183-184
   lz_propagate(m_mix, dprime, xi, v_w, window_lz, steps)  no fpy counterpart (north_star (1))
+  profile_crossings(knots, phi, Phi, y_B, y_chi, lam, v_w)  PAPER eqs.(5)-(8) (the absent modules of fpy:173)
+  lz_propagate_profile(knots, phi, Phi, y_B, y_chi, lam, v_w) time-ordered P through a bounce profile
   install(fpy_module)                                     monkey-patches fpy's BoltzmannSystem
 
 The library is found at $LZQ_LIB, else at <repo>/<package>/_build/liblzq.so next to this
@@ -42,7 +44,12 @@ class lzq_yield(ctypes.Structure):  # include/lzq.h: struct lzq_yield (48 B)
                                                 "P_used")]
 
 
-assert ctypes.sizeof(lzq_point) == 136 and ctypes.sizeof(lzq_yield) == 48
+class lzq_profile_point(ctypes.Structure):  # include/lzq.h: struct lzq_profile_point (40 B)
+    _fields_ = [(n, ctypes.c_double) for n in ("y_B", "y_chi", "lambda_tr_eff", "v_w")] + \
+        [(n, ctypes.c_int32) for n in ("shape", "reserved")]
+
+
+assert ctypes.sizeof(lzq_point) == 136 and ctypes.sizeof(lzq_yield) == 48 and ctypes.sizeof(lzq_profile_point) == 40
 
 _hip = None
 _lzq = None
@@ -66,6 +73,9 @@ def _libs():
         L.lzq_yields_batch.argtypes = [vp, i64, i32, vp, vp, vp, vp, vp]
         L.lzq_p_closed_form.argtypes = [vp, i64, vp, vp]
         L.lzq_lz_propagate.argtypes = [vp, vp, vp, i64, i32, d, d, i32, vp, vp]
+        L.lzq_profile_splines.argtypes = [vp, vp, vp, i32, i32, vp, vp, vp]
+        L.lzq_profile_crossings.argtypes = [vp, vp, i32, i32, vp, i64, i32, vp, vp, vp, vp, vp, vp]
+        L.lzq_lz_propagate_profile.argtypes = [vp, vp, i32, i32, vp, i64, d, i32, vp, vp]
         dev = ctypes.c_int(0)
         _ok(hip.hipGetDevice(ctypes.byref(dev)) == 0, "hipGetDevice failed (no GPU?)")
         _hip = hip
@@ -168,6 +178,69 @@ def lz_propagate(m_mix, dprime, xi, v_w: float, window_lz: float = 20.0, steps: 
     with _Dev(8 * n_cross, m) as d_m, _Dev(8 * n_cross, d) as d_d, _Dev(8 * n_cross, x) as d_x, _Dev(8) as d_P:
         _check(L.lzq_lz_propagate(d_m.p, d_d.p, d_x.p, 1, n_cross, float(v_w), float(window_lz), int(steps),
                                   d_P.p, None))
+        d_P.read(P)
+    return P.value
+
+
+class _Shape:
+    """One bounce profile on the device: knots + the not-a-knot splines of phi, Phi."""
+
+    def __init__(self, knots, phi, Phi):
+        _, L = _libs()
+        n = len(knots)
+        _ok(n >= 4 and len(phi) == n and len(Phi) == n, "a profile needs >= 4 knots and equal-length columns")
+        self.n = n
+        self.x = _Dev(8 * n, _doubles(knots))
+        self.coef = _Dev(8 * 8 * (n - 1))
+        bad = ctypes.c_int32()
+        with _Dev(8 * n, _doubles(phi)) as d_a, _Dev(8 * n, _doubles(Phi)) as d_b, _Dev(4) as d_bad:
+            _check(L.lzq_profile_splines(self.x.p, d_a.p, d_b.p, 1, n, self.coef.p, d_bad.p, None))
+            d_bad.read(bad)
+        if bad.value:
+            self.close()
+            raise ValueError("profile knots must be strictly increasing (scipy CubicSpline rule)")
+
+    def close(self):
+        self.x.__exit__()
+        self.coef.__exit__()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def profile_crossings(knots, phi, Phi, y_B, y_chi, lambda_tr_eff, v_w, max_cross: int = 256) -> list:
+    """PAPER eqs.(5)-(8) on the GPU: [(xi*, Delta'*, m_mix(xi*), delta_LZ)] of every sign change
+    of Delta = y_B phi - y_chi Phi, phi and Phi not-a-knot cubic splines of the samples."""
+    _, L = _libs()
+    pt = lzq_profile_point(y_B, y_chi, lambda_tr_eff, v_w, 0, 0)
+    cnt = ctypes.c_int32()
+    with _Shape(knots, phi, Phi) as sh, _Dev(40, pt) as d_pt, _Dev(4) as d_cnt, \
+            _Dev(8 * max_cross) as d_x, _Dev(8 * max_cross) as d_d, _Dev(8 * max_cross) as d_m, _Dev(8 * max_cross) as d_l:
+        _check(L.lzq_profile_crossings(sh.x.p, sh.coef.p, 1, sh.n, d_pt.p, 1, max_cross, d_x.p, d_d.p, d_m.p, d_l.p,
+                                       d_cnt.p, None))
+        d_cnt.read(cnt)
+        _ok(cnt.value <= max_cross, f"more than {max_cross} crossings")
+        cols = []
+        for dv in (d_x, d_d, d_m, d_l):
+            h = (ctypes.c_double * max_cross)()
+            dv.read(h)
+            cols.append(list(h)[:cnt.value])
+    return list(zip(*cols))
+
+
+def lz_propagate_profile(knots, phi, Phi, y_B, y_chi, lambda_tr_eff, v_w, steps_per_radian: float = 3.0,
+                         min_steps: int = 8) -> float:
+    """Time-ordered conversion probability through the whole bounce profile
+    (lzq_lz_propagate_profile): H = Delta(xi) sz + m_mix(xi) sx, xi = v_w t."""
+    _, L = _libs()
+    pt = lzq_profile_point(y_B, y_chi, lambda_tr_eff, v_w, 0, 0)
+    P = ctypes.c_double()
+    with _Shape(knots, phi, Phi) as sh, _Dev(40, pt) as d_pt, _Dev(8) as d_P:
+        _check(L.lzq_lz_propagate_profile(sh.x.p, sh.coef.p, 1, sh.n, d_pt.p, 1, float(steps_per_radian),
+                                          int(min_steps), d_P.p, None))
         d_P.read(P)
     return P.value
 

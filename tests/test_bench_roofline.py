@@ -1,6 +1,8 @@
 """bench.py's roofline fields are reproducible by hand from the committed rocprofv3 CSVs
-(profiles/round2): executed FP64 FLOP per point from the PMC instruction-mix pass, the
-kernel's average duration from the kernel-trace stats of the bench command itself."""
+(profiles/round3): executed FP64 FLOP per point from the PMC instruction-mix pass, the
+kernel's average duration from the kernel-trace stats of the bench command itself.  The
+counters are used only for the code object they were measured on (its sha256 is in
+pmc_summary.json); any other build gets frac = null and a "stale profile" note."""
 import csv
 import importlib
 import os
@@ -8,7 +10,7 @@ import sys
 
 from conftest import ROOT
 
-PROF = os.path.join(ROOT, "profiles", "round2")
+PROF = os.path.join(ROOT, "profiles", "round3")
 
 
 def counters(path, kernel="yields_grid_kernel"):
@@ -29,6 +31,12 @@ def test_executed_flop_from_committed_csv():
     assert len(stats) == 1 and int(stats[0]["Calls"]) == 25     # bench.py --steps 20 --warmup 5
     kern_ms = float(stats[0]["AverageNs"]) / 1e6
     rf = bench.roofline(1_000_000, kern_ms)
+    import json
+    summ = json.load(open(os.path.join(PROF, "pmc_summary.json")))
+    if rf["code_object_sha256"] != summ["code_object_sha256"]:
+        # the library here is another build of the kernel than the profiled one
+        assert rf["frac"] is None and rf["note"].startswith("stale profile"), rf
+        return
     assert abs(rf["flop_per_point_executed"] / flop_pt - 1) < 1e-12
     frac = flop_pt * 1e6 / (kern_ms / 1e3) / 1e12 / 78.6
     assert abs(rf["frac"] - frac) < 1e-12 and 0.5 < frac < 1.0

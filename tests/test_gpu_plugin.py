@@ -5,8 +5,10 @@
   yields_out.json finals within 1e-11;
 - the shipped plug-in module plugins/transport_from_profile.py picked up by the hook in the
   fpy:173 order: a one-crossing CSV reproduces P = 1 - exp(-2 pi delta) (eq.(9)) to 1e-8, a
-  multi-crossing list gives the propagator's coherent P, a sampled bounce profile
-  (xi, Delta, m_mix) is reduced to its crossings, and the CLI prints the reference's
+  multi-crossing list gives the propagator's coherent P, a sampled profile (xi, Delta, m_mix)
+  is reduced to its spline crossings (estimator = linear) or propagated through (default), the
+  paper's phi/Phi bounce format (eqs.(5)-(8)) reproduces a tanh wall's closed-form delta_LZ,
+  the module's own command line (PAPER App. A) runs, and the CLI prints the reference's
   `[info] Using P_chi_to_B from profile: ...` line byte-exactly for that P;
 - plugins/lzq_binding.py (the reference-side ctypes binding, no torch): the quadrature
   operator on a stand-in with the reference BoltzmannSystem's attributes (self.cfg, self.P,
@@ -101,11 +103,82 @@ def test_shipped_module_multi_crossing_and_profile(tmp_path, plugin_path, gpu_en
     # Delta is continuous at the joins, which are the model's turning points
     assert abs(0.5 * 22.5 - (-0.3) * (22.5 - 60.0)) < 1e-12 and abs(-0.3 * (95.0 - 60.0) - 0.7 * (95.0 - 110.0)) < 1e-12
     mm = np.where(xs < 22.5, 0.05, np.where(xs < 95.0, 0.08, 0.04))
-    (tmp_path / "prof.csv").write_text("xi,Delta,m_mix\n" + "".join(f"{float(a)!r},{float(b)!r},{float(c)!r}\n" for a, b, c in zip(xs, D, mm)))
+    body = "xi,Delta,m_mix\n" + "".join(f"{float(a)!r},{float(b)!r},{float(c)!r}\n" for a, b, c in zip(xs, D, mm))
+    (tmp_path / "prof.csv").write_text(body)
+    (tmp_path / "prof_lin.csv").write_text("# estimator = linear\n" + body)
     xc, mc, dc, _ = tfp.read_profile(str(tmp_path / "prof.csv"))
     assert np.allclose(xc, x, atol=1e-9) and np.allclose(mc, m) and np.allclose(dc, d, rtol=1e-9)
-    P2 = tfp.compute_prob_from_profile(str(tmp_path / "prof.csv"), V_W)
+    # estimator = linear: the crossings (spline roots) through lzq_lz_propagate's model
+    P2 = tfp.compute_prob_from_profile(str(tmp_path / "prof_lin.csv"), V_W)
     assert abs(P2 - P) <= 1e-9
+    # default (several crossings): time-ordered through the profile itself, as the engine does it
+    P3 = tfp.compute_prob_from_profile(str(tmp_path / "prof.csv"), V_W)
+    sh = gpu_engine.profile_shapes(xs, mm, -D)
+    assert P3 == gpu_engine.lz_propagate_profile(sh, gpu_engine.profile_points(0.0, 1.0, 1.0, V_W, 0)).cpu().item()
+    assert 0.0 < P3 < 1.0
+
+
+def _tanh_csv(path, yB, ychi, lam, extra="", header="xi,phi,Phi", shift=0.0, n=8001, span=4.0):
+    xs = np.linspace(-span, span, n)
+    phi, Phi = 0.5 * (1.0 - np.tanh(xs)), 0.65 * (1.0 + np.tanh(xs))
+    lines = [f"# y_B = {yB!r}", f"# y_chi = {ychi!r}", f"# lambda_tr_eff = {lam!r}"] + ([extra] if extra else [])
+    lines.append(header)
+    lines += [f"{float(a + shift)!r},{float(b)!r},{float(c)!r}" for a, b, c in zip(xs, phi, Phi)]
+    path.write_text("\n".join(lines) + "\n")
+
+
+def test_shipped_module_bounce_fields(tmp_path, plugin_path, gpu_engine):
+    """The paper's profile format (PAPER p.3 eqs.(5)-(8)): phi, Phi samples + y_B, y_chi,
+    lambda_tr_eff.  A tanh wall (v = 1, V = 1.3) has its crossing in closed form; lambda_eff is
+    delta_LZ of eq.(8) to <= 1e-10, P the minimal estimator eq.(9); r = xi + R0 with `# R0`
+    gives the same; a missing coupling is an error (parity unpinned against the absent
+    upstream module, PAPER-pinned)."""
+    tfp = importlib.import_module("transport_from_profile")
+    yB, ychi, lam = 1.3, 0.8, 0.1
+    t = (yB - ychi * 1.3) / (yB + ychi * 1.3)
+    dp = (yB + ychi * 1.3) * (1.0 - t * t) / 2.0
+    m = lam * 0.5 * (1.0 - t)
+    delta = m * m / (2 * V_W * dp)
+    _tanh_csv(tmp_path / "wall.csv", yB, ychi, lam, f"# v_w = {V_W!r}")
+    lam_eff = tfp.compute_lambda_eff_from_profile(str(tmp_path / "wall.csv"))
+    assert abs(lam_eff - delta) <= 1e-10 * delta, (lam_eff, delta)
+    P = tfp.compute_prob_from_profile(str(tmp_path / "wall.csv"), V_W)
+    assert P == 1.0 - math.exp(-2.0 * math.pi * lam_eff)            # fpy:183-184 on the GPU
+    _tanh_csv(tmp_path / "wall_r.csv", yB, ychi, lam, "# R0 = 7.25", header="r,phi,Phi", shift=7.25)
+    (x_r,), _, _, _ = tfp.read_profile(str(tmp_path / "wall_r.csv"))
+    assert abs(x_r - math.atanh(t)) <= 1e-10
+    # the whole-profile propagation of the same wall (estimator = propagate) is a different,
+    # finite-wall quantity; for this wide, smooth wall it is close to eq.(9)
+    _tanh_csv(tmp_path / "wall_p.csv", yB, ychi, lam, "# estimator = propagate", n=401, span=12.0)
+    Pp = tfp.compute_prob_from_profile(str(tmp_path / "wall_p.csv"), V_W)
+    assert abs(Pp - P) <= 0.05 * P, (Pp, P)
+    (tmp_path / "nocoupling.csv").write_text("# y_B = 1.0\nxi,phi,Phi\n0,1,0\n1,1,1\n2,1,2\n3,1,3\n")
+    with pytest.raises(ValueError):
+        tfp.compute_prob_from_profile(str(tmp_path / "nocoupling.csv"), V_W)
+
+
+def test_transport_from_profile_command_line(tmp_path, plugin_path, gpu_engine, capsys):
+    """PAPER App. A: python transport_from_profile.py --params transport_params.json."""
+    tfp = importlib.import_module("transport_from_profile")
+    _tanh_csv(tmp_path / "wall.csv", 1.0, 1.0, 0.2, n=401)
+    (tmp_path / "transport_params.json").write_text(json.dumps({"profile_csv": "wall.csv", "v_w": V_W}))
+    assert tfp.main(["--params", str(tmp_path / "transport_params.json"), "--out", str(tmp_path / "P.json")]) == 0
+    out = capsys.readouterr().out
+    res = json.loads((tmp_path / "P.json").read_text())
+    assert out.splitlines()[-1] == f"P_chi_to_B = {res['P_chi_to_B']!r}"
+    assert len(res["crossings"]) == 1
+    assert res["P_chi_to_B"] == tfp.compute_prob_from_profile(str(tmp_path / "wall.csv"), V_W)
+
+
+def test_cli_bounce_fields_info_line(tmp_path, plugin_path, gpu_engine):
+    """lzq's driver with --maybe-compute-P-from-profile on a phi/Phi profile: the reference's
+    `[info] Using P_chi_to_B from profile: {P:.6g}` line (fpy:322) and P_used."""
+    tfp = importlib.import_module("transport_from_profile")
+    _tanh_csv(tmp_path / "bounce.csv", 1.0, 1.0, 0.2, n=401)
+    P = tfp.compute_prob_from_profile(str(tmp_path / "bounce.csv"), 0.30)
+    out = run_cli(["--config", equal_mass_cfg(tmp_path), "--maybe-compute-P-from-profile", "bounce.csv"], tmp_path)
+    assert out.splitlines()[0] == f"[info] Using P_chi_to_B from profile: {P:.6g}"
+    assert json.loads((tmp_path / "yields_out.json").read_text())["inputs"]["P_used"] == P
 
 
 def test_cli_picks_up_shipped_module(tmp_path, plugin_path, gpu_engine):

@@ -1,4 +1,5 @@
-"""Sweep driver host logic on CPU: sharding, gloo all-gather at world_size 2 and 3, chunk
+"""Sweep driver host logic on CPU: sharding, gloo all-gather at world_size 2, 3, 4 and 8 (even and
+uneven shards, the gather's chunked rounds), chunk
 checkpoints and resume, spec decoding.  The per-point compute is replaced by a
 deterministic function of the global flat index, so any sharding / ordering / gather bug
 shows up as a wrong row (the GPU compute itself is covered by tests/test_gpu_*.py)."""
@@ -28,28 +29,32 @@ def free_port():
     return p
 
 
-def _worker(rank, world, port, total, chunk, out_dir, res_path):
+def _worker(rank, world, port, total, chunk, out_dir, res_path, rows_per_round=1 << 18):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sw = pkg("sweep")
     s, e = sw.shard_range(total, rank, world)
     local = sw.run_local(fake_compute, s, e, lambda n: torch.empty((n, 6), dtype=torch.float64), chunk, out_dir)
-    table = sw.gather_table(local, total, rank, world)
-    if rank == 0:
-        np.save(res_path, table.numpy())
+    table = sw.gather_table(local, total, rank, world, rows_per_round=rows_per_round)
+    # every rank holds the whole table
+    np.save(res_path + f".{rank}.npy", table.numpy())
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,total,chunk", [(2, 1001, 97), (3, 20, 4)])
-def test_gloo_gather_matches_single_rank(world, total, chunk):
+@pytest.mark.parametrize("world,total,chunk,rounds", [
+    (2, 1001, 97, 1 << 18), (3, 20, 4, 1 << 18), (3, 2, 1, 1 << 18),      # total < world: empty shards
+    (4, 100_003, 8192, 7_000),         # uneven (25001 / 25000 rows), several gather rounds
+    (8, 100_003, 4096, 1 << 18),       # uneven at the C4 world size
+    (8, 80_000, 4096, 1 << 18)])       # equal shards (C4's case): one direct all_gather_into_tensor
+def test_gloo_gather_matches_single_rank(world, total, chunk, rounds):
     sw = pkg("sweep")
     ref = torch.empty((total, 6), dtype=torch.float64)
     fake_compute(0, total, ref)
     with tempfile.TemporaryDirectory() as d:
-        res = os.path.join(d, "res.npy")
-        mp.spawn(_worker, args=(world, free_port(), total, chunk, d, res), nprocs=world, join=True)
-        got = np.load(res)
-        assert np.array_equal(got, ref.numpy())
+        res = os.path.join(d, "res")
+        mp.spawn(_worker, args=(world, free_port(), total, chunk, d, res, rounds), nprocs=world, join=True)
+        for r in range(world):
+            assert np.array_equal(np.load(res + f".{r}.npy"), ref.numpy()), r
         # every chunk of every shard was checkpointed
         files = sorted(f for f in os.listdir(d) if f.startswith("shard_"))
         covered = sum(int(f.split("_")[2].split(".")[0]) for f in files)

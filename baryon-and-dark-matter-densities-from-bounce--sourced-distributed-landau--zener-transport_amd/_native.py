@@ -45,10 +45,11 @@ ODE_DTYPE = np.dtype([("sigma_v_chi_GeV_m2", "<f8"), ("Gamma_wash_over_H", "<f8"
                       ("deplete_DM_from_source", "<i4"), ("reserved", "<i4")])
 assert ctypes.sizeof(LzqOdeParams) == 24 == ODE_DTYPE.itemsize
 ODE_NT, ODE_WS_PER_POINT = 800, 3200  # LZQ_ODE_NT, LZQ_ODE_WS_PER_POINT
-ODE_OK, ODE_BAD_GRID, ODE_BAD_STEP, ODE_TOO_MANY_STEPS, ODE_NEWTON, ODE_NOT_LINEAR = range(6)  # enum lzq_ode_status
+ODE_OK, ODE_BAD_GRID, ODE_BAD_STEP, ODE_TOO_MANY_STEPS, ODE_NEWTON, ODE_NOT_LINEAR, ODE_UNRESOLVED = range(7)  # enum lzq_ode_status
 ODE_STATUS = {0: "ok", 1: "`x` must be strictly increasing sequence.", 2: "`max_step` must be positive.",
               3: "more than max_steps integration steps", 4: "Radau stage Newton iteration did not converge",
-              5: "sigma_v != 0: the quadrature form needs a linear Y_chi equation"}
+              5: "sigma_v != 0: the quadrature form needs a linear Y_chi equation",
+              6: "quadrature form: a knot interval needs more than 4096 sub-intervals"}
 
 # struct lzq_profile_point (40 B): a bounce-profile shape + the couplings of PAPER eqs.(5)-(8)
 PROFILE_POINT_DTYPE = np.dtype([("y_B", "<f8"), ("y_chi", "<f8"), ("lambda_tr_eff", "<f8"), ("v_w", "<f8"),
@@ -66,7 +67,25 @@ FIELD.update({"delta_LZ": 32, "m_mix": 33, "dprime": 34})
 FERMION, BOSON = 0, 1
 THERMAL, NONTHERMAL, REGIME_OTHER = 0, 1, 2
 LZQ_NZ = 1200
-TUNE_EXP, TUNE_TRUNCATE, TUNE_ODE_COOP = 0, 1, 2  # enum lzq_tune_key
+TUNE_EXP, TUNE_TRUNCATE, TUNE_ODE_COOP, TUNE_ODE_LAUNCH_STEPS = 0, 1, 2, 3  # enum lzq_tune_key
+ODE_MAX_LAUNCHES = 65536  # lzq_ode_*: max_steps <= 65536 x 2^(launch log2)
+# tuning state that changes result bits (the inner-loop exponential, ~1e-14): part of the
+# sweep checkpoint key (sweep.spec_key); Engine.tune_exp keeps it current
+TUNE_STATE = {"exp": "table"}
+
+
+def library_id(path: str | None = None) -> str | None:
+    """sha256 (16 hex) of every gfx950 code object in the library: changes whenever any kernel's
+    machine code does (sweep.spec_key: checkpoints of another build are never mixed in)."""
+    import hashlib
+    from . import codeobj
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        return None
+    h = hashlib.sha256()
+    for obj in codeobj.device_objects(p):
+        h.update(obj)
+    return h.hexdigest()[:16]
 EXP_POLY11, EXP_TABLE = 0, 1  # enum lzq_exp_variant
 LZQ_MAX_AXES = 8
 ABI_VERSION = 1  # LZQ_ABI_VERSION (tests/test_capi.py checks it against the library)
@@ -74,7 +93,8 @@ ABI_VERSION = 1  # LZQ_ABI_VERSION (tests/test_capi.py checks it against the lib
 # Symbols declared in include/lzq.h (checked by tests/test_capi.py against the header).
 EXPORTS = ("lzq_abi_version", "lzq_last_error", "lzq_init", "lzq_ztables", "lzq_tune", "lzq_aov_batch",
            "lzq_jchi_batch", "lzq_yields_batch", "lzq_sweep_grid", "lzq_sweep_grid_reuse_workspace",
-           "lzq_sweep_grid_reuse", "lzq_yields_batch_reuse", "lzq_p_closed_form",
+           "lzq_sweep_grid_reuse", "lzq_sweep_grid_ztables", "lzq_sweep_grid_from_ztables",
+           "lzq_yields_batch_reuse", "lzq_p_closed_form",
            "lzq_lz_propagate", "lzq_lz_propagate_v", "lzq_ode_tables", "lzq_ode_integrate", "lzq_ode_integrate_shared", "lzq_ode_quadrature", "lzq_ode_batch",
            "lzq_ode_aov_T", "lzq_ode_rhs", "lzq_profile_splines", "lzq_profile_crossings",
            "lzq_lz_propagate_profile")
@@ -122,6 +142,8 @@ def load(path: str | None = None):
     L.lzq_sweep_grid.argtypes = [P(LzqPoint), P(LzqAxis), i32, i64, i64, i32, vp, vp, vp]
     L.lzq_sweep_grid_reuse_workspace.argtypes = [P(LzqAxis), i32, i32]
     L.lzq_sweep_grid_reuse.argtypes = [P(LzqPoint), P(LzqAxis), i32, i64, i64, i32, vp, vp, i64, vp, vp]
+    L.lzq_sweep_grid_ztables.argtypes = [P(LzqPoint), P(LzqAxis), i32, i32, vp, i64, vp]
+    L.lzq_sweep_grid_from_ztables.argtypes = [P(LzqPoint), P(LzqAxis), i32, i64, i64, i32, vp, vp, i64, vp, vp]
     L.lzq_yields_batch_reuse.argtypes = [vp, i64, i32, vp, vp, vp, i64, vp, i64, vp, vp]
     L.lzq_p_closed_form.argtypes = [vp, i64, vp, vp]
     L.lzq_lz_propagate.argtypes = [vp, vp, vp, i64, i32, d, d, i32, vp, vp]

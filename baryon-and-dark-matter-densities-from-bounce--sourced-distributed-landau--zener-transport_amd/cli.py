@@ -59,9 +59,7 @@ def main(argv=None):
             raise ValueError(_native.ODE_STATUS[st])
         if st == _native.ODE_NEWTON:  # fpy:408-410: warn, then report the state where the solver stopped
             print("[warn] ODE solver reported failure:", _native.ODE_STATUS[st])
-        elif st != 0:
-            # LZQ_ODE_TOO_MANY_STEPS: a window needing > 2^26 fixed Radau steps (|x1-x0|/max_step,
-            # fpy:404) is deliberately unsupported (the reference would run for days); exit loudly
+        elif st != 0:  # not reachable for a window the reference accepts (Engine.ode sizes max_steps)
             raise RuntimeError(f"lzq ODE fallback: {_native.ODE_STATUS[st]}")
     YB_fin, Ychi_fin, rhoB0, rhoDM0, ratio, _ = (float(v) for v in table[0].cpu().numpy())
 

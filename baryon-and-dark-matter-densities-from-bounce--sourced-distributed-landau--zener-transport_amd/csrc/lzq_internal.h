@@ -19,8 +19,9 @@ constexpr int kOdeWS = LZQ_ODE_WS_PER_POINT;  // workspace doubles per point
 int launch_ode_aov_tables(const lzq_point* d_points, int64_t n, const double* d_T_lo, const double* d_T_hi,
                           double* d_work, hipStream_t stream);
 
-// lzq_tune(LZQ_TUNE_ODE_COOP) state, read by lzq_ode.hip's launches
+// lzq_tune(LZQ_TUNE_ODE_COOP) / (LZQ_TUNE_ODE_LAUNCH_STEPS) state, read by lzq_ode.hip's launches
 extern int g_ode_coop;
+extern int g_ode_launch_log2;
 
 }  // namespace lzq
 

@@ -1143,6 +1143,12 @@ int lzq_tune(int32_t key, int32_t value) {
     g_truncate = value;
     return prev;
   }
+  if (key == LZQ_TUNE_ODE_LAUNCH_STEPS) {
+    if (value < 6 || value > 40) return fail(LZQ_EINVAL, "lzq_tune: ode launch steps log2 must be in [6, 40], got %d", value);
+    int prev = lzq::g_ode_launch_log2;
+    lzq::g_ode_launch_log2 = value;
+    return prev;
+  }
   if (key == LZQ_TUNE_ODE_COOP) {
     if (value != 0 && value != 1) return fail(LZQ_EINVAL, "lzq_tune: ode_coop must be 0 or 1, got %d", value);
     int prev = lzq::g_ode_coop;
@@ -1328,18 +1334,21 @@ int64_t lzq_sweep_grid_reuse_workspace(const lzq_axis* axes, int32_t n_axes, int
   return n * (ny + lzq::kTabHdr);
 }
 
-int lzq_sweep_grid_reuse(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int64_t start, int64_t count,
-                         int32_t n_y, const double* d_P, double* d_work, int64_t work_doubles, lzq_yield* d_out,
-                         void* stream) {
+// lzq_sweep_grid_reuse in its two halves: build every z-sum table of the grid (parts & 1) and
+// integrate [start, start + count) from them (parts & 2).
+static int sweep_grid_reuse_parts(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int64_t start,
+                                  int64_t count, int32_t n_y, const double* d_P, double* d_work, int64_t work_doubles,
+                                  lzq_yield* d_out, void* stream, int parts, const char* fn) {
   lzq::GridSpec g;
-  int rc = make_grid(base, axes, n_axes, start, count, d_out, "lzq_sweep_grid_reuse", g);
+  int rc = make_grid(base, axes, n_axes, start, count, d_out, fn, g);
   if (rc) return rc;
   const int64_t need = lzq_sweep_grid_reuse_workspace(axes, n_axes, n_y);
   if (need < 0) return (int)need;
-  if (count > 0 && (!d_work || work_doubles < need))
-    return fail(LZQ_EINVAL, "lzq_sweep_grid_reuse: workspace of %lld doubles < %lld needed", (long long)work_doubles,
+  const bool work = (parts & 1) || count > 0;
+  if (work && (!d_work || work_doubles < need))
+    return fail(LZQ_EINVAL, "%s: workspace of %lld doubles < %lld needed", fn, (long long)work_doubles,
                 (long long)need);
-  if (count == 0) return LZQ_OK;
+  if (!(parts & 1) && count == 0) return LZQ_OK;
   int dev;
   rc = ensure_device(&dev);
   if (rc) return rc;
@@ -1352,19 +1361,47 @@ int lzq_sweep_grid_reuse(const lzq_point* base, const lzq_axis* axes, int32_t n_
     }
   const int64_t stride = (n_y > LZQ_NY_MIN ? n_y : LZQ_NY_MIN) + lzq::kTabHdr;
   const int64_t nbt = blocks_for(n_tab, lzq::kWavesPerBlock), nb = blocks_for(count, lzq::kWavesPerBlock);
-  if (nbt > kMaxGrid || nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_sweep_grid_reuse: too large for one launch");
-  // the tables always use the exact-underflow truncation: bit-identical to the dense sums
-  if (g_exp_variant == lzq::kExpTable)
-    hipLaunchKernelGGL((lzq::grid_ztable_kernel<lzq::kExpTable>), dim3((unsigned)nbt), dim3(lzq::kBlock), 0,
-                       (hipStream_t)stream, *base, g, n_tab, n_y, stride, g_dev_tab[dev], exp_table(dev), d_work, 1);
-  else
-    hipLaunchKernelGGL((lzq::grid_ztable_kernel<lzq::kExpPoly11>), dim3((unsigned)nbt), dim3(lzq::kBlock), 0,
-                       (hipStream_t)stream, *base, g, n_tab, n_y, stride, g_dev_tab[dev], exp_table(dev), d_work, 1);
-  LZQ_HIP(hipGetLastError());
-  hipLaunchKernelGGL(lzq::grid_reuse_kernel, dim3((unsigned)nb), dim3(lzq::kBlock), 0, (hipStream_t)stream, *base, g,
-                     start, count, n_y, d_P, d_work, stride, d_out);
-  LZQ_HIP(hipGetLastError());
+  if (nbt > kMaxGrid || nb > kMaxGrid) return fail(LZQ_EINVAL, "%s: too large for one launch", fn);
+  if (parts & 1) {
+    // the tables always use the exact-underflow truncation: bit-identical to the dense sums
+    if (g_exp_variant == lzq::kExpTable)
+      hipLaunchKernelGGL((lzq::grid_ztable_kernel<lzq::kExpTable>), dim3((unsigned)nbt), dim3(lzq::kBlock), 0,
+                         (hipStream_t)stream, *base, g, n_tab, n_y, stride, g_dev_tab[dev], exp_table(dev), d_work, 1);
+    else
+      hipLaunchKernelGGL((lzq::grid_ztable_kernel<lzq::kExpPoly11>), dim3((unsigned)nbt), dim3(lzq::kBlock), 0,
+                         (hipStream_t)stream, *base, g, n_tab, n_y, stride, g_dev_tab[dev], exp_table(dev), d_work, 1);
+    LZQ_HIP(hipGetLastError());
+  }
+  if ((parts & 2) && count > 0) {
+    hipLaunchKernelGGL(lzq::grid_reuse_kernel, dim3((unsigned)nb), dim3(lzq::kBlock), 0, (hipStream_t)stream, *base, g,
+                       start, count, n_y, d_P, d_work, stride, d_out);
+    LZQ_HIP(hipGetLastError());
+  }
   return LZQ_OK;
+}
+
+int lzq_sweep_grid_reuse(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int64_t start, int64_t count,
+                         int32_t n_y, const double* d_P, double* d_work, int64_t work_doubles, lzq_yield* d_out,
+                         void* stream) {
+  if (count == 0) {  // nothing to integrate: validate only (tables need not be built)
+    lzq::GridSpec g;
+    return make_grid(base, axes, n_axes, start, count, d_out, "lzq_sweep_grid_reuse", g);
+  }
+  return sweep_grid_reuse_parts(base, axes, n_axes, start, count, n_y, d_P, d_work, work_doubles, d_out, stream, 3,
+                                "lzq_sweep_grid_reuse");
+}
+
+int lzq_sweep_grid_ztables(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int32_t n_y, double* d_work,
+                           int64_t work_doubles, void* stream) {
+  return sweep_grid_reuse_parts(base, axes, n_axes, 0, 0, n_y, nullptr, d_work, work_doubles, nullptr, stream, 1,
+                                "lzq_sweep_grid_ztables");
+}
+
+int lzq_sweep_grid_from_ztables(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int64_t start,
+                                int64_t count, int32_t n_y, const double* d_P, const double* d_work,
+                                int64_t work_doubles, lzq_yield* d_out, void* stream) {
+  return sweep_grid_reuse_parts(base, axes, n_axes, start, count, n_y, d_P, const_cast<double*>(d_work), work_doubles,
+                                d_out, stream, 2, "lzq_sweep_grid_from_ztables");
 }
 
 int lzq_p_closed_form(const double* d_lambda, int64_t n, double* d_P, void* stream) {

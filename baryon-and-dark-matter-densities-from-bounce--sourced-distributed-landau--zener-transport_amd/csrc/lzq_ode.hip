@@ -30,7 +30,8 @@ namespace lzq {
 #define LZQ_ODE_MIN_WAVES 2
 #endif
 constexpr int kOdeBlock = 256;
-int g_ode_coop = 1;  // lzq_tune(LZQ_TUNE_ODE_COOP)
+int g_ode_coop = 1;          // lzq_tune(LZQ_TUNE_ODE_COOP)
+int g_ode_launch_log2 = 24;  // lzq_tune(LZQ_TUNE_ODE_LAUNCH_STEPS): <= 2^24 Radau steps per launch
 constexpr double kInvMplGeV = 1.0 / kMplGeV;
 
 // ---------------------------------------------------------------------------------------
@@ -560,13 +561,26 @@ __device__ __forceinline__ double branch_x(const OdePoint& o, double x0, double 
 // quadrature (exact for every sigma_v: its equation is linear); step only the Riccati equation
 // of Y_chi, with ode_stage_chi when there is no source term.  Points with sigma_v = 0 return
 // at once (the quadrature has done both).
+// Continuation (OdeState != nullptr): the launch advances every point by the steps
+// [k_lo, k_lo + k_cnt) of its fixed-step sequence only, carrying (Y_chi, Y_B, the predictor's
+// previous start and stages) between launches in HBM, so a window of any length runs as a
+// series of bounded launches (lzq_ode_launches); the arithmetic of every step is the single
+// launch's, so the result is bit-identical to one launch over [0, N).
+struct OdeState {
+  double Ychi, YB, Yp, Z[3];
+  int32_t status, have;  // status: kOdeInProgress while steps remain
+};
+constexpr int32_t kOdeInProgress = 64;
+
 template <bool kChiOnly>
 __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_kernel(const lzq_point* __restrict__ pts,
                                                                   const lzq_ode_params* __restrict__ ode, int64_t n,
                                                                   const int32_t* __restrict__ tidx,
                                                                   const double* __restrict__ ws, int64_t max_steps,
                                                                   lzq_yield* __restrict__ out,
-                                                                  int32_t* __restrict__ status, int coop_on) {
+                                                                  int32_t* __restrict__ status, int coop_on,
+                                                                  int64_t k_lo, int64_t k_cnt,
+                                                                  OdeState* __restrict__ state) {
   __shared__ StageBase s_base[kOdeBlock / 64][64][3];  // cooperative mode
   // Lanes past the end of the batch are clones of their wavefront's first point (they compute
   // it again and write nothing), so a partial wavefront -- a single CLI point included -- is
@@ -576,9 +590,14 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
   const int64_t i_self = (int64_t)blockIdx.x * kOdeBlock + threadIdx.x;
   const bool real = i_self < n;
   const int64_t i = real ? i_self : wave0;
+  const bool cont = state != nullptr, first = !cont || k_lo == 0;
+  if (cont && !first && state[i].status != kOdeInProgress) return;  // finished in an earlier launch
   const lzq_point pt = pts[i];
   const OdePoint o = ode_point(pt, ode[i]);
-  if (kChiOnly && (o.sigmav == 0.0 || (status && status[i] != LZQ_ODE_NOT_LINEAR))) return;
+  if (kChiOnly && first && (o.sigmav == 0.0 || (status && status[i] != LZQ_ODE_NOT_LINEAR))) {
+    if (cont && real) state[i].status = LZQ_ODE_OK;  // nothing to step (the quadrature did it)
+    return;
+  }
   const double* w = ws + (tidx ? (int64_t)tidx[i] : i) * (int64_t)kOdeWS;
   const double nan = __builtin_nan("");
   lzq_yield r = {nan, nan, nan, nan, nan, pt.P_chi_to_B};
@@ -607,8 +626,12 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
       if (!(steps <= (double)max_steps)) st = LZQ_ODE_TOO_MANY_STEPS;
     }
   }
+  bool finished = true;  // this launch ends the point (continuation: else its state is saved)
   if (st == LZQ_ODE_OK) {
     const int64_t N = (int64_t)steps;
+    const int64_t k_begin = cont ? k_lo : 0;
+    const int64_t k_stop = cont ? (k_lo + k_cnt < N ? k_lo + k_cnt : N) : N;
+    finished = k_stop >= N;
     const double h = (x1 - x0) / (double)N;
     const Radau R = radau_tableau();
     // n_chi_eq / vbar_chi switch formula at the strict T > m/3 (fpy:100, 111): the rhs jumps at
@@ -620,6 +643,16 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
     const bool riccati = LZQ_ODE_PREDICT && o.sigmav != 0.0;
     double Zs[3] = {Ychi, Ychi, Ychi}, Yp = Ychi;  // previous step's start and stages (predictor)
     bool have = false, done = false;
+    if (!first) {  // continue from the previous launch's state
+      const OdeState sv = state[i];
+      Ychi = sv.Ychi;
+      YB = sv.YB;
+      Yp = sv.Yp;
+      Zs[0] = sv.Z[0];
+      Zs[1] = sv.Z[1];
+      Zs[2] = sv.Z[2];
+      have = sv.have != 0;
+    }
     // Cooperative mode (a full wavefront whose points agree in everything ode_stage_base (or
     // ode_stage_chi_base: kChiOnly, the same deplete flag) reads:
     // they differ at most in P, flux, sigma_v, Gamma_wash, deplete and the initial state, as in
@@ -644,11 +677,11 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
 #endif
     }
     const int64_t block = coop ? 64 : N;
-    for (int64_t kb = 0; kb < N; kb += block) {
-      const int64_t kend = kb + block < N ? kb + block : N;
+    for (int64_t kb = k_begin; kb < k_stop; kb += block) {
+      const int64_t kend = kb + block < k_stop ? kb + block : k_stop;
       if (coop) {
         const int64_t kl = kb + lane;
-        if (kl < N) {
+        if (kl < kend) {
           const double xk = x0 + (double)kl * h;
 #pragma unroll
           for (int j = 0; j < 3; ++j)
@@ -714,7 +747,22 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
       }
       if (coop) __builtin_amdgcn_wave_barrier();  // every lane is done with this block's table
     }
+    if (done) finished = true;
+    if (!finished && real) {  // save the state for the next launch
+      OdeState sv;
+      sv.Ychi = Ychi;
+      sv.YB = YB;
+      sv.Yp = Yp;
+      sv.Z[0] = Zs[0];
+      sv.Z[1] = Zs[1];
+      sv.Z[2] = Zs[2];
+      sv.status = kOdeInProgress;
+      sv.have = have ? 1 : 0;
+      state[i] = sv;
+    }
   }
+  if (!finished) return;
+  if (cont && real) state[i].status = st;
   if (st == LZQ_ODE_OK || st == LZQ_ODE_NEWTON) {  // fpy:412-417
     const double nB0 = YB * kS0M3, nDM0 = Ychi * kS0M3;
     r.Y_B = YB;
@@ -751,7 +799,7 @@ __constant__ double kGLx[8] = {-0x1.ebab1cb0acc66p-1, -0x1.97e4ab249f41ep-1, -0x
                                0x1.97e4ab249f41ep-1,  0x1.ebab1cb0acc66p-1};
 __constant__ double kGLw[8] = {0x1.9ea1d04ca0393p-4, 0x1.c76fb531d2b91p-3, 0x1.413c50a255611p-2, 0x1.736360b19933fp-2,
                                0x1.736360b19933fp-2, 0x1.413c50a255611p-2, 0x1.c76fb531d2b91p-3, 0x1.9ea1d04ca0393p-4};
-constexpr int kQuadMaxSub = 256;
+constexpr int kQuadMaxSub = 4096;  // per knot interval; beyond: status LZQ_ODE_UNRESOLVED
 #ifndef LZQ_QUAD_UNROLL
 #define LZQ_QUAD_UNROLL 1
 #endif
@@ -824,30 +872,44 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_QUAD_MIN_WAVES) void ode_quad_kernel
     Ychi = n_chi_eq(o.T_hi, m, pt.g_chi, pt.stats) / s_entropy(o.T_hi, pt.g_star_s);
   }
   double accB = 0.0, accC = 0.0;
+  bool unresolved = false;
   if (st == LZQ_OK || st == LZQ_ODE_NOT_LINEAR) {  // Y_B's equation is linear for every sigma_v
     const double gam = o.gamma_w;
     const double Bt = o.B * T_p * T_p;
+    // where the source window exp(-q^2/2), q = y(T)/sigma, y = B/2 ((T_p/T)^2 - 1), is not exactly
+    // 0 in double: |q| <= 40 <=> T in [T_p / sqrt(1 + r), T_p / sqrt(1 - r)], r = 80 sigma / B
+    const double rw = o.B > 0.0 ? 80.0 * o.sig / o.B : INFINITY;
+    const double Tw_lo = rw < INFINITY ? T_p / sqrt(1.0 + rw) : 0.0;
+    const double Tw_hi = rw < 1.0 ? T_p / sqrt(1.0 - rw) : INFINITY;
     for (int k = lane; k < kOdeNT - 1; k += kW) {
       const double Tk = linspace_at(o.T_lo, o.T_hi, o.stepT, k, kOdeNT);
       const double Tk1 = linspace_at(o.T_lo, o.T_hi, o.stepT, k + 1, kOdeNT);
       const double c[4] = {w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]};
       const bool split = Tk < o.m3 && o.m3 < Tk1;
       for (int part = 0; part < (split ? 2 : 1); ++part) {
-        const double a = (split && part == 1) ? o.m3 : Tk;
-        const double b = (split && part == 0) ? o.m3 : Tk1;
-        // the window exp(-q^2/2), q = y(T)/sigma, y monotone in T: beyond |q| = 40 on the whole
-        // [a, b] it is below e^-800, i.e. exactly 0 in double -- skip (no sub-intervals wasted
-        // where the source is off)
+        double a = (split && part == 1) ? o.m3 : Tk;
+        double b = (split && part == 0) ? o.m3 : Tk1;
+        // the window exp(-q^2/2), q = y(T)/sigma, y monotone in T: beyond |q| = 40 it is below
+        // e^-800, i.e. exactly 0 in double -- the integral is taken over the part of [a, b] where
+        // it is not (no sub-intervals wasted where the source is off, and a narrow window
+        // (small sigma_y, large beta/H) gets its sub-intervals where it is)
         const double qa = 0.5 * o.B * ((T_p / a) * (T_p / a) - 1.0) * o.inv_sig;
         const double qb = 0.5 * o.B * ((T_p / b) * (T_p / b) - 1.0) * o.inv_sig;
         if (qa * qb > 0.0 && pymin(fabs(qa), fabs(qb)) > 40.0) continue;
+        a = pymax(a, Tw_lo);
+        b = pymin(b, Tw_hi);
+        if (!(b > a)) continue;
         // narrowest local scale of the smooth factors on [a, b] (all shrink as T falls):
         // window width in T, integrating factor / power laws, Boltzmann factor below m/3
         double scale = o.sig * a * a * a / pymax(Bt, 1e-300);
         scale = pymin(scale, a / (gam + 6.0));
         if (a <= o.m3) scale = pymin(scale, a * a / m);
         const double ns = ceil((b - a) / (0.5 * scale));
-        const int nsub = ns < 1.0 ? 1 : (ns > (double)kQuadMaxSub ? kQuadMaxSub : (int)ns);
+        if (!(ns <= (double)kQuadMaxSub)) {  // a scale the rule would not resolve: no silent answer
+          unresolved = true;
+          continue;
+        }
+        const int nsub = ns < 1.0 ? 1 : (int)ns;
         const double hs = (b - a) / (double)nsub;
         for (int j = 0; j < nsub; ++j) {
           const double mid = a + ((double)j + 0.5) * hs;
@@ -868,6 +930,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_QUAD_MIN_WAVES) void ode_quad_kernel
     accB += __shfl_xor(accB, d, kW);
     accC += __shfl_xor(accC, d, kW);
   }
+  if (__any(unresolved)) st = LZQ_ODE_UNRESOLVED;
   if (lane != 0) return;
   if (st == LZQ_ODE_NOT_LINEAR) r.Y_B = accB;  // Y_chi: the Riccati stepping (ode_integrate_kernel<true>)
   if (st == LZQ_OK) {  // fpy:412-417
@@ -914,6 +977,44 @@ __global__ __launch_bounds__(kOdeBlock) void ode_eval_kernel(lzq_point pt, lzq_o
 namespace {
 
 int64_t ode_blocks(int64_t n) { return (n + lzq::kOdeBlock - 1) / lzq::kOdeBlock; }
+
+int hip_check(hipError_t e, const char* what);
+
+// The fixed-step integration of a batch as continuation launches of <= 2^g_ode_launch_log2
+// steps each (lzq_tune(LZQ_TUNE_ODE_LAUNCH_STEPS)): ceil(max_steps / 2^log2) launches, every
+// point advancing through steps [j 2^log2, (j+1) 2^log2) of its own sequence in launch j and
+// finishing in the launch that reaches its N (points done early return at once).  One launch
+// when max_steps fits.  The per-point state (64 B) is stream-ordered scratch (hipMallocAsync).
+template <bool kChiOnly>
+int launch_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, const int32_t* d_tidx,
+                     const double* d_work, int64_t max_steps, lzq_yield* d_out, int32_t* d_status, hipStream_t s,
+                     const char* fn) {
+  const int64_t per = (int64_t)1 << lzq::g_ode_launch_log2;
+  const int64_t launches = max_steps <= per ? 1 : (max_steps + per - 1) / per;
+  if (launches > 65536) {
+    char buf[160];
+    snprintf(buf, sizeof(buf), "%s: max_steps %lld needs more than 65536 launches of 2^%d steps", fn,
+             (long long)max_steps, lzq::g_ode_launch_log2);
+    return lzq_set_error(LZQ_EINVAL, buf);
+  }
+  if (launches == 1) {
+    hipLaunchKernelGGL(lzq::ode_integrate_kernel<kChiOnly>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, s,
+                       d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, lzq::g_ode_coop, (int64_t)0,
+                       (int64_t)0, (lzq::OdeState*)nullptr);
+    return hip_check(hipGetLastError(), fn);
+  }
+  lzq::OdeState* st = nullptr;
+  int rc = hip_check(hipMallocAsync((void**)&st, sizeof(lzq::OdeState) * (size_t)n, s), fn);
+  if (rc) return rc;
+  for (int64_t j = 0; j < launches && rc == LZQ_OK; ++j) {
+    hipLaunchKernelGGL(lzq::ode_integrate_kernel<kChiOnly>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, s,
+                       d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, lzq::g_ode_coop, j * per, per,
+                       st);
+    rc = hip_check(hipGetLastError(), fn);
+  }
+  const int rf = hip_check(hipFreeAsync(st, s), fn);
+  return rc ? rc : rf;
+}
 
 int hip_check(hipError_t e, const char* what) {
   if (e == hipSuccess) return LZQ_OK;
@@ -967,10 +1068,8 @@ int lzq_ode_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, in
   if (n > 0 && (!d_points || !d_ode || !d_out)) return lzq_set_error(LZQ_EINVAL, "lzq_ode_integrate: bad arguments");
   if (max_steps < 0) return lzq_set_error(LZQ_EINVAL, "lzq_ode_integrate: max_steps < 0");
   if (n == 0) return LZQ_OK;
-  hipLaunchKernelGGL(lzq::ode_integrate_kernel<false>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0,
-                     (hipStream_t)stream, d_points, d_ode, n, (const int32_t*)nullptr, d_work, max_steps, d_out,
-                     d_status, lzq::g_ode_coop);
-  return hip_check(hipGetLastError(), "lzq_ode_integrate");
+  return launch_integrate<false>(d_points, d_ode, n, nullptr, d_work, max_steps, d_out, d_status, (hipStream_t)stream,
+                                 "lzq_ode_integrate");
 }
 
 int lzq_ode_integrate_shared(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n,
@@ -984,10 +1083,8 @@ int lzq_ode_integrate_shared(const lzq_point* d_points, const lzq_ode_params* d_
   if (max_steps < 0) return lzq_set_error(LZQ_EINVAL, "lzq_ode_integrate_shared: max_steps < 0");
   if (ode_blocks(n) > 2147483647LL) return lzq_set_error(LZQ_EINVAL, "lzq_ode_integrate_shared: n too large");
   if (n == 0) return LZQ_OK;
-  hipLaunchKernelGGL(lzq::ode_integrate_kernel<false>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0,
-                     (hipStream_t)stream, d_points, d_ode, n, d_table_index, d_work, max_steps, d_out, d_status,
-                     lzq::g_ode_coop);
-  return hip_check(hipGetLastError(), "lzq_ode_integrate_shared");
+  return launch_integrate<false>(d_points, d_ode, n, d_table_index, d_work, max_steps, d_out, d_status,
+                                 (hipStream_t)stream, "lzq_ode_integrate_shared");
 }
 
 int lzq_ode_quadrature(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n,
@@ -1006,10 +1103,8 @@ int lzq_ode_quadrature(const lzq_point* d_points, const lzq_ode_params* d_ode, i
   rc = hip_check(hipGetLastError(), "lzq_ode_quadrature");
   if (rc) return rc;
   // sigma_v != 0: Y_chi's Riccati equation by the Radau stepping (Y_B from the quadrature above)
-  hipLaunchKernelGGL(lzq::ode_integrate_kernel<true>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0,
-                     (hipStream_t)stream, d_points, d_ode, n, d_table_index, d_work, max_steps, d_out, d_status,
-                     lzq::g_ode_coop);
-  return hip_check(hipGetLastError(), "lzq_ode_quadrature");
+  return launch_integrate<true>(d_points, d_ode, n, d_table_index, d_work, max_steps, d_out, d_status,
+                                (hipStream_t)stream, "lzq_ode_quadrature");
 }
 
 int lzq_ode_batch(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, double* d_work,

@@ -11,8 +11,12 @@ from typing import Iterable, Optional, Sequence
 import numpy as np
 import torch
 
+import logging
+
 from . import _native
 from .config import to_ctypes_ode, to_ctypes_point, to_point
+
+_log = logging.getLogger("lzq")
 
 YIELD_FIELDS = _native.YIELD_FIELDS
 
@@ -31,6 +35,9 @@ class Engine:
         self.lib = _native.load(lib_path)
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         self._zwork = None  # lzq_sweep_grid_reuse's z-sum tables (grown on demand)
+        self._ztab_key = None  # the grid whose tables _zwork holds (Engine.sweep reuse)
+        self._exp_variant = "table"
+        self.last_reuse = None
         with torch.cuda.device(self.device):
             self._check(self.lib.lzq_init(self.device.index))
 
@@ -40,6 +47,8 @@ class Engine:
         prev = self.lib.lzq_tune(_native.TUNE_EXP, v)
         if prev < 0:
             self._check(prev)
+        self._exp_variant = variant
+        _native.TUNE_STATE["exp"] = variant
         return {_native.EXP_POLY11: "poly11", _native.EXP_TABLE: "table"}[prev]
 
     def tune_ode_coop(self, on: bool) -> bool:
@@ -49,6 +58,15 @@ class Engine:
         if prev < 0:
             self._check(prev)
         return bool(prev)
+
+    def tune_ode_launch_steps(self, log2: int) -> int:
+        """Fixed Radau steps per ODE continuation launch, as a power of two (include/lzq.h
+        LZQ_TUNE_ODE_LAUNCH_STEPS, default 24; bit-identical results).  Returns the previous."""
+        prev = self.lib.lzq_tune(_native.TUNE_ODE_LAUNCH_STEPS, int(log2))
+        if prev < 0:
+            self._check(prev)
+        self._ode_launch_log2 = int(log2)
+        return prev
 
     def tune_truncate(self, on: bool) -> bool:
         """Exact-underflow truncation of the z-sums (bit-identical results, fewer nodes
@@ -114,6 +132,7 @@ class Engine:
                 need = rep.numel() * stride
                 if self._zwork is None or self._zwork.numel() < need:
                     self._zwork = torch.empty(need, dtype=torch.float64, device=self.device)
+                self._ztab_key = None   # the grid tables in _zwork are overwritten
                 idx = inv.to(torch.int32)
                 self._check(self.lib.lzq_yields_batch_reuse(_vp(d_pts), n, int(n_y), _vp(Pv), _vp(rep), _vp(idx),
                                                               rep.numel(), _vp(self._zwork), self._zwork.numel(),
@@ -155,16 +174,32 @@ class Engine:
             if need < 0:
                 self._check(int(need))
             n_tables = need // (max(int(n_y), 2000) + 4)
-            # every table costs one dense point, so they pay only with at least as many points as
-            # tables; and their workspace stays bounded (REUSE_MAX_BYTES): otherwise the dense path,
-            # which gives the same bits
-            reuse = reuse and 0 < n_tables <= count and need * 8 <= REUSE_MAX_BYTES
+            # the tables of a grid are built once and reused by every later chunk of the same sweep
+            # (base, axes, n_y and exponential variant: tkey); every table costs one dense point, so
+            # building them pays only with at least as many points to come as tables; and their
+            # workspace stays bounded (REUSE_MAX_BYTES): otherwise the dense path, same bits
+            tkey = None
             if reuse:
-                if self._zwork is None or self._zwork.numel() < need:
-                    self._zwork = torch.empty(max(int(need), 1), dtype=torch.float64, device=self.device)
-                self._check(self.lib.lzq_sweep_grid_reuse(ctypes.byref(base), arr, len(axes), int(start), int(count),
-                                                          int(n_y), _vp(Pp), _vp(self._zwork), self._zwork.numel(),
-                                                          _vp(out), self._stream()))
+                tkey = (bytes(base), tuple((n, np.asarray(v, dtype=np.float64).tobytes()) for n, v in axes), int(n_y),
+                        self._exp_variant)
+                built = tkey == self._ztab_key
+                why = None if need * 8 <= REUSE_MAX_BYTES else f"{n_tables} z-sum tables exceed REUSE_MAX_BYTES"
+                if why is None and not built and not 0 < n_tables <= count:
+                    why = f"{n_tables} z-sum tables for a chunk of {count} points"
+                if why:
+                    _log.warning("lzq reuse_zsums: dense path (same bits): %s", why)
+                    reuse = False
+            self.last_reuse = "tables" if reuse else "dense"
+            if reuse:
+                if not built:
+                    if self._zwork is None or self._zwork.numel() < need:
+                        self._zwork = torch.empty(max(int(need), 1), dtype=torch.float64, device=self.device)
+                    self._check(self.lib.lzq_sweep_grid_ztables(ctypes.byref(base), arr, len(axes), int(n_y),
+                                                                _vp(self._zwork), self._zwork.numel(), self._stream()))
+                    self._ztab_key = tkey
+                self._check(self.lib.lzq_sweep_grid_from_ztables(
+                    ctypes.byref(base), arr, len(axes), int(start), int(count), int(n_y), _vp(Pp), _vp(self._zwork),
+                    self._zwork.numel(), _vp(out), self._stream()))
             else:
                 self._check(self.lib.lzq_sweep_grid(ctypes.byref(base), arr, len(axes), int(start), int(count),
                                                       int(n_y), _vp(Pp), _vp(out), self._stream()))
@@ -189,7 +224,7 @@ class Engine:
                                                 self._stream()))
         return work, status
 
-    def ode(self, points, ode_params, max_steps: int = 1 << 26, chunk: int = 1 << 18,
+    def ode(self, points, ode_params, max_steps: Optional[int] = None, chunk: int = 1 << 18,
             share_tables: bool = True, method: str = "radau", group_waves: bool = True) -> tuple:
         """fpy:385-417 for n points (POINT_DTYPE records + ODE_DTYPE records): (n, 6) yields
         table and (n,) int32 status (enum lzq_ode_status), both on the device.  Points are
@@ -205,7 +240,11 @@ class Engine:
         group_waves: launch the points in an order that puts points with equal stage keys
         (_native.ODE_STAGE_KEY, + deplete) next to each other, so that whole wavefronts qualify
         for the integrator's cooperative mode; results are scattered back to the input order.
-        Each point's result is the same bits in either order."""
+        Each point's result is the same bits in either order.
+        max_steps: cap on the fixed Radau steps of a point (LZQ_ODE_TOO_MANY_STEPS beyond it).
+        None (default): the batch's own largest step count (ode_step_counts), i.e. every window
+        the reference accepts is integrated, however long (fpy:403-407): the library runs it as
+        continuation launches of <= 2^24 steps."""
         if method not in ("radau", "quadrature"):
             raise ValueError(f"method must be 'radau' or 'quadrature', got {method!r}")
         pts = np.ascontiguousarray(points, dtype=_native.POINT_DTYPE).reshape(-1)
@@ -213,6 +252,11 @@ class Engine:
         if pts.size != ods.size:
             raise ValueError("points and ode_params must have the same length")
         n = pts.size
+        if max_steps is None:
+            need = ode_step_counts(pts)
+            need = need[np.isfinite(need)]
+            per = 1 << getattr(self, "_ode_launch_log2", 24)
+            max_steps = int(min(need.max() + 64 if need.size else 0, _native.ODE_MAX_LAUNCHES * per))
         d_pts_all = self.points_to_device(pts)
         d_ode_all = torch.from_numpy(ods.view(np.uint8).copy()).to(self.device)
         order = wave_order(d_pts_all, d_ode_all, n) if group_waves else None
@@ -387,6 +431,21 @@ class Engine:
                 _vp(shapes.knots), _vp(shapes.coef), shapes.n_shapes, shapes.n_knots, _vp(points), n,
                 float(steps_per_radian), int(min_steps), _vp(out), self._stream()))
         return out
+
+
+def ode_step_counts(pts: np.ndarray) -> np.ndarray:
+    """Fixed Radau steps of each point's fpy:385-407 window, N = ceil(|x1 - x0| / max_step) with
+    max_step = min(|x1 - x0|/20000, x_p/1000, 5e-4) (fpy:403-404), on the host (the device
+    computes the same; this sizes the continuation launches)."""
+    m = pts["m_chi_GeV"].astype(np.float64)
+    Tp = pts["T_p_GeV"]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        x0 = m / (pts["T_max_over_Tp"] * Tp)
+        x1 = m / np.maximum(pts["T_min_over_Tp"] * Tp, 1e-30)
+        x_p = m / np.maximum(Tp, 1e-30)
+        dx = np.abs(x1 - x0)
+        ms = np.minimum(np.minimum(dx / 20000.0, x_p / 1000.0), 5e-4)
+        return np.where(ms > 0.0, np.ceil(dx / ms), np.nan)
 
 
 class ProfileShapes:

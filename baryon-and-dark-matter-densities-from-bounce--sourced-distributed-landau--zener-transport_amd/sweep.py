@@ -228,8 +228,12 @@ def shard_range(total: int, rank: int, world: int) -> Tuple[int, int]:
 
 def spec_key(spec: SweepSpec) -> str:
     """Hash of everything a shard's contents depend on: the sweep definition (axes, base
-    config, n_y, crossings) and the library's ABI version."""
-    d = {"spec": spec.to_json(), "abi": _native.ABI_VERSION}
+    config, n_y, crossings, ODE method), the library's ABI version, its machine code
+    (_native.library_id: any rebuild that changes a kernel changes the key) and the bit-changing
+    tuning state (the inner-loop exponential).  --resume after such a change starts afresh
+    instead of mixing shards of different numerics."""
+    d = {"spec": spec.to_json(), "abi": _native.ABI_VERSION, "lib": _native.library_id(),
+         "tune": dict(_native.TUNE_STATE)}
     d["spec"].pop("notes", None)
     return hashlib.sha256(json.dumps(d, sort_keys=True).encode()).hexdigest()[:16]
 
@@ -253,7 +257,8 @@ def prepare_out_dir(out_dir: str, spec: SweepSpec, resume: bool, rank: int = 0) 
     if rank == 0:
         tmp = man + f".tmp{os.getpid()}"
         with open(tmp, "w") as f:
-            json.dump({"key": key, "abi": _native.ABI_VERSION, "spec_def": spec.to_json()}, f, indent=1)
+            json.dump({"key": key, "abi": _native.ABI_VERSION, "lib": _native.library_id(),
+                       "tune": dict(_native.TUNE_STATE), "spec_def": spec.to_json()}, f, indent=1)
         os.replace(tmp, man)
     return key
 
@@ -423,6 +428,24 @@ def summarize(table: np.ndarray, spec: SweepSpec, elapsed: Optional[float] = Non
             "elapsed_s": elapsed}
 
 
+def ode_status_summary(counts, group=None, device=None) -> Optional[dict]:
+    """Grid-wide ODE point counts per lzq_ode_status (summed over ranks in rank order)."""
+    if counts is None:
+        return None
+    import torch
+    import torch.distributed as dist
+    c = torch.as_tensor(np.asarray(counts, dtype=np.int64))
+    if dist.is_available() and dist.is_initialized():
+        if dist.get_backend(group) == "nccl":
+            c = c.to(device)
+        dist.all_reduce(c, group=group)
+    c = c.cpu().numpy()
+    names = {_native.ODE_OK: "ok", _native.ODE_BAD_GRID: "bad_grid", _native.ODE_BAD_STEP: "bad_step",
+             _native.ODE_TOO_MANY_STEPS: "too_many_steps", _native.ODE_NEWTON: "newton_failed",
+             _native.ODE_NOT_LINEAR: "not_linear", _native.ODE_UNRESOLVED: "quadrature_unresolved"}
+    return {names.get(k, str(k)): int(v) for k, v in enumerate(c) if v}
+
+
 def run_sweep(spec: SweepSpec, engine=None, rank: int = 0, world: int = 1, chunk: int = 1 << 20,
               out_dir: Optional[str] = None, resume: bool = False, group=None, log=print, reuse: bool = False):
     """Evaluate `spec` on this rank's shard, all-gather, return the full table (torch, on
@@ -434,9 +457,11 @@ def run_sweep(spec: SweepSpec, engine=None, rank: int = 0, world: int = 1, chunk
     start, end = shard_range(spec.total, rank, world)
     key = prepare_out_dir(out_dir, spec, resume, rank) if out_dir else ""
 
-    local = run_local(make_compute(spec, engine, reuse=reuse), start, end,
+    compute = make_compute(spec, engine, reuse=reuse)
+    local = run_local(compute, start, end,
                       lambda n: torch.empty((n, 6), dtype=torch.float64, device=engine.device), chunk,
                       out_dir, resume, sync=torch.cuda.synchronize, log=log, key=key)
+    run_sweep.ode_status = ode_status_summary(getattr(compute, "ode_status", None), group, engine.device)
     return gather_table(local, spec.total, rank, world, group)
 
 
@@ -454,6 +479,7 @@ def make_compute(spec: SweepSpec, engine, reuse: bool = False) -> ComputeFn:
     without crossings).  reuse: the quadrature's z-sums shared across points with the same
     y-grid and A/V kernel (lzq_sweep_grid_reuse; bit-identical, not the dense headline path)."""
     if is_ode_spec(spec):
+        counts = np.zeros(8, dtype=np.int64)   # ODE points per lzq_ode_status, this rank
 
         def compute_ode(s, n, out):
             import torch
@@ -465,11 +491,18 @@ def make_compute(spec: SweepSpec, engine, reuse: bool = False) -> ComputeFn:
                   (ods["deplete_DM_from_source"] != 0)
             sel = np.nonzero(ode)[0]
             if sel.size:
-                tab, _status = engine.ode(pts[sel], ods[sel], method=spec.ode_method)  # failed points: NaN rows
+                tab, status = engine.ode(pts[sel], ods[sel], method=spec.ode_method)
+                # a point the integrator did not finish normally (a Radau Newton failure reports the
+                # state where it stopped, as fpy:408-410 does for the CLI) is a NaN row in a sweep
+                # table, counted per status in the summary ("ode_status")
+                bad = status != 0
+                tab = torch.where(bad[:, None], torch.full_like(tab, float("nan")), tab)
+                counts[:] += np.bincount(status.clamp(0, 7).cpu().numpy(), minlength=8)[:8]
                 out[torch.as_tensor(sel, device=out.device)] = tab
             sel = np.nonzero(~ode)[0]
             if sel.size:
                 out[torch.as_tensor(sel, device=out.device)] = engine.yields(pts[sel], n_y=spec.n_y, reuse=reuse)
+        compute_ode.ode_status = counts
         return compute_ode
 
     def compute(s, n, out):
@@ -519,10 +552,12 @@ def main(argv=None):
     start, end = shard_range(spec_total, rank, world)
     key = prepare_out_dir(args.out, spec, args.resume, rank) if args.out else ""
 
-    local = run_local(make_compute(spec, eng, reuse=args.reuse_zsums), start, end,
+    compute = make_compute(spec, eng, reuse=args.reuse_zsums)
+    local = run_local(compute, start, end,
                       lambda n: torch.empty((n, 6), dtype=torch.float64, device=eng.device), args.chunk,
                       args.out, args.resume, sync=torch.cuda.synchronize,
                       log=(print if rank == 0 else (lambda s: None)), key=key)
+    ode_status = ode_status_summary(getattr(compute, "ode_status", None), None, eng.device)
     table = gather_table(local, spec_total, rank, world)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -531,6 +566,10 @@ def main(argv=None):
         summ = summarize(tab, spec, elapsed)
         summ["points_per_s"] = spec_total / elapsed
         summ["n_gpus"] = world
+        if ode_status is not None:
+            summ["ode_status"] = ode_status   # ODE-path points per status (non-ok rows are NaN)
+        if args.reuse_zsums:
+            summ["reuse_zsums"] = eng.last_reuse
         if args.out:
             np.save(os.path.join(args.out, "table.npy"), tab, allow_pickle=False)
             with open(os.path.join(args.out, "summary.json"), "w") as f:

@@ -127,7 +127,12 @@ int lzq_ztables(double* z, double* gamma4, double* omega);
  * where a full wavefront of points that differ only in P, flux, sigma_v, Gamma_wash, deplete
  * and the initial state evaluates each step's stage ingredients once for the whole wavefront.
  * Results are bit-identical either way (tests/test_gpu_ode.py). */
-enum lzq_tune_key { LZQ_TUNE_EXP = 0, LZQ_TUNE_TRUNCATE = 1, LZQ_TUNE_ODE_COOP = 2 };
+/* LZQ_TUNE_ODE_LAUNCH_STEPS (value = log2 of the steps per launch, 6..40; default 24): the ODE
+ * integrator runs a batch as continuation launches of at most 2^value fixed Radau steps each,
+ * ceil(max_steps / 2^value) launches (<= 65536), the per-point state carried between them in
+ * stream-ordered scratch (64 B per point), so any window the reference accepts completes in
+ * bounded launches.  Results are bit-identical for every value (tests/test_gpu_ode.py). */
+enum lzq_tune_key { LZQ_TUNE_EXP = 0, LZQ_TUNE_TRUNCATE = 1, LZQ_TUNE_ODE_COOP = 2, LZQ_TUNE_ODE_LAUNCH_STEPS = 3 };
 enum lzq_exp_variant { LZQ_EXP_POLY11 = 0, LZQ_EXP_TABLE = 1 };
 int lzq_tune(int32_t key, int32_t value);
 
@@ -178,6 +183,17 @@ int lzq_sweep_grid_reuse(const lzq_point* base, const lzq_axis* axes, int32_t n_
                          int32_t n_y, const double* d_P, double* d_work, int64_t work_doubles, lzq_yield* d_out,
                          void* stream);
 
+/* lzq_sweep_grid_reuse in two halves, so a sweep evaluated in chunks (or shards) builds its
+ * z-sum tables once: lzq_sweep_grid_ztables writes every table of the grid into d_work (the
+ * whole grid's, independent of any range); lzq_sweep_grid_from_ztables integrates points
+ * [start, start+count) from tables built by it for the same base, axes and n_y (and exponential
+ * variant).  Together they are lzq_sweep_grid_reuse, bit for bit. */
+int lzq_sweep_grid_ztables(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int32_t n_y, double* d_work,
+                           int64_t work_doubles, void* stream);
+int lzq_sweep_grid_from_ztables(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int64_t start,
+                                int64_t count, int32_t n_y, const double* d_P, const double* d_work,
+                                int64_t work_doubles, lzq_yield* d_out, void* stream);
+
 /* fpy:183-184: P[i] = clamp(1 - exp(-2 pi max(lambda[i], 0)), 0, 1) (naive 1-exp kept). */
 int lzq_p_closed_form(const double* d_lambda, int64_t n, double* d_P, void* stream);
 
@@ -200,6 +216,8 @@ enum lzq_ode_status {
   LZQ_ODE_BAD_STEP = 2,       /* max_step <= 0 (zero-width x range): solve_ivp raises ValueError */
   LZQ_ODE_TOO_MANY_STEPS = 3, /* more than max_steps integration steps: not attempted */
   LZQ_ODE_NOT_LINEAR = 5,     /* internal to lzq_ode_quadrature: Y_chi still to be stepped */
+  LZQ_ODE_UNRESOLVED = 6,     /* lzq_ode_quadrature: a knot interval needs more than 4096
+                                 Gauss sub-intervals to resolve its scales (NaN yields) */
   LZQ_ODE_NEWTON = 4          /* a Radau stage system did not converge: the yields are the
                                  state at the start of the failed step (fpy:408-410 reports
                                  sol.y[:, -1] after a failed solve) */
@@ -217,8 +235,10 @@ int lzq_ode_tables(const lzq_point* d_points, int64_t n, const double* d_T_lo, c
 /* fpy:385-417 on built tables: Y_chi(x1), Y_B(x1) of rhs (fpy:270-286) from x0 = m/T_hi to
  * x1 = m/max(T_lo, 1e-30), Y(x0) = (Y_chi0 of fpy:389-399, 0), by the reference's method
  * (3-stage Radau IIA) on uniform steps h = (x1 - x0)/ceil(|x1 - x0|/max_step) <= max_step of
- * fpy:404, one point per lane; then the densities epilogue.  Points needing more than
- * max_steps steps are not integrated (status LZQ_ODE_TOO_MANY_STEPS, NaN yields); so are
+ * fpy:404, one point per lane; then the densities epilogue.  The steps run as continuation
+ * launches of <= 2^24 steps (LZQ_TUNE_ODE_LAUNCH_STEPS), so max_steps only caps the work: points
+ * needing more than max_steps steps are not integrated (status LZQ_ODE_TOO_MANY_STEPS, NaN
+ * yields; max_steps <= 65536 x the launch size); so are
  * points whose T grid CubicSpline would reject (LZQ_ODE_BAD_GRID).  A Newton failure
  * (LZQ_ODE_NEWTON) stops the point and reports the state reached.  d_status: optional [n]
  * int32 output (enum lzq_ode_status). */

@@ -113,8 +113,8 @@ def test_incoherent_composition():
 
 
 def test_plugin_profile_formats(tmp_path):
-    """plugins/transport_from_profile.py reads the two documented CSV formats (host logic;
-    the propagation itself is tests/test_gpu_plugin.py)."""
+    """plugins/transport_from_profile.py parses its documented CSV formats (host logic; the
+    splines, crossings and propagation are tests/test_gpu_plugin.py)."""
     import importlib.util
     spec = importlib.util.spec_from_file_location(
         "tfp_cpu", os.path.join(os.path.dirname(os.path.dirname(__file__)), "plugins", "transport_from_profile.py"))
@@ -124,15 +124,14 @@ def test_plugin_profile_formats(tmp_path):
     xs, ms, ds, o = tfp.read_profile(str(tmp_path / "a.csv"))
     assert xs == [0.0, 50.0] and ms == [0.1, 0.2] and ds == [1.0, 2.0]
     assert o["window_lz"] == 30.0 and o["v_w"] == 0.3 and o["steps"] == 1000.0
-    # sampled profile: Delta = x - 1 on [0, 2] crosses once at x = 1, slope 1, m interpolated
-    rows = "".join(f"{x!r},{x - 1.0!r},{0.1 + 0.1 * x!r}\n" for x in (0.0, 0.5, 0.75, 1.25, 2.0))
-    (tmp_path / "b.csv").write_text("xi,Delta,m_mix\n" + rows)
-    xs, ms, ds, _ = tfp.read_profile(str(tmp_path / "b.csv"))
-    assert len(xs) == 1 and abs(xs[0] - 1.0) < 1e-15 and abs(ds[0] - 1.0) < 1e-15 and abs(ms[0] - 0.2) < 1e-15
-    # a sample exactly on the crossing, then a second crossing going down
-    (tmp_path / "c.csv").write_text("xi,Delta,m_mix\n-1,-1,0.1\n0,0,0.1\n1,1,0.1\n2,-1,0.3\n")
-    xs, ms, ds, _ = tfp.read_profile(str(tmp_path / "c.csv"))
-    assert xs == [0.0, 1.5] and ds == [1.0, 2.0] and ms == [0.1, 0.2]
+    # the sampled formats' crossings come from the GPU splines (tests/test_gpu_plugin.py); their
+    # header / size / option errors are caught on the host
+    (tmp_path / "p.csv").write_text("xi,phi,Phi\n0,1,0\n1,1,1\n2,1,2\n3,1,3\n")
+    with pytest.raises(ValueError, match="y_B"):
+        tfp.read_profile(str(tmp_path / "p.csv"))
+    (tmp_path / "e.csv").write_text("# estimator = bogus\nxi,m_mix,dprime\n0,0.1,1\n")
+    with pytest.raises(ValueError, match="estimator"):
+        tfp.read_profile(str(tmp_path / "e.csv"))
     for bad in ("xi,foo\n1,2\n", "xi,m_mix,dprime\n", "xi,m_mix,dprime\n1,0.1,1\n0,0.1,1\n",
                 "xi,Delta,m_mix\n0,1,0.1\n1,2,0.1\n"):
         (tmp_path / "bad.csv").write_text(bad)

@@ -328,3 +328,116 @@ def test_ode_cooperative_waves_bit_identical(gpu_engine):
         if s1 == 0 and s2 == 0:
             for v, w in zip(row[:5], rr[:5]):
                 assert rel_err(v, w) < 1e-10, (v, w)
+
+
+def test_ode_continuation_launches_bit_identical(gpu_engine):
+    """The fixed-step integration as continuation launches (include/lzq.h
+    LZQ_TUNE_ODE_LAUNCH_STEPS): 20000-step windows split into 3 launches of 2^13 steps (and 40
+    launches of 2^9) give the same bits as one launch -- cooperative and per-lane waves, split
+    steps at T = m/3, Riccati (sigma_v != 0) with its predictor, thermal/nonthermal, and the
+    quadrature method's Riccati stepping."""
+    rng = np.random.default_rng(41)
+    cfgs = []
+    for m_chi in (0.95, 40.0):
+        for _ in range(70):
+            c = full_cfg(BASE_CFG)
+            c.update(NARROW, m_chi_GeV=m_chi, P_chi_to_B=float(rng.uniform(0.05, 1.0)),
+                     Gamma_wash_over_H=float(rng.choice([0.0, 0.5, 2.0])),
+                     sigma_v_chi_GeV_m2=float(rng.choice([0.0, 1e-16, 1e-12])),
+                     deplete_DM_from_source=bool(rng.uniform() < 0.3),
+                     regime=str(rng.choice(["thermal", "nonthermal"])))
+            if c["Gamma_wash_over_H"] == 0.0 and c["sigma_v_chi_GeV_m2"] == 0.0:
+                c["deplete_DM_from_source"] = True
+            cfgs.append(c)
+    cfgs += seeded_cfgs(12, seed=8)
+    p, o = recs(cfgs)
+    steps = pkg("engine").ode_step_counts(p)
+    assert steps.max() > 2 ** 13
+    one = {m: gpu_engine.ode(p, o, method=m) for m in ("radau", "quadrature")}
+    mixed = gpu_engine.ode(p, o, group_waves=False)
+    for log2 in (13, 9):
+        prev = gpu_engine.tune_ode_launch_steps(log2)
+        try:
+            for m in ("radau", "quadrature"):
+                t, st = gpu_engine.ode(p, o, method=m)
+                assert torch_equal(t, one[m][0]) and torch_equal(st, one[m][1]), (log2, m)
+            t, st = gpu_engine.ode(p, o, group_waves=False)
+            assert torch_equal(t, mixed[0]) and torch_equal(st, mixed[1])
+        finally:
+            gpu_engine.tune_ode_launch_steps(prev)
+    assert bool((one["radau"][1] == 0).all())
+    # the cap still applies across launches
+    prev = gpu_engine.tune_ode_launch_steps(10)
+    try:
+        t, st = gpu_engine.ode(p[:2], o[:2], max_steps=5000)
+    finally:
+        gpu_engine.tune_ode_launch_steps(prev)
+    assert st.cpu().tolist() == [3, 3] and bool(torch_isnan(t[:, :5]))
+
+
+def torch_isnan(t):
+    import torch
+    return torch.isnan(t).all()
+
+
+def test_long_window_completes_through_cli(gpu_engine, tmp_path):
+    """m_chi = 3500 GeV with sigma_v = 1e-12 over the shipped window needs ~7e7 fixed Radau steps
+    (fpy:403-404), beyond round 2's 2^26 cap: the reference integrates it (slowly), and so does
+    lzq now, in continuation launches, through the CLI (yields_out.json written, no [warn]).
+    Y_B does not depend on sigma_v (its equation is linear, fpy:285), so it is checked against
+    the exact quadrature form of the same window at sigma_v = 0."""
+    import json
+    from test_cli import run_cli
+    cfg = dict(full_cfg(BASE_CFG), m_chi_GeV=3500.0, sigma_v_chi_GeV_m2=1e-12)
+    p, _ = recs([cfg])
+    n = pkg("engine").ode_step_counts(p)[0]
+    assert n > 2 ** 26, n
+    (tmp_path / "cfg.json").write_text(json.dumps({k: v for k, v in cfg.items()}))
+    out = run_cli(["--config", "cfg.json"], tmp_path)
+    assert "[warn]" not in out and "Wrote yields_out.json" in out
+    fin = json.loads((tmp_path / "yields_out.json").read_text())["final"]
+    assert all(np.isfinite(v) for v in fin.values()), fin
+    assert 0.0 < fin["Y_chi"] <= cfg["Y_chi_init"]
+    q, sq = gpu_engine.ode(*recs([dict(cfg, sigma_v_chi_GeV_m2=0.0)]), method="quadrature")
+    yb = float(q.cpu().numpy()[0, 0])
+    print(f"m_chi = 3500 GeV, {n:.3g} Radau steps: Y_B {fin['Y_B']!r} vs converged quadrature {yb!r} "
+          f"(rel {rel_err(fin['Y_B'], yb):.2e}); Y_chi {fin['Y_chi']!r}")
+    assert int(sq[0]) == 0 and rel_err(fin["Y_B"], yb) < 1e-6
+
+
+def test_ode_quadrature_narrow_window_resolved(gpu_engine):
+    """the quadrature form clamped its sub-intervals and could miss a narrow source
+    window.  It now integrates only where the window is not exactly 0 in double (|q| <= 40), so
+    the sub-interval count no longer grows as sigma_y shrinks: Y_B / sigma_y converges as
+    sigma_y -> 0 (the window integrates to sigma sqrt(2 pi)); a scale it still cannot resolve
+    (a wash-out rate of 1e9) is reported as LZQ_ODE_UNRESOLVED with NaN yields, never a silent
+    answer."""
+    rows = []
+    for sig in (1e-4, 1e-5, 1e-6):
+        cfg = full_cfg({**BASE_CFG, **NARROW, "Gamma_wash_over_H": 0.5, "source_shape_sigma_y": sig})
+        q, sq = gpu_engine.ode(*recs([cfg]), method="quadrature")
+        assert int(sq[0]) == 0
+        rows.append(float(q.cpu().numpy()[0, 0]) / sig)
+    print("Y_B / sigma_y:", rows)
+    assert rows[2] > 0 and abs(rows[1] / rows[2] - 1.0) < 1e-6 and abs(rows[0] / rows[2] - 1.0) < 1e-4
+    cfg = full_cfg({**BASE_CFG, **NARROW, "Gamma_wash_over_H": 1e9})
+    q, sq = gpu_engine.ode(*recs([cfg]), method="quadrature")
+    assert int(sq[0]) == pkg("_native").ODE_UNRESOLVED and np.isnan(q.cpu().numpy()[0, :5]).all()
+
+
+def test_sweep_masks_failed_ode_points(gpu_engine, tmp_path):
+    """ODE-path points that did not finish normally are NaN rows of a sweep
+    table and are counted per status in summary.json (here: the quadrature form's unresolved
+    status next to normal points)."""
+    import json
+    sw = pkg("sweep")
+    spec_d = {"name": "fail", "base": {**NARROW}, "ode_method": "quadrature",
+              "axes": [{"field": "Gamma_wash_over_H", "values": [0.5, 1e9]},
+                       {"field": "delta_LZ", "values": [1e-3, 0.1]}]}
+    (tmp_path / "spec.json").write_text(json.dumps(spec_d))
+    sw.main(["--spec", str(tmp_path / "spec.json"), "--out", str(tmp_path / "out")])
+    tab = np.load(tmp_path / "out" / "table.npy")
+    summ = json.loads((tmp_path / "out" / "summary.json").read_text())
+    assert np.isfinite(tab[:2]).all() and np.isnan(tab[2:, :5]).all()
+    assert summ["ode_status"] == {"ok": 2, "quadrature_unresolved": 2}
+    assert summ["final"]["Y_B"]["n_nonfinite"] == 2

@@ -118,6 +118,26 @@ def test_shipped_module_multi_crossing_and_profile(tmp_path, plugin_path, gpu_en
     assert 0.0 < P3 < 1.0
 
 
+def test_sampled_levels_format_spline_crossings(tmp_path, plugin_path, gpu_engine):
+    """xi,Delta,m_mix samples through the GPU splines: linear samples are reproduced exactly
+    (crossing at xi = 1, |Delta'| = 1, m_mix = 0.2); a zero sample that is a sign change is a
+    crossing on the knot, and a later root of the cubic is found as the numpy restatement finds
+    it."""
+    import profile_ref as R
+    tfp = importlib.import_module("transport_from_profile")
+    rows = "".join(f"{x!r},{x - 1.0!r},{0.1 + 0.1 * x!r}\n" for x in (0.0, 0.5, 0.75, 1.25, 2.0))
+    (tmp_path / "b.csv").write_text("xi,Delta,m_mix\n" + rows)
+    xs, ms, ds, _ = tfp.read_profile(str(tmp_path / "b.csv"))
+    assert len(xs) == 1 and abs(xs[0] - 1.0) < 1e-15 and abs(ds[0] - 1.0) < 1e-14 and abs(ms[0] - 0.2) < 1e-15
+    x, D, m = [-1.0, 0.0, 1.0, 2.0], [-1.0, 0.0, 1.0, -1.0], [0.1, 0.1, 0.1, 0.3]
+    (tmp_path / "c.csv").write_text("xi,Delta,m_mix\n" + "".join(f"{a},{b},{c}\n" for a, b, c in zip(x, D, m)))
+    xs, ms, ds, _ = tfp.read_profile(str(tmp_path / "c.csv"))
+    ref = R.crossings(x, R.spline_coefs(x, m), R.spline_coefs(x, [-d for d in D]), 0.0, 1.0, 1.0, 1.0)
+    assert len(xs) == 2 == len(ref) and xs[0] == 0.0
+    for (a, b, c), (rx, rd, rm, _) in zip(zip(xs, ms, ds), ref):
+        assert abs(a - rx) < 1e-14 and abs(b - rm) < 1e-14 and abs(c - abs(rd)) < 1e-14
+
+
 def _tanh_csv(path, yB, ychi, lam, extra="", header="xi,phi,Phi", shift=0.0, n=8001, span=4.0):
     xs = np.linspace(-span, span, n)
     phi, Phi = 0.5 * (1.0 - np.tanh(xs)), 0.65 * (1.0 + np.tanh(xs))

@@ -1,0 +1,66 @@
+"""Bounce-profile batches for the GPU profile path (include/lzq.h lzq_profile_*; PAPER p.3 §3,
+eqs.(5)-(9); the reference's hook imports the absent `transport_from_profile` for this, fpy:173).
+
+A batch is a set of profile SHAPES (the bounce's background fields phi(xi), Phi(xi) on knots)
+and POINTS (a shape + the couplings y_B, y_chi, lambda_tr_eff and the wall speed v_w).  The
+reference ships no bounce solution, so `synthetic_shapes` generates a reproducible family with
+the structure of one: phi a kink wall, Phi a wall displaced from it with a bounce-shaped bump
+(several Delta = 0 crossings for a range of couplings).  Its only use is as benchmark and test
+input; users pass their own solver's samples.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def synthetic_shapes(n_shapes: int = 16, n_knots: int = 256, span: float = 12.0, seed: int = 6):
+    """(knots, phi, Phi), each [n_shapes, n_knots]: xi in [-span, span] (wall width 1),
+    phi = v/2 (1 - tanh(xi)), Phi = V/2 (1 + tanh(xi - s)) + A exp(-((xi - c)/b)^2) sin(k xi),
+    with (v, V, s, A, c, b, k) drawn from numpy default_rng(seed)."""
+    rng = np.random.default_rng(seed)
+    x = np.linspace(-span, span, n_knots)
+    X = np.broadcast_to(x, (n_shapes, n_knots)).copy()
+    v = rng.uniform(0.8, 1.2, (n_shapes, 1))
+    V = rng.uniform(0.8, 1.6, (n_shapes, 1))
+    s = rng.uniform(-1.0, 1.0, (n_shapes, 1))
+    A = rng.uniform(0.5, 1.5, (n_shapes, 1))
+    c = rng.uniform(-2.0, 2.0, (n_shapes, 1))
+    b = rng.uniform(1.0, 3.0, (n_shapes, 1))
+    k = rng.uniform(1.0, 3.0, (n_shapes, 1))
+    phi = 0.5 * v * (1.0 - np.tanh(X))
+    Phi = 0.5 * V * (1.0 + np.tanh(X - s)) + A * np.exp(-((X - c) / b) ** 2) * np.sin(k * X)
+    return X, phi, Phi
+
+
+def synthetic_couplings(n_points: int, n_shapes: int, seed: int = 6):
+    """Per-point (y_B, y_chi, lambda_tr_eff, v_w, shape), points grouped by shape (the launch order
+    the kernel's per-block LDS staging of a shape wants): y_B, y_chi ~ U(0.5, 2),
+    lambda_tr_eff log-uniform on [1e-3, 1], v_w ~ U(0.1, 0.9), numpy default_rng(seed + 1)."""
+    rng = np.random.default_rng(seed + 1)
+    yB = rng.uniform(0.5, 2.0, n_points)
+    ychi = rng.uniform(0.5, 2.0, n_points)
+    lam = 10.0 ** rng.uniform(-3.0, 0.0, n_points)
+    vw = rng.uniform(0.1, 0.9, n_points)
+    shape = (np.arange(n_points) * n_shapes) // n_points
+    return yB, ychi, lam, vw, shape.astype(np.int32)
+
+
+def interval_steps(knots, coef, yB, ychi, lam, vw, spr: float = 3.0, n_min: int = 1,
+                   hdot_rate: float = 4.0) -> np.ndarray:
+    """Magnus steps per point of lzq_lz_propagate_profile (its per-interval rule, vectorised over
+    points; knots [n_knots], coef [n_knots - 1, 8] of ONE shape): the launch's work model."""
+    total = np.zeros(np.broadcast(yB, ychi, lam, vw).shape)
+    for j in range(len(knots) - 1):
+        L = knots[j + 1] - knots[j]
+        w = np.zeros_like(total)
+        for f in (0.0, 0.25, 0.5, 0.75, 1.0):
+            t = f * L
+            pw = np.array([1.0, t, t * t, t * t * t])
+            dpw = np.array([0.0, 1.0, 2.0 * t, 3.0 * t * t])
+            a, b = coef[j, :4] @ pw, coef[j, 4:] @ pw
+            da, db = coef[j, :4] @ dpw, coef[j, 4:] @ dpw
+            D, m = yB * a - ychi * b, lam * a
+            Dd, md = yB * da - ychi * db, lam * da
+            w = np.maximum(w, np.maximum(np.sqrt(D * D + m * m), hdot_rate * np.sqrt(vw * np.sqrt(Dd * Dd + md * md))))
+        total += np.maximum(n_min, np.ceil(spr * (L / vw) * w))
+    return total

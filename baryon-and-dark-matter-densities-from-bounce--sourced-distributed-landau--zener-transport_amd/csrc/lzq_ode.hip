@@ -86,6 +86,9 @@ __device__ __forceinline__ OdePoint ode_point(const lzq_point& pt, const lzq_ode
   return o;
 }
 
+#ifndef LZQ_ODE_MIN_GROUP
+#define LZQ_ODE_MIN_GROUP 8  // smallest cooperative segment (64: whole wavefronts only, round 2)
+#endif
 #ifndef LZQ_ODE_PREDICT
 #define LZQ_ODE_PREDICT 1  // Radau5 collocation predictor for the Riccati Newton iteration
 #endif
@@ -661,26 +664,35 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
     // them.  The ingredients of a step are computed once instead of 64 times; the arithmetic is
     // the same (ode_stage = stage_scale(ode_stage_base)), so results are bit-identical to the
     // per-lane mode.  Split steps (the T = m/3 branch) always evaluate their own stages.
+    // Sub-groups: a wave whose aligned G-lane segments (G = 32, 16, 8) are each uniform, though
+    // the wave is not (sweeps with fewer than 64 points per stage key, e.g. many m_chi values),
+    // runs the same scheme per segment: lane l of a segment evaluates step kb + l of ITS
+    // segment's key into its own LDS row, and the segment integrates blocks of G steps from its G
+    // rows (segments may differ in N and h; they never touch each other's rows).
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    bool coop = false;
-    if (LZQ_ODE_COOP && coop_on) {
-      auto same = [](double v) {  // bit-equal to lane 0's value (the wave is full here)
-        const uint64_t b = __builtin_bit_cast(uint64_t, v);
-        return b == __builtin_bit_cast(uint64_t, __shfl(v, 0, 64));
-      };
-      const bool eq = same(o.m) && same(o.Tp) && same(o.B) && same(o.sig) && same(o.H0) && same(o.s0) &&
-                      same(o.c_rel) && same(o.c_nr) && same(o.v0) && same(o.T_lo) && same(o.T_hi) &&
-                      same(__builtin_bit_cast(double, w)) && (!kChiOnly || same((double)o.deplete));
-      coop = __ballot(1) == ~0ull && __all(eq);
+    int G = 0;  // cooperative segment width (0: per-lane)
+    if (LZQ_ODE_COOP && coop_on && __ballot(1) == ~0ull) {
+      for (int g = 64; g >= LZQ_ODE_MIN_GROUP && G == 0; g >>= 1) {
+        auto same = [g](double v) {  // bit-equal to the value of the first lane of the g-segment
+          const uint64_t b = __builtin_bit_cast(uint64_t, v);
+          return b == __builtin_bit_cast(uint64_t, __shfl(v, 0, g));
+        };
+        const bool eq = same(o.m) && same(o.Tp) && same(o.B) && same(o.sig) && same(o.H0) && same(o.s0) &&
+                        same(o.c_rel) && same(o.c_nr) && same(o.v0) && same(o.T_lo) && same(o.T_hi) &&
+                        same(__builtin_bit_cast(double, w)) && (!kChiOnly || same((double)o.deplete));
+        if (__all(eq)) G = g;
+      }
 #ifdef LZQ_ODE_COOP_DEBUG
-      dbg_coop = coop ? 1.0 : 0.0;
+      dbg_coop = (double)G;
 #endif
     }
-    const int64_t block = coop ? 64 : N;
+    const bool coop = G > 0;
+    const int seg = lane & ~(G - 1);  // first LDS row of this lane's segment (G > 0)
+    const int64_t block = coop ? G : N;
     for (int64_t kb = k_begin; kb < k_stop; kb += block) {
       const int64_t kend = kb + block < k_stop ? kb + block : k_stop;
       if (coop) {
-        const int64_t kl = kb + lane;
+        const int64_t kl = kb + (lane - seg);
         if (kl < kend) {
           const double xk = x0 + (double)kl * h;
 #pragma unroll
@@ -720,7 +732,8 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
           if (coop && !split) {
 #pragma unroll
             for (int j = 0; j < 3; ++j)
-              sg[j] = (kChiOnly && !o.deplete) ? chi_scale(o, s_base[wv][k - kb][j]) : stage_scale(o, s_base[wv][k - kb][j]);
+              sg[j] = (kChiOnly && !o.deplete) ? chi_scale(o, s_base[wv][seg + (k - kb)][j])
+                                               : stage_scale(o, s_base[wv][seg + (k - kb)][j]);
           } else {
 #pragma unroll
             for (int j = 0; j < 3; ++j)
@@ -772,7 +785,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
     r.DM_over_B = r.rho_DM_kg_m3 / pymax(r.rho_B_kg_m3, 1e-300);
   }
 #ifdef LZQ_ODE_COOP_DEBUG
-  r.P_used = dbg_coop;  // debug builds only: 1 = cooperative wavefront, 0 = per-lane
+  r.P_used = dbg_coop;  // debug builds only: the cooperative segment width G (64 = whole wave), 0 = per-lane
 #endif
   if (!real) return;
   out[i] = r;

@@ -421,7 +421,7 @@ class Engine:
         return out
 
     def lz_propagate_profile(self, shapes: "ProfileShapes", points: torch.Tensor, steps_per_radian: float = 3.0,
-                             min_steps: int = 8) -> torch.Tensor:
+                             min_steps: int = 1) -> torch.Tensor:
         """Coherent conversion probability through each point's whole profile
         (lzq_lz_propagate_profile)."""
         n = points.numel() // _native.PROFILE_POINT_DTYPE.itemsize

@@ -164,7 +164,7 @@ def _edge(cD, cM, t, v_w):
 
 # ---- propagation ---------------------------------------------------------------------------
 STEPS_PER_RADIAN = 3.0
-MIN_STEPS = 8
+MIN_STEPS = 1
 HDOT_RATE = 4.0   # the crossing region's rate: HDOT_RATE / (LZ time), LZ time = |dH/dt|^-1/2
 
 

@@ -112,6 +112,27 @@ def test_config_grid_vs_oracle(gpu_engine, name):
             assert len(seen) >= 5, field
 
 
+@pytest.mark.parametrize("name,start", [("C2", 123_456), ("C3", 50 * 100_000 + 20_000)])
+def test_config_full_occupancy_launch(gpu_engine, name, start):
+    """One lzq_sweep_grid launch over a contiguous 65,536-index slice (1024 blocks of 16
+    wavefronts: the multi-wave, many-block geometry of the production sweeps, which the one-point
+    launches of test_config_grid_vs_oracle do not exercise), 256 default_rng(0)-sampled rows vs the
+    oracle at the guard band.  The C3 slice (m_chi index 50, m_chi = 59 GeV) has its T = m/3
+    branch inside the integration window."""
+    spec = pkg("sweep").builtin_specs()[name]
+    n = 65_536
+    t = gpu_engine.sweep(spec.base, spec.axes, start, n).cpu().numpy()
+    assert np.isfinite(t).all()
+    sub = np.sort(np.random.default_rng(0).choice(n, 256, replace=False))
+    cfgs = [oracle_cfg(spec, start + int(i)) for i in sub]
+    if name == "C3":
+        m = {c["m_chi_GeV"] for c in cfgs}
+        assert all(0.1 < mm / 3 < 500.0 for mm in m), m
+    check_vs_oracle(t[sub], cfgs, f"{name} 65536-point launch")
+    # the same rows from one-point launches: bit-identical (geometry-independent results)
+    assert np.array_equal(grid_rows(gpu_engine, spec, [start + int(i) for i in sub[:16]]), t[sub[:16]])
+
+
 def test_config_C4_full_block_properties(gpu_engine):
     """One contiguous 1e6-point block of the 1e8-point C4 grid (beta/H index 3, I_p indices
     40..49, every other axis in full): size-independent properties of the reference's formulas."""

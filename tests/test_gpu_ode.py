@@ -441,3 +441,39 @@ def test_sweep_masks_failed_ode_points(gpu_engine, tmp_path):
     assert np.isfinite(tab[:2]).all() and np.isnan(tab[2:, :5]).all()
     assert summ["ode_status"] == {"ok": 2, "quadrature_unresolved": 2}
     assert summ["final"]["Y_B"]["n_nonfinite"] == 2
+
+
+def test_ode_cooperative_subgroups_bit_identical(gpu_engine):
+    """Cooperative sub-groups: waves whose aligned 32/16/8-lane segments are each uniform in the
+    stage key (here 16 and 8 points per m_chi value, in launch order) run cooperatively per
+    segment, with segments of different N and step size in one wave; results equal the per-lane
+    mode bit for bit, for the Radau path and the quadrature method's Riccati stepping, also as
+    continuation launches."""
+    rng = np.random.default_rng(77)
+    cfgs = []
+    for block, n_keys in ((16, 8), (8, 16)):
+        for kk in range(n_keys):
+            m_chi = float(10 ** rng.uniform(-0.5, 1.8))
+            win = dict(T_max_over_Tp=float(rng.uniform(1.3, 1.8)), T_min_over_Tp=float(rng.uniform(0.5, 0.7)))
+            for _ in range(block):
+                c = full_cfg(BASE_CFG)
+                c.update(win, m_chi_GeV=m_chi, P_chi_to_B=float(rng.uniform(0.05, 1.0)),
+                         Gamma_wash_over_H=float(rng.choice([0.5, 2.0])),
+                         sigma_v_chi_GeV_m2=float(rng.choice([0.0, 1e-16, 1e-12])),
+                         regime=str(rng.choice(["thermal", "nonthermal"])))
+                cfgs.append(c)
+    p, o = recs(cfgs)
+    for method in ("radau", "quadrature"):
+        a, sa = gpu_engine.ode(p, o, method=method, group_waves=False)
+        prev = gpu_engine.tune_ode_coop(False)
+        try:
+            b, sb = gpu_engine.ode(p, o, method=method, group_waves=False)
+        finally:
+            gpu_engine.tune_ode_coop(prev)
+        assert bool((sa == 0).all()) and torch_equal(sa, sb) and torch_equal(a, b), method
+        prev = gpu_engine.tune_ode_launch_steps(11)
+        try:
+            c, sc = gpu_engine.ode(p, o, method=method, group_waves=False)
+        finally:
+            gpu_engine.tune_ode_launch_steps(prev)
+        assert torch_equal(a, c) and torch_equal(sa, sc), method

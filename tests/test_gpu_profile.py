@@ -179,7 +179,7 @@ def _linear_shape(engine, c):
 
 def _profile_P(engine, c, spr):
     sh = _linear_shape(engine, c)
-    return engine.lz_propagate_profile(sh, engine.profile_points(0.0, -1.0, 1.0, WEBER["v_w"], 0), spr, 8)
+    return engine.lz_propagate_profile(sh, engine.profile_points(0.0, -1.0, 1.0, WEBER["v_w"], 0), spr)
 
 
 def test_piecewise_linear_profile_matches_lz_propagate(gpu_engine):

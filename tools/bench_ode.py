@@ -109,6 +109,27 @@ def main():
                       "bit_identical": bool(torch.equal(res[True][1], res[False][1])),
                       "all_ok": bool((res[True][2] == 0).all())}), flush=True)
 
+    # a sweep with only 16 points per stage key (n/16 m_chi values x 16 sigma_v values): whole
+    # wavefronts can never be uniform, so cooperation happens in 16-lane sub-groups
+    cfgs = cfgs_for({"T_max_over_Tp": 1.6, "T_min_over_Tp": 0.6}, n)
+    mchi = np.logspace(-0.5, 1.8, n // 16)
+    for i, c in enumerate(cfgs):
+        c["m_chi_GeV"] = float(mchi[i // 16])
+        c["sigma_v_chi_GeV_m2"] = float(10.0 ** (-20 + (i % 16) * 0.5))
+    pts = np.concatenate([cfgm.to_point(c) for c in cfgs])
+    ods = np.concatenate([cfgm.to_ode_params(c) for c in cfgs])
+    eng.ode(pts[:4096], ods[:4096])
+    (tab, st), dt = timed(lambda: eng.ode(pts, ods, chunk=chunk))
+    prev = eng.tune_ode_coop(False)
+    try:
+        (tab0, st0), dt0 = timed(lambda: eng.ode(pts, ods, chunk=chunk))
+    finally:
+        eng.tune_ode_coop(prev)
+    print(json.dumps({"config": "narrow_riccati_16_per_key", "points": n, "stage_keys": n // 16,
+                      "gpu_points_per_s_subgroups": n / dt, "gpu_points_per_s_per_lane": n / dt0,
+                      "bit_identical": bool(torch.equal(tab, tab0)) and bool(torch.equal(st, st0)),
+                      "all_ok": bool((st == 0).all())}), flush=True)
+
 
 if __name__ == "__main__":
     main()

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Which mode ode_integrate_kernel's wavefronts ran in, with a -DLZQ_ODE_COOP_DEBUG build under
-<package>/_build/variants (the kernel then writes 1 = cooperative / 0 = per-lane into P_used):
+<package>/_build/variants (the kernel then writes the cooperative segment width G -- 64 = whole
+wavefront, 32/16/8 = sub-groups -- or 0 = per-lane into P_used):
     python tools/build_variants.py LZQ_ODE_COOP_DEBUG=1 && python tools/dbg_ode_coop.py"""
 import sys, glob, importlib, numpy as np
 sys.path.insert(0,'.'); sys.path.insert(0,'tools')

@@ -64,3 +64,37 @@ def interval_steps(knots, coef, yB, ychi, lam, vw, spr: float = 3.0, n_min: int 
             w = np.maximum(w, np.maximum(np.sqrt(D * D + m * m), hdot_rate * np.sqrt(vw * np.sqrt(Dd * Dd + md * md))))
         total += np.maximum(n_min, np.ceil(spr * (L / vw) * w))
     return total
+
+
+def read_bounce_csv(path: str):
+    """The bounce-profile CSV of plugins/transport_from_profile.py (header `xi,phi,Phi`, or
+    `r,phi,Phi` with `# R0 = ...`; `# key = value` option lines) -> (xi, phi, Phi, options)."""
+    opts, header, rows = {}, None, []
+    with open(path) as f:
+        for raw in f:
+            line = raw.strip()
+            if not line:
+                continue
+            if line.startswith("#"):
+                body = line.lstrip("#").strip()
+                if "=" in body:
+                    k, v = (t.strip() for t in body.split("=", 1))
+                    try:
+                        opts[k] = float(v)
+                    except ValueError:
+                        opts[k] = v
+                continue
+            cells = [c.strip() for c in line.split(",")]
+            if header is None:
+                header = cells
+            else:
+                rows.append([float(c) for c in cells])
+    if header is None or len(rows) < 4:
+        raise ValueError(f"{path}: a bounce profile needs a header and >= 4 rows")
+    col = {h: i for i, h in enumerate(header)}
+    low = {h.lower(): i for i, h in enumerate(header)}
+    if not ("phi" in col and "Phi" in col and ("xi" in low or "r" in low)):
+        raise ValueError(f"{path}: header must be 'xi,phi,Phi' or 'r,phi,Phi', got {header}")
+    a = np.asarray(rows, dtype=np.float64)
+    xi = a[:, low["xi"]] if "xi" in low else a[:, low["r"]] - float(opts.get("R0", 0.0))
+    return xi, a[:, col["phi"]], a[:, col["Phi"]], opts

@@ -52,6 +52,9 @@ constexpr int kProfBlock = 256;
 #ifndef LZQ_PROF_MIN_WAVES
 #define LZQ_PROF_MIN_WAVES 2
 #endif
+#ifndef LZQ_PROF_UNROLL
+#define LZQ_PROF_UNROLL 2  // Magnus steps per loop iteration (ILP across steps)
+#endif
 constexpr double kMaxIntervalSteps = 16777216.0;  // per knot interval; beyond: P = NaN (absurd input)
 constexpr int kProfCoef = 8;                      // doubles per interval row
 constexpr double kHdotRate = 4.0;  // crossing-region rate: kHdotRate / (LZ time), LZ time = |dH/dt|^-1/2
@@ -266,8 +269,9 @@ __global__ __launch_bounds__(kProfBlock) void profile_crossings_kernel(
 // (md, mdd) (lzq_propagator.hip dressed_basis with m(t) varying; tests/profile_ref.py
 // dressed_chi_like): theta = atan2(m, D)/2, theta' = (m' D - m D')/(2 E^2), eps = theta'/(2E),
 // eps' = theta''/(2E) - theta' E'/(2E^2), beta = -i eps - eps'/(2E).
-__device__ void dressed_chi_like(double D, double Dd, double Ddd, double m, double md, double mdd, Cplx& u0,
-                                 Cplx& u1) {
+// (out of line: its atan2 / sincos would otherwise set the step loop's register budget)
+__device__ __noinline__ void dressed_chi_like(double D, double Dd, double Ddd, double m, double md, double mdd,
+                                              Cplx& u0, Cplx& u1) {
   const double E2 = D * D + m * m;
   const double E = sqrt(E2);
   const double th = 0.5 * atan2(m, D);
@@ -297,6 +301,26 @@ __device__ __forceinline__ void edge_state(const double* cD, const double* cM, d
   const double v2 = vw * vw;
   dressed_chi_like(pp0(cD, t), vw * pp1(cD, t), v2 * pp2(cD, t), pp0(cM, t), vw * pp1(cM, t), v2 * pp2(cM, t), u0,
                    u1);
+}
+
+// cos|n| and sin|n|/|n| from |n|^2: at >= 3 steps per radian |n|^2 <~ 0.12, where the Taylor
+// series need only 7 (sinc) and 8 (cos) terms for < 1e-16 at |n|^2 <= 1/4 (lzq_su2.h cos_sinc,
+// 9 and 10 terms up to 1, beyond it).
+#ifndef LZQ_PROF_SHORTSC
+#define LZQ_PROF_SHORTSC 1
+#endif
+__device__ __forceinline__ void cos_sinc_short(double x2, double& cs, double& sc) {
+  if (LZQ_PROF_SHORTSC && x2 <= 0.25) {
+    double ps = kSincC[6], pc = kCosC[7];
+#pragma unroll
+    for (int k = 5; k >= 0; --k) ps = __builtin_fma(ps, x2, kSincC[k]);
+#pragma unroll
+    for (int k = 6; k >= 0; --k) pc = __builtin_fma(pc, x2, kCosC[k]);
+    sc = ps;
+    cs = pc;
+  } else {
+    cos_sinc(x2, cs, sc);
+  }
 }
 
 // uniform Magnus steps on one interval (tests/profile_ref.py interval_steps, same operations)
@@ -364,7 +388,7 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_propag
     const double k2 = (kSq15 / 3.0) * dt, k3 = (10.0 / 3.0) * dt;
     const double gh1 = g1 * h, gh2 = 0.5 * h, gh3 = g3 * h;
 #define FMA __builtin_fma
-#pragma unroll 2
+#pragma unroll LZQ_PROF_UNROLL
     for (int st = 0; st < S; ++st) {
       const double t0 = (double)st * h;
       const double t1 = t0 + gh1, t2 = t0 + gh2, t3 = t0 + gh3;
@@ -390,7 +414,7 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_propag
       const double ny = FMA(Lz, Rx, -(Lx * Rz)) * (1.0 / 120.0);
       const double nz = FMA(FMA(Lx, C2y, -(c * Rx)), 1.0 / 120.0, FMA(z3, 1.0 / 12.0, z1));
       double cs, sc;
-      cos_sinc(FMA(nx, nx, FMA(ny, ny, nz * nz)), cs, sc);
+      cos_sinc_short(FMA(nx, nx, FMA(ny, ny, nz * nz)), cs, sc);
       su2_apply(cs, sc * nx, sc * ny, sc * nz, p0, p1);
     }
 #undef FMA

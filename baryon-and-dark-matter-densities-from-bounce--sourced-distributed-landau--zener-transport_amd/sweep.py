@@ -66,6 +66,36 @@ class CrossingSpec:
         return np.random.default_rng(self.seed).uniform(-1.0, 1.0, (3, self.n_cross))
 
 
+PROFILE_FIELDS = ("y_B", "y_chi", "lambda_tr_eff")   # PAPER eqs.(5),(7): sweep axes of a profile spec
+
+
+@dataclass
+class ProfileSpec:
+    """P of every grid point from ONE bounce profile (PAPER p.3 eqs.(5)-(9); the plug-in path of
+    fpy:170-187 as a sweep): the profile's phi, Phi (a CSV in transport_from_profile's `xi,phi,Phi`
+    format, or shape `synthetic` of bounce.synthetic_shapes) with the couplings y_B, y_chi,
+    lambda_tr_eff (these defaults, or sweep axes of those names) and the point's v_w.
+    estimator: "auto" (one crossing -> eq.(9) of its delta_LZ; otherwise the time-ordered
+    propagation through the profile), "minimal" (eq.(9); points without exactly one crossing get
+    P = NaN) or "propagate" (every point through the whole profile)."""
+    csv: Optional[str] = None
+    synthetic: int = 0
+    estimator: str = "auto"
+    y_B: float = 1.0
+    y_chi: float = 1.0
+    lambda_tr_eff: float = 0.1
+    steps_per_radian: float = 3.0
+    min_steps: int = 1
+
+    def arrays(self):
+        from . import bounce
+        if self.csv:
+            x, a, b, _ = bounce.read_bounce_csv(self.csv)
+            return x, a, b
+        X, A, B = bounce.synthetic_shapes(max(self.synthetic + 1, 1))
+        return X[self.synthetic], A[self.synthetic], B[self.synthetic]
+
+
 @dataclass
 class SweepSpec:
     name: str
@@ -75,6 +105,7 @@ class SweepSpec:
     notes: str = ""
     crossings: Optional[CrossingSpec] = None
     ode_method: str = "radau"   # ODE-path points: "radau" (the reference's integrator) | "quadrature" (opt-in)
+    profile: Optional[ProfileSpec] = None
 
     @property
     def total(self) -> int:
@@ -98,7 +129,20 @@ class SweepSpec:
             d["crossings"] = dict(self.crossings.__dict__)
         if self.ode_method != "radau":
             d["ode_method"] = self.ode_method
+        if self.profile is not None:
+            d["profile"] = dict(self.profile.__dict__)
         return d
+
+    def axis_values(self, start: int, count: int, device) -> dict:
+        """{axis name: [count] torch tensor} of grid indices [start, start+count) (C order)."""
+        import torch
+        idx = torch.arange(start, start + count, dtype=torch.int64, device=device)
+        vals, stride = {}, 1
+        for name, v in reversed(self.axes):
+            t = torch.as_tensor(np.asarray(v, dtype=np.float64), device=device)
+            vals[name] = t[(idx // stride) % len(v)]
+            stride *= len(v)
+        return vals
 
     def crossing_arrays(self, start: int, count: int, device):
         """Per-point crossing parameters [count, n_cross] (torch, on `device`) for C5."""
@@ -151,6 +195,8 @@ def grid_records(spec: "SweepSpec", start: int, count: int, engine=None):
         stride *= len(vals)
         if name in ("delta_LZ", "m_mix", "dprime"):
             lz[name] = v
+        elif name in PROFILE_FIELDS:
+            continue          # P comes from the profile (profile_P)
         elif name in ODE_FIELDS:
             ods[name] = v if name != "deplete_DM_from_source" else (v != 0).astype(np.int32)
         elif name == "Y_chi_init":
@@ -180,7 +226,7 @@ def _axis_from_json(a: dict) -> Tuple[str, np.ndarray]:
         v = np.linspace(*a["linspace"][:2], int(a["linspace"][2]))
     else:
         raise ValueError(f"axis {a!r} needs values / linspace / logspace")
-    if a["field"] not in _native.FIELD and a["field"] not in ODE_FIELDS:
+    if a["field"] not in _native.FIELD and a["field"] not in ODE_FIELDS and a["field"] not in PROFILE_FIELDS:
         raise ValueError(f"unknown sweep field {a['field']!r}")
     return a["field"], v
 
@@ -195,8 +241,15 @@ def spec_from_json(d: dict) -> SweepSpec:
     method = d.get("ode_method", "radau")
     if method not in ("radau", "quadrature"):
         raise ValueError(f"ode_method must be 'radau' or 'quadrature', got {method!r}")
-    return SweepSpec(d.get("name", "custom"), base, [_axis_from_json(a) for a in d["axes"]], int(d.get("n_y", 8000)),
-                     d.get("notes", ""), cr, method)
+    prof = ProfileSpec(**d["profile"]) if d.get("profile") else None
+    if prof is not None and prof.estimator not in ("auto", "minimal", "propagate"):
+        raise ValueError(f"profile estimator must be auto / minimal / propagate, got {prof.estimator!r}")
+    axes = [_axis_from_json(a) for a in d["axes"]]
+    if prof is None and any(n in PROFILE_FIELDS for n, _ in axes):
+        raise ValueError(f"axes {PROFILE_FIELDS} need a 'profile' section")
+    if prof is not None and cr is not None:
+        raise ValueError("a spec takes either 'crossings' or 'profile'")
+    return SweepSpec(d.get("name", "custom"), base, axes, int(d.get("n_y", 8000)), d.get("notes", ""), cr, method, prof)
 
 
 def builtin_specs() -> dict:
@@ -213,6 +266,11 @@ def builtin_specs() -> dict:
                         [("m_mix", ls(-3, 0, 1000)), ("dprime", ls(-3, 1, 1000))],
                         notes="C2 grid, 8 jittered sequential crossings per point, coherent P (propagator)",
                         crossings=CrossingSpec()),
+        "P1": SweepSpec("P1", dict(EQUAL_MASS),
+                        [("y_B", lin(0.5, 2.0, 100)), ("y_chi", lin(0.5, 2.0, 100)), ("lambda_tr_eff", ls(-3, 0, 100))],
+                        notes="P from a bounce profile (synthetic shape 0; PAPER eqs.(5)-(9)) over the couplings "
+                              "y_B x y_chi x lambda_tr_eff, then the dense quadrature",
+                        profile=ProfileSpec()),
         "C4": SweepSpec("C4", dict(EQUAL_MASS),
                         [("beta_over_H", ls(1, 3, 10)), ("I_p", lin(0.05, 1, 100)), ("v_w", lin(0.05, 0.95, 10)),
                          ("source_shape_sigma_y", lin(3, 30, 10)), ("m_chi_GeV", ls(-1, 3.5, 10)),
@@ -473,11 +531,48 @@ def coherent_P(spec: SweepSpec, s: int, n: int, engine):
     return engine.lz_propagate(m, dp, xi, vw, spec.crossings.window_lz, spec.crossings.steps)
 
 
+def profile_P(spec: SweepSpec, s: int, n: int, engine, cache: dict):
+    """P of grid points [s, s+n) from the spec's bounce profile (ProfileSpec; PAPER eqs.(5)-(9)):
+    the profile's splines once per sweep (cache), then per point the crossings and eq.(9) and/or
+    the time-ordered propagation through the profile, all on the GPU; a device tensor."""
+    import torch
+    ps = spec.profile
+    if "shape" not in cache:
+        cache["shape"] = engine.profile_shapes(*ps.arrays())
+    sh = cache["shape"]
+    vals = spec.axis_values(s, n, engine.device)
+    full = lambda k, d: vals[k] if k in vals else torch.full((n,), float(d), dtype=torch.float64, device=engine.device)
+    cols = [full("y_B", ps.y_B), full("y_chi", ps.y_chi), full("lambda_tr_eff", ps.lambda_tr_eff),
+            full("v_w", spec.base["v_w"])]
+    rec = torch.zeros((n, 5), dtype=torch.float64, device=engine.device)
+    for j, c in enumerate(cols):
+        rec[:, j] = c
+    pts = rec.view(torch.uint8)[:, :40].contiguous().view(-1)   # lzq_profile_point rows (shape 0, reserved 0)
+    if ps.estimator == "propagate":
+        return engine.lz_propagate_profile(sh, pts, ps.steps_per_radian, ps.min_steps)
+    cr = engine.profile_crossings(sh, pts, 1)
+    one = cr["count"] == 1
+    P = torch.where(one, engine.p_closed_form(cr["delta_lz"][:, 0]), torch.full_like(cols[0], float("nan")))
+    if ps.estimator == "auto" and not bool(one.all()):
+        sel = torch.nonzero(~one).reshape(-1)
+        P[sel] = engine.lz_propagate_profile(sh, pts.view(n, 40)[sel].contiguous().view(-1), ps.steps_per_radian,
+                                             ps.min_steps)
+    return P
+
+
+def grid_axes_for_kernel(spec: SweepSpec):
+    """The spec's axes for lzq_sweep_grid: a profile coupling axis has no lzq_point field, so it
+    rides on P_chi_to_B, which the per-point P override replaces (the flat-index decode of the
+    other axes is unchanged)."""
+    return [("P_chi_to_B" if n in PROFILE_FIELDS else n, v) for n, v in spec.axes]
+
+
 def make_compute(spec: SweepSpec, engine, reuse: bool = False) -> ComputeFn:
     """(start, count, out) -> None on the GPU: [coherent multi-crossing P ->] quadrature, or
     the ODE fallback (lzq_ode_batch) for sweeps over sigma_v / Gamma_wash / depletion (with or
     without crossings).  reuse: the quadrature's z-sums shared across points with the same
     y-grid and A/V kernel (lzq_sweep_grid_reuse; bit-identical, not the dense headline path)."""
+    pcache = {}   # the profile's device splines, built once per sweep
     if is_ode_spec(spec):
         counts = np.zeros(8, dtype=np.int64)   # ODE points per lzq_ode_status, this rank
 
@@ -486,6 +581,8 @@ def make_compute(spec: SweepSpec, engine, reuse: bool = False) -> ComputeFn:
             pts, ods = grid_records(spec, s, n, engine)
             if spec.crossings is not None:   # coherent multi-crossing P (propagator) for every point
                 pts["P_chi_to_B"] = coherent_P(spec, s, n, engine).cpu().numpy()
+            if spec.profile is not None:     # P from the bounce profile
+                pts["P_chi_to_B"] = profile_P(spec, s, n, engine, pcache).cpu().numpy()
             # fpy:372 per point: points with no sink/depletion take the quadrature, the rest the ODE
             ode = (ods["sigma_v_chi_GeV_m2"] != 0.0) | (ods["Gamma_wash_over_H"] != 0.0) | \
                   (ods["deplete_DM_from_source"] != 0)
@@ -507,7 +604,10 @@ def make_compute(spec: SweepSpec, engine, reuse: bool = False) -> ComputeFn:
 
     def compute(s, n, out):
         P_points = coherent_P(spec, s, n, engine) if spec.crossings is not None else None
-        engine.sweep(spec.base, spec.axes, s, n, n_y=spec.n_y, out=out, P_points=P_points, reuse=reuse)
+        if spec.profile is not None:
+            P_points = profile_P(spec, s, n, engine, pcache)
+        engine.sweep(spec.base, grid_axes_for_kernel(spec), s, n, n_y=spec.n_y, out=out, P_points=P_points,
+                     reuse=reuse)
     return compute
 
 
@@ -515,7 +615,7 @@ def main(argv=None):
     import torch
     import torch.distributed as dist
     ap = argparse.ArgumentParser(description="lzq parameter sweep (1..8 GPUs, RCCL all-gather)")
-    ap.add_argument("--spec", required=True, help="C2 | C3 | C4 | path to a sweep-spec JSON")
+    ap.add_argument("--spec", required=True, help="C2 | C3 | C4 | C5 | P1 | path to a sweep-spec JSON")
     ap.add_argument("--out", default=None, help="directory for shard checkpoints, table.npy, summary.json")
     ap.add_argument("--resume", action="store_true")
     ap.add_argument("--chunk", type=int, default=1 << 20)

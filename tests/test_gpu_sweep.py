@@ -185,3 +185,61 @@ def test_reuse_zsums_table_axes_and_overrides(gpu_engine):
     finally:
         gpu_engine.tune_exp(prev)
     assert torch.equal(dense, reuse)
+
+
+def test_profile_sweep_P1(gpu_engine):
+    """P1: P of every grid point from a bounce profile (PAPER eqs.(5)-(9)) through the sweep
+    driver.  P_used equals the engine's profile kernels on the same couplings bit for bit (eq.(9)
+    of the crossing's delta for one crossing, the propagation through the profile otherwise),
+    Y_B / P_used is the shipped config's quadrature per unit P, and 64 rows match the oracle."""
+    import torch
+    sw = pkg("sweep")
+    spec = sw.builtin_specs()["P1"]
+    s, n = 345_000, 4096
+    out = torch.empty((n, 6), dtype=torch.float64, device=gpu_engine.device)
+    sw.make_compute(spec, gpu_engine)(s, n, out)
+    t = out.cpu().numpy()
+    assert np.isfinite(t).all()
+    vals = {k: v.cpu().numpy() for k, v in spec.axis_values(s, n, "cpu").items()}
+    sh = gpu_engine.profile_shapes(*spec.profile.arrays())
+    pts = gpu_engine.profile_points(vals["y_B"], vals["y_chi"], vals["lambda_tr_eff"], spec.base["v_w"], 0)
+    cr = gpu_engine.profile_crossings(sh, pts, 1)
+    cnt = cr["count"].cpu().numpy()
+    P9 = gpu_engine.p_closed_form(cr["delta_lz"][:, 0]).cpu().numpy()
+    Pp = gpu_engine.lz_propagate_profile(sh, pts).cpu().numpy()
+    want = np.where(cnt == 1, P9, Pp)
+    assert (cnt == 1).any() and (cnt != 1).any(), np.unique(cnt)
+    assert np.array_equal(t[:, 5], want)
+    YB1 = 8.720885362714675e-11 / 0.14925839040304145
+    pos = t[:, 5] > 1e-6
+    assert np.max(np.abs(t[pos, 0] / t[pos, 5] / YB1 - 1.0)) < 1e-11
+    sub = np.sort(np.random.default_rng(2).choice(n, 64, replace=False))
+    cfgs = [full_cfg({**BASE_CFG, "P_chi_to_B": float(t[i, 5])}) for i in sub]
+    ref = O.points_batch(cfgs, nthreads=16)
+    assert np.max(np.abs(t[sub] - ref) / np.abs(ref)) < 1e-11
+
+
+def test_profile_sweep_csv_matches_plugin(gpu_engine, tmp_path, monkeypatch):
+    """A profile sweep over y_B from a bounce-profile CSV: its P_used is the plug-in module's
+    compute_prob_from_profile for the same couplings (the reference hook's path), bit for bit."""
+    import importlib
+    import json
+    import os
+    import torch
+    from conftest import ROOT
+    sw = pkg("sweep")
+    xs = np.linspace(-4.0, 4.0, 2001)
+    phi, Phi = 0.5 * (1.0 - np.tanh(xs)), 0.65 * (1.0 + np.tanh(xs))
+    body = "xi,phi,Phi\n" + "".join(f"{float(a)!r},{float(b)!r},{float(c)!r}\n" for a, b, c in zip(xs, phi, Phi))
+    (tmp_path / "bounce.csv").write_text(body)
+    yBs = [0.7, 1.0, 1.3, 1.9]
+    spec = sw.spec_from_json({"name": "csv", "profile": {"csv": str(tmp_path / "bounce.csv"), "y_chi": 0.8,
+                                                          "lambda_tr_eff": 0.1},
+                              "axes": [{"field": "y_B", "values": yBs}]})
+    out = torch.empty((4, 6), dtype=torch.float64, device=gpu_engine.device)
+    sw.make_compute(spec, gpu_engine)(0, 4, out)
+    monkeypatch.syspath_prepend(os.path.join(ROOT, "plugins"))
+    tfp = importlib.import_module("transport_from_profile")
+    for i, yB in enumerate(yBs):
+        (tmp_path / "p.csv").write_text(f"# y_B = {yB!r}\n# y_chi = 0.8\n# lambda_tr_eff = 0.1\n" + body)
+        assert out[i, 5].item() == tfp.compute_prob_from_profile(str(tmp_path / "p.csv"), 0.30), yB

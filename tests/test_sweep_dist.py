@@ -151,3 +151,26 @@ def test_spec_ode_method_roundtrip():
     assert sw.spec_key(again) != sw.spec_key(sw.spec_from_json({**d, "ode_method": "radau"}))
     with pytest.raises(ValueError):
         sw.spec_from_json({**d, "ode_method": "rk4"})
+
+
+def test_profile_spec_json_and_axis_mapping():
+    """A profile sweep (P from a bounce profile, PAPER eqs.(5)-(9)): JSON round trip, coupling axes
+    ride on P_chi_to_B for the grid kernel (overridden per point), and their names are rejected
+    without a 'profile' section."""
+    sw = pkg("sweep")
+    d = {"name": "prof", "profile": {"estimator": "propagate", "y_chi": 1.2},
+         "axes": [{"field": "y_B", "linspace": [0.5, 2.0, 4]}, {"field": "v_w", "values": [0.2, 0.4]}]}
+    spec = sw.spec_from_json(d)
+    assert spec.profile.estimator == "propagate" and spec.profile.y_chi == 1.2 and spec.total == 8
+    again = sw.spec_from_json(spec.to_json())
+    assert again.profile == spec.profile and sw.spec_key(again) == sw.spec_key(spec)
+    assert [n for n, _ in sw.grid_axes_for_kernel(spec)] == ["P_chi_to_B", "v_w"]
+    assert sw.spec_key(sw.spec_from_json({**d, "profile": {"estimator": "minimal"}})) != sw.spec_key(spec)
+    with pytest.raises(ValueError):
+        sw.spec_from_json({"axes": [{"field": "y_B", "values": [1.0]}]})
+    with pytest.raises(ValueError):
+        sw.spec_from_json({**d, "profile": {"estimator": "nope"}})
+    p1 = sw.builtin_specs()["P1"]
+    assert p1.total == 10**6 and p1.profile is not None
+    x, a, b = p1.profile.arrays()
+    assert x.shape == a.shape == b.shape and np.all(np.diff(x) > 0)

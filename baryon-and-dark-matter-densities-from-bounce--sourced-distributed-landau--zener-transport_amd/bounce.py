@@ -45,23 +45,25 @@ def synthetic_couplings(n_points: int, n_shapes: int, seed: int = 6):
     return yB, ychi, lam, vw, shape.astype(np.int32)
 
 
-def interval_steps(knots, coef, yB, ychi, lam, vw, spr: float = 3.0, n_min: int = 1,
+def interval_steps(knots, coef, yB, ychi, lam, vw, spr: float = 4.0, n_min: int = 1,
                    hdot_rate: float = 4.0) -> np.ndarray:
     """Magnus steps per point of lzq_lz_propagate_profile (its per-interval rule, vectorised over
     points; knots [n_knots], coef [n_knots - 1, 8] of ONE shape): the launch's work model."""
     total = np.zeros(np.broadcast(yB, ychi, lam, vw).shape)
     for j in range(len(knots) - 1):
         L = knots[j + 1] - knots[j]
-        w = np.zeros_like(total)
+        e2, h2 = np.zeros_like(total), np.zeros_like(total)
         for f in (0.0, 0.25, 0.5, 0.75, 1.0):
             t = f * L
-            pw = np.array([1.0, t, t * t, t * t * t])
-            dpw = np.array([0.0, 1.0, 2.0 * t, 3.0 * t * t])
-            a, b = coef[j, :4] @ pw, coef[j, 4:] @ pw
-            da, db = coef[j, :4] @ dpw, coef[j, 4:] @ dpw
+            a = coef[j, 0] + t * (coef[j, 1] + t * (coef[j, 2] + t * coef[j, 3]))
+            b = coef[j, 4] + t * (coef[j, 5] + t * (coef[j, 6] + t * coef[j, 7]))
+            da = coef[j, 1] + t * (2.0 * coef[j, 2] + t * 3.0 * coef[j, 3])
+            db = coef[j, 5] + t * (2.0 * coef[j, 6] + t * 3.0 * coef[j, 7])
             D, m = yB * a - ychi * b, lam * a
             Dd, md = yB * da - ychi * db, lam * da
-            w = np.maximum(w, np.maximum(np.sqrt(D * D + m * m), hdot_rate * np.sqrt(vw * np.sqrt(Dd * Dd + md * md))))
+            e2 = np.maximum(e2, D * D + m * m)
+            h2 = np.maximum(h2, Dd * Dd + md * md)
+        w = np.maximum(np.sqrt(e2), hdot_rate * np.sqrt(vw * np.sqrt(h2)))
         total += np.maximum(n_min, np.ceil(spr * (L / vw) * w))
     return total
 

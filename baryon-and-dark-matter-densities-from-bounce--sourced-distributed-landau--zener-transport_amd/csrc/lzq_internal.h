@@ -19,6 +19,13 @@ constexpr int kOdeWS = LZQ_ODE_WS_PER_POINT;  // workspace doubles per point
 int launch_ode_aov_tables(const lzq_point* d_points, int64_t n, const double* d_T_lo, const double* d_T_hi,
                           double* d_work, hipStream_t stream);
 
+// Longest-first launch order (lzq_propagator.hip): cost bins per point (0 = costliest, kCostBins
+// of them) and their histogram -> offs (kCostBins scratch) and order[n] (a counting sort: one
+// scan, one scatter; stable across bins, atomics order within one).  Sets lzq_last_error.
+constexpr int kCostBins = 128;  // 4 bins per octave of a point's step count
+int launch_bin_order(const int32_t* bins, const int32_t* hist, int32_t* offs, int64_t n, int32_t* order,
+                     hipStream_t st);
+
 // lzq_tune(LZQ_TUNE_ODE_COOP) / (LZQ_TUNE_ODE_LAUNCH_STEPS) state, read by lzq_ode.hip's launches
 extern int g_ode_coop;
 extern int g_ode_launch_log2;

@@ -39,6 +39,7 @@
 #include <math.h>
 
 #include "../../include/lzq.h"
+#include "lzq_internal.h"
 #include "lzq_su2.h"
 
 int lzq_set_error(int code, const char* msg);
@@ -47,14 +48,19 @@ namespace lzq {
 
 constexpr int kProfBlock = 256;
 #ifndef LZQ_PROF_LDS_KNOTS
-#define LZQ_PROF_LDS_KNOTS 512  // shapes up to this many knots are staged in LDS (36.9 KB per block)
+#define LZQ_PROF_LDS_KNOTS 256  // shapes up to this many knots are staged in LDS (57 KB per block)
 #endif
 #ifndef LZQ_PROF_MIN_WAVES
 #define LZQ_PROF_MIN_WAVES 2
 #endif
 #ifndef LZQ_PROF_UNROLL
-#define LZQ_PROF_UNROLL 2  // Magnus steps per loop iteration (ILP across steps)
+#define LZQ_PROF_UNROLL 1  // Magnus steps per loop iteration (A/B: 2 is 4% slower, tools/ablate_profile.py)
 #endif
+#ifndef LZQ_PROF_SORT
+#define LZQ_PROF_SORT 1  // cost-ordered launch for batches of >= kProfSortMin points (0: index order)
+#endif
+constexpr int64_t kProfSortMin = 16384;
+constexpr int kProfCostStride = 4;  // the launch-order cost model samples every 4th knot interval
 constexpr double kMaxIntervalSteps = 16777216.0;  // per knot interval; beyond: P = NaN (absurd input)
 constexpr int kProfCoef = 8;                      // doubles per interval row
 constexpr double kHdotRate = 4.0;  // crossing-region rate: kHdotRate / (LZ time), LZ time = |dH/dt|^-1/2
@@ -323,26 +329,92 @@ __device__ __forceinline__ void cos_sinc_short(double x2, double& cs, double& sc
   }
 }
 
-// uniform Magnus steps on one interval (tests/profile_ref.py interval_steps, same operations)
-__device__ __forceinline__ double interval_steps(const double* cD, const double* cM, double L, double vw, double spr,
-                                                 int32_t n_min) {
-  double w = 0.0;
+// The step rule samples each knot interval at t_q = (q/4) L, q = 0..4.  The shape's values there
+// -- phi, Phi, phi', Phi' -- do not depend on the point, so they are evaluated once per launch
+// per (shape, interval) (profile_samples_kernel, stream-ordered scratch, staged in LDS next to the
+// coefficients); a point only combines them with its couplings.
+constexpr int kProfSamp = 20;  // doubles per interval: [q][phi, Phi, phi', Phi'], q = 0..4
+
+__global__ __launch_bounds__(kProfBlock) void profile_samples_kernel(const double* __restrict__ knots,
+                                                                     const double* __restrict__ coef, int64_t n_rows,
+                                                                     int32_t K, double* __restrict__ samp) {
+  const int64_t r = (int64_t)blockIdx.x * kProfBlock + threadIdx.x;  // row = shape * (K - 1) + interval
+  if (r >= n_rows) return;
+  const int64_t s = r / (K - 1), j = r - s * (K - 1);
+  const double L = knots[s * K + j + 1] - knots[s * K + j];
+  const double* c = coef + r * kProfCoef;
+  double* o = samp + r * kProfSamp;
 #pragma unroll
   for (int q = 0; q < 5; ++q) {
     const double t = (0.25 * q) * L;
-    const double D = pp0(cD, t), m = pp0(cM, t);
-    const double Dd = pp1(cD, t), md = pp1(cM, t);
-    w = fmax(w, fmax(sqrt(D * D + m * m), kHdotRate * sqrt(vw * sqrt(Dd * Dd + md * md))));
+    o[4 * q + 0] = pp0(c, t);
+    o[4 * q + 1] = pp0(c + 4, t);
+    o[4 * q + 2] = pp1(c, t);
+    o[4 * q + 3] = pp1(c + 4, t);
   }
+}
+
+// uniform Magnus steps on one interval (tests/profile_ref.py interval_steps): the largest E^2
+// and |dH/dt|^2 over the samples, then the square roots once (sqrt is monotone and correctly
+// rounded, so this equals the restatement's max of the roots)
+__device__ __forceinline__ double interval_steps(const double* __restrict__ sr, const ProfPt& p, double L, double vw,
+                                                 double spr, int32_t n_min) {
+  double e2 = 0.0, h2 = 0.0;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const double a = sr[4 * q], b = sr[4 * q + 1], da = sr[4 * q + 2], db = sr[4 * q + 3];
+    const double D = p.yB * a - p.ychi * b, m = p.lam * a;
+    const double Dd = p.yB * da - p.ychi * db, md = p.lam * da;
+    e2 = fmax(e2, D * D + m * m);
+    h2 = fmax(h2, Dd * Dd + md * md);
+  }
+  const double w = fmax(sqrt(e2), kHdotRate * sqrt(vw * sqrt(h2)));
   return fmax((double)n_min, ceil(spr * (L / vw) * w));
+}
+
+// Launch order.  A lane's cost is its Magnus step count, which scales as 1/v_w and with the
+// couplings, so a wave of random points waits on its slowest lane in every knot interval.  For
+// large batches the points are binned by an estimate of their step count (the step rule on every
+// kProfCostStride-th interval, x kProfCostStride; 4 bins per octave), laid out longest-first by
+// the counting sort shared with lzq_lz_propagate, and the kernel reads its point index from that
+// order.  Each lane still computes one point from its own inputs, so P is bit-identical to index
+// order.
+__global__ __launch_bounds__(kProfBlock) void profile_cost_kernel(const double* __restrict__ knots, int32_t n_shapes,
+                                                                  int32_t K, const lzq_profile_point* __restrict__ pts,
+                                                                  int64_t n, double spr, int32_t n_min,
+                                                                  const double* __restrict__ samp,
+                                                                  int32_t* __restrict__ bins, int32_t* __restrict__ hist) {
+  __shared__ int32_t lh[kCostBins];
+  for (int t = threadIdx.x; t < kCostBins; t += kProfBlock) lh[t] = 0;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * kProfBlock + threadIdx.x;
+  if (i < n) {
+    const ProfPt p = load_point(pts + i);
+    double st = 0.0;
+    if (p.vw > 0.0 && p.shape >= 0 && p.shape < n_shapes) {
+      const double* x = knots + (int64_t)p.shape * K;
+      const double* sm = samp + (int64_t)p.shape * (K - 1) * kProfSamp;
+      for (int j = 0; j + 1 < K; j += kProfCostStride)
+        st += interval_steps(sm + j * kProfSamp, p, x[j + 1] - x[j], p.vw, spr, n_min);
+      st *= kProfCostStride;
+    }
+    const double key = st == st ? fmin(fmax(4.0 * log2(1.0 + st), 0.0), (double)(kCostBins - 1)) : 0.0;
+    const int32_t b = (kCostBins - 1) - (int32_t)key;
+    bins[i] = b;
+    atomicAdd(&lh[b], 1);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < kCostBins; t += kProfBlock)
+    if (lh[t]) atomicAdd(&hist[t], lh[t]);
 }
 
 __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_propagate_kernel(
     const double* __restrict__ knots, const double* __restrict__ coef, int32_t n_shapes, int32_t K,
     const lzq_profile_point* __restrict__ pts, int64_t n, double spr, int32_t n_min, const int32_t* __restrict__ order,
-    double* __restrict__ P_out) {
+    const double* __restrict__ samp, double* __restrict__ P_out) {
   __shared__ double s_knots[LZQ_PROF_LDS_KNOTS];
   __shared__ double s_coef[(LZQ_PROF_LDS_KNOTS - 1) * kProfCoef];
+  __shared__ double s_samp[(LZQ_PROF_LDS_KNOTS - 1) * kProfSamp];
   const int64_t tid = (int64_t)blockIdx.x * kProfBlock + threadIdx.x;
   // stage the shape of the block's first point (block-uniform)
   const int64_t first = (int64_t)blockIdx.x * kProfBlock;
@@ -353,6 +425,8 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_propag
     const double* gc = coef + (int64_t)s0 * (K - 1) * kProfCoef;
     for (int q = threadIdx.x; q < K; q += kProfBlock) s_knots[q] = gk[q];
     for (int q = threadIdx.x; q < (K - 1) * kProfCoef; q += kProfBlock) s_coef[q] = gc[q];
+    const double* gs = samp + (int64_t)s0 * (K - 1) * kProfSamp;
+    for (int q = threadIdx.x; q < (K - 1) * kProfSamp; q += kProfBlock) s_samp[q] = gs[q];
   }
   __syncthreads();
   if (tid >= n) return;
@@ -365,6 +439,7 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_propag
   const bool mine = staged && p.shape == s0;
   const double* x = mine ? s_knots : knots + (int64_t)p.shape * K;
   const double* cf = mine ? s_coef : coef + (int64_t)p.shape * (K - 1) * kProfCoef;
+  const double* sm = mine ? s_samp : samp + (int64_t)p.shape * (K - 1) * kProfSamp;
   const double ivw = 1.0 / p.vw;
   constexpr double kSq15 = 3.872983346207416885;  // sqrt(15)
   constexpr double g1 = 0.5 - kSq15 / 10.0, g3 = 0.5 + kSq15 / 10.0;
@@ -377,7 +452,7 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_propag
   for (int j = 0; j + 1 < K; ++j) {
     if (j > 0) interval_coefs(cf + j * kProfCoef, p, cD, cM);
     L = x[j + 1] - x[j];
-    const double Sd = interval_steps(cD, cM, L, p.vw, spr, n_min);
+    const double Sd = interval_steps(sm + j * kProfSamp, p, L, p.vw, spr, n_min);
     if (!(Sd <= kMaxIntervalSteps)) {  // non-finite or absurd input
       P_out[i] = __builtin_nan("");
       return;
@@ -478,10 +553,44 @@ extern "C" int lzq_lz_propagate_profile(const double* d_knots, const double* d_c
   if (n == 0) return LZQ_OK;
   if (n > 2147483647LL) return lzq_set_error(LZQ_EINVAL, "lzq_lz_propagate_profile: n too large");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(lzq::profile_propagate_kernel, dim3((unsigned)((n + lzq::kProfBlock - 1) / lzq::kProfBlock)),
-                     dim3(lzq::kProfBlock), 0, st, d_knots, d_coef, n_shapes, n_knots, d_points, n, steps_per_radian, min_steps,
-                     (const int32_t*)nullptr, d_P);
-  const hipError_t e = hipGetLastError();
+  // the shapes' step-rule samples: stream-ordered scratch
+  const int64_t rows = (int64_t)n_shapes * (n_knots - 1);
+  double* samp = nullptr;
+  hipError_t e = hipMallocAsync((void**)&samp, sizeof(double) * lzq::kProfSamp * (size_t)rows, st);
+  if (e != hipSuccess) return lzq_set_error(LZQ_EHIP, hipGetErrorString(e));
+  hipLaunchKernelGGL(lzq::profile_samples_kernel, dim3((unsigned)((rows + lzq::kProfBlock - 1) / lzq::kProfBlock)),
+                     dim3(lzq::kProfBlock), 0, st, d_knots, d_coef, rows, n_knots, samp);
+  const int64_t nb = (n + lzq::kProfBlock - 1) / lzq::kProfBlock;
+  // cost-ordered launch (profile_cost_kernel): bins, order, histogram, offsets in one scratch
+  int32_t* ws = nullptr;
+  const int32_t* order = nullptr;
+  int rc = LZQ_OK;
+  if (LZQ_PROF_SORT && n >= lzq::kProfSortMin) {
+    e = hipMallocAsync((void**)&ws, sizeof(int32_t) * (size_t)(2 * n + 2 * lzq::kCostBins), st);
+    if (e == hipSuccess) {
+      int32_t *bins = ws, *ord = ws + n, *hist = ws + 2 * n, *offs = hist + lzq::kCostBins;
+      e = hipMemsetAsync(hist, 0, sizeof(int32_t) * lzq::kCostBins, st);
+      if (e == hipSuccess) {
+        hipLaunchKernelGGL(lzq::profile_cost_kernel, dim3((unsigned)nb), dim3(lzq::kProfBlock), 0, st, d_knots,
+                           n_shapes, n_knots, d_points, n, steps_per_radian, min_steps, (const double*)samp, bins,
+                           hist);
+        rc = lzq::launch_bin_order(bins, hist, offs, n, ord, st);
+        order = ord;
+      }
+    }
+  }
+  if (e == hipSuccess && rc == LZQ_OK) {
+    hipLaunchKernelGGL(lzq::profile_propagate_kernel, dim3((unsigned)nb), dim3(lzq::kProfBlock), 0, st, d_knots, d_coef,
+                       n_shapes, n_knots, d_points, n, steps_per_radian, min_steps, order, (const double*)samp, d_P);
+    e = hipGetLastError();
+  }
+  if (ws) {
+    const hipError_t ef = hipFreeAsync(ws, st);
+    if (e == hipSuccess) e = ef;
+  }
+  const hipError_t ef = hipFreeAsync(samp, st);
+  if (e == hipSuccess) e = ef;
+  if (rc != LZQ_OK) return rc;
   if (e != hipSuccess) return lzq_set_error(LZQ_EHIP, hipGetErrorString(e));
   return LZQ_OK;
 }

@@ -52,6 +52,7 @@
 #include <math.h>
 
 #include "../../include/lzq.h"
+#include "lzq_internal.h"
 #include "lzq_su2.h"
 
 namespace lzq {
@@ -184,7 +185,6 @@ __device__ __forceinline__ void dressed_follow(Cplx& p0, Cplx& p1, double m, dou
 #ifndef LZQ_PROP_SORT
 #define LZQ_PROP_SORT 1  // 0: index order (tools/ablate_prop.py)
 #endif
-constexpr int kCostBins = 128;           // 4 bins per octave of the step count
 constexpr int64_t kSortMinPoints = 16384;  // below this the three extra launches do not pay
 
 // Magnus steps of one point: the cell loop of lz_propagate_kernel without the propagation.
@@ -431,6 +431,20 @@ int propagate_launch(const double* d_m_mix, const double* d_dprime, const double
   return LZQ_OK;
 }
 
+}  // namespace
+
+// Longest-first launch order from per-point cost bins (0 = costliest) and their histogram
+// (lzq_internal.h; shared with lzq_profile.hip): the scan and scatter kernels above.
+int lzq::launch_bin_order(const int32_t* bins, const int32_t* hist, int32_t* offs, int64_t n, int32_t* order,
+                          hipStream_t st) {
+  const int64_t nb = (n + lzq::kPropBlock - 1) / lzq::kPropBlock;
+  hipLaunchKernelGGL(lzq::lz_bin_scan_kernel, dim3(1), dim3(64), 0, st, hist, offs);
+  hipLaunchKernelGGL(lzq::lz_scatter_kernel, dim3((unsigned)nb), dim3(lzq::kPropBlock), 0, st, bins, n, offs, order);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? LZQ_OK : lzq_set_error(LZQ_EHIP, hipGetErrorString(e));
+}
+
+namespace {
 bool propagate_args_ok(int64_t n, int32_t n_cross, double window_lz, int32_t steps_per_crossing) {
   return n >= 0 && n_cross > 0 && steps_per_crossing > 0 && steps_per_crossing <= 1000000 && window_lz > 0.0 &&
          window_lz <= 200.0;

@@ -420,7 +420,7 @@ class Engine:
                 self._stream()))
         return out
 
-    def lz_propagate_profile(self, shapes: "ProfileShapes", points: torch.Tensor, steps_per_radian: float = 3.0,
+    def lz_propagate_profile(self, shapes: "ProfileShapes", points: torch.Tensor, steps_per_radian: float = 4.0,
                              min_steps: int = 1) -> torch.Tensor:
         """Coherent conversion probability through each point's whole profile
         (lzq_lz_propagate_profile)."""

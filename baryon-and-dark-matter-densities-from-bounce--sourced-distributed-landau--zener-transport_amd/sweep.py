@@ -84,7 +84,7 @@ class ProfileSpec:
     y_B: float = 1.0
     y_chi: float = 1.0
     lambda_tr_eff: float = 0.1
-    steps_per_radian: float = 3.0
+    steps_per_radian: float = 4.0
     min_steps: int = 1
 
     def arrays(self):

@@ -231,7 +231,7 @@ def profile_crossings(knots, phi, Phi, y_B, y_chi, lambda_tr_eff, v_w, max_cross
     return list(zip(*cols))
 
 
-def lz_propagate_profile(knots, phi, Phi, y_B, y_chi, lambda_tr_eff, v_w, steps_per_radian: float = 3.0,
+def lz_propagate_profile(knots, phi, Phi, y_B, y_chi, lambda_tr_eff, v_w, steps_per_radian: float = 4.0,
                          min_steps: int = 1) -> float:
     """Time-ordered conversion probability through the whole bounce profile
     (lzq_lz_propagate_profile): H = Delta(xi) sz + m_mix(xi) sx, xi = v_w t."""

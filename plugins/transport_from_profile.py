@@ -33,7 +33,7 @@ row, '#' lines are comments, `# key = value` comment lines set options):
               crossings' energy dependence and their interference are kept
     linear    each crossing linearised (Delta' and m_mix at xi*), coherent through the
               piecewise-linear model (lzq_lz_propagate); window_lz (20), steps (1000)
-  steps_per_radian (3), min_steps (1): the profile propagator's step control.
+  steps_per_radian (4), min_steps (1): the profile propagator's step control.
   v_w: only for compute_lambda_eff_from_profile, whose signature has no v_w.
 
 Command line (PAPER App. A): python transport_from_profile.py --params transport_params.json
@@ -52,7 +52,7 @@ if _HERE not in sys.path:   # lzq_binding lives next to this module
     sys.path.insert(0, _HERE)
 import lzq_binding  # noqa: E402
 
-DEFAULTS = {"window_lz": 20.0, "steps": 1000.0, "steps_per_radian": 3.0, "min_steps": 1.0, "estimator": "auto",
+DEFAULTS = {"window_lz": 20.0, "steps": 1000.0, "steps_per_radian": 4.0, "min_steps": 1.0, "estimator": "auto",
             "R0": 0.0}
 ESTIMATORS = ("auto", "minimal", "propagate", "linear")
 

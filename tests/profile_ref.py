@@ -163,19 +163,24 @@ def _edge(cD, cM, t, v_w):
 
 
 # ---- propagation ---------------------------------------------------------------------------
-STEPS_PER_RADIAN = 3.0
+STEPS_PER_RADIAN = 4.0
 MIN_STEPS = 1
 HDOT_RATE = 4.0   # the crossing region's rate: HDOT_RATE / (LZ time), LZ time = |dH/dt|^-1/2
 
 
-def interval_steps(cD, cM, L, v_w, spr=STEPS_PER_RADIAN, n_min=MIN_STEPS):
+def interval_steps(cphi, cPhi, yB, ychi, lam, L, v_w, spr=STEPS_PER_RADIAN, n_min=MIN_STEPS):
     """Uniform Magnus steps on one knot interval: spr x the interval's largest local rate
-    omega = max(E, HDOT_RATE sqrt(|dH/dt|)) (sampled at 5 points) x its duration, at least n_min."""
+    omega = max(E, HDOT_RATE sqrt(|dH/dt|)) x its duration, at least n_min.  The rate is sampled at
+    5 points t_q = (q/4) L from the shape's samples phi(t_q), Phi(t_q), phi'(t_q), Phi'(t_q)
+    (coupling-independent: the kernel precomputes them per shape) combined with the point's
+    couplings: Delta = y_B phi - y_chi Phi, m = lambda phi (eqs.(5),(7))."""
     w = 0.0
     for f in (0.0, 0.25, 0.5, 0.75, 1.0):
         t = f * L
-        D, m = pp_eval(cD, t), pp_eval(cM, t)
-        Dd, md = pp_eval(cD, t, 1), pp_eval(cM, t, 1)
+        a, b = pp_eval(cphi, t), pp_eval(cPhi, t)
+        da, db = pp_eval(cphi, t, 1), pp_eval(cPhi, t, 1)
+        D, m = yB * a - ychi * b, lam * a
+        Dd, md = yB * da - ychi * db, lam * da
         w = max(w, math.sqrt(D * D + m * m), HDOT_RATE * math.sqrt(v_w * math.sqrt(Dd * Dd + md * md)))
     return max(n_min, int(math.ceil(spr * (L / v_w) * w)))
 
@@ -209,14 +214,17 @@ def su2(nx, ny, nz):
 
 def propagate_profile(knots, cphi, cPhi, yB, ychi, lam, v_w, spr=STEPS_PER_RADIAN, n_min=MIN_STEPS,
                       cD=None, cM=None):
-    """Coherent conversion probability through the whole profile [x_0, x_{n-1}]."""
-    if cD is None:
-        cD, cM = dm_coefs(cphi, cPhi, yB, ychi, lam)
+    """Coherent conversion probability through the whole profile [x_0, x_{n-1}].  (cD, cM):
+    Delta and m_mix rows given directly = phi := m, Phi := Delta with y_B = 0, y_chi = -1,
+    lambda = 1 (exact)."""
+    if cD is not None:
+        cphi, cPhi, yB, ychi, lam = np.asarray(cM), np.asarray(cD), 0.0, -1.0, 1.0
+    cD, cM = dm_coefs(cphi, cPhi, yB, ychi, lam)
     nI = len(knots) - 1
     p = _edge(cD[0], cM[0], 0.0, v_w)
     for j in range(nI):
         L = knots[j + 1] - knots[j]
-        S = interval_steps(cD[j], cM[j], L, v_w, spr, n_min)
+        S = interval_steps(cphi[j], cPhi[j], yB, ychi, lam, L, v_w, spr, n_min)
         h = L / S
         dt = h / v_w
         for i in range(S):

@@ -151,10 +151,16 @@ def test_propagation_matches_restatement(gpu_engine):
     coef = sh.coef.cpu().numpy()
     cases = [(1.0, 1.1, 0.2, 0.3, 0), (0.8, 1.5, 0.05, 0.6, 1), (1.6, 0.9, 0.4, 0.2, 0), (1.2, 1.2, 1.0, 0.9, 1)]
     got = gpu_engine.lz_propagate_profile(sh, gpu_engine.profile_points(*zip(*cases)), 3.0, 8).cpu().numpy()
+    got1 = gpu_engine.lz_propagate_profile(sh, gpu_engine.profile_points(*zip(*cases))).cpu().numpy()
     for i, (yB, ychi, lam, vw, s) in enumerate(cases):
-        ref = R.propagate_profile(shapes[s][0], coef[s][:, :4], coef[s][:, 4:], yB, ychi, lam, vw)
+        ref = R.propagate_profile(shapes[s][0], coef[s][:, :4], coef[s][:, 4:], yB, ychi, lam, vw, spr=3.0, n_min=8)
         assert 0.0 <= got[i] <= 1.0
         assert abs(got[i] - ref) <= 1e-11, (i, got[i], ref)
+        ref1 = R.propagate_profile(shapes[s][0], coef[s][:, :4], coef[s][:, 4:], yB, ychi, lam, vw)   # the defaults
+        assert abs(got1[i] - ref1) <= 1e-11, (i, got1[i], ref1)
+    # the defaults (4 steps per radian, min_steps 1) against the step-converged result (16)
+    conv = gpu_engine.lz_propagate_profile(sh, gpu_engine.profile_points(*zip(*cases)), 16.0).cpu().numpy()
+    assert np.max(np.abs(got1 - conv)) <= 2e-9, (got1, conv)
 
 
 def _linear_shape(engine, c):
@@ -194,14 +200,17 @@ def test_piecewise_linear_profile_matches_lz_propagate(gpu_engine):
 
 
 def test_weber_fixtures_default_steps(gpu_engine):
-    """All 53 exact Weber-function solutions at the default 3 steps per radian: <= 2e-9 (measured
-    9.2e-10; lzq_lz_propagate at the C5 default: 7.2e-10)."""
-    worst = 0.0
+    """All 53 exact Weber-function solutions at 3 steps per radian: <= 2e-9 (measured 9.2e-10;
+    lzq_lz_propagate at the C5 default: 7.2e-10); at the default 4: <= 5e-10."""
+    worst, worst4 = 0.0, 0.0
     for c in WEBER["cases"]:
+        P4 = float(_profile_P(gpu_engine, c, 4.0).cpu().numpy()[0])
+        worst4 = max(worst4, abs(P4 - c["P"]))
         P = float(_profile_P(gpu_engine, c, 3.0).cpu().numpy()[0])
         worst = max(worst, abs(P - c["P"]))
         assert abs(P - c["P"]) <= 2e-9, (c["kind"], c["m"], c["d"], P, c["P"])
-    print(f"profile propagator vs 53 Weber fixtures: worst {worst:.3g}")
+    print(f"profile propagator vs 53 Weber fixtures: worst {worst:.3g} (3 steps/rad), {worst4:.3g} (4)")
+    assert worst4 <= 5e-10
 
 
 def test_single_linear_crossing_is_eq9(gpu_engine):
@@ -234,6 +243,16 @@ def test_batch_invariance_and_bad_inputs(gpu_engine):
     grouped = gpu_engine.lz_propagate_profile(
         sh, gpu_engine.profile_points(*(a[order] for a in args), shp[order])).cpu().numpy()
     assert np.array_equal(mixed[order], grouped)
+    # >= 16384 points run cost-ordered (profile_cost_kernel + counting sort); < 16384 in index
+    # order: the same bits
+    n2 = 20_000
+    big = (rng.uniform(0.5, 2.0, n2), rng.uniform(0.5, 2.0, n2), 10 ** rng.uniform(-3, 0, n2), rng.uniform(0.1, 0.9, n2))
+    shp2 = rng.integers(0, 3, n2)
+    whole = gpu_engine.lz_propagate_profile(sh, gpu_engine.profile_points(*big, shp2)).cpu().numpy()
+    parts = np.concatenate([gpu_engine.lz_propagate_profile(
+        sh, gpu_engine.profile_points(*(a[k:k + 5000] for a in big), shp2[k:k + 5000])).cpu().numpy()
+        for k in range(0, n2, 5000)])
+    assert np.array_equal(whole, parts) and np.isfinite(whole).all()
     bad = gpu_engine.lz_propagate_profile(sh, gpu_engine.profile_points(1.0, 1.0, 0.1, [0.3, 0.0, 0.3, 0.3],
                                                                          [0, 0, 3, -2])).cpu().numpy()
     assert np.isfinite(bad[0]) and np.isnan(bad[1:]).all()

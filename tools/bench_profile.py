@@ -46,17 +46,23 @@ def main():
     ap.add_argument("reps", type=int, nargs="?", default=3)
     ap.add_argument("--shapes", type=int, default=16)
     ap.add_argument("--knots", type=int, default=256)
-    ap.add_argument("--spr", type=float, default=3.0)
+    ap.add_argument("--spr", type=float, default=4.0)
     ap.add_argument("--min-steps", type=int, default=1)
     ap.add_argument("--only", default=None, help="propagate | crossings: time that stage alone (profiling)")
+    ap.add_argument("--sort-vw", action="store_true", help="launch the points ordered by (shape, v_w): the "
+                    "cost-ordered launch's upper bound (a lane's step count scales as 1/v_w)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     B = importlib.import_module(PKG + ".bounce")
     eng = importlib.import_module(PKG + ".engine").Engine(0)
     X, phi, Phi = B.synthetic_shapes(a.shapes, a.knots)
     yB, ychi, lam, vw, shape = B.synthetic_couplings(a.n, a.shapes)
+    if a.sort_vw:
+        o = np.lexsort((vw, shape))
+        yB, ychi, lam, vw, shape = yB[o], ychi[o], lam[o], vw[o], shape[o]
     pts = eng.profile_points(yB, ychi, lam, vw, shape)
-    rec = {"points": a.n, "shapes": a.shapes, "knots": a.knots, "steps_per_radian": a.spr, "min_steps": a.min_steps}
+    rec = {"points": a.n, "shapes": a.shapes, "knots": a.knots, "steps_per_radian": a.spr, "min_steps": a.min_steps,
+           "order": "shape, v_w" if a.sort_vw else "shape, random"}
     sh = eng.profile_shapes(X, phi, Phi)
     if a.only in (None, "propagate"):
         t_p, P = timed(lambda: eng.lz_propagate_profile(sh, pts, a.spr, a.min_steps), a.reps)

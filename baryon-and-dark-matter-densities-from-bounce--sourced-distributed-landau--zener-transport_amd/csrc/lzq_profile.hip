@@ -28,11 +28,13 @@
 //                               exponential; on knot interval j, S_j = max(min_steps,
 //                               ceil(steps_per_radian * (len_j / v_w) * omega_j)) uniform steps,
 //                               omega_j = the largest of E = sqrt(Delta^2 + m^2) and
-//                               4 sqrt(|dH/dt|) (4 / the LZ time) at 5 points of the interval.  The shape's knots and
-//                               coefficients are staged in LDS once per block (lanes whose point
-//                               has another shape read them from HBM through the same pointer);
-//                               a lane keeps its interval's Delta and m coefficients, the state
-//                               and the step in registers.
+//                               4 sqrt(|dH/dt|) (4 / the LZ time) at 5 points of the interval
+//                               (from per-shape samples, profile_samples_kernel).  A lane keeps
+//                               its interval's Delta and m coefficients, the state and the step
+//                               in registers; the shape's rows are read once per interval, and
+//                               the lanes of a wave read the same rows (L1/L2 hits: staging them
+//                               in LDS per block, LZQ_PROF_LDS=1, measured 5% slower).  Large
+//                               batches launch cost-ordered (profile_cost_kernel).
 // tests/profile_ref.py restates all three in numpy; tests/test_gpu_profile.py checks them.
 #include <hip/hip_runtime.h>
 
@@ -47,8 +49,12 @@ int lzq_set_error(int code, const char* msg);
 namespace lzq {
 
 constexpr int kProfBlock = 256;
+#ifndef LZQ_PROF_LDS
+#define LZQ_PROF_LDS 0  // 1: stage the block's shape in LDS (A/B, 1e6 points: 5% slower -- 57 KB per block
+                        // caps the CU at 2 blocks, while every wave's row reads hit L1/L2 anyway)
+#endif
 #ifndef LZQ_PROF_LDS_KNOTS
-#define LZQ_PROF_LDS_KNOTS 256  // shapes up to this many knots are staged in LDS (57 KB per block)
+#define LZQ_PROF_LDS_KNOTS (LZQ_PROF_LDS ? 256 : 4)  // shapes up to this many knots are staged (LZQ_PROF_LDS)
 #endif
 #ifndef LZQ_PROF_MIN_WAVES
 #define LZQ_PROF_MIN_WAVES 2
@@ -419,7 +425,7 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_propag
   // stage the shape of the block's first point (block-uniform)
   const int64_t first = (int64_t)blockIdx.x * kProfBlock;
   const int32_t s0 = pts[order ? (int64_t)order[first] : first].shape;
-  const bool staged = K <= LZQ_PROF_LDS_KNOTS && s0 >= 0 && s0 < n_shapes;
+  const bool staged = LZQ_PROF_LDS && K <= LZQ_PROF_LDS_KNOTS && s0 >= 0 && s0 < n_shapes;
   if (staged) {
     const double* gk = knots + (int64_t)s0 * K;
     const double* gc = coef + (int64_t)s0 * (K - 1) * kProfCoef;

@@ -79,7 +79,7 @@ class ProfileSpec:
     propagation through the profile), "minimal" (eq.(9); points without exactly one crossing get
     P = NaN) or "propagate" (every point through the whole profile)."""
     csv: Optional[str] = None
-    synthetic: int = 0
+    synthetic: int = 12     # bounce.synthetic_shapes index (12: one or three crossings across P1's couplings)
     estimator: str = "auto"
     y_B: float = 1.0
     y_chi: float = 1.0
@@ -268,7 +268,7 @@ def builtin_specs() -> dict:
                         crossings=CrossingSpec()),
         "P1": SweepSpec("P1", dict(EQUAL_MASS),
                         [("y_B", lin(0.5, 2.0, 100)), ("y_chi", lin(0.5, 2.0, 100)), ("lambda_tr_eff", ls(-3, 0, 100))],
-                        notes="P from a bounce profile (synthetic shape 0; PAPER eqs.(5)-(9)) over the couplings "
+                        notes="P from a bounce profile (synthetic shape 12; PAPER eqs.(5)-(9)) over the couplings "
                               "y_B x y_chi x lambda_tr_eff, then the dense quadrature",
                         profile=ProfileSpec()),
         "C4": SweepSpec("C4", dict(EQUAL_MASS),

@@ -195,7 +195,7 @@ def test_profile_sweep_P1(gpu_engine):
     import torch
     sw = pkg("sweep")
     spec = sw.builtin_specs()["P1"]
-    s, n = 345_000, 4096
+    s, n = 302_000, 4096      # y_B index 30, y_chi 20..61: one and three crossings
     out = torch.empty((n, 6), dtype=torch.float64, device=gpu_engine.device)
     sw.make_compute(spec, gpu_engine)(s, n, out)
     t = out.cpu().numpy()

@@ -92,7 +92,9 @@ class ProfileSpec:
         if self.csv:
             x, a, b, _ = bounce.read_bounce_csv(self.csv)
             return x, a, b
-        X, A, B = bounce.synthetic_shapes(max(self.synthetic + 1, 1))
+        if not 0 <= self.synthetic < 16:
+            raise ValueError("profile.synthetic must index the 16-shape synthetic family (0..15)")
+        X, A, B = bounce.synthetic_shapes(16)   # the family as tools/bench_profile.py draws it
         return X[self.synthetic], A[self.synthetic], B[self.synthetic]
 
 

@@ -27,6 +27,9 @@ def main():
     E = importlib.import_module(PKG + ".engine").Engine
     paths = sorted(glob.glob(os.path.join(ROOT, PKG, "_build", "variants", "*.so")))
     engs = {os.path.basename(p)[7:-3]: E(0, lib_path=p) for p in paths}
+    if not engs:
+        print(json.dumps({"note": "no variants under _build/variants (tools/build_variants.py)"}))
+        return
     X, phi, Phi = B.synthetic_shapes()
     cols = B.synthetic_couplings(n, X.shape[0])
     e0 = next(iter(engs.values()))

@@ -397,11 +397,15 @@ __constant__ double kRadauPred[3][4] = {
 // Zs: in, Newton starting stages when `guess` (else Ychi for all three); out, the converged
 // stages (the next predictor's data).  A predicted start that does not converge is retried
 // from Ychi, so the predictor can only save iterations, never lose a step.
+#ifndef LZQ_ODE_PEEL
+#define LZQ_ODE_PEEL 1  // the first two Newton iterations (and the Y_B solve) as one straight-line block
+#endif
+
 template <bool kWithYB = true>
 __device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st)[3], double& Ychi, double& YB,
                                            double (&Zs)[3], bool guess) {
   // Y_B: (I + hA diag(beta)) Z = YB + hA alpha, exactly; Z_3 = Y_B(x + h)
-  if (kWithYB) {
+  auto yb_step = [&]() {
     double M[3][3], b[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -413,31 +417,23 @@ __device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st
       }
       b[i] = acc;
     }
-    YB = solve3_last(M, b);
-  }
-  // Y_chi: Z_i = Y + h sum_j a_ij f_j(Z_j), f_j(Z) = -lam_j (Z^2 - E2_j) - S_j
-  const bool nonlinear = st[0].lam != 0.0 || st[1].lam != 0.0 || st[2].lam != 0.0;
-  if (!nonlinear) {  // f_j = -S_j: Z_3 = Y - sum_j hA_3j S_j
-    double acc = Ychi;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) acc = __builtin_fma(-hA.a[2][j], st[j].S, acc);
-    Ychi = acc;
-    return true;
-  }
-  for (int attempt = guess ? 0 : 1; attempt < 2; ++attempt) {
-  double Z[3] = {attempt == 0 ? Zs[0] : Ychi, attempt == 0 ? Zs[1] : Ychi, attempt == 0 ? Zs[2] : Ychi};
-  for (int it = 0; it < 40; ++it) {
+    return solve3_last(M, b);
+  };
+  // Y_chi: Z_i = Y + h sum_j a_ij f_j(Z_j), f_j(Z) = -lam_j (Z^2 - E2_j) - S_j; one Newton
+  // iteration on Z, true when its correction is below 1e-15 of the stages
+  const double Y0 = Ychi;
+  auto newton = [&](double (&Z)[3]) {
     double M[3][3], g[3];
     double f[3], jf[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       f[j] = LZQ_ODE_FMA ? __builtin_fma(-st[j].lam, __builtin_fma(Z[j], Z[j], -st[j].E2), -st[j].S)
-                              : -st[j].lam * (Z[j] * Z[j] - st[j].E2) - st[j].S;
+                         : -st[j].lam * (Z[j] * Z[j] - st[j].E2) - st[j].S;
       jf[j] = -st[j].lam * (2.0 * Z[j]);
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      double acc = Z[i] - Ychi;
+      double acc = Z[i] - Y0;
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         acc = __builtin_fma(-hA.a[i][j], f[j], acc);
@@ -457,14 +453,60 @@ __device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st
       dmax = pymax(dmax, fabs(g[i]));
       zmax = pymax(zmax, fabs(Z[i]));
     }
-    if (!(dmax > 1e-15 * zmax)) {
-      Zs[0] = Z[0];
-      Zs[1] = Z[1];
-      Zs[2] = Z[2];
-      Ychi = Z[2];
-      return true;
-    }
+    return !(dmax > 1e-15 * zmax);
+  };
+  auto accept = [&](const double (&Z)[3]) {
+    Zs[0] = Z[0];
+    Zs[1] = Z[1];
+    Zs[2] = Z[2];
+    Ychi = Z[2];
+  };
+  const bool nonlinear = st[0].lam != 0.0 || st[1].lam != 0.0 || st[2].lam != 0.0;
+  if (!nonlinear) {  // f_j = -S_j: Z_3 = Y - sum_j hA_3j S_j
+    if (kWithYB) YB = yb_step();
+    double acc = Ychi;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc = __builtin_fma(-hA.a[2][j], st[j].S, acc);
+    Ychi = acc;
+    return true;
   }
+  for (int attempt = guess ? 0 : 1; attempt < 2; ++attempt) {
+    double Z[3] = {attempt == 0 ? Zs[0] : Y0, attempt == 0 ? Zs[1] : Y0, attempt == 0 ? Zs[2] : Y0};
+    int it = 0;
+#if LZQ_ODE_PEEL
+    if (attempt == (guess ? 0 : 1)) {
+      // the first two iterations (and Y_B's independent solve) in one basic block, so the
+      // scheduler interleaves their dependent chains; the second is applied only if the first
+      // did not converge -- the same iterates as the loop below, bit for bit
+      if (kWithYB) YB = yb_step();
+      double Z2[3];
+      const bool c1 = newton(Z);
+      Z2[0] = Z[0];
+      Z2[1] = Z[1];
+      Z2[2] = Z[2];
+      const bool c2 = newton(Z2);
+      if (c1) {
+        accept(Z);
+        return true;
+      }
+      if (c2) {
+        accept(Z2);
+        return true;
+      }
+      Z[0] = Z2[0];
+      Z[1] = Z2[1];
+      Z[2] = Z2[2];
+      it = 2;
+    }
+#else
+    if (kWithYB && attempt == (guess ? 0 : 1)) YB = yb_step();
+#endif
+    for (; it < 40; ++it) {
+      if (newton(Z)) {
+        accept(Z);
+        return true;
+      }
+    }
   }
   return false;
 }

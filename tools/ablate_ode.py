@@ -32,10 +32,15 @@ def main():
     engs = {os.path.basename(p)[7:-3]: E(0, lib_path=p) for p in paths}
     cases = {"narrow_wash": {"Gamma_wash_over_H": 1.0, "T_max_over_Tp": 1.6, "T_min_over_Tp": 0.6},
              "stiff_thermal": {"sigma_v_chi_GeV_m2": 1e-9, "regime": "thermal", "m_chi_GeV": 300.0,
-                               "T_max_over_Tp": 1.3, "T_min_over_Tp": 0.2}}
+                               "T_max_over_Tp": 1.3, "T_min_over_Tp": 0.2},
+             "riccati_mchi_sv": {"T_max_over_Tp": 1.6, "T_min_over_Tp": 0.6}}
     out = {}
     for cname, over in cases.items():
         cfgs = cfgs_for(over, n)
+        if cname == "riccati_mchi_sv":   # m_chi fastest over 4 values x 16 sigma_v values
+            for i, c in enumerate(cfgs):
+                c["m_chi_GeV"] = (0.95, 3.0, 10.0, 30.0)[i % 4]
+                c["sigma_v_chi_GeV_m2"] = 10.0 ** (-20 + ((i // 4) % 16) * 0.6)
         pts = np.concatenate([cfgm.to_point(c) for c in cfgs])
         ods = np.concatenate([cfgm.to_ode_params(c) for c in cfgs])
         ref = None

@@ -151,6 +151,7 @@ __device__ __forceinline__ double exp_nonpos(double v) {
 //   dY_B/dx   = alpha - beta Y_B               alpha = (SB/s)/(H x), beta = (gamma_w H)/(H x)
 struct OdeStage {
   double lam, E2, S, alpha, beta;
+  double a;  // alpha per unit P * flux (the Y_B recurrence forms P * flux * (its coefficient of a))
 };
 
 // The same with the per-point scalars factored out: alpha (and S) per unit P * flux, lam per
@@ -213,6 +214,7 @@ __device__ __forceinline__ OdeStage stage_scale(const OdePoint& o, const StageBa
   st.lam = o.sigmav * b.lam;
   st.E2 = b.E2;
   st.beta = o.gamma_w * b.beta;
+  st.a = b.a;
   return st;
 }
 
@@ -256,6 +258,7 @@ __device__ __forceinline__ OdeStage chi_scale(const OdePoint& o, const StageBase
   st.S = 0.0;
   st.alpha = 0.0;
   st.beta = 0.0;
+  st.a = 0.0;
   return st;
 }
 
@@ -383,6 +386,39 @@ __device__ __forceinline__ void solve3_adj(const double (&M)[3][3], double (&b)[
   b[2] = x2;
 }
 
+// Y_B's Radau step as an affine map (LZQ_ODE_YBREC): the stage system (I + hA diag(beta)) Z =
+// Y_B 1 + hA alpha, alpha_j = P flux a_j, gives by Cramer's rule Z_3 = c Y_B + P flux d with
+// c = (w0 + w1 + w2)/det and d = sum_j (sum_i w_i hA_ij) a_j / det, w_i the cofactors of the last
+// column's numerator (solve3_last's).  c and d depend on the point only through Gamma_wash (beta)
+// and the stage bases, so a cooperative segment with one Gamma_wash forms them once per step
+// for all its lanes; every mode forms them with these operations, so the result does not depend
+// on the mode.
+struct YbRec {
+  double c, d;
+};
+__device__ __forceinline__ YbRec yb_rec(const RadauH& hA, const double (&beta)[3], const double (&a)[3]) {
+  double M[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) M[i][j] = __builtin_fma(hA.a[i][j], beta[j], i == j ? 1.0 : 0.0);
+  const double w0 = M[1][0] * M[2][1] - M[1][1] * M[2][0];
+  const double w1 = M[0][1] * M[2][0] - M[0][0] * M[2][1];
+  const double w2 = M[0][0] * M[1][1] - M[0][1] * M[1][0];
+  const double det = M[0][0] * (M[1][1] * M[2][2] - M[1][2] * M[2][1]) -
+                     M[0][1] * (M[1][0] * M[2][2] - M[1][2] * M[2][0]) + M[0][2] * w0;
+  const double id = 1.0 / det;
+  double d = 0.0;
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+    d = __builtin_fma(__builtin_fma(w2, hA.a[2][j], __builtin_fma(w1, hA.a[1][j], w0 * hA.a[0][j])), a[j], d);
+  return {((w0 + w1) + w2) * id, d * id};
+}
+__device__ __forceinline__ YbRec yb_rec(const RadauH& hA, const OdeStage (&st)[3]) {
+  const double beta[3] = {st[0].beta, st[1].beta, st[2].beta}, a[3] = {st[0].a, st[1].a, st[2].a};
+  return yb_rec(hA, beta, a);
+}
+
 // One Radau step for both equations (hA = h * A of the step); false when the Y_chi Newton
 // iteration fails.  The stage sums are explicit fmas (hA_ij * f_j + acc); only the last stage
 // of each equation is the step's result, so the linear cases form only what they need.
@@ -399,6 +435,9 @@ __constant__ double kRadauPred[3][4] = {
 // from Ychi, so the predictor can only save iterations, never lose a step.
 #ifndef LZQ_ODE_PEEL
 #define LZQ_ODE_PEEL 1  // the first two Newton iterations (and the Y_B solve) as one straight-line block
+#endif
+#ifndef LZQ_ODE_YBREC
+#define LZQ_ODE_YBREC 1  // Y_B by its affine step map (yb_rec), shared per cooperative segment
 #endif
 
 template <bool kWithYB = true>
@@ -627,6 +666,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
                                                                   int64_t k_lo, int64_t k_cnt,
                                                                   OdeState* __restrict__ state) {
   __shared__ StageBase s_base[kOdeBlock / 64][64][3];  // cooperative mode
+  __shared__ YbRec s_rec[LZQ_ODE_YBREC && !kChiOnly ? kOdeBlock / 64 : 1][64];  // shared Y_B step maps
   // Lanes past the end of the batch are clones of their wavefront's first point (they compute
   // it again and write nothing), so a partial wavefront -- a single CLI point included -- is
   // still full and can run cooperatively.
@@ -730,6 +770,12 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
     }
     const bool coop = G > 0;
     const int seg = lane & ~(G - 1);  // first LDS row of this lane's segment (G > 0)
+    // Y_B's step maps shared by the segment when it has one Gamma_wash (LZQ_ODE_YBREC)
+    bool rec_shared = false;
+    if (LZQ_ODE_YBREC && !kChiOnly && coop) {
+      const uint64_t gb = __builtin_bit_cast(uint64_t, o.gamma_w);
+      rec_shared = __all(gb == __builtin_bit_cast(uint64_t, __shfl(o.gamma_w, 0, G)));
+    }
     const int64_t block = coop ? G : N;
     for (int64_t kb = k_begin; kb < k_stop; kb += block) {
       const int64_t kend = kb + block < k_stop ? kb + block : k_stop;
@@ -737,10 +783,19 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
         const int64_t kl = kb + (lane - seg);
         if (kl < kend) {
           const double xk = x0 + (double)kl * h;
+          StageBase bs[3];
 #pragma unroll
-          for (int j = 0; j < 3; ++j)
-            s_base[wv][lane][j] = (kChiOnly && !o.deplete) ? ode_stage_chi_base(o, xk + R.c[j] * h)
-                                                           : ode_stage_base(o, w, xk + R.c[j] * h);
+          for (int j = 0; j < 3; ++j) {
+            bs[j] = (kChiOnly && !o.deplete) ? ode_stage_chi_base(o, xk + R.c[j] * h)
+                                             : ode_stage_base(o, w, xk + R.c[j] * h);
+            s_base[wv][lane][j] = bs[j];
+          }
+          if (LZQ_ODE_YBREC && !kChiOnly && rec_shared) {
+            // beta_j as stage_scale forms it (Gamma_wash * base), a_j the base: the step map
+            const double beta[3] = {o.gamma_w * bs[0].beta, o.gamma_w * bs[1].beta, o.gamma_w * bs[2].beta};
+            const double a[3] = {bs[0].a, bs[1].a, bs[2].a};
+            s_rec[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][lane] = yb_rec(hA, beta, a);
+          }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -781,7 +836,14 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
             for (int j = 0; j < 3; ++j)
               sg[j] = (kChiOnly && !o.deplete) ? ode_stage_chi(o, xk + R.c[j] * hs) : ode_stage(o, w, xk + R.c[j] * hs);
           }
-          ok = radau_step<!kChiOnly>(split ? radau_h(R, hs) : hA, sg, Ychi, YB, Zs, use_guess);
+          if (LZQ_ODE_YBREC && !kChiOnly) {  // Y_B by its step map, then Y_chi alone
+            const YbRec r = (rec_shared && !split) ? s_rec[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][seg + (k - kb)]
+                                                   : yb_rec(split ? radau_h(R, hs) : hA, sg);
+            YB = __builtin_fma(r.c, YB, o.Pf * r.d);
+            ok = radau_step<false>(split ? radau_h(R, hs) : hA, sg, Ychi, YB, Zs, use_guess);
+          } else {
+            ok = radau_step<!kChiOnly>(split ? radau_h(R, hs) : hA, sg, Ychi, YB, Zs, use_guess);
+          }
         }
         if (ok && split && xk + h > xb) {
           const double hs = (xk + h) - xb;
@@ -790,7 +852,13 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
 #pragma unroll
           for (int j = 0; j < 3; ++j)
             sg[j] = (kChiOnly && !o.deplete) ? ode_stage_chi(o, xb + R.c[j] * hs) : ode_stage(o, w, xb + R.c[j] * hs);
-          ok = radau_step<!kChiOnly>(radau_h(R, hs), sg, Ychi, YB, Zs, false);
+          if (LZQ_ODE_YBREC && !kChiOnly) {
+            const YbRec r = yb_rec(radau_h(R, hs), sg);
+            YB = __builtin_fma(r.c, YB, o.Pf * r.d);
+            ok = radau_step<false>(radau_h(R, hs), sg, Ychi, YB, Zs, false);
+          } else {
+            ok = radau_step<!kChiOnly>(radau_h(R, hs), sg, Ychi, YB, Zs, false);
+          }
         }
         have = !split;   // the predictor needs a full regular step behind it
         Yp = Ystart;

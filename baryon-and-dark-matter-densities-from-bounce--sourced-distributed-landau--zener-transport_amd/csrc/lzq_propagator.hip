@@ -22,12 +22,16 @@
 //
 // Integrator, per cell c with delta_c = m_c^2 / (2 v_w |Delta'_c|):
 //  * delta_c <= kDeltaAdiabatic: eighth-order Magnus with the exact SU(2) exponential on the
-//    cell's CORE [xi_c - W_c, xi_c + W_c] (core_halfwidth: 2K LZ lengths for delta <= 1, else
-//    out to where the adiabaticity eps = m|alpha|/(4E^3) falls to kCoreEps), with
-//    S_c = max(S, ceil(Phi_core * kStepsPerRadian)) uniform steps, Phi_core the core's adiabatic
-//    phase (closed form below); the parts of the cell outside the core are followed in the
-//    dressed basis with no stepping (dressed_follow).  The step count is thereby bounded by
-//    the core (<= 3 (2K)^2 max(1, delta) + S) whatever the crossing spacing.  H = D(t) sz + m sx is linear in t, so its Magnus series over a step of length dt
+//    cell's CORE [xi_c - W_c, xi_c + W_c] with S_c = max(S, ceil(Phi_core * kStepsPerRadian))
+//    uniform steps, Phi_core the core's adiabatic phase (closed form below).  Outside the core
+//    the state is followed in the superadiabatic frame of order 10 (lzq_superadiabatic.h: ten
+//    iterated adiabatic rotations built from Taylor jets), where it only picks up the frame's
+//    phase; the error of that is the first neglected rotation angle at the core edge, and the
+//    core ends where that falls to kSATol = 1e-11: E = (kSAC mh / kSATol)^(1/21) in units of
+//    sqrt(alpha) (~4-7 LZ lengths, against 40 for round 2's second-order dressed basis).  The
+//    follow stretches do not depend on the state, so lz_follow_kernel computes their SU(2)
+//    transfer matrices first (one thread per point and cell) and this kernel applies them.
+//    H = D(t) sz + m sx is linear in t, so its Magnus series over a step of length dt
 //    centred on D is known in closed form (derived symbolically: Dyson series, then log):
 //      Omega = -i (n . sigma),  U = cos|n| - i sin|n| (n/|n|) . sigma,  D' = dD/dt, E2 = D^2 + m^2
 //      n_x = m dt [1 - D'^2 dt^4/60 - D'^2 dt^6 (3D^2 + 4m^2)/1890]
@@ -51,9 +55,12 @@
 
 #include <math.h>
 
+#include <algorithm>
+
 #include "../../include/lzq.h"
 #include "lzq_internal.h"
 #include "lzq_su2.h"
+#include "lzq_superadiabatic.h"
 
 namespace lzq {
 
@@ -65,14 +72,8 @@ constexpr int kPropBlock = 256;
 #define LZQ_PROP_MIN_WAVES 2  // 217 VGPRs with the 3-step unroll, no spills (3 waves/SIMD: 168 VGPRs, spills; same time)
 #endif
 constexpr double kDeltaAdiabatic = 16.0;              // e^{-2 pi 16} = 2e-44
-constexpr double kStepsPerRadian = 3.0;              // ~1/3 rad of adiabatic phase per step at most
-constexpr double kCoreEps = 1e-5;                    // dressed following outside eps = m|alpha|/(4E^3) <= this
+constexpr double kStepsPerRadian = 6.0;              // Magnus steps per radian of adiabatic phase in a core
 constexpr double kMaxCellSteps = 16777216.0;         // per-cell Magnus steps beyond this: P = NaN (bad input)
-
-// G(x) = int_0^x sqrt(t^2 + m^2) dt
-__device__ __forceinline__ double wkb_G(double x, double m) {
-  return 0.5 * (x * sqrt(x * x + m * m) + (m > 0.0 ? m * m * asinh(x / m) : 0.0));
-}
 
 // LZ length of a crossing in xi: sqrt(v_w/|Delta'|) * max(1, sqrt(delta)).
 __device__ __forceinline__ double lz_length(double m, double a, double v_w) {
@@ -118,57 +119,15 @@ __device__ __forceinline__ void chi_like_dressed(double d, double ddot, double m
   u1 = plus ? b.p1 : b.q1;
 }
 
-// T(x0) = int_{|x0|}^inf dx / (x^2 + m^2)^{5/2}: closed form, or its series in u = m^2/x0^2 where
-// the closed form cancels (u < 1e-3; truncation ~u^4).
-__device__ __forceinline__ double tail_T(double x0, double m) {
-  x0 = fabs(x0);
-  const double u = (m * m) / (x0 * x0);
-  if (u < 1e-3) {
-    const double ix2 = 1.0 / (x0 * x0);
-    return (0.25 - u * (5.0 / 12.0 - u * (35.0 / 64.0 - u * (21.0 / 32.0)))) * ix2 * ix2;
-  }
-  const double E = sqrt(x0 * x0 + m * m);
-  const double m2 = m * m;
-  return (2.0 - x0 * (2.0 * x0 * x0 + 3.0 * m2) / (E * E * E)) / (3.0 * m2 * m2);
-}
-
-// Half-width (in xi) of a Magnus cell's core (tests/lz_ref.py core_halfwidth): 2K LZ lengths
-// for delta <= 1 (there the transition builds up over the whole crossing region and the
-// dressed-following error is set by the distance in LZ lengths: ~1e-12 at 40); for delta > 1
-// out to |D| where eps = m|alpha|/(4E^3) = kCoreEps (following error ~eps^2), clamped to
-// [1, 2K] LZ lengths.
 #ifndef LZQ_PROP_CORE
 #define LZQ_PROP_CORE 1  // 0: Magnus over every whole cell (round-1 scheme; tools/ablate_prop.py)
 #endif
-__device__ __forceinline__ double core_halfwidth(double m, double a, double v_w, double K) {
-  if (!LZQ_PROP_CORE) return INFINITY;
-  const double L = lz_length(m, a, v_w);
-  if (m * m <= 2.0 * v_w * a) return 2.0 * K * L;
-  const double Ec = cbrt(m * a * v_w / (4.0 * kCoreEps));
-  const double Dc = sqrt(fmax(Ec * Ec - m * m, 0.0));
-  return fmin(2.0 * K * L, fmax(L, Dc / a));
-}
 
-// Dressed-basis following of psi from xa to xb on one side of crossing xc (tests/lz_ref.py
-// far_segment): the dressed amplitudes pick up exp(-+ i (Phi + (m^2 |alpha|/8) |int dD/E^5|)),
-// the WKB phase plus the second-order dressed energy over the segment (the adiabatic cells'
-// tail_T terms).
-__device__ __forceinline__ void dressed_follow(Cplx& p0, Cplx& p1, double m, double a, double slope, double xc,
-                                               double xa, double xb, double v_w) {
-  const double Da = slope * (xa - xc), Db = slope * (xb - xc);
-  const double ddot = slope * v_w;
-  const Dressed A = dressed_basis(Da, ddot, m), B = dressed_basis(Db, ddot, m);
-  const Cplx bp = inner(A.p0, A.p1, p0, p1), bm = inner(A.q0, A.q1, p0, p1);
-  const double Phi = (wkb_G(a * (xb - xc), m) - wkb_G(a * (xa - xc), m)) / (a * v_w);
-  const double corr = 0.125 * m * m * a * v_w * fabs(tail_T(Da, m) - tail_T(Db, m));
-  double sn, cs;
-  sincos(Phi + corr, &sn, &cs);
-  const Cplx bp2 = {bp.re * cs + bp.im * sn, bp.im * cs - bp.re * sn};  // * e^{-i ph}
-  const Cplx bm2 = {bm.re * cs - bm.im * sn, bm.im * cs + bm.re * sn};  // * e^{+i ph}
-  p0 = {bp2.re * B.p0.re - bp2.im * B.p0.im + bm2.re * B.q0.re - bm2.im * B.q0.im,
-        bp2.re * B.p0.im + bp2.im * B.p0.re + bm2.re * B.q0.im + bm2.im * B.q0.re};
-  p1 = {bp2.re * B.p1.re - bp2.im * B.p1.im + bm2.re * B.q1.re - bm2.im * B.q1.im,
-        bp2.re * B.p1.im + bp2.im * B.p1.re + bm2.re * B.q1.im + bm2.im * B.q1.re};
+// Core of a delta <= 16 cell in xi: [xc - W, xc + W], W = tau_c v_w / sqrt(alpha)
+__device__ __forceinline__ double core_halfwidth(double m, double a, double v_w) {
+  if (!LZQ_PROP_CORE) return INFINITY;
+  const double sa = sqrt(a * v_w);
+  return sa_core_tau(m / sa) * v_w / sa;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -205,7 +164,7 @@ __device__ double point_steps(const double* mm, const double* dp, const double* 
     if (delta > kDeltaAdiabatic) {
       total += 4.0;  // closed-form cell: a few steps' worth of work
     } else {
-      const double W = core_halfwidth(mc, ac, v_w, K);
+      const double W = core_halfwidth(mc, ac, v_w);
       const double cl = fmax(left, xcc - W), cr = fmin(right, xcc + W);
       const double Phic = (wkb_G(ac * (cr - xcc), mc) - wkb_G(ac * (cl - xcc), mc)) / (ac * v_w);
       total += fmax((double)S, ceil(Phic * kStepsPerRadian));
@@ -271,12 +230,69 @@ __global__ __launch_bounds__(kPropBlock) void lz_scatter_kernel(const int32_t* _
   if (p < n) order[base[b] + r] = (int32_t)p;
 }
 
+constexpr int kFollowDoubles = 10;  // per (point, cell): two SU(2) matrices, the core's edges
+
+// Follow matrices of every (point, cell): one thread each.  Cell c's edges are computed with the
+// propagate kernel's own expressions (so bit-identical), and for a delta <= 16 cell whose core is
+// narrower than the cell the superadiabatic transfer matrices of the stretch left of the core and
+// right of it go to follow[(p n_cross + c) 10 + 0..3 / 4..7] as (a.re, a.im, b.re, b.im), and
+// the core's edges cl, cr to + 8, 9 (so the propagate kernel never evaluates the core width).
+__global__ __launch_bounds__(kPropBlock) void lz_follow_kernel(const double* __restrict__ m_mix,
+                                                               const double* __restrict__ dprime,
+                                                               const double* __restrict__ xi,
+                                                               const double* __restrict__ vw, int64_t n,
+                                                               int32_t n_cross, double v_w0, double K,
+                                                               double* __restrict__ follow) {
+  const int64_t t = (int64_t)blockIdx.x * kPropBlock + threadIdx.x;
+  if (t >= n * n_cross) return;
+  const int64_t p = t / n_cross;
+  const int c = (int)(t - p * n_cross);
+  const double v_w = vw ? vw[p] : v_w0;
+  if (!(v_w > 0.0)) return;  // the propagate kernel writes NaN for this point
+  const double* mm = m_mix + p * n_cross;
+  const double* dp = dprime + p * n_cross;
+  const double* xc = xi + p * n_cross;
+  const double ac = fabs(dp[c]), mc = mm[c], xcc = xc[c];
+  double left, right;
+  if (c == 0) {
+    left = xc[0] - K * lz_length(mm[0], fabs(dp[0]), v_w);
+  } else {
+    const double ap = fabs(dp[c - 1]);
+    left = (ap * xc[c - 1] + ac * xcc) / (ap + ac);
+  }
+  if (c + 1 < n_cross) {
+    const double an = fabs(dp[c + 1]);
+    right = (ac * xcc + an * xc[c + 1]) / (ac + an);
+  } else {
+    right = xcc + K * lz_length(mc, ac, v_w);
+  }
+  const double delta = mc * mc / (2.0 * v_w * ac);
+  if (delta > kDeltaAdiabatic) return;
+  const double W = core_halfwidth(mc, ac, v_w);  // INFINITY without cores (LZQ_PROP_CORE=0)
+  const double cl = fmax(left, xcc - W), cr = fmin(right, xcc + W);
+  const double inv_vw = 1.0 / v_w;
+  const double sa = sqrt(ac * v_w), mh = mc / sa, sg = (c % 2 == 0) ? 1.0 : -1.0;
+  const double tau_c = W * sa * inv_vw;
+  double* out = follow + (p * n_cross + c) * kFollowDoubles;
+  out[8] = cl;
+  out[9] = cr;
+  if (left < cl) {
+    const SU2 m = sa_follow_matrix(mh, sg, sa * (left - xcc) * inv_vw, -tau_c);
+    out[0] = m.a.re, out[1] = m.a.im, out[2] = m.b.re, out[3] = m.b.im;
+  }
+  if (cr < right) {
+    const SU2 m = sa_follow_matrix(mh, sg, tau_c, sa * (right - xcc) * inv_vw);
+    out[4] = m.a.re, out[5] = m.a.im, out[6] = m.b.re, out[7] = m.b.im;
+  }
+}
+
 __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_kernel(const double* __restrict__ m_mix,
                                                                   const double* __restrict__ dprime,
                                                                   const double* __restrict__ xi,
                                                                   const double* __restrict__ vw, int64_t n,
                                                                   int32_t n_cross, double v_w0, double K,
                                                                   int32_t S, const int32_t* __restrict__ order,
+                                                                  const double* __restrict__ follow,
                                                                   double* __restrict__ P_out) {
   const int64_t tid = (int64_t)blockIdx.x * kPropBlock + threadIdx.x;
   if (tid >= n) return;
@@ -332,10 +348,10 @@ __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_k
       p1 = {bp2.re * R.p1.re - bp2.im * R.p1.im + bm2.re * R.q1.re - bm2.im * R.q1.im,
             bp2.re * R.p1.im + bp2.im * R.p1.re + bm2.re * R.q1.im + bm2.im * R.q1.re};
     } else {
-      // Magnus on the core, dressed following on either side of it
-      const double W = core_halfwidth(mc, ac, v_w, K);
-      const double cl = fmax(left, xcc - W), cr = fmin(right, xcc + W);
-      if (left < cl) dressed_follow(p0, p1, mc, ac, slope, xcc, left, cl, v_w);
+      // Magnus on the core, superadiabatic following on either side of it
+      const double* Mc = follow + (p * n_cross + c) * kFollowDoubles;  // lz_follow_kernel's output
+      const double cl = Mc[8], cr = Mc[9];
+      if (left < cl) su2_apply_mat({{Mc[0], Mc[1]}, {Mc[2], Mc[3]}}, p0, p1);
       const double Phic = (wkb_G(ac * (cr - xcc), mc) - wkb_G(ac * (cl - xcc), mc)) / (ac * v_w);
       const double Sd = fmax((double)S, ceil(Phic * kStepsPerRadian));
       if (!(Sd <= kMaxCellSteps)) {  // non-finite or absurd input (bounded for any valid one)
@@ -371,7 +387,7 @@ __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_k
         su2_apply(cs, sc * nx, sc * ny, sc * nz, p0, p1);
       }
 #undef FMA
-      if (cr < right) dressed_follow(p0, p1, mc, ac, slope, xcc, cr, right, v_w);
+      if (cr < right) su2_apply_mat({{Mc[4], Mc[5]}, {Mc[6], Mc[7]}}, p0, p1);
     }
     left = right;
     sgn = -sgn;
@@ -393,41 +409,71 @@ __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_k
 int lzq_set_error(int code, const char* msg);
 
 namespace {
-int propagate_launch(const double* d_m_mix, const double* d_dprime, const double* d_xi, const double* d_v_w, int64_t n,
-                     int32_t n_cross, double v_w, double window_lz, int32_t steps_per_crossing, double* d_P,
-                     void* stream) {
-  if (n == 0) return LZQ_OK;
-  if (n > 2147483647LL) return lzq_set_error(LZQ_EINVAL, "lzq_lz_propagate: n too large (int32 point order)");
+// Follow data take 80 B per (point, cell): batches are run in slices of at most this many
+// (point, cell) pairs (640 MiB).
+constexpr int64_t kFollowMaxPairs = (int64_t)1 << 23;
+
+int propagate_slice(const double* d_m_mix, const double* d_dprime, const double* d_xi, const double* d_v_w, int64_t n,
+                    int32_t n_cross, double v_w, double window_lz, int32_t steps_per_crossing, double* d_P,
+                    hipStream_t st) {
   const int64_t nb = (n + lzq::kPropBlock - 1) / lzq::kPropBlock;
-  hipStream_t st = (hipStream_t)stream;
-  // longest-first launch order (see lz_cost_kernel); stream-ordered scratch, so calls on
-  // different streams stay independent
-  int32_t* ws = nullptr;
-  const int32_t* order = nullptr;
-  if (LZQ_PROP_SORT && n >= lzq::kSortMinPoints) {
-    const size_t bytes = (size_t)(2 * n + 2 * lzq::kCostBins) * sizeof(int32_t);
-    hipError_t e = hipMallocAsync((void**)&ws, bytes, st);
+  // stream-ordered scratch (calls on different streams stay independent): the follow matrices,
+  // then the longest-first launch order (see lz_cost_kernel) for large batches
+  const bool sort = LZQ_PROP_SORT && n >= lzq::kSortMinPoints;
+  const size_t follow_bytes = (size_t)(n * n_cross) * lzq::kFollowDoubles * sizeof(double);
+  const size_t sort_bytes = sort ? (size_t)(2 * n + 2 * lzq::kCostBins) * sizeof(int32_t) : 0;
+  char* ws = nullptr;
+  {
+    hipError_t e = hipMallocAsync((void**)&ws, follow_bytes + sort_bytes, st);
     if (e != hipSuccess) return lzq_set_error(LZQ_EHIP, hipGetErrorString(e));
-    int32_t *bins = ws, *ord = ws + n, *hist = ws + 2 * n, *offs = hist + lzq::kCostBins;
-    e = hipMemsetAsync(hist, 0, lzq::kCostBins * sizeof(int32_t), st);
-    if (e != hipSuccess) {
-      (void)hipFreeAsync(ws, st);
-      return lzq_set_error(LZQ_EHIP, hipGetErrorString(e));
-    }
-    hipLaunchKernelGGL(lzq::lz_cost_kernel, dim3((unsigned)nb), dim3(lzq::kPropBlock), 0, st, d_m_mix, d_dprime, d_xi,
-                       d_v_w, n, n_cross, v_w, window_lz, steps_per_crossing, bins, hist);
-    hipLaunchKernelGGL(lzq::lz_bin_scan_kernel, dim3(1), dim3(64), 0, st, hist, offs);
-    hipLaunchKernelGGL(lzq::lz_scatter_kernel, dim3((unsigned)nb), dim3(lzq::kPropBlock), 0, st, bins, n, offs, ord);
-    order = ord;
   }
-  hipLaunchKernelGGL(lzq::lz_propagate_kernel, dim3((unsigned)nb), dim3(lzq::kPropBlock), 0, st,
-                     d_m_mix, d_dprime, d_xi, d_v_w, n, n_cross, v_w, window_lz, steps_per_crossing, order, d_P);
-  hipError_t e = hipGetLastError();
+  double* follow = (double*)ws;
+  const int32_t* order = nullptr;
+  hipError_t e = hipSuccess;
+  {
+    const int64_t nf = (n * n_cross + lzq::kPropBlock - 1) / lzq::kPropBlock;
+    hipLaunchKernelGGL(lzq::lz_follow_kernel, dim3((unsigned)nf), dim3(lzq::kPropBlock), 0, st, d_m_mix, d_dprime,
+                       d_xi, d_v_w, n, n_cross, v_w, window_lz, follow);
+  }
+  if (sort) {
+    int32_t* iw = (int32_t*)(ws + follow_bytes);
+    int32_t *bins = iw, *ord = iw + n, *hist = iw + 2 * n, *offs = hist + lzq::kCostBins;
+    e = hipMemsetAsync(hist, 0, lzq::kCostBins * sizeof(int32_t), st);
+    if (e == hipSuccess) {
+      hipLaunchKernelGGL(lzq::lz_cost_kernel, dim3((unsigned)nb), dim3(lzq::kPropBlock), 0, st, d_m_mix, d_dprime,
+                         d_xi, d_v_w, n, n_cross, v_w, window_lz, steps_per_crossing, bins, hist);
+      hipLaunchKernelGGL(lzq::lz_bin_scan_kernel, dim3(1), dim3(64), 0, st, hist, offs);
+      hipLaunchKernelGGL(lzq::lz_scatter_kernel, dim3((unsigned)nb), dim3(lzq::kPropBlock), 0, st, bins, n, offs,
+                         ord);
+      order = ord;
+    }
+  }
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(lzq::lz_propagate_kernel, dim3((unsigned)nb), dim3(lzq::kPropBlock), 0, st, d_m_mix, d_dprime,
+                       d_xi, d_v_w, n, n_cross, v_w, window_lz, steps_per_crossing, order, follow, d_P);
+    e = hipGetLastError();
+  }
   if (ws) {
     const hipError_t ef = hipFreeAsync(ws, st);
     if (e == hipSuccess) e = ef;
   }
   if (e != hipSuccess) return lzq_set_error(LZQ_EHIP, hipGetErrorString(e));
+  return LZQ_OK;
+}
+
+int propagate_launch(const double* d_m_mix, const double* d_dprime, const double* d_xi, const double* d_v_w, int64_t n,
+                     int32_t n_cross, double v_w, double window_lz, int32_t steps_per_crossing, double* d_P,
+                     void* stream) {
+  if (n == 0) return LZQ_OK;
+  if (n > 2147483647LL) return lzq_set_error(LZQ_EINVAL, "lzq_lz_propagate: n too large (int32 point order)");
+  const int64_t slice = std::max<int64_t>(1, kFollowMaxPairs / n_cross);
+  for (int64_t s0 = 0; s0 < n; s0 += slice) {
+    const int64_t k = std::min(slice, n - s0);
+    const int rc = propagate_slice(d_m_mix + s0 * n_cross, d_dprime + s0 * n_cross, d_xi + s0 * n_cross,
+                                   d_v_w ? d_v_w + s0 : nullptr, k, n_cross, v_w, window_lz, steps_per_crossing,
+                                   d_P + s0, (hipStream_t)stream);
+    if (rc != LZQ_OK) return rc;
+  }
   return LZQ_OK;
 }
 

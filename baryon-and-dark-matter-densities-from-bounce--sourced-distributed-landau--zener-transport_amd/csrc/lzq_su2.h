@@ -10,7 +10,7 @@ struct Cplx {
 };
 
 // <u|psi> for u = (u0, u1)
-__device__ __forceinline__ Cplx inner(Cplx u0, Cplx u1, Cplx p0, Cplx p1) {
+__host__ __device__ __forceinline__ Cplx inner(Cplx u0, Cplx u1, Cplx p0, Cplx p1) {
   return {u0.re * p0.re + u0.im * p0.im + u1.re * p1.re + u1.im * p1.im,
           u0.re * p0.im - u0.im * p0.re + u1.re * p1.im - u1.im * p1.re};
 }
@@ -25,13 +25,26 @@ static __constant__ double kCosC[10] = {0x1.0000000000000p+0,  -0x1.000000000000
                                         -0x1.6c16c16c16c17p-10, 0x1.a01a01a01a01ap-16, -0x1.27e4fb7789f5cp-22,
                                         0x1.1eed8eff8d898p-29,  -0x1.93974a8c07c9dp-37, 0x1.ae7f3e733b81fp-45,
                                         -0x1.6827863b97d97p-53};
+// Three-address FP64 fma.  The Horner steps below add a loop-invariant coefficient; written as
+// __builtin_fma the compiler picks the two-address v_fmac_f64 and copies the coefficient into the
+// accumulator first (one v_mov_b64 per term, ~19 per Magnus step); v_fma_f64 needs no copy.
+#ifndef LZQ_SU2_FMA3
+#define LZQ_SU2_FMA3 1  // 0: __builtin_fma (tools/ablate_prop.py)
+#endif
+__device__ __forceinline__ double fma3(double a, double b, double c) {
+  if (!LZQ_SU2_FMA3) return __builtin_fma(a, b, c);
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 __device__ __forceinline__ void cos_sinc(double x2, double& cs, double& sc) {
   if (x2 <= 1.0) {
     double ps = kSincC[8], pc = kCosC[9];
 #pragma unroll
-    for (int k = 7; k >= 0; --k) ps = __builtin_fma(ps, x2, kSincC[k]);
+    for (int k = 7; k >= 0; --k) ps = fma3(ps, x2, kSincC[k]);
 #pragma unroll
-    for (int k = 8; k >= 0; --k) pc = __builtin_fma(pc, x2, kCosC[k]);
+    for (int k = 8; k >= 0; --k) pc = fma3(pc, x2, kCosC[k]);
     sc = ps;
     cs = pc;
   } else {

@@ -1,0 +1,304 @@
+// lzq_superadiabatic.h -- superadiabatic frames of a two-level crossing, shared
+// device code of the LZ propagator.  Not ABI.  tests/lz_ref.py (sa_levels, sa_to_frame,
+// sa_from_frame, sa_phase, sa_core_tau) restates every function here.
+//
+// Units: alpha = |dD/dt| of the cell, tau = sqrt(alpha) t, Dh = D/sqrt(alpha) = sg tau (sg = +-1),
+// mh = m/sqrt(alpha).  Iterated adiabatic frames (Berry's superadiabatic iteration):
+//   level j: H_j = e_j sz + g_j sigma_a,  a = x for even j, y for odd j,  e_0 = Dh, g_0 = mh;
+//   V_j = exp(-i theta_j sy) (even j) or exp(+i theta_j sx) (odd j), theta_j = atan2(g_j, e_j)/2,
+//   diagonalises it; in the next frame e_{j+1} = sqrt(e_j^2 + g_j^2) and the coupling is
+//   g_{j+1} = -theta_j' (even j) or +theta_j' (odd j).
+// Far from the crossing the couplings fall like g_j ~ mh E^-(2j+1): a state is followed in the
+// frame of order N (psi = V_0 .. V_{N-1} phi) with phi's components only picking up
+// exp(-+ i int e_N dtau), and the error is the first neglected angle, |theta_N| at the inner end
+// of the stretch (measured against a converged ODE solve for N = 6 .. 10; tests/lz_ref.py).
+// theta_j' needs the j-th derivative of the level-0 data, so the levels run on truncated Taylor
+// series ("jets") in tau of length N.  The half-angles come from cos 2theta = e/r and
+// sin 2theta = g/r with r = e_{j+1} (already computed): no atan2, no sincos.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+
+#include "lzq_su2.h"
+
+namespace lzq {
+
+constexpr int kSALevels = 10;      // frame order outside a Magnus core (rotations V_0 .. V_9)
+constexpr double kSATol = 1e-11;   // core edge: first neglected angle |theta_10| <= this
+constexpr double kSAC = 3.2e5;     // |theta_10| <= kSAC mh / E^21 (fitted; conservative for mh > 1)
+constexpr int kSAFarLevels = 6;    // the outer end of a follow stretch, when that order is enough:
+constexpr double kSAFarC = 80.0;   //   |theta_6| <= kSAFarC mh / E^13 (fitted) <= kSATol / 10
+
+// cos theta, sin theta from cos 2theta = c2, sin 2theta = s2 >= 0 (theta in [0, pi/2]) or any
+// s2 with c2 > 0, without cancellation
+__host__ __device__ __forceinline__ void half_angle(double c2, double s2, bool pos, double& c, double& s) {
+  if (pos) {
+    c = sqrt(0.5 * (1.0 + c2));
+    s = s2 / (2.0 * c);
+  } else {
+    s = sqrt(0.5 * (1.0 - c2));
+    c = s2 / (2.0 * s);
+  }
+}
+
+// The frame rotation U = V_0 V_1 .. V_{N-1} accumulated as it is built: an SU(2) element
+// [[a, -conj(b)], [b, conj(a)]], so 4 doubles instead of every level's (cos, sin).
+struct SU2 {
+  Cplx a, b;
+};
+
+// U <- U V_j with V_j = [[c, -s], [s, c]] (even j) or [[c, i s], [i s, c]] (odd j)
+template <bool kEven>
+__host__ __device__ __forceinline__ void su2_right_mul(SU2& u, double c, double s) {
+  Cplx na, nb;
+  if constexpr (kEven) {  // V = (a2 = c, b2 = s): a = a1 c - conj(b1) s, b = b1 c + conj(a1) s
+    na = {u.a.re * c - u.b.re * s, u.a.im * c + u.b.im * s};
+    nb = {u.b.re * c + u.a.re * s, u.b.im * c - u.a.im * s};
+  } else {  // V = (a2 = c, b2 = i s): a = a1 c - conj(b1) i s, b = b1 c + conj(a1) i s
+    na = {u.a.re * c - u.b.im * s, u.a.im * c - u.b.re * s};
+    nb = {u.b.re * c + u.a.im * s, u.b.im * c + u.a.re * s};
+  }
+  u.a = na;
+  u.b = nb;
+}
+
+// Generic levels J0 + J .. of jets e, g of length M - J (in place).  Accumulates the frame
+// rotation into u (kRot) and stores ev[lev] = e_{lev+1}, gv[lev] = g_lev (kEG).
+template <int M, int J, int J0, bool kRot, bool kEG>
+__host__ __device__ __forceinline__ void sa_chain(double (&e)[M], double (&g)[M], SU2& u, double* ev, double* gv) {
+  if constexpr (J < M) {
+    constexpr int n = M - J;
+    constexpr int lev = J0 + J;
+    double q[n];  // e^2 + g^2, later its square root (e_{lev+1}); symmetric sums: half the terms
+#pragma unroll
+    for (int l = 0; l < n; ++l) {
+      double acc = 0.0;
+#pragma unroll
+      for (int i = 0; 2 * i < l; ++i) acc = __builtin_fma(e[i], e[l - i], __builtin_fma(g[i], g[l - i], acc));
+      acc += acc;
+      if (l % 2 == 0) acc = __builtin_fma(e[l / 2], e[l / 2], __builtin_fma(g[l / 2], g[l / 2], acc));
+      q[l] = acc;
+    }
+    const double r0 = sqrt(q[0]);
+    if constexpr (kRot) {
+      const double ir = 1.0 / r0;
+      double c, s;
+      half_angle(e[0] * ir, g[0] * ir, e[0] >= 0.0, c, s);
+      su2_right_mul<lev % 2 == 0>(u, c, s);
+    }
+    if constexpr (kEG) {
+      ev[lev] = r0;
+      gv[lev] = g[0];
+    }
+    if constexpr (n > 1) {
+      // theta' = (e g' - g e') / (2 q): w = num / q, g_next = -+ w / 2
+      const double iq = 1.0 / q[0];
+      double w[n - 1];
+#pragma unroll
+      for (int l = 0; l < n - 1; ++l) {
+        // num_l = sum_{i + j = l + 1} j (e_i g_j - g_i e_j); the pairs (i, j), (j, i) with i, j >= 1
+        // combine to (j - i) (e_i g_j - g_i e_j)
+        double acc = (double)(l + 1) * __builtin_fma(e[0], g[l + 1], -(g[0] * e[l + 1]));
+#pragma unroll
+        for (int i = 1; 2 * i < l + 1; ++i) {
+          const double k = (double)(l + 1 - 2 * i);
+          acc = __builtin_fma(k, __builtin_fma(e[i], g[l + 1 - i], -(g[i] * e[l + 1 - i])), acc);
+        }
+#pragma unroll
+        for (int i = 0; i < l; ++i) acc = __builtin_fma(-w[i], q[l - i], acc);
+        w[l] = acc * iq;
+      }
+      // sqrt(q) in place: r_l = (q_l - sum_{i=1}^{l-1} r_i r_{l-i}) / (2 r_0)
+      const double h0 = 0.5 / r0;
+      q[0] = r0;
+#pragma unroll
+      for (int l = 1; l < n - 1; ++l) {
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 1; 2 * i < l; ++i) acc = __builtin_fma(q[i], q[l - i], acc);
+        acc += acc;
+        if (l % 2 == 0) acc = __builtin_fma(q[l / 2], q[l / 2], acc);
+        q[l] = (q[l] - acc) * h0;
+      }
+      constexpr double f = (lev % 2 == 0) ? -0.5 : 0.5;
+#pragma unroll
+      for (int l = 0; l < n - 1; ++l) {
+        g[l] = f * w[l];
+        e[l] = q[l];
+      }
+      sa_chain<M, J + 1, J0, kRot, kEG>(e, g, u, ev, gv);
+    }
+  }
+}
+
+// Levels 0 .. N-1 of the linear crossing Dh(tau0 + h) = Dh + sg h, constant mh: the frame
+// rotation U = V_0 .. V_{N-1} (kRot) and ev[j] = e_{j+1}, gv[j] = g_j (kEG).  Level 0 is done in
+// closed form (its jets are sparse).
+template <int N, bool kRot, bool kEG>
+__host__ __device__ __forceinline__ void sa_levels_linear(double Dh, double sg, double mh, SU2& u, double* ev, double* gv) {
+  // q = (Dh + sg h)^2 + mh^2 = [E^2, 2 sg Dh, 1]
+  const double q0 = __builtin_fma(Dh, Dh, mh * mh), q1 = 2.0 * sg * Dh;
+  const double E = sqrt(q0);
+  const double iE = 1.0 / E;
+  if constexpr (kRot) {
+    double c, s;
+    half_angle(Dh * iE, mh * iE, Dh >= 0.0, c, s);
+    u.a = {c, 0.0};
+    u.b = {s, 0.0};
+  }
+  if constexpr (kEG) {
+    ev[0] = E;
+    gv[0] = mh;
+  }
+  if constexpr (N > 1) {
+    constexpr int M = N - 1;
+    double e[M], g[M];
+    // e_1 = sqrt(q) (jet); theta_0' = w/2 with w = -mh sg / q, g_1 = -w/2
+    const double h0 = 0.5 * iE;
+    e[0] = E;
+    if constexpr (M > 1) e[1] = q1 * h0;
+#pragma unroll
+    for (int l = 2; l < M; ++l) {
+      double acc = 0.0;
+#pragma unroll
+      for (int i = 1; 2 * i < l; ++i) acc = __builtin_fma(e[i], e[l - i], acc);
+      acc += acc;
+      if (l % 2 == 0) acc = __builtin_fma(e[l / 2], e[l / 2], acc);
+      e[l] = ((l == 2 ? 1.0 : 0.0) - acc) * h0;
+    }
+    const double iq = 1.0 / q0;
+    double w[M];
+    w[0] = -mh * sg * iq;
+#pragma unroll
+    for (int l = 1; l < M; ++l) {
+      double acc = -w[l - 1] * q1;
+      if (l >= 2) acc = acc - w[l - 2];
+      w[l] = acc * iq;
+    }
+#pragma unroll
+    for (int l = 0; l < M; ++l) g[l] = -0.5 * w[l];
+    sa_chain<M, 0, 1, kRot, kEG>(e, g, u, ev, gv);
+  }
+}
+
+// psi <- U^+ psi (diabatic -> frame), U = [[a, -conj(b)], [b, conj(a)]]
+__host__ __device__ __forceinline__ void su2_apply_adj(const SU2& u, Cplx& p0, Cplx& p1) {
+  // U^+ = [[conj(a), conj(b)], [-b, a]]
+  const Cplx q0 = {u.a.re * p0.re + u.a.im * p0.im + u.b.re * p1.re + u.b.im * p1.im,
+                   u.a.re * p0.im - u.a.im * p0.re + u.b.re * p1.im - u.b.im * p1.re};
+  const Cplx q1 = {-(u.b.re * p0.re - u.b.im * p0.im) + u.a.re * p1.re - u.a.im * p1.im,
+                   -(u.b.re * p0.im + u.b.im * p0.re) + u.a.re * p1.im + u.a.im * p1.re};
+  p0 = q0;
+  p1 = q1;
+}
+
+// psi <- U psi (frame -> diabatic)
+__host__ __device__ __forceinline__ void su2_apply_mat(const SU2& u, Cplx& p0, Cplx& p1) {
+  const Cplx q0 = {u.a.re * p0.re - u.a.im * p0.im - (u.b.re * p1.re + u.b.im * p1.im),
+                   u.a.re * p0.im + u.a.im * p0.re - (u.b.re * p1.im - u.b.im * p1.re)};
+  const Cplx q1 = {u.b.re * p0.re - u.b.im * p0.im + u.a.re * p1.re + u.a.im * p1.im,
+                   u.b.re * p0.im + u.b.im * p0.re + u.a.re * p1.im - u.a.im * p1.re};
+  p0 = q0;
+  p1 = q1;
+}
+
+// Core half-width in tau: out to E = sqrt(tau^2 + mh^2) where kSAC max(mh, kSAMFloor) / E^21
+// = kSATol, at least 1.  The following error is an amplitude ~ |theta_10| ~ mh / E^21, and for
+// small mh the conversion probability is P ~ pi mh^2, so its relative error ~ 1/E^21 would grow as
+// mh shrinks: the floor keeps it <= ~1e-10 (E >= 5.4) however small the coupling.
+constexpr double kSAMFloor = 0.05;
+__host__ __device__ __forceinline__ double sa_core_tau(double mh) {
+  const double Ec = pow(kSAC * fmax(mh, kSAMFloor) / kSATol, 1.0 / (2.0 * kSALevels + 1.0));
+  return sqrt(fmax(Ec * Ec - mh * mh, 1.0));
+}
+
+// G(x) = int_0^x sqrt(t^2 + m^2) dt
+__host__ __device__ __forceinline__ double wkb_G(double x, double m) {
+  return 0.5 * (x * sqrt(x * x + m * m) + (m > 0.0 ? m * m * asinh(x / m) : 0.0));
+}
+
+// T(x0) = int_{|x0|}^inf dx / (x^2 + m^2)^{5/2}: closed form, or its series in u = m^2/x0^2 where
+// the closed form cancels (u < 1e-3; truncation ~u^4).
+__host__ __device__ __forceinline__ double tail_T(double x0, double m) {
+  x0 = fabs(x0);
+  const double u = (m * m) / (x0 * x0);
+  if (u < 1e-3) {
+    const double ix2 = 1.0 / (x0 * x0);
+    return (0.25 - u * (5.0 / 12.0 - u * (35.0 / 64.0 - u * (21.0 / 32.0)))) * ix2 * ix2;
+  }
+  const double E = sqrt(x0 * x0 + m * m);
+  const double m2 = m * m;
+  return (2.0 - x0 * (2.0 * x0 * x0 + 3.0 * m2) / (E * E * E)) / (3.0 * m2 * m2);
+}
+
+// int_ta^tb e_4 dtau on one side of a crossing (1 <= |ta|, |tb|; tests/lz_ref.py sa_phase): the
+// WKB phase G, the leading dressed-energy term mh^2/(8E^5) in closed form (tail_T), and the rest,
+// e_4 - E - mh^2/(8E^5) = O(E^-9) (differences e_{j+1} - e_j = g_j^2/(e_j + e_{j+1}), no
+// cancellation), by 4-point Gauss-Legendre in u = 1/|tau|.  e_5 - e_4 < 1e-12 beyond the core.
+__host__ __device__ __forceinline__ double sa_phase(double ta, double tb, double mh) {
+  constexpr double gx[4] = {-0.8611363115940526, -0.3399810435848563, 0.3399810435848563, 0.8611363115940526};
+  constexpr double gw[4] = {0.3478548451374538, 0.6521451548625461, 0.6521451548625461, 0.3478548451374538};
+  const double base = wkb_G(tb, mh) - wkb_G(ta, mh);
+  const double lead = mh * mh * 0.125 * fabs(tail_T(ta, mh) - tail_T(tb, mh));
+  const double u1 = 1.0 / fabs(ta), u2 = 1.0 / fabs(tb);
+  const double ulo = fmin(u1, u2), uhi = fmax(u1, u2);
+  const double half = 0.5 * (uhi - ulo), mid = 0.5 * (uhi + ulo);
+  double acc = 0.0;
+#pragma nounroll
+  for (int k = 0; k < 4; ++k) {
+    const double u = __builtin_fma(half, gx[k], mid);
+    SU2 unused;
+    double ev[4], gv[4];
+    sa_levels_linear<4, false, true>(1.0 / u, 1.0, mh, unused, ev, gv);
+    const double E = ev[0];
+    const double d1 = gv[1] * gv[1] / (E + ev[1]);
+    const double d2 = gv[2] * gv[2] / (ev[1] + ev[2]);
+    const double d3 = gv[3] * gv[3] / (ev[2] + ev[3]);
+    const double E5 = E * E * E * E * E;
+    const double f = d3 + d2 - mh * mh * d1 / (8.0 * E5 * (E + ev[1]));
+    acc = __builtin_fma(gw[k], f / (u * u), acc);
+  }
+  return base + lead + half * acc;
+}
+
+// Transfer matrix of superadiabatic following from tau = ta to tb (ta < tb, one side of the
+// crossing; the cell's own units, tests/lz_ref.py sa_follow): U(tb) diag(e^{-i ph}, e^{+i ph})
+// U(ta)^+ with U the frame rotation of order kSALevels and ph = int e dtau.  Error ~ |theta_10| at
+// the inner end.  It does not depend on the state, so lz_follow_kernel computes it ahead of the
+// propagation (the jets need ~90 VGPRs of their own).
+__host__ __device__ __forceinline__ SU2 sa_follow_matrix(double mh, double sg, double ta, double tb) {
+  // the outer end (|tau| larger) may use the order-6 frame: the two frames differ there by the
+  // neglected angles theta_6 .. theta_9 ~ kSAFarC mh / E^13
+  const double tf = fmax(fabs(ta), fabs(tb));
+  const double Ef2 = tf * tf + mh * mh, Ef4 = Ef2 * Ef2, Ef12 = Ef4 * Ef4 * Ef4;
+  const bool far6 = kSAFarC * fmax(mh, kSAMFloor) <= 0.1 * kSATol * Ef12 * sqrt(Ef2);
+  SU2 m;
+  // one frame evaluation per iteration: two side by side (they are independent) need ~250 VGPRs
+#pragma nounroll
+  for (int end = 0; end < 2; ++end) {
+    const double tau = end ? tb : ta;
+    SU2 u;
+    if (far6 && fabs(tau) == tf)
+      sa_levels_linear<kSAFarLevels, true, false>(sg * tau, sg, mh, u, nullptr, nullptr);
+    else
+      sa_levels_linear<kSALevels, true, false>(sg * tau, sg, mh, u, nullptr, nullptr);
+    if (end == 0) {
+      // m = P U(ta)^+ with P = diag(e^{-i ph}, e^{i ph}) = (a = e^{-i ph}, b = 0), U^+ = (conj(a), -b)
+      const double ph = sa_phase(ta, tb, mh);
+      const double sn = sin(ph), cs = cos(ph);
+      m.a = {cs * u.a.re - sn * u.a.im, -sn * u.a.re - cs * u.a.im};   // e^{-i ph} conj(a)
+      m.b = {sn * u.b.im - cs * u.b.re, -(cs * u.b.im + sn * u.b.re)};  // e^{+i ph} (-b)
+    } else {
+      // m = U(tb) m: a = a1 a2 - conj(b1) b2, b = b1 a2 + conj(a1) b2
+      const SU2 r = m;
+      m.a = {u.a.re * r.a.re - u.a.im * r.a.im - (u.b.re * r.b.re + u.b.im * r.b.im),
+             u.a.re * r.a.im + u.a.im * r.a.re - (u.b.re * r.b.im - u.b.im * r.b.re)};
+      m.b = {u.b.re * r.a.re - u.b.im * r.a.im + u.a.re * r.b.re + u.a.im * r.b.im,
+             u.b.re * r.a.im + u.b.im * r.a.re + u.a.re * r.b.im - u.a.im * r.b.re};
+    }
+  }
+  return m;
+}
+
+}  // namespace lzq

@@ -59,7 +59,7 @@ class CrossingSpec:
     spacing_lz: float = 40.0
     jitter: float = 0.1
     window_lz: float = 20.0
-    steps: int = 1000      # Magnus steps per crossing (floor): <= 2e-9 from the exact solution
+    steps: int = 64        # Magnus steps per crossing core (floor): <= 1e-10 from the exact solution
     seed: int = 5
 
     def pattern(self) -> np.ndarray:

@@ -58,40 +58,125 @@ def tail_T(x0, m):
 
 
 DELTA_ADIABATIC = 16.0
-STEPS_PER_RADIAN = 3.0
-CORE_EPS = 1e-5   # Magnus core of a cell: where the adiabaticity eps = m|alpha|/(4E^3) exceeds this
+STEPS_PER_RADIAN = 6.0   # Magnus steps per radian of adiabatic phase in a cell's core
+SA_LEVELS = 10           # superadiabatic frame order outside the core (rotations V_0 .. V_9)
+SA_TOL = 1e-11           # core edge: next rotation angle |theta_10| ~ SA_C m / E^21 <= SA_TOL
+SA_C = 3.2e5             # fitted: |theta_10| <= 3.2e5 m / E^21 (alpha = 1 units), conservative for m > 1
+SA_M_FLOOR = 0.05        # core width floor: relative P error <= ~1e-10 for small couplings
+SA_FAR_LEVELS = 6        # order of the frame at a follow stretch's outer end when
+SA_FAR_C = 80.0          #   |theta_6| ~ SA_FAR_C max(mh, floor) / E^13 <= SA_TOL / 10
+GL4_X = (-0.8611363115940526, -0.3399810435848563, 0.3399810435848563, 0.8611363115940526)
+GL4_W = (0.3478548451374538, 0.6521451548625461, 0.6521451548625461, 0.3478548451374538)
 
 
-def core_halfwidth(m, a, v_w, K):
-    """Half-width (in xi) of the cell's Magnus core.  delta <= 1: 2K LZ lengths (the
-    transition builds up over the whole crossing region, so the dressed following error is set
-    by the distance in LZ lengths: ~1e-12 at 2K = 40, 2e-11 at K = 20).  delta > 1: out to
-    |D| where eps = m|alpha|/(4E^3) falls to CORE_EPS (beyond it the dressed basis follows the
-    state to ~eps^2), at least one and at most 2K LZ lengths.  Cells narrower than the core
-    (C5's are +-20 LZ lengths) are stepped end to end as before."""
-    L = xi_lz(m, a, v_w)
-    if m * m <= 2.0 * v_w * a:     # delta <= 1
-        return 2.0 * K * L
-    Ec = (m * a * v_w / (4.0 * CORE_EPS)) ** (1.0 / 3.0)
-    Dc = math.sqrt(max(Ec * Ec - m * m, 0.0))
-    return min(2.0 * K * L, max(L, Dc / a))
+def sa_levels(Dh, s, mh, N):
+    """Superadiabatic frames of H = Dh sz + mh sx (alpha = 1 units: dDh/dtau = s = +-1) at one
+    instant, by Taylor jets of length N in tau.  Level j: H_j = e_j sz + g_j sigma_(x if j even
+    else y); the rotation V_j (about y for even j, about x for odd j) by theta_j = atan2(g_j, e_j)/2
+    diagonalises it, and the frame after it has e_{j+1} = sqrt(e_j^2 + g_j^2), coupling
+    g_{j+1} = -theta_j' (j even) or +theta_j' (j odd).  Returns [(cos theta_j, sin theta_j)],
+    the values e_1 .. e_N and g_0 .. g_{N-1}."""
+    e = [Dh, s] + [0.0] * (N - 2) if N >= 2 else [Dh]
+    g = [mh] + [0.0] * (N - 1)
+    cs, ev, gv = [], [], []
+    for j in range(N):
+        n = N - j
+        q = [sum(e[i] * e[l - i] + g[i] * g[l - i] for i in range(l + 1)) for l in range(n)]
+        r = [math.sqrt(q[0])]
+        for l in range(1, max(n - 1, 1)):
+            r.append((q[l] - sum(r[i] * r[l - i] for i in range(1, l))) / (2.0 * r[0]))
+        c2, s2 = e[0] / r[0], g[0] / r[0]
+        if e[0] >= 0.0:
+            c = math.sqrt(0.5 * (1.0 + c2))
+            sn = s2 / (2.0 * c)
+        else:
+            sn = math.sqrt(0.5 * (1.0 - c2))
+            c = s2 / (2.0 * sn)
+        cs.append((c, sn))
+        ev.append(r[0])
+        gv.append(g[0])
+        if n == 1:
+            break
+        # theta_j' = (e g' - g e') / (2 q)
+        num = [sum(e[i] * (l - i + 1) * g[l - i + 1] - g[i] * (l - i + 1) * e[l - i + 1] for i in range(l + 1))
+               for l in range(n - 1)]
+        w = []
+        for l in range(n - 1):
+            w.append((num[l] - sum(w[i] * q[l - i] for i in range(l))) / q[0])
+        f = -0.5 if j % 2 == 0 else 0.5
+        g = [f * x for x in w]
+        e = r[:n - 1]
+    return cs, ev, gv
 
 
-def far_segment(p, m, a, slope, xc, xa, xb, v_w):
-    """Dressed-basis following from xa to xb on one side of crossing xc (no stepping): the
-    dressed amplitudes pick up exp(-+ i (Phi + (m^2 |alpha|/8) |int dD/E^5|)) over the segment
-    (the second-order dressed energy; the same terms as adiabatic_cell's tails)."""
-    Da, Db = slope * (xa - xc), slope * (xb - xc)
-    ddot = slope * v_w
-    lp, lm = dressed_basis(Da, ddot, m)
-    rp, rm = dressed_basis(Db, ddot, m)
-    bp, bm = np.vdot(lp, p), np.vdot(lm, p)
-    Phi = (wkb_G(a * (xb - xc), m) - wkb_G(a * (xa - xc), m)) / (a * v_w)
-    corr = m * m * a * v_w / 8.0 * abs(tail_T(Da, m) - tail_T(Db, m))
-    ph = Phi + corr
-    bp *= complex(math.cos(ph), -math.sin(ph))
-    bm *= complex(math.cos(ph), math.sin(ph))
-    return bp * rp + bm * rm
+def sa_to_frame(p, cs):
+    """phi = V_{N-1}^+ ... V_0^+ p (diabatic -> frame N)."""
+    a, b = complex(p[0]), complex(p[1])
+    for j, (c, sn) in enumerate(cs):
+        if j % 2 == 0:
+            a, b = c * a + sn * b, c * b - sn * a
+        else:
+            a, b = c * a - 1j * sn * b, c * b - 1j * sn * a
+    return a, b
+
+
+def sa_from_frame(a, b, cs):
+    """p = V_0 ... V_{N-1} (a, b) (frame N -> diabatic)."""
+    for j in range(len(cs) - 1, -1, -1):
+        c, sn = cs[j]
+        if j % 2 == 0:
+            a, b = c * a - sn * b, c * b + sn * a
+        else:
+            a, b = c * a + 1j * sn * b, c * b + 1j * sn * a
+    return np.array([a, b])
+
+
+def sa_core_tau(mh):
+    """Core half-width in tau = sqrt(alpha) (xi - xi_c)/v_w: out to E = sqrt(tau^2 + mh^2) where
+    the first neglected rotation, |theta_10| ~ SA_C mh / E^21, falls to SA_TOL, with mh floored at
+    SA_M_FLOOR (for small mh, P ~ pi mh^2 and the relative error ~ 1/E^21); at least 1."""
+    Ec = (SA_C * max(mh, SA_M_FLOOR) / SA_TOL) ** (1.0 / (2 * SA_LEVELS + 1))
+    return math.sqrt(max(Ec * Ec - mh * mh, 1.0))
+
+
+def sa_phase(ta, tb, mh):
+    """int_ta^tb e_4 dtau on one side of the crossing (|ta|, |tb| >= 1): the WKB phase G, the
+    leading dressed-energy term mh^2/(8E^5) in closed form (tail_T), and the rest,
+    e_4 - E - mh^2/(8E^5) = O(E^-9), by 4-point Gauss-Legendre in u = 1/|tau|."""
+    base = wkb_G(tb, mh) - wkb_G(ta, mh)
+    lead = mh * mh * 0.125 * abs(tail_T(ta, mh) - tail_T(tb, mh))
+    u1, u2 = 1.0 / abs(ta), 1.0 / abs(tb)
+    ulo, uhi = min(u1, u2), max(u1, u2)
+    half, mid = 0.5 * (uhi - ulo), 0.5 * (uhi + ulo)
+    acc = 0.0
+    for x, w in zip(GL4_X, GL4_W):
+        u = mid + half * x
+        _, ev, gv = sa_levels(1.0 / u, 1.0, mh, 4)
+        E = ev[0]
+        d1 = gv[1] * gv[1] / (E + ev[1])
+        d2 = gv[2] * gv[2] / (ev[1] + ev[2])
+        d3 = gv[3] * gv[3] / (ev[2] + ev[3])
+        E5 = E * E * E * E * E
+        f = d3 + d2 - mh * mh * d1 / (8.0 * E5 * (E + ev[1]))
+        acc += w * f / (u * u)
+    return base + lead + half * acc
+
+
+def sa_follow(p, mh, s, ta, tb):
+    """Superadiabatic following from tau = ta to tb (ta < tb, same side of the crossing): p to
+    the frame of order SA_LEVELS at ta, the frame amplitudes pick up exp(-+ i int e dtau), back
+    to the diabatic basis at tb.  Error ~ the first neglected rotation angle at the inner end."""
+    tf = max(abs(ta), abs(tb))
+    Ef2 = tf * tf + mh * mh
+    Ef12 = (Ef2 * Ef2) * (Ef2 * Ef2) * (Ef2 * Ef2)
+    far6 = SA_FAR_C * max(mh, SA_M_FLOOR) <= 0.1 * SA_TOL * Ef12 * math.sqrt(Ef2)
+    ca, _, _ = sa_levels(s * ta, s, mh, SA_FAR_LEVELS if far6 and abs(ta) == tf else SA_LEVELS)
+    cb, _, _ = sa_levels(s * tb, s, mh, SA_FAR_LEVELS if far6 and abs(tb) == tf else SA_LEVELS)
+    a, b = sa_to_frame(p, ca)
+    ph = sa_phase(ta, tb, mh)
+    a *= complex(math.cos(ph), -math.sin(ph))
+    b *= complex(math.cos(ph), math.sin(ph))
+    return sa_from_frame(a, b, cb)
 
 
 def wkb_G(x, m):
@@ -147,12 +232,17 @@ def propagate(m_mix, dprime, xi, v_w, K, S, hybrid=True):
             sgn = -sgn
             continue
         cell_right = right
-        if hybrid:   # Magnus only on the cell's core; dressed following outside it
-            W = core_halfwidth(m_mix[c], ac, v_w, K)
-            cl, cr = max(left, xi[c] - W), min(right, xi[c] + W)
-            if left < cl:
-                p = far_segment(p, m_mix[c], ac, slope, xi[c], left, cl, v_w)
-            left, right = cl, cr
+        if hybrid:   # Magnus only on the cell's core; superadiabatic following outside it
+            sa = math.sqrt(ac * v_w)
+            mh = m_mix[c] / sa
+            tc = sa_core_tau(mh)
+            sgn_s = 1.0 if slope > 0 else -1.0
+            tl, tr = sa * (left - xi[c]) / v_w, sa * (right - xi[c]) / v_w
+            if tl < -tc:
+                p = sa_follow(p, mh, sgn_s, tl, -tc)
+                left = xi[c] - tc * v_w / sa
+            if tr > tc:
+                right = xi[c] + tc * v_w / sa
         Phi = (wkb_G(ac * (right - xi[c]), m_mix[c]) - wkb_G(ac * (left - xi[c]), m_mix[c])) / (ac * v_w)
         Sc = int(max(S, math.ceil(Phi * STEPS_PER_RADIAN))) if hybrid else S
         h = (right - left) / Sc
@@ -184,8 +274,8 @@ def propagate(m_mix, dprime, xi, v_w, K, S, hybrid=True):
             sx, sy, sz = sc * nx, sc * ny, sc * nz
             U = np.array([[cs - 1j * sz, -sy - 1j * sx], [sy - 1j * sx, cs + 1j * sz]])
             p = U @ p
-        if right < cell_right:
-            p = far_segment(p, m_mix[c], ac, slope, xi[c], right, cell_right, v_w)
+        if hybrid and right < cell_right:
+            p = sa_follow(p, mh, sgn_s, tc, sa * (cell_right - xi[c]) / v_w)
         left = right = cell_right
         sgn = -sgn
     slope = -sgn * abs(dprime[-1])

@@ -3,10 +3,11 @@ sequence) against the EXACT finite-window solution of the same model: cell-by-ce
 (parabolic-cylinder) functions, tests/weber_ref.py, committed as tests/golden/golden_weber.json
 by tests/golden/make_golden_weber.py.
 
-Stated accuracy of the kernel's scheme (eighth-order Magnus, >= 3 steps per radian of
-adiabatic phase) at K = 20 LZ lengths: the C5 default S = 1000 steps per cell: |P - P_exact|
-<= 2e-9 (measured 7.2e-10); S = 16000: <= 1e-11 (measured 9e-14), exact adiabatic cells
-(delta > 16, dressed basis) included.  The Magnus error falls as S^-8.  The exact
+Stated accuracy of the kernel's scheme (eighth-order Magnus on each cell's core at 6 steps per
+radian of adiabatic phase, superadiabatic following of order 10 outside it, exact adiabatic cells
+for delta > 16) at K = 20 LZ lengths: |P - P_exact| <= 1e-10 at the C5 default S = 64 (measured
+3.4e-11) and step-converged (S = 16000; measured 4.2e-11, the following error).  The Magnus
+error falls as S^-8 (brute force, whole cells).  The exact
 single-crossing P at K = 20 (dressed window edges) is within 5e-9 relative of eq.(9)
 (measured 1.95e-9).
 """
@@ -52,10 +53,11 @@ def test_brute_force_magnus_matches_exact(i):
 
 def test_hybrid_at_production_settings():
     from conftest import pkg
-    assert pkg("sweep").CrossingSpec().steps == 1000          # the C5 default
-    for c in GOLD["cases"]:
-        P = propagate(c["m"], c["d"], c["x"], V_W, c["K"], 1000)
-        assert abs(P - c["P"]) <= 2e-9, (c, P)
+    assert pkg("sweep").CrossingSpec().steps == 64          # the C5 default
+    for S in (64, 16000):
+        for c in GOLD["cases"]:
+            P = propagate(c["m"], c["d"], c["x"], V_W, c["K"], S)
+            assert abs(P - c["P"]) <= 1e-10, (S, c, P)
 
 
 def test_hybrid_step_converged_with_adiabatic_cell():

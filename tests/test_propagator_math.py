@@ -21,10 +21,13 @@ def test_single_crossing_reduces_to_closed_form(m, dp):
 def test_window_convergence_order():
     m, dp, v_w = 0.1, 1.0, 0.3
     P_cf = 1.0 - math.exp(-2.0 * math.pi * m * m / (2 * v_w * dp))
-    e20 = abs(propagate([m], [dp], [0.0], v_w, 20, 2000) - P_cf)
-    e40 = abs(propagate([m], [dp], [0.0], v_w, 40, 16000) - P_cf)
+    # whole-window Magnus (hybrid=False), so only the window's own error is left
+    e20 = abs(propagate([m], [dp], [0.0], v_w, 20, 2000, hybrid=False) - P_cf)
+    e40 = abs(propagate([m], [dp], [0.0], v_w, 40, 16000, hybrid=False) - P_cf)
     assert e40 < e20 / 50                              # dressed-edge window error ~ K^-7 (measured 125x)
     assert e20 < 5e-9 * P_cf
+    # the kernel's scheme (core + superadiabatic following) leaves the window error as it is
+    assert abs(propagate([m], [dp], [0.0], v_w, 20, 1) - P_cf) < 5e-9 * P_cf
 
 
 def test_norm_and_trivial_limits():

@@ -1,0 +1,90 @@
+"""The LZ propagator's superadiabatic-frame code (csrc/lzq_superadiabatic.h, __host__ __device__:
+the same source the GPU kernels inline), built for the host (tests/sa_host.cpp) and checked on
+the CPU against the numpy restatement tests/lz_ref.py: the frame rotation U = V_0 .. V_9, the
+phase-node levels, the follow phase, the core width and the composed follow matrix
+U(tb) diag(e^{-i ph}, e^{i ph}) U(ta)^+ against lz_ref.sa_follow applied to a state.  No GPU."""
+import ctypes
+import math
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import lz_ref as R
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "sa_host.cpp")
+HDR = os.path.join(HERE, "..", "baryon-and-dark-matter-densities-from-bounce--sourced-distributed-landau--zener-transport_amd",
+                   "csrc", "lzq_superadiabatic.h")
+LIB = os.path.join(HERE, "_build", "libsa_host.so")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    newest = max(os.path.getmtime(SRC), os.path.getmtime(HDR))
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < newest:
+        os.makedirs(os.path.dirname(LIB), exist_ok=True)
+        subprocess.run(["/opt/rocm/bin/hipcc", "-x", "hip", "-O2", "-std=c++17", "-fPIC", "-shared",
+                        "--offload-arch=gfx950", "-o", LIB + ".tmp", SRC], check=True)
+        os.replace(LIB + ".tmp", LIB)
+    L = ctypes.CDLL(LIB)
+    d, P = ctypes.c_double, ctypes.POINTER(ctypes.c_double)
+    L.sa_frame_host.argtypes = [d, d, d, P]
+    L.sa_levels4_host.argtypes = [d, d, d, P, P]
+    L.sa_phase_host.argtypes = [d, d, d]
+    L.sa_phase_host.restype = d
+    L.sa_core_tau_host.argtypes = [d]
+    L.sa_core_tau_host.restype = d
+    L.sa_follow_matrix_host.argtypes = [d, d, d, d, P]
+    return L
+
+
+def _buf(n):
+    return (ctypes.c_double * n)()
+
+
+def _su2(v):
+    a, b = complex(v[0], v[1]), complex(v[2], v[3])
+    return np.array([[a, -b.conjugate()], [b, a.conjugate()]])
+
+
+CASES = [(mh, sg, t) for mh in (1e-4, 0.05, 0.7, 1.4, 3.0, 5.6) for sg in (1.0, -1.0) for t in (-30.0, -6.5, 4.2, 9.0)]
+
+
+def test_levels_count(lib):
+    assert lib.sa_levels_count() == R.SA_LEVELS
+
+
+@pytest.mark.parametrize("mh,sg,t", CASES)
+def test_frame_rotation(lib, mh, sg, t):
+    out = _buf(4)
+    lib.sa_frame_host(sg * t, sg, mh, out)
+    cs, _, _ = R.sa_levels(sg * t, sg, mh, R.SA_LEVELS)
+    U = R.sa_from_frame(1.0, 0.0, cs), R.sa_from_frame(0.0, 1.0, cs)
+    U = np.array(U).T
+    assert np.max(np.abs(_su2(out) - U)) < 1e-14
+
+
+def test_levels_and_phase(lib):
+    for mh in (1e-4, 0.3, 1.4, 5.6):
+        for D in (1.2, 4.0, 17.0):
+            ev, gv = _buf(4), _buf(4)
+            lib.sa_levels4_host(D, 1.0, mh, ev, gv)
+            _, e, g = R.sa_levels(D, 1.0, mh, 4)
+            assert np.allclose(list(ev), e, rtol=1e-14, atol=0) and np.allclose(list(gv), g, rtol=1e-12, atol=1e-300)
+        for ta, tb in ((-40.0, -5.0), (3.5, 12.0), (6.0, 400.0)):
+            assert abs(lib.sa_phase_host(ta, tb, mh) - R.sa_phase(ta, tb, mh)) <= 1e-13 * abs(R.sa_phase(ta, tb, mh))
+        assert abs(lib.sa_core_tau_host(mh) - R.sa_core_tau(mh)) <= 1e-14 * R.sa_core_tau(mh)
+
+
+@pytest.mark.parametrize("mh,sg", [(0.05, 1.0), (1.4, -1.0), (5.6, 1.0)])
+def test_follow_matrix_vs_restatement(lib, mh, sg):
+    rng = np.random.default_rng(3)
+    for ta, tb in ((-25.0, -R.sa_core_tau(mh)), (R.sa_core_tau(mh), 31.0)):
+        out = _buf(4)
+        lib.sa_follow_matrix_host(mh, sg, ta, tb, out)
+        M = _su2(out)
+        for _ in range(3):
+            p = rng.normal(size=2) + 1j * rng.normal(size=2)
+            assert np.max(np.abs(M @ p - R.sa_follow(p, mh, sg, ta, tb))) < 1e-12 * np.linalg.norm(p)

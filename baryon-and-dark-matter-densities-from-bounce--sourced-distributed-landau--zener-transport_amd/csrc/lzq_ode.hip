@@ -367,24 +367,53 @@ __device__ __forceinline__ RadauH radau_h(const Radau& R, double h) {
 // systems M = I - hA diag(jf) of the Riccati equation: well conditioned like the Y_B system
 // (jf = -2 lam Z <= 0 near the solution), so the cofactor form loses nothing against pivoted
 // elimination (tests/test_gpu_ode.py: oracle at 1e-11, stiff cases at 1e-10 of converged).
-__device__ __forceinline__ void solve3_adj(const double (&M)[3][3], double (&b)[3]) {
-  const double a00 = M[1][1] * M[2][2] - M[1][2] * M[2][1];
-  const double a01 = M[0][2] * M[2][1] - M[0][1] * M[2][2];
-  const double a02 = M[0][1] * M[1][2] - M[0][2] * M[1][1];
-  const double a10 = M[1][2] * M[2][0] - M[1][0] * M[2][2];
-  const double a11 = M[0][0] * M[2][2] - M[0][2] * M[2][0];
-  const double a12 = M[0][2] * M[1][0] - M[0][0] * M[1][2];
-  const double a20 = M[1][0] * M[2][1] - M[1][1] * M[2][0];
-  const double a21 = M[0][1] * M[2][0] - M[0][0] * M[2][1];
-  const double a22 = M[0][0] * M[1][1] - M[0][1] * M[1][0];
-  const double id = 1.0 / (M[0][0] * a00 + M[0][1] * a10 + M[0][2] * a20);
-  const double x0 = (a00 * b[0] + a01 * b[1] + a02 * b[2]) * id;
-  const double x1 = (a10 * b[0] + a11 * b[1] + a12 * b[2]) * id;
-  const double x2 = (a20 * b[0] + a21 * b[1] + a22 * b[2]) * id;
-  b[0] = x0;
-  b[1] = x1;
-  b[2] = x2;
+#ifndef LZQ_ODE_ADJFMA
+#define LZQ_ODE_ADJFMA 1  // the adjugate, determinant and products as explicit fmas (the file builds with -ffp-contract=off)
+#endif
+struct Adj3 {
+  double a[3][3];  // adjugate of M
+  double id;       // 1 / det M
+};
+__device__ __forceinline__ Adj3 adj3(const double (&M)[3][3]) {
+  Adj3 r;
+  if (LZQ_ODE_ADJFMA) {
+#define FMA __builtin_fma
+    r.a[0][0] = FMA(M[1][1], M[2][2], -(M[1][2] * M[2][1]));
+    r.a[0][1] = FMA(M[0][2], M[2][1], -(M[0][1] * M[2][2]));
+    r.a[0][2] = FMA(M[0][1], M[1][2], -(M[0][2] * M[1][1]));
+    r.a[1][0] = FMA(M[1][2], M[2][0], -(M[1][0] * M[2][2]));
+    r.a[1][1] = FMA(M[0][0], M[2][2], -(M[0][2] * M[2][0]));
+    r.a[1][2] = FMA(M[0][2], M[1][0], -(M[0][0] * M[1][2]));
+    r.a[2][0] = FMA(M[1][0], M[2][1], -(M[1][1] * M[2][0]));
+    r.a[2][1] = FMA(M[0][1], M[2][0], -(M[0][0] * M[2][1]));
+    r.a[2][2] = FMA(M[0][0], M[1][1], -(M[0][1] * M[1][0]));
+    r.id = 1.0 / FMA(M[0][0], r.a[0][0], FMA(M[0][1], r.a[1][0], M[0][2] * r.a[2][0]));
+#undef FMA
+  } else {
+    r.a[0][0] = M[1][1] * M[2][2] - M[1][2] * M[2][1];
+    r.a[0][1] = M[0][2] * M[2][1] - M[0][1] * M[2][2];
+    r.a[0][2] = M[0][1] * M[1][2] - M[0][2] * M[1][1];
+    r.a[1][0] = M[1][2] * M[2][0] - M[1][0] * M[2][2];
+    r.a[1][1] = M[0][0] * M[2][2] - M[0][2] * M[2][0];
+    r.a[1][2] = M[0][2] * M[1][0] - M[0][0] * M[1][2];
+    r.a[2][0] = M[1][0] * M[2][1] - M[1][1] * M[2][0];
+    r.a[2][1] = M[0][1] * M[2][0] - M[0][0] * M[2][1];
+    r.a[2][2] = M[0][0] * M[1][1] - M[0][1] * M[1][0];
+    r.id = 1.0 / (M[0][0] * r.a[0][0] + M[0][1] * r.a[1][0] + M[0][2] * r.a[2][0]);
+  }
+  return r;
 }
+__device__ __forceinline__ void adj3_apply(const Adj3& A, double (&b)[3]) {
+  double x[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    x[i] = LZQ_ODE_ADJFMA ? __builtin_fma(A.a[i][0], b[0], __builtin_fma(A.a[i][1], b[1], A.a[i][2] * b[2])) * A.id
+                          : (A.a[i][0] * b[0] + A.a[i][1] * b[1] + A.a[i][2] * b[2]) * A.id;
+  b[0] = x[0];
+  b[1] = x[1];
+  b[2] = x[2];
+}
+__device__ __forceinline__ void solve3_adj(const double (&M)[3][3], double (&b)[3]) { adj3_apply(adj3(M), b); }
 
 // Y_B's Radau step as an affine map (LZQ_ODE_YBREC): the stage system (I + hA diag(beta)) Z =
 // Y_B 1 + hA alpha, alpha_j = P flux a_j, gives by Cramer's rule Z_3 = c Y_B + P flux d with

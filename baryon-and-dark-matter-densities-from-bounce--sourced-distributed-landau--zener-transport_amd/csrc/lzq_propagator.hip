@@ -230,18 +230,20 @@ __global__ __launch_bounds__(kPropBlock) void lz_scatter_kernel(const int32_t* _
   if (p < n) order[base[b] + r] = (int32_t)p;
 }
 
-constexpr int kFollowDoubles = 10;  // per (point, cell): two SU(2) matrices, the core's edges
+constexpr int kFollowDoubles = 11;  // per (point, cell): two SU(2) matrices, the core's edges, its steps
 
-// Follow matrices of every (point, cell): one thread each.  Cell c's edges are computed with the
-// propagate kernel's own expressions (so bit-identical), and for a delta <= 16 cell whose core is
-// narrower than the cell the superadiabatic transfer matrices of the stretch left of the core and
-// right of it go to follow[(p n_cross + c) 10 + 0..3 / 4..7] as (a.re, a.im, b.re, b.im), and
-// the core's edges cl, cr to + 8, 9 (so the propagate kernel never evaluates the core width).
+// Per-cell data of every (point, cell), one thread each: everything about a cell that does not
+// depend on the state.  Cell c's edges are computed with the propagate kernel's own expressions
+// (so bit-identical).  A delta <= 16 cell gets the superadiabatic transfer matrices of the
+// stretches left and right of its core at follow[(p n_cross + c) 11 + 0..3 / 4..7] as (a.re,
+// a.im, b.re, b.im), the core's edges cl, cr at + 8, 9 and its Magnus step count at + 10 (NaN for
+// an absurd count).  A delta > 16 cell gets its closed-form adiabatic transfer matrix (dressed
+// bases, WKB + Stokes phase, header) at + 0..3 and -1 at + 10.
 __global__ __launch_bounds__(kPropBlock) void lz_follow_kernel(const double* __restrict__ m_mix,
                                                                const double* __restrict__ dprime,
                                                                const double* __restrict__ xi,
                                                                const double* __restrict__ vw, int64_t n,
-                                                               int32_t n_cross, double v_w0, double K,
+                                                               int32_t n_cross, double v_w0, double K, int32_t S,
                                                                double* __restrict__ follow) {
   const int64_t t = (int64_t)blockIdx.x * kPropBlock + threadIdx.x;
   if (t >= n * n_cross) return;
@@ -267,15 +269,36 @@ __global__ __launch_bounds__(kPropBlock) void lz_follow_kernel(const double* __r
     right = xcc + K * lz_length(mc, ac, v_w);
   }
   const double delta = mc * mc / (2.0 * v_w * ac);
-  if (delta > kDeltaAdiabatic) return;
+  const double sg = (c % 2 == 0) ? 1.0 : -1.0;
+  double* out = follow + (p * n_cross + c) * kFollowDoubles;
+  if (delta > kDeltaAdiabatic) {
+    // exact adiabatic following through the cell, in its dressed basis (header): the WKB phase
+    // int E dt (closed form) + the Stokes phase - the dressed-energy tails beyond the edges
+    const double slope = sg * ac;
+    const double Phi = (wkb_G(ac * (right - xcc), mc) - wkb_G(ac * (left - xcc), mc)) / (ac * v_w);
+    const double DL = slope * (left - xcc), DR = slope * (right - xcc);
+    const double ddot = slope * v_w;
+    const Dressed L = dressed_basis(DL, ddot, mc), R = dressed_basis(DR, ddot, mc);
+    const double id = 1.0 / delta, id2 = id * id;
+    const double phiS = id * (1.0 / 12.0 + id2 * (1.0 / 360.0 + id2 * (1.0 / 1260.0 + id2 * (1.0 / 1680.0))));
+    const double tails = 0.125 * mc * mc * ac * v_w * (tail_T(DL, mc) + tail_T(DR, mc));
+    // [R.p R.q] diag(e^{-i ph}, e^{i ph}) [L.p L.q]^+; a dressed basis is an SU(2) element with
+    // first column |+~>
+    const SU2 m = su2_mul({R.p0, R.p1}, su2_phase_adj(Phi + phiS - tails, {L.p0, L.p1}));
+    out[0] = m.a.re, out[1] = m.a.im, out[2] = m.b.re, out[3] = m.b.im;
+    out[10] = -1.0;
+    return;
+  }
   const double W = core_halfwidth(mc, ac, v_w);  // INFINITY without cores (LZQ_PROP_CORE=0)
   const double cl = fmax(left, xcc - W), cr = fmin(right, xcc + W);
+  const double Phic = (wkb_G(ac * (cr - xcc), mc) - wkb_G(ac * (cl - xcc), mc)) / (ac * v_w);
+  const double Sd = fmax((double)S, ceil(Phic * kStepsPerRadian));
   const double inv_vw = 1.0 / v_w;
-  const double sa = sqrt(ac * v_w), mh = mc / sa, sg = (c % 2 == 0) ? 1.0 : -1.0;
+  const double sa = sqrt(ac * v_w), mh = mc / sa;
   const double tau_c = W * sa * inv_vw;
-  double* out = follow + (p * n_cross + c) * kFollowDoubles;
   out[8] = cl;
   out[9] = cr;
+  out[10] = Sd <= kMaxCellSteps ? Sd : __builtin_nan("");  // non-finite or absurd input: P = NaN
   if (left < cl) {
     const SU2 m = sa_follow_matrix(mh, sg, sa * (left - xcc) * inv_vw, -tau_c);
     out[0] = m.a.re, out[1] = m.a.im, out[2] = m.b.re, out[3] = m.b.im;
@@ -327,37 +350,18 @@ __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_k
       right = xcc + K * lz_length(mc, ac, v_w);
     }
     const double slope = sgn * ac;
-    const double delta = mc * mc / (2.0 * v_w * ac);
-    if (delta > kDeltaAdiabatic) {
-      // adiabatic phase of the cell, int E dt (closed form)
-      const double Phi = (wkb_G(ac * (right - xcc), mc) - wkb_G(ac * (left - xcc), mc)) / (ac * v_w);
-      // exact adiabatic following through the cell, in its dressed basis (see header)
-      const double DL = slope * (left - xcc), DR = slope * (right - xcc);
-      const double ddot = slope * v_w;
-      const Dressed L = dressed_basis(DL, ddot, mc), R = dressed_basis(DR, ddot, mc);
-      const Cplx bp = inner(L.p0, L.p1, p0, p1), bm = inner(L.q0, L.q1, p0, p1);
-      const double id = 1.0 / delta, id2 = id * id;
-      const double phiS = id * (1.0 / 12.0 + id2 * (1.0 / 360.0 + id2 * (1.0 / 1260.0 + id2 * (1.0 / 1680.0))));
-      const double tails = 0.125 * mc * mc * ac * v_w * (tail_T(DL, mc) + tail_T(DR, mc));
-      double sn, cs;
-      sincos(Phi + phiS - tails, &sn, &cs);
-      const Cplx bp2 = {bp.re * cs + bp.im * sn, bp.im * cs - bp.re * sn};  // * e^{-i a}
-      const Cplx bm2 = {bm.re * cs - bm.im * sn, bm.im * cs + bm.re * sn};  // * e^{+i a}
-      p0 = {bp2.re * R.p0.re - bp2.im * R.p0.im + bm2.re * R.q0.re - bm2.im * R.q0.im,
-            bp2.re * R.p0.im + bp2.im * R.p0.re + bm2.re * R.q0.im + bm2.im * R.q0.re};
-      p1 = {bp2.re * R.p1.re - bp2.im * R.p1.im + bm2.re * R.q1.re - bm2.im * R.q1.im,
-            bp2.re * R.p1.im + bp2.im * R.p1.re + bm2.re * R.q1.im + bm2.im * R.q1.re};
+    const double* Mc = follow + (p * n_cross + c) * kFollowDoubles;  // lz_follow_kernel's cell data
+    const double Sd = Mc[10];
+    if (Sd < 0.0) {
+      su2_apply_mat({{Mc[0], Mc[1]}, {Mc[2], Mc[3]}}, p0, p1);  // closed-form adiabatic cell
     } else {
       // Magnus on the core, superadiabatic following on either side of it
-      const double* Mc = follow + (p * n_cross + c) * kFollowDoubles;  // lz_follow_kernel's output
       const double cl = Mc[8], cr = Mc[9];
-      if (left < cl) su2_apply_mat({{Mc[0], Mc[1]}, {Mc[2], Mc[3]}}, p0, p1);
-      const double Phic = (wkb_G(ac * (cr - xcc), mc) - wkb_G(ac * (cl - xcc), mc)) / (ac * v_w);
-      const double Sd = fmax((double)S, ceil(Phic * kStepsPerRadian));
       if (!(Sd <= kMaxCellSteps)) {  // non-finite or absurd input (bounded for any valid one)
         P_out[p] = __builtin_nan("");
         return;
       }
+      if (left < cl) su2_apply_mat({{Mc[0], Mc[1]}, {Mc[2], Mc[3]}}, p0, p1);
       const int Sc = (int)Sd;
       const double h = (cr - cl) / (double)Sc;  // step in xi
       const double dt = h * inv_vw;                  // step in t
@@ -374,8 +378,7 @@ __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_k
       // oracle-matching kernels, so contraction is spelled out): 63 VALU per step where the
       // separate products and sums took 84.
 #define FMA __builtin_fma
-#pragma unroll LZQ_PROP_UNROLL
-      for (int i = 0; i < Sc; ++i) {
+      auto step = [&](int i) {
         const double xm = FMA((double)i + 0.5, h, cl);
         const double D = slope * (xm - xcc);
         const double D2 = D * D, E2 = D2 + m2;
@@ -385,7 +388,15 @@ __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_k
         double cs, sc;  // cos|n| and sin|n|/|n|, both functions of |n|^2
         cos_sinc(FMA(nx, nx, FMA(ny, ny, nz * nz)), cs, sc);
         su2_apply(cs, sc * nx, sc * ny, sc * nz, p0, p1);
+      };
+      // unrolled by hand: the polynomial's inline asm (fma3) is convergent, which rules out
+      // the compiler's runtime unrolling
+      int i = 0;
+      for (; i + LZQ_PROP_UNROLL <= Sc; i += LZQ_PROP_UNROLL) {
+#pragma unroll
+        for (int u = 0; u < LZQ_PROP_UNROLL; ++u) step(i + u);
       }
+      for (; i < Sc; ++i) step(i);
 #undef FMA
       if (cr < right) su2_apply_mat({{Mc[4], Mc[5]}, {Mc[6], Mc[7]}}, p0, p1);
     }
@@ -409,8 +420,8 @@ __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_k
 int lzq_set_error(int code, const char* msg);
 
 namespace {
-// Follow data take 80 B per (point, cell): batches are run in slices of at most this many
-// (point, cell) pairs (640 MiB).
+// Cell data take 88 B per (point, cell): batches are run in slices of at most this many
+// (point, cell) pairs (704 MiB).
 constexpr int64_t kFollowMaxPairs = (int64_t)1 << 23;
 
 int propagate_slice(const double* d_m_mix, const double* d_dprime, const double* d_xi, const double* d_v_w, int64_t n,
@@ -433,7 +444,7 @@ int propagate_slice(const double* d_m_mix, const double* d_dprime, const double*
   {
     const int64_t nf = (n * n_cross + lzq::kPropBlock - 1) / lzq::kPropBlock;
     hipLaunchKernelGGL(lzq::lz_follow_kernel, dim3((unsigned)nf), dim3(lzq::kPropBlock), 0, st, d_m_mix, d_dprime,
-                       d_xi, d_v_w, n, n_cross, v_w, window_lz, follow);
+                       d_xi, d_v_w, n, n_cross, v_w, window_lz, steps_per_crossing, follow);
   }
   if (sort) {
     int32_t* iw = (int32_t*)(ws + follow_bytes);

@@ -182,6 +182,25 @@ __host__ __device__ __forceinline__ void sa_levels_linear(double Dh, double sg, 
   }
 }
 
+// P U^+ with P = diag(e^{-i ph}, e^{i ph}) = (a = e^{-i ph}, b = 0) and U^+ = (conj(a), -b)
+__host__ __device__ __forceinline__ SU2 su2_phase_adj(double ph, const SU2& u) {
+  const double sn = sin(ph), cs = cos(ph);
+  SU2 m;
+  m.a = {cs * u.a.re - sn * u.a.im, -sn * u.a.re - cs * u.a.im};   // e^{-i ph} conj(a)
+  m.b = {sn * u.b.im - cs * u.b.re, -(cs * u.b.im + sn * u.b.re)};  // e^{+i ph} (-b)
+  return m;
+}
+
+// u r: a = a1 a2 - conj(b1) b2, b = b1 a2 + conj(a1) b2
+__host__ __device__ __forceinline__ SU2 su2_mul(const SU2& u, const SU2& r) {
+  SU2 m;
+  m.a = {u.a.re * r.a.re - u.a.im * r.a.im - (u.b.re * r.b.re + u.b.im * r.b.im),
+         u.a.re * r.a.im + u.a.im * r.a.re - (u.b.re * r.b.im - u.b.im * r.b.re)};
+  m.b = {u.b.re * r.a.re - u.b.im * r.a.im + u.a.re * r.b.re + u.a.im * r.b.im,
+         u.b.re * r.a.im + u.b.im * r.a.re + u.a.re * r.b.im - u.a.im * r.b.re};
+  return m;
+}
+
 // psi <- U^+ psi (diabatic -> frame), U = [[a, -conj(b)], [b, conj(a)]]
 __host__ __device__ __forceinline__ void su2_apply_adj(const SU2& u, Cplx& p0, Cplx& p1) {
   // U^+ = [[conj(a), conj(b)], [-b, a]]
@@ -283,20 +302,10 @@ __host__ __device__ __forceinline__ SU2 sa_follow_matrix(double mh, double sg, d
       sa_levels_linear<kSAFarLevels, true, false>(sg * tau, sg, mh, u, nullptr, nullptr);
     else
       sa_levels_linear<kSALevels, true, false>(sg * tau, sg, mh, u, nullptr, nullptr);
-    if (end == 0) {
-      // m = P U(ta)^+ with P = diag(e^{-i ph}, e^{i ph}) = (a = e^{-i ph}, b = 0), U^+ = (conj(a), -b)
-      const double ph = sa_phase(ta, tb, mh);
-      const double sn = sin(ph), cs = cos(ph);
-      m.a = {cs * u.a.re - sn * u.a.im, -sn * u.a.re - cs * u.a.im};   // e^{-i ph} conj(a)
-      m.b = {sn * u.b.im - cs * u.b.re, -(cs * u.b.im + sn * u.b.re)};  // e^{+i ph} (-b)
-    } else {
-      // m = U(tb) m: a = a1 a2 - conj(b1) b2, b = b1 a2 + conj(a1) b2
-      const SU2 r = m;
-      m.a = {u.a.re * r.a.re - u.a.im * r.a.im - (u.b.re * r.b.re + u.b.im * r.b.im),
-             u.a.re * r.a.im + u.a.im * r.a.re - (u.b.re * r.b.im - u.b.im * r.b.re)};
-      m.b = {u.b.re * r.a.re - u.b.im * r.a.im + u.a.re * r.b.re + u.a.im * r.b.im,
-             u.b.re * r.a.im + u.b.im * r.a.re + u.a.re * r.b.im - u.a.im * r.b.re};
-    }
+    if (end == 0)
+      m = su2_phase_adj(sa_phase(ta, tb, mh), u);  // P U(ta)^+
+    else
+      m = su2_mul(u, m);                           // U(tb) P U(ta)^+
   }
   return m;
 }

@@ -292,20 +292,22 @@ int lzq_ode_rhs(const lzq_point* pt, const lzq_ode_params* ode, double T_lo, dou
  * with slope (-1)^c |Delta'_c| through crossing c at xi_c (continuous at the turning points
  * between crossings).  The outer half-windows are window_lz LZ lengths of the first/last
  * crossing (L = sqrt(v_w/|Delta'|) max(1, sqrt(delta))).  Each cell with delta <= 16 takes
- * max(steps_per_crossing, 3 x the adiabatic phase in radians of its core) eighth-order Magnus
- * steps (exact SU(2) exponentials) on a core around its crossing (2 window_lz LZ lengths for
- * delta <= 1, else out to adiabaticity 1e-5) and follows the state in the second-order dressed
- * basis outside it, so the step count is bounded for any crossing spacing; cells with
- * delta > 16 are propagated in closed form.  Arrays are [n][n_cross] row-major device buffers
- * (xi increasing per point).  0 < window_lz <= 200, 0 < steps_per_crossing <= 1e6 (else
- * LZQ_EINVAL); a point whose inputs are not finite gets P = NaN.  Output d_P[n]: conversion probability
- * 1 - |<chi-like dressed state | psi_end>|^2, psi_start = chi-like dressed state, where
- * "dressed" = second-order superadiabatic state of the outer cell (the adiabatic state carried
- * in from / out to infinity).  For one crossing this is 1 - exp(-2 pi delta) (fpy:183-184,
- * PAPER eq.(9)) to <= 1e-8 relative at window_lz = 20, steps_per_crossing = 1000; DESIGN.md §6
- * states the window / step tolerances.  Batches of n >= 16384 points run longest-first (points
- * binned by their step count, a counting sort in three small kernels, scratch of 8n bytes from
- * hipMallocAsync on `stream`, freed stream-ordered); d_P is bit-identical to index order.
+ * max(steps_per_crossing, 6 x the adiabatic phase in radians of its core) eighth-order Magnus
+ * steps (exact SU(2) exponentials) on a core around its crossing (~5-7 LZ lengths: out to where
+ * the first neglected angle of the order-10 superadiabatic frame falls to 1e-11) and follows the
+ * state in that frame outside it, so the step count is bounded for any crossing spacing; cells
+ * with delta > 16 are propagated in closed form.  Arrays are [n][n_cross] row-major device
+ * buffers (xi increasing per point).  0 < window_lz <= 200, 0 < steps_per_crossing <= 1e6 (else
+ * LZQ_EINVAL); a point whose inputs are not finite gets P = NaN.  Output d_P[n]: conversion
+ * probability 1 - |<chi-like dressed state | psi_end>|^2, psi_start = chi-like dressed state,
+ * where "dressed" = second-order superadiabatic state of the outer cell (the adiabatic state
+ * carried in from / out to infinity).  For one crossing this is 1 - exp(-2 pi delta)
+ * (fpy:183-184, PAPER eq.(9)) to <= 1e-8 relative at window_lz = 20 for any steps_per_crossing;
+ * DESIGN.md §6 states the window / step tolerances (the C5 default is steps_per_crossing = 64).
+ * Scratch from hipMallocAsync on `stream`, freed stream-ordered: 80 bytes per (point, crossing)
+ * for the follow matrices (lz_follow_kernel; batches beyond 2^23 pairs run in slices) and, for
+ * n >= 16384 points, 8n bytes for the longest-first launch order (points binned by their step
+ * count, a counting sort in three small kernels); d_P is bit-identical to index order.
  * n < 2^31. */
 int lzq_lz_propagate(const double* d_m_mix, const double* d_dprime, const double* d_xi,
                      int64_t n, int32_t n_cross, double v_w, double window_lz,

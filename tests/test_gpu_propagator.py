@@ -148,3 +148,24 @@ def test_multicrossing_sweep_over_wall_speed(gpu_engine):
     m, dp, xi, vw = spec.crossing_arrays(0, n, gpu_engine.device)
     P = gpu_engine.lz_propagate(m, dp, xi, vw, spec.crossings.window_lz, spec.crossings.steps)
     assert torch.equal(out[:, 5], P) and bool(torch.isfinite(out).all())
+
+
+def test_follow_slices_bit_identical(gpu_engine):
+    """Batches of more than 2^23 (point, cell) pairs run in slices (the follow matrices take 80 B
+    per pair, lzq_propagator.hip kFollowMaxPairs): 270,000 points x 32 crossings (two slices) give
+    the same P bit for bit as the points run in separate smaller calls."""
+    import dataclasses
+
+    import torch
+    sw = pkg("sweep")
+    spec = sw.builtin_specs()["C5"]
+    spec = dataclasses.replace(spec, crossings=dataclasses.replace(spec.crossings, n_cross=32))
+    n = 270_000
+    m, dp, xi, v_w = spec.crossing_arrays((spec.total - n) // 2, n, gpu_engine.device)
+    args = (float(v_w[0]), spec.crossings.window_lz, spec.crossings.steps)
+    whole = gpu_engine.lz_propagate(m, dp, xi, *args)
+    cut = 100_000
+    parts = torch.cat([gpu_engine.lz_propagate(m[:cut], dp[:cut], xi[:cut], *args),
+                       gpu_engine.lz_propagate(m[cut:], dp[cut:], xi[cut:], *args)])
+    assert bool(torch.isfinite(whole).all())
+    assert torch.equal(whole, parts)

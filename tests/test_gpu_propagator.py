@@ -169,3 +169,24 @@ def test_follow_slices_bit_identical(gpu_engine):
                        gpu_engine.lz_propagate(m[cut:], dp[cut:], xi[cut:], *args)])
     assert bool(torch.isfinite(whole).all())
     assert torch.equal(whole, parts)
+
+
+def test_edge_couplings_match_restatement(gpu_engine):
+    """Cells at the edges of the superadiabatic scheme, kernel vs the numpy restatement: zero
+    coupling (P = 0: the frames are the diabatic basis), couplings below the core-width floor
+    (m_hat < 0.05), delta just below / above the closed-form threshold 16, a mix of adiabatic and
+    Magnus cells in one point, and very unequal slopes (long follow stretches)."""
+    cases = [([0.0], [1.0], [0.0]),
+             ([0.0, 0.0], [1.0, 2.0], [0.0, 30.0]),
+             ([1e-4], [5.0], [0.0]),
+             ([1e-3, 2e-4], [10.0, 0.5], [0.0, 25.0]),
+             ([math.sqrt(2 * 16 * V_W * 0.5) * 0.999], [0.5], [0.0]),      # delta = 15.97
+             ([math.sqrt(2 * 16 * V_W * 0.5) * 1.001], [0.5], [0.0]),      # delta = 16.03 (closed form)
+             ([0.3, 2.5, 0.05], [0.25, 0.5, 1.0], [0.0, 120.0, 400.0]),    # Magnus, adiabatic, Magnus
+             ([0.1, 0.1], [0.01, 5.0], [0.0, 400.0])]
+    for m, d, x in cases:
+        got = gpu_engine.lz_propagate([m], [d], [x], V_W, 20.0, 64).cpu().numpy()[0]
+        ref = propagate(m, d, x, V_W, 20.0, 64)
+        assert abs(got - ref) <= 1e-11 * max(abs(ref), 1e-3), (m, d, x, got, ref)
+        if max(m) == 0.0:
+            assert abs(got) < 1e-15, got

@@ -131,9 +131,9 @@ __device__ __forceinline__ double core_halfwidth(double m, double a, double v_w)
 }
 
 // ---------------------------------------------------------------------------------------
-// Launch order.  A lane's cost is its Magnus step count, which delta sets per cell: ~1000-1200
-// steps for delta <= 1, up to ~6e4 in core-limited cells with 1 < delta <= 16, none in the
-// closed-form cells (C5 slice: median 9.9e3 per point, 99th percentile 5.3e4).  In index order
+// Launch order.  A lane's cost is its Magnus step count, which its cells' cores set (C5 slice:
+// ~170-280 steps per delta <= 16 cell, none in the closed-form cells; round 2's 40-LZ-length
+// cores took 1000-1200 for delta <= 1 and up to ~6e4 for 1 < delta <= 16).  In index order
 // a wave waits on its slowest lane in every cell and the launch ends on a few long waves.  So,
 // for large batches, the points are first binned by their step count (the kernel's own cell
 // geometry, point_steps), the bins laid out longest-first (a counting sort: LDS histograms, one
@@ -299,14 +299,11 @@ __global__ __launch_bounds__(kPropBlock) void lz_follow_kernel(const double* __r
   out[8] = cl;
   out[9] = cr;
   out[10] = Sd <= kMaxCellSteps ? Sd : __builtin_nan("");  // non-finite or absurd input: P = NaN
-  if (left < cl) {
-    const SU2 m = sa_follow_matrix(mh, sg, sa * (left - xcc) * inv_vw, -tau_c);
-    out[0] = m.a.re, out[1] = m.a.im, out[2] = m.b.re, out[3] = m.b.im;
-  }
-  if (cr < right) {
-    const SU2 m = sa_follow_matrix(mh, sg, tau_c, sa * (right - xcc) * inv_vw);
-    out[4] = m.a.re, out[5] = m.a.im, out[6] = m.b.re, out[7] = m.b.im;
-  }
+  SU2 ML, MR;
+  const bool has_left = left < cl, has_right = cr < right;
+  sa_cell_follow(mh, sg, sa * (left - xcc) * inv_vw, sa * (right - xcc) * inv_vw, tau_c, has_left, has_right, ML, MR);
+  if (has_left) out[0] = ML.a.re, out[1] = ML.a.im, out[2] = ML.b.re, out[3] = ML.b.im;
+  if (has_right) out[4] = MR.a.re, out[5] = MR.a.im, out[6] = MR.b.re, out[7] = MR.b.im;
 }
 
 __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_kernel(const double* __restrict__ m_mix,

@@ -310,4 +310,41 @@ __host__ __device__ __forceinline__ SU2 sa_follow_matrix(double mh, double sg, d
   return m;
 }
 
+// The frame at -tau from the frame at +tau: U(-tau) = -sz U(tau) sx exactly (H(-tau) = sx H(tau) sx
+// and the jets' derivatives flip sign with tau; checked bit for bit on the restatement), i.e.
+// (a, b) -> (conj(b), conj(a)).
+__host__ __device__ __forceinline__ SU2 sa_reflect(const SU2& u) {
+  SU2 r;
+  r.a = {u.b.re, -u.b.im};
+  r.b = {u.a.re, -u.a.im};
+  return r;
+}
+
+// Both follow stretches of one cell with core [-tau_c, tau_c]: ML from tl (< -tau_c) to -tau_c
+// when has_left, MR from tau_c to tr (> tau_c) when has_right; the same matrices as
+// sa_follow_matrix, with the core-edge frame computed once (the one at -tau_c by sa_reflect).
+// One frame per loop iteration (register pressure, see sa_follow_matrix).
+__host__ __device__ __forceinline__ void sa_cell_follow(double mh, double sg, double tl, double tr, double tau_c,
+                                                        bool has_left, bool has_right, SU2& ML, SU2& MR) {
+  SU2 uc;
+#pragma nounroll
+  for (int job = 0; job < 3; ++job) {
+    if ((job == 0 && !(has_left || has_right)) || (job == 1 && !has_left) || (job == 2 && !has_right)) continue;
+    const double tau = job == 0 ? tau_c : (job == 1 ? tl : tr);
+    const double Ef2 = tau * tau + mh * mh, Ef4 = Ef2 * Ef2, Ef12 = Ef4 * Ef4 * Ef4;
+    const bool far6 = job > 0 && kSAFarC * fmax(mh, kSAMFloor) <= 0.1 * kSATol * Ef12 * sqrt(Ef2);
+    SU2 u;
+    if (far6)
+      sa_levels_linear<kSAFarLevels, true, false>(sg * tau, sg, mh, u, nullptr, nullptr);
+    else
+      sa_levels_linear<kSALevels, true, false>(sg * tau, sg, mh, u, nullptr, nullptr);
+    if (job == 0)
+      uc = u;
+    else if (job == 1)
+      ML = su2_mul(sa_reflect(uc), su2_phase_adj(sa_phase(tl, -tau_c, mh), u));  // U(-tau_c) P U(tl)^+
+    else
+      MR = su2_mul(u, su2_phase_adj(sa_phase(tau_c, tr, mh), uc));               // U(tr) P U(tau_c)^+
+  }
+}
+
 }  // namespace lzq

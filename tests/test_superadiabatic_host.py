@@ -37,6 +37,7 @@ def lib():
     L.sa_core_tau_host.argtypes = [d]
     L.sa_core_tau_host.restype = d
     L.sa_follow_matrix_host.argtypes = [d, d, d, d, P]
+    L.sa_cell_follow_host.argtypes = [d, d, d, d, d, ctypes.c_int, ctypes.c_int, P]
     return L
 
 
@@ -88,3 +89,19 @@ def test_follow_matrix_vs_restatement(lib, mh, sg):
         for _ in range(3):
             p = rng.normal(size=2) + 1j * rng.normal(size=2)
             assert np.max(np.abs(M @ p - R.sa_follow(p, mh, sg, ta, tb))) < 1e-12 * np.linalg.norm(p)
+
+
+@pytest.mark.parametrize("mh,sg", [(1e-3, -1.0), (0.05, 1.0), (1.4, -1.0), (5.6, 1.0)])
+def test_cell_follow_vs_restatement(lib, mh, sg):
+    """sa_cell_follow (the core-edge frame computed once, the one at -tau_c by the reflection
+    U(-tau) = -sz U(tau) sx) against lz_ref.sa_follow on both stretches of a cell."""
+    rng = np.random.default_rng(4)
+    tc = R.sa_core_tau(mh)
+    for tl, tr in ((-25.0, 31.0), (-tc - 0.5, 400.0)):
+        out = _buf(8)
+        lib.sa_cell_follow_host(mh, sg, tl, tr, tc, 1, 1, out)
+        ML, MR = _su2(out[0:4]), _su2(out[4:8])
+        for _ in range(3):
+            p = rng.normal(size=2) + 1j * rng.normal(size=2)
+            assert np.max(np.abs(ML @ p - R.sa_follow(p, mh, sg, tl, -tc))) < 1e-12 * np.linalg.norm(p)
+            assert np.max(np.abs(MR @ p - R.sa_follow(p, mh, sg, tc, tr))) < 1e-12 * np.linalg.norm(p)

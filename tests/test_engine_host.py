@@ -63,3 +63,25 @@ def test_wave_order_no_repeats_or_small():
     order = _order(p, o)
     d = o["deplete_DM_from_source"][order]
     assert int(np.count_nonzero(d[1:] != d[:-1])) == 1
+
+
+def test_ode_step_counts_device_equals_host():
+    """Engine.ode sizes its continuation launches from ode_step_counts_device (torch ops on the
+    device records); it must give the numpy ode_step_counts' values exactly, edge cases included
+    (T_min = 0, m = 0, NaN T_p).  Run here on CPU tensors."""
+    import numpy as np
+    import torch
+    eng, nat = pkg("engine"), pkg("_native")
+    rng = np.random.default_rng(1)
+    n = 20000
+    pts = np.zeros(n, dtype=nat.POINT_DTYPE)
+    pts["m_chi_GeV"] = 10 ** rng.uniform(-1, 3.5, n)
+    pts["T_p_GeV"] = 10 ** rng.uniform(0, 3, n)
+    pts["T_max_over_Tp"] = rng.uniform(0.5, 3, n)
+    pts["T_min_over_Tp"] = rng.uniform(0, 1.5, n)
+    pts["T_min_over_Tp"][:10] = 0.0
+    pts["m_chi_GeV"][10:20] = 0.0
+    pts["T_p_GeV"][20:25] = np.nan
+    host = eng.ode_step_counts(pts)
+    dev = eng.ode_step_counts_device(torch.from_numpy(pts.view(np.uint8).copy()), n).numpy()
+    assert np.array_equal(host, dev, equal_nan=True)

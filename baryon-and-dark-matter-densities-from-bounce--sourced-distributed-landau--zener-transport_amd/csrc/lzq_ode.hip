@@ -465,6 +465,9 @@ __constant__ double kRadauPred[3][4] = {
 #ifndef LZQ_ODE_PEEL
 #define LZQ_ODE_PEEL 1  // the first two Newton iterations (and the Y_B solve) as one straight-line block
 #endif
+#ifndef LZQ_ODE_LINFAST
+#define LZQ_ODE_LINFAST 1  // one fma per regular step on linear cooperative waves (sigma_v = 0, no depletion)
+#endif
 #ifndef LZQ_ODE_YBREC
 #define LZQ_ODE_YBREC 1  // Y_B by its affine step map (yb_rec), shared per cooperative segment
 #endif
@@ -805,6 +808,12 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
       const uint64_t gb = __builtin_bit_cast(uint64_t, o.gamma_w);
       rec_shared = __all(gb == __builtin_bit_cast(uint64_t, __shfl(o.gamma_w, 0, G)));
     }
+    // Linear waves (LZQ_ODE_LINFAST): with sigma_v = 0 on every lane, Y_chi's Radau step is
+    // radau_step's linear branch, Z_3 = Y - sum_j hA_3j S_j with S_j = P flux a_j when depleting and
+    // +0 otherwise (then Y_chi is unchanged, exactly), and Y_B's is the segment's shared map: a
+    // regular step is one fma on the LDS row (+ three with depletion) -- the general path's
+    // operations on the same values, hence the same bits.  Split steps take the general path.
+    const bool lin_fast = LZQ_ODE_LINFAST && LZQ_ODE_YBREC && !kChiOnly && rec_shared && __all(o.sigmav == 0.0);
     const int64_t block = coop ? G : N;
     for (int64_t kb = k_begin; kb < k_stop; kb += block) {
       const int64_t kend = kb + block < k_stop ? kb + block : k_stop;
@@ -833,6 +842,20 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
       for (int64_t k = kb; k < kend && !done; ++k) {
         const double xk = x0 + (double)k * h;
         const bool split = xk < xb && xb <= xk + h;  // the last stage (x = xk + h) would see the other branch
+        if (lin_fast && !split) {
+          const int row = seg + (int)(k - kb);
+          const YbRec r = s_rec[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][row];
+          YB = __builtin_fma(r.c, YB, o.Pf * r.d);
+          Yp = Ychi;  // the general path's Ystart
+          if (o.deplete) {
+            double acc = Ychi;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) acc = __builtin_fma(-hA.a[2][j], o.Pf * s_base[wv][row][j].a, acc);
+            Ychi = acc;
+          }
+          have = true;  // its !split
+          continue;
+        }
         const double xa = split ? nextafter(xb, -INFINITY) : xk + h;
         double YB_prev = YB;
         bool ok = true;

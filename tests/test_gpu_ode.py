@@ -268,6 +268,44 @@ def test_ode_quadrature_sweep_shared_and_deterministic(gpu_engine):
     assert np.max(np.abs(q.cpu().numpy()[:, :2] - rr[:, :2]) / np.abs(rr[:, :2])) < 1e-11
 
 
+def test_ode_linear_waves_bit_identical(gpu_engine):
+    """The linear-wave fast path (lzq_ode.hip LZQ_ODE_LINFAST: sigma_v = 0 on every lane of a
+    cooperative wave with one Gamma_wash per segment; a regular step is Y_B's shared affine map,
+    plus Y_chi's three depletion fmas) gives the per-lane mode's bits: wash-out with and without
+    depletion, thermal and non-thermal starts, a window crossing T = m/3 (split steps take the
+    general path), a group whose Gamma_wash varies within every wave (no fast path), and the same
+    batch as continuation launches of 2^12 steps."""
+    rng = np.random.default_rng(47)
+    cfgs = []
+    for m_chi, gw in ((0.95, 0.5), (300.0, 2.0), (3.0, None)):   # 300 GeV: T = m/3 = T_p is inside the window
+        for _ in range(128):
+            c = full_cfg(BASE_CFG)
+            c.update(NARROW, m_chi_GeV=m_chi, P_chi_to_B=float(rng.uniform(0.05, 1.0)),
+                     incident_flux_scale=float(10 ** rng.uniform(-10, -8)),
+                     Gamma_wash_over_H=float(gw if gw is not None else rng.choice([0.5, 1.0, 2.0])),
+                     sigma_v_chi_GeV_m2=0.0, deplete_DM_from_source=bool(rng.uniform() < 0.4),
+                     regime=str(rng.choice(["thermal", "nonthermal"])))
+            cfgs.append(c)
+    p, o = recs(cfgs)
+    a, sa = gpu_engine.ode(p, o, share_tables=True)
+    prev = gpu_engine.tune_ode_coop(False)
+    try:
+        b, sb = gpu_engine.ode(p, o, share_tables=True)
+    finally:
+        gpu_engine.tune_ode_coop(prev)
+    assert bool((sa == 0).all()) and torch_equal(sa, sb) and torch_equal(a, b)
+    prev = gpu_engine.tune_ode_launch_steps(12)
+    try:
+        c, sc = gpu_engine.ode(p, o, share_tables=True)
+    finally:
+        gpu_engine.tune_ode_launch_steps(prev)
+    assert torch_equal(sa, sc) and torch_equal(a, c)
+    ref, sr = O.ode_batch(cfgs[::16], nthreads=16)
+    for row, rr in zip(a.cpu().numpy()[::16], ref):
+        for v, w in zip(row[:5], rr[:5]):
+            assert rel_err(v, w) < 1e-10, (v, w)
+
+
 def test_ode_cooperative_waves_bit_identical(gpu_engine):
     """ode_integrate_kernel's cooperative mode (a full wavefront whose points differ only in P,
     flux, sigma_v, Gamma_wash, deplete and the initial state computes each step's stage

@@ -105,3 +105,26 @@ def test_cell_follow_vs_restatement(lib, mh, sg):
             p = rng.normal(size=2) + 1j * rng.normal(size=2)
             assert np.max(np.abs(ML @ p - R.sa_follow(p, mh, sg, tl, -tc))) < 1e-12 * np.linalg.norm(p)
             assert np.max(np.abs(MR @ p - R.sa_follow(p, mh, sg, tc, tr))) < 1e-12 * np.linalg.norm(p)
+
+
+def test_cell_follow_randomized(lib):
+    """Randomized cells (seeded): couplings m_hat 1e-6 .. 5.6, stretch ends out to |tau| = 1e5,
+    both slope signs.  The host build of the frame code against the numpy restatement, and the
+    follow matrices unitary to rounding (|a|^2 + |b|^2 = 1)."""
+    rng = np.random.default_rng(11)
+    for _ in range(60):
+        mh = float(10 ** rng.uniform(-6, math.log10(5.6)))
+        sg = float(rng.choice([-1.0, 1.0]))
+        tc = R.sa_core_tau(mh)
+        tl = -tc - float(10 ** rng.uniform(-2, 5))
+        tr = tc + float(10 ** rng.uniform(-2, 5))
+        out = _buf(8)
+        lib.sa_cell_follow_host(mh, sg, tl, tr, tc, 1, 1, out)
+        ML, MR = _su2(out[0:4]), _su2(out[4:8])
+        for M in (ML, MR):
+            assert abs(abs(M[0, 0]) ** 2 + abs(M[1, 0]) ** 2 - 1.0) < 1e-14
+        p = rng.normal(size=2) + 1j * rng.normal(size=2)
+        # the phase grows like tau^2 / 2: compare at the restatement's own rounding of it
+        tol = 1e-12 * max(1.0, 0.5 * max(tl * tl, tr * tr) * 1e-3)
+        assert np.max(np.abs(ML @ p - R.sa_follow(p, mh, sg, tl, -tc))) < tol * np.linalg.norm(p), (mh, sg, tl)
+        assert np.max(np.abs(MR @ p - R.sa_follow(p, mh, sg, tc, tr))) < tol * np.linalg.norm(p), (mh, sg, tr)

@@ -281,35 +281,6 @@ __host__ __device__ __forceinline__ double sa_phase(double ta, double tb, double
   return base + lead + half * acc;
 }
 
-// Transfer matrix of superadiabatic following from tau = ta to tb (ta < tb, one side of the
-// crossing; the cell's own units, tests/lz_ref.py sa_follow): U(tb) diag(e^{-i ph}, e^{+i ph})
-// U(ta)^+ with U the frame rotation of order kSALevels and ph = int e dtau.  Error ~ |theta_10| at
-// the inner end.  It does not depend on the state, so lz_follow_kernel computes it ahead of the
-// propagation (the jets need ~90 VGPRs of their own).
-__host__ __device__ __forceinline__ SU2 sa_follow_matrix(double mh, double sg, double ta, double tb) {
-  // the outer end (|tau| larger) may use the order-6 frame: the two frames differ there by the
-  // neglected angles theta_6 .. theta_9 ~ kSAFarC mh / E^13
-  const double tf = fmax(fabs(ta), fabs(tb));
-  const double Ef2 = tf * tf + mh * mh, Ef4 = Ef2 * Ef2, Ef12 = Ef4 * Ef4 * Ef4;
-  const bool far6 = kSAFarC * fmax(mh, kSAMFloor) <= 0.1 * kSATol * Ef12 * sqrt(Ef2);
-  SU2 m;
-  // one frame evaluation per iteration: two side by side (they are independent) need ~250 VGPRs
-#pragma nounroll
-  for (int end = 0; end < 2; ++end) {
-    const double tau = end ? tb : ta;
-    SU2 u;
-    if (far6 && fabs(tau) == tf)
-      sa_levels_linear<kSAFarLevels, true, false>(sg * tau, sg, mh, u, nullptr, nullptr);
-    else
-      sa_levels_linear<kSALevels, true, false>(sg * tau, sg, mh, u, nullptr, nullptr);
-    if (end == 0)
-      m = su2_phase_adj(sa_phase(ta, tb, mh), u);  // P U(ta)^+
-    else
-      m = su2_mul(u, m);                           // U(tb) P U(ta)^+
-  }
-  return m;
-}
-
 // The frame at -tau from the frame at +tau: U(-tau) = -sz U(tau) sx exactly (H(-tau) = sx H(tau) sx
 // and the jets' derivatives flip sign with tau; checked bit for bit on the restatement), i.e.
 // (a, b) -> (conj(b), conj(a)).
@@ -320,10 +291,14 @@ __host__ __device__ __forceinline__ SU2 sa_reflect(const SU2& u) {
   return r;
 }
 
-// Both follow stretches of one cell with core [-tau_c, tau_c]: ML from tl (< -tau_c) to -tau_c
-// when has_left, MR from tau_c to tr (> tau_c) when has_right; the same matrices as
-// sa_follow_matrix, with the core-edge frame computed once (the one at -tau_c by sa_reflect).
-// One frame per loop iteration (register pressure, see sa_follow_matrix).
+// Transfer matrices of superadiabatic following (tests/lz_ref.py sa_follow) on both sides of a
+// cell's core [-tau_c, tau_c]: ML from tl (< -tau_c) to -tau_c when has_left, MR from tau_c to
+// tr (> tau_c) when has_right, each U(tb) diag(e^{-i ph}, e^{i ph}) U(ta)^+ with U the frame
+// rotation of order kSALevels (kSAFarLevels at an outer end where that is enough) and
+// ph = int e dtau (sa_phase).  Error ~ |theta_10| at the inner end.  They do not depend on the
+// state, so lz_follow_kernel computes them ahead of the propagation.  The core-edge frame is
+// computed once (the one at -tau_c by sa_reflect), and one frame per loop iteration: two side by
+// side (they are independent) would need ~250 VGPRs.
 __host__ __device__ __forceinline__ void sa_cell_follow(double mh, double sg, double tl, double tr, double tau_c,
                                                         bool has_left, bool has_right, SU2& ML, SU2& MR) {
   SU2 uc;

@@ -24,11 +24,6 @@ double sa_phase_host(double ta, double tb, double mh) { return sa_phase(ta, tb, 
 
 double sa_core_tau_host(double mh) { return sa_core_tau(mh); }
 
-void sa_follow_matrix_host(double mh, double sg, double ta, double tb, double* out) {
-  const SU2 m = sa_follow_matrix(mh, sg, ta, tb);
-  out[0] = m.a.re, out[1] = m.a.im, out[2] = m.b.re, out[3] = m.b.im;
-}
-
 // both stretches of a cell: out = ML (4), MR (4)
 void sa_cell_follow_host(double mh, double sg, double tl, double tr, double tau_c, int has_left, int has_right,
                          double* out) {

@@ -1,7 +1,7 @@
 """The LZ propagator's superadiabatic-frame code (csrc/lzq_superadiabatic.h, __host__ __device__:
 the same source the GPU kernels inline), built for the host (tests/sa_host.cpp) and checked on
 the CPU against the numpy restatement tests/lz_ref.py: the frame rotation U = V_0 .. V_9, the
-phase-node levels, the follow phase, the core width and the composed follow matrix
+phase-node levels, the follow phase, the core width and a cell's two composed follow matrices
 U(tb) diag(e^{-i ph}, e^{i ph}) U(ta)^+ against lz_ref.sa_follow applied to a state.  No GPU."""
 import ctypes
 import math
@@ -36,7 +36,6 @@ def lib():
     L.sa_phase_host.restype = d
     L.sa_core_tau_host.argtypes = [d]
     L.sa_core_tau_host.restype = d
-    L.sa_follow_matrix_host.argtypes = [d, d, d, d, P]
     L.sa_cell_follow_host.argtypes = [d, d, d, d, d, ctypes.c_int, ctypes.c_int, P]
     return L
 
@@ -77,18 +76,6 @@ def test_levels_and_phase(lib):
         for ta, tb in ((-40.0, -5.0), (3.5, 12.0), (6.0, 400.0)):
             assert abs(lib.sa_phase_host(ta, tb, mh) - R.sa_phase(ta, tb, mh)) <= 1e-13 * abs(R.sa_phase(ta, tb, mh))
         assert abs(lib.sa_core_tau_host(mh) - R.sa_core_tau(mh)) <= 1e-14 * R.sa_core_tau(mh)
-
-
-@pytest.mark.parametrize("mh,sg", [(0.05, 1.0), (1.4, -1.0), (5.6, 1.0)])
-def test_follow_matrix_vs_restatement(lib, mh, sg):
-    rng = np.random.default_rng(3)
-    for ta, tb in ((-25.0, -R.sa_core_tau(mh)), (R.sa_core_tau(mh), 31.0)):
-        out = _buf(4)
-        lib.sa_follow_matrix_host(mh, sg, ta, tb, out)
-        M = _su2(out)
-        for _ in range(3):
-            p = rng.normal(size=2) + 1j * rng.normal(size=2)
-            assert np.max(np.abs(M @ p - R.sa_follow(p, mh, sg, ta, tb))) < 1e-12 * np.linalg.norm(p)
 
 
 @pytest.mark.parametrize("mh,sg", [(1e-3, -1.0), (0.05, 1.0), (1.4, -1.0), (5.6, 1.0)])

@@ -90,8 +90,7 @@ class Engine:
 
     def points_to_device(self, recs: np.ndarray) -> torch.Tensor:
         """lzq_point records (numpy POINT_DTYPE array) -> device byte tensor."""
-        recs = np.ascontiguousarray(recs, dtype=_native.POINT_DTYPE)
-        return torch.from_numpy(recs.view(np.uint8).copy()).to(self.device)
+        return _to_device_bytes(np.ascontiguousarray(recs, dtype=_native.POINT_DTYPE), self.device)
 
     # -- fpy:158-165 -----------------------------------------------------------------------
     def aov(self, cfg, ys) -> torch.Tensor:
@@ -253,7 +252,7 @@ class Engine:
             raise ValueError("points and ode_params must have the same length")
         n = pts.size
         d_pts_all = self.points_to_device(pts)
-        d_ode_all = torch.from_numpy(ods.view(np.uint8).copy()).to(self.device)
+        d_ode_all = _to_device_bytes(ods, self.device)
         if max_steps is None:
             need = ode_step_counts_device(d_pts_all, n)   # same values as ode_step_counts, on the device
             need = need[torch.isfinite(need)]
@@ -404,7 +403,7 @@ class Engine:
         rec = np.zeros(cols[0].size, dtype=_native.PROFILE_POINT_DTYPE)
         for name, c in zip(("y_B", "y_chi", "lambda_tr_eff", "v_w", "shape"), cols):
             rec[name] = c.reshape(-1)
-        return torch.from_numpy(rec.view(np.uint8).copy()).to(self.device)
+        return _to_device_bytes(rec, self.device)
 
     def profile_crossings(self, shapes: "ProfileShapes", points: torch.Tensor, max_cross: int = 8) -> dict:
         """eqs.(5)-(8) per point: {'xi', 'dprime', 'm_mix', 'delta_lz'} [n, max_cross] and
@@ -446,6 +445,17 @@ def ode_step_counts(pts: np.ndarray) -> np.ndarray:
         dx = np.abs(x1 - x0)
         ms = np.minimum(np.minimum(dx / 20000.0, x_p / 1000.0), 5e-4)
         return np.where(ms > 0.0, np.ceil(dx / ms), np.nan)
+
+
+def _to_device_bytes(arr: np.ndarray, device) -> torch.Tensor:
+    """A contiguous record array as a device byte tensor.  The host bytes go to the device
+    straight from the caller's buffer (a host-side copy first cost ~5-40 ms per 35 MB of records,
+    mostly page faults on the fresh allocation); read-only buffers are copied, since torch only
+    wraps writable ones."""
+    b = np.ascontiguousarray(arr).view(np.uint8)
+    if not b.flags.writeable:
+        b = b.copy()
+    return torch.from_numpy(b).to(device)
 
 
 def ode_step_counts_device(d_pts: torch.Tensor, n: int) -> torch.Tensor:

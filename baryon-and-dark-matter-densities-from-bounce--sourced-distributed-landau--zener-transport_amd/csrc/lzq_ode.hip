@@ -688,7 +688,10 @@ struct OdeState {
 };
 constexpr int32_t kOdeInProgress = 64;
 
-template <bool kChiOnly>
+// kLin: the variant for linear cooperative waves (see lin_wave below); every launch runs both
+// variants, each stepping only its own wavefronts (the other variant's return at once), so the
+// linear waves' tight loop does not share a register allocation with the Riccati Newton path.
+template <bool kChiOnly, bool kLin = false>
 __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_kernel(const lzq_point* __restrict__ pts,
                                                                   const lzq_ode_params* __restrict__ ode, int64_t n,
                                                                   const int32_t* __restrict__ tidx,
@@ -744,6 +747,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
     }
   }
   bool finished = true;  // this launch ends the point (continuation: else its state is saved)
+  if (kLin && st != LZQ_ODE_OK) return;  // the general variant reports it (its wave is not linear)
   if (st == LZQ_ODE_OK) {
     const int64_t N = (int64_t)steps;
     const int64_t k_begin = cont ? k_lo : 0;
@@ -757,7 +761,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
     // the same with its own T; tests/golden/golden_ode_stiff.json).
     const double xb = branch_x(o, x0, x1);
     const RadauH hA = radau_h(R, h);
-    const bool riccati = LZQ_ODE_PREDICT && o.sigmav != 0.0;
+    const bool riccati = LZQ_ODE_PREDICT && !kLin && o.sigmav != 0.0;  // kLin: sigma_v = 0 on every lane
     double Zs[3] = {Ychi, Ychi, Ychi}, Yp = Ychi;  // previous step's start and stages (predictor)
     bool have = false, done = false;
     if (!first) {  // continue from the previous launch's state
@@ -813,7 +817,34 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
     // +0 otherwise (then Y_chi is unchanged, exactly), and Y_B's is the segment's shared map: a
     // regular step is one fma on the LDS row (+ three with depletion) -- the general path's
     // operations on the same values, hence the same bits.  Split steps take the general path.
-    const bool lin_fast = LZQ_ODE_LINFAST && LZQ_ODE_YBREC && !kChiOnly && rec_shared && __all(o.sigmav == 0.0);
+    const bool lin_wave = LZQ_ODE_LINFAST && LZQ_ODE_YBREC && !kChiOnly && rec_shared && __all(o.sigmav == 0.0);
+    if (lin_wave != kLin) return;  // the other variant of this launch steps this wavefront
+    const bool lin_fast = kLin;
+    // Linear waves: the first split step (xk < xb <= xk + h), found once.  x_k's rounding error is
+    // far below h, so it can only be within a step of (xb - x0)/h: the predicate is checked on a
+    // few candidates around it (a lane whose x scale would make the rounding comparable to h
+    // takes every step on the general path, k_split = -1).  The general path takes that step and
+    // the next (a rounding may split two consecutive steps); the rest run as the tight loop.
+    int64_t k_split = INT64_MAX;
+    bool prev_split = false;
+    if (lin_fast && xb < INFINITY) {  // branch_x: +inf when no step splits
+      const double kf = floor((xb - x0) / h);
+      const double margin = 2.0 + floor(8.0 * __DBL_EPSILON__ * (fabs(x0) + fabs(x1)) / h);
+      if (!(margin <= 16.0)) {
+        k_split = -1;
+      } else if (kf - margin < (double)N && kf + margin >= 0.0) {  // false for NaN
+        const int64_t c0 = kf - margin > 0.0 ? (int64_t)(kf - margin) : 0;
+        const int64_t c1 = kf + margin < (double)(N - 1) ? (int64_t)(kf + margin) : N - 1;
+#pragma nounroll
+        for (int64_t c = c0; c <= c1; ++c) {
+          const double xc = x0 + (double)c * h;
+          if (xc < xb && xb <= xc + h) {
+            k_split = c;
+            break;
+          }
+        }
+      }
+    }
     const int64_t block = coop ? G : N;
     for (int64_t kb = k_begin; kb < k_stop; kb += block) {
       const int64_t kend = kb + block < k_stop ? kb + block : k_stop;
@@ -839,23 +870,33 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
-      for (int64_t k = kb; k < kend && !done; ++k) {
+      int64_t k = kb;
+      while (k < kend && !done) {
+        if (lin_fast && !prev_split) {
+          // the block's regular steps up to its next split step in one tight loop
+          const int64_t kg = k_split < 0 ? k : (k_split >= k && k_split < kend ? k_split : kend);
+          const int nf = (int)(kg - k);
+          if (nf > 0) {
+            const int r0 = seg + (int)(k - kb);
+            const YbRec* rr = &s_rec[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][r0];
+            if (o.deplete) {
+              for (int jj = 0; jj < nf; ++jj) {
+                YB = __builtin_fma(rr[jj].c, YB, o.Pf * rr[jj].d);
+                double acc = Ychi;
+#pragma unroll
+                for (int j = 0; j < 3; ++j) acc = __builtin_fma(-hA.a[2][j], o.Pf * s_base[wv][r0 + jj][j].a, acc);
+                Ychi = acc;
+              }
+            } else {
+#pragma unroll 4
+              for (int jj = 0; jj < nf; ++jj) YB = __builtin_fma(rr[jj].c, YB, o.Pf * rr[jj].d);
+            }
+            k = kg;
+          }
+          if (k >= kend) break;
+        }
         const double xk = x0 + (double)k * h;
         const bool split = xk < xb && xb <= xk + h;  // the last stage (x = xk + h) would see the other branch
-        if (lin_fast && !split) {
-          const int row = seg + (int)(k - kb);
-          const YbRec r = s_rec[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][row];
-          YB = __builtin_fma(r.c, YB, o.Pf * r.d);
-          Yp = Ychi;  // the general path's Ystart
-          if (o.deplete) {
-            double acc = Ychi;
-#pragma unroll
-            for (int j = 0; j < 3; ++j) acc = __builtin_fma(-hA.a[2][j], o.Pf * s_base[wv][row][j].a, acc);
-            Ychi = acc;
-          }
-          have = true;  // its !split
-          continue;
-        }
         const double xa = split ? nextafter(xb, -INFINITY) : xk + h;
         double YB_prev = YB;
         bool ok = true;
@@ -913,12 +954,14 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
           }
         }
         have = !split;   // the predictor needs a full regular step behind it
+        prev_split = split;
         Yp = Ystart;
         if (!ok) {
           YB = YB_prev;  // report the state at the start of the failed step, like sol.y[:, -1] (fpy:408-410)
           st = LZQ_ODE_NEWTON;
           done = true;
         }
+        ++k;
       }
       if (coop) __builtin_amdgcn_wave_barrier();  // every lane is done with this block's table
     }
@@ -927,12 +970,13 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
       OdeState sv;
       sv.Ychi = Ychi;
       sv.YB = YB;
-      sv.Yp = Yp;
-      sv.Z[0] = Zs[0];
-      sv.Z[1] = Zs[1];
-      sv.Z[2] = Zs[2];
+      // the predictor's data (only sigma_v != 0 lanes read it; kLin's have sigma_v = 0)
+      sv.Yp = kLin ? Ychi : Yp;
+      sv.Z[0] = kLin ? Ychi : Zs[0];
+      sv.Z[1] = kLin ? Ychi : Zs[1];
+      sv.Z[2] = kLin ? Ychi : Zs[2];
       sv.status = kOdeInProgress;
-      sv.have = have ? 1 : 0;
+      sv.have = !kLin && have ? 1 : 0;
       state[i] = sv;
     }
   }
@@ -1172,21 +1216,26 @@ int launch_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int
              (long long)max_steps, lzq::g_ode_launch_log2);
     return lzq_set_error(LZQ_EINVAL, buf);
   }
-  if (launches == 1) {
+  // both variants (ode_integrate_kernel's kLin) per launch; none for kChiOnly (no linear waves)
+  auto launch = [&](int64_t k_lo, int64_t k_cnt, lzq::OdeState* st) {
     hipLaunchKernelGGL(lzq::ode_integrate_kernel<kChiOnly>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, s,
-                       d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, lzq::g_ode_coop, (int64_t)0,
-                       (int64_t)0, (lzq::OdeState*)nullptr);
-    return hip_check(hipGetLastError(), fn);
-  }
+                       d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, lzq::g_ode_coop, k_lo, k_cnt,
+                       st);
+    int rc = hip_check(hipGetLastError(), fn);
+    if constexpr (LZQ_ODE_LINFAST && LZQ_ODE_YBREC && !kChiOnly) {
+      if (rc != LZQ_OK) return rc;
+      hipLaunchKernelGGL((lzq::ode_integrate_kernel<kChiOnly, true>), dim3((unsigned)ode_blocks(n)),
+                         dim3(lzq::kOdeBlock), 0, s, d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status,
+                         lzq::g_ode_coop, k_lo, k_cnt, st);
+      rc = hip_check(hipGetLastError(), fn);
+    }
+    return rc;
+  };
+  if (launches == 1) return launch(0, 0, nullptr);
   lzq::OdeState* st = nullptr;
   int rc = hip_check(hipMallocAsync((void**)&st, sizeof(lzq::OdeState) * (size_t)n, s), fn);
   if (rc) return rc;
-  for (int64_t j = 0; j < launches && rc == LZQ_OK; ++j) {
-    hipLaunchKernelGGL(lzq::ode_integrate_kernel<kChiOnly>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, s,
-                       d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, lzq::g_ode_coop, j * per, per,
-                       st);
-    rc = hip_check(hipGetLastError(), fn);
-  }
+  for (int64_t j = 0; j < launches && rc == LZQ_OK; ++j) rc = launch(j * per, per, st);
   const int rf = hip_check(hipFreeAsync(st, s), fn);
   return rc ? rc : rf;
 }

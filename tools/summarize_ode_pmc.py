@@ -15,21 +15,31 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CONFIGS = [("narrow_wash", 262144, 20000), ("stiff_thermal", 262144, 25385), ("full_window_wash", 16384, 999800)]
 
 
-def main_cases(src: str, tag: str) -> None:
+def main_cases(src: str, tag: str, fname: str = "ode_pmc.json") -> None:
     """tools/gpu_ode_pmc3.sh layout: tools/ode_pmc_run.py's three cases, one 262,144-point
     ode_integrate_kernel<false> dispatch each (after a 64-point warm-up), in CASES order."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from ode_pmc_run import CASES, N
+    # ode_integrate_kernel<false> (one dispatch per case), or since the linear-wave variant
+    # <false, false> + <false, true> (two per case, each stepping its own wavefronts: summed)
+    per = 1
     rows = list(csv.DictReader(open(os.path.join(src, "pmc", "run_counter_collection.csv"))))
     disp = defaultdict(dict)
     for r in rows:
-        if "ode_integrate_kernel<false>" in r["Kernel_Name"]:
+        if "ode_integrate_kernel<false" in r["Kernel_Name"]:
+            per = 2 if "ode_integrate_kernel<false, " in r["Kernel_Name"] else per
             d = disp[int(r["Dispatch_Id"])]
             d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-    big_p = [disp[k] for k in sorted(disp) if disp[k].get("SQ_WAVES", 0) >= N // 64]
+    big = [disp[k] for k in sorted(disp) if disp[k].get("SQ_WAVES", 0) >= N // 64]
+    big_p = []
+    for j in range(0, len(big), per):
+        c = {k: sum(d.get(k, 0.0) for d in big[j:j + per]) for k in big[j]}
+        c["SQ_WAVES"] = big[j]["SQ_WAVES"]  # every variant launches every wavefront
+        big_p.append(c)
     tr = [r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv")))
-          if "ode_integrate_kernel<false>" in r["Kernel_Name"] and int(r["Grid_Size_X"]) >= N]
-    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9 for r in tr]
+          if "ode_integrate_kernel<false" in r["Kernel_Name"] and int(r["Grid_Size_X"]) >= N]
+    d1 = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9 for r in tr]
+    durs = [sum(d1[j:j + per]) for j in range(0, len(d1), per)]
     assert len(big_p) == len(CASES) and len(durs) == len(CASES), (len(big_p), len(durs))
     lines = {}
     for f in ("pmc.jsonl", "trace.jsonl"):
@@ -38,7 +48,8 @@ def main_cases(src: str, tag: str) -> None:
                 j = json.loads(ln)
                 lines.setdefault(j["config"], j)
     out = {"source": "tools/gpu_ode_pmc3.sh (tools/ode_pmc_run.py) + tools/summarize_ode_pmc.py " + tag,
-           "kernel": "ode_integrate_kernel<false>", "peak_tflops": 78.6,
+           "kernel": "ode_integrate_kernel<false>" if per == 1 else "ode_integrate_kernel<false, kLin> (both variants)",
+           "peak_tflops": 78.6,
            "note": "executed FP64 FLOP = 64 x (2 FMA + MUL + ADD) instructions; cooperative waves evaluate a "
                    "step's stage ingredients once per wave (or per 32/16/8-lane segment), so executed FLOP "
                    "per point-step falls as sharing rises: points_per_s is the figure of merit, the executed "
@@ -58,14 +69,14 @@ def main_cases(src: str, tag: str) -> None:
             "fp64_pipe_busy_frac": f64 * 4.0 / (t * 1024 * 2.4e9)}
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
-    with open(os.path.join(dst, "ode_pmc.json"), "w") as f:
+    with open(os.path.join(dst, fname), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
 
 
 def main():
     if len(sys.argv) > 3 and sys.argv[3] == "cases":
-        return main_cases(sys.argv[1], sys.argv[2])
+        return main_cases(sys.argv[1], sys.argv[2], *sys.argv[4:5])
     src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "odepmc")
     tag = sys.argv[2] if len(sys.argv) > 2 else "round2"
     rows = list(csv.DictReader(open(os.path.join(src, "pmc", "run_counter_collection.csv"))))

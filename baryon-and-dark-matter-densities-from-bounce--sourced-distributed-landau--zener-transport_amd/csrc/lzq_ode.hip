@@ -910,7 +910,9 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
           use_guess = true;
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
-            g[j] = kRadauPred[j][0] * Yp + kRadauPred[j][1] * Zs[0] + kRadauPred[j][2] * Zs[1] + kRadauPred[j][3] * Zs[2];
+            g[j] = __builtin_fma(kRadauPred[j][3], Zs[2],
+                                 __builtin_fma(kRadauPred[j][2], Zs[1],
+                                               __builtin_fma(kRadauPred[j][1], Zs[0], kRadauPred[j][0] * Yp)));
             use_guess = use_guess && fabs(g[j] - Ychi) <= 0.25 * fabs(Ychi);
           }
 #pragma unroll

@@ -54,7 +54,7 @@ def main():
             for k, e in engs.items():
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
-                e.ode(pts, ods, chunk=1 << 16, method=method)
+                e.ode(pts, ods, chunk=1 << 18, method=method)
                 torch.cuda.synchronize()
                 res[k].append(n / (time.perf_counter() - t0))
         out[cname] = {k: round(max(v)) for k, v in res.items()}

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Time the ODE fallback (lzq_ode_batch) of every library variant under
+"""Time the ODE fallback (Engine.ode, one chunk of up to 2^18 points) of every library variant under
 <package>/_build/variants/ in ONE process, interleaved rounds, on tools/bench_ode.py's
 narrow-window and stiff cases.  Variants must agree with the first one to 1e-11.
 

@@ -515,3 +515,29 @@ def test_ode_cooperative_subgroups_bit_identical(gpu_engine):
         finally:
             gpu_engine.tune_ode_launch_steps(prev)
         assert torch_equal(a, c) and torch_equal(sa, sc), method
+
+
+def test_ode_linear_waves_degenerate_step(gpu_engine):
+    """A window so narrow that a step is below x's rounding (T_max / T_min - 1 = 2e-12: h ~ 1e-16 x,
+    so xk + h == xk on many steps and the general path skips them): the linear integrator
+    variant must not step where the general path does not, so it takes every step on the
+    general path there (lzq_ode.hip k_split = -1) -- bits equal to the per-lane mode, and to a
+    wider window's linear waves run next to it in the same batch."""
+    rng = np.random.default_rng(53)
+    cfgs = []
+    for win in ({"T_max_over_Tp": 1.0 + 2e-12, "T_min_over_Tp": 1.0}, NARROW):
+        for _ in range(64):
+            c = full_cfg(BASE_CFG)
+            c.update(win, m_chi_GeV=3.0, P_chi_to_B=float(rng.uniform(0.05, 1.0)),
+                     incident_flux_scale=float(10 ** rng.uniform(-10, -8)), Gamma_wash_over_H=1.0,
+                     sigma_v_chi_GeV_m2=0.0, deplete_DM_from_source=bool(rng.uniform() < 0.5))
+            cfgs.append(c)
+    p, o = recs(cfgs)
+    a, sa = gpu_engine.ode(p, o)
+    prev = gpu_engine.tune_ode_coop(False)
+    try:
+        b, sb = gpu_engine.ode(p, o)
+    finally:
+        gpu_engine.tune_ode_coop(prev)
+    assert torch_equal(sa, sb) and torch_equal(a, b)
+    assert bool((sa[64:] == 0).all())

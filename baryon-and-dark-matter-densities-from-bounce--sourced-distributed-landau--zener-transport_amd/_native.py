@@ -66,7 +66,10 @@ FIELD = {n: i for i, n in enumerate(POINT_DOUBLE_FIELDS)}
 FIELD.update({"delta_LZ": 32, "m_mix": 33, "dprime": 34})
 FERMION, BOSON = 0, 1
 THERMAL, NONTHERMAL, REGIME_OTHER = 0, 1, 2
-LZQ_NZ = 1200
+LZQ_NZ, LZQ_Z_MAX = 1200, 30.0  # fpy:142 AoverVKernel defaults, main()'s grid (fpy:197)
+LZQ_NZ_MAX = 1 << 22
+ODE_NT_MAX = 1 << 20
+REUSE_TABLE_HEADER = 6  # LZQ_REUSE_TABLE_HEADER
 TUNE_EXP, TUNE_TRUNCATE, TUNE_ODE_COOP, TUNE_ODE_LAUNCH_STEPS = 0, 1, 2, 3  # enum lzq_tune_key
 ODE_MAX_LAUNCHES = 65536  # lzq_ode_*: max_steps <= 65536 x 2^(launch log2)
 # tuning state that changes result bits (the inner-loop exponential, ~1e-14): part of the
@@ -88,10 +91,10 @@ def library_id(path: str | None = None) -> str | None:
     return h.hexdigest()[:16]
 EXP_POLY11, EXP_TABLE = 0, 1  # enum lzq_exp_variant
 LZQ_MAX_AXES = 8
-ABI_VERSION = 1  # LZQ_ABI_VERSION (tests/test_capi.py checks it against the library)
+ABI_VERSION = 2  # LZQ_ABI_VERSION (tests/test_capi.py checks it against the library)
 
 # Symbols declared in include/lzq.h (checked by tests/test_capi.py against the header).
-EXPORTS = ("lzq_abi_version", "lzq_last_error", "lzq_init", "lzq_ztables", "lzq_tune", "lzq_aov_batch",
+EXPORTS = ("lzq_abi_version", "lzq_last_error", "lzq_init", "lzq_zgrid_init", "lzq_ztables", "lzq_tune", "lzq_aov_batch",
            "lzq_jchi_batch", "lzq_yields_batch", "lzq_sweep_grid", "lzq_sweep_grid_reuse_workspace",
            "lzq_sweep_grid_reuse", "lzq_sweep_grid_ztables", "lzq_sweep_grid_from_ztables",
            "lzq_yields_batch_reuse", "lzq_p_closed_form",
@@ -134,27 +137,29 @@ def load(path: str | None = None):
     L.lzq_abi_version.restype = ctypes.c_int
     L.lzq_last_error.restype = ctypes.c_char_p
     L.lzq_init.argtypes = [ctypes.c_int]
-    L.lzq_ztables.argtypes = [P(d), P(d), P(d)]
+    L.lzq_zgrid_init.argtypes = [ctypes.c_int, i32, d]
+    L.lzq_ztables.argtypes = [i32, d, P(d), P(d), P(d)]
     L.lzq_tune.argtypes = [i32, i32]
-    L.lzq_aov_batch.argtypes = [P(LzqPoint), vp, i64, vp, vp]
+    L.lzq_aov_batch.argtypes = [P(LzqPoint), vp, i64, i32, d, vp, vp]
     L.lzq_jchi_batch.argtypes = [P(LzqPoint), vp, i64, vp, vp]
-    L.lzq_yields_batch.argtypes = [vp, i64, i32, vp, vp, vp, vp, vp]
-    L.lzq_sweep_grid.argtypes = [P(LzqPoint), P(LzqAxis), i32, i64, i64, i32, vp, vp, vp]
+    L.lzq_yields_batch.argtypes = [vp, i64, i32, i32, d, vp, vp, vp, vp, vp]
+    L.lzq_sweep_grid.argtypes = [P(LzqPoint), P(LzqAxis), i32, i64, i64, i32, i32, d, vp, vp, vp]
     L.lzq_sweep_grid_reuse_workspace.argtypes = [P(LzqAxis), i32, i32]
-    L.lzq_sweep_grid_reuse.argtypes = [P(LzqPoint), P(LzqAxis), i32, i64, i64, i32, vp, vp, i64, vp, vp]
-    L.lzq_sweep_grid_ztables.argtypes = [P(LzqPoint), P(LzqAxis), i32, i32, vp, i64, vp]
-    L.lzq_sweep_grid_from_ztables.argtypes = [P(LzqPoint), P(LzqAxis), i32, i64, i64, i32, vp, vp, i64, vp, vp]
-    L.lzq_yields_batch_reuse.argtypes = [vp, i64, i32, vp, vp, vp, i64, vp, i64, vp, vp]
+    L.lzq_sweep_grid_reuse.argtypes = [P(LzqPoint), P(LzqAxis), i32, i64, i64, i32, i32, d, vp, vp, i64, vp, vp]
+    L.lzq_sweep_grid_ztables.argtypes = [P(LzqPoint), P(LzqAxis), i32, i32, i32, d, vp, i64, vp]
+    L.lzq_sweep_grid_from_ztables.argtypes = [P(LzqPoint), P(LzqAxis), i32, i64, i64, i32, i32, d, vp, vp, i64, vp,
+                                              vp]
+    L.lzq_yields_batch_reuse.argtypes = [vp, i64, i32, i32, d, vp, vp, vp, i64, vp, i64, vp, vp]
     L.lzq_p_closed_form.argtypes = [vp, i64, vp, vp]
     L.lzq_lz_propagate.argtypes = [vp, vp, vp, i64, i32, d, d, i32, vp, vp]
     L.lzq_lz_propagate_v.argtypes = [vp, vp, vp, vp, i64, i32, d, i32, vp, vp]
-    L.lzq_ode_tables.argtypes = [vp, i64, vp, vp, vp, i64, vp, vp]
+    L.lzq_ode_tables.argtypes = [vp, i64, vp, vp, i32, i32, d, vp, i64, vp, vp]
     L.lzq_ode_integrate.argtypes = [vp, vp, i64, vp, i64, i64, vp, vp, vp]
     L.lzq_ode_integrate_shared.argtypes = [vp, vp, i64, vp, i64, vp, i64, i64, vp, vp, vp]
     L.lzq_ode_quadrature.argtypes = [vp, vp, i64, vp, i64, vp, i64, i64, vp, vp, vp]
-    L.lzq_ode_batch.argtypes = [vp, vp, i64, vp, i64, i64, vp, vp, vp]
-    L.lzq_ode_aov_T.argtypes = [P(LzqPoint), d, d, vp, vp, i64, vp, vp]
-    L.lzq_ode_rhs.argtypes = [P(LzqPoint), P(LzqOdeParams), d, d, vp, vp, vp, i64, vp, vp]
+    L.lzq_ode_batch.argtypes = [vp, vp, i64, i32, d, vp, i64, i64, vp, vp, vp]
+    L.lzq_ode_aov_T.argtypes = [P(LzqPoint), d, d, i32, vp, vp, i64, vp, vp]
+    L.lzq_ode_rhs.argtypes = [P(LzqPoint), P(LzqOdeParams), d, d, i32, vp, vp, vp, i64, vp, vp]
     L.lzq_profile_splines.argtypes = [vp, vp, vp, i32, i32, vp, vp, vp]
     L.lzq_profile_crossings.argtypes = [vp, vp, i32, i32, vp, i64, i32, vp, vp, vp, vp, vp, vp]
     L.lzq_lz_propagate_profile.argtypes = [vp, vp, i32, i32, vp, i64, d, i32, vp, vp]
@@ -173,9 +178,22 @@ def check(rc: int, lib=None) -> None:
         raise LzqError(rc, msg.decode() if msg else "")
 
 
-def ztables() -> tuple[np.ndarray, np.ndarray, np.ndarray]:
-    """Host copies of the z grid, gamma4 and the quadrature weights built by the library."""
-    z, g4, om = (np.empty(LZQ_NZ) for _ in range(3))
+def ztables(nz: int = LZQ_NZ, z_max: float = LZQ_Z_MAX) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Host copies of the z grid, gamma4 and the quadrature weights the library builds for the
+    A/V kernel's grid linspace(0, z_max, nz) (fpy:154-156)."""
+    n = max(int(nz), 0)
+    z, g4, om = (np.empty(n) for _ in range(3))
     dp = ctypes.POINTER(ctypes.c_double)
-    check(load().lzq_ztables(z.ctypes.data_as(dp), g4.ctypes.data_as(dp), om.ctypes.data_as(dp)))
+    check(load().lzq_ztables(int(nz), float(z_max), z.ctypes.data_as(dp), g4.ctypes.data_as(dp),
+                             om.ctypes.data_as(dp)))
     return z, g4, om
+
+
+def zgrid(nz, z_max) -> tuple[int, float]:
+    """Validate an AoverVKernel (nz, z_max) the way numpy's linspace takes them (fpy:154): nz an
+    integer (operator.index, TypeError otherwise) >= 0 (ValueError), z_max a float."""
+    import operator
+    n = operator.index(nz)
+    if n < 0:
+        raise ValueError(f"Number of samples, {n}, must be non-negative.")
+    return int(n), float(z_max)

@@ -12,29 +12,53 @@ import math
 
 import numpy as np
 
+from . import _native
 from .config import Config, fast_path_ok, to_ode_params, to_point
 from .engine import default_engine
+from .physics_host import H_std
 
-LZQ_NZ, LZQ_ZMAX = 1200, 30.0
+LZQ_NZ, LZQ_ZMAX = _native.LZQ_NZ, _native.LZQ_Z_MAX
 
 
 class AoverVKernel:
-    """fpy:140-165.  Only the reference's own (z_max=30, nz=1200) grid is supported."""
+    """fpy:140-165 for any z grid: z = linspace(0, z_max, nz) and the cancelling gamma4 are built
+    by the library (lzq_ztables) and uploaded once per grid; every A_over_V_y runs on the GPU."""
 
     def __init__(self, I_p: float, beta_over_H: float, T_p: float, v_w: float, g_star: float,
                  z_max: float = LZQ_ZMAX, nz: int = LZQ_NZ):
-        if z_max != LZQ_ZMAX or nz != LZQ_NZ:
-            raise NotImplementedError("the lzq kernels are built for z_max=30, nz=1200 (fpy:142,197)")
-        self.I_p, self.beta_over_H, self.T_p, self.v_w, self.g_star = I_p, beta_over_H, T_p, v_w, g_star
+        self.nz, self.z_max = _native.zgrid(nz, z_max)  # numpy linspace's TypeError / ValueError
+        self.I_p = I_p
+        self.beta_over_H = beta_over_H
+        self.T_p = T_p
+        self.v_w = max(v_w, 1e-12)                      # fpy:146
+        self.g_star = g_star
+        self.H_p = H_std(T_p, g_star)                   # fpy:150-151
+        self.beta = self.beta_over_H * self.H_p
         self._cfg = {**Config().__dict__, "I_p": I_p, "beta_over_H": beta_over_H, "T_p_GeV": T_p,
                      "v_w": v_w, "g_star": g_star, "P_chi_to_B": 0.0}
+        self._tables = None
+
+    @property
+    def z(self) -> np.ndarray:
+        """fpy:154 (the library's host copy of the grid it integrates on)."""
+        return self._ztables()[0]
+
+    @property
+    def g4(self) -> np.ndarray:
+        """fpy:155-156, the cancelling form verbatim."""
+        return self._ztables()[1]
+
+    def _ztables(self):
+        if self._tables is None:
+            self._tables = _native.ztables(self.nz, self.z_max)
+        return self._tables
 
     def A_over_V_y(self, y: float) -> float:
         return float(self.A_over_V_ys([y])[0])
 
     def A_over_V_ys(self, ys) -> np.ndarray:
         """Batched fpy:158-165 (one GPU lane per y)."""
-        return default_engine().aov(self._cfg, ys).cpu().numpy()
+        return default_engine().aov(self._cfg, ys, nz=self.nz, z_max=self.z_max).cpu().numpy()
 
 
 class BoltzmannSystem:
@@ -72,20 +96,27 @@ class BoltzmannSystem:
     def integrate_YB_by_quadrature(self, T_lo: float, T_hi: float, n_y: int = 6000) -> float:
         """fpy:231-267 on the GPU (one wavefront)."""
         rec = to_point(self.cfg, P=self.P)
-        out = default_engine().yields(rec, n_y=int(n_y), T_lo=[float(T_lo)], T_hi=[float(T_hi)], P=[self.P])
+        out = default_engine().yields(rec, n_y=int(n_y), T_lo=[float(T_lo)], T_hi=[float(T_hi)], P=[self.P],
+                                      nz=self.aov.nz, z_max=self.aov.z_max)
         return float(out[0, 0].item())
 
     # ---- ODE fallback operators (fpy:207-219, 270-286) --------------------------------------
     def build_tables(self, T_lo: float, T_hi: float, n: int = 800):
-        """fpy:207-212 on the GPU: A/V at linspace(T_lo, T_hi, 800) + not-a-knot cubic spline."""
-        if int(n) != 800:
-            raise NotImplementedError("the lzq ODE tables have n = 800 knots (fpy:207, fpy:386)")
+        """fpy:207-212 on the GPU: A/V (on self.aov's z grid) at linspace(T_lo, T_hi, n) + the
+        not-a-knot cubic spline.  4 <= n <= LZQ_ODE_NT_MAX (scipy's not-a-knot spline needs at
+        least 4 knots for the cubic form the library evaluates)."""
+        import operator
+        n = operator.index(n)
+        if not 4 <= n <= _native.ODE_NT_MAX:
+            raise ValueError(f"build_tables: n = {n} outside [4, {_native.ODE_NT_MAX}]")
         if not (float(T_hi) > float(T_lo)):
             raise ValueError("`x` must be strictly increasing sequence.")
         eng = default_engine()
         self._T_lo, self._T_hi = float(T_lo), float(T_hi)
+        self._nt = int(n)
         self._rec = to_point(self.cfg, P=self.P)
-        self._work, status = eng.ode_tables(self._rec, [self._T_lo], [self._T_hi])
+        self._work, status = eng.ode_tables(self._rec, [self._T_lo], [self._T_hi], nt=self._nt, nz=self.aov.nz,
+                                            z_max=self.aov.z_max)
         if int(status[0].item()) != 0:
             raise ValueError("`x` must be strictly increasing sequence.")
 
@@ -94,19 +125,23 @@ class BoltzmannSystem:
             raise RuntimeError("call build_tables(T_lo, T_hi) first (fpy:207)")
 
     def A_over_V_Ts(self, Ts) -> np.ndarray:
-        """Batched fpy:214-218."""
-        self._need_tables()
-        return default_engine().ode_aov_T(self._rec, self._T_lo, self._T_hi, self._work, Ts).cpu().numpy()
+        """Batched fpy:214-218: the spline after build_tables, else A/V(y(T)) directly (fpy:218-219)."""
+        if getattr(self, "_work", None) is None:
+            from .physics_host import y_of_T
+            ys = [y_of_T(float(T), self.cfg.T_p_GeV, self.cfg.beta_over_H) for T in np.atleast_1d(Ts)]
+            return self.aov.A_over_V_ys(ys)
+        return default_engine().ode_aov_T(self._rec, self._T_lo, self._T_hi, self._work, Ts,
+                                          nt=self._nt).cpu().numpy()
 
     def A_over_V_T(self, T: float) -> float:
-        """fpy:214-218 (needs build_tables, like the reference's spline path)."""
+        """fpy:214-219."""
         return float(self.A_over_V_Ts([T])[0])
 
     def rhs_batch(self, xs, Ys) -> np.ndarray:
         """Batched fpy:270-286: (n, 2) array of (dY_chi/dx, dY_B/dx)."""
         self._need_tables()
         return default_engine().ode_rhs(self._rec, to_ode_params(self.cfg), self._T_lo, self._T_hi, self._work, xs,
-                                        Ys).cpu().numpy()
+                                        Ys, nt=self._nt).cpu().numpy()
 
     def rhs(self, x: float, Y) -> np.ndarray:
         """fpy:270-286."""

@@ -14,10 +14,11 @@ constexpr int kOdeWS = LZQ_ODE_WS_PER_POINT;  // workspace doubles per point
 // (value c0 s^3 + c1 s^2 + c2 s + c3, s = T - T_k); w[kOdeWS - 1] holds A/V at the last knot
 // while the spline is built.
 
-// A/V at the 800 T-knots of every point into w[4k + 3] / w[kOdeWS - 1] (lzq_kernels.hip: the
-// quadrature kernels' z-sum, one wavefront per point).  Host-side launch; sets lzq_last_error.
+// A/V at the nt T-knots of every point (z grid (nz, z_max)) into w[4k + 3] / w[4 nt - 1] of its
+// 4 nt doubles (lzq_kernels.hip: the quadrature kernels' z-sum, one wavefront per point).
+// Host-side launch; sets lzq_last_error.
 int launch_ode_aov_tables(const lzq_point* d_points, int64_t n, const double* d_T_lo, const double* d_T_hi,
-                          double* d_work, hipStream_t stream);
+                          int32_t nt, int32_t nz, double z_max, double* d_work, hipStream_t stream);
 
 // Longest-first launch order (lzq_propagator.hip): cost bins per point (0 = costliest, kCostBins
 // of them) and their histogram -> offs (kCostBins scratch) and order[n] (a counting sort: one

@@ -330,7 +330,7 @@ __device__ __forceinline__ double c2_scale() { return EXPV == kExpTable ? (doubl
 // N*1534 (no node can leave the clamp range); zsum_dispatch picks it per pass.
 template <int YB, int EXPV, bool CLAMP = true>
 __device__ __forceinline__ void zsum(const ZNode* __restrict__ zt, const double* tab, const double (&c2)[YB],
-                                     double (&F)[YB], int kend = kNZ) {
+                                     double (&F)[YB], int kend) {
 #pragma unroll
   for (int b = 0; b < YB; ++b) F[b] = 0.0;
   if constexpr (EXPV == kExpTable) {
@@ -401,16 +401,29 @@ __device__ __forceinline__ void zsum(const ZNode* __restrict__ zt, const double*
 
 // Pass-level wrapper: "dead" lanes, c2 * g4_1 <= -N*1077 (every node k >= 1 underflows to
 // exactly 0: g4 is increasing and omega_0 = 0), run the loop with c2 = 0 and are zeroed
-// afterwards -- the same instruction stream, the exact zero, and no |u| >= 2^51 in the loop.
+// afterwards -- the same instruction stream, the exact zero.
+//
+// The z grid: NZ > 0 is the compile-time node count of the reference's default grid
+// (fpy:142, LZQ_NZ = 1200: the headline kernels); NZ = 0 reads the padded node count nzp of a
+// runtime (nz, z_max) grid (AoverVKernel(..., z_max, nz), fpy:141-156).  Padding nodes repeat the
+// last g4 with omega = 0: each adds an exact +0, so F is the sum over the nz real nodes.  On a
+// fine grid (small g4_1) a live lane can reach |u| >= 2^51 at later nodes, where the magic-
+// constant reduction is inexact; every such node has u < KMIN, takes the clamped path (the
+// clamp-free test below sees it), and its term omega' * T''(KMIN) * ((A + O(|u| 2^-52))^2 + beta)
+// stays below 2^-1074 for |u| < 2^200, so it rounds away exactly like the underflow it stands
+// for (tests/test_exp2_host.py); build_ztable bounds |u| by that on the host.
 //
 // truncate != 0 (lzq_tune LZQ_TUNE_TRUNCATE; NOT used by the headline bench, which is dense
 // per SURVEY §8d): the pass stops at kend, the first z-node (rounded up to the unroll) beyond
 // which every live lane has c2*g4_k < -1080 octaves.  Those nodes add omega*2^u < 2^-1080 to
 // F, which the accumulate's rounding discards exactly, so F is bit-identical to the dense sum.
-template <int YB, int EXPV>
-__device__ __forceinline__ void zsum_dispatch(const ZNode* __restrict__ zt, const double* tab,
+// (Needs g4 non-decreasing over the grid: the host passes truncate = 0 for a grid whose
+// rounded g4 is not.)
+template <int YB, int EXPV, int NZ = 0>
+__device__ __forceinline__ void zsum_dispatch(const ZNode* __restrict__ zt, int nzp, const double* tab,
                                               const double (&c2)[YB], double (&F)[YB], int truncate = 0) {
-  const double g_1 = zt[1].g4, g_max = zt[kNZ - 1].g4;
+  const int nz = NZ > 0 ? NZ : nzp;
+  const double g_1 = zt[1].g4, g_max = zt[nz - 1].g4;
   bool dead[YB], small = true;
   double c2e[YB];
 #pragma unroll
@@ -419,7 +432,7 @@ __device__ __forceinline__ void zsum_dispatch(const ZNode* __restrict__ zt, cons
     c2e[b] = dead[b] ? 0.0 : c2[b];
     small = small && c2e[b] * g_max >= (double)kTabKMin;  // every node stays >= KMIN
   }
-  int kend = kNZ;
+  int kend = nz;
   if (truncate) {
     // largest per-lane threshold g_thr = -1080 N / c2 (live lanes; dead lanes impose none,
     // c2 = 0 lanes never underflow)
@@ -433,7 +446,7 @@ __device__ __forceinline__ void zsum_dispatch(const ZNode* __restrict__ zt, cons
     for (int off = 32; off >= 1; off >>= 1) thr = pymax(thr, __shfl_xor(thr, off, kWaveSize));
     thr = uniform(thr);
     // first k with g4_k > thr (g4 increasing): scalar binary search over the z table
-    int lo = 0, hi = kNZ;
+    int lo = 0, hi = nz;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
       if (zt[mid].g4 > thr) hi = mid;
@@ -505,8 +518,8 @@ __device__ __forceinline__ int lane_id() {
 // operations in the same lane order in every mode, so Y_B is bit-identical.
 enum YbMode { kYbDense = 0, kYbReuse = 1, kYbTable = 2 };
 
-template <int YB, int EXPV, int MODE = kYbDense, typename Slot>
-__device__ double yb_wave(Slot* slots, int w, const ZNode* __restrict__ zt, const double* tab, int truncate,
+template <int YB, int EXPV, int MODE = kYbDense, int NZ = 0, typename Slot>
+__device__ double yb_wave(Slot* slots, int w, const ZNode* __restrict__ zt, int nzp, const double* tab, int truncate,
                           const double* __restrict__ Fin = nullptr, double* __restrict__ Fout = nullptr) {
   static_assert(MODE == kYbDense || !LZQ_YFACT_EARLY, "table modes re-form the y-factors after the z-loop");
   if (slots[w].s.empty) return 0.0;
@@ -552,7 +565,7 @@ __device__ double yb_wave(Slot* slots, int w, const ZNode* __restrict__ zt, cons
         fy[b] = y_factors(s, yv[b], ey[b], wt[b]);
 #endif
       }
-      zsum_dispatch<YB, EXPV>(zt, tab, c2, F, truncate);
+      zsum_dispatch<YB, EXPV, NZ>(zt, nzp, tab, c2, F, truncate);
       if constexpr (MODE == kYbTable) {
 #pragma unroll
         for (int b = 0; b < YB; ++b) {
@@ -663,10 +676,10 @@ __device__ __forceinline__ void park(WaveSlot& slot, const QuadSetup& s, const E
 }
 
 // Quadrature of the parked point, then lane 0 stores its yields.
-template <int YB, int EXPV>
-__device__ __forceinline__ void point_yields(WaveSlot* slots, int w, const ZNode* __restrict__ zt,
+template <int YB, int EXPV, int NZ>
+__device__ __forceinline__ void point_yields(WaveSlot* slots, int w, const ZNode* __restrict__ zt, int nzp,
                                              const double* tab, int lane, int truncate, lzq_yield* out) {
-  const double Y_B = yb_wave<YB, EXPV>(slots, w, zt, tab, truncate);
+  const double Y_B = yb_wave<YB, EXPV, kYbDense, NZ>(slots, w, zt, nzp, tab, truncate);
   if (lane == 0) *out = epilogue_finish(slots[w].e, Y_B);
 }
 
@@ -727,23 +740,36 @@ __device__ __forceinline__ double grid_point(const lzq_point& base, const GridSp
 // ---------------------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------------------
-template <int YB, int EXPV>
+// Block-level table staging of the dense kernels: the exp table into LDS, and with LZQ_ZLDS
+// (an ablation build) the default grid's z nodes too; runtime grids (NZ = 0) keep theirs global.
+#if LZQ_ZLDS
+#define LZQ_STAGE_TABLES(NZ)                                   \
+  __shared__ LdsTables lds;                                    \
+  const double* tab;                                           \
+  if constexpr (NZ == kNZ) {                                   \
+    stage_tables<EXPV>(zt, &lds);                              \
+    tab = lds.t;                                               \
+    zt = lds.z;                                                \
+  } else {                                                     \
+    tab = stage_table<EXPV>(gtab, lds.t);                      \
+  }
+#else
+#define LZQ_STAGE_TABLES(NZ)          \
+  __shared__ double lds_tab[kTabN]; \
+  const double* tab = stage_table<EXPV>(gtab, lds_tab);
+#endif
+
+// NZ: kNZ for the reference's default z grid (the headline build, node count a compile-time
+// constant), 0 for a runtime grid of nzp (padded) nodes -- see zsum_dispatch.
+template <int YB, int EXPV, int NZ>
 __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void yields_points_kernel(const lzq_point* __restrict__ pts, int64_t n,
                                                               int32_t n_y, const double* __restrict__ T_lo,
                                                               const double* __restrict__ T_hi,
                                                               const double* __restrict__ Pov,
-                                                              const ZNode* __restrict__ zt,
+                                                              const ZNode* __restrict__ zt, int32_t nzp,
                                                               const double* __restrict__ gtab,
                                                               lzq_yield* __restrict__ out, int truncate) {
-#if LZQ_ZLDS
-  __shared__ LdsTables lds;
-  stage_tables<EXPV>(zt, &lds);
-  const double* tab = lds.t;
-  zt = lds.z;
-#else
-  __shared__ double lds_tab[kTabN];
-  const double* tab = stage_table<EXPV>(gtab, lds_tab);
-#endif
+  LZQ_STAGE_TABLES(NZ)
   __shared__ WaveSlot slots[kWavesPerBlock];
   const int lane = threadIdx.x & (kWaveSize - 1);
   // wave index and point index formed from readfirstlane, so they live in SGPRs (a VGPR copy
@@ -758,25 +784,17 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void yields_points_kernel(co
     const double thi = T_hi ? T_hi[idx] : pt.T_max_over_Tp * pt.T_p_GeV;  // fpy:368
     park(slots[w], quad_setup(pt, P, tlo, thi, n_y), epilogue_pre(pt, P), lane);
   }
-  point_yields<YB, EXPV>(slots, w, zt, tab, lane, truncate, out + idx);
+  point_yields<YB, EXPV, NZ>(slots, w, zt, nzp, tab, lane, truncate, out + idx);
 }
 
-template <int YB, int EXPV>
+template <int YB, int EXPV, int NZ>
 __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void yields_grid_kernel(lzq_point base, GridSpec grid, int64_t start,
                                                             int64_t count, int32_t n_y,
                                                             const double* __restrict__ Pov,
-                                                            const ZNode* __restrict__ zt,
+                                                            const ZNode* __restrict__ zt, int32_t nzp,
                                                             const double* __restrict__ gtab,
                                                             lzq_yield* __restrict__ out, int truncate) {
-#if LZQ_ZLDS
-  __shared__ LdsTables lds;
-  stage_tables<EXPV>(zt, &lds);
-  const double* tab = lds.t;
-  zt = lds.z;
-#else
-  __shared__ double lds_tab[kTabN];
-  const double* tab = stage_table<EXPV>(gtab, lds_tab);
-#endif
+  LZQ_STAGE_TABLES(NZ)
   __shared__ WaveSlot slots[kWavesPerBlock];
   const int lane = threadIdx.x & (kWaveSize - 1);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // SGPR (see yields_points_kernel)
@@ -789,7 +807,7 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void yields_grid_kernel(lzq_
     park(slots[w], quad_setup(pt, P, pt.T_min_over_Tp * pt.T_p_GeV, pt.T_max_over_Tp * pt.T_p_GeV, n_y),
          epilogue_pre(pt, P), lane);
   }
-  point_yields<YB, EXPV>(slots, w, zt, tab, lane, truncate, out + local);
+  point_yields<YB, EXPV, NZ>(slots, w, zt, nzp, tab, lane, truncate, out + local);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -799,9 +817,15 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void yields_grid_kernel(lzq_
 // table, kYbTable: the dense kernel's passes, F stored instead of integrated); the reuse kernel
 // then integrates every point from its table (kYbReuse).  Same operations, same lane order: Y_B
 // is bit-identical to lzq_sweep_grid.  Table t: kTabHdr header doubles (the y-grid and c of the
-// QuadSetup it was made for; a point whose own setup differs gets NaN yields, never a wrong
-// table), then its F values.
-constexpr int kTabHdr = 4;
+// QuadSetup it was made for, and the z grid's (nz, z_max); a point whose own setup or grid
+// differs gets NaN yields, never a wrong table), then its F values.
+constexpr int kTabHdr = 6;
+static_assert(kTabHdr == LZQ_REUSE_TABLE_HEADER, "include/lzq.h");
+
+// The z grid a table is made for, as its header stores it.
+struct ZKey {
+  double nz, z_max;
+};
 
 __device__ __forceinline__ int64_t table_of(const GridSpec& g, int64_t idx) {
   int64_t t = 0;
@@ -820,24 +844,28 @@ __device__ __forceinline__ int64_t table_rep(const GridSpec& g, int64_t t) {
 // Table t of one wavefront: header + the F values of the point parked in the wave's slot.
 template <int EXPV>
 __device__ __forceinline__ void ztable_wave(WaveSlot* slots, int w, int lane, const QuadSetup& qs, const EpiPre& e,
-                                            const ZNode* __restrict__ zt, const double* tab, int truncate, double* F) {
+                                            const ZNode* __restrict__ zt, int nzp, ZKey zk, const double* tab,
+                                            int truncate, double* F) {
   if (lane == 0) {
     F[0] = qs.y_lo;
     F[1] = qs.y_hi;
     F[2] = (double)qs.n;
     F[3] = qs.cneg;
+    F[4] = zk.nz;
+    F[5] = zk.z_max;
   }
   park(slots[w], qs, e, lane);
-  yb_wave<kYB, EXPV, kYbTable>(slots, w, zt, tab, truncate, nullptr, F + kTabHdr);
+  yb_wave<kYB, EXPV, kYbTable>(slots, w, zt, nzp, tab, truncate, nullptr, F + kTabHdr);
 }
 
 // One point integrated from its table F (NaN yields if the table was made for another y-grid).
 __device__ __forceinline__ void reuse_wave(WaveSlot* slots, int w, int lane, const QuadSetup& qs, const EpiPre& e,
-                                           const double* __restrict__ F, lzq_yield* out) {
+                                           ZKey zk, const double* __restrict__ F, lzq_yield* out) {
   // match is wave-uniform: every lane formed the same setup
-  const bool match = qs.empty || (F[0] == qs.y_lo && F[1] == qs.y_hi && F[2] == (double)qs.n && F[3] == qs.cneg);
+  const bool match = qs.empty || (F[0] == qs.y_lo && F[1] == qs.y_hi && F[2] == (double)qs.n && F[3] == qs.cneg &&
+                                  F[4] == zk.nz && F[5] == zk.z_max);
   park(slots[w], qs, e, lane);
-  const double Y_B = match ? yb_wave<kYB, kExpTable, kYbReuse>(slots, w, nullptr, nullptr, 0, F + kTabHdr) : 0.0;
+  const double Y_B = match ? yb_wave<kYB, kExpTable, kYbReuse>(slots, w, nullptr, 0, nullptr, 0, F + kTabHdr) : 0.0;
   if (lane == 0) {
     lzq_yield o = epilogue_finish(slots[w].e, Y_B);
     if (!match) o.Y_B = o.rho_B_kg_m3 = o.DM_over_B = __builtin_nan("");
@@ -848,8 +876,8 @@ __device__ __forceinline__ void reuse_wave(WaveSlot* slots, int w, int lane, con
 template <int EXPV>
 __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void grid_ztable_kernel(lzq_point base, GridSpec grid,
                                                                           int64_t n_tab, int32_t n_y, int64_t tstride,
-                                                                          const ZNode* __restrict__ zt,
-                                                                          const double* __restrict__ gtab,
+                                                                          const ZNode* __restrict__ zt, int32_t nzp,
+                                                                          ZKey zk, const double* __restrict__ gtab,
                                                                           double* __restrict__ Fw, int truncate) {
   __shared__ double lds_tab[kTabN];
   const double* tab = stage_table<EXPV>(gtab, lds_tab);
@@ -861,7 +889,7 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void grid_ztable_kernel(lzq_
   lzq_point pt;
   const double P = grid_point(base, grid, table_rep(grid, t), pt);
   const QuadSetup qs = quad_setup(pt, P, pt.T_min_over_Tp * pt.T_p_GeV, pt.T_max_over_Tp * pt.T_p_GeV, n_y);
-  ztable_wave<EXPV>(slots, w, lane, qs, epilogue_pre(pt, P), zt, tab, truncate, Fw + t * tstride);
+  ztable_wave<EXPV>(slots, w, lane, qs, epilogue_pre(pt, P), zt, nzp, zk, tab, truncate, Fw + t * tstride);
 }
 
 #ifndef LZQ_REUSE_MIN_WAVES
@@ -869,7 +897,7 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void grid_ztable_kernel(lzq_
 #endif
 __global__ __launch_bounds__(kBlock, LZQ_REUSE_MIN_WAVES) void grid_reuse_kernel(lzq_point base, GridSpec grid, int64_t start,
                                                            int64_t count, int32_t n_y,
-                                                           const double* __restrict__ Pov,
+                                                           const double* __restrict__ Pov, ZKey zk,
                                                            const double* __restrict__ Fw, int64_t tstride,
                                                            lzq_yield* __restrict__ out) {
   __shared__ WaveSlot slots[kWavesPerBlock];
@@ -881,7 +909,7 @@ __global__ __launch_bounds__(kBlock, LZQ_REUSE_MIN_WAVES) void grid_reuse_kernel
   const double Pg = grid_point(base, grid, start + local, pt);
   const double P = Pov ? Pov[local] : Pg;
   const QuadSetup qs = quad_setup(pt, P, pt.T_min_over_Tp * pt.T_p_GeV, pt.T_max_over_Tp * pt.T_p_GeV, n_y);
-  reuse_wave(slots, w, lane, qs, epilogue_pre(pt, P), Fw + table_of(grid, start + local) * tstride, out + local);
+  reuse_wave(slots, w, lane, qs, epilogue_pre(pt, P), zk, Fw + table_of(grid, start + local) * tstride, out + local);
 }
 
 // The same for explicit points (lzq_yields_batch_reuse): table t is made for point reps[t];
@@ -890,8 +918,8 @@ template <int EXPV>
 __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void points_ztable_kernel(const lzq_point* __restrict__ pts,
                                                                             const int64_t* __restrict__ reps,
                                                                             int64_t n_tab, int32_t n_y, int64_t tstride,
-                                                                            const ZNode* __restrict__ zt,
-                                                                            const double* __restrict__ gtab,
+                                                                            const ZNode* __restrict__ zt, int32_t nzp,
+                                                                            ZKey zk, const double* __restrict__ gtab,
                                                                             double* __restrict__ Fw, int truncate) {
   __shared__ double lds_tab[kTabN];
   const double* tab = stage_table<EXPV>(gtab, lds_tab);
@@ -903,11 +931,11 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void points_ztable_kernel(co
   const lzq_point pt = pts[reps[t]];
   const double P = pt.P_chi_to_B;
   const QuadSetup qs = quad_setup(pt, P, pt.T_min_over_Tp * pt.T_p_GeV, pt.T_max_over_Tp * pt.T_p_GeV, n_y);
-  ztable_wave<EXPV>(slots, w, lane, qs, epilogue_pre(pt, P), zt, tab, truncate, Fw + t * tstride);
+  ztable_wave<EXPV>(slots, w, lane, qs, epilogue_pre(pt, P), zt, nzp, zk, tab, truncate, Fw + t * tstride);
 }
 
 __global__ __launch_bounds__(kBlock, LZQ_REUSE_MIN_WAVES) void points_reuse_kernel(const lzq_point* __restrict__ pts, int64_t n,
-                                                             int32_t n_y, const double* __restrict__ Pov,
+                                                             int32_t n_y, const double* __restrict__ Pov, ZKey zk,
                                                              const int32_t* __restrict__ tidx,
                                                              const double* __restrict__ Fw, int64_t tstride,
                                                              lzq_yield* __restrict__ out) {
@@ -919,14 +947,14 @@ __global__ __launch_bounds__(kBlock, LZQ_REUSE_MIN_WAVES) void points_reuse_kern
   const lzq_point pt = pts[idx];
   const double P = Pov ? Pov[idx] : pt.P_chi_to_B;
   const QuadSetup qs = quad_setup(pt, P, pt.T_min_over_Tp * pt.T_p_GeV, pt.T_max_over_Tp * pt.T_p_GeV, n_y);
-  reuse_wave(slots, w, lane, qs, epilogue_pre(pt, P), Fw + (int64_t)tidx[idx] * tstride, out + idx);
+  reuse_wave(slots, w, lane, qs, epilogue_pre(pt, P), zk, Fw + (int64_t)tidx[idx] * tstride, out + idx);
 }
 
 // fpy:158-165, one lane per y value
 template <int EXPV>
 __global__ __launch_bounds__(kBlock) void aov_kernel(lzq_point pt, const double* __restrict__ ys, int64_t n,
-                                                    const ZNode* __restrict__ zt, const double* __restrict__ gtab,
-                                                    double* __restrict__ out) {
+                                                    const ZNode* __restrict__ zt, int32_t nzp,
+                                                    const double* __restrict__ gtab, double* __restrict__ out) {
   __shared__ double lds_tab[kTabN];
   const double* tab = stage_table<EXPV>(gtab, lds_tab);
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -935,16 +963,18 @@ __global__ __launch_bounds__(kBlock) void aov_kernel(lzq_point pt, const double*
   QuadSetup s = quad_setup(pt, pt.P_chi_to_B, 1.0, 1.0, LZQ_NY_MIN);
   double expy = exp_sc(pymax(pymin(y, 50.0), -50.0));
   double c2[1] = {((s.cneg * expy) * kLog2E) * c2_scale<EXPV>()}, F[1];
-  zsum_dispatch<1, EXPV>(zt, tab, c2, F);
+  zsum_dispatch<1, EXPV>(zt, nzp, tab, c2, F);
   if (live) out[i] = (y > 50.0) ? 0.0 : (s.pref0 * expy) * F[0];
 }
 
-// fpy:207-212 build_tables, first half: A/V at the 800 knots Ts = linspace(T_lo, T_hi, 800)
-// of main()'s window (fpy:368-369), np.maximum(Av, 0), one wavefront per point (lane i takes
-// knots i, i+64, ...).  The spline is fitted by lzq_ode.hip's ode_spline_kernel.
+// fpy:207-212 build_tables, first half: A/V at the nt knots Ts = linspace(T_lo, T_hi, nt)
+// (main() uses n = 800) of main()'s window (fpy:368-369) or the given one, np.maximum(Av, 0),
+// one wavefront per point (lane i takes knots i, i+64, ...), into the point's 4 nt doubles.  The
+// spline is fitted by lzq_ode.hip's ode_spline_kernel.
 template <int EXPV>
 __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void ode_aov_table_kernel(const lzq_point* __restrict__ pts,
-                                                                               int64_t n, const ZNode* __restrict__ zt,
+                                                                               int64_t n, int32_t nt,
+                                                                               const ZNode* __restrict__ zt, int32_t nzp,
                                                                                const double* __restrict__ gtab,
                                                                                const double* __restrict__ Tlo,
                                                                                const double* __restrict__ Thi,
@@ -960,20 +990,21 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void ode_aov_table_kernel(co
   const double Tp = uniform(pt.T_p_GeV), B = uniform(pt.beta_over_H);
   const double T_lo = uniform(Tlo ? Tlo[idx] : pt.T_min_over_Tp * Tp);
   const double T_hi = uniform(Thi ? Thi[idx] : pt.T_max_over_Tp * Tp);
-  const double stepT = uniform((T_hi - T_lo) / (double)(kOdeNT - 1));
+  const double stepT = uniform((T_hi - T_lo) / (double)(nt - 1));
   const QuadSetup s = quad_setup(pt, 0.0, 1.0, 1.0, LZQ_NY_MIN);  // only pref0 / cneg are used
   const double pref0 = uniform(s.pref0), cneg = uniform(s.cneg);
-  double* w = ws + idx * (int64_t)kOdeWS;
-  for (int base = 0; base < kOdeNT; base += kWaveSize) {
+  const int64_t ws_pt = 4 * (int64_t)nt;
+  double* w = ws + idx * ws_pt;
+  for (int base = 0; base < nt; base += kWaveSize) {
     const int i = base + lane;
-    const int ii = i < kOdeNT ? i : kOdeNT - 1;
-    const double T = linspace_at(T_lo, T_hi, stepT, ii, kOdeNT);
+    const int ii = i < nt ? i : nt - 1;
+    const double T = linspace_at(T_lo, T_hi, stepT, ii, nt);
     const double y = y_of_T(T, Tp, B);
     const double expy = exp_sc(pymax(pymin(y, 50.0), -50.0));  // fpy:161
     double c2[1] = {((cneg * expy) * kLog2E) * c2_scale<EXPV>()}, F[1];
-    zsum_dispatch<1, EXPV>(zt, tab, c2, F, truncate);
+    zsum_dispatch<1, EXPV>(zt, nzp, tab, c2, F, truncate);
     const double Av = (y > 50.0) ? 0.0 : (pref0 * expy) * F[0];  // fpy:159-165
-    if (i < kOdeNT) w[i < kOdeNT - 1 ? 4 * i + 3 : kOdeWS - 1] = pymax(Av, 0.0);
+    if (i < nt) w[i < nt - 1 ? 4 * i + 3 : ws_pt - 1] = pymax(Av, 0.0);
   }
 }
 
@@ -1004,10 +1035,10 @@ namespace {
 thread_local char g_err[512] = "";
 std::mutex g_mu;
 constexpr int kMaxDevices = 64;
-lzq::ZNode* g_dev_tab[kMaxDevices] = {nullptr};  // [LZQ_NZ] ZNode followed by kTabN doubles
-bool g_host_ready = false;
-double g_z[LZQ_NZ], g_g4[LZQ_NZ], g_omega[LZQ_NZ];
+// per device: the default grid's [LZQ_NZ] ZNode followed by the kTabN-entry exp table
+lzq::ZNode* g_dev_tab[kMaxDevices] = {nullptr};
 uint64_t g_exp2tab[lzq::kTabN];  // lzq::tab_entry_bits layout
+bool g_exp_ready = false;
 int g_exp_variant = lzq::kExpTable;
 int g_truncate = 0;  // LZQ_TUNE_TRUNCATE
 
@@ -1027,36 +1058,92 @@ int fail(int code, const char* fmt, ...) {
     if (e_ != hipSuccess) return fail(LZQ_EHIP, "%s: %s", #call, hipGetErrorString(e_));      \
   } while (0)
 
-// fpy:154-156 on the host, libm exp/pow (the table is point-invariant; built once).
-int build_host_tables() {
-  if (g_host_ready) return LZQ_OK;
-  const int n = LZQ_NZ;
-  const double step = (LZQ_Z_MAX - 0.0) / (double)(n - 1);
-  for (int k = 0; k < n; ++k) g_z[k] = (k == n - 1) ? LZQ_Z_MAX : (double)k * step + 0.0;  // np.linspace
-  double w[LZQ_NZ];
-  for (int k = 0; k < n; ++k) {
-    const double z = g_z[k];
+// One z grid of AoverVKernel(..., z_max, nz) (fpy:141-156) on the host: z = linspace(0, z_max, nz),
+// the verbatim cancelling gamma4, and the trapezoid weights omega_k = z_k^2 e^{-z_k} (d_{k-1} +
+// d_k)/2 with d = diff(z) (np.trapezoid, fpy:164, as a weighted sum).  libm exp/pow; built once
+// per grid.
+struct HostZGrid {
+  int32_t nz = 0;
+  double z_max = 0.0;
+  std::vector<double> z, g4, omega;
+  bool monotone = true;  // g4 non-decreasing (the truncation's binary search needs it)
+};
+
+int build_ztable(int32_t nz, double z_max, HostZGrid& h) {
+  if (nz < 0) return fail(LZQ_EINVAL, "Number of samples, %d, must be non-negative.", nz);  // np.linspace
+  if (nz > LZQ_NZ_MAX) return fail(LZQ_EINVAL, "nz = %d exceeds LZQ_NZ_MAX (%d)", nz, LZQ_NZ_MAX);
+  if (!(z_max >= 0.0) || !isfinite(z_max))
+    return fail(LZQ_EINVAL, "z_max = %g: the z grid must be finite and >= 0 (fpy:154)", z_max);
+  h.nz = nz;
+  h.z_max = z_max;
+  h.z.assign(nz, 0.0);
+  h.g4.assign(nz, 0.0);
+  h.omega.assign(nz, 0.0);
+  if (nz == 1) h.z[0] = 0.0;  // np.linspace(0, z_max, 1) = [0.]
+  if (nz >= 2) {
+    const double step = (z_max - 0.0) / (double)(nz - 1);
+    for (int k = 0; k < nz; ++k)  // np.linspace (numpy's step == 0 branch when z_max underflows the step)
+      h.z[k] = (k == nz - 1) ? z_max : (step == 0.0 ? ((double)k / (double)(nz - 1)) * z_max : (double)k * step) + 0.0;
+  }
+  std::vector<double> w(nz);
+  for (int k = 0; k < nz; ++k) {
+    const double z = h.z[k];
     const double ez = exp(-z);
     const double zz = z * z;
-    g_g4[k] = 6.0 - ez * (((pow(z, 3.0) + 3.0 * zz) + 6.0 * z) + 6.0);
+    h.g4[k] = 6.0 - ez * (((pow(z, 3.0) + 3.0 * zz) + 6.0 * z) + 6.0);
     w[k] = zz * ez;
-    if (!(g_g4[k] >= 0.0)) return fail(LZQ_EINVAL, "gamma4[%d] = %g < 0 breaks exp2_nonpos", k, g_g4[k]);
+    // the reference's cancelling form rounds below 0 only on grids far finer than its default
+    // (z_1 < ~3e-4): exp of a positive argument there, which the inner loop does not evaluate
+    if (!(h.g4[k] >= 0.0))
+      return fail(LZQ_EINVAL, "gamma4[%d] = %g < 0 (nz = %d, z_max = %g): the cancelling form of fpy:156 rounds "
+                  "below 0 on this grid", k, h.g4[k], nz, z_max);
+    if (k > 0 && h.g4[k] < h.g4[k - 1]) h.monotone = false;
   }
-  for (int k = 0; k < n; ++k) {
-    const double dl = k > 0 ? g_z[k] - g_z[k - 1] : 0.0;
-    const double dr = k + 1 < n ? g_z[k + 1] - g_z[k] : 0.0;
-    g_omega[k] = w[k] * (0.5 * (dl + dr));
+  for (int k = 0; k < nz; ++k) {
+    const double dl = k > 0 ? h.z[k] - h.z[k - 1] : 0.0;
+    const double dr = k + 1 < nz ? h.z[k + 1] - h.z[k] : 0.0;
+    h.omega[k] = w[k] * (0.5 * (dl + dr));
   }
+  // zsum_dispatch: a lane is dead (zeroed) iff c2N g4_1 <= -1077 N, so a live lane has
+  // |u| < 1077 N g4_max / g4_1; nodes beyond 2^51 are clamped and round away while |u| < 2^200
+  if (nz >= 2 && z_max > 0.0) {
+    const double g1 = h.g4[1], gmax = h.g4[nz - 1];
+    if (!(g1 > 0.0) || !((double)lzq::kTabN * 1077.0 * gmax / g1 < 0x1p200))
+      return fail(LZQ_EINVAL, "z grid (nz = %d, z_max = %g): gamma4[1] = %g breaks the inner loop's reduction", nz,
+                  z_max, g1);
+  }
+  return LZQ_OK;
+}
+
+const HostZGrid& default_host_grid() {
+  static HostZGrid h;
+  static int rc = build_ztable(LZQ_NZ, LZQ_Z_MAX, h);
+  (void)rc;  // the default grid always builds (tests/test_capi.py)
+  return h;
+}
+
+void build_exp_table() {
+  if (g_exp_ready) return;
   // T[j] = 2^(j/N): x87 long double exp2 (64-bit mantissa) rounded once to double, stored
   // with the pre-biased high word of lzq::tab_entry_bits
-  for (int j = 0; j < lzq::kTabN; ++j)
-    g_exp2tab[j] = lzq::tab_entry_bits(lzq::tab_exact(j), j);
-  // the kernel's magic-constant reduction needs |c2N*g| < 2^51 on every non-dead lane
-  // (zsum_dispatch: dead iff c2N*g_1 <= -N*1077), i.e. N*1077*g_max/g_1 < 2^51
-  if (!((double)lzq::kTabN * 1077.0 * g_g4[n - 1] / g_g4[1] < 0x1p50))
-    return fail(LZQ_EINVAL, "gamma4 table range breaks the magic-constant reduction");
-  g_host_ready = true;
-  return LZQ_OK;
+  for (int j = 0; j < lzq::kTabN; ++j) g_exp2tab[j] = lzq::tab_entry_bits(lzq::tab_exact(j), j);
+  g_exp_ready = true;
+}
+
+// Device image of a grid: nzp >= max(nz, kKUnroll) nodes, a multiple of the unroll; the padding
+// repeats the last g4 with omega' = 0 (an exact +0 per node).  Weights carry 2^-512 (the exp
+// table's T' carries 2^+512, lzq_exp2.h).
+int32_t padded_nodes(int32_t nz) {
+  const int32_t u = lzq::kKUnroll;
+  const int32_t n = nz > u ? nz : u;
+  return (n + u - 1) / u * u;
+}
+
+void device_nodes(const HostZGrid& h, lzq::ZNode* dst) {
+  const int32_t nzp = padded_nodes(h.nz);
+  const double glast = h.nz > 0 ? h.g4[h.nz - 1] : 0.0;
+  for (int k = 0; k < nzp; ++k)
+    dst[k] = k < h.nz ? lzq::ZNode{h.g4[k], ldexp(h.omega[k], -lzq::kOmegaBias)} : lzq::ZNode{glast, 0.0};
 }
 
 int ensure_device(int* dev_out) {
@@ -1067,18 +1154,80 @@ int ensure_device(int* dev_out) {
   if (g_dev_tab[dev]) return LZQ_OK;
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_dev_tab[dev]) return LZQ_OK;
-  int rc = build_host_tables();
-  if (rc) return rc;
+  const HostZGrid& h = default_host_grid();
+  if ((int)h.g4.size() != LZQ_NZ) return fail(LZQ_EINVAL, "default z grid failed to build");
+  build_exp_table();
   static_assert(sizeof(lzq::ZNode) == 2 * sizeof(double), "ZNode layout");
+  static_assert(LZQ_NZ % lzq::kKUnroll == 0, "the default grid needs no padding");
   std::vector<lzq::ZNode> host(LZQ_NZ + lzq::kTabN / 2);
-  // device weights carry 2^-512 (the exp table's T' carries 2^+512, lzq_exp2.h)
-  for (int k = 0; k < LZQ_NZ; ++k) host[k] = {g_g4[k], ldexp(g_omega[k], -lzq::kOmegaBias)};
+  device_nodes(h, host.data());
   memcpy(&host[LZQ_NZ], g_exp2tab, sizeof(g_exp2tab));
   const size_t bytes = host.size() * sizeof(lzq::ZNode);
   lzq::ZNode* d = nullptr;
   LZQ_HIP(hipMalloc(&d, bytes));
   LZQ_HIP(hipMemcpy(d, host.data(), bytes, hipMemcpyHostToDevice));
   g_dev_tab[dev] = d;
+  return LZQ_OK;
+}
+
+// A z grid on a device, as the kernels take it.
+struct DevZGrid {
+  const lzq::ZNode* zt = nullptr;
+  int32_t nzp = 0;
+  bool is_default = false;  // the compile-time LZQ_NZ kernels apply
+  bool monotone = true;
+  lzq::ZKey key{0.0, 0.0};
+};
+
+struct ZGridEntry {
+  int dev;
+  int32_t nz;
+  uint64_t zbits;
+  lzq::ZNode* d;
+  int32_t nzp;
+  bool monotone;
+};
+std::vector<ZGridEntry> g_zgrids;  // runtime grids, uploaded on first use (guarded by g_mu)
+
+bool is_default_grid(int32_t nz, double z_max) { return nz == LZQ_NZ && z_max == LZQ_Z_MAX; }
+
+// The device tables of (nz, z_max) on the current device: the default grid's (lzq_init), or a
+// runtime grid's, built and uploaded once per (device, nz, z_max) (a synchronous copy: call
+// lzq_zgrid_init before capturing launches into a graph).
+int zgrid_for(int32_t nz, double z_max, DevZGrid& g, int* dev_out) {
+  int dev, rc = ensure_device(&dev);
+  if (rc) return rc;
+  if (dev_out) *dev_out = dev;
+  g.key = lzq::ZKey{(double)nz, z_max};
+  if (is_default_grid(nz, z_max)) {
+    g.zt = g_dev_tab[dev];
+    g.nzp = LZQ_NZ;
+    g.is_default = true;
+    g.monotone = default_host_grid().monotone;
+    return LZQ_OK;
+  }
+  const uint64_t zb = __builtin_bit_cast(uint64_t, z_max);
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (const ZGridEntry& e : g_zgrids)
+    if (e.dev == dev && e.nz == nz && e.zbits == zb) {
+      g.zt = e.d;
+      g.nzp = e.nzp;
+      g.monotone = e.monotone;
+      return LZQ_OK;
+    }
+  HostZGrid h;
+  rc = build_ztable(nz, z_max, h);
+  if (rc) return rc;
+  const int32_t nzp = padded_nodes(nz);
+  std::vector<lzq::ZNode> host(nzp);
+  device_nodes(h, host.data());
+  lzq::ZNode* d = nullptr;
+  LZQ_HIP(hipMalloc(&d, host.size() * sizeof(lzq::ZNode)));
+  LZQ_HIP(hipMemcpy(d, host.data(), host.size() * sizeof(lzq::ZNode), hipMemcpyHostToDevice));
+  g_zgrids.push_back(ZGridEntry{dev, nz, zb, d, nzp, h.monotone});
+  g.zt = d;
+  g.nzp = nzp;
+  g.monotone = h.monotone;
   return LZQ_OK;
 }
 
@@ -1091,22 +1240,24 @@ constexpr int64_t kMaxGrid = 2147483647LL;
 int lzq_set_error(int code, const char* msg) { return fail(code, "%s", msg); }
 
 int lzq::launch_ode_aov_tables(const lzq_point* d_points, int64_t n, const double* d_T_lo, const double* d_T_hi,
-                               double* d_work, hipStream_t stream) {
+                               int32_t nt, int32_t nz, double z_max, double* d_work, hipStream_t stream) {
   if (n == 0) return LZQ_OK;
-  int dev, rc = ensure_device(&dev);
+  int dev;
+  DevZGrid g;
+  int rc = zgrid_for(nz, z_max, g, &dev);
   if (rc) return rc;
   const int64_t nb = blocks_for(n, lzq::kWavesPerBlock);
   if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_ode_tables: n too large");
   // The ODE tables always use the exact-underflow truncation of the z-sums: it is bit-identical
   // to the dense sum (tests/test_gpu_parity.py::test_truncation_is_bit_identical) and this path
   // is not the dense headline benchmark, so there is nothing to keep dense for.
-  const int truncate = 1;
+  const int truncate = g.monotone ? 1 : 0;
   if (g_exp_variant == lzq::kExpTable)
     hipLaunchKernelGGL(lzq::ode_aov_table_kernel<lzq::kExpTable>, dim3((unsigned)nb), dim3(lzq::kBlock), 0, stream,
-                       d_points, n, g_dev_tab[dev], exp_table(dev), d_T_lo, d_T_hi, d_work, truncate);
+                       d_points, n, nt, g.zt, g.nzp, exp_table(dev), d_T_lo, d_T_hi, d_work, truncate);
   else
     hipLaunchKernelGGL(lzq::ode_aov_table_kernel<lzq::kExpPoly11>, dim3((unsigned)nb), dim3(lzq::kBlock), 0, stream,
-                       d_points, n, g_dev_tab[dev], exp_table(dev), d_T_lo, d_T_hi, d_work, truncate);
+                       d_points, n, nt, g.zt, g.nzp, exp_table(dev), d_T_lo, d_T_hi, d_work, truncate);
   LZQ_HIP(hipGetLastError());
   return LZQ_OK;
 }
@@ -1117,11 +1268,14 @@ int lzq_abi_version(void) { return LZQ_ABI_VERSION; }
 
 const char* lzq_last_error(void) { return g_err; }
 
-int lzq_init(int device) {
+int lzq_init(int device) { return lzq_zgrid_init(device, LZQ_NZ, LZQ_Z_MAX); }
+
+int lzq_zgrid_init(int device, int32_t nz, double z_max) {
   int cur = 0;
   LZQ_HIP(hipGetDevice(&cur));
   if (device != cur) LZQ_HIP(hipSetDevice(device));
-  int rc = ensure_device(nullptr);
+  DevZGrid g;
+  int rc = zgrid_for(nz, z_max, g, nullptr);
   if (device != cur) {
     hipError_t e = hipSetDevice(cur);
     if (e != hipSuccess && rc == LZQ_OK) return fail(LZQ_EHIP, "hipSetDevice: %s", hipGetErrorString(e));
@@ -1158,29 +1312,37 @@ int lzq_tune(int32_t key, int32_t value) {
   return fail(LZQ_EINVAL, "lzq_tune: unknown key %d", key);
 }
 
-int lzq_ztables(double* z, double* gamma4, double* omega) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  int rc = build_host_tables();
+int lzq_ztables(int32_t nz, double z_max, double* z, double* gamma4, double* omega) {
+  HostZGrid h;
+  int rc;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    rc = build_ztable(nz, z_max, h);
+  }
   if (rc) return rc;
-  if (z) memcpy(z, g_z, sizeof(g_z));
-  if (gamma4) memcpy(gamma4, g_g4, sizeof(g_g4));
-  if (omega) memcpy(omega, g_omega, sizeof(g_omega));
+  const size_t bytes = sizeof(double) * (size_t)nz;
+  if (z && nz) memcpy(z, h.z.data(), bytes);
+  if (gamma4 && nz) memcpy(gamma4, h.g4.data(), bytes);
+  if (omega && nz) memcpy(omega, h.omega.data(), bytes);
   return LZQ_OK;
 }
 
-int lzq_aov_batch(const lzq_point* pt, const double* d_y, int64_t n, double* d_out, void* stream) {
+int lzq_aov_batch(const lzq_point* pt, const double* d_y, int64_t n, int32_t nz, double z_max, double* d_out,
+                  void* stream) {
   if (!pt || n < 0 || (n > 0 && (!d_y || !d_out))) return fail(LZQ_EINVAL, "lzq_aov_batch: bad arguments");
   if (n == 0) return LZQ_OK;
-  int dev, rc = ensure_device(&dev);
+  int dev;
+  DevZGrid g;
+  int rc = zgrid_for(nz, z_max, g, &dev);
   if (rc) return rc;
   int64_t nb = blocks_for(n, lzq::kBlock);
   if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_aov_batch: n too large");
   if (g_exp_variant == lzq::kExpTable)
     hipLaunchKernelGGL(lzq::aov_kernel<lzq::kExpTable>, dim3((unsigned)nb), dim3(lzq::kBlock), 0,
-                       (hipStream_t)stream, *pt, d_y, n, g_dev_tab[dev], exp_table(dev), d_out);
+                       (hipStream_t)stream, *pt, d_y, n, g.zt, g.nzp, exp_table(dev), d_out);
   else
     hipLaunchKernelGGL(lzq::aov_kernel<lzq::kExpPoly11>, dim3((unsigned)nb), dim3(lzq::kBlock), 0,
-                       (hipStream_t)stream, *pt, d_y, n, g_dev_tab[dev], exp_table(dev), d_out);
+                       (hipStream_t)stream, *pt, d_y, n, g.zt, g.nzp, exp_table(dev), d_out);
   LZQ_HIP(hipGetLastError());
   return LZQ_OK;
 }
@@ -1196,24 +1358,31 @@ int lzq_jchi_batch(const lzq_point* pt, const double* d_T, int64_t n, double* d_
   return LZQ_OK;
 }
 
-int lzq_yields_batch(const lzq_point* d_points, int64_t n, int32_t n_y, const double* d_T_lo,
-                     const double* d_T_hi, const double* d_P, lzq_yield* d_out, void* stream) {
+int lzq_yields_batch(const lzq_point* d_points, int64_t n, int32_t n_y, int32_t nz, double z_max,
+                     const double* d_T_lo, const double* d_T_hi, const double* d_P, lzq_yield* d_out, void* stream) {
   if (n < 0 || (n > 0 && (!d_points || !d_out))) return fail(LZQ_EINVAL, "lzq_yields_batch: bad arguments");
   if ((d_T_lo == nullptr) != (d_T_hi == nullptr))
     return fail(LZQ_EINVAL, "lzq_yields_batch: T_lo and T_hi must both be given or both be NULL");
   if (n == 0) return LZQ_OK;
-  int dev, rc = ensure_device(&dev);
+  int dev;
+  DevZGrid g;
+  int rc = zgrid_for(nz, z_max, g, &dev);
   if (rc) return rc;
   int64_t nb = blocks_for(n, lzq::kWavesPerBlock);
   if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_yields_batch: n too large");
-  if (g_exp_variant == lzq::kExpTable)
-    hipLaunchKernelGGL((lzq::yields_points_kernel<lzq::kYB, lzq::kExpTable>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
-                       (hipStream_t)stream, d_points, n, n_y, d_T_lo, d_T_hi, d_P, g_dev_tab[dev], exp_table(dev),
-                       d_out, g_truncate);
-  else
-    hipLaunchKernelGGL((lzq::yields_points_kernel<lzq::kYB, lzq::kExpPoly11>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
-                       (hipStream_t)stream, d_points, n, n_y, d_T_lo, d_T_hi, d_P, g_dev_tab[dev], exp_table(dev),
-                       d_out, g_truncate);
+  const int trunc = g.monotone ? g_truncate : 0;
+  const hipStream_t s = (hipStream_t)stream;
+#define LZQ_POINTS(EXPV, NZ)                                                                                        \
+  hipLaunchKernelGGL((lzq::yields_points_kernel<lzq::kYB, EXPV, NZ>), dim3((unsigned)nb), dim3(lzq::kBlock), 0, s, \
+                     d_points, n, n_y, d_T_lo, d_T_hi, d_P, g.zt, g.nzp, exp_table(dev), d_out, trunc)
+  if (g_exp_variant == lzq::kExpTable) {
+    if (g.is_default) LZQ_POINTS(lzq::kExpTable, lzq::kNZ);
+    else LZQ_POINTS(lzq::kExpTable, 0);
+  } else {
+    if (g.is_default) LZQ_POINTS(lzq::kExpPoly11, lzq::kNZ);
+    else LZQ_POINTS(lzq::kExpPoly11, 0);
+  }
+#undef LZQ_POINTS
   LZQ_HIP(hipGetLastError());
   return LZQ_OK;
 }
@@ -1267,31 +1436,37 @@ int64_t ztable_count(const lzq::GridSpec& g) {
 }  // namespace
 
 int lzq_sweep_grid(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int64_t start, int64_t count,
-                   int32_t n_y, const double* d_P, lzq_yield* d_out, void* stream) {
-  lzq::GridSpec g;
-  int rc = make_grid(base, axes, n_axes, start, count, d_out, "lzq_sweep_grid", g);
+                   int32_t n_y, int32_t nz, double z_max, const double* d_P, lzq_yield* d_out, void* stream) {
+  lzq::GridSpec gs;
+  int rc = make_grid(base, axes, n_axes, start, count, d_out, "lzq_sweep_grid", gs);
   if (rc) return rc;
   if (count == 0) return LZQ_OK;
   int dev;
-  rc = ensure_device(&dev);
+  DevZGrid g;
+  rc = zgrid_for(nz, z_max, g, &dev);
   if (rc) return rc;
   int64_t nb = blocks_for(count, lzq::kWavesPerBlock);
   if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_sweep_grid: count too large for one launch");
-  if (g_exp_variant == lzq::kExpTable)
-    hipLaunchKernelGGL((lzq::yields_grid_kernel<lzq::kYB, lzq::kExpTable>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
-                       (hipStream_t)stream, *base, g, start, count, n_y, d_P, g_dev_tab[dev], exp_table(dev), d_out,
-                       g_truncate);
-  else
-    hipLaunchKernelGGL((lzq::yields_grid_kernel<lzq::kYB, lzq::kExpPoly11>), dim3((unsigned)nb), dim3(lzq::kBlock), 0,
-                       (hipStream_t)stream, *base, g, start, count, n_y, d_P, g_dev_tab[dev], exp_table(dev), d_out,
-                       g_truncate);
+  const int trunc = g.monotone ? g_truncate : 0;
+  const hipStream_t s = (hipStream_t)stream;
+#define LZQ_GRID(EXPV, NZ)                                                                                         \
+  hipLaunchKernelGGL((lzq::yields_grid_kernel<lzq::kYB, EXPV, NZ>), dim3((unsigned)nb), dim3(lzq::kBlock), 0, s,  \
+                     *base, gs, start, count, n_y, d_P, g.zt, g.nzp, exp_table(dev), d_out, trunc)
+  if (g_exp_variant == lzq::kExpTable) {
+    if (g.is_default) LZQ_GRID(lzq::kExpTable, lzq::kNZ);
+    else LZQ_GRID(lzq::kExpTable, 0);
+  } else {
+    if (g.is_default) LZQ_GRID(lzq::kExpPoly11, lzq::kNZ);
+    else LZQ_GRID(lzq::kExpPoly11, 0);
+  }
+#undef LZQ_GRID
   LZQ_HIP(hipGetLastError());
   return LZQ_OK;
 }
 
-int lzq_yields_batch_reuse(const lzq_point* d_points, int64_t n, int32_t n_y, const double* d_P,
-                           const int64_t* d_rep, const int32_t* d_table_index, int64_t n_tables, double* d_work,
-                           int64_t work_doubles, lzq_yield* d_out, void* stream) {
+int lzq_yields_batch_reuse(const lzq_point* d_points, int64_t n, int32_t n_y, int32_t nz, double z_max,
+                           const double* d_P, const int64_t* d_rep, const int32_t* d_table_index, int64_t n_tables,
+                           double* d_work, int64_t work_doubles, lzq_yield* d_out, void* stream) {
   if (n < 0 || n_tables < 0 || (n > 0 && (!d_points || !d_out || !d_rep || !d_table_index || n_tables == 0)))
     return fail(LZQ_EINVAL, "lzq_yields_batch_reuse: bad arguments");
   const int64_t stride = (n_y > LZQ_NY_MIN ? n_y : LZQ_NY_MIN) + lzq::kTabHdr;
@@ -1300,21 +1475,24 @@ int lzq_yields_batch_reuse(const lzq_point* d_points, int64_t n, int32_t n_y, co
     return fail(LZQ_EINVAL, "lzq_yields_batch_reuse: workspace of %lld doubles < %lld needed", (long long)work_doubles,
                 (long long)(n_tables * stride));
   if (n == 0) return LZQ_OK;
-  int dev, rc = ensure_device(&dev);
+  int dev;
+  DevZGrid g;
+  int rc = zgrid_for(nz, z_max, g, &dev);
   if (rc) return rc;
   const int64_t nbt = blocks_for(n_tables, lzq::kWavesPerBlock), nb = blocks_for(n, lzq::kWavesPerBlock);
   if (nbt > kMaxGrid || nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_yields_batch_reuse: too large for one launch");
+  const int trunc = g.monotone ? 1 : 0;  // bit-identical to the dense sums either way
   if (g_exp_variant == lzq::kExpTable)
     hipLaunchKernelGGL((lzq::points_ztable_kernel<lzq::kExpTable>), dim3((unsigned)nbt), dim3(lzq::kBlock), 0,
-                       (hipStream_t)stream, d_points, d_rep, n_tables, n_y, stride, g_dev_tab[dev], exp_table(dev),
-                       d_work, 1);
+                       (hipStream_t)stream, d_points, d_rep, n_tables, n_y, stride, g.zt, g.nzp, g.key,
+                       exp_table(dev), d_work, trunc);
   else
     hipLaunchKernelGGL((lzq::points_ztable_kernel<lzq::kExpPoly11>), dim3((unsigned)nbt), dim3(lzq::kBlock), 0,
-                       (hipStream_t)stream, d_points, d_rep, n_tables, n_y, stride, g_dev_tab[dev], exp_table(dev),
-                       d_work, 1);
+                       (hipStream_t)stream, d_points, d_rep, n_tables, n_y, stride, g.zt, g.nzp, g.key,
+                       exp_table(dev), d_work, trunc);
   LZQ_HIP(hipGetLastError());
   hipLaunchKernelGGL(lzq::points_reuse_kernel, dim3((unsigned)nb), dim3(lzq::kBlock), 0, (hipStream_t)stream, d_points,
-                     n, n_y, d_P, d_table_index, d_work, stride, d_out);
+                     n, n_y, d_P, g.key, d_table_index, d_work, stride, d_out);
   LZQ_HIP(hipGetLastError());
   return LZQ_OK;
 }
@@ -1337,10 +1515,11 @@ int64_t lzq_sweep_grid_reuse_workspace(const lzq_axis* axes, int32_t n_axes, int
 // lzq_sweep_grid_reuse in its two halves: build every z-sum table of the grid (parts & 1) and
 // integrate [start, start + count) from them (parts & 2).
 static int sweep_grid_reuse_parts(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int64_t start,
-                                  int64_t count, int32_t n_y, const double* d_P, double* d_work, int64_t work_doubles,
-                                  lzq_yield* d_out, void* stream, int parts, const char* fn) {
-  lzq::GridSpec g;
-  int rc = make_grid(base, axes, n_axes, start, count, d_out, fn, g);
+                                  int64_t count, int32_t n_y, int32_t nz, double z_max, const double* d_P,
+                                  double* d_work, int64_t work_doubles, lzq_yield* d_out, void* stream, int parts,
+                                  const char* fn) {
+  lzq::GridSpec gs;
+  int rc = make_grid(base, axes, n_axes, start, count, d_out, fn, gs);
   if (rc) return rc;
   const int64_t need = lzq_sweep_grid_reuse_workspace(axes, n_axes, n_y);
   if (need < 0) return (int)need;
@@ -1350,58 +1529,62 @@ static int sweep_grid_reuse_parts(const lzq_point* base, const lzq_axis* axes, i
                 (long long)need);
   if (!(parts & 1) && count == 0) return LZQ_OK;
   int dev;
-  rc = ensure_device(&dev);
+  DevZGrid g;
+  rc = zgrid_for(nz, z_max, g, &dev);
   if (rc) return rc;
-  const int64_t n_tab = ztable_count(g);
+  const int64_t n_tab = ztable_count(gs);
   int64_t ts = 1;
-  for (int a = g.n_axes - 1; a >= 0; --a)
-    if (ztable_field(g.field[a])) {
-      g.tstride[a] = ts;
-      ts *= g.n[a];
+  for (int a = gs.n_axes - 1; a >= 0; --a)
+    if (ztable_field(gs.field[a])) {
+      gs.tstride[a] = ts;
+      ts *= gs.n[a];
     }
   const int64_t stride = (n_y > LZQ_NY_MIN ? n_y : LZQ_NY_MIN) + lzq::kTabHdr;
   const int64_t nbt = blocks_for(n_tab, lzq::kWavesPerBlock), nb = blocks_for(count, lzq::kWavesPerBlock);
   if (nbt > kMaxGrid || nb > kMaxGrid) return fail(LZQ_EINVAL, "%s: too large for one launch", fn);
   if (parts & 1) {
-    // the tables always use the exact-underflow truncation: bit-identical to the dense sums
+    // the tables use the exact-underflow truncation: bit-identical to the dense sums
+    const int trunc = g.monotone ? 1 : 0;
     if (g_exp_variant == lzq::kExpTable)
       hipLaunchKernelGGL((lzq::grid_ztable_kernel<lzq::kExpTable>), dim3((unsigned)nbt), dim3(lzq::kBlock), 0,
-                         (hipStream_t)stream, *base, g, n_tab, n_y, stride, g_dev_tab[dev], exp_table(dev), d_work, 1);
+                         (hipStream_t)stream, *base, gs, n_tab, n_y, stride, g.zt, g.nzp, g.key, exp_table(dev), d_work,
+                         trunc);
     else
       hipLaunchKernelGGL((lzq::grid_ztable_kernel<lzq::kExpPoly11>), dim3((unsigned)nbt), dim3(lzq::kBlock), 0,
-                         (hipStream_t)stream, *base, g, n_tab, n_y, stride, g_dev_tab[dev], exp_table(dev), d_work, 1);
+                         (hipStream_t)stream, *base, gs, n_tab, n_y, stride, g.zt, g.nzp, g.key, exp_table(dev), d_work,
+                         trunc);
     LZQ_HIP(hipGetLastError());
   }
   if ((parts & 2) && count > 0) {
-    hipLaunchKernelGGL(lzq::grid_reuse_kernel, dim3((unsigned)nb), dim3(lzq::kBlock), 0, (hipStream_t)stream, *base, g,
-                       start, count, n_y, d_P, d_work, stride, d_out);
+    hipLaunchKernelGGL(lzq::grid_reuse_kernel, dim3((unsigned)nb), dim3(lzq::kBlock), 0, (hipStream_t)stream, *base, gs,
+                       start, count, n_y, d_P, g.key, d_work, stride, d_out);
     LZQ_HIP(hipGetLastError());
   }
   return LZQ_OK;
 }
 
 int lzq_sweep_grid_reuse(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int64_t start, int64_t count,
-                         int32_t n_y, const double* d_P, double* d_work, int64_t work_doubles, lzq_yield* d_out,
-                         void* stream) {
+                         int32_t n_y, int32_t nz, double z_max, const double* d_P, double* d_work, int64_t work_doubles,
+                         lzq_yield* d_out, void* stream) {
   if (count == 0) {  // nothing to integrate: validate only (tables need not be built)
     lzq::GridSpec g;
     return make_grid(base, axes, n_axes, start, count, d_out, "lzq_sweep_grid_reuse", g);
   }
-  return sweep_grid_reuse_parts(base, axes, n_axes, start, count, n_y, d_P, d_work, work_doubles, d_out, stream, 3,
-                                "lzq_sweep_grid_reuse");
+  return sweep_grid_reuse_parts(base, axes, n_axes, start, count, n_y, nz, z_max, d_P, d_work, work_doubles, d_out,
+                                stream, 3, "lzq_sweep_grid_reuse");
 }
 
-int lzq_sweep_grid_ztables(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int32_t n_y, double* d_work,
-                           int64_t work_doubles, void* stream) {
-  return sweep_grid_reuse_parts(base, axes, n_axes, 0, 0, n_y, nullptr, d_work, work_doubles, nullptr, stream, 1,
-                                "lzq_sweep_grid_ztables");
+int lzq_sweep_grid_ztables(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int32_t n_y, int32_t nz,
+                           double z_max, double* d_work, int64_t work_doubles, void* stream) {
+  return sweep_grid_reuse_parts(base, axes, n_axes, 0, 0, n_y, nz, z_max, nullptr, d_work, work_doubles, nullptr,
+                                stream, 1, "lzq_sweep_grid_ztables");
 }
 
 int lzq_sweep_grid_from_ztables(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int64_t start,
-                                int64_t count, int32_t n_y, const double* d_P, const double* d_work,
-                                int64_t work_doubles, lzq_yield* d_out, void* stream) {
-  return sweep_grid_reuse_parts(base, axes, n_axes, start, count, n_y, d_P, const_cast<double*>(d_work), work_doubles,
-                                d_out, stream, 2, "lzq_sweep_grid_from_ztables");
+                                int64_t count, int32_t n_y, int32_t nz, double z_max, const double* d_P,
+                                const double* d_work, int64_t work_doubles, lzq_yield* d_out, void* stream) {
+  return sweep_grid_reuse_parts(base, axes, n_axes, start, count, n_y, nz, z_max, d_P, const_cast<double*>(d_work),
+                                work_doubles, d_out, stream, 2, "lzq_sweep_grid_from_ztables");
 }
 
 int lzq_p_closed_form(const double* d_lambda, int64_t n, double* d_P, void* stream) {

@@ -104,15 +104,17 @@ __device__ __forceinline__ OdePoint ode_point(const lzq_point& pt, const lzq_ode
 
 // fpy:214-218 A_over_V_T: min(max(T, T_lo), T_hi), then the PPoly of scipy (_ppoly.pyx:
 // interval k with T_k <= T < T_{k+1}, T == T_hi in the last one; c3 + c2 s + c1 s^2 + c0 s^3
-// accumulated in that order, powers by repeated multiplication).
-__device__ __forceinline__ double spline_eval(const OdePoint& o, const double* __restrict__ w, double T) {
+// accumulated in that order, powers by repeated multiplication).  nt: the table's knot count
+// (the integrators read main()'s LZQ_ODE_NT tables; the operator kernel any build_tables n).
+__device__ __forceinline__ double spline_eval(const OdePoint& o, const double* __restrict__ w, double T,
+                                              int nt = kOdeNT) {
   const double Tq = pymin(pymax(T, o.T_lo), o.T_hi);
   int k = (int)((Tq - o.T_lo) * o.inv_stepT);
-  k = k < 0 ? 0 : (k > kOdeNT - 2 ? kOdeNT - 2 : k);
+  k = k < 0 ? 0 : (k > nt - 2 ? nt - 2 : k);
   // the quotient can land one knot off after rounding: settle against the knots themselves
-  if (Tq < linspace_at(o.T_lo, o.T_hi, o.stepT, k, kOdeNT) && k > 0) --k;
-  else if (k < kOdeNT - 2 && Tq >= linspace_at(o.T_lo, o.T_hi, o.stepT, k + 1, kOdeNT)) ++k;
-  const double s = Tq - linspace_at(o.T_lo, o.T_hi, o.stepT, k, kOdeNT);
+  if (Tq < linspace_at(o.T_lo, o.T_hi, o.stepT, k, nt) && k > 0) --k;
+  else if (k < nt - 2 && Tq >= linspace_at(o.T_lo, o.T_hi, o.stepT, k + 1, nt)) ++k;
+  const double s = Tq - linspace_at(o.T_lo, o.T_hi, o.stepT, k, nt);
   const double* c = w + 4 * k;
   const double c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3];
   if (LZQ_ODE_FMA) return __builtin_fma(__builtin_fma(__builtin_fma(c0, s, c1), s, c2), s, c3);  // Horner, 3 fma
@@ -164,7 +166,7 @@ struct StageBase {
 };
 
 __device__ __forceinline__ StageBase ode_stage_base(const OdePoint& o, const double* __restrict__ w, double x,
-                                                    double* Av_out = nullptr) {
+                                                    double* Av_out = nullptr, int nt = kOdeNT) {
   // One division per call (1/x); every other quotient of fpy:270-286 is a product with a
   // per-point reciprocal or with powers of 1/T: 1/s = (1/T)^3 / s0 and 1/(H x) =
   // (M_Pl/H0) (1/T)^2 / x, exact rewrites of s = s0 T^3 and H = H0 T^2 / M_Pl (fpy:85, 88)
@@ -191,7 +193,7 @@ __device__ __forceinline__ StageBase ode_stage_base(const OdePoint& o, const dou
     vbar = sqrt(pymax(8.0 * T * o.inv_v0, 0.0));
   }
   const double Jb = 0.25 * n_eq * vbar;                       // fpy:222-223, J / flux
-  const double Av = spline_eval(o, w, T);                     // fpy:214-218
+  const double Av = spline_eval(o, w, T, nt);                 // fpy:214-218
   if (Av_out) *Av_out = Av;
   const double SBb = (Jb * Av) * window;                      // fpy:277, SB / (P flux)
   const bool plain = H > 1e-290 && s > 1e-290 && x == xc;     // the max() guards are inactive
@@ -219,8 +221,8 @@ __device__ __forceinline__ OdeStage stage_scale(const OdePoint& o, const StageBa
 }
 
 __device__ __forceinline__ OdeStage ode_stage(const OdePoint& o, const double* __restrict__ w, double x,
-                                              double* Av_out = nullptr) {
-  return stage_scale(o, ode_stage_base(o, w, x, Av_out));
+                                              double* Av_out = nullptr, int nt = kOdeNT) {
+  return stage_scale(o, ode_stage_base(o, w, x, Av_out, nt));
 }
 
 // The Y_chi-only stage of the Riccati equation with no source term (deplete off):
@@ -266,12 +268,12 @@ __device__ __forceinline__ OdeStage ode_stage_chi(const OdePoint& o, double x) {
   return chi_scale(o, ode_stage_chi_base(o, x));
 }
 
-// CubicSpline's check of the knots linspace(T_lo, T_hi, 800): strictly increasing.
-__device__ __forceinline__ bool ode_grid_ok(double T_lo, double T_hi, double stepT) {
+// CubicSpline's check of the knots linspace(T_lo, T_hi, nt): strictly increasing.
+__device__ __forceinline__ bool ode_grid_ok(double T_lo, double T_hi, double stepT, int nt = kOdeNT) {
   bool ok = true;
-  double prev = linspace_at(T_lo, T_hi, stepT, 0, kOdeNT);
-  for (int k = 1; k < kOdeNT; ++k) {
-    const double xk = linspace_at(T_lo, T_hi, stepT, k, kOdeNT);
+  double prev = linspace_at(T_lo, T_hi, stepT, 0, nt);
+  for (int k = 1; k < nt; ++k) {
+    const double xk = linspace_at(T_lo, T_hi, stepT, k, nt);
     ok = ok && (xk > prev);
     prev = xk;
   }
@@ -590,7 +592,7 @@ __device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st
 // elimination (scipy: banded LU with partial pivoting; equal to rounding); the forward sweep
 // parks (c', d') in the c0/c1 slots of the point's workspace.
 __global__ __launch_bounds__(kOdeBlock) void ode_spline_kernel(const lzq_point* __restrict__ pts, int64_t n,
-                                                               const double* __restrict__ Tlo,
+                                                               int32_t nt, const double* __restrict__ Tlo,
                                                                const double* __restrict__ Thi,
                                                                double* __restrict__ ws, int32_t* __restrict__ status) {
   const int64_t i = (int64_t)blockIdx.x * kOdeBlock + threadIdx.x;
@@ -598,12 +600,13 @@ __global__ __launch_bounds__(kOdeBlock) void ode_spline_kernel(const lzq_point* 
   const lzq_point pt = pts[i];
   const double T_lo = Tlo ? Tlo[i] : pt.T_min_over_Tp * pt.T_p_GeV;
   const double T_hi = Thi ? Thi[i] : pt.T_max_over_Tp * pt.T_p_GeV;
-  const double stepT = (T_hi - T_lo) / (double)(kOdeNT - 1);
-  double* w = ws + i * (int64_t)kOdeWS;
-  constexpr int N = kOdeNT;
+  const int N = nt;
+  const int64_t ws_pt = 4 * (int64_t)N;  // the point's 4 nt doubles; A/V at the last knot in the last one
+  const double stepT = (T_hi - T_lo) / (double)(N - 1);
+  double* w = ws + i * ws_pt;
   auto X = [&](int k) { return linspace_at(T_lo, T_hi, stepT, k, N); };
-  auto Yk = [&](int k) { return k < N - 1 ? w[4 * k + 3] : w[kOdeWS - 1]; };
-  if (!ode_grid_ok(T_lo, T_hi, stepT)) {
+  auto Yk = [&](int k) { return k < N - 1 ? w[4 * k + 3] : w[ws_pt - 1]; };
+  if (!ode_grid_ok(T_lo, T_hi, stepT, N)) {
     if (status) status[i] = LZQ_ODE_BAD_GRID;
     return;
   }
@@ -640,7 +643,7 @@ __global__ __launch_bounds__(kOdeBlock) void ode_spline_kernel(const lzq_point* 
     s_next = (r - d * dpm1) / (dx2 - d * cpm1);
   }
   // back substitution, forming the PPoly coefficients of interval k on the way
-  const double y_last = w[kOdeWS - 1];
+  const double y_last = w[ws_pt - 1];
   for (int k = N - 2; k >= 0; --k) {
     const double sk = w[4 * k + 1] - w[4 * k + 0] * s_next;
     const double dxk = X(k + 1) - X(k);
@@ -1170,7 +1173,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_QUAD_MIN_WAVES) void ode_quad_kernel
 
 // BoltzmannSystem.A_over_V_T / .rhs of one point at n arguments (lane per argument).
 __global__ __launch_bounds__(kOdeBlock) void ode_eval_kernel(lzq_point pt, lzq_ode_params od, double T_lo,
-                                                             double T_hi, const double* __restrict__ w,
+                                                             double T_hi, int32_t nt, const double* __restrict__ w,
                                                              const double* __restrict__ T, const double* __restrict__ x,
                                                              const double* __restrict__ Y, int64_t n,
                                                              double* __restrict__ out_Av, double* __restrict__ out_dY) {
@@ -1179,11 +1182,11 @@ __global__ __launch_bounds__(kOdeBlock) void ode_eval_kernel(lzq_point pt, lzq_o
   OdePoint o = ode_point(pt, od);
   o.T_lo = T_lo;
   o.T_hi = T_hi;
-  o.stepT = (T_hi - T_lo) / (double)(kOdeNT - 1);
+  o.stepT = (T_hi - T_lo) / (double)(nt - 1);
   ode_point_recips(o);
-  if (out_Av) out_Av[i] = spline_eval(o, w, T[i]);
+  if (out_Av) out_Av[i] = spline_eval(o, w, T[i], nt);
   if (out_dY) {
-    const OdeStage s = ode_stage(o, w, x[i]);
+    const OdeStage s = ode_stage(o, w, x[i], nullptr, nt);
     const double yc = Y[2 * i], yb = Y[2 * i + 1];
     out_dY[2 * i] = -s.lam * (yc * yc - s.E2) - s.S;
     out_dY[2 * i + 1] = s.alpha - s.beta * yb;
@@ -1249,15 +1252,16 @@ int hip_check(hipError_t e, const char* what) {
   return lzq_set_error(LZQ_EHIP, buf);
 }
 
-int check_ws(int64_t n, const double* d_work, int64_t work_doubles, const char* fn) {
+int check_ws(int64_t n, const double* d_work, int64_t work_doubles, const char* fn,
+             int64_t per_table = LZQ_ODE_WS_PER_POINT) {
   char buf[160];
   if (n < 0 || (n > 0 && !d_work)) {
     snprintf(buf, sizeof(buf), "%s: bad arguments", fn);
     return lzq_set_error(LZQ_EINVAL, buf);
   }
-  if (n > 0 && (work_doubles / LZQ_ODE_WS_PER_POINT) < n) {
-    snprintf(buf, sizeof(buf), "%s: workspace of %lld doubles < n * %d", fn, (long long)work_doubles,
-             LZQ_ODE_WS_PER_POINT);
+  if (n > 0 && (work_doubles / per_table) < n) {
+    snprintf(buf, sizeof(buf), "%s: workspace of %lld doubles < n * %lld", fn, (long long)work_doubles,
+             (long long)per_table);
     return lzq_set_error(LZQ_EINVAL, buf);
   }
   if (ode_blocks(n) > 2147483647LL) {
@@ -1271,19 +1275,24 @@ int check_ws(int64_t n, const double* d_work, int64_t work_doubles, const char* 
 
 extern "C" {
 
-int lzq_ode_tables(const lzq_point* d_points, int64_t n, const double* d_T_lo, const double* d_T_hi, double* d_work,
-                   int64_t work_doubles, int32_t* d_status, void* stream) {
-  int rc = check_ws(n, d_work, work_doubles, "lzq_ode_tables");
+int lzq_ode_tables(const lzq_point* d_points, int64_t n, const double* d_T_lo, const double* d_T_hi, int32_t nt,
+                   int32_t nz, double z_max, double* d_work, int64_t work_doubles, int32_t* d_status, void* stream) {
+  if (nt < 4 || nt > LZQ_ODE_NT_MAX) {
+    char buf[128];
+    snprintf(buf, sizeof(buf), "lzq_ode_tables: nt = %d knots outside [4, %d]", nt, LZQ_ODE_NT_MAX);
+    return lzq_set_error(LZQ_EINVAL, buf);
+  }
+  int rc = check_ws(n, d_work, work_doubles, "lzq_ode_tables", 4 * (int64_t)nt);
   if (rc) return rc;
   if (n > 0 && !d_points) return lzq_set_error(LZQ_EINVAL, "lzq_ode_tables: bad arguments");
   if ((d_T_lo == nullptr) != (d_T_hi == nullptr))
     return lzq_set_error(LZQ_EINVAL, "lzq_ode_tables: T_lo and T_hi must both be given or both be NULL");
   if (n == 0) return LZQ_OK;
   hipStream_t s = (hipStream_t)stream;
-  rc = lzq::launch_ode_aov_tables(d_points, n, d_T_lo, d_T_hi, d_work, s);
+  rc = lzq::launch_ode_aov_tables(d_points, n, d_T_lo, d_T_hi, nt, nz, z_max, d_work, s);
   if (rc) return rc;
   hipLaunchKernelGGL(lzq::ode_spline_kernel, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, s, d_points, n,
-                     d_T_lo, d_T_hi, d_work, d_status);
+                     nt, d_T_lo, d_T_hi, d_work, d_status);
   return hip_check(hipGetLastError(), "lzq_ode_tables");
 }
 
@@ -1333,33 +1342,35 @@ int lzq_ode_quadrature(const lzq_point* d_points, const lzq_ode_params* d_ode, i
                                 (hipStream_t)stream, "lzq_ode_quadrature");
 }
 
-int lzq_ode_batch(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, double* d_work,
-                  int64_t work_doubles, int64_t max_steps, lzq_yield* d_out, int32_t* d_status, void* stream) {
-  int rc = lzq_ode_tables(d_points, n, nullptr, nullptr, d_work, work_doubles, d_status, stream);
+int lzq_ode_batch(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, int32_t nz, double z_max,
+                  double* d_work, int64_t work_doubles, int64_t max_steps, lzq_yield* d_out, int32_t* d_status,
+                  void* stream) {
+  int rc = lzq_ode_tables(d_points, n, nullptr, nullptr, LZQ_ODE_NT, nz, z_max, d_work, work_doubles, d_status, stream);
   if (rc) return rc;
   return lzq_ode_integrate(d_points, d_ode, n, d_work, work_doubles, max_steps, d_out, d_status, stream);
 }
 
-int lzq_ode_aov_T(const lzq_point* pt, double T_lo, double T_hi, const double* d_work_point, const double* d_T,
-                  int64_t n, double* d_out_Av, void* stream) {
-  if (!pt || n < 0 || (n > 0 && (!d_work_point || !d_T || !d_out_Av)))
+int lzq_ode_aov_T(const lzq_point* pt, double T_lo, double T_hi, int32_t nt, const double* d_work_point,
+                  const double* d_T, int64_t n, double* d_out_Av, void* stream) {
+  if (!pt || n < 0 || nt < 4 || nt > LZQ_ODE_NT_MAX || (n > 0 && (!d_work_point || !d_T || !d_out_Av)))
     return lzq_set_error(LZQ_EINVAL, "lzq_ode_aov_T: bad arguments");
   if (n == 0) return LZQ_OK;
   if (ode_blocks(n) > 2147483647LL) return lzq_set_error(LZQ_EINVAL, "lzq_ode_aov_T: n too large");
   lzq_ode_params od = {0.0, 0.0, 0, 0};
   hipLaunchKernelGGL(lzq::ode_eval_kernel, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, (hipStream_t)stream,
-                     *pt, od, T_lo, T_hi, d_work_point, d_T, nullptr, nullptr, n, d_out_Av, nullptr);
+                     *pt, od, T_lo, T_hi, nt, d_work_point, d_T, nullptr, nullptr, n, d_out_Av, nullptr);
   return hip_check(hipGetLastError(), "lzq_ode_aov_T");
 }
 
-int lzq_ode_rhs(const lzq_point* pt, const lzq_ode_params* ode, double T_lo, double T_hi, const double* d_work_point,
-                const double* d_x, const double* d_Y, int64_t n, double* d_out_dY, void* stream) {
-  if (!pt || !ode || n < 0 || (n > 0 && (!d_work_point || !d_x || !d_Y || !d_out_dY)))
+int lzq_ode_rhs(const lzq_point* pt, const lzq_ode_params* ode, double T_lo, double T_hi, int32_t nt,
+                const double* d_work_point, const double* d_x, const double* d_Y, int64_t n, double* d_out_dY,
+                void* stream) {
+  if (!pt || !ode || n < 0 || nt < 4 || nt > LZQ_ODE_NT_MAX || (n > 0 && (!d_work_point || !d_x || !d_Y || !d_out_dY)))
     return lzq_set_error(LZQ_EINVAL, "lzq_ode_rhs: bad arguments");
   if (n == 0) return LZQ_OK;
   if (ode_blocks(n) > 2147483647LL) return lzq_set_error(LZQ_EINVAL, "lzq_ode_rhs: n too large");
   hipLaunchKernelGGL(lzq::ode_eval_kernel, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, (hipStream_t)stream,
-                     *pt, *ode, T_lo, T_hi, d_work_point, nullptr, d_x, d_Y, n, nullptr, d_out_dY);
+                     *pt, *ode, T_lo, T_hi, nt, d_work_point, nullptr, d_x, d_Y, n, nullptr, d_out_dY);
   return hip_check(hipGetLastError(), "lzq_ode_rhs");
 }
 

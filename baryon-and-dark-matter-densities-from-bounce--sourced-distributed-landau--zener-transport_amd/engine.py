@@ -93,12 +93,15 @@ class Engine:
         return _to_device_bytes(np.ascontiguousarray(recs, dtype=_native.POINT_DTYPE), self.device)
 
     # -- fpy:158-165 -----------------------------------------------------------------------
-    def aov(self, cfg, ys) -> torch.Tensor:
+    def aov(self, cfg, ys, nz: int = _native.LZQ_NZ, z_max: float = _native.LZQ_Z_MAX) -> torch.Tensor:
+        """A_over_V_y at every y for the kernel AoverVKernel(..., z_max, nz) of cfg (fpy:141-165)."""
+        nz, z_max = _native.zgrid(nz, z_max)
         y = self._f64(ys).reshape(-1)
         out = torch.empty_like(y)
         p = to_ctypes_point(to_point(cfg, P=0.0))
         with torch.cuda.device(self.device):
-            self._check(self.lib.lzq_aov_batch(ctypes.byref(p), _vp(y), y.numel(), _vp(out), self._stream()))
+            self._check(self.lib.lzq_aov_batch(ctypes.byref(p), _vp(y), y.numel(), nz, z_max, _vp(out),
+                                               self._stream()))
         return out
 
     # -- fpy:222-223 ------------------------------------------------------------------------
@@ -111,12 +114,15 @@ class Engine:
         return out
 
     # -- fpy:231-267 + epilogue ----------------------------------------------------------------
-    def yields(self, points, n_y: int = 8000, T_lo=None, T_hi=None, P=None, reuse: bool = False) -> torch.Tensor:
+    def yields(self, points, n_y: int = 8000, T_lo=None, T_hi=None, P=None, reuse: bool = False,
+               nz: int = _native.LZQ_NZ, z_max: float = _native.LZQ_Z_MAX) -> torch.Tensor:
         """points: POINT_DTYPE numpy array or a device byte tensor from points_to_device.
         Returns (n, 6) float64 device tensor in YIELD_FIELDS order.
         reuse: lzq_yields_batch_reuse -- points equal in _native.ZSUM_KEY share one table of
         z-sums (bit-identical; not the dense headline path).  Used only with main()'s window
-        and when points do share; otherwise the dense path."""
+        and when points do share; otherwise the dense path.
+        nz, z_max: the A/V kernel's z grid (AoverVKernel(..., z_max, nz), fpy:141-156)."""
+        nz, z_max = _native.zgrid(nz, z_max)
         d_pts = points if isinstance(points, torch.Tensor) else self.points_to_device(points)
         n = d_pts.numel() // _native.POINT_DTYPE.itemsize
         out = torch.empty((n, 6), dtype=torch.float64, device=self.device)
@@ -125,7 +131,7 @@ class Engine:
         Pv = None if P is None else self._f64(P)
         with torch.cuda.device(self.device):
             groups = table_groups(d_pts, n, _ZSUM_WORDS) if reuse and tl is None and th is None else None
-            stride = max(int(n_y), 2000) + 4
+            stride = max(int(n_y), 2000) + _native.REUSE_TABLE_HEADER
             if groups is not None and groups[0].numel() * stride * 8 <= REUSE_MAX_BYTES:
                 rep, inv = groups
                 need = rep.numel() * stride
@@ -133,25 +139,28 @@ class Engine:
                     self._zwork = torch.empty(need, dtype=torch.float64, device=self.device)
                 self._ztab_key = None   # the grid tables in _zwork are overwritten
                 idx = inv.to(torch.int32)
-                self._check(self.lib.lzq_yields_batch_reuse(_vp(d_pts), n, int(n_y), _vp(Pv), _vp(rep), _vp(idx),
-                                                              rep.numel(), _vp(self._zwork), self._zwork.numel(),
-                                                              _vp(out), self._stream()))
+                self._check(self.lib.lzq_yields_batch_reuse(_vp(d_pts), n, int(n_y), nz, z_max, _vp(Pv), _vp(rep),
+                                                              _vp(idx), rep.numel(), _vp(self._zwork),
+                                                              self._zwork.numel(), _vp(out), self._stream()))
                 self._keepalive_reuse = (rep, idx, d_pts)
             else:
-                self._check(self.lib.lzq_yields_batch(_vp(d_pts), n, int(n_y), _vp(tl), _vp(th), _vp(Pv), _vp(out),
-                                                        self._stream()))
+                self._check(self.lib.lzq_yields_batch(_vp(d_pts), n, int(n_y), nz, z_max, _vp(tl), _vp(th), _vp(Pv),
+                                                        _vp(out), self._stream()))
         return out
 
     # -- grid sweep ----------------------------------------------------------------------------
     def sweep(self, base_cfg, axes: Sequence[tuple], start: int, count: int, n_y: int = 8000,
               out: Optional[torch.Tensor] = None, P: Optional[float] = None,
-              P_points: Optional[torch.Tensor] = None, reuse: bool = False) -> torch.Tensor:
+              P_points: Optional[torch.Tensor] = None, reuse: bool = False, nz: int = _native.LZQ_NZ,
+              z_max: float = _native.LZQ_Z_MAX) -> torch.Tensor:
         """axes: sequence of (field_name, values) (C order, last fastest); field names are
         the lzq_point double fields or 'delta_LZ' / 'm_mix' / 'dprime'.  P_points: optional
         per-point P override ([count], device), e.g. from lz_propagate (config C5).
         reuse: lzq_sweep_grid_reuse -- the z-sums computed once per combination of the grid's
         I_p / beta_over_H / T_p_GeV / T_min_over_Tp / T_max_over_Tp values and shared by the
-        points (bit-identical results; NOT the dense headline path)."""
+        points (bit-identical results; NOT the dense headline path).
+        nz, z_max: the A/V kernel's z grid (fpy:141-156; main()'s default 1200, 30)."""
+        nz, z_max = _native.zgrid(nz, z_max)
         if len(axes) > _native.LZQ_MAX_AXES:
             raise ValueError(f"at most {_native.LZQ_MAX_AXES} sweep axes")
         dev_vals = [self._f64(v).reshape(-1) for _, v in axes]
@@ -172,7 +181,7 @@ class Engine:
             need = self.lib.lzq_sweep_grid_reuse_workspace(arr, len(axes), int(n_y)) if reuse else 0
             if need < 0:
                 self._check(int(need))
-            n_tables = need // (max(int(n_y), 2000) + 4)
+            n_tables = need // (max(int(n_y), 2000) + _native.REUSE_TABLE_HEADER)
             # the tables of a grid are built once and reused by every later chunk of the same sweep
             # (base, axes, n_y and exponential variant: tkey); every table costs one dense point, so
             # building them pays only with at least as many points to come as tables; and their
@@ -180,7 +189,7 @@ class Engine:
             tkey = None
             if reuse:
                 tkey = (bytes(base), tuple((n, np.asarray(v, dtype=np.float64).tobytes()) for n, v in axes), int(n_y),
-                        self._exp_variant)
+                        self._exp_variant, nz, z_max)
                 built = tkey == self._ztab_key
                 why = None if need * 8 <= REUSE_MAX_BYTES else f"{n_tables} z-sum tables exceed REUSE_MAX_BYTES"
                 if why is None and not built and not 0 < n_tables <= count:
@@ -193,38 +202,43 @@ class Engine:
                 if not built:
                     if self._zwork is None or self._zwork.numel() < need:
                         self._zwork = torch.empty(max(int(need), 1), dtype=torch.float64, device=self.device)
-                    self._check(self.lib.lzq_sweep_grid_ztables(ctypes.byref(base), arr, len(axes), int(n_y),
-                                                                _vp(self._zwork), self._zwork.numel(), self._stream()))
+                    self._check(self.lib.lzq_sweep_grid_ztables(ctypes.byref(base), arr, len(axes), int(n_y), nz,
+                                                                z_max, _vp(self._zwork), self._zwork.numel(),
+                                                                self._stream()))
                     self._ztab_key = tkey
                 self._check(self.lib.lzq_sweep_grid_from_ztables(
-                    ctypes.byref(base), arr, len(axes), int(start), int(count), int(n_y), _vp(Pp), _vp(self._zwork),
-                    self._zwork.numel(), _vp(out), self._stream()))
+                    ctypes.byref(base), arr, len(axes), int(start), int(count), int(n_y), nz, z_max, _vp(Pp),
+                    _vp(self._zwork), self._zwork.numel(), _vp(out), self._stream()))
             else:
                 self._check(self.lib.lzq_sweep_grid(ctypes.byref(base), arr, len(axes), int(start), int(count),
-                                                      int(n_y), _vp(Pp), _vp(out), self._stream()))
+                                                      int(n_y), nz, z_max, _vp(Pp), _vp(out), self._stream()))
         self._keepalive = dev_vals  # axis buffers must outlive the async launch
         return out
 
     # -- ODE fallback (fpy:200-219, 270-286, 385-417) ---------------------------------------
-    def ode_workspace(self, n: int) -> torch.Tensor:
-        return torch.empty(n * _native.ODE_WS_PER_POINT, dtype=torch.float64, device=self.device)
+    def ode_workspace(self, n: int, nt: int = _native.ODE_NT) -> torch.Tensor:
+        return torch.empty(n * 4 * int(nt), dtype=torch.float64, device=self.device)
 
-    def ode_tables(self, points, T_lo=None, T_hi=None, work: Optional[torch.Tensor] = None) -> tuple:
-        """BoltzmannSystem.build_tables for each point (window T_lo/T_hi per point, or main()'s
-        window): returns the (n * LZQ_ODE_WS_PER_POINT) spline workspace and the int32 status."""
+    def ode_tables(self, points, T_lo=None, T_hi=None, work: Optional[torch.Tensor] = None, nt: int = _native.ODE_NT,
+                   nz: int = _native.LZQ_NZ, z_max: float = _native.LZQ_Z_MAX) -> tuple:
+        """BoltzmannSystem.build_tables(T_lo, T_hi, n=nt) for each point (window T_lo/T_hi per
+        point, or main()'s window) with the A/V kernel's z grid (nz, z_max): returns the (n * 4 nt)
+        spline workspace and the int32 status."""
+        nz, z_max = _native.zgrid(nz, z_max)
         d_pts = points if isinstance(points, torch.Tensor) else self.points_to_device(points)
         n = d_pts.numel() // _native.POINT_DTYPE.itemsize
-        work = self.ode_workspace(n) if work is None else work
+        work = self.ode_workspace(n, nt) if work is None else work
         tl = None if T_lo is None else self._f64(T_lo).reshape(-1)
         th = None if T_hi is None else self._f64(T_hi).reshape(-1)
         status = torch.zeros(n, dtype=torch.int32, device=self.device)
         with torch.cuda.device(self.device):
-            self._check(self.lib.lzq_ode_tables(_vp(d_pts), n, _vp(tl), _vp(th), _vp(work), work.numel(), _vp(status),
-                                                self._stream()))
+            self._check(self.lib.lzq_ode_tables(_vp(d_pts), n, _vp(tl), _vp(th), int(nt), nz, z_max, _vp(work),
+                                                work.numel(), _vp(status), self._stream()))
         return work, status
 
     def ode(self, points, ode_params, max_steps: Optional[int] = None, chunk: int = 1 << 18,
-            share_tables: bool = True, method: str = "radau", group_waves: bool = True) -> tuple:
+            share_tables: bool = True, method: str = "radau", group_waves: bool = True, nz: int = _native.LZQ_NZ,
+            z_max: float = _native.LZQ_Z_MAX) -> tuple:
         """fpy:385-417 for n points (POINT_DTYPE records + ODE_DTYPE records): (n, 6) yields
         table and (n,) int32 status (enum lzq_ode_status), both on the device.  Points are
         processed in chunks so that the spline workspace stays <= chunk * 25.6 KB (6.7 GB at the
@@ -240,10 +254,12 @@ class Engine:
         (_native.ODE_STAGE_KEY, + deplete) next to each other, so that whole wavefronts qualify
         for the integrator's cooperative mode; results are scattered back to the input order.
         Each point's result is the same bits in either order.
-        max_steps: cap on the fixed Radau steps of a point (LZQ_ODE_TOO_MANY_STEPS beyond it).
-        None (default): the batch's own largest step count (ode_step_counts), i.e. every window
-        the reference accepts is integrated, however long (fpy:403-407): the library runs it as
-        continuation launches of <= 2^24 steps."""
+        max_steps: cap on the fixed Radau steps of a point (LZQ_ODE_TOO_MANY_STEPS beyond it; the
+        sweeps pass sweep.ODE_MAX_STEPS).  None (default): the batch's own largest step count
+        (ode_step_counts), i.e. every window the reference accepts is integrated, however long
+        (fpy:403-407): the library runs it as continuation launches of <= 2^24 steps.
+        nz, z_max: the z grid of the A/V kernel behind the spline tables (fpy:141-156, 207-212)."""
+        nz, z_max = _native.zgrid(nz, z_max)
         if method not in ("radau", "quadrature"):
             raise ValueError(f"method must be 'radau' or 'quadrature', got {method!r}")
         pts = np.ascontiguousarray(points, dtype=_native.POINT_DTYPE).reshape(-1)
@@ -253,11 +269,13 @@ class Engine:
         n = pts.size
         d_pts_all = self.points_to_device(pts)
         d_ode_all = _to_device_bytes(ods, self.device)
-        if max_steps is None:
-            need = ode_step_counts_device(d_pts_all, n)   # same values as ode_step_counts, on the device
-            need = need[torch.isfinite(need)]
-            per = 1 << getattr(self, "_ode_launch_log2", 24)
-            max_steps = int(min(float(need.max()) + 64 if need.numel() else 0, _native.ODE_MAX_LAUNCHES * per))
+        # the launches cover the batch's own largest step count (or the cap, when a point needs more:
+        # those points come back LZQ_ODE_TOO_MANY_STEPS), not the cap itself
+        need = ode_step_counts_device(d_pts_all, n)   # same values as ode_step_counts, on the device
+        need = need[torch.isfinite(need)]
+        per = 1 << getattr(self, "_ode_launch_log2", 24)
+        longest = int(min(float(need.max()) + 64 if need.numel() else 0, _native.ODE_MAX_LAUNCHES * per))
+        max_steps = longest if max_steps is None else min(int(max_steps), longest)
         order = wave_order(d_pts_all, d_ode_all, n) if group_waves else None
         if order is not None:
             d_pts_all = d_pts_all.view(n, -1)[order].contiguous().view(-1)
@@ -279,29 +297,30 @@ class Engine:
                 work = self.ode_workspace(max(n_tab, min(n, chunk) if rep is None else n_tab))
             with torch.cuda.device(self.device):
                 if method == "quadrature":
+                    nt = _native.ODE_NT
                     if rep is None:
-                        self._check(self.lib.lzq_ode_tables(_vp(d_pts), c1 - c0, None, None, _vp(work), work.numel(),
-                                                            None, self._stream()))
+                        self._check(self.lib.lzq_ode_tables(_vp(d_pts), c1 - c0, None, None, nt, nz, z_max, _vp(work),
+                                                            work.numel(), None, self._stream()))
                         d_idx = None
                     else:
                         d_rep = d_pts.view(c1 - c0, _native.POINT_DTYPE.itemsize)[rep].contiguous()
                         d_idx = inv.to(torch.int32)
-                        self._check(self.lib.lzq_ode_tables(_vp(d_rep), n_tab, None, None, _vp(work), work.numel(),
-                                                            None, self._stream()))
+                        self._check(self.lib.lzq_ode_tables(_vp(d_rep), n_tab, None, None, nt, nz, z_max, _vp(work),
+                                                            work.numel(), None, self._stream()))
                         keep.append((d_rep, d_idx))
                     self._check(self.lib.lzq_ode_quadrature(_vp(d_pts), _vp(d_ode), c1 - c0, _vp(d_idx), n_tab,
                                                             _vp(work), work.numel(), int(max_steps), _vp(out[c0:c1]),
                                                             _vp(status[c0:c1]), self._stream()))
                 elif rep is None:
-                    self._check(self.lib.lzq_ode_batch(_vp(d_pts), _vp(d_ode), c1 - c0, _vp(work), work.numel(),
-                                                       int(max_steps), _vp(out[c0:c1]), _vp(status[c0:c1]),
-                                                       self._stream()))
+                    self._check(self.lib.lzq_ode_batch(_vp(d_pts), _vp(d_ode), c1 - c0, nz, z_max, _vp(work),
+                                                       work.numel(), int(max_steps), _vp(out[c0:c1]),
+                                                       _vp(status[c0:c1]), self._stream()))
                 else:
                     rec = _native.POINT_DTYPE.itemsize
                     d_rep = d_pts.view(c1 - c0, rec)[rep].contiguous()
                     d_idx = inv.to(torch.int32)
-                    self._check(self.lib.lzq_ode_tables(_vp(d_rep), n_tab, None, None, _vp(work), work.numel(),
-                                                        None, self._stream()))
+                    self._check(self.lib.lzq_ode_tables(_vp(d_rep), n_tab, None, None, _native.ODE_NT, nz, z_max,
+                                                        _vp(work), work.numel(), None, self._stream()))
                     self._check(self.lib.lzq_ode_integrate_shared(_vp(d_pts), _vp(d_ode), c1 - c0, _vp(d_idx),
                                                                   n_tab, _vp(work), work.numel(), int(max_steps),
                                                                   _vp(out[c0:c1]), _vp(status[c0:c1]),
@@ -316,17 +335,19 @@ class Engine:
             out, status = out_in, st_in
         return out, status
 
-    def ode_aov_T(self, point, T_lo: float, T_hi: float, work_point: torch.Tensor, Ts) -> torch.Tensor:
-        """BoltzmannSystem.A_over_V_T (fpy:214-218) of one point at several T."""
+    def ode_aov_T(self, point, T_lo: float, T_hi: float, work_point: torch.Tensor, Ts,
+                  nt: int = _native.ODE_NT) -> torch.Tensor:
+        """BoltzmannSystem.A_over_V_T (fpy:214-218) of one point at several T (nt-knot tables)."""
         T = self._f64(Ts).reshape(-1)
         out = torch.empty_like(T)
         p = to_ctypes_point(np.asarray(point, dtype=_native.POINT_DTYPE).reshape(1))
         with torch.cuda.device(self.device):
-            self._check(self.lib.lzq_ode_aov_T(ctypes.byref(p), float(T_lo), float(T_hi), _vp(work_point), _vp(T),
-                                               T.numel(), _vp(out), self._stream()))
+            self._check(self.lib.lzq_ode_aov_T(ctypes.byref(p), float(T_lo), float(T_hi), int(nt), _vp(work_point),
+                                               _vp(T), T.numel(), _vp(out), self._stream()))
         return out
 
-    def ode_rhs(self, point, ode_params, T_lo: float, T_hi: float, work_point: torch.Tensor, xs, Ys) -> torch.Tensor:
+    def ode_rhs(self, point, ode_params, T_lo: float, T_hi: float, work_point: torch.Tensor, xs, Ys,
+                nt: int = _native.ODE_NT) -> torch.Tensor:
         """BoltzmannSystem.rhs (fpy:270-286) of one point: (n, 2) dY/dx at (x[i], Y[i])."""
         x = self._f64(xs).reshape(-1)
         Y = self._f64(Ys).reshape(-1, 2).contiguous()
@@ -336,7 +357,7 @@ class Engine:
         p = to_ctypes_point(np.asarray(point, dtype=_native.POINT_DTYPE).reshape(1))
         o = to_ctypes_ode(np.asarray(ode_params, dtype=_native.ODE_DTYPE).reshape(1))
         with torch.cuda.device(self.device):
-            self._check(self.lib.lzq_ode_rhs(ctypes.byref(p), ctypes.byref(o), float(T_lo), float(T_hi),
+            self._check(self.lib.lzq_ode_rhs(ctypes.byref(p), ctypes.byref(o), float(T_lo), float(T_hi), int(nt),
                                              _vp(work_point), _vp(x), _vp(Y), x.numel(), _vp(out), self._stream()))
         return out
 

@@ -98,6 +98,9 @@ class ProfileSpec:
         return X[self.synthetic], A[self.synthetic], B[self.synthetic]
 
 
+ODE_MAX_STEPS = 1 << 26   # a sweep's default cap on one ODE point's fixed Radau steps (LZQ_ODE_TOO_MANY_STEPS beyond)
+
+
 @dataclass
 class SweepSpec:
     name: str
@@ -108,6 +111,12 @@ class SweepSpec:
     crossings: Optional[CrossingSpec] = None
     ode_method: str = "radau"   # ODE-path points: "radau" (the reference's integrator) | "quadrature" (opt-in)
     profile: Optional[ProfileSpec] = None
+    nz: int = _native.LZQ_NZ          # the A/V kernel's z grid, AoverVKernel(..., z_max, nz) (fpy:141-156)
+    z_max: float = _native.LZQ_Z_MAX
+    # ODE-path points needing more fixed Radau steps than this are not integrated (a NaN row counted
+    # as too_many_steps in summary.json): one long window would otherwise hold its shard for hours.
+    # None = no cap (every window the reference accepts, as the single-point CLI does).
+    ode_max_steps: Optional[int] = ODE_MAX_STEPS
 
     @property
     def total(self) -> int:
@@ -133,6 +142,10 @@ class SweepSpec:
             d["ode_method"] = self.ode_method
         if self.profile is not None:
             d["profile"] = dict(self.profile.__dict__)
+        if (self.nz, self.z_max) != (_native.LZQ_NZ, _native.LZQ_Z_MAX):
+            d["nz"], d["z_max"] = int(self.nz), float(self.z_max)
+        if self.ode_max_steps != ODE_MAX_STEPS:
+            d["ode_max_steps"] = self.ode_max_steps
         return d
 
     def axis_values(self, start: int, count: int, device) -> dict:
@@ -251,7 +264,12 @@ def spec_from_json(d: dict) -> SweepSpec:
         raise ValueError(f"axes {PROFILE_FIELDS} need a 'profile' section")
     if prof is not None and cr is not None:
         raise ValueError("a spec takes either 'crossings' or 'profile'")
-    return SweepSpec(d.get("name", "custom"), base, axes, int(d.get("n_y", 8000)), d.get("notes", ""), cr, method, prof)
+    nz, z_max = _native.zgrid(d.get("nz", _native.LZQ_NZ), d.get("z_max", _native.LZQ_Z_MAX))
+    ms = d.get("ode_max_steps", ODE_MAX_STEPS)
+    if ms is not None and int(ms) < 0:
+        raise ValueError("ode_max_steps must be >= 0 or null")
+    return SweepSpec(d.get("name", "custom"), base, axes, int(d.get("n_y", 8000)), d.get("notes", ""), cr, method, prof,
+                     nz, z_max, None if ms is None else int(ms))
 
 
 def builtin_specs() -> dict:
@@ -590,7 +608,8 @@ def make_compute(spec: SweepSpec, engine, reuse: bool = False) -> ComputeFn:
                   (ods["deplete_DM_from_source"] != 0)
             sel = np.nonzero(ode)[0]
             if sel.size:
-                tab, status = engine.ode(pts[sel], ods[sel], method=spec.ode_method)
+                tab, status = engine.ode(pts[sel], ods[sel], method=spec.ode_method, max_steps=spec.ode_max_steps,
+                                         nz=spec.nz, z_max=spec.z_max)
                 # a point the integrator did not finish normally (a Radau Newton failure reports the
                 # state where it stopped, as fpy:408-410 does for the CLI) is a NaN row in a sweep
                 # table, counted per status in the summary ("ode_status")
@@ -600,7 +619,8 @@ def make_compute(spec: SweepSpec, engine, reuse: bool = False) -> ComputeFn:
                 out[torch.as_tensor(sel, device=out.device)] = tab
             sel = np.nonzero(~ode)[0]
             if sel.size:
-                out[torch.as_tensor(sel, device=out.device)] = engine.yields(pts[sel], n_y=spec.n_y, reuse=reuse)
+                out[torch.as_tensor(sel, device=out.device)] = engine.yields(pts[sel], n_y=spec.n_y, reuse=reuse,
+                                                                             nz=spec.nz, z_max=spec.z_max)
         compute_ode.ode_status = counts
         return compute_ode
 
@@ -609,7 +629,7 @@ def make_compute(spec: SweepSpec, engine, reuse: bool = False) -> ComputeFn:
         if spec.profile is not None:
             P_points = profile_P(spec, s, n, engine, pcache)
         engine.sweep(spec.base, grid_axes_for_kernel(spec), s, n, n_y=spec.n_y, out=out, P_points=P_points,
-                     reuse=reuse)
+                     reuse=reuse, nz=spec.nz, z_max=spec.z_max)
     return compute
 
 
@@ -625,6 +645,10 @@ def main(argv=None):
     ap.add_argument("--reuse-zsums", action="store_true",
                     help="share the quadrature's z-sums between points with the same y-grid and A/V kernel "
                          "(lzq_sweep_grid_reuse: bit-identical, much faster; not the dense headline mode)")
+    ap.add_argument("--nz", type=int, default=None, help="z nodes of the A/V kernel (AoverVKernel nz, fpy:142)")
+    ap.add_argument("--z-max", type=float, default=None, help="z_max of the A/V kernel (fpy:142)")
+    ap.add_argument("--ode-max-steps", type=int, default=None,
+                    help=f"cap on one ODE point's Radau steps (default {ODE_MAX_STEPS}; 0 = no cap)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI, default) | gloo (rehearsal: several ranks on one GPU)")
     args = ap.parse_args(argv)
@@ -635,6 +659,11 @@ def main(argv=None):
     else:
         with open(args.spec) as f:
             spec = spec_from_json(json.load(f))
+    if args.nz is not None or args.z_max is not None:
+        spec.nz, spec.z_max = _native.zgrid(spec.nz if args.nz is None else args.nz,
+                                            spec.z_max if args.z_max is None else args.z_max)
+    if args.ode_max_steps is not None:
+        spec.ode_max_steps = None if args.ode_max_steps == 0 else args.ode_max_steps
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

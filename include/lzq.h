@@ -3,7 +3,7 @@
  *
  * Drop-in boundary for the hot path of /root/reference/first_principles_yields.py ("fpy"):
  *
- *   fpy:141-165  AoverVKernel / A_over_V_y           -> lzq_aov_batch
+ *   fpy:141-165  AoverVKernel(..., z_max, nz) / A_over_V_y -> lzq_aov_batch (any z grid: nz, z_max)
  *   fpy:231-267  integrate_YB_by_quadrature           -> lzq_yields_batch (out->Y_B), lzq_sweep_grid
  *   fpy:372-384, fpy:413-417  Y_chi + densities        -> lzq_yields_batch / lzq_sweep_grid epilogue
  *   fpy:170-187  LZ plug-in closed form (fpy:183-184)  -> lzq_p_closed_form
@@ -34,9 +34,10 @@
 extern "C" {
 #endif
 
-#define LZQ_ABI_VERSION 1
+#define LZQ_ABI_VERSION 2
 #define LZQ_NZ 1200          /* fpy:142 nz default, used unchanged at fpy:197 */
 #define LZQ_Z_MAX 30.0       /* fpy:142 z_max default */
+#define LZQ_NZ_MAX (1 << 22) /* largest z grid accepted (64 MB of device nodes) */
 #define LZQ_NY_MAIN 8000     /* fpy:374 */
 #define LZQ_NY_MIN 2000      /* fpy:246 */
 
@@ -107,12 +108,25 @@ typedef struct lzq_axis {
 /* ---- library / device management ---------------------------------------------------- */
 int lzq_abi_version(void);
 const char* lzq_last_error(void);
-/* Builds and uploads the point-invariant z tables (fpy:154-156) for `device`.  Called
+/* The z grid.  Every entry point that evaluates A/V (fpy:158-165) takes the grid of the
+ * reference operator AoverVKernel(I_p, beta_over_H, T_p, v_w, g_star, z_max=30.0, nz=1200)
+ * (fpy:141-156) as (int32 nz, double z_max): z = linspace(0, z_max, nz), the cancelling gamma4
+ * of fpy:156 verbatim, the trapezoid of fpy:164.  (LZQ_NZ, LZQ_Z_MAX) is the grid main() uses
+ * (fpy:197) and runs the compile-time-sized headline kernels; any other grid is built on the
+ * host and uploaded once per (device, nz, z_max) on first use (a synchronous copy), then kept.
+ * 0 <= nz <= LZQ_NZ_MAX and 0 <= z_max < inf (numpy accepts the same; nz < 0 is its ValueError);
+ * nz <= 1 or z_max = 0 give A/V = 0 exactly, as numpy's trapezoid of <= 1 node / zero width does.
+ * A grid so fine that the cancelling gamma4 rounds below 0 (z_1 below ~3e-4, i.e. nz > ~1e5 on
+ * [0, 30]) is refused with LZQ_EINVAL: the reference then exponentiates positive arguments. */
+/* Builds and uploads the default z tables (fpy:154-156) and the exp table for `device`.  Called
  * lazily by every entry point; call it up front before capturing launches into a graph. */
 int lzq_init(int device);
-/* Host copies of the z tables: z (fpy:154), gamma4 (fpy:156) and the quadrature weights
- * omega_k = z_k^2 e^{-z_k} * (trapezoid weight of node k).  Each array has LZQ_NZ entries. */
-int lzq_ztables(double* z, double* gamma4, double* omega);
+/* The same for the grid (nz, z_max) (lzq_init = lzq_zgrid_init(device, LZQ_NZ, LZQ_Z_MAX)). */
+int lzq_zgrid_init(int device, int32_t nz, double z_max);
+/* Host copies of the z tables of the grid (nz, z_max): z (fpy:154), gamma4 (fpy:156) and the
+ * quadrature weights omega_k = z_k^2 e^{-z_k} * (trapezoid weight of node k); nz entries each
+ * (any pointer may be NULL). */
+int lzq_ztables(int32_t nz, double z_max, double* z, double* gamma4, double* omega);
 
 /* Tuning knobs for ablations (process-wide, not thread-safe against concurrent launches).
  * LZQ_TUNE_EXP selects the inner-loop exponential: LZQ_EXP_TABLE (default; 2^(j/N) LDS table,
@@ -137,8 +151,10 @@ enum lzq_exp_variant { LZQ_EXP_POLY11 = 0, LZQ_EXP_TABLE = 1 };
 int lzq_tune(int32_t key, int32_t value);
 
 /* ---- hot path -------------------------------------------------------------------------- */
-/* fpy:158-165: out[i] = A_over_V_y(y[i]) for the kernel of point *pt (host struct). */
-int lzq_aov_batch(const lzq_point* pt, const double* d_y, int64_t n, double* d_out, void* stream);
+/* fpy:158-165: out[i] = A_over_V_y(y[i]) for the kernel AoverVKernel(I_p, beta_over_H, T_p_GeV, v_w,
+ * g_star, z_max, nz) of point *pt (host struct). */
+int lzq_aov_batch(const lzq_point* pt, const double* d_y, int64_t n, int32_t nz, double z_max, double* d_out,
+                  void* stream);
 
 /* fpy:222-223: out[i] = BoltzmannSystem.J_chi(T[i]) for point *pt (diagnostics table). */
 int lzq_jchi_batch(const lzq_point* pt, const double* d_T, int64_t n, double* d_out, void* stream);
@@ -148,8 +164,9 @@ int lzq_jchi_batch(const lzq_point* pt, const double* d_T, int64_t n, double* d_
  * T_lo = T_min_over_Tp*T_p, T_hi = T_max_over_Tp*T_p, fpy:367-369).
  * d_P: optional per-point P override (NULL: point.P_chi_to_B), e.g. lzq_lz_propagate output.
  * n_y: y-grid size as passed to integrate_YB_by_quadrature (fpy:374 uses 8000; raised to
- * LZQ_NY_MIN as fpy:246). */
-int lzq_yields_batch(const lzq_point* d_points, int64_t n, int32_t n_y,
+ * LZQ_NY_MIN as fpy:246).  (nz, z_max): the A/V kernel's z grid (fpy:141-142; main(): LZQ_NZ,
+ * LZQ_Z_MAX). */
+int lzq_yields_batch(const lzq_point* d_points, int64_t n, int32_t n_y, int32_t nz, double z_max,
                      const double* d_T_lo, const double* d_T_hi, const double* d_P,
                      lzq_yield* d_out, void* stream);
 
@@ -158,7 +175,7 @@ int lzq_yields_batch(const lzq_point* d_points, int64_t n, int32_t n_y,
  * d_P: optional [count] per-point P override (e.g. lzq_lz_propagate output for multi-crossing
  * profiles, config C5); it takes precedence over P_chi_to_B and the LZ axes. */
 int lzq_sweep_grid(const lzq_point* base, const lzq_axis* axes, int32_t n_axes,
-                   int64_t start, int64_t count, int32_t n_y, const double* d_P,
+                   int64_t start, int64_t count, int32_t n_y, int32_t nz, double z_max, const double* d_P,
                    lzq_yield* d_out, void* stream);
 
 /* lzq_sweep_grid with the z-sums shared -- a separate mode, NOT the dense headline path
@@ -169,30 +186,33 @@ int lzq_sweep_grid(const lzq_point* base, const lzq_axis* axes, int32_t n_axes,
  * kernel's passes for the combination's first grid point, into d_work), then every point of
  * [start, start+count) is integrated from its table.  Yields are bit-identical to
  * lzq_sweep_grid (same operations, same lane order).  d_work: >= lzq_sweep_grid_reuse_workspace
- * doubles (tables x (max(n_y, LZQ_NY_MIN) + 4)); a negative return is an error code. */
+ * doubles (tables x (max(n_y, LZQ_NY_MIN) + LZQ_REUSE_TABLE_HEADER)); a negative return is an
+ * error code.  A table's header records the y grid, c and the z grid (nz, z_max) it was made
+ * for: a point integrated from a table of another setup or z grid gets NaN yields. */
+#define LZQ_REUSE_TABLE_HEADER 6
 int64_t lzq_sweep_grid_reuse_workspace(const lzq_axis* axes, int32_t n_axes, int32_t n_y);
 /* The same for n explicit points: d_rep[n_tables] (int64) names one point per table, whose
  * I_p, beta_over_H, T_p_GeV, T_min_over_Tp, T_max_over_Tp the table is made for;
  * d_table_index[n] (int32) gives each point's table.  main()'s window only (no T_lo/T_hi
- * overrides).  d_work >= n_tables * (max(n_y, LZQ_NY_MIN) + 4) doubles.  A point whose y-grid or
- * c differs from its table's gets NaN yields.  Bit-identical to lzq_yields_batch. */
-int lzq_yields_batch_reuse(const lzq_point* d_points, int64_t n, int32_t n_y, const double* d_P,
-                           const int64_t* d_rep, const int32_t* d_table_index, int64_t n_tables, double* d_work,
-                           int64_t work_doubles, lzq_yield* d_out, void* stream);
+ * overrides).  d_work >= n_tables * (max(n_y, LZQ_NY_MIN) + LZQ_REUSE_TABLE_HEADER) doubles.  A point
+ * whose y-grid or c differs from its table's gets NaN yields.  Bit-identical to lzq_yields_batch. */
+int lzq_yields_batch_reuse(const lzq_point* d_points, int64_t n, int32_t n_y, int32_t nz, double z_max,
+                           const double* d_P, const int64_t* d_rep, const int32_t* d_table_index, int64_t n_tables,
+                           double* d_work, int64_t work_doubles, lzq_yield* d_out, void* stream);
 int lzq_sweep_grid_reuse(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int64_t start, int64_t count,
-                         int32_t n_y, const double* d_P, double* d_work, int64_t work_doubles, lzq_yield* d_out,
-                         void* stream);
+                         int32_t n_y, int32_t nz, double z_max, const double* d_P, double* d_work,
+                         int64_t work_doubles, lzq_yield* d_out, void* stream);
 
 /* lzq_sweep_grid_reuse in two halves, so a sweep evaluated in chunks (or shards) builds its
  * z-sum tables once: lzq_sweep_grid_ztables writes every table of the grid into d_work (the
  * whole grid's, independent of any range); lzq_sweep_grid_from_ztables integrates points
  * [start, start+count) from tables built by it for the same base, axes and n_y (and exponential
  * variant).  Together they are lzq_sweep_grid_reuse, bit for bit. */
-int lzq_sweep_grid_ztables(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int32_t n_y, double* d_work,
-                           int64_t work_doubles, void* stream);
+int lzq_sweep_grid_ztables(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int32_t n_y, int32_t nz,
+                           double z_max, double* d_work, int64_t work_doubles, void* stream);
 int lzq_sweep_grid_from_ztables(const lzq_point* base, const lzq_axis* axes, int32_t n_axes, int64_t start,
-                                int64_t count, int32_t n_y, const double* d_P, const double* d_work,
-                                int64_t work_doubles, lzq_yield* d_out, void* stream);
+                                int64_t count, int32_t n_y, int32_t nz, double z_max, const double* d_P,
+                                const double* d_work, int64_t work_doubles, lzq_yield* d_out, void* stream);
 
 /* fpy:183-184: P[i] = clamp(1 - exp(-2 pi max(lambda[i], 0)), 0, 1) (naive 1-exp kept). */
 int lzq_p_closed_form(const double* d_lambda, int64_t n, double* d_P, void* stream);
@@ -208,8 +228,9 @@ typedef struct lzq_ode_params {
   int32_t reserved;                /* 0 */
 } lzq_ode_params;                  /* 24 bytes */
 
-#define LZQ_ODE_NT 800             /* fpy:207 build_tables(n=800) */
-#define LZQ_ODE_WS_PER_POINT 3200  /* workspace doubles per point (spline coefficients) */
+#define LZQ_ODE_NT 800             /* fpy:207 build_tables(n=800), the n main() uses (fpy:387) */
+#define LZQ_ODE_WS_PER_POINT 3200  /* workspace doubles per point (spline coefficients): 4 x LZQ_ODE_NT */
+#define LZQ_ODE_NT_MAX (1 << 20)   /* largest build_tables n accepted */
 enum lzq_ode_status {
   LZQ_ODE_OK = 0,
   LZQ_ODE_BAD_GRID = 1,       /* T grid not strictly increasing: CubicSpline raises ValueError */
@@ -223,14 +244,16 @@ enum lzq_ode_status {
                                  sol.y[:, -1] after a failed solve) */
 };
 
-/* BoltzmannSystem.build_tables(T_lo, T_hi, n=800) (fpy:207-212) for n points, at per-point
- * windows d_T_lo/d_T_hi ([n] each) or, both NULL, main()'s window T_lo = T_min_over_Tp T_p,
- * T_hi = T_max_over_Tp T_p (fpy:368-369, what lzq_ode_integrate needs): A/V at linspace(T_lo, T_hi, 800)
- * (the quadrature kernels' z-sum) and its not-a-knot cubic spline (scipy CubicSpline), into
- * d_work[i * LZQ_ODE_WS_PER_POINT ...] (work_doubles >= n * LZQ_ODE_WS_PER_POINT).
+/* BoltzmannSystem.build_tables(T_lo, T_hi, n=nt) (fpy:207-212) with self.aov = AoverVKernel(...,
+ * z_max, nz) for n points, at per-point windows d_T_lo/d_T_hi ([n] each) or, both NULL, main()'s
+ * window T_lo = T_min_over_Tp T_p, T_hi = T_max_over_Tp T_p (fpy:368-369, what lzq_ode_integrate
+ * needs): A/V at linspace(T_lo, T_hi, nt) (the quadrature kernels' z-sum on the grid (nz, z_max))
+ * and its not-a-knot cubic spline (scipy CubicSpline), into d_work[i * 4 nt ...] (work_doubles >=
+ * n * 4 nt; 4 <= nt <= LZQ_ODE_NT_MAX).  The integrators (lzq_ode_integrate*, lzq_ode_quadrature)
+ * read tables of nt = LZQ_ODE_NT knots, main()'s build_tables (fpy:387), on any z grid.
  * d_status (optional, [n] int32): LZQ_ODE_BAD_GRID for a window CubicSpline rejects. */
-int lzq_ode_tables(const lzq_point* d_points, int64_t n, const double* d_T_lo, const double* d_T_hi,
-                   double* d_work, int64_t work_doubles, int32_t* d_status, void* stream);
+int lzq_ode_tables(const lzq_point* d_points, int64_t n, const double* d_T_lo, const double* d_T_hi, int32_t nt,
+                   int32_t nz, double z_max, double* d_work, int64_t work_doubles, int32_t* d_status, void* stream);
 
 /* fpy:385-417 on built tables: Y_chi(x1), Y_B(x1) of rhs (fpy:270-286) from x0 = m/T_hi to
  * x1 = m/max(T_lo, 1e-30), Y(x0) = (Y_chi0 of fpy:389-399, 0), by the reference's method
@@ -274,17 +297,20 @@ int lzq_ode_quadrature(const lzq_point* d_points, const lzq_ode_params* d_ode, i
                        const int32_t* d_table_index, int64_t n_tables, const double* d_work, int64_t work_doubles,
                        int64_t max_steps, lzq_yield* d_out, int32_t* d_status, void* stream);
 
-/* lzq_ode_tables + lzq_ode_integrate (d_status may be NULL). */
-int lzq_ode_batch(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, double* d_work,
-                  int64_t work_doubles, int64_t max_steps, lzq_yield* d_out, int32_t* d_status, void* stream);
+/* lzq_ode_tables (nt = LZQ_ODE_NT, main()'s window, the z grid (nz, z_max)) + lzq_ode_integrate
+ * (d_status may be NULL). */
+int lzq_ode_batch(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, int32_t nz, double z_max,
+                  double* d_work, int64_t work_doubles, int64_t max_steps, lzq_yield* d_out, int32_t* d_status,
+                  void* stream);
 
 /* BoltzmannSystem.A_over_V_T (fpy:214-218) and .rhs (fpy:270-286) of ONE point (host structs)
- * whose tables for the window (T_lo, T_hi) are at d_work_point: out_Av[i] = A_over_V_T(T[i]);
- * out_dY[2i..2i+1] = rhs(x[i], (Y[2i], Y[2i+1])). */
-int lzq_ode_aov_T(const lzq_point* pt, double T_lo, double T_hi, const double* d_work_point, const double* d_T,
-                  int64_t n, double* d_out_Av, void* stream);
-int lzq_ode_rhs(const lzq_point* pt, const lzq_ode_params* ode, double T_lo, double T_hi, const double* d_work_point,
-                const double* d_x, const double* d_Y, int64_t n, double* d_out_dY, void* stream);
+ * whose nt-knot tables for the window (T_lo, T_hi) are at d_work_point (4 nt doubles, from
+ * lzq_ode_tables): out_Av[i] = A_over_V_T(T[i]); out_dY[2i..2i+1] = rhs(x[i], (Y[2i], Y[2i+1])). */
+int lzq_ode_aov_T(const lzq_point* pt, double T_lo, double T_hi, int32_t nt, const double* d_work_point,
+                  const double* d_T, int64_t n, double* d_out_Av, void* stream);
+int lzq_ode_rhs(const lzq_point* pt, const lzq_ode_params* ode, double T_lo, double T_hi, int32_t nt,
+                const double* d_work_point, const double* d_x, const double* d_Y, int64_t n, double* d_out_dY,
+                void* stream);
 
 /* ---- Landau-Zener propagator (north_star (1); no reference counterpart) --------------- */
 /* Coherent two-level propagation through n_cross sequential linear avoided crossings per

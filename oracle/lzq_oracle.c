@@ -118,22 +118,60 @@ static double y_of_T(double T, double T_p, double B) {
   return 0.5 * B * (q * q - 1.0);
 }
 
-/* fpy:141-156: z = linspace(0, z_max, nz); g4 = 6 - e^{-z}(z^3 + 3 z^2 + 6 z + 6) (verbatim). */
-typedef struct { double z[ORACLE_NZ], w[ORACLE_NZ], g4[ORACLE_NZ]; } ztab_t;
+/* fpy:141-156: z = linspace(0, z_max, nz); g4 = 6 - e^{-z}(z^3 + 3 z^2 + 6 z + 6) (verbatim).
+ * One table per AoverVKernel z grid; the default (1200, 30) one is built once and shared. */
+typedef struct {
+  int64_t nz;
+  double *z, *w, *g4;
+} ztab_t;
 static ztab_t g_ztab;
 static int g_ztab_ready = 0;
 
-static void ztab_init(void) {
-  if (g_ztab_ready) return;
-  oracle_linspace(0.0, ORACLE_ZMAX, ORACLE_NZ, g_ztab.z);
-  for (int k = 0; k < ORACLE_NZ; k++) {
-    double z = g_ztab.z[k];
+static void ztab_build(ztab_t* t, int64_t nz, double z_max) {
+  t->nz = nz;
+  size_t n = (size_t)(nz > 0 ? nz : 1);
+  t->z = (double*)malloc(sizeof(double) * n);
+  t->w = (double*)malloc(sizeof(double) * n);
+  t->g4 = (double*)malloc(sizeof(double) * n);
+  oracle_linspace(0.0, z_max, nz, t->z);
+  for (int64_t k = 0; k < nz; k++) {
+    double z = t->z[k];
     double ez = exp(-z);
     double zz = z * z; /* numpy z**2 is square() */
-    g_ztab.g4[k] = 6.0 - ez * (((pow(z, 3.0) + 3.0 * zz) + 6.0 * z) + 6.0);
-    g_ztab.w[k] = zz * ez; /* z**2 * exp(-z) */
+    t->g4[k] = 6.0 - ez * (((pow(z, 3.0) + 3.0 * zz) + 6.0 * z) + 6.0);
+    t->w[k] = zz * ez; /* z**2 * exp(-z) */
   }
-  g_ztab_ready = 1;
+}
+
+static void ztab_free(ztab_t* t) {
+  free(t->z);
+  free(t->w);
+  free(t->g4);
+}
+
+static void ztab_init(void) {
+  if (g_ztab_ready) return;
+#pragma omp critical(lzq_oracle_ztab)
+  {
+    if (!g_ztab_ready) {
+      ztab_build(&g_ztab, ORACLE_NZ, ORACLE_ZMAX);
+      g_ztab_ready = 1;
+    }
+  }
+}
+
+/* The table of grid (nz, z_max): the shared default, or a new one the caller frees (ztab_put). */
+static const ztab_t* ztab_get(int64_t nz, double z_max, ztab_t* scratch) {
+  if (nz == ORACLE_NZ && z_max == ORACLE_ZMAX) {
+    ztab_init();
+    return &g_ztab;
+  }
+  ztab_build(scratch, nz, z_max);
+  return scratch;
+}
+
+static void ztab_put(const ztab_t* t) {
+  if (t != &g_ztab) ztab_free((ztab_t*)t);
 }
 
 /* fpy:158-165 A_over_V_y, kernel constants from fpy:143-151. */
@@ -148,26 +186,38 @@ static aov_t aov_make(double I_p, double B, double T_p, double v_w, double g_sta
   return a;
 }
 
-static double aov_eval(const aov_t* a, double y, double* f, double* scratch) {
+/* f, scratch: >= max(nz, 1) doubles.  np.trapezoid of fewer than 2 nodes is 0.0. */
+static double aov_eval(const aov_t* a, const ztab_t* zt, double y, double* f, double* scratch) {
   if (y > 50.0) return 0.0;
   double expy = exp(pymax(pymin(y, 50.0), -50.0));
   double pref = (a->I_p / 2.0) * (a->beta / a->v_w) * expy;
   double c = -(a->I_p / 6.0) * expy;
-  for (int k = 0; k < ORACLE_NZ; k++) f[k] = g_ztab.w[k] * exp(c * g_ztab.g4[k]);
-  double F = trapezoid(f, g_ztab.z, ORACLE_NZ, scratch);
+  for (int64_t k = 0; k < zt->nz; k++) f[k] = zt->w[k] * exp(c * zt->g4[k]);
+  double F = zt->nz >= 2 ? trapezoid(f, zt->z, zt->nz, scratch) : 0.0;
   return pref * F;
 }
 
-double oracle_aov(double I_p, double B, double T_p, double v_w, double g_star, double y) {
-  ztab_init();
-  double f[ORACLE_NZ], s[ORACLE_NZ];
+double oracle_aov_z(double I_p, double B, double T_p, double v_w, double g_star, double y, int64_t nz,
+                    double z_max) {
+  ztab_t own;
+  const ztab_t* zt = ztab_get(nz, z_max, &own);
+  size_t n = (size_t)(nz > 1 ? nz : 1);
+  double* f = (double*)malloc(sizeof(double) * n);
+  double* s = (double*)malloc(sizeof(double) * n);
   aov_t a = aov_make(I_p, B, T_p, v_w, g_star);
-  return aov_eval(&a, y, f, s);
+  double r = aov_eval(&a, zt, y, f, s);
+  free(f);
+  free(s);
+  ztab_put(zt);
+  return r;
 }
 
-/* fpy:231-267 integrate_YB_by_quadrature */
-double oracle_yb_quadrature(const oracle_point* p, double T_lo, double T_hi, int32_t n_y) {
-  ztab_init();
+double oracle_aov(double I_p, double B, double T_p, double v_w, double g_star, double y) {
+  return oracle_aov_z(I_p, B, T_p, v_w, g_star, y, ORACLE_NZ, ORACLE_ZMAX);
+}
+
+/* fpy:231-267 integrate_YB_by_quadrature, A/V on the grid zt */
+static double yb_quadrature(const oracle_point* p, const ztab_t* zt, double T_lo, double T_hi, int32_t n_y) {
   double B = p->beta_over_H, Tp = p->T_p_GeV, m = p->m_chi_GeV;
   double y_lo_raw = y_of_T(T_hi, Tp, B);
   double y_hi_raw = y_of_T(T_lo, Tp, B);
@@ -178,8 +228,8 @@ double oracle_yb_quadrature(const oracle_point* p, double T_lo, double T_hi, int
 
   double* ys = (double*)malloc(sizeof(double) * (size_t)n);
   double* integ = (double*)malloc(sizeof(double) * (size_t)n);
-  double* scratch = (double*)malloc(sizeof(double) * (size_t)(n > ORACLE_NZ ? n : ORACLE_NZ));
-  double f[ORACLE_NZ];
+  double* scratch = (double*)malloc(sizeof(double) * (size_t)(n > zt->nz ? n : zt->nz));
+  double* f = (double*)malloc(sizeof(double) * (size_t)(zt->nz > 1 ? zt->nz : 1));
   oracle_linspace(y_lo, y_hi, n, ys);
 
   aov_t a = aov_make(p->I_p, B, Tp, p->v_w, p->g_star);
@@ -195,7 +245,7 @@ double oracle_yb_quadrature(const oracle_point* p, double T_lo, double T_hi, int
     double H = 1.66 * sqrtg * T * T / MPL_GEV;
     double s = (2.0 * (PI * PI) / 45.0) * p->g_star_s * pow(T, 3.0);
     double J = p->incident_flux_scale * 0.25 * n_chi_eq(T, m, p->g_chi, p->stats) * vbar_chi(T, m);
-    double Av = aov_eval(&a, y, f, scratch);
+    double Av = aov_eval(&a, zt, y, f, scratch);
     double q = y / sig;
     double window = exp(-0.5 * (q * q));
     double SB = p->P_chi_to_B * J * Av * window;
@@ -205,15 +255,29 @@ double oracle_yb_quadrature(const oracle_point* p, double T_lo, double T_hi, int
   free(ys);
   free(integ);
   free(scratch);
+  free(f);
   return r;
 }
 
+double oracle_yb_quadrature_z(const oracle_point* p, double T_lo, double T_hi, int32_t n_y, int64_t nz,
+                              double z_max) {
+  ztab_t own;
+  const ztab_t* zt = ztab_get(nz, z_max, &own);
+  double r = yb_quadrature(p, zt, T_lo, T_hi, n_y);
+  ztab_put(zt);
+  return r;
+}
+
+double oracle_yb_quadrature(const oracle_point* p, double T_lo, double T_hi, int32_t n_y) {
+  return oracle_yb_quadrature_z(p, T_lo, T_hi, n_y, ORACLE_NZ, ORACLE_ZMAX);
+}
+
 /* fpy:361-417 (fast path only: the callers gate on fpy:372). */
-int oracle_point_yields(const oracle_point* p, oracle_yield* o) {
+static int point_yields(const oracle_point* p, const ztab_t* zt, oracle_yield* o) {
   double T_p = p->T_p_GeV;
   double T_hi = p->T_max_over_Tp * T_p;
   double T_lo = p->T_min_over_Tp * T_p;
-  double YB = oracle_yb_quadrature(p, T_lo, T_hi, 8000);
+  double YB = yb_quadrature(p, zt, T_lo, T_hi, 8000);
   double Ychi;
   if (p->regime == 0) {
     Ychi = n_chi_eq(T_hi, p->m_chi_GeV, p->g_chi, p->stats) / s_entropy(T_hi, p->g_star_s);
@@ -236,8 +300,22 @@ int oracle_point_yields(const oracle_point* p, oracle_yield* o) {
   return 0;
 }
 
-int64_t oracle_points_batch(const oracle_point* p, int64_t n, oracle_yield* out, int32_t nthreads) {
-  ztab_init();
+int oracle_point_yields_z(const oracle_point* p, int64_t nz, double z_max, oracle_yield* o) {
+  ztab_t own;
+  const ztab_t* zt = ztab_get(nz, z_max, &own);
+  int r = point_yields(p, zt, o);
+  ztab_put(zt);
+  return r;
+}
+
+int oracle_point_yields(const oracle_point* p, oracle_yield* o) {
+  return oracle_point_yields_z(p, ORACLE_NZ, ORACLE_ZMAX, o);
+}
+
+int64_t oracle_points_batch_z(const oracle_point* p, int64_t n, int64_t nz, double z_max, oracle_yield* out,
+                              int32_t nthreads) {
+  ztab_t own;
+  const ztab_t* zt = ztab_get(nz, z_max, &own);
   int64_t bad = 0;
 #ifdef _OPENMP
   if (nthreads > 0) omp_set_num_threads(nthreads);
@@ -246,12 +324,17 @@ int64_t oracle_points_batch(const oracle_point* p, int64_t n, oracle_yield* out,
 #endif
 #pragma omp parallel for schedule(dynamic, 1) reduction(+ : bad)
   for (int64_t i = 0; i < n; i++) {
-    if (oracle_point_yields(&p[i], &out[i]) != 0) {
+    if (point_yields(&p[i], zt, &out[i]) != 0) {
       bad++;
       memset(&out[i], 0xff, sizeof(oracle_yield)); /* NaN pattern */
     }
   }
+  ztab_put(zt);
   return bad;
+}
+
+int64_t oracle_points_batch(const oracle_point* p, int64_t n, oracle_yield* out, int32_t nthreads) {
+  return oracle_points_batch_z(p, n, ORACLE_NZ, ORACLE_ZMAX, out, nthreads);
 }
 
 /* fpy:183-184 */
@@ -281,9 +364,9 @@ double oracle_j_chi(const oracle_point* p, double T) {
  * coefficients of CubicHermiteSpline).  The tridiagonal solve is Thomas elimination
  * (scipy: LAPACK gbsv with partial pivoting; the two agree to rounding).  coef[4k+0..3] =
  * c[0..3][k], the PPoly coefficients of interval k (value c0 s^3 + c1 s^2 + c2 s + c3). */
-static void spline_notaknot(const double* x, const double* y, double* coef) {
-  const int n = ODE_NT;
-  double dx[ODE_NT], slope[ODE_NT], cp[ODE_NT], dp[ODE_NT], s[ODE_NT];
+static void spline_notaknot(const double* x, const double* y, int n, double* coef) {
+  double* buf = (double*)malloc(sizeof(double) * 5 * (size_t)n);
+  double *dx = buf, *slope = buf + n, *cp = buf + 2 * n, *dp = buf + 3 * n, *s = buf + 4 * n;
   for (int k = 0; k + 1 < n; k++) {
     dx[k] = x[k + 1] - x[k];
     slope[k] = (y[k + 1] - y[k]) / dx[k];
@@ -317,31 +400,56 @@ static void spline_notaknot(const double* x, const double* y, double* coef) {
     coef[4 * k + 2] = s[k];
     coef[4 * k + 3] = y[k];
   }
+  free(buf);
+}
+
+/* build_tables(T_lo, T_hi, n=nt) with self.aov on the grid zt. */
+static int ode_tables(const oracle_point* p, const ztab_t* zt, double T_lo, double T_hi, int nt, double* coef) {
+  size_t nzb = (size_t)(zt->nz > 1 ? zt->nz : 1);
+  double* Ts = (double*)malloc(sizeof(double) * 2 * (size_t)nt);
+  double* Av = Ts + nt;
+  double* f = (double*)malloc(sizeof(double) * 2 * nzb);
+  double* scratch = f + nzb;
+  int rc = 0;
+  oracle_linspace(T_lo, T_hi, nt, Ts);
+  for (int k = 0; k + 1 < nt; k++)
+    if (!(Ts[k + 1] > Ts[k])) rc = -1; /* CubicSpline: `x` must be strictly increasing */
+  if (rc == 0) {
+    aov_t a = aov_make(p->I_p, p->beta_over_H, p->T_p_GeV, p->v_w, p->g_star);
+    for (int k = 0; k < nt; k++) {
+      double y = y_of_T(Ts[k], p->T_p_GeV, p->beta_over_H);
+      Av[k] = pymax(aov_eval(&a, zt, y, f, scratch), 0.0); /* np.maximum(Av, 0.0) */
+    }
+    spline_notaknot(Ts, Av, nt, coef);
+  }
+  free(Ts);
+  free(f);
+  return rc;
+}
+
+int oracle_ode_tables_z(const oracle_point* p, double T_lo, double T_hi, int32_t nt, int64_t nz, double z_max,
+                        double* coef) {
+  if (nt < 4) return -2;
+  ztab_t own;
+  const ztab_t* zt = ztab_get(nz, z_max, &own);
+  int rc = ode_tables(p, zt, T_lo, T_hi, nt, coef);
+  ztab_put(zt);
+  return rc;
 }
 
 int oracle_ode_tables(const oracle_point* p, double T_lo, double T_hi, double* coef) {
-  ztab_init();
-  double Ts[ODE_NT], Av[ODE_NT], f[ORACLE_NZ], scratch[ORACLE_NZ];
-  oracle_linspace(T_lo, T_hi, ODE_NT, Ts);
-  for (int k = 0; k + 1 < ODE_NT; k++)
-    if (!(Ts[k + 1] > Ts[k])) return -1; /* CubicSpline: `x` must be strictly increasing */
-  aov_t a = aov_make(p->I_p, p->beta_over_H, p->T_p_GeV, p->v_w, p->g_star);
-  for (int k = 0; k < ODE_NT; k++) {
-    double y = y_of_T(Ts[k], p->T_p_GeV, p->beta_over_H);
-    Av[k] = pymax(aov_eval(&a, y, f, scratch), 0.0); /* np.maximum(Av, 0.0) */
-  }
-  spline_notaknot(Ts, Av, coef);
-  return 0;
+  return oracle_ode_tables_z(p, T_lo, T_hi, ODE_NT, ORACLE_NZ, ORACLE_ZMAX, coef);
 }
 
 /* fpy:214-218 A_over_V_T: clamp T into [T_lo, T_hi], evaluate the PPoly (scipy _ppoly:
  * interval k with x[k] <= T < x[k+1], T == x[-1] in the last one; value accumulated as
  * c3 + c2 s + c1 s^2 + c0 s^3, powers by repeated multiplication). */
-double oracle_ode_aov_T(const double* coef, double T_lo, double T_hi, double T) {
-  double Ts[ODE_NT];
-  oracle_linspace(T_lo, T_hi, ODE_NT, Ts);
+static double ode_aov_T(const double* coef, int nt, double T_lo, double T_hi, double T) {
+  double stackbuf[ODE_NT]; /* main()'s tables (the integrator's rhs) need no allocation */
+  double* Ts = nt <= ODE_NT ? stackbuf : (double*)malloc(sizeof(double) * (size_t)nt);
+  oracle_linspace(T_lo, T_hi, nt, Ts);
   double Tq = pymin(pymax(T, T_lo), T_hi);
-  int lo = 0, hi = ODE_NT - 1; /* largest k <= n-2 with Ts[k] <= Tq */
+  int lo = 0, hi = nt - 1; /* largest k <= n-2 with Ts[k] <= Tq */
   while (hi - lo > 1) {
     int mid = (lo + hi) / 2;
     if (Ts[mid] <= Tq) lo = mid;
@@ -349,6 +457,7 @@ double oracle_ode_aov_T(const double* coef, double T_lo, double T_hi, double T) 
   }
   const double* c = coef + 4 * lo;
   double s = Tq - Ts[lo];
+  if (Ts != stackbuf) free(Ts);
   double z = s, res = c[3];
   res = res + c[2] * z;
   z = z * s;
@@ -358,11 +467,20 @@ double oracle_ode_aov_T(const double* coef, double T_lo, double T_hi, double T) 
   return res;
 }
 
+double oracle_ode_aov_T_n(const double* coef, int32_t nt, double T_lo, double T_hi, double T) {
+  return ode_aov_T(coef, nt, T_lo, T_hi, T);
+}
+
+double oracle_ode_aov_T(const double* coef, double T_lo, double T_hi, double T) {
+  return ode_aov_T(coef, ODE_NT, T_lo, T_hi, T);
+}
+
 typedef struct {
   const oracle_point* p;
   const oracle_ode* o;
   const double* coef;
   double T_lo, T_hi;
+  int nt;
 } ode_ctx;
 
 /* fpy:270-286 rhs(x, Y), plus the diagonal of its Jacobian (the two equations decouple). */
@@ -376,7 +494,7 @@ static void ode_rhs(const ode_ctx* c, double x, const double Y[2], double dY[2],
   double q = y / pymax(p->source_shape_sigma_y, 1e-6);
   double window = exp(-0.5 * (q * q));
   double J_chi = p->incident_flux_scale * (0.25 * n_chi_eq(T, m, p->g_chi, p->stats) * vbar_chi(T, m));
-  double SB = p->P_chi_to_B * J_chi * oracle_ode_aov_T(c->coef, c->T_lo, c->T_hi, T) * window;
+  double SB = p->P_chi_to_B * J_chi * ode_aov_T(c->coef, c->nt, c->T_lo, c->T_hi, T) * window;
   double sigmav = pymax(c->o->sigma_v_chi_GeV_m2, 0.0);
   double Yeq = n_chi_eq(T, m, p->g_chi, p->stats) / s;
   double SB_term = c->o->deplete_DM_from_source ? (SB / s) : 0.0;
@@ -388,11 +506,16 @@ static void ode_rhs(const ode_ctx* c, double x, const double Y[2], double dY[2],
   J[1] = (-gamma_w * H) / Hx;
 }
 
-void oracle_ode_rhs(const oracle_point* p, const oracle_ode* o, const double* coef, double T_lo, double T_hi,
-                    double x, const double* Y, double* dY) {
-  ode_ctx c = {p, o, coef, T_lo, T_hi};
+void oracle_ode_rhs_n(const oracle_point* p, const oracle_ode* o, const double* coef, int32_t nt, double T_lo,
+                      double T_hi, double x, const double* Y, double* dY) {
+  ode_ctx c = {p, o, coef, T_lo, T_hi, nt};
   double J[2];
   ode_rhs(&c, x, Y, dY, J);
+}
+
+void oracle_ode_rhs(const oracle_point* p, const oracle_ode* o, const double* coef, double T_lo, double T_hi,
+                    double x, const double* Y, double* dY) {
+  oracle_ode_rhs_n(p, o, coef, ODE_NT, T_lo, T_hi, x, Y, dY);
 }
 
 /* 3x3 solve with partial pivoting (M is overwritten). */
@@ -476,15 +599,15 @@ static int radau_step(const ode_ctx* c, const double C[3], const double A[3][3],
 
 /* fpy:361-417 for a point on the ODE path; status 0 ok, 1 bad T grid (CubicSpline raises),
  * 2 max_step <= 0 (solve_ivp raises), 3 more than max_steps steps, 4 Newton failure. */
-int oracle_ode_point(const oracle_point* p, const oracle_ode* o, int64_t max_steps, oracle_yield* out,
-                     int64_t* n_steps) {
+static int ode_point(const oracle_point* p, const oracle_ode* o, const ztab_t* zt, int64_t max_steps,
+                     oracle_yield* out, int64_t* n_steps) {
   double T_p = p->T_p_GeV, m = p->m_chi_GeV;
   double T_hi = p->T_max_over_Tp * T_p, T_lo = p->T_min_over_Tp * T_p;
   double* coef = (double*)malloc(sizeof(double) * 4 * ODE_NT);
   int st = 0;
   *n_steps = 0;
   memset(out, 0xff, sizeof(*out)); /* NaN unless filled */
-  if (oracle_ode_tables(p, T_lo, T_hi, coef) != 0) {
+  if (ode_tables(p, zt, T_lo, T_hi, ODE_NT, coef) != 0) {
     free(coef);
     return 1;
   }
@@ -512,7 +635,7 @@ int oracle_ode_point(const oracle_point* p, const oracle_ode* o, int64_t max_ste
   double h = (x1 - x0) / (double)N;
   double C[3], A[3][3];
   radau_tableau(C, A);
-  ode_ctx c = {p, o, coef, T_lo, T_hi};
+  ode_ctx c = {p, o, coef, T_lo, T_hi, ODE_NT};
   double Y[2] = {Ychi0, 0.0};
   /* n_chi_eq / vbar_chi switch formula at the strict T > m/3 (fpy:100, 111): the rhs jumps at
    * the first x whose T = m/max(x, 1e-30) is not > m/3.  A step that straddles that point is
@@ -554,6 +677,20 @@ int oracle_ode_point(const oracle_point* p, const oracle_ode* o, int64_t max_ste
   out->DM_over_B = rhoDM / pymax(rhoB, 1e-300);
   out->P_used = p->P_chi_to_B;
   return st;
+}
+
+int oracle_ode_point_z(const oracle_point* p, const oracle_ode* o, int64_t nz, double z_max, int64_t max_steps,
+                       oracle_yield* out, int64_t* n_steps) {
+  ztab_t own;
+  const ztab_t* zt = ztab_get(nz, z_max, &own);
+  int r = ode_point(p, o, zt, max_steps, out, n_steps);
+  ztab_put(zt);
+  return r;
+}
+
+int oracle_ode_point(const oracle_point* p, const oracle_ode* o, int64_t max_steps, oracle_yield* out,
+                     int64_t* n_steps) {
+  return oracle_ode_point_z(p, o, ORACLE_NZ, ORACLE_ZMAX, max_steps, out, n_steps);
 }
 
 int64_t oracle_ode_batch(const oracle_point* p, const oracle_ode* o, int64_t n, int64_t max_steps, oracle_yield* out,

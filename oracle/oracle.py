@@ -66,6 +66,14 @@ def lib():
         L.oracle_pairwise_sum.argtypes = [P(d), i64]
         L.oracle_linspace.restype = None
         L.oracle_linspace.argtypes = [d, d, i64, P(d)]
+        L.oracle_aov_z.restype = d
+        L.oracle_aov_z.argtypes = [d, d, d, d, d, d, i64, d]
+        L.oracle_yb_quadrature_z.restype = d
+        L.oracle_yb_quadrature_z.argtypes = [P(OraclePoint), d, d, i32, i64, d]
+        L.oracle_point_yields_z.restype = ctypes.c_int
+        L.oracle_point_yields_z.argtypes = [P(OraclePoint), i64, d, P(OracleYield)]
+        L.oracle_points_batch_z.restype = i64
+        L.oracle_points_batch_z.argtypes = [P(OraclePoint), i64, i64, d, P(OracleYield), i32]
         _lib = L
     return _lib
 
@@ -87,26 +95,36 @@ def point_from_config(cfg: dict) -> OraclePoint:
     return p
 
 
-def point_yields(cfg: dict) -> dict:
+NZ, Z_MAX = 1200, 30.0   # fpy:142 defaults, main()'s grid (fpy:197)
+
+
+def point_yields(cfg: dict, nz: int = NZ, z_max: float = Z_MAX) -> dict:
+    """main()'s fast path (fpy:361-417) for one config, A/V on AoverVKernel(..., z_max, nz)."""
     p = point_from_config(cfg)
     o = OracleYield()
-    rc = lib().oracle_point_yields(ctypes.byref(p), ctypes.byref(o))
+    rc = lib().oracle_point_yields_z(ctypes.byref(p), int(nz), float(z_max), ctypes.byref(o))
     if rc != 0:
         raise UnboundLocalError("local variable 'Ychi_fin' referenced before assignment")
     return {n: getattr(o, n) for n in YIELD_FIELDS}
 
 
-def points_batch(cfgs: list[dict], nthreads: int = 0) -> np.ndarray:
+def points_batch(cfgs: list[dict], nthreads: int = 0, nz: int = NZ, z_max: float = Z_MAX) -> np.ndarray:
     """Returns an (n, 6) float64 array in YIELD_FIELDS order (NaN rows for failed points)."""
     n = len(cfgs)
     arr = (OraclePoint * n)(*[point_from_config(c) for c in cfgs])
     out = (OracleYield * n)()
-    lib().oracle_points_batch(arr, n, out, int(nthreads))
+    lib().oracle_points_batch_z(arr, n, int(nz), float(z_max), out, int(nthreads))
     return np.frombuffer(out, dtype=np.float64).reshape(n, 6).copy()
 
 
-def aov(I_p, beta_over_H, T_p, v_w, g_star, y) -> float:
-    return lib().oracle_aov(I_p, beta_over_H, T_p, v_w, g_star, y)
+def yb_quadrature(cfg: dict, T_lo: float, T_hi: float, n_y: int = 8000, nz: int = NZ, z_max: float = Z_MAX) -> float:
+    """BoltzmannSystem.integrate_YB_by_quadrature (fpy:231-267) with bs.aov on (nz, z_max)."""
+    p = point_from_config(cfg)
+    return lib().oracle_yb_quadrature_z(ctypes.byref(p), float(T_lo), float(T_hi), int(n_y), int(nz), float(z_max))
+
+
+def aov(I_p, beta_over_H, T_p, v_w, g_star, y, nz: int = NZ, z_max: float = Z_MAX) -> float:
+    return lib().oracle_aov_z(I_p, beta_over_H, T_p, v_w, g_star, y, int(nz), float(z_max))
 
 
 def p_closed_form(lam: float) -> float:
@@ -154,6 +172,14 @@ def _ode_lib():
         L.oracle_ode_point.argtypes = [P(OraclePoint), P(OracleOde), i64, P(OracleYield), P(i64)]
         L.oracle_ode_batch.restype = i64
         L.oracle_ode_batch.argtypes = [P(OraclePoint), P(OracleOde), i64, i64, P(OracleYield), P(i32), i32]
+        L.oracle_ode_tables_z.restype = ctypes.c_int
+        L.oracle_ode_tables_z.argtypes = [P(OraclePoint), d, d, i32, i64, d, P(d)]
+        L.oracle_ode_aov_T_n.restype = d
+        L.oracle_ode_aov_T_n.argtypes = [P(d), i32, d, d, d]
+        L.oracle_ode_rhs_n.restype = None
+        L.oracle_ode_rhs_n.argtypes = [P(OraclePoint), P(OracleOde), P(d), i32, d, d, d, P(d), P(d)]
+        L.oracle_ode_point_z.restype = ctypes.c_int
+        L.oracle_ode_point_z.argtypes = [P(OraclePoint), P(OracleOde), i64, d, i64, P(OracleYield), P(i64)]
         L._ode_ready = True
     return L
 
@@ -206,10 +232,36 @@ def ode_aov_T(cfg: dict, T: float) -> float:
     return L.oracle_ode_aov_T(coef.ctypes.data_as(dp), T_lo, T_hi, float(T))
 
 
-def ode_point(cfg: dict, max_steps: int = 1 << 26) -> dict:
+class OdeTables:
+    """build_tables(T_lo, T_hi, n=nt) with bs.aov on (nz, z_max) (fpy:207-212), then A_over_V_T
+    (fpy:214-218) and rhs (fpy:270-286) on them."""
+
+    def __init__(self, cfg: dict, T_lo: float, T_hi: float, nt: int = ODE_NT, nz: int = NZ, z_max: float = Z_MAX):
+        self.p, self.o = point_from_config(cfg), ode_from_config(cfg)
+        self.T_lo, self.T_hi, self.nt = float(T_lo), float(T_hi), int(nt)
+        self.coef = np.zeros(4 * self.nt)
+        rc = _ode_lib().oracle_ode_tables_z(ctypes.byref(self.p), self.T_lo, self.T_hi, self.nt, int(nz), float(z_max),
+                                            self.coef.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+        if rc != 0:
+            raise ValueError("`x` must be strictly increasing sequence.")
+
+    def aov_T(self, T: float) -> float:
+        return _ode_lib().oracle_ode_aov_T_n(self.coef.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), self.nt,
+                                             self.T_lo, self.T_hi, float(T))
+
+    def rhs(self, x: float, Y) -> tuple:
+        dp = ctypes.POINTER(ctypes.c_double)
+        Yv = np.asarray(Y, dtype=np.float64)
+        dY = np.zeros(2)
+        _ode_lib().oracle_ode_rhs_n(ctypes.byref(self.p), ctypes.byref(self.o), self.coef.ctypes.data_as(dp), self.nt,
+                                    self.T_lo, self.T_hi, float(x), Yv.ctypes.data_as(dp), dY.ctypes.data_as(dp))
+        return float(dY[0]), float(dY[1])
+
+
+def ode_point(cfg: dict, max_steps: int = 1 << 26, nz: int = NZ, z_max: float = Z_MAX) -> dict:
     p, o, out, ns = point_from_config(cfg), ode_from_config(cfg), OracleYield(), ctypes.c_int64()
-    st = _ode_lib().oracle_ode_point(ctypes.byref(p), ctypes.byref(o), int(max_steps), ctypes.byref(out),
-                                     ctypes.byref(ns))
+    st = _ode_lib().oracle_ode_point_z(ctypes.byref(p), ctypes.byref(o), int(nz), float(z_max), int(max_steps),
+                                       ctypes.byref(out), ctypes.byref(ns))
     r = {n: getattr(out, n) for n in YIELD_FIELDS}
     r["status"], r["n_steps"] = st, ns.value
     return r

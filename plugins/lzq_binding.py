@@ -8,13 +8,15 @@ buffers come from hipMalloc through ctypes, and every number is computed by libl
     lzq_binding.install(first_principles_yields)   # BoltzmannSystem.integrate_YB_by_quadrature -> GPU
 
 Entry points (each cites the fpy code it replaces):
-  integrate_YB_by_quadrature(self, T_lo, T_hi, n_y=6000)  fpy:231-267 (method replacement)
-  yields(cfg, P, T_lo=None, T_hi=None, n_y=8000)          fpy:231-267 + fpy:372-384 + fpy:413-417
+  integrate_YB_by_quadrature(self, T_lo, T_hi, n_y=6000)  fpy:231-267 (method replacement; self.aov's z grid)
+  A_over_V_y(self, y)                                     fpy:158-165 (AoverVKernel method replacement, any z grid)
+  yields(cfg, P, T_lo=None, T_hi=None, n_y=8000, nz=1200, z_max=30.0)
+                                                          fpy:231-267 + fpy:372-384 + fpy:413-417
   p_closed_form(lams)                                     fpy:183-184
   lz_propagate(m_mix, dprime, xi, v_w, window_lz, steps)  no fpy counterpart (north_star (1))
   profile_crossings(knots, phi, Phi, y_B, y_chi, lam, v_w)  PAPER eqs.(5)-(8) (the absent modules of fpy:173)
   lz_propagate_profile(knots, phi, Phi, y_B, y_chi, lam, v_w) time-ordered P through a bounce profile
-  install(fpy_module)                                     monkey-patches fpy's BoltzmannSystem
+  install(fpy_module)                                     monkey-patches fpy's BoltzmannSystem and AoverVKernel
 
 The library is found at $LZQ_LIB, else at <repo>/<package>/_build/liblzq.so next to this
 file's directory.  Failures raise RuntimeError with lzq_last_error(); there is no CPU path.
@@ -70,7 +72,8 @@ def _libs():
         hip.hipGetDevice.argtypes = [ctypes.POINTER(ctypes.c_int)]
         L.lzq_last_error.restype = ctypes.c_char_p
         L.lzq_init.argtypes = [ctypes.c_int]
-        L.lzq_yields_batch.argtypes = [vp, i64, i32, vp, vp, vp, vp, vp]
+        L.lzq_yields_batch.argtypes = [vp, i64, i32, i32, d, vp, vp, vp, vp, vp]
+        L.lzq_aov_batch.argtypes = [ctypes.POINTER(lzq_point), vp, i64, i32, d, vp, vp]
         L.lzq_p_closed_form.argtypes = [vp, i64, vp, vp]
         L.lzq_lz_propagate.argtypes = [vp, vp, vp, i64, i32, d, d, i32, vp, vp]
         L.lzq_profile_splines.argtypes = [vp, vp, vp, i32, i32, vp, vp, vp]
@@ -135,24 +138,49 @@ def point_from_cfg(c, P: float) -> lzq_point:
                      int(c.Y_chi_init is not None), int(c.n_chi_at_Tp_GeV3 is not None))
 
 
-def yields(cfg, P: float, T_lo=None, T_hi=None, n_y: int = 8000) -> dict:
+def yields(cfg, P: float, T_lo=None, T_hi=None, n_y: int = 8000, nz: int = 1200, z_max: float = 30.0) -> dict:
     """fpy:231-267 (Y_B) + fpy:372-384, 413-417 (Y_chi, densities) for one config on the GPU
-    (T_lo/T_hi default to main()'s window, fpy:367-369)."""
+    (T_lo/T_hi default to main()'s window, fpy:367-369), A/V on the z grid linspace(0, z_max, nz)
+    (fpy:141-156)."""
     _, L = _libs()
     pt = point_from_cfg(cfg, P)
     out = lzq_yield()
     tl, th = ctypes.c_double(T_lo or 0.0), ctypes.c_double(T_hi or 0.0)
     with _Dev(136, pt) as d_pt, _Dev(8, tl) as d_tl, _Dev(8, th) as d_th, _Dev(48) as d_out:
-        _check(L.lzq_yields_batch(d_pt.p, 1, int(n_y), d_tl.p if T_lo is not None else None,
+        _check(L.lzq_yields_batch(d_pt.p, 1, int(n_y), int(nz), float(z_max), d_tl.p if T_lo is not None else None,
                                   d_th.p if T_hi is not None else None, None, d_out.p, None))
         d_out.read(out)
     return {n: getattr(out, n) for n, _ in lzq_yield._fields_}
 
 
+def zgrid_of(aov) -> tuple:
+    """(nz, z_max) of a reference AoverVKernel from its z array (fpy:154: linspace sets
+    z[-1] = z_max exactly; with fewer than 2 nodes A/V is 0 whatever z_max is)."""
+    z = aov.z
+    nz = len(z)
+    return nz, (float(z[-1]) if nz >= 2 else 0.0)
+
+
 def integrate_YB_by_quadrature(self, T_lo: float, T_hi: float, n_y: int = 6000) -> float:
     """Drop-in for BoltzmannSystem.integrate_YB_by_quadrature (fpy:231-267): same arguments,
-    same result (north_star tolerance 1e-8; measured ~1e-13), computed by lzq_yields_batch."""
-    return yields(self.cfg, self.P, T_lo, T_hi, n_y)["Y_B"]
+    same result (north_star tolerance 1e-8; measured ~1e-13), computed by lzq_yields_batch on
+    self.aov's z grid (any AoverVKernel(..., z_max, nz))."""
+    nz, z_max = zgrid_of(self.aov)
+    return yields(self.cfg, self.P, T_lo, T_hi, n_y, nz, z_max)["Y_B"]
+
+
+def A_over_V_y(self, y: float) -> float:
+    """Drop-in for AoverVKernel.A_over_V_y (fpy:158-165) on the kernel's own z grid
+    (lzq_aov_batch).  Reads I_p, beta_over_H, T_p, v_w and g_star from the kernel object."""
+    _, L = _libs()
+    nz, z_max = zgrid_of(self)
+    pt = lzq_point()
+    pt.I_p, pt.beta_over_H, pt.T_p_GeV, pt.v_w, pt.g_star = self.I_p, self.beta_over_H, self.T_p, self.v_w, self.g_star
+    yv, out = ctypes.c_double(float(y)), ctypes.c_double()
+    with _Dev(8, yv) as d_y, _Dev(8) as d_out:
+        _check(L.lzq_aov_batch(ctypes.byref(pt), d_y.p, 1, nz, z_max, d_out.p, None))
+        d_out.read(out)
+    return out.value
 
 
 def p_closed_form(lams) -> list:
@@ -246,5 +274,7 @@ def lz_propagate_profile(knots, phi, Phi, y_B, y_chi, lambda_tr_eff, v_w, steps_
 
 
 def install(fpy_module) -> None:
-    """Route the reference's quadrature operator through the GPU."""
+    """Route the reference's quadrature operator and its A/V kernel through the GPU
+    (INTEGRATION.md §2)."""
     fpy_module.BoltzmannSystem.integrate_YB_by_quadrature = integrate_YB_by_quadrature
+    fpy_module.AoverVKernel.A_over_V_y = A_over_V_y

@@ -30,7 +30,7 @@ def test_library_builds_and_exports_header_symbols():
 def test_abi_version_and_struct_layout():
     n = pkg("_native")
     L = n.load()
-    assert L.lzq_abi_version() == pkg("_native").ABI_VERSION == 1
+    assert L.lzq_abi_version() == pkg("_native").ABI_VERSION == 2
     assert ctypes.sizeof(n.LzqPoint) == 136 and ctypes.sizeof(n.LzqYield) == 48
 
 
@@ -46,11 +46,58 @@ def test_ztables_match_reference_grid():
     assert abs(om.sum() - 2.0) < 1e-8
 
 
+ZGRIDS = [(600, 30.0), (2400, 30.0), (12000, 30.0), (1200, 20.0), (1200, 60.0), (2400, 60.0), (37, 7.5)]
+
+
+def test_ztables_runtime_grids():
+    """AoverVKernel(..., z_max, nz) (fpy:141-156) for any grid: the library's host tables are
+    numpy's linspace bit for bit, gamma4 the cancelling form to a few eps, and the weights
+    integrate z^2 e^-z over [0, z_max] to the trapezoid's accuracy."""
+    nat = pkg("_native")
+    for nz, zmax in ZGRIDS:
+        z, g4, om = nat.ztables(nz, zmax)
+        assert np.array_equal(z, np.linspace(0.0, zmax, nz)), (nz, zmax)
+        ez = np.exp(-z)
+        g4_np = 6.0 - ez * (z ** 3 + 3.0 * z ** 2 + 6.0 * z + 6.0)
+        assert np.max(np.abs(g4 - g4_np)) <= 16 * np.finfo(float).eps, (nz, zmax)   # 2 ulp(6)
+        f = z * z * ez
+        assert abs(om.sum() - np.trapezoid(f, z)) <= 1e-13, (nz, zmax)
+    # numpy's degenerate grids: no node / one node / zero width -> A/V = 0 (empty trapezoid)
+    for nz, zmax in ((0, 30.0), (1, 30.0), (5, 0.0)):
+        z, g4, om = nat.ztables(nz, zmax)
+        assert np.array_equal(z, np.linspace(0.0, zmax, nz)) and not np.any(om), (nz, zmax)
+
+
+def test_ztables_refuse_bad_grids():
+    """nz < 0 is numpy's ValueError; non-finite / negative z_max and grids so fine that the
+    cancelling gamma4 of fpy:156 rounds below 0 are refused (LZQ_EINVAL) before any GPU work."""
+    import pytest
+    nat = pkg("_native")
+    L = nat.load()
+    for nz, zmax, msg in ((-1, 30.0, b"non-negative"), (1200, float("nan"), b"finite"), (1200, -1.0, b"finite"),
+                          (1200, float("inf"), b"finite"), (nat.LZQ_NZ_MAX + 1, 30.0, b"LZQ_NZ_MAX"),
+                          (2_000_000, 30.0, b"gamma4")):
+        assert L.lzq_ztables(nz, zmax, None, None, None) == -1, (nz, zmax)
+        assert msg in L.lzq_last_error(), (nz, zmax, L.lzq_last_error())
+    with pytest.raises(ValueError, match="non-negative"):
+        nat.zgrid(-3, 30.0)
+    with pytest.raises(TypeError):
+        nat.zgrid(1200.0, 30.0)   # numpy.linspace: 'float' object cannot be interpreted as an integer
+    assert nat.zgrid(np.int64(600), 20) == (600, 20.0)
+
+
 def test_host_side_argument_validation():
     n = pkg("_native")
     L = n.load()
-    rc = L.lzq_yields_batch(None, -1, 8000, None, None, None, None, None)
+    rc = L.lzq_yields_batch(None, -1, 8000, 1200, 30.0, None, None, None, None, None)
     assert rc == -1 and b"bad arguments" in L.lzq_last_error()
+    rc = L.lzq_aov_batch(None, None, 1, 1200, 30.0, None, None)
+    assert rc == -1 and b"bad arguments" in L.lzq_last_error()
+    assert L.lzq_ode_tables(8, 1, None, None, 3, 1200, 30.0, 8, 12, None, None) == -1   # nt < 4
+    assert b"nt = 3" in L.lzq_last_error()
+    assert L.lzq_ode_tables(8, 2, None, None, 100, 1200, 30.0, 8, 799, None, None) == -1  # < 2 x 4 nt
+    assert b"workspace" in L.lzq_last_error()
+    assert L.lzq_ode_aov_T(None, 1.0, 2.0, 800, None, None, 1, None, None) == -1
     rc = L.lzq_p_closed_form(None, 0, None, None)  # n == 0 is a no-op
     assert rc == 0
     rc = L.lzq_lz_propagate(None, None, None, 4, 0, 0.3, 1.0, 10, None, None)
@@ -67,16 +114,16 @@ def test_host_side_argument_validation():
     base = cfgm.to_ctypes_point(cfgm.to_point({**cfgm.default_config(), "P_chi_to_B": 0.1}))
     ax = (n.LzqAxis * 1)()
     ax[0].field, ax[0].n, ax[0].values = 99, 3, 8
-    rc = L.lzq_sweep_grid(ctypes.byref(base), ax, 1, 0, 1, 8000, None, 8, None)
+    rc = L.lzq_sweep_grid(ctypes.byref(base), ax, 1, 0, 1, 8000, 1200, 30.0, None, 8, None)
     assert rc == -1 and b"unknown field" in L.lzq_last_error()
     ax[0].field = n.FIELD["m_mix"]
-    rc = L.lzq_sweep_grid(ctypes.byref(base), ax, 1, 0, 1, 8000, None, 8, None)
+    rc = L.lzq_sweep_grid(ctypes.byref(base), ax, 1, 0, 1, 8000, 1200, 30.0, None, 8, None)
     assert rc == -1 and b"swept together" in L.lzq_last_error()
     ax[0].field = n.FIELD["I_p"]
-    rc = L.lzq_sweep_grid(ctypes.byref(base), ax, 1, 2, 5, 8000, None, 8, None)
+    rc = L.lzq_sweep_grid(ctypes.byref(base), ax, 1, 2, 5, 8000, 1200, 30.0, None, 8, None)
     assert rc == -1 and b"outside grid" in L.lzq_last_error()
     base.regime = n.REGIME_OTHER
-    rc = L.lzq_sweep_grid(ctypes.byref(base), ax, 1, 0, 1, 8000, None, 8, None)
+    rc = L.lzq_sweep_grid(ctypes.byref(base), ax, 1, 0, 1, 8000, 1200, 30.0, None, 8, None)
     assert rc == -3
 
 
@@ -126,7 +173,7 @@ def test_tune_ode_coop_knob():
 
 
 def test_sweep_grid_reuse_workspace_and_validation():
-    """lzq_sweep_grid_reuse_workspace: one table of max(n_y, 2000) + 4 doubles per combination of
+    """lzq_sweep_grid_reuse_workspace: one table of max(n_y, 2000) + 6 doubles per combination of
     the grid's I_p / beta_over_H / T_p / T_min / T_max values; lzq_sweep_grid_reuse refuses a
     smaller workspace (no GPU work is launched on these paths)."""
     n = pkg("_native")
@@ -144,14 +191,15 @@ def test_sweep_grid_reuse_workspace_and_validation():
     specs = sw.builtin_specs()
     for name, tables in (("C2", 1), ("C3", 100), ("C4", 1000)):
         spec = specs[name]
-        assert L.lzq_sweep_grid_reuse_workspace(axes_of(spec), len(spec.axes), 8000) == tables * 8004, name
-        assert L.lzq_sweep_grid_reuse_workspace(axes_of(spec), len(spec.axes), 100) == tables * 2004, name
+        assert L.lzq_sweep_grid_reuse_workspace(axes_of(spec), len(spec.axes), 8000) == tables * 8006, name
+        assert L.lzq_sweep_grid_reuse_workspace(axes_of(spec), len(spec.axes), 100) == tables * 2006, name
     spec = specs["C3"]
     base = cfgm.to_ctypes_point(cfgm.to_point({**cfgm.default_config(), "P_chi_to_B": 0.1}))
-    rc = L.lzq_sweep_grid_reuse(ctypes.byref(base), axes_of(spec), len(spec.axes), 0, 10, 8000, None, 8, 100 * 8004 - 1,
-                                8, None)
+    rc = L.lzq_sweep_grid_reuse(ctypes.byref(base), axes_of(spec), len(spec.axes), 0, 10, 8000, 1200, 30.0, None, 8,
+                                100 * 8006 - 1, 8, None)
     assert rc < 0 and b"workspace" in L.lzq_last_error()
-    rc = L.lzq_sweep_grid_reuse(ctypes.byref(base), axes_of(spec), len(spec.axes), 0, 0, 8000, None, None, 0, None, None)
+    rc = L.lzq_sweep_grid_reuse(ctypes.byref(base), axes_of(spec), len(spec.axes), 0, 0, 8000, 1200, 30.0, None, None, 0,
+                                None, None)
     assert rc == 0   # empty range: nothing to do
 
 
@@ -165,8 +213,8 @@ def test_new_entry_points_validate_arguments():
     rc = L.lzq_lz_propagate_v(8, 8, 8, 8, 4, 1, 300.0, 1000, 8, None)          # window too wide
     assert rc < 0 and b"window_lz <= 200" in L.lzq_last_error()
     assert L.lzq_lz_propagate_v(None, None, None, None, 0, 1, 20.0, 1000, None, None) == 0
-    rc = L.lzq_yields_batch_reuse(8, 4, 8000, None, None, 8, 1, 8, 10 ** 6, 8, None)   # no rep array
+    rc = L.lzq_yields_batch_reuse(8, 4, 8000, 1200, 30.0, None, None, 8, 1, 8, 10 ** 6, 8, None)   # no rep array
     assert rc < 0 and b"lzq_yields_batch_reuse" in L.lzq_last_error()
-    rc = L.lzq_yields_batch_reuse(8, 4, 8000, None, 8, 8, 2, 8, 2 * 8004 - 1, 8, None)  # workspace short
+    rc = L.lzq_yields_batch_reuse(8, 4, 8000, 1200, 30.0, None, 8, 8, 2, 8, 2 * 8006 - 1, 8, None)  # workspace short
     assert rc < 0 and b"workspace" in L.lzq_last_error()
-    assert L.lzq_yields_batch_reuse(None, 0, 8000, None, None, None, 0, None, 0, None, None) == 0
+    assert L.lzq_yields_batch_reuse(None, 0, 8000, 1200, 30.0, None, None, None, 0, None, 0, None, None) == 0

@@ -228,11 +228,19 @@ def test_reference_side_binding(plugin_path, gpu_engine):
     B = importlib.import_module("lzq_binding")
     cfgm = pkg("config")
 
-    class StandIn:  # the attributes of the reference's BoltzmannSystem that the binding reads (fpy:193-196)
+    import numpy as np
+
+    class KernelStandIn:  # the attributes of the reference's AoverVKernel the binding reads (fpy:141-156)
+        def __init__(self, I_p, beta_over_H, T_p, v_w, g_star, z_max=30.0, nz=1200):
+            self.I_p, self.beta_over_H, self.T_p, self.v_w, self.g_star = I_p, beta_over_H, T_p, max(v_w, 1e-12), g_star
+            self.z = np.linspace(0.0, z_max, nz)
+
+    class StandIn:  # the attributes of the reference's BoltzmannSystem that the binding reads (fpy:193-197)
         def __init__(self, cfg, P):
             self.cfg, self.P = cfg, float(P)
+            self.aov = KernelStandIn(cfg.I_p, cfg.beta_over_H, cfg.T_p_GeV, cfg.v_w, cfg.g_star)
 
-    ns = types.SimpleNamespace(BoltzmannSystem=StandIn)
+    ns = types.SimpleNamespace(BoltzmannSystem=StandIn, AoverVKernel=KernelStandIn)
     B.install(ns)
     cfg = cfgm.Config(**full_cfg(BASE_CFG))
     bs = ns.BoltzmannSystem(cfg, cfg.P_chi_to_B)
@@ -242,6 +250,14 @@ def test_reference_side_binding(plugin_path, gpu_engine):
         got = bs.integrate_YB_by_quadrature(tlo, thi, n_y=ny)
         ref = O.lib().oracle_yb_quadrature(ctypes.byref(p), tlo, thi, ny)
         assert rel_err(got, ref) < 1e-11, (tlo, thi, ny, got, ref)
+    # the operator on another z grid (bs.aov = AoverVKernel(..., z_max, nz), fpy:141-142)
+    bs.aov = ns.AoverVKernel(cfg.I_p, cfg.beta_over_H, cfg.T_p_GeV, cfg.v_w, cfg.g_star, z_max=45.0, nz=2400)
+    got = bs.integrate_YB_by_quadrature(0.1, 500.0, n_y=8000)
+    ref = O.yb_quadrature(full_cfg(BASE_CFG), 0.1, 500.0, 8000, 2400, 45.0)
+    assert rel_err(got, ref) < 1e-11, (got, ref)
+    for y in (-20.0, 0.0, 15.975, 49.0, 51.0):
+        g, r = bs.aov.A_over_V_y(y), O.aov(cfg.I_p, cfg.beta_over_H, cfg.T_p_GeV, cfg.v_w, cfg.g_star, y, 2400, 45.0)
+        assert (g == r == 0.0) or rel_err(g, r) < 1e-11, (y, g, r)
     y = B.yields(cfg, cfg.P_chi_to_B)
     assert f"{y['Y_B']:.10e}" == "8.7208853627e-11"
     d = golden("golden_lz.json")

@@ -85,3 +85,73 @@ def test_oracle_under_asan_ubsan():
                        timeout=300)
     assert r.returncode == 0, (r.stdout, r.stderr[-3000:])
     assert "ok (0 failures)" in r.stdout
+
+
+# ---- the A/V kernel's z grid: AoverVKernel(..., z_max, nz) (fpy:141-156) ----------------------
+def _zgrid_cases():
+    return golden("golden_zgrid.json")
+
+
+def test_golden_zgrid_yields():
+    """Y_B of bs.integrate_YB_by_quadrature with bs.aov = AoverVKernel(..., z_max, nz), run by the
+    reference (tests/golden/make_golden_zgrid.py) on 10 grids incl. nz = 12000 and the degenerate
+    nz <= 1 / z_max = 0 ones (A/V = 0)."""
+    d = _zgrid_cases()
+    worst = 0.0
+    for r in d["yields"]:
+        cfg = full_cfg(r["config"])
+        T_p = cfg["T_p_GeV"]
+        got = O.yb_quadrature(cfg, cfg["T_min_over_Tp"] * T_p, cfg["T_max_over_Tp"] * T_p, 8000, r["nz"], r["z_max"])
+        if r["Y_B"] == 0.0:
+            assert got == 0.0, r
+            continue
+        worst = max(worst, rel_err(got, r["Y_B"]))
+    # the cancelling gamma4 (fpy:156) inherits numpy's 1-ulp exp differences as an absolute ~7e-16,
+    # relatively larger on the finer grids' small-z nodes: measured 2.4e-13 (nz = 600) ...
+    # 2.8e-12 (nz = 12000); the guard band of the GPU golden tests, 1e-11
+    assert worst < 1e-11, worst
+    # the study the grid exists for: Y_B is not converged in nz (SURVEY §0.5)
+    base = {(r["nz"], r["z_max"]): r["Y_B"] for r in d["yields"] if r["config"] == d["yields"][0]["config"]}
+    assert base[(2400, 30.0)] / base[(600, 30.0)] > 1.6 and base[(12000, 30.0)] > base[(2400, 30.0)]
+
+
+def test_golden_zgrid_aov():
+    for case in _zgrid_cases()["aov"]:
+        c = full_cfg(case["config"])
+        for y, ref in zip(case["y"], case["Av"]):
+            got = O.aov(c["I_p"], c["beta_over_H"], c["T_p_GeV"], c["v_w"], c["g_star"], y, case["nz"], case["z_max"])
+            # gamma4's cancellation error (numpy vs libm exp, above) weighs more on finer grids:
+            # measured 2.3e-11 at nz = 12000, y = 15.975 (c = -5e5)
+            tol = TOL_AOV * max(1.0, case["nz"] / 1200)
+            assert rel_err(got, ref) < tol, (case["nz"], case["z_max"], y, got, ref)
+
+
+def test_golden_zgrid_tables_and_rhs():
+    """build_tables(T_lo, T_hi, n) for n = 50 / 200 / 800 / 1600 on three grids, then A_over_V_T and
+    rhs at sample points, against the reference's own spline (scipy CubicSpline)."""
+    for t in _zgrid_cases()["tables"]:
+        c = full_cfg(t["config"])
+        T_p = c["T_p_GeV"]
+        tab = O.OdeTables(c, c["T_min_over_Tp"] * T_p, c["T_max_over_Tp"] * T_p, t["nt"], t["nz"], t["z_max"])
+        scale = max(abs(v) for v in t["Av"])
+        for T, ref in zip(t["T"], t["Av"]):
+            assert abs(tab.aov_T(T) - ref) <= 1e-11 * abs(ref) + 1e-13 * scale, (t["nt"], T, tab.aov_T(T), ref)
+        k = 0
+        for x in t["x"]:
+            for Y in t["Y"]:
+                got, ref = tab.rhs(x, Y), t["rhs"][k]
+                k += 1
+                for g, r in zip(got, ref):
+                    assert abs(g - r) <= 1e-10 * abs(r) + 1e-300, (t["nt"], x, Y, got, ref)
+
+
+def test_golden_zgrid_ode():
+    """main()'s ODE fallback with bs.aov on non-default grids: the reference's adaptive Radau vs the
+    oracle's fixed-step Radau (narrow wash-out windows, where the reference sits ~1e-13 from its
+    converged solution)."""
+    for r in _zgrid_cases()["ode"]:
+        assert r["success"]
+        o = O.ode_point(full_cfg(r["config"]), nz=r["nz"], z_max=r["z_max"])
+        assert o["status"] == 0
+        assert rel_err(o["Y_B"], r["Y_B"]) < 1e-10, (o["Y_B"], r["Y_B"])
+        assert rel_err(o["Y_chi"], r["Y_chi"]) < 1e-10, (o["Y_chi"], r["Y_chi"])

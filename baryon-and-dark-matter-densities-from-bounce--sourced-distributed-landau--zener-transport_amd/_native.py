@@ -77,17 +77,28 @@ ODE_MAX_LAUNCHES = 65536  # lzq_ode_*: max_steps <= 65536 x 2^(launch log2)
 TUNE_STATE = {"exp": "table"}
 
 
+_loaded_path = None   # the library load() opened last (what the engines run)
+
+
 def library_id(path: str | None = None) -> str | None:
-    """sha256 (16 hex) of every gfx950 code object in the library: changes whenever any kernel's
-    machine code does (sweep.spec_key: checkpoints of another build are never mixed in)."""
+    """sha256 (16 hex) of every device code object (build.ARCH) in the library the engine loaded
+    (else `path`, else LIB_PATH): changes whenever any kernel's machine code does
+    (sweep.spec_key: checkpoints of another build are never mixed in).  A library with no such
+    uncompressed bundle entry (another arch, compressed bundles) is hashed whole, never as the
+    empty input."""
     import hashlib
     from . import codeobj
-    p = path or LIB_PATH
+    p = path or _loaded_path or LIB_PATH
     if not os.path.exists(p):
         return None
+    objs = codeobj.device_objects(p, _build.ARCH)
     h = hashlib.sha256()
-    for obj in codeobj.device_objects(p):
-        h.update(obj)
+    if objs:
+        for obj in objs:
+            h.update(obj)
+    else:
+        with open(p, "rb") as f:
+            h.update(b"whole-file:" + f.read())
     return h.hexdigest()[:16]
 EXP_POLY11, EXP_TABLE = 0, 1  # enum lzq_exp_variant
 LZQ_MAX_AXES = 8
@@ -132,6 +143,8 @@ def load(path: str | None = None):
         raise RuntimeError(f"lzq HIP library not built ({p}); run __graft_entry__.build() "
                            "or python -m <package>.build")
     L = ctypes.CDLL(p)
+    global _loaded_path
+    _loaded_path = p
     i32, i64, d, vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
     P = ctypes.POINTER
     L.lzq_abi_version.restype = ctypes.c_int

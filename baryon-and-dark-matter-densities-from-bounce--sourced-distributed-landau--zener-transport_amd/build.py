@@ -5,6 +5,8 @@ git-ignored but travels to the GPU box with the gpurun snapshot.
 """
 from __future__ import annotations
 
+import glob
+import hashlib
 import os
 import shutil
 import subprocess
@@ -15,7 +17,9 @@ INCLUDE = os.path.normpath(os.path.join(HERE, "..", "include"))
 BUILD_DIR = os.path.join(HERE, "_build")
 LIB_PATH = os.path.join(BUILD_DIR, "liblzq.so")
 SOURCES = ["lzq_kernels.hip", "lzq_propagator.hip", "lzq_ode.hip", "lzq_profile.hip"]
-HEADERS = ["lzq_exp2.h", "lzq_physics.h", "lzq_internal.h", "lzq_su2.h"]
+# every header next to the sources (tests/test_engine_host.py checks each #include "..." of the
+# sources resolves to one of the build inputs)
+HEADERS = sorted(os.path.basename(h) for h in glob.glob(os.path.join(CSRC, "*.h")))
 ARCH = os.environ.get("LZQ_OFFLOAD_ARCH", "gfx950")
 # -ffp-contract=off: every a*b+c rounds twice exactly like numpy; fused ops are explicit
 # __builtin_fma in the hot loops.
@@ -29,11 +33,34 @@ def _inputs():
     return files
 
 
-def up_to_date() -> bool:
-    if not os.path.exists(LIB_PATH):
+def inputs_hash(defines: dict | None = None) -> str:
+    """sha256 over the build's inputs (sources, headers, flags, defines), by content: the stamp
+    written next to the library, so a shipped build can be matched to its sources on any machine
+    (mtimes do not survive the copy to the GPU box)."""
+    h = hashlib.sha256()
+    for f in _inputs():
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update(repr((FLAGS, sorted((defines or {}).items()))).encode())
+    return h.hexdigest()
+
+
+def stamp_path(lib: str = LIB_PATH) -> str:
+    return lib + ".inputs.sha256"
+
+
+def stamp_matches(lib: str = LIB_PATH) -> bool:
+    """True when the library's stamp equals the current sources' inputs_hash()."""
+    try:
+        with open(stamp_path(lib)) as f:
+            return f.read().strip() == inputs_hash()
+    except OSError:
         return False
-    t = os.path.getmtime(LIB_PATH)
-    return all(os.path.getmtime(f) <= t for f in _inputs())
+
+
+def up_to_date() -> bool:
+    return os.path.exists(LIB_PATH) and stamp_matches(LIB_PATH)
 
 
 def hipcc() -> str:
@@ -57,6 +84,8 @@ def build(force: bool = False, verbose: bool = False, defines: dict | None = Non
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
     os.replace(tmp, target)
+    with open(stamp_path(target), "w") as f:
+        f.write(inputs_hash(defines) + "\n")
     return target
 
 

@@ -829,7 +829,14 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
     // takes every step on the general path, k_split = -1).  The general path takes that step and
     // the next (a rounding may split two consecutive steps); the rest run as the tight loop.
     int64_t k_split = INT64_MAX;
+    // whether the previous step was split: a continuation launch starts with the single launch's
+    // value, the predicate of step k_begin - 1 (else a launch boundary right after a split step
+    // would send the next -- possibly split again -- step through the tight loop)
     bool prev_split = false;
+    if (k_begin > 0) {
+      const double xq = x0 + (double)(k_begin - 1) * h;
+      prev_split = xq < xb && xb <= xq + h;
+    }
     if (lin_fast && xb < INFINITY) {  // branch_x: +inf when no step splits
       const double kf = floor((xb - x0) / h);
       const double margin = 2.0 + floor(8.0 * __DBL_EPSILON__ * (fabs(x0) + fabs(x1)) / h);

@@ -75,9 +75,10 @@ class ProfileSpec:
     fpy:170-187 as a sweep): the profile's phi, Phi (a CSV in transport_from_profile's `xi,phi,Phi`
     format, or shape `synthetic` of bounce.synthetic_shapes) with the couplings y_B, y_chi,
     lambda_tr_eff (these defaults, or sweep axes of those names) and the point's v_w.
-    estimator: "auto" (one crossing -> eq.(9) of its delta_LZ; otherwise the time-ordered
-    propagation through the profile), "minimal" (eq.(9); points without exactly one crossing get
-    P = NaN) or "propagate" (every point through the whole profile)."""
+    estimator: "auto" (one crossing -> eq.(9) of its delta_LZ; several -> the time-ordered
+    propagation through the profile; none -> P = NaN, as the plug-in's Profile.probability raises
+    'no avoided crossing' for it), "minimal" (eq.(9); points without exactly one crossing get
+    P = NaN) or "propagate" (every point through the whole profile, crossings or not)."""
     csv: Optional[str] = None
     synthetic: int = 12     # bounce.synthetic_shapes index (12: one or three crossings across P1's couplings)
     estimator: str = "auto"
@@ -345,6 +346,12 @@ ComputeFn = Callable[[int, int, "object"], None]  # (start, count, out_tensor[co
 MAX_INFLIGHT_WRITES = 3   # checkpoint chunks copied out and waiting for the disk (pinned ring of <= 4)
 
 
+def _status_file(shard_path: str) -> str:
+    """The ODE status counts of one checkpointed chunk (int64[8] per lzq_ode_status), so a resumed
+    sweep's summary counts every chunk, not only those computed by this run."""
+    return shard_path[:-len(".npy")] + ".status.npy"
+
+
 def _save_shard(path: str, arr: np.ndarray) -> None:
     tmp = path + ".tmp.npy"
     np.save(tmp, arr, allow_pickle=False)
@@ -389,12 +396,20 @@ def run_local(compute: ComputeFn, start: int, end: int, make_out: Callable[[int]
                 if arr.shape != (n, 6):
                     raise RuntimeError(f"checkpoint {path} has shape {arr.shape}, expected {(n, 6)}")
                 view.copy_(torch.from_numpy(arr))
+                counts = getattr(compute, "ode_status", None)
+                if counts is not None:   # the resumed chunk's ODE status counts (summary.json ode_status)
+                    st = _status_file(path)
+                    if not os.path.exists(st):
+                        raise RuntimeError(f"checkpoint {path} has no ODE status record {st}")
+                    counts += np.load(st, allow_pickle=False)
                 log(f"resumed {path}")
                 continue
             compute(c0, n, view)
             log(f"chunk [{c0}, {c0 + n}) launched")
             if not path:
                 continue
+            if getattr(compute, "ode_status", None) is not None:
+                _save_shard(_status_file(path), np.asarray(compute.last_chunk, dtype=np.int64))
             if not on_gpu:
                 sync()
                 _save_shard(path, view.detach().cpu().numpy())
@@ -572,9 +587,12 @@ def profile_P(spec: SweepSpec, s: int, n: int, engine, cache: dict):
         return engine.lz_propagate_profile(sh, pts, ps.steps_per_radian, ps.min_steps)
     cr = engine.profile_crossings(sh, pts, 1)
     one = cr["count"] == 1
-    P = torch.where(one, engine.p_closed_form(cr["delta_lz"][:, 0]), torch.full_like(cols[0], float("nan")))
-    if ps.estimator == "auto" and not bool(one.all()):
-        sel = torch.nonzero(~one).reshape(-1)
+    # delta_lz[:, 0] is written only where a crossing was found: mask the rest before eq.(9)
+    delta = torch.where(one, cr["delta_lz"][:, 0], torch.zeros_like(cols[0]))
+    P = torch.where(one, engine.p_closed_form(delta), torch.full_like(cols[0], float("nan")))
+    many = cr["count"] > 1
+    if ps.estimator == "auto" and bool(many.any()):
+        sel = torch.nonzero(many).reshape(-1)
         P[sel] = engine.lz_propagate_profile(sh, pts.view(n, 40)[sel].contiguous().view(-1), ps.steps_per_radian,
                                              ps.min_steps)
     return P
@@ -594,7 +612,7 @@ def make_compute(spec: SweepSpec, engine, reuse: bool = False) -> ComputeFn:
     y-grid and A/V kernel (lzq_sweep_grid_reuse; bit-identical, not the dense headline path)."""
     pcache = {}   # the profile's device splines, built once per sweep
     if is_ode_spec(spec):
-        counts = np.zeros(8, dtype=np.int64)   # ODE points per lzq_ode_status, this rank
+        counts = np.zeros(8, dtype=np.int64)   # ODE points per lzq_ode_status, this rank (all chunks)
 
         def compute_ode(s, n, out):
             import torch
@@ -615,13 +633,18 @@ def make_compute(spec: SweepSpec, engine, reuse: bool = False) -> ComputeFn:
                 # table, counted per status in the summary ("ode_status")
                 bad = status != 0
                 tab = torch.where(bad[:, None], torch.full_like(tab, float("nan")), tab)
-                counts[:] += np.bincount(status.clamp(0, 7).cpu().numpy(), minlength=8)[:8]
+                chunk = np.bincount(status.clamp(0, 7).cpu().numpy(), minlength=8)[:8]
+                counts[:] += chunk
+                compute_ode.last_chunk = chunk.astype(np.int64)   # written beside the chunk's checkpoint
                 out[torch.as_tensor(sel, device=out.device)] = tab
+            else:
+                compute_ode.last_chunk = np.zeros(8, dtype=np.int64)
             sel = np.nonzero(~ode)[0]
             if sel.size:
                 out[torch.as_tensor(sel, device=out.device)] = engine.yields(pts[sel], n_y=spec.n_y, reuse=reuse,
                                                                              nz=spec.nz, z_max=spec.z_max)
         compute_ode.ode_status = counts
+        compute_ode.last_chunk = np.zeros(8, dtype=np.int64)
         return compute_ode
 
     def compute(s, n, out):

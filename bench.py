@@ -14,12 +14,14 @@ all-gathered over RCCL at the end of every step (north_star (3)).
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 Prints one JSON line (rank 0).  `roofline` = the kernel's executed FP64 FLOP (PMC
-instruction mix of profiles/round3, used only if that profile's code-object sha256 is the timed
+instruction mix of profiles/round4, used only if that profile's code-object sha256 is the timed
 library's) over its HIP-event time in this run, against the 78.6 TFLOP/s FP64 vector peak, with
-the FP64-pipe and VALU issue fractions beside it; `parity_spot` checks 64 rows of the timed table
-against the C oracle after the timed region; `cpu_baseline` times the C oracle (the CPU
-restatement, OpenMP) on a bounded random sample of the same grid on every CPU of this job, and
-on one core.
+the FP64-pipe and VALU issue fractions beside it; `kernel_ms` / `allgather_ms` decompose a step
+per rank (min / max / mean); `parity_spot` checks 64 rows of the last timed step's table against
+the C oracle right after the timed region, before any secondary leg reuses the buffer (the exit
+status is non-zero if it, or the table's finiteness / shard placement, fails); `cpu_baseline`
+times the C oracle (the CPU restatement, OpenMP) on a bounded random sample of the same grid on
+every CPU of this job, and on one core.
 """
 from __future__ import annotations
 
@@ -52,7 +54,7 @@ BASE = {  # /root/reference/yields_config_equal_mass.json
 }
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "round3", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "round4", "pmc_summary.json")
 WAVE_NODES_PER_POINT = 8000 * 1200 // 64
 
 
@@ -75,7 +77,7 @@ def roofline(points_per_launch: int, kern_ms: float) -> dict:
     """FP64 VALU roofline of yields_grid_kernel for this run.
 
     achieved = EXECUTED FP64 FLOP per launch / this run's HIP-event kernel time.  The executed
-    FLOP per point come from the rocprofv3 PMC pass of the same build (profiles/round2, tools/
+    FLOP per point come from the rocprofv3 PMC pass of the same build (profiles/round4, tools/
     gpu_profile.sh): (2 x SQ_INSTS_VALU_FMA_F64 + SQ_INSTS_VALU_MUL_F64 + SQ_INSTS_VALU_ADD_F64)
     x 64 lanes / points; peak = 78.6 TFLOP/s (256 CU x 2.4 GHz x 128 FP64 FLOP/clk/CU, every
     issue slot an FMA).  Also reported: the FP64 pipe's busy fraction (FP64 instructions x 4
@@ -242,7 +244,39 @@ def parity_spot(axes, start: int, table: torch.Tensor, n: int = 64) -> dict:
                       f"vs oracle/lzq_oracle.c (pinned to the reference's golden outputs)"}
 
 
-def main():
+class Clock:
+    """Marks on the timed stream: HIP events on the GPU (elapsed on the device clock), host
+    perf_counter after a synchronize otherwise (the CPU rehearsal of tests/test_bench_roofline.py)."""
+
+    def __init__(self, cuda: bool):
+        self.cuda = cuda
+        self.stream = torch.cuda.current_stream() if cuda else None
+
+    def mark(self):
+        if self.cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(self.stream)
+            return e
+        return time.perf_counter()
+
+    def ms(self, a, b) -> float:
+        return a.elapsed_time(b) if self.cuda else 1e3 * (b - a)
+
+    def sync(self):
+        if self.cuda:
+            torch.cuda.synchronize()
+
+
+def spread(vals) -> dict:
+    v = [float(x) for x in vals]
+    return {"min": min(v), "max": max(v), "mean": float(np.mean(v)), "per_rank": v}
+
+
+def main(argv=None, engine=None) -> int:
+    """The bench (one JSON line on rank 0).  engine: a stand-in with Engine.sweep's signature and a
+    torch `device` (tests only: the CPU rehearsal of the timing / evidence order); None = the HIP
+    engine on this rank's GPU.  Returns the exit status: non-zero when the timed table fails its
+    evidence checks (non-finite rows, a misplaced shard, parity_spot beyond the guard band)."""
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -258,25 +292,28 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI, default) | gloo (rehearsal of the N>1 path on one GPU)")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"[bench] WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE", file=sys.stderr)
-    local = local % max(1, torch.cuda.device_count())  # gloo rehearsal: several ranks may share a GPU
-    torch.cuda.set_device(local)
+    cuda = engine is None
+    if cuda:
+        local = local % max(1, torch.cuda.device_count())  # gloo rehearsal: several ranks may share a GPU
+        torch.cuda.set_device(local)
     # a process group whenever a launcher started us (torchrun sets MASTER_ADDR/PORT), so a
     # 1-rank torchrun runs the same RCCL all-gather as N ranks; plain `python bench.py` has none
     use_dist = world > 1 or ("MASTER_ADDR" in os.environ and "MASTER_PORT" in os.environ)
+    nccl = cuda and args.dist_backend == "nccl"
     if use_dist:
-        if args.dist_backend == "nccl":
+        if nccl:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
-            dist.init_process_group(args.dist_backend)
+            dist.init_process_group("gloo")
 
-    eng = importlib.import_module(PKG + ".engine").Engine(local)
+    eng = engine if engine is not None else importlib.import_module(PKG + ".engine").Engine(local)
     axes = grid_axes(world)
     per = args.points
     total = per * world
@@ -285,62 +322,79 @@ def main():
     start = rank * per
     local_tab = torch.empty((per, 6), dtype=torch.float64, device=eng.device)
     gathered = torch.empty((total, 6), dtype=torch.float64, device=eng.device) if use_dist else local_tab
-    stream = torch.cuda.current_stream()
-    k_ev = []
+    clock = Clock(cuda)
+    marks = []
+
+    def gather():
+        if nccl:
+            dist.all_gather_into_tensor(gathered, local_tab)  # RCCL over xGMI
+        else:
+            parts = [torch.empty((per, 6), dtype=torch.float64) for _ in range(world)]
+            dist.all_gather(parts, local_tab.cpu())
+            gathered.copy_(torch.cat(parts))
 
     def step(record: bool):
-        if record:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
+        k0 = clock.mark() if record else None
         eng.sweep(BASE, axes, start, per, out=local_tab)
-        if record:
-            e1.record(stream)
-            k_ev.append((e0, e1))
+        k1 = clock.mark() if record else None
         if use_dist:
-            if args.dist_backend == "nccl":
-                dist.all_gather_into_tensor(gathered, local_tab)  # RCCL over xGMI
-            else:
-                parts = [torch.empty((per, 6), dtype=torch.float64) for _ in range(world)]
-                dist.all_gather(parts, local_tab.cpu())
-                gathered.copy_(torch.cat(parts))
+            gather()
+        if record:
+            marks.append((k0, k1, clock.mark()))
 
     for _ in range(args.warmup):
         step(False)
-    torch.cuda.synchronize()
+    clock.sync()
     if use_dist:
         dist.barrier()
-    torch.cuda.synchronize()
+    clock.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
-    torch.cuda.synchronize()
+    clock.sync()
     if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in k_ev]))
+    kern = float(np.mean([clock.ms(a, b) for a, b, _ in marks]))          # this rank's sweep kernel
+    gath = float(np.mean([clock.ms(b, c) for _, b, c in marks]))          # this rank's all-gather
+    mine = torch.tensor([elapsed, kern, gath], dtype=torch.float64, device=eng.device if nccl else "cpu")
     if use_dist:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64,
-                         device=eng.device if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+        every = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(every, mine)
+        every = torch.stack(every).cpu().numpy()
+    else:
+        every = mine.cpu().numpy()[None, :]
+    elapsed = float(every[:, 0].max())   # max over ranks
+    kern_ms = float(every[:, 1].max())
+
+    # Evidence on the TIMED table, before the secondary legs below overwrite local_tab: every row
+    # of the gathered table finite, rank r's rows at [r*per, (r+1)*per), and parity_spot's oracle
+    # rows (rank 0) from the dense table of the last timed step.
+    finite = bool(torch.isfinite(gathered).all())
+    placed = bool(torch.equal(gathered[start:start + per], local_tab)) if use_dist else True
+    spot = parity_spot(axes, start, local_tab) if rank == 0 and not args.no_parity_spot else None
+    ok = torch.tensor([1.0 if finite and placed else 0.0], dtype=torch.float64, device=eng.device if nccl else "cpu")
+    if use_dist:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    evidence = {"table": "dense timed table (last timed step), checked before the secondary legs",
+                "all_finite_and_placed": bool(ok.item() == 1.0), "parity_spot_ok": None if spot is None else spot["ok"]}
 
     # Secondary (NOT the headline): the same step with exact-underflow truncation of the
     # z-sums (LZQ_TUNE_TRUNCATE), which skips nodes whose terms cannot change the FP64 sums;
     # its table must be bit-identical to the dense one.
+    dense_tab = local_tab.clone() if (args.truncated or args.reuse) else None
     trunc = None
     if args.truncated:
-        dense_tab = local_tab.clone()
         eng.tune_truncate(True)
-        torch.cuda.synchronize()
+        clock.sync()
         t1 = time.perf_counter()
         eng.sweep(BASE, axes, start, per, out=local_tab)
-        torch.cuda.synchronize()
+        clock.sync()
         t_tr = time.perf_counter() - t1
         eng.tune_truncate(False)
         same = bool(torch.equal(dense_tab, local_tab))
         if use_dist:
-            t = torch.tensor([t_tr, 0.0 if same else 1.0], dtype=torch.float64,
-                             device=eng.device if args.dist_backend == "nccl" else "cpu")
+            t = torch.tensor([t_tr, 0.0 if same else 1.0], dtype=torch.float64, device=eng.device if nccl else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             t_tr, same = float(t[0]), float(t[1]) == 0.0
         trunc = {"value": total / t_tr, "unit": "points/s", "bit_identical_to_dense": same,
@@ -351,30 +405,22 @@ def main():
     # by the points (lzq_sweep_grid_reuse); the table must be bit-identical to the dense one.
     reuse = None
     if args.reuse:
-        dense_tab = local_tab.clone()
         eng.sweep(BASE, axes, start, per, out=local_tab, reuse=True)   # warm-up (table workspace)
-        torch.cuda.synchronize()
+        clock.sync()
         t1 = time.perf_counter()
         eng.sweep(BASE, axes, start, per, out=local_tab, reuse=True)
-        torch.cuda.synchronize()
+        clock.sync()
         t_re = time.perf_counter() - t1
         same = bool(torch.equal(dense_tab, local_tab))
         if use_dist:
-            t = torch.tensor([t_re, 0.0 if same else 1.0], dtype=torch.float64,
-                             device=eng.device if args.dist_backend == "nccl" else "cpu")
+            t = torch.tensor([t_re, 0.0 if same else 1.0], dtype=torch.float64, device=eng.device if nccl else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             t_re, same = float(t[0]), float(t[1]) == 0.0
         reuse = {"value": total / t_re, "unit": "points/s", "bit_identical_to_dense": same,
                  "note": "z-sums shared by the points of one y-grid / A/V kernel (include/lzq.h "
                          "lzq_sweep_grid_reuse; the C2 grid has one); one step, not the headline"}
 
-    # sanity: every shard of the gathered table is finite and the gather put rank r's rows at
-    # [r*per, (r+1)*per)
-    assert bool(torch.isfinite(gathered).all()), "non-finite yields"
-    if use_dist:
-        assert torch.equal(gathered[start:start + per], local_tab), "all-gather misplaced a shard"
-    spot = parity_spot(axes, start, local_tab) if rank == 0 and not args.no_parity_spot else None
-
+    status = 0 if evidence["all_finite_and_placed"] and (spot is None or spot["ok"]) else 1
     if rank == 0:
         rec = {
             "metric": METRIC,
@@ -393,9 +439,15 @@ def main():
                                    "|Delta'|=logspace(-3,1,1000*N), v_w=0.30, delta->P->dense Y_B (n_y=8000, "
                                    "nz=1200) + epilogue; 1e6 points per GPU per step",
                        "points_per_gpu": per, "global_points_per_step": total, "n_y": 8000, "nz": 1200,
-                       "parallelism": f"grid-sharded x{world}, {'RCCL' if args.dist_backend == 'nccl' else args.dist_backend} "
+                       "parallelism": f"grid-sharded x{world}, {'RCCL' if nccl else 'gloo'} "
                                       f"all-gather of 48 B/point yield tables"},
-            "roofline": roofline(per, kern_ms),
+            "roofline": roofline(per, kern_ms) if cuda else None,
+            # the step decomposed per rank (means over the timed steps): the sweep kernel (HIP
+            # events around it) and the all-gather of the yield table (events after it), so a
+            # sub-linear SCALE curve can be attributed to compute imbalance or to the collective
+            "kernel_ms": spread(every[:, 1]),
+            "allgather_ms": spread(every[:, 2]) if use_dist else None,
+            "evidence": evidence,
         }
         if spot is not None:
             rec["parity_spot"] = spot
@@ -406,9 +458,12 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(axes, grid_total, args.cpu_seconds)
         print(json.dumps(rec), flush=True)
+        if status:
+            print(f"[bench] evidence check failed: {evidence}", file=sys.stderr)
     if use_dist:
         dist.destroy_process_group()
+    return status
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

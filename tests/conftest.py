@@ -55,7 +55,11 @@ def gpu_engine():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     # the library is built on the CPU side (__graft_entry__.build()) and shipped in-tree; never
-    # rebuild on the GPU box (a rebuild there is a different build than the one profiled)
-    if not pkg("build").up_to_date():
-        print("WARNING: liblzq.so is older than its sources; testing the shipped build", flush=True)
+    # rebuild on the GPU box (a rebuild there is a different build than the one profiled).  Its
+    # stamp (sha256 of the sources, headers and flags it was built from) must match the sources
+    # here: testing a stale library would pass or fail on code that is not the tree's.
+    b = pkg("build")
+    if not b.up_to_date():
+        pytest.fail(f"{b.LIB_PATH} was not built from these sources (stamp {b.stamp_path()} != inputs_hash()); "
+                    "run __graft_entry__.build()", pytrace=False)
     return pkg("engine").Engine()

@@ -10,7 +10,10 @@ import sys
 
 from conftest import ROOT
 
-PROF = os.path.join(ROOT, "profiles", "round3")
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+PROF = os.path.dirname(bench.PMC_SUMMARY)   # this round's committed profile (profiles/round4)
 
 
 def counters(path, kernel="yields_grid_kernel"):
@@ -22,8 +25,9 @@ def counters(path, kernel="yields_grid_kernel"):
 
 
 def test_executed_flop_from_committed_csv():
-    sys.path.insert(0, ROOT)
-    bench = importlib.import_module("bench")
+    import pytest
+    if not os.path.exists(os.path.join(PROF, "pmc_mix.csv")):
+        pytest.skip(f"{os.path.relpath(PROF, ROOT)} holds no PMC pass yet")
     c = counters(os.path.join(PROF, "pmc_mix.csv"))
     points = 200_000                                     # tools/gpu_profile.sh PMC launch size
     flop_pt = 64 * (2 * c["SQ_INSTS_VALU_FMA_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + c["SQ_INSTS_VALU_ADD_F64"]) / points
@@ -45,3 +49,66 @@ def test_executed_flop_from_committed_csv():
     write = counters(os.path.join(PROF, "pmc_write.csv"))["WRITE_SIZE"] * 1024
     assert abs(rf["traffic"] / ((2 * fetch + write) / points * 1e6) - 1) < 1e-12
     assert write / points == 48.0 and rf["traffic"] < 1.2 * rf["algorithmic_bytes"]
+
+
+# ---- the bench's evidence chain and step decomposition, rehearsed on the CPU -----------------
+import json
+import socket
+import subprocess
+
+FAKE = os.path.join(ROOT, "tests", "bench_fake.py")
+SMALL = ["--points", "64", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+
+
+def _run(cmd, env=None):
+    e = dict(os.environ, **(env or {}))
+    e.pop("MASTER_ADDR", None), e.pop("MASTER_PORT", None)
+    return subprocess.run(cmd, cwd=ROOT, env=e, capture_output=True, text=True, timeout=600)
+
+
+def _line(out):
+    recs = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+    assert len(recs) == 1, out
+    return recs[0]
+
+
+def test_evidence_checks_the_dense_timed_table():
+    """parity_spot and the finiteness check run on the last timed step's dense table, before the
+    truncated / reuse legs reuse the buffer (the stand-in engine writes NaN in those modes): the
+    line's evidence is clean and the exit status 0; the secondary legs' own comparisons see the
+    NaN rows and report bit_identical_to_dense = false."""
+    r = _run([sys.executable, FAKE, *SMALL, "--truncated"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _line(r.stdout)
+    assert rec["parity_spot"]["ok"] and rec["parity_spot"]["n"] == 64
+    assert rec["evidence"]["all_finite_and_placed"] and rec["evidence"]["parity_spot_ok"]
+    assert rec["truncated"]["bit_identical_to_dense"] is False and rec["reuse_zsums"]["bit_identical_to_dense"] is False
+    assert rec["kernel_ms"]["max"] >= rec["kernel_ms"]["min"] > 0 and rec["allgather_ms"] is None
+
+
+def test_parity_failure_exits_nonzero():
+    """One timed row off by 1e-6 relative: the line is still printed, parity_spot.ok is false and
+    bench.py exits non-zero."""
+    r = _run([sys.executable, FAKE, *SMALL, "--no-reuse"], env={"FAKE_BAD_ROW": "5"})
+    assert r.returncode == 1
+    rec = _line(r.stdout)
+    assert rec["parity_spot"]["ok"] is False and rec["evidence"]["parity_spot_ok"] is False
+
+
+def test_two_rank_line_is_decomposed():
+    """The N > 1 path under torchrun (2 gloo ranks on the CPU): the value counts both shards, and the
+    line carries per-rank kernel and all-gather times (min / max / mean / per_rank)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2", "--master-addr",
+              "127.0.0.1", "--master-port", str(port), FAKE, "--gpus", "2", *SMALL, "--no-reuse", "--no-parity-spot",
+              "--dist-backend", "gloo"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _line(r.stdout)
+    assert rec["n_gpus"] == 2 and rec["config"]["global_points_per_step"] == 128
+    for k in ("kernel_ms", "allgather_ms"):
+        assert len(rec[k]["per_rank"]) == 2 and rec[k]["max"] >= rec[k]["mean"] >= rec[k]["min"] >= 0.0, rec[k]
+    assert rec["evidence"]["all_finite_and_placed"]
+    assert abs(rec["value"] - 128 / (rec["ms_per_step"] / 1e3)) <= 1e-6 * rec["value"]

@@ -1,6 +1,7 @@
 """Host-side logic of engine.py that needs no GPU: the ODE launch order (wave_order), which
 puts points with equal stage keys next to each other so that whole wavefronts qualify for the
 integrator's cooperative mode."""
+import os
 import numpy as np
 import torch
 
@@ -85,3 +86,56 @@ def test_ode_step_counts_device_equals_host():
     host = eng.ode_step_counts(pts)
     dev = eng.ode_step_counts_device(torch.from_numpy(pts.view(np.uint8).copy()), n).numpy()
     assert np.array_equal(host, dev, equal_nan=True)
+
+
+def test_build_inputs_cover_every_include():
+    """Every #include "..." of the HIP sources and headers is one of build._inputs(), so the build
+    stamp (a content hash of those inputs) changes with any file the library is compiled from."""
+    import re
+    b = pkg("build")
+    inputs = {os.path.normpath(f) for f in b._inputs()}
+    for f in list(inputs):
+        if not f.endswith((".hip", ".h")):
+            continue
+        for inc in re.findall(r'^\s*#\s*include\s+"([^"]+)"', open(f).read(), flags=re.M):
+            path = os.path.normpath(os.path.join(os.path.dirname(f), inc))
+            assert path in inputs, (f, inc)
+    assert "lzq_superadiabatic.h" in b.HEADERS
+
+
+def test_build_stamp_tracks_content():
+    """inputs_hash() is a content hash: it changes with a header's bytes (not its mtime), and the
+    stamp written by build() is what up_to_date() compares."""
+    import shutil
+    import tempfile
+    b = pkg("build")
+    h0 = b.inputs_hash()
+    assert h0 == b.inputs_hash() and h0 != b.inputs_hash({"LZQ_X": 1})
+    hdr = os.path.join(b.CSRC, "lzq_superadiabatic.h")
+    tmp = tempfile.mktemp()
+    shutil.copy2(hdr, tmp)
+    try:
+        with open(hdr, "a") as f:
+            f.write("\n")
+        assert b.inputs_hash() != h0
+    finally:
+        shutil.copy2(tmp, hdr)
+        os.remove(tmp)
+    assert b.inputs_hash() == h0
+
+
+def test_library_id_is_a_real_digest():
+    """sweep.spec_key's library id: the shipped library's device code objects, never the digest of
+    empty input; a library without a matching bundle entry is hashed whole."""
+    import hashlib
+    import tempfile
+    nat = pkg("_native")
+    lid = nat.library_id(nat.LIB_PATH)
+    assert lid is not None and lid != hashlib.sha256(b"").hexdigest()[:16]
+    with tempfile.NamedTemporaryFile(suffix=".so", delete=False) as f:
+        f.write(b"not a fat binary")
+    try:
+        other = nat.library_id(f.name)
+        assert other not in (None, lid, hashlib.sha256(b"").hexdigest()[:16])
+    finally:
+        os.remove(f.name)

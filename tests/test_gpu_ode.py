@@ -541,3 +541,60 @@ def test_ode_linear_waves_degenerate_step(gpu_engine):
         gpu_engine.tune_ode_coop(prev)
     assert torch_equal(sa, sb) and torch_equal(a, b)
     assert bool((sa[64:] == 0).all())
+
+
+def _split_step(m, T_lo, T_hi, T_p):
+    """Host restatement of the integrator's first split step (lzq_ode.hip branch_x and the linear
+    waves' k_split): the step k with x_k < x_b <= x_k + h, x_b the first x whose T = m (1/x) is no
+    longer > m/3 (same IEEE operations)."""
+    x0, x1 = m / T_hi, m / max(T_lo, 1e-30)
+    x_p = m / max(T_p, 1e-30)
+    ms = min(min(abs(x1 - x0) / 20000.0, x_p / 1000.0), 5e-4)
+    N = int(np.ceil(abs(x1 - x0) / ms))
+    h = (x1 - x0) / N
+    m3 = m / 3.0
+    rel = lambda x: m * (1.0 / max(x, 1e-30)) > m3
+    xg = m / m3
+    if rel(xg):
+        while rel(xg):
+            xg = np.nextafter(xg, np.inf)
+    else:
+        while not rel(np.nextafter(xg, -np.inf)):
+            xg = np.nextafter(xg, -np.inf)
+    kf = int(np.floor((xg - x0) / h))
+    for c in range(max(kf - 3, 0), min(kf + 4, N)):
+        xc = x0 + c * h
+        if xc < xg <= xc + h:
+            return c, N
+    return None, N
+
+
+@pytest.mark.parametrize("offset", [-1, 0])
+def test_ode_launch_boundary_at_split_step(gpu_engine, offset):
+    """Continuation launches whose boundary falls right after (offset -1: the next launch starts at
+    k_split + 1) or right at (offset 0) the T = m/3 split step of a linear cooperative wave: the
+    next launch resumes with the single launch's prev_split, so the results are the single
+    launch's bits (prev_split was reset at every launch)."""
+    L = 6   # 2^6 = 64 steps per launch
+    T_p, m = 100.0, 300.0
+    for t in np.arange(1.55, 1.75, 1e-4):
+        k, N = _split_step(m, 0.6 * T_p, float(t) * T_p, T_p)
+        if k is not None and (k - offset) % (1 << L) == 0:
+            break
+    else:
+        pytest.fail("no window puts the split step on a launch boundary")
+    rng = np.random.default_rng(5)
+    cfgs = []
+    for _ in range(64):
+        c = full_cfg(BASE_CFG)
+        c.update(m_chi_GeV=m, T_max_over_Tp=float(t), T_min_over_Tp=0.6, Gamma_wash_over_H=0.5, sigma_v_chi_GeV_m2=0.0,
+                 deplete_DM_from_source=True, P_chi_to_B=float(rng.uniform(0.05, 1.0)))
+        cfgs.append(c)
+    p, o = recs(cfgs)
+    a, sa = gpu_engine.ode(p, o)
+    prev = gpu_engine.tune_ode_launch_steps(L)
+    try:
+        b, sb = gpu_engine.ode(p, o)
+    finally:
+        gpu_engine.tune_ode_launch_steps(prev)
+    assert bool((sa == 0).all()) and torch_equal(sa, sb) and torch_equal(a, b), (k, N, float(t))

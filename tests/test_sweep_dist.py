@@ -174,3 +174,41 @@ def test_profile_spec_json_and_axis_mapping():
     assert p1.total == 10**6 and p1.profile is not None
     x, a, b = p1.profile.arrays()
     assert x.shape == a.shape == b.shape and np.all(np.diff(x) > 0)
+
+
+def test_resumed_ode_status_counts_every_chunk():
+    """ODE status counts (summary.json ode_status) after --resume: each checkpointed chunk carries
+    its counts in a .status.npy record, so a resumed run reports the same totals as an
+    uninterrupted one, not only the chunks it computed itself."""
+    sw = pkg("sweep")
+
+    def make():
+        counts = np.zeros(8, dtype=np.int64)
+
+        def comp(start, n, out):
+            fake_compute(start, n, out)
+            chunk = np.zeros(8, dtype=np.int64)
+            chunk[0], chunk[3] = n - (start % 3), start % 3     # "ok" and "too_many_steps" per chunk
+            counts[:] += chunk
+            comp.last_chunk = chunk
+        comp.ode_status = counts
+        comp.last_chunk = np.zeros(8, dtype=np.int64)
+        return comp
+
+    mk = lambda n: torch.empty((n, 6), dtype=torch.float64)
+    with tempfile.TemporaryDirectory() as d:
+        full = make()
+        os.makedirs(os.path.join(d, "a"))
+        ref = sw.run_local(full, 0, 1000, mk, 64, os.path.join(d, "a"))
+        # an interrupted run: the first 5 chunks only, then a resume over the whole range
+        os.makedirs(os.path.join(d, "b"))
+        sw.run_local(make(), 0, 320, mk, 64, os.path.join(d, "b"))
+        res = make()
+        tab = sw.run_local(res, 0, 1000, mk, 64, os.path.join(d, "b"), resume=True)
+        assert np.array_equal(tab.numpy(), ref.numpy())
+        assert np.array_equal(res.ode_status, full.ode_status) and full.ode_status[3] > 0
+        # a checkpoint without its status record is refused, never silently under-counted
+        st = [f for f in os.listdir(os.path.join(d, "b")) if f.endswith(".status.npy")]
+        os.remove(os.path.join(d, "b", st[0]))
+        with pytest.raises(RuntimeError, match="status"):
+            sw.run_local(make(), 0, 1000, mk, 64, os.path.join(d, "b"), resume=True)

@@ -1,0 +1,74 @@
+# The one GPU-box launcher (run through gpurun from the repo root):
+#
+#   gpurun -- bash tools/gpu.sh tests [pytest args ...]   the -m gpu suite (or a selection), one process
+#   gpurun -- bash tools/gpu.sh final                     full -m gpu suite, smoke(), the default bench line
+#   gpurun -- bash tools/gpu.sh profile ROUND             rocprofv3 --kernel-trace --stats of the driver's
+#                                                         bench command, the PMC passes of the headline
+#                                                         kernel, profiles/ROUND summary, then the bench
+#   gpurun -- bash tools/gpu.sh bench [bench args ...]    one bench line
+#   gpurun -- bash tools/gpu.sh py SCRIPT [args ...]      any tools/ script (ablations, ODE / profile benches)
+#
+# Every GPU step runs under its own timeout and the steps are chained: a failure, abort or
+# time limit ends the call there (tail of the step's log on stdout, output under gpurun_out/).
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+cmd=${1:-tests}
+shift || true
+OUT=gpurun_out/$cmd
+mkdir -p "$OUT"
+
+run_tests() {  # pytest args...
+  timeout -k 10 1500 python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread -s "$@" \
+    > "$OUT/pytest_gpu.log" 2>&1 || { tail -60 "$OUT/pytest_gpu.log"; return 1; }
+  grep -E "worst|passed|failed" "$OUT/pytest_gpu.log" | tail -40
+}
+
+case "$cmd" in
+  tests)
+    run_tests "${@:-tests}"
+    ;;
+  final)
+    run_tests tests || exit 1
+    timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+      || { tail -20 "$OUT/smoke.log"; exit 2; }
+    tail -1 "$OUT/smoke.log"
+    timeout -k 10 400 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 3; }
+    cut -c1-600 "$OUT/bench.json"
+    ;;
+  profile)
+    ROUND=${1:?profile ROUND}
+    rm -rf "$OUT"; mkdir -p "$OUT"
+    timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
+      python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_traced.json" 2> "$OUT/bench_traced.err" \
+      || { tail -5 "$OUT/bench_traced.err"; exit 2; }
+    cut -c1-300 "$OUT/bench_traced.json"
+    P="--points 200000 --steps 1 --warmup 0 --no-cpu-baseline --no-reuse --no-parity-spot"
+    pmc() { tag=$1; shift; timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/pmc_$tag" -o run -- \
+      python3 bench.py $P > "$OUT/pmc_$tag.json" 2> "$OUT/pmc_$tag.err" || { echo "pmc $tag failed"; return 1; }; }
+    pmc fetch FETCH_SIZE && pmc write WRITE_SIZE && \
+    pmc sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT && \
+    pmc inst SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_SALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE GRBM_COUNT && \
+    pmc mix SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_INT32 || exit 4
+    # the summary in the box's copy, so the plain bench below reports this build's roofline (the
+    # host re-runs tools/summarize_profile.py on the merged gpurun_out to commit profiles/ROUND)
+    python3 tools/summarize_profile.py "$OUT" "$ROUND" > "$OUT/summary.log" 2>&1 || { tail "$OUT/summary.log"; exit 5; }
+    timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_plain.json" 2> "$OUT/bench_plain.err" \
+      || { tail -20 "$OUT/bench_plain.err"; exit 3; }
+    cut -c1-600 "$OUT/bench_plain.json"
+    ;;
+  bench)
+    timeout -k 10 600 python3 -u bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 3; }
+    cut -c1-800 "$OUT/bench.json"
+    ;;
+  py)
+    script=${1:?py SCRIPT}
+    shift
+    timeout -k 10 1100 python3 -u "$script" "$@" > "$OUT/$(basename "$script" .py).log" 2>&1 \
+      || { tail -40 "$OUT/$(basename "$script" .py).log"; exit 6; }
+    tail -40 "$OUT/$(basename "$script" .py).log"
+    ;;
+  *)
+    echo "usage: tools/gpu.sh tests|final|profile ROUND|bench|py SCRIPT ..."; exit 64
+    ;;
+esac

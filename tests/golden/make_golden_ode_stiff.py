@@ -12,7 +12,9 @@ max_step (fpy:404), with the state carried across x* (the ODE's solution is cont
 only its right-hand side jumps).  Also recorded: a LSODA solve of the same split, as a check
 that the split solution is converged (the two agree to ~1e-12).
 
-    python tests/golden/make_golden_ode_stiff.py     # ~1 min; -> golden_ode_stiff.json
+    python tests/golden/make_golden_ode_stiff.py             # ~1 min; -> golden_ode_stiff.json
+    python tests/golden/make_golden_ode_stiff.py --cli-only  # the reference CLI's bytes on the two
+                                                             # cases -> golden_cli_ode_stiff.json
 """
 import json
 import os
@@ -51,7 +53,36 @@ def split_solve(cfg: dict, P_used: float, method: str) -> dict:
     return {"Y_chi": float(Y[0]), "Y_B": float(Y[1]), "pieces": pieces, "method": method}
 
 
+def cli_stiff_cases() -> list[dict]:
+    """Byte-exact stdout + yields_out.json of the reference CLI (fpy:346-438) on the two stiff cases:
+    its Radau gives up at the T = m/3 jump, main() prints the [warn] line (fpy:408-409) and reports
+    the state where the solver stopped (fpy:410)."""
+    import subprocess
+    import tempfile
+    gold = json.load(open(os.path.join(HERE, "golden_ode.json")))
+    out = []
+    for i, r in enumerate(gold["points"]):
+        if "error" in r or r["tight"]["success"]:
+            continue
+        with tempfile.TemporaryDirectory() as d:
+            cfg_text = json.dumps(r["config"], indent=2)
+            with open(os.path.join(d, "cfg.json"), "w") as f:
+                f.write(cfg_text)
+            res = subprocess.run([sys.executable, "-B", os.path.join(MGO.MG.REF_DIR, "first_principles_yields.py"),
+                                  "--config", "cfg.json"], cwd=d, capture_output=True, text=True)
+            with open(os.path.join(d, "yields_out.json")) as f:
+                yo = f.read()
+        out.append({"name": f"ode_stiff_{i}", "index": i, "flags": [], "config_text": cfg_text,
+                    "returncode": res.returncode, "stdout": res.stdout, "yields_out_json": yo})
+        print(i, res.stdout.splitlines()[:2])
+    return out
+
+
 def main():
+    if "--cli-only" in sys.argv:
+        with open(os.path.join(HERE, "golden_cli_ode_stiff.json"), "w") as f:
+            json.dump(cli_stiff_cases(), f, indent=1)
+        return
     gold = json.load(open(os.path.join(HERE, "golden_ode.json")))
     out = []
     for i, r in enumerate(gold["points"]):

@@ -43,3 +43,35 @@ def test_cli_ode_path_matches_reference(case, tmp_path, gpu_engine):
     assert ours["inputs"] == ref["inputs"]
     for k, v in ref["final"].items():
         assert rel_err(ours["final"][k], v) < 1e-10, (k, ours["final"][k], v)
+
+
+@pytest.mark.parametrize("case", golden("golden_cli_ode_stiff.json"), ids=lambda c: c["name"])
+def test_cli_stiff_cases_documented_divergence(case, tmp_path, gpu_engine):
+    """The two stiff cases (m_chi = 300 GeV, sigma_v = 1e-9, thermal) where the reference's adaptive
+    Radau gives up at the T = m/3 jump: the reference CLI prints `[warn] ODE solver reported
+    failure: ...` (fpy:408-409) and reports the state where it stopped (fpy:410), Y_B ~68x below
+    the converged one.  lzq splits the straddling fixed step at the branch point and integrates
+    through: its stdout is the reference's without the [warn] line,
+    with the same result block layout, and its finals are the converged solution of the
+    reference's own equations (golden_ode_stiff.json, two-piece rtol-1e-12 solve)."""
+    import re
+    (tmp_path / "cfg.json").write_text(case["config_text"])
+    out = run_cli(["--config", "cfg.json"], tmp_path)
+    ref_lines, our_lines = case["stdout"].splitlines(), out.splitlines()
+    assert ref_lines[0].startswith("[warn] ODE solver reported failure:")
+    assert not any(l.startswith("[warn]") for l in our_lines)
+    rest = ref_lines[1:]
+    assert len(our_lines) == len(rest)
+    differ = [i for i, (a, b) in enumerate(zip(our_lines, rest)) if a != b]
+    # exactly the three value lines of the result block (fpy:419-422) differ, in format only the numbers
+    assert [rest[i].split("=")[0] for i in differ] == ["rho_B^0   ", "rho_DM^0  ", "DM/B ratio"], differ
+    num = re.compile(r"[-+0-9.e]+")
+    for i in differ:
+        assert num.sub("#", our_lines[i]) == num.sub("#", rest[i]), (our_lines[i], rest[i])
+    conv = next(c for c in golden("golden_ode_stiff.json")["cases"] if c["index"] == case["index"])
+    ours = json.loads((tmp_path / "yields_out.json").read_text())
+    ref = json.loads(case["yields_out_json"])
+    assert ours["inputs"] == ref["inputs"] and list(ours["final"]) == list(ref["final"])
+    for k in ("Y_B", "Y_chi"):
+        assert rel_err(ours["final"][k], conv["split_radau"][k]) < 1e-10, (k, ours["final"][k], conv["split_radau"][k])
+    assert ours["final"]["Y_B"] / ref["final"]["Y_B"] > 50.0   # the reference stopped early

@@ -68,30 +68,25 @@ def interval_steps(knots, coef, yB, ychi, lam, vw, spr: float = 4.0, n_min: int 
     return total
 
 
+def _plugin_reader():
+    """plugins/transport_from_profile.py's CSV reader: the one parser of the profile format (the
+    plug-in is torch-free and loads its GPU binding lazily, so importing it costs nothing)."""
+    import importlib.util
+    import os
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "plugins",
+                        "transport_from_profile.py")
+    spec = importlib.util.spec_from_file_location("_lzq_transport_from_profile", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.read_csv
+
+
 def read_bounce_csv(path: str):
     """The bounce-profile CSV of plugins/transport_from_profile.py (header `xi,phi,Phi`, or
-    `r,phi,Phi` with `# R0 = ...`; `# key = value` option lines) -> (xi, phi, Phi, options)."""
-    opts, header, rows = {}, None, []
-    with open(path) as f:
-        for raw in f:
-            line = raw.strip()
-            if not line:
-                continue
-            if line.startswith("#"):
-                body = line.lstrip("#").strip()
-                if "=" in body:
-                    k, v = (t.strip() for t in body.split("=", 1))
-                    try:
-                        opts[k] = float(v)
-                    except ValueError:
-                        opts[k] = v
-                continue
-            cells = [c.strip() for c in line.split(",")]
-            if header is None:
-                header = cells
-            else:
-                rows.append([float(c) for c in cells])
-    if header is None or len(rows) < 4:
+    `r,phi,Phi` with `# R0 = ...`; `# key = value` option lines) -> (xi, phi, Phi, options),
+    parsed by the plug-in's own reader."""
+    header, rows, opts = _plugin_reader()(path)
+    if len(rows) < 4:
         raise ValueError(f"{path}: a bounce profile needs a header and >= 4 rows")
     col = {h: i for i, h in enumerate(header)}
     low = {h.lower(): i for i, h in enumerate(header)}

@@ -1303,6 +1303,12 @@ int lzq_tune(int32_t key, int32_t value) {
     lzq::g_ode_launch_log2 = value;
     return prev;
   }
+  if (key == LZQ_TUNE_PROFILE_FLAT) {
+    if (value != 0 && value != 1) return fail(LZQ_EINVAL, "lzq_tune: profile_flat must be 0 or 1, got %d", value);
+    int prev = lzq::g_profile_flat;
+    lzq::g_profile_flat = value;
+    return prev;
+  }
   if (key == LZQ_TUNE_ODE_COOP) {
     if (value != 0 && value != 1) return fail(LZQ_EINVAL, "lzq_tune: ode_coop must be 0 or 1, got %d", value);
     int prev = lzq::g_ode_coop;

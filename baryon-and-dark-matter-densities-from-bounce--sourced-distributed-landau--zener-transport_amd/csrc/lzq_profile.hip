@@ -40,6 +40,8 @@
 
 #include <math.h>
 
+#include <algorithm>
+
 #include "../../include/lzq.h"
 #include "lzq_internal.h"
 #include "lzq_su2.h"
@@ -335,6 +337,60 @@ __device__ __forceinline__ void cos_sinc_short(double x2, double& cs, double& sc
   }
 }
 
+// One sixth-order Magnus step of H = Delta sz + m sx on [t0, t0 + h] of the current knot interval
+// (cD, cM its cubics in t = xi - xi_j; dt = h / v_w the step in time): H at the three Gauss nodes,
+// the Blanes-Casas-Ros commutator form (the alphas lie in the x-z plane, so the commutators are
+// cross products), the exact SU(2) exponential.  ~90 VALU.
+constexpr double kSq15 = 3.872983346207416885;  // sqrt(15)
+struct StepGeom {
+  double h, dt, k2, k3, gh1, gh2, gh3;
+};
+
+__device__ __forceinline__ StepGeom step_geom(double L, double Sd, double ivw) {
+  constexpr double g1 = 0.5 - kSq15 / 10.0, g3 = 0.5 + kSq15 / 10.0;
+  StepGeom g;
+  g.h = L / Sd;
+  g.dt = g.h * ivw;
+  g.k2 = (kSq15 / 3.0) * g.dt;
+  g.k3 = (10.0 / 3.0) * g.dt;
+  g.gh1 = g1 * g.h;
+  g.gh2 = 0.5 * g.h;
+  g.gh3 = g3 * g.h;
+  return g;
+}
+
+__device__ __forceinline__ void magnus6_step(const double (&cD)[4], const double (&cM)[4], double t0, const StepGeom& g,
+                                             Cplx& p0, Cplx& p1) {
+#define FMA __builtin_fma
+  const double dt = g.dt, k2 = g.k2, k3 = g.k3;
+  const double t1 = t0 + g.gh1, t2 = t0 + g.gh2, t3 = t0 + g.gh3;
+  // H at the three Gauss nodes: (x, z) = (m, Delta)
+  const double X1 = FMA(FMA(FMA(cM[3], t1, cM[2]), t1, cM[1]), t1, cM[0]);
+  const double X2 = FMA(FMA(FMA(cM[3], t2, cM[2]), t2, cM[1]), t2, cM[0]);
+  const double X3 = FMA(FMA(FMA(cM[3], t3, cM[2]), t3, cM[1]), t3, cM[0]);
+  const double Z1 = FMA(FMA(FMA(cD[3], t1, cD[2]), t1, cD[1]), t1, cD[0]);
+  const double Z2 = FMA(FMA(FMA(cD[3], t2, cD[2]), t2, cD[1]), t2, cD[0]);
+  const double Z3 = FMA(FMA(FMA(cD[3], t3, cD[2]), t3, cD[1]), t3, cD[0]);
+  // alpha1 = dt A2, alpha2 = sqrt15/3 dt (A3 - A1), alpha3 = 10/3 dt (A3 - 2 A2 + A1)
+  const double x1 = dt * X2, z1 = dt * Z2;
+  const double x2 = k2 * (X3 - X1), z2 = k2 * (Z3 - Z1);
+  const double x3 = k3 * FMA(-2.0, X2, X1 + X3), z3 = k3 * FMA(-2.0, Z2, Z1 + Z3);
+  // Lie bracket of -i a.sigma, -i b.sigma is -i (2 a x b).sigma; the alphas lie in the x-z plane
+  const double c = 2.0 * FMA(z1, x2, -(x1 * z2));                 // C1 = [alpha1, alpha2]  (y only)
+  const double C2x = z1 * c * (1.0 / 30.0);                         // C2 = -[alpha1, 2 alpha3 + C1]/60
+  const double C2y = FMA(x1, z3, -(z1 * x3)) * (1.0 / 15.0);
+  const double C2z = -(x1 * c) * (1.0 / 30.0);
+  const double Lx = FMA(-20.0, x1, -x3), Lz = FMA(-20.0, z1, -z3);  // -20 alpha1 - alpha3 + C1
+  const double Rx = x2 + C2x, Rz = z2 + C2z;                        // alpha2 + C2  (Ry = C2y)
+  const double nx = FMA(FMA(c, Rz, -(Lz * C2y)), 1.0 / 120.0, FMA(x3, 1.0 / 12.0, x1));
+  const double ny = FMA(Lz, Rx, -(Lx * Rz)) * (1.0 / 120.0);
+  const double nz = FMA(FMA(Lx, C2y, -(c * Rx)), 1.0 / 120.0, FMA(z3, 1.0 / 12.0, z1));
+  double cs, sc;
+  cos_sinc_short(FMA(nx, nx, FMA(ny, ny, nz * nz)), cs, sc);
+  su2_apply(cs, sc * nx, sc * ny, sc * nz, p0, p1);
+#undef FMA
+}
+
 // The step rule samples each knot interval at t_q = (q/4) L, q = 0..4.  The shape's values there
 // -- phi, Phi, phi', Phi' -- do not depend on the point, so they are evaluated once per launch
 // per (shape, interval) (profile_samples_kernel, stream-ordered scratch, staged in LDS next to the
@@ -447,8 +503,6 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_propag
   const double* cf = mine ? s_coef : coef + (int64_t)p.shape * (K - 1) * kProfCoef;
   const double* sm = mine ? s_samp : samp + (int64_t)p.shape * (K - 1) * kProfSamp;
   const double ivw = 1.0 / p.vw;
-  constexpr double kSq15 = 3.872983346207416885;  // sqrt(15)
-  constexpr double g1 = 0.5 - kSq15 / 10.0, g3 = 0.5 + kSq15 / 10.0;
 
   double cD[4], cM[4];
   interval_coefs(cf, p, cD, cM);
@@ -464,41 +518,9 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_propag
       return;
     }
     const int S = (int)Sd;
-    const double h = L / Sd;
-    const double dt = h * ivw;
-    const double k2 = (kSq15 / 3.0) * dt, k3 = (10.0 / 3.0) * dt;
-    const double gh1 = g1 * h, gh2 = 0.5 * h, gh3 = g3 * h;
-#define FMA __builtin_fma
+    const StepGeom g = step_geom(L, Sd, ivw);
 #pragma unroll LZQ_PROF_UNROLL
-    for (int st = 0; st < S; ++st) {
-      const double t0 = (double)st * h;
-      const double t1 = t0 + gh1, t2 = t0 + gh2, t3 = t0 + gh3;
-      // H at the three Gauss nodes: (x, z) = (m, Delta)
-      const double X1 = FMA(FMA(FMA(cM[3], t1, cM[2]), t1, cM[1]), t1, cM[0]);
-      const double X2 = FMA(FMA(FMA(cM[3], t2, cM[2]), t2, cM[1]), t2, cM[0]);
-      const double X3 = FMA(FMA(FMA(cM[3], t3, cM[2]), t3, cM[1]), t3, cM[0]);
-      const double Z1 = FMA(FMA(FMA(cD[3], t1, cD[2]), t1, cD[1]), t1, cD[0]);
-      const double Z2 = FMA(FMA(FMA(cD[3], t2, cD[2]), t2, cD[1]), t2, cD[0]);
-      const double Z3 = FMA(FMA(FMA(cD[3], t3, cD[2]), t3, cD[1]), t3, cD[0]);
-      // alpha1 = dt A2, alpha2 = sqrt15/3 dt (A3 - A1), alpha3 = 10/3 dt (A3 - 2 A2 + A1)
-      const double x1 = dt * X2, z1 = dt * Z2;
-      const double x2 = k2 * (X3 - X1), z2 = k2 * (Z3 - Z1);
-      const double x3 = k3 * FMA(-2.0, X2, X1 + X3), z3 = k3 * FMA(-2.0, Z2, Z1 + Z3);
-      // Lie bracket of -i a.sigma, -i b.sigma is -i (2 a x b).sigma; the alphas lie in the x-z plane
-      const double c = 2.0 * FMA(z1, x2, -(x1 * z2));                 // C1 = [alpha1, alpha2]  (y only)
-      const double C2x = z1 * c * (1.0 / 30.0);                         // C2 = -[alpha1, 2 alpha3 + C1]/60
-      const double C2y = FMA(x1, z3, -(z1 * x3)) * (1.0 / 15.0);
-      const double C2z = -(x1 * c) * (1.0 / 30.0);
-      const double Lx = FMA(-20.0, x1, -x3), Lz = FMA(-20.0, z1, -z3);  // -20 alpha1 - alpha3 + C1
-      const double Rx = x2 + C2x, Rz = z2 + C2z;                        // alpha2 + C2  (Ry = C2y)
-      const double nx = FMA(FMA(c, Rz, -(Lz * C2y)), 1.0 / 120.0, FMA(x3, 1.0 / 12.0, x1));
-      const double ny = FMA(Lz, Rx, -(Lx * Rz)) * (1.0 / 120.0);
-      const double nz = FMA(FMA(Lx, C2y, -(c * Rx)), 1.0 / 120.0, FMA(z3, 1.0 / 12.0, z1));
-      double cs, sc;
-      cos_sinc_short(FMA(nx, nx, FMA(ny, ny, nz * nz)), cs, sc);
-      su2_apply(cs, sc * nx, sc * ny, sc * nz, p0, p1);
-    }
-#undef FMA
+    for (int st = 0; st < S; ++st) magnus6_step(cD, cM, (double)st * g.h, g, p0, p1);
   }
   Cplx u0, u1;
   edge_state(cD, cM, L, p.vw, u0, u1);
@@ -507,11 +529,167 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_propag
   P_out[i] = 1.0 - (a.re * a.re + a.im * a.im) / norm;
 }
 
+// ---------------------------------------------------------------------------------------
+// Flattened propagation (LZQ_TUNE_PROFILE_FLAT, the default).  The interval-by-interval loop
+// above runs, per knot interval, the step rule and the coefficient rows for every lane and then
+// max-over-the-wave Magnus steps: with ~2.2 steps per interval on typical profiles, lanes idle
+// while the wave finishes its longest lane's steps, and the per-interval work is paid once per
+// interval whatever a lane needs (253 VALU per useful lane-step, profiles/round3/profile_pmc.json).
+// Here the step rule runs ahead of the propagation, one lane per point over all its intervals
+// (profile_steps_kernel: no lane waits, and the exact step totals order the launch), and the
+// propagation is ONE loop of Magnus steps per lane: a lane whose interval is done enters its next
+// one (its Delta / m rows and step geometry, ~35 VALU) in the same iteration while the other lanes
+// keep stepping.  Every lane performs exactly the interval loop's operations on its own point, so
+// P is bit-identical to profile_propagate_kernel (tests/test_gpu_profile.py).
+//
+// Step counts: uint16 per (point, interval), [point][interval] so a lane walks one row (one 64-B
+// line per 32 intervals).  0 = non-finite / absurd (P = NaN); kStepsRecompute = the count did
+// not fit (the lane re-derives it from the samples).
+constexpr uint16_t kStepsRecompute = 0xFFFF;
+
+__global__ __launch_bounds__(kProfBlock) void profile_steps_kernel(const double* __restrict__ knots, int32_t n_shapes,
+                                                                   int32_t K, const lzq_profile_point* __restrict__ pts,
+                                                                   int64_t n, double spr, int32_t n_min,
+                                                                   const double* __restrict__ samp,
+                                                                   uint16_t* __restrict__ steps,
+                                                                   int32_t* __restrict__ bins, int32_t* __restrict__ hist) {
+  __shared__ int32_t lh[kCostBins];
+  if (bins)
+    for (int t = threadIdx.x; t < kCostBins; t += kProfBlock) lh[t] = 0;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * kProfBlock + threadIdx.x;
+  if (i < n) {
+    const ProfPt p = load_point(pts + i);
+    double tot = 0.0;
+    if (p.vw > 0.0 && p.shape >= 0 && p.shape < n_shapes) {
+      const double* x = knots + (int64_t)p.shape * K;
+      const double* sm = samp + (int64_t)p.shape * (K - 1) * kProfSamp;
+      uint16_t* row = steps + i * (int64_t)(K - 1);
+      for (int j = 0; j + 1 < K; ++j) {
+        const double Sd = interval_steps(sm + j * kProfSamp, p, x[j + 1] - x[j], p.vw, spr, n_min);
+        row[j] = !(Sd <= kMaxIntervalSteps) ? (uint16_t)0 : (Sd < (double)kStepsRecompute ? (uint16_t)Sd : kStepsRecompute);
+        tot += Sd;
+      }
+    }
+    if (bins) {
+      const double key = tot == tot ? fmin(fmax(4.0 * log2(1.0 + tot), 0.0), (double)(kCostBins - 1)) : 0.0;
+      const int32_t b = (kCostBins - 1) - (int32_t)key;
+      bins[i] = b;
+      atomicAdd(&lh[b], 1);
+    }
+  }
+  if (!bins) return;
+  __syncthreads();
+  for (int t = threadIdx.x; t < kCostBins; t += kProfBlock)
+    if (lh[t]) atomicAdd(&hist[t], lh[t]);
+}
+
+__global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_flat_kernel(
+    const double* __restrict__ knots, const double* __restrict__ coef, int32_t n_shapes, int32_t K,
+    const lzq_profile_point* __restrict__ pts, int64_t n, double spr, int32_t n_min, const int32_t* __restrict__ order,
+    const double* __restrict__ samp, const uint16_t* __restrict__ steps, double* __restrict__ P_out) {
+  const int64_t tid = (int64_t)blockIdx.x * kProfBlock + threadIdx.x;
+  if (tid >= n) return;
+  const int64_t i = order ? (int64_t)order[tid] : tid;
+  const ProfPt p = load_point(pts + i);
+  if (!(p.vw > 0.0) || p.shape < 0 || p.shape >= n_shapes) {  // bad wall speed or shape index
+    P_out[i] = __builtin_nan("");
+    return;
+  }
+  const double* x = knots + (int64_t)p.shape * K;
+  const double* cf = coef + (int64_t)p.shape * (K - 1) * kProfCoef;
+  const double* sm = samp + (int64_t)p.shape * (K - 1) * kProfSamp;
+  const uint16_t* srow = steps + i * (int64_t)(K - 1);
+  const double ivw = 1.0 / p.vw;
+  double cD[4], cM[4];
+  interval_coefs(cf, p, cD, cM);
+  Cplx p0, p1;
+  edge_state(cD, cM, 0.0, p.vw, p0, p1);
+  // interval j's step count and geometry; false for a non-finite / absurd count (P = NaN)
+  double L = 0.0;
+  int S = 0;
+  StepGeom g;
+  auto enter = [&](int j) -> bool {
+    L = x[j + 1] - x[j];
+    const uint16_t sr = srow[j];
+    const double Sd = sr == kStepsRecompute ? interval_steps(sm + j * kProfSamp, p, L, p.vw, spr, n_min) : (double)sr;
+    if (sr == 0 || !(Sd <= kMaxIntervalSteps)) return false;
+    S = (int)Sd;
+    g = step_geom(L, Sd, ivw);
+    return true;
+  };
+  bool ok = enter(0);
+  int j = 0, st = 0;
+  while (ok) {
+    if (st == S) {  // this lane's interval is done: enter the next one (the others keep stepping)
+      if (++j == K - 1) break;
+      interval_coefs(cf + j * kProfCoef, p, cD, cM);
+      ok = enter(j);
+      if (!ok) break;
+      st = 0;
+    }
+    magnus6_step(cD, cM, (double)st * g.h, g, p0, p1);
+    ++st;
+  }
+  if (!ok) {
+    P_out[i] = __builtin_nan("");
+    return;
+  }
+  Cplx u0, u1;
+  edge_state(cD, cM, L, p.vw, u0, u1);
+  const Cplx a = inner(u0, u1, p0, p1);
+  const double norm = p0.re * p0.re + p0.im * p0.im + p1.re * p1.re + p1.im * p1.im;
+  P_out[i] = 1.0 - (a.re * a.re + a.im * a.im) / norm;
+}
+
+int g_profile_flat = 1;  // lzq_tune(LZQ_TUNE_PROFILE_FLAT)
+
 }  // namespace lzq
 
 namespace {
 bool shape_args_ok(const double* knots, const double* coef, int32_t n_shapes, int32_t K) {
   return knots && coef && n_shapes > 0 && K >= 4;
+}
+
+constexpr int64_t kStepsScratchBytes = int64_t(1) << 29;  // per slice of the flattened propagation
+
+// The flattened propagation in slices of points whose step-count rows fit kStepsScratchBytes: per
+// slice the step rule (+ the longest-first order for slices of >= kProfSortMin points) and the
+// Magnus loop, all stream-ordered.
+int profile_flat_launch(const double* d_knots, const double* d_coef, int32_t n_shapes, int32_t K,
+                        const lzq_profile_point* d_points, int64_t n, double spr, int32_t n_min, const double* samp,
+                        double* d_P, hipStream_t st) {
+  const int64_t row = 2 * (int64_t)(K - 1);
+  const int64_t per = std::max<int64_t>(1024, std::min<int64_t>(n, kStepsScratchBytes / row));
+  const int64_t m_max = std::min(per, n);
+  char* ws = nullptr;
+  const size_t bytes = (size_t)m_max * (size_t)row + sizeof(int32_t) * (size_t)(2 * m_max + 2 * lzq::kCostBins) + 256;
+  hipError_t e = hipMallocAsync((void**)&ws, bytes, st);
+  if (e != hipSuccess) return lzq_set_error(LZQ_EHIP, hipGetErrorString(e));
+  uint16_t* steps = reinterpret_cast<uint16_t*>(ws);
+  int32_t* bins = reinterpret_cast<int32_t*>(ws + (((size_t)m_max * (size_t)row + 255) & ~(size_t)255));
+  int32_t *ord = bins + m_max, *hist = ord + m_max, *offs = hist + lzq::kCostBins;
+  int rc = LZQ_OK;
+  for (int64_t s0 = 0; s0 < n && rc == LZQ_OK && e == hipSuccess; s0 += per) {
+    const int64_t m = std::min(per, n - s0);
+    const int64_t nb = (m + lzq::kProfBlock - 1) / lzq::kProfBlock;
+    const bool sort = LZQ_PROF_SORT && m >= lzq::kProfSortMin;
+    if (sort) e = hipMemsetAsync(hist, 0, sizeof(int32_t) * lzq::kCostBins, st);
+    if (e != hipSuccess) break;
+    hipLaunchKernelGGL(lzq::profile_steps_kernel, dim3((unsigned)nb), dim3(lzq::kProfBlock), 0, st, d_knots, n_shapes, K,
+                       d_points + s0, m, spr, n_min, samp, steps, sort ? bins : nullptr, sort ? hist : nullptr);
+    if (sort) rc = lzq::launch_bin_order(bins, hist, offs, m, ord, st);
+    if (rc != LZQ_OK) break;
+    hipLaunchKernelGGL(lzq::profile_flat_kernel, dim3((unsigned)nb), dim3(lzq::kProfBlock), 0, st, d_knots, d_coef,
+                       n_shapes, K, d_points + s0, m, spr, n_min, sort ? (const int32_t*)ord : nullptr, samp,
+                       (const uint16_t*)steps, d_P + s0);
+    e = hipGetLastError();
+  }
+  const hipError_t ef = hipFreeAsync(ws, st);
+  if (rc != LZQ_OK) return rc;
+  if (e == hipSuccess) e = ef;
+  if (e != hipSuccess) return lzq_set_error(LZQ_EHIP, hipGetErrorString(e));
+  return LZQ_OK;
 }
 }  // namespace
 
@@ -566,6 +744,14 @@ extern "C" int lzq_lz_propagate_profile(const double* d_knots, const double* d_c
   if (e != hipSuccess) return lzq_set_error(LZQ_EHIP, hipGetErrorString(e));
   hipLaunchKernelGGL(lzq::profile_samples_kernel, dim3((unsigned)((rows + lzq::kProfBlock - 1) / lzq::kProfBlock)),
                      dim3(lzq::kProfBlock), 0, st, d_knots, d_coef, rows, n_knots, samp);
+  if (lzq::g_profile_flat) {
+    const int rc2 = profile_flat_launch(d_knots, d_coef, n_shapes, n_knots, d_points, n, steps_per_radian, min_steps,
+                                        samp, d_P, st);
+    const hipError_t ef = hipFreeAsync(samp, st);
+    if (rc2 != LZQ_OK) return rc2;
+    if (ef != hipSuccess) return lzq_set_error(LZQ_EHIP, hipGetErrorString(ef));
+    return LZQ_OK;
+  }
   const int64_t nb = (n + lzq::kProfBlock - 1) / lzq::kProfBlock;
   // cost-ordered launch (profile_cost_kernel): bins, order, histogram, offsets in one scratch
   int32_t* ws = nullptr;

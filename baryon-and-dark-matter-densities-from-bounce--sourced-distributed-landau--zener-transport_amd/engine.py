@@ -68,6 +68,14 @@ class Engine:
         self._ode_launch_log2 = int(log2)
         return prev
 
+    def tune_profile_flat(self, on: bool) -> bool:
+        """lzq_lz_propagate_profile's flattened propagation (include/lzq.h LZQ_TUNE_PROFILE_FLAT; on by
+        default, bit-identical P either way).  Returns the previous setting."""
+        prev = self.lib.lzq_tune(_native.TUNE_PROFILE_FLAT, 1 if on else 0)
+        if prev < 0:
+            self._check(prev)
+        return bool(prev)
+
     def tune_truncate(self, on: bool) -> bool:
         """Exact-underflow truncation of the z-sums (bit-identical results, fewer nodes
         executed; include/lzq.h LZQ_TUNE_TRUNCATE).  Returns the previous setting."""
@@ -285,6 +293,7 @@ class Engine:
         status = torch.zeros(n, dtype=torch.int32, device=self.device)
         work = None
         keep = []
+        tables = {"points": n, "tables": 0, "per_point_chunks": 0, "chunks": 0}
         for c0 in range(0, n, chunk):
             c1 = min(n, c0 + chunk)
             d_pts = d_pts_all[c0 * rp:c1 * rp]
@@ -293,6 +302,16 @@ class Engine:
             if rep is not None:
                 rep, inv = rep
             n_tab = (c1 - c0) if rep is None else rep.numel()
+            tables["tables"] += n_tab
+            tables["chunks"] += 1
+            if rep is None and c1 - c0 > 1:
+                tables["per_point_chunks"] += 1
+                if share_tables and c1 - c0 >= 4096:
+                    _log.warning(
+                        "lzq ODE: %d of %d points differ in the A/V kernel or window (ODE_TABLE_KEY: %s): a spline "
+                        "table per point, and waves whose points differ in them integrate per lane (no shared stage "
+                        "rows) -- on long windows ~40x the cost per point of a shared-table sweep (DESIGN §5.3)",
+                        c1 - c0, c1 - c0, ", ".join(_native.ODE_TABLE_KEY))
             if work is None or work.numel() < n_tab * _native.ODE_WS_PER_POINT:
                 work = self.ode_workspace(max(n_tab, min(n, chunk) if rep is None else n_tab))
             with torch.cuda.device(self.device):
@@ -329,6 +348,9 @@ class Engine:
             keep.append((d_pts, d_ode))
         keep.append((d_pts_all, d_ode_all))
         self._keepalive = (keep, work)
+        tables["mode"] = "shared" if tables["per_point_chunks"] == 0 else (
+            "per_point" if tables["per_point_chunks"] == tables["chunks"] else "mixed")
+        self.last_ode_tables = tables   # sweep summary.json "ode_tables"
         if order is not None:
             out_in, st_in = torch.empty_like(out), torch.empty_like(status)
             out_in[order], st_in[order] = out, status

@@ -613,6 +613,7 @@ def make_compute(spec: SweepSpec, engine, reuse: bool = False) -> ComputeFn:
     pcache = {}   # the profile's device splines, built once per sweep
     if is_ode_spec(spec):
         counts = np.zeros(8, dtype=np.int64)   # ODE points per lzq_ode_status, this rank (all chunks)
+        tables = {"points": 0, "tables": 0, "per_point_chunks": 0, "chunks": 0}   # this run's chunks
 
         def compute_ode(s, n, out):
             import torch
@@ -628,6 +629,8 @@ def make_compute(spec: SweepSpec, engine, reuse: bool = False) -> ComputeFn:
             if sel.size:
                 tab, status = engine.ode(pts[sel], ods[sel], method=spec.ode_method, max_steps=spec.ode_max_steps,
                                          nz=spec.nz, z_max=spec.z_max)
+                for k in tables:
+                    tables[k] += engine.last_ode_tables[k]
                 # a point the integrator did not finish normally (a Radau Newton failure reports the
                 # state where it stopped, as fpy:408-410 does for the CLI) is a NaN row in a sweep
                 # table, counted per status in the summary ("ode_status")
@@ -644,6 +647,7 @@ def make_compute(spec: SweepSpec, engine, reuse: bool = False) -> ComputeFn:
                 out[torch.as_tensor(sel, device=out.device)] = engine.yields(pts[sel], n_y=spec.n_y, reuse=reuse,
                                                                              nz=spec.nz, z_max=spec.z_max)
         compute_ode.ode_status = counts
+        compute_ode.ode_tables = tables
         compute_ode.last_chunk = np.zeros(8, dtype=np.int64)
         return compute_ode
 
@@ -722,6 +726,10 @@ def main(argv=None):
         summ["n_gpus"] = world
         if ode_status is not None:
             summ["ode_status"] = ode_status   # ODE-path points per status (non-ok rows are NaN)
+            t = getattr(compute, "ode_tables", None)
+            if t is not None:   # rank 0's chunks computed by this run: shared A/V spline tables or one per point
+                summ["ode_tables"] = dict(t, mode="shared" if t["per_point_chunks"] == 0 else (
+                    "per_point" if t["per_point_chunks"] == t["chunks"] else "mixed"))
         if args.reuse_zsums:
             summ["reuse_zsums"] = eng.last_reuse
         if args.out:

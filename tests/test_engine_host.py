@@ -139,3 +139,18 @@ def test_library_id_is_a_real_digest():
         assert other not in (None, lid, hashlib.sha256(b"").hexdigest()[:16])
     finally:
         os.remove(f.name)
+
+
+def test_bounce_csv_reader_is_the_plugins(tmp_path):
+    """sweep ProfileSpec(csv=...) reads the plug-in's xi,phi,Phi format through the plug-in's own
+    parser (one reader of the format): options, comments, r + R0 positions."""
+    B = pkg("bounce")
+    (tmp_path / "p.csv").write_text("# y_B = 1.0\n# R0 = 2.5\nr,phi,Phi\n2.5,0.1,0.3\n3.0,0.2,0.25\n"
+                                    "# a comment\n3.5,0.3,0.2\n4.0,0.4,0.1\n")
+    xi, a, b, opts = B.read_bounce_csv(str(tmp_path / "p.csv"))
+    assert np.array_equal(xi, [0.0, 0.5, 1.0, 1.5]) and np.array_equal(a, [0.1, 0.2, 0.3, 0.4])
+    assert np.array_equal(b, [0.3, 0.25, 0.2, 0.1]) and opts["y_B"] == 1.0 and opts["R0"] == 2.5
+    (tmp_path / "q.csv").write_text("xi,Delta,m\n0,1,2\n")
+    import pytest
+    with pytest.raises(ValueError):
+        B.read_bounce_csv(str(tmp_path / "q.csv"))

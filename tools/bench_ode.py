@@ -8,6 +8,7 @@ table (Engine.ode share_tables); each case is also timed with a table per point
 JSON line per config.
 
     python tools/bench_ode.py [n_narrow] [n_full] [chunk]
+    python tools/bench_ode.py kernels      # the 4096-kernel Riccati sweep alone
 """
 import importlib
 import json
@@ -131,5 +132,32 @@ def main():
                       "all_ok": bool((st == 0).all())}), flush=True)
 
 
+def kernels_sweep(eng, cfgm, n: int = 262144, chunk: int = 1 << 18):
+    """a 262,144-point ODE sweep with 4096 distinct A/V kernels (I_p x v_w, 64 x 64)
+    x 64 sigma_v values (Riccati, narrow window): Engine.ode shares one spline table per kernel and
+    groups each kernel's 64 points into one cooperative wavefront; the same points with a table per
+    point (share_tables=False) show the per-point-table cost (waves integrate per lane)."""
+    ips, vws = np.linspace(0.1, 1.0, 64), np.linspace(0.1, 0.9, 64)
+    svs = 10.0 ** np.linspace(-20, -11, 64)
+    cfgs = cfgs_for({"T_max_over_Tp": 1.6, "T_min_over_Tp": 0.6}, n)
+    for i, c in enumerate(cfgs):   # sigma_v fastest, then v_w, then I_p (C order)
+        c["I_p"], c["v_w"], c["sigma_v_chi_GeV_m2"] = float(ips[(i // 4096) % 64]), float(vws[(i // 64) % 64]), \
+            float(svs[i % 64])
+    pts = np.concatenate([cfgm.to_point(c) for c in cfgs])
+    ods = np.concatenate([cfgm.to_ode_params(c) for c in cfgs])
+    eng.ode(pts[:4096], ods[:4096])
+    (tab, st), dt = timed(lambda: eng.ode(pts, ods, chunk=chunk))
+    shared = dict(eng.last_ode_tables)
+    (tab_u, st_u), dt_u = timed(lambda: eng.ode(pts, ods, chunk=chunk, share_tables=False), reps=1)
+    print(json.dumps({"config": "riccati_4096_kernels", "points": n, "kernels": 4096, "gpu_points_per_s": n / dt,
+                      "ode_tables": shared, "gpu_points_per_s_table_per_point": n / dt_u,
+                      "ode_tables_unshared": eng.last_ode_tables,
+                      "bit_identical": bool(torch.equal(tab, tab_u)),
+                      "all_ok": bool((st == 0).all()) and bool((st_u == 0).all())}), flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "kernels":
+        kernels_sweep(importlib.import_module(PKG + ".engine").Engine(0), importlib.import_module(PKG + ".config"))
+    else:
+        main()

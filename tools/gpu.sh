@@ -5,6 +5,7 @@
 #   gpurun -- bash tools/gpu.sh profile ROUND             rocprofv3 --kernel-trace --stats of the driver's
 #                                                         bench command, the PMC passes of the headline
 #                                                         kernel, profiles/ROUND summary, then the bench
+#   gpurun -- bash tools/gpu.sh ode-pmc                   ODE integrator PMC + kernel trace (tools/ode_pmc_run.py)
 #   gpurun -- bash tools/gpu.sh bench [bench args ...]    one bench line
 #   gpurun -- bash tools/gpu.sh py SCRIPT [args ...]      any tools/ script (ablations, ODE / profile benches)
 #
@@ -56,6 +57,16 @@ case "$cmd" in
     timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_plain.json" 2> "$OUT/bench_plain.err" \
       || { tail -20 "$OUT/bench_plain.err"; exit 3; }
     cut -c1-600 "$OUT/bench_plain.json"
+    ;;
+  ode-pmc)   # the ODE integrator's instruction mix and kernel time on tools/ode_pmc_run.py's three cases;
+             # summarise with: python tools/summarize_ode_pmc.py gpurun_out/ode-pmc ROUND cases
+    rm -rf "$OUT"; mkdir -p "$OUT"
+    timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 \
+      SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 --output-format csv -d "$OUT/pmc" -o run -- \
+      python3 tools/ode_pmc_run.py > "$OUT/pmc.jsonl" 2> "$OUT/pmc.err" || { tail -5 "$OUT/pmc.err"; exit 1; }
+    timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
+      python3 tools/ode_pmc_run.py > "$OUT/trace.jsonl" 2> "$OUT/trace.err" || { tail -5 "$OUT/trace.err"; exit 2; }
+    cat "$OUT/trace.jsonl"
     ;;
   bench)
     timeout -k 10 600 python3 -u bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 3; }

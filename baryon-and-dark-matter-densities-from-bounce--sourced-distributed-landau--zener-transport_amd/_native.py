@@ -120,6 +120,10 @@ ZSUM_KEY = ("I_p", "beta_over_H", "T_p_GeV", "T_min_over_Tp", "T_max_over_Tp")
 # parameters (ode_stage_base / ode_stage_chi_base + the spline table): points equal in these can
 # share a cooperative wavefront (include/lzq.h LZQ_TUNE_ODE_COOP)
 ODE_STAGE_KEY = ODE_TABLE_KEY + ("m_chi_GeV", "g_chi", "g_star_s", "source_shape_sigma_y", "stats")
+# the stage key without the fields that enter only through the spline table: points equal in these
+# share a cooperative segment even when their tables differ (round 4: each lane then scales the
+# shared rows by its own table's A/V, ode_integrate_kernel tab_vary)
+ODE_COOP_KEY = tuple(f for f in ODE_STAGE_KEY if f not in ("I_p", "v_w"))
 
 
 class LzqError(RuntimeError):

@@ -46,26 +46,42 @@ def synthetic_couplings(n_points: int, n_shapes: int, seed: int = 6):
 
 
 def interval_steps(knots, coef, yB, ychi, lam, vw, spr: float = 4.0, n_min: int = 1,
-                   hdot_rate: float = 4.0) -> np.ndarray:
+                   hdot_rate: float = 4.0, per_interval: bool = False) -> np.ndarray:
     """Magnus steps per point of lzq_lz_propagate_profile (its per-interval rule, vectorised over
-    points; knots [n_knots], coef [n_knots - 1, 8] of ONE shape): the launch's work model."""
+    points; knots [n_knots], coef [n_knots - 1, 8] of ONE shape): the launch's work model.  The
+    kernel's rule (tests/profile_ref.py interval_steps restates it exactly): rates at t = (q/4) L,
+    q = 0..3, and at the interval's end from the next interval's cubic (the last: its own),
+    W2 = max(max E^2, hdot_rate^2 v_w sqrt(max |dH/dt|^2)), S = ceil(spr L / v_w sqrt(W2)).  numpy
+    has no fused multiply-add, so a count can differ from the kernel's where spr L / v_w sqrt(W2)
+    lies within rounding of an integer (reporting only).  per_interval: the [point, interval]
+    counts instead of their sum."""
     total = np.zeros(np.broadcast(yB, ychi, lam, vw).shape)
-    for j in range(len(knots) - 1):
+    cols = []
+    ivw = 1.0 / np.asarray(vw, dtype=float)
+    nI = len(knots) - 1
+
+    def rates(j, t):
+        a = coef[j, 0] + t * (coef[j, 1] + t * (coef[j, 2] + t * coef[j, 3]))
+        b = coef[j, 4] + t * (coef[j, 5] + t * (coef[j, 6] + t * coef[j, 7]))
+        da = coef[j, 1] + t * (2.0 * coef[j, 2] + t * 3.0 * coef[j, 3])
+        db = coef[j, 5] + t * (2.0 * coef[j, 6] + t * 3.0 * coef[j, 7])
+        D, m = yB * a - ychi * b, lam * a
+        Dd, md = yB * da - ychi * db, lam * da
+        return D * D + m * m, Dd * Dd + md * md
+
+    for j in range(nI):
         L = knots[j + 1] - knots[j]
         e2, h2 = np.zeros_like(total), np.zeros_like(total)
-        for f in (0.0, 0.25, 0.5, 0.75, 1.0):
-            t = f * L
-            a = coef[j, 0] + t * (coef[j, 1] + t * (coef[j, 2] + t * coef[j, 3]))
-            b = coef[j, 4] + t * (coef[j, 5] + t * (coef[j, 6] + t * coef[j, 7]))
-            da = coef[j, 1] + t * (2.0 * coef[j, 2] + t * 3.0 * coef[j, 3])
-            db = coef[j, 5] + t * (2.0 * coef[j, 6] + t * 3.0 * coef[j, 7])
-            D, m = yB * a - ychi * b, lam * a
-            Dd, md = yB * da - ychi * db, lam * da
-            e2 = np.maximum(e2, D * D + m * m)
-            h2 = np.maximum(h2, Dd * Dd + md * md)
-        w = np.maximum(np.sqrt(e2), hdot_rate * np.sqrt(vw * np.sqrt(h2)))
-        total += np.maximum(n_min, np.ceil(spr * (L / vw) * w))
-    return total
+        pts = [(j, (0.25 * q) * L) for q in range(4)] + [(j + 1, 0.0) if j + 1 < nI else (j, L)]
+        for jj, t in pts:
+            e, h = rates(jj, t)
+            e2, h2 = np.maximum(e2, e), np.maximum(h2, h)
+        W2 = np.maximum(e2, (hdot_rate * hdot_rate) * (vw * np.sqrt(h2)))
+        Sj = np.maximum(n_min, np.ceil((spr * (L * ivw)) * np.sqrt(W2)))
+        total += Sj
+        if per_interval:
+            cols.append(Sj)
+    return np.stack(cols, axis=-1) if per_interval else total
 
 
 def _plugin_reader():

@@ -106,15 +106,24 @@ __device__ __forceinline__ OdePoint ode_point(const lzq_point& pt, const lzq_ode
 // interval k with T_k <= T < T_{k+1}, T == T_hi in the last one; c3 + c2 s + c1 s^2 + c0 s^3
 // accumulated in that order, powers by repeated multiplication).  nt: the table's knot count
 // (the integrators read main()'s LZQ_ODE_NT tables; the operator kernel any build_tables n).
-__device__ __forceinline__ double spline_eval(const OdePoint& o, const double* __restrict__ w, double T,
-                                              int nt = kOdeNT) {
+// Split into the interval search, which depends on the point only through its window (shared by
+// the cooperative segments, whose points agree in it), and the cubic of one table.
+struct SplineLoc {
+  double s;  // T - T_k
+  int k;     // interval
+};
+
+__device__ __forceinline__ SplineLoc spline_loc(const OdePoint& o, double T, int nt = kOdeNT) {
   const double Tq = pymin(pymax(T, o.T_lo), o.T_hi);
   int k = (int)((Tq - o.T_lo) * o.inv_stepT);
   k = k < 0 ? 0 : (k > nt - 2 ? nt - 2 : k);
   // the quotient can land one knot off after rounding: settle against the knots themselves
   if (Tq < linspace_at(o.T_lo, o.T_hi, o.stepT, k, nt) && k > 0) --k;
   else if (k < nt - 2 && Tq >= linspace_at(o.T_lo, o.T_hi, o.stepT, k + 1, nt)) ++k;
-  const double s = Tq - linspace_at(o.T_lo, o.T_hi, o.stepT, k, nt);
+  return {Tq - linspace_at(o.T_lo, o.T_hi, o.stepT, k, nt), k};
+}
+
+__device__ __forceinline__ double spline_at(const double* __restrict__ w, double s, int k) {
   const double* c = w + 4 * k;
   const double c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3];
   if (LZQ_ODE_FMA) return __builtin_fma(__builtin_fma(__builtin_fma(c0, s, c1), s, c2), s, c3);  // Horner, 3 fma
@@ -125,6 +134,12 @@ __device__ __forceinline__ double spline_eval(const OdePoint& o, const double* _
   z = z * s;
   res = res + c0 * z;
   return res;
+}
+
+__device__ __forceinline__ double spline_eval(const OdePoint& o, const double* __restrict__ w, double T,
+                                              int nt = kOdeNT) {
+  const SplineLoc l = spline_loc(o, T, nt);
+  return spline_at(w, l.s, l.k);
 }
 
 
@@ -160,9 +175,14 @@ struct OdeStage {
 // unit sigma_v, beta per unit gamma_w.  Points that differ only in those scalars (and in their
 // initial state) share these values -- the cooperative mode of ode_integrate_kernel computes
 // them once per step for a whole wavefront.  Every stage goes through this split, so a point's
-// result does not depend on which mode its wavefront ran in.
+// result does not depend on which mode its wavefront ran in.  a = Av * ap: the A/V spline value
+// times the rest of the source term, so points that differ also in the A/V kernel (I_p, v_w: their
+// own spline tables) share ap and the spline location (s, k) and form a from their own table.
 struct StageBase {
   double a, lam, E2, beta;
+  double ap;  // a / Av
+  double s;   // spline location of the stage's T (spline_loc)
+  int k;
 };
 
 __device__ __forceinline__ StageBase ode_stage_base(const OdePoint& o, const double* __restrict__ w, double x,
@@ -193,16 +213,20 @@ __device__ __forceinline__ StageBase ode_stage_base(const OdePoint& o, const dou
     vbar = sqrt(pymax(8.0 * T * o.inv_v0, 0.0));
   }
   const double Jb = 0.25 * n_eq * vbar;                       // fpy:222-223, J / flux
-  const double Av = spline_eval(o, w, T, nt);                 // fpy:214-218
+  const SplineLoc loc = spline_loc(o, T, nt);
+  const double Av = spline_at(w, loc.s, loc.k);               // fpy:214-218
   if (Av_out) *Av_out = Av;
-  const double SBb = (Jb * Av) * window;                      // fpy:277, SB / (P flux)
+  const double SBb = Jb * window;                             // fpy:277, SB / (P flux Av)
   const bool plain = H > 1e-290 && s > 1e-290 && x == xc;     // the max() guards are inactive
   const double iT2 = iT * iT;
   const double is = plain ? (iT2 * iT) * o.inv_s0 : 1.0 / s;
   const double E = n_eq * is;                                 // fpy:280
   const double iHx = plain ? (o.mpl_over_h0 * iT2) * ixc : 1.0 / (H * x);
   StageBase b;
-  b.a = (SBb * is) * iHx;                                     // fpy:282, 285
+  b.ap = (SBb * is) * iHx;
+  b.a = Av * b.ap;                                            // fpy:282, 285
+  b.s = loc.s;
+  b.k = loc.k;
   b.lam = s * iHx;                                            // fpy:279-281
   b.E2 = E * E;
   b.beta = H * iHx;                                           // fpy:284-285
@@ -247,6 +271,9 @@ __device__ __forceinline__ StageBase ode_stage_chi_base(const OdePoint& o, doubl
   const double iHx = plain ? (o.mpl_over_h0 * iT2) * ixc : 1.0 / (H * x);
   StageBase b;
   b.a = 0.0;
+  b.ap = 0.0;
+  b.s = 0.0;
+  b.k = 0;
   b.lam = s * iHx;
   b.E2 = E * E;
   b.beta = 0.0;
@@ -428,7 +455,14 @@ __device__ __forceinline__ void solve3_adj(const double (&M)[3][3], double (&b)[
 // on the mode.
 struct YbRec {
   double c, d;
+  double W[3], id;  // d = (sum_j W_j a_j) id: a lane whose a_j differ from the segment's forms its own d (yb_d)
 };
+__device__ __forceinline__ double yb_d(const YbRec& r, const double (&a)[3]) {
+  double d = 0.0;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) d = __builtin_fma(r.W[j], a[j], d);
+  return d * r.id;
+}
 __device__ __forceinline__ YbRec yb_rec(const RadauH& hA, const double (&beta)[3], const double (&a)[3]) {
   double M[3][3];
 #pragma unroll
@@ -440,12 +474,13 @@ __device__ __forceinline__ YbRec yb_rec(const RadauH& hA, const double (&beta)[3
   const double w2 = M[0][0] * M[1][1] - M[0][1] * M[1][0];
   const double det = M[0][0] * (M[1][1] * M[2][2] - M[1][2] * M[2][1]) -
                      M[0][1] * (M[1][0] * M[2][2] - M[1][2] * M[2][0]) + M[0][2] * w0;
-  const double id = 1.0 / det;
-  double d = 0.0;
+  YbRec r;
+  r.id = 1.0 / det;
 #pragma unroll
-  for (int j = 0; j < 3; ++j)
-    d = __builtin_fma(__builtin_fma(w2, hA.a[2][j], __builtin_fma(w1, hA.a[1][j], w0 * hA.a[0][j])), a[j], d);
-  return {((w0 + w1) + w2) * id, d * id};
+  for (int j = 0; j < 3; ++j) r.W[j] = __builtin_fma(w2, hA.a[2][j], __builtin_fma(w1, hA.a[1][j], w0 * hA.a[0][j]));
+  r.c = ((w0 + w1) + w2) * r.id;
+  r.d = yb_d(r, a);
+  return r;
 }
 __device__ __forceinline__ YbRec yb_rec(const RadauH& hA, const OdeStage (&st)[3]) {
   const double beta[3] = {st[0].beta, st[1].beta, st[2].beta}, a[3] = {st[0].a, st[1].a, st[2].a};
@@ -475,6 +510,9 @@ __constant__ double kRadauAinvP[9] = {-0x1.fbb0962b0c0cap+2, 0x1.e8360f1027593p+
                                       0x1.adf74aa6f6bf3p+4,  0x1.9d782ab97a58ap+2,  -0x1.0aaaaaaaaaaabp+2};
 #ifndef LZQ_ODE_TNEWTON
 #define LZQ_ODE_TNEWTON 1  // the Riccati Newton iteration in the transformed form (constant off-diagonals)
+#endif
+#ifndef LZQ_ODE_NEWTON_RCP
+#define LZQ_ODE_NEWTON_RCP 1  // the Newton solve's 1/det by rcp_pos (5 VALU) instead of the IEEE quotient (~14)
 #endif
 
 // Zs: in, Newton starting stages when `guess` (else Ychi for all three); out, the converged
@@ -544,18 +582,22 @@ __device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st
     const double b11 = FMA(k[0], k[2], -kRadauAinvP[4]), b12 = FMA(-kRadauAinv[1][2], k[0], kRadauAinvP[5]);
     const double b20 = FMA(-kRadauAinv[2][0], k[1], kRadauAinvP[6]), b21 = FMA(-kRadauAinv[2][1], k[0], kRadauAinvP[7]);
     const double b22 = FMA(k[0], k[1], -kRadauAinvP[8]);
-    const double id = 1.0 / FMA(k[0], b00, FMA(kRadauAinv[0][1], b10, kRadauAinv[0][2] * b20));
+    // 1/det only scales the correction: a reciprocal within 1 ulp leaves the fixed point (the
+    // stage equations) as it is and changes the iterates by rounding
+    const double den = FMA(k[0], b00, FMA(kRadauAinv[0][1], b10, kRadauAinv[0][2] * b20));
+    const double id = LZQ_ODE_NEWTON_RCP ? rcp_pos(den) : 1.0 / den;
     double g[3];
     g[0] = FMA(b00, r[0], FMA(b01, r[1], b02 * r[2])) * id;
     g[1] = FMA(b10, r[0], FMA(b11, r[1], b12 * r[2])) * id;
     g[2] = FMA(b20, r[0], FMA(b21, r[1], b22 * r[2])) * id;
 #undef FMA
+    // running maxima from +0 of |.| (never NaN on the left): fmax is pymax here, one v_max_f64
     double dmax = 0.0, zmax = 0.0;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       Z[i] = Z[i] + g[i];
-      dmax = pymax(dmax, fabs(g[i]));
-      zmax = pymax(zmax, fabs(Z[i]));
+      dmax = fmax(dmax, fabs(g[i]));
+      zmax = fmax(zmax, fabs(Z[i]));
     }
     return !(dmax > 1e-15 * zmax);
   };
@@ -588,8 +630,8 @@ __device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       Z[i] = Z[i] + g[i];
-      dmax = pymax(dmax, fabs(g[i]));
-      zmax = pymax(zmax, fabs(Z[i]));
+      dmax = fmax(dmax, fabs(g[i]));
+      zmax = fmax(zmax, fabs(Z[i]));
     }
     return !(dmax > 1e-15 * zmax);
   };
@@ -829,6 +871,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
     // split there, ending one ulp before it, so no stage sees both branches (the oracle does
     // the same with its own T; tests/golden/golden_ode_stiff.json).
     const double xb = branch_x(o, x0, x1);
+    const double xb_below = nextafter(xb, -INFINITY);  // where a split step's first part ends
     const RadauH hA = radau_h(R, h);
     const bool riccati = LZQ_ODE_PREDICT && !kLin && o.sigmav != 0.0;  // kLin: sigma_v = 0 on every lane
     double Zs[3] = {Ychi, Ychi, Ychi}, Yp = Ychi;  // previous step's start and stages (predictor)
@@ -856,8 +899,13 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
     // runs the same scheme per segment: lane l of a segment evaluates step kb + l of ITS
     // segment's key into its own LDS row, and the segment integrates blocks of G steps from its G
     // rows (segments may differ in N and h; they never touch each other's rows).
+    // Table-varying segments (round 4): points that agree in all of that but the A/V kernel
+    // (I_p, v_w: each has its own spline table) share the rows too; the rows then carry a / Av
+    // and the spline location (StageBase ap, s, k), and each lane forms a = Av * ap from its own
+    // table -- the operations ode_stage_base performs, so still the per-lane bits.
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    int G = 0;  // cooperative segment width (0: per-lane)
+    int G = 0;             // cooperative segment width (0: per-lane)
+    bool tab_vary = false;  // the segment's points read different spline tables
     if (LZQ_ODE_COOP && coop_on && __ballot(1) == ~0ull) {
       for (int g = 64; g >= LZQ_ODE_MIN_GROUP && G == 0; g >>= 1) {
         auto same = [g](double v) {  // bit-equal to the value of the first lane of the g-segment
@@ -866,15 +914,20 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
         };
         const bool eq = same(o.m) && same(o.Tp) && same(o.B) && same(o.sig) && same(o.H0) && same(o.s0) &&
                         same(o.c_rel) && same(o.c_nr) && same(o.v0) && same(o.T_lo) && same(o.T_hi) &&
-                        same(__builtin_bit_cast(double, w)) && (!kChiOnly || same((double)o.deplete));
-        if (__all(eq)) G = g;
+                        (!kChiOnly || same((double)o.deplete));
+        if (__all(eq)) {
+          G = g;
+          tab_vary = !__all(same(__builtin_bit_cast(double, w)));
+        }
       }
 #ifdef LZQ_ODE_COOP_DEBUG
-      dbg_coop = (double)G;
+      dbg_coop = (double)G + (tab_vary ? 0.5 : 0.0);
 #endif
     }
     const bool coop = G > 0;
     const int seg = lane & ~(G - 1);  // first LDS row of this lane's segment (G > 0)
+    // this lane's a of a shared row's stage (its own table in a table-varying segment)
+    auto row_a = [&](const StageBase& b) -> double { return tab_vary ? spline_at(w, b.s, b.k) * b.ap : b.a; };
     // Y_B's step maps shared by the segment when it has one Gamma_wash (LZQ_ODE_YBREC)
     bool rec_shared = false;
     if (LZQ_ODE_YBREC && !kChiOnly && coop) {
@@ -936,7 +989,8 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
             s_base[wv][lane][j] = bs[j];
           }
           if (LZQ_ODE_YBREC && !kChiOnly && rec_shared) {
-            // beta_j as stage_scale forms it (Gamma_wash * base), a_j the base: the step map
+            // beta_j as stage_scale forms it (Gamma_wash * base), a_j the base: the step map (its d
+            // is this lane's; a table-varying segment's lanes form theirs from W and id)
             const double beta[3] = {o.gamma_w * bs[0].beta, o.gamma_w * bs[1].beta, o.gamma_w * bs[2].beta};
             const double a[3] = {bs[0].a, bs[1].a, bs[2].a};
             s_rec[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][lane] = yb_rec(hA, beta, a);
@@ -955,7 +1009,20 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
           if (nf > 0) {
             const int r0 = seg + (int)(k - kb);
             const YbRec* rr = &s_rec[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][r0];
-            if (o.deplete) {
+            if (tab_vary) {  // each step's a_j from this lane's table, then its own d
+              for (int jj = 0; jj < nf; ++jj) {
+                double a[3];
+#pragma unroll
+                for (int j = 0; j < 3; ++j) a[j] = row_a(s_base[wv][r0 + jj][j]);
+                YB = __builtin_fma(rr[jj].c, YB, o.Pf * yb_d(rr[jj], a));
+                if (o.deplete) {
+                  double acc = Ychi;
+#pragma unroll
+                  for (int j = 0; j < 3; ++j) acc = __builtin_fma(-hA.a[2][j], o.Pf * a[j], acc);
+                  Ychi = acc;
+                }
+              }
+            } else if (o.deplete) {
               for (int jj = 0; jj < nf; ++jj) {
                 YB = __builtin_fma(rr[jj].c, YB, o.Pf * rr[jj].d);
                 double acc = Ychi;
@@ -973,7 +1040,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
         }
         const double xk = x0 + (double)k * h;
         const bool split = xk < xb && xb <= xk + h;  // the last stage (x = xk + h) would see the other branch
-        const double xa = split ? nextafter(xb, -INFINITY) : xk + h;
+        const double xa = split ? xb_below : xk + h;
         double YB_prev = YB;
         bool ok = true;
         const double Ystart = Ychi;
@@ -999,17 +1066,27 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
           OdeStage sg[3];
           if (coop && !split) {
 #pragma unroll
-            for (int j = 0; j < 3; ++j)
-              sg[j] = (kChiOnly && !o.deplete) ? chi_scale(o, s_base[wv][seg + (k - kb)][j])
-                                               : stage_scale(o, s_base[wv][seg + (k - kb)][j]);
+            for (int j = 0; j < 3; ++j) {
+              StageBase b = s_base[wv][seg + (k - kb)][j];
+              if (!(kChiOnly && !o.deplete)) b.a = row_a(b);
+              sg[j] = (kChiOnly && !o.deplete) ? chi_scale(o, b) : stage_scale(o, b);
+            }
           } else {
 #pragma unroll
             for (int j = 0; j < 3; ++j)
               sg[j] = (kChiOnly && !o.deplete) ? ode_stage_chi(o, xk + R.c[j] * hs) : ode_stage(o, w, xk + R.c[j] * hs);
           }
           if (LZQ_ODE_YBREC && !kChiOnly) {  // Y_B by its step map, then Y_chi alone
-            const YbRec r = (rec_shared && !split) ? s_rec[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][seg + (k - kb)]
-                                                   : yb_rec(split ? radau_h(R, hs) : hA, sg);
+            YbRec r;
+            if (rec_shared && !split) {
+              r = s_rec[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][seg + (k - kb)];
+              if (tab_vary) {
+                const double a[3] = {sg[0].a, sg[1].a, sg[2].a};
+                r.d = yb_d(r, a);
+              }
+            } else {
+              r = yb_rec(split ? radau_h(R, hs) : hA, sg);
+            }
             YB = __builtin_fma(r.c, YB, o.Pf * r.d);
             ok = radau_step<false>(split ? radau_h(R, hs) : hA, sg, Ychi, YB, Zs, use_guess);
           } else {

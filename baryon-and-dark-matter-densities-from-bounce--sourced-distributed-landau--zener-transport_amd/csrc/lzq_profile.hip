@@ -34,13 +34,15 @@
 //                               in registers; the shape's rows are read once per interval, and
 //                               the lanes of a wave read the same rows (L1/L2 hits: staging them
 //                               in LDS per block, LZQ_PROF_LDS=1, measured 5% slower).  Large
-//                               batches launch cost-ordered (profile_cost_kernel).
+//                               batches launch in (shape, cost, coupling angle) order
+//                               (profile_key_kernel + a radix sort).
 // tests/profile_ref.py restates all three in numpy; tests/test_gpu_profile.py checks them.
 #include <hip/hip_runtime.h>
 
 #include <math.h>
 
 #include <algorithm>
+#include <hipcub/hipcub.hpp>
 
 #include "../../include/lzq.h"
 #include "lzq_internal.h"
@@ -65,7 +67,7 @@ constexpr int kProfBlock = 256;
 #define LZQ_PROF_UNROLL 1  // Magnus steps per loop iteration (A/B: 2 is 4% slower, tools/ablate_profile.py)
 #endif
 #ifndef LZQ_PROF_SORT
-#define LZQ_PROF_SORT 1  // cost-ordered launch for batches of >= kProfSortMin points (0: index order)
+#define LZQ_PROF_SORT 1  // keyed launch order for batches of >= kProfSortMin points (0: index order)
 #endif
 constexpr int64_t kProfSortMin = 16384;
 constexpr int kProfCostStride = 4;  // the launch-order cost model samples every 4th knot interval
@@ -94,6 +96,18 @@ __device__ __forceinline__ void interval_coefs(const double* __restrict__ row, c
   for (int k = 0; k < 4; ++k) {
     const double a = row[k], b = row[4 + k];
     cD[k] = p.yB * a - p.ychi * b;
+    cM[k] = p.lam * a;
+  }
+}
+
+// the same for the propagation (fused: D_k = fma(y_B, phi_k, -(y_chi Phi_k)), 8 VALU fewer per
+// interval entry; the crossings keep interval_coefs, the restatement's operations)
+__device__ __forceinline__ void interval_coefs_fma(const double* __restrict__ row, const ProfPt& p, double* cD,
+                                                   double* cM) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const double a = row[k], b = row[4 + k];
+    cD[k] = __builtin_fma(p.yB, a, -(p.ychi * b));
     cM[k] = p.lam * a;
   }
 }
@@ -349,7 +363,14 @@ struct StepGeom {
 __device__ __forceinline__ StepGeom step_geom(double L, double Sd, double ivw) {
   constexpr double g1 = 0.5 - kSq15 / 10.0, g3 = 0.5 + kSq15 / 10.0;
   StepGeom g;
-  g.h = L / Sd;
+  // h = L / S by a refined reciprocal (<= 1 ulp from the quotient; the restatement divides): S is
+  // an integer >= 1, so v_rcp_f64 + two Newton steps
+  double r = __builtin_amdgcn_rcp(Sd);
+  double e = __builtin_fma(-Sd, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-Sd, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  g.h = L * r;
   g.dt = g.h * ivw;
   g.k2 = (kSq15 / 3.0) * g.dt;
   g.k3 = (10.0 / 3.0) * g.dt;
@@ -416,58 +437,97 @@ __global__ __launch_bounds__(kProfBlock) void profile_samples_kernel(const doubl
   }
 }
 
-// uniform Magnus steps on one interval (tests/profile_ref.py interval_steps): the largest E^2
-// and |dH/dt|^2 over the samples, then the square roots once (sqrt is monotone and correctly
-// rounded, so this equals the restatement's max of the roots)
-__device__ __forceinline__ double interval_steps(const double* __restrict__ sr, const ProfPt& p, double L, double vw,
-                                                 double spr, int32_t n_min) {
-  double e2 = 0.0, h2 = 0.0;
+// Uniform Magnus steps on one interval (tests/profile_ref.py interval_steps).  The rate is
+// sampled at t_q = (q/4) L, q = 0..3, from the interval's own samples and at its end from the NEXT
+// interval's q = 0 sample (the same knot, whose spline value every interval but the last takes
+// from the next piece; the last takes its own q = 4): a lane walking the intervals in order carries
+// that end sample over as the next interval's start, 4 new samples per interval instead of 5.
+// Per sample E^2 = D^2 + m^2 and |dH/dt|^2 = D'^2 + m'^2 (D = y_B phi - y_chi Phi, m = lambda phi,
+// fused multiply-adds); over the interval their maxima e2, h2, then in squares
+//   W2 = max(e2, kHdotRate^2 v_w sqrt(h2)),  S = max(n_min, ceil(spr (L (1/v_w)) sqrt(W2)))
+// -- max(E, kHdotRate sqrt(v_w |dH/dt|)) squared: two correctly rounded square roots, no division.
+struct Rates {
+  double e2, h2;
+};
+
+__device__ __forceinline__ Rates sample_rates(const double* __restrict__ sr, const ProfPt& p) {
+  const double a = sr[0], b = sr[1], da = sr[2], db = sr[3];
+  const double D = __builtin_fma(p.yB, a, -(p.ychi * b)), m = p.lam * a;
+  const double Dd = __builtin_fma(p.yB, da, -(p.ychi * db)), md = p.lam * da;
+  return {__builtin_fma(D, D, m * m), __builtin_fma(Dd, Dd, md * md)};
+}
+
+__device__ __forceinline__ Rates rates_max(Rates u, Rates v) { return {fmax(u.e2, v.e2), fmax(u.h2, v.h2)}; }
+
+// the end sample of interval j (of K - 1): the next interval's q = 0, or the last interval's own q = 4
+__device__ __forceinline__ const double* end_sample(const double* __restrict__ sm, int j, int K) {
+  return j + 2 < K ? sm + (j + 1) * kProfSamp : sm + j * kProfSamp + 16;
+}
+
+// interval j's rates from its start sample's (`start`, carried) and its q = 1..3 and end samples;
+// `end` returns the end sample's rates (the next interval's start)
+__device__ __forceinline__ Rates interval_rates(const double* __restrict__ sm, int j, int K, const ProfPt& p,
+                                                Rates start, Rates& end) {
+  const double* sr = sm + j * kProfSamp;
+  Rates r = start;
 #pragma unroll
-  for (int q = 0; q < 5; ++q) {
-    const double a = sr[4 * q], b = sr[4 * q + 1], da = sr[4 * q + 2], db = sr[4 * q + 3];
-    const double D = p.yB * a - p.ychi * b, m = p.lam * a;
-    const double Dd = p.yB * da - p.ychi * db, md = p.lam * da;
-    e2 = fmax(e2, D * D + m * m);
-    h2 = fmax(h2, Dd * Dd + md * md);
-  }
-  const double w = fmax(sqrt(e2), kHdotRate * sqrt(vw * sqrt(h2)));
-  return fmax((double)n_min, ceil(spr * (L / vw) * w));
+  for (int q = 1; q < 4; ++q) r = rates_max(r, sample_rates(sr + 4 * q, p));
+  end = sample_rates(end_sample(sm, j, K), p);
+  return rates_max(r, end);
+}
+
+__device__ __forceinline__ double steps_of(Rates r, double L, const ProfPt& p, double ivw, double spr, int32_t n_min) {
+  const double W2 = fmax(r.e2, (kHdotRate * kHdotRate) * (p.vw * sqrt(r.h2)));
+  return fmax((double)n_min, ceil((spr * (L * ivw)) * sqrt(W2)));
+}
+
+// interval j on its own (no carried start): the same samples and operations, the same count
+__device__ __forceinline__ double interval_steps(const double* __restrict__ sm, int j, int K, const ProfPt& p,
+                                                 double L, double ivw, double spr, int32_t n_min) {
+  Rates end;
+  const Rates r = interval_rates(sm, j, K, p, sample_rates(sm + j * kProfSamp, p), end);
+  return steps_of(r, L, p, ivw, spr, n_min);
 }
 
 // Launch order.  A lane's cost is its Magnus step count, which scales as 1/v_w and with the
 // couplings, so a wave of random points waits on its slowest lane in every knot interval.  For
-// large batches the points are binned by an estimate of their step count (the step rule on every
-// kProfCostStride-th interval, x kProfCostStride; 4 bins per octave), laid out longest-first by
-// the counting sort shared with lzq_lz_propagate, and the kernel reads its point index from that
-// order.  Each lane still computes one point from its own inputs, so P is bit-identical to index
-// order.
-__global__ __launch_bounds__(kProfBlock) void profile_cost_kernel(const double* __restrict__ knots, int32_t n_shapes,
-                                                                  int32_t K, const lzq_profile_point* __restrict__ pts,
-                                                                  int64_t n, double spr, int32_t n_min,
-                                                                  const double* __restrict__ samp,
-                                                                  int32_t* __restrict__ bins, int32_t* __restrict__ hist) {
-  __shared__ int32_t lh[kCostBins];
-  for (int t = threadIdx.x; t < kCostBins; t += kProfBlock) lh[t] = 0;
-  __syncthreads();
+// large batches the kernel reads its point index from a launch order; each lane still computes
+// one point from its own inputs, so P is bit-identical to index order.  The estimate of a point's
+// step count: the step rule on every kProfCostStride-th interval, x kProfCostStride, 4 bins per
+// octave (0 = costliest).
+// Launch key of the interval loop (round 4): the loop kernel steps a wave through interval j for
+// its lanes' largest S_j, so lanes should agree in the whole step PROFILE, not only in the total.
+// Points of one shape whose totals are close and whose couplings put Delta's zeros at the same
+// places (Delta = y_B phi - y_chi Phi vanishes where phi / Phi = y_chi / y_B: the angle
+// atan(y_chi / y_B)) have nearly the same S_j, so the key is (shape, cost bin, angle bin), radix
+// sorted (stable) -- tools/profile_order_model.py: executed / useful lane-steps 1.31 with the cost
+// bins alone, 1.16 with this key, on tools/bench_profile.py's workload.
+constexpr int kAngleBins = 256;
+__global__ __launch_bounds__(kProfBlock) void profile_key_kernel(const double* __restrict__ knots, int32_t n_shapes,
+                                                                 int32_t K, const lzq_profile_point* __restrict__ pts,
+                                                                 int64_t n, double spr, int32_t n_min,
+                                                                 const double* __restrict__ samp,
+                                                                 uint32_t* __restrict__ keys, int32_t* __restrict__ idx) {
   const int64_t i = (int64_t)blockIdx.x * kProfBlock + threadIdx.x;
-  if (i < n) {
-    const ProfPt p = load_point(pts + i);
-    double st = 0.0;
-    if (p.vw > 0.0 && p.shape >= 0 && p.shape < n_shapes) {
-      const double* x = knots + (int64_t)p.shape * K;
-      const double* sm = samp + (int64_t)p.shape * (K - 1) * kProfSamp;
-      for (int j = 0; j + 1 < K; j += kProfCostStride)
-        st += interval_steps(sm + j * kProfSamp, p, x[j + 1] - x[j], p.vw, spr, n_min);
-      st *= kProfCostStride;
-    }
-    const double key = st == st ? fmin(fmax(4.0 * log2(1.0 + st), 0.0), (double)(kCostBins - 1)) : 0.0;
-    const int32_t b = (kCostBins - 1) - (int32_t)key;
-    bins[i] = b;
-    atomicAdd(&lh[b], 1);
+  if (i >= n) return;
+  const ProfPt p = load_point(pts + i);
+  double st = 0.0;
+  const bool valid = p.vw > 0.0 && p.shape >= 0 && p.shape < n_shapes;
+  if (valid) {
+    const double* x = knots + (int64_t)p.shape * K;
+    const double* sm = samp + (int64_t)p.shape * (K - 1) * kProfSamp;
+    const double ivw = 1.0 / p.vw;
+    for (int j = 0; j + 1 < K; j += kProfCostStride) st += interval_steps(sm, j, K, p, x[j + 1] - x[j], ivw, spr, n_min);
+    st *= kProfCostStride;
   }
-  __syncthreads();
-  for (int t = threadIdx.x; t < kCostBins; t += kProfBlock)
-    if (lh[t]) atomicAdd(&hist[t], lh[t]);
+  const double cb = st == st ? fmin(fmax(4.0 * log2(1.0 + st), 0.0), (double)(kCostBins - 1)) : 0.0;
+  const uint32_t cost = (uint32_t)((kCostBins - 1) - (int32_t)cb);  // 0 = costliest
+  const double ang = atan(p.ychi / p.yB);                            // (-pi/2, pi/2); NaN for 0/0
+  const double af = ang == ang ? (ang * (1.0 / 3.141592653589793) + 0.5) * kAngleBins : 0.0;
+  const uint32_t ab = (uint32_t)fmin(fmax(af, 0.0), (double)(kAngleBins - 1));
+  const uint32_t sh = valid ? (uint32_t)min(p.shape, 65535) : 65535u;
+  keys[i] = (sh << 15) | (cost << 8) | ab;  // 16 + 7 + 8 bits
+  idx[i] = (int32_t)i;
 }
 
 __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_propagate_kernel(
@@ -505,14 +565,17 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_propag
   const double ivw = 1.0 / p.vw;
 
   double cD[4], cM[4];
-  interval_coefs(cf, p, cD, cM);
+  interval_coefs_fma(cf, p, cD, cM);
   Cplx p0, p1;
   edge_state(cD, cM, 0.0, p.vw, p0, p1);
   double L = 0.0;
+  Rates start = sample_rates(sm, p);  // interval 0's q = 0; then each interval's end is the next one's start
   for (int j = 0; j + 1 < K; ++j) {
-    if (j > 0) interval_coefs(cf + j * kProfCoef, p, cD, cM);
+    if (j > 0) interval_coefs_fma(cf + j * kProfCoef, p, cD, cM);
     L = x[j + 1] - x[j];
-    const double Sd = interval_steps(sm + j * kProfSamp, p, L, p.vw, spr, n_min);
+    Rates end;
+    const double Sd = steps_of(interval_rates(sm, j, K, p, start, end), L, p, ivw, spr, n_min);
+    start = end;
     if (!(Sd <= kMaxIntervalSteps)) {  // non-finite or absurd input
       P_out[i] = __builtin_nan("");
       return;
@@ -565,8 +628,12 @@ __global__ __launch_bounds__(kProfBlock) void profile_steps_kernel(const double*
       const double* x = knots + (int64_t)p.shape * K;
       const double* sm = samp + (int64_t)p.shape * (K - 1) * kProfSamp;
       uint16_t* row = steps + i * (int64_t)(K - 1);
+      const double ivw = 1.0 / p.vw;
+      Rates start = sample_rates(sm, p);
       for (int j = 0; j + 1 < K; ++j) {
-        const double Sd = interval_steps(sm + j * kProfSamp, p, x[j + 1] - x[j], p.vw, spr, n_min);
+        Rates end;
+        const double Sd = steps_of(interval_rates(sm, j, K, p, start, end), x[j + 1] - x[j], p, ivw, spr, n_min);
+        start = end;
         row[j] = !(Sd <= kMaxIntervalSteps) ? (uint16_t)0 : (Sd < (double)kStepsRecompute ? (uint16_t)Sd : kStepsRecompute);
         tot += Sd;
       }
@@ -602,7 +669,7 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_flat_k
   const uint16_t* srow = steps + i * (int64_t)(K - 1);
   const double ivw = 1.0 / p.vw;
   double cD[4], cM[4];
-  interval_coefs(cf, p, cD, cM);
+  interval_coefs_fma(cf, p, cD, cM);
   Cplx p0, p1;
   edge_state(cD, cM, 0.0, p.vw, p0, p1);
   // interval j's step count and geometry; false for a non-finite / absurd count (P = NaN)
@@ -612,7 +679,7 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_flat_k
   auto enter = [&](int j) -> bool {
     L = x[j + 1] - x[j];
     const uint16_t sr = srow[j];
-    const double Sd = sr == kStepsRecompute ? interval_steps(sm + j * kProfSamp, p, L, p.vw, spr, n_min) : (double)sr;
+    const double Sd = sr == kStepsRecompute ? interval_steps(sm, j, K, p, L, ivw, spr, n_min) : (double)sr;
     if (sr == 0 || !(Sd <= kMaxIntervalSteps)) return false;
     S = (int)Sd;
     g = step_geom(L, Sd, ivw);
@@ -623,7 +690,7 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_flat_k
   while (ok) {
     if (st == S) {  // this lane's interval is done: enter the next one (the others keep stepping)
       if (++j == K - 1) break;
-      interval_coefs(cf + j * kProfCoef, p, cD, cM);
+      interval_coefs_fma(cf + j * kProfCoef, p, cD, cM);
       ok = enter(j);
       if (!ok) break;
       st = 0;
@@ -642,7 +709,7 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_flat_k
   P_out[i] = 1.0 - (a.re * a.re + a.im * a.im) / norm;
 }
 
-int g_profile_flat = 1;  // lzq_tune(LZQ_TUNE_PROFILE_FLAT)
+int g_profile_flat = 0;  // lzq_tune(LZQ_TUNE_PROFILE_FLAT): the interval loop is the default
 
 }  // namespace lzq
 
@@ -753,22 +820,29 @@ extern "C" int lzq_lz_propagate_profile(const double* d_knots, const double* d_c
     return LZQ_OK;
   }
   const int64_t nb = (n + lzq::kProfBlock - 1) / lzq::kProfBlock;
-  // cost-ordered launch (profile_cost_kernel): bins, order, histogram, offsets in one scratch
-  int32_t* ws = nullptr;
+  // launch order (profile_key_kernel): keys and indices, their sorted copies and the radix sort's
+  // temporary storage in one scratch
+  char* ws = nullptr;
   const int32_t* order = nullptr;
   int rc = LZQ_OK;
   if (LZQ_PROF_SORT && n >= lzq::kProfSortMin) {
-    e = hipMallocAsync((void**)&ws, sizeof(int32_t) * (size_t)(2 * n + 2 * lzq::kCostBins), st);
+    size_t tmp_bytes = 0;
+    e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                           (const int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, 31, st);
+    const size_t arr = ((size_t)n * 4 + 255) & ~(size_t)255;
+    if (e == hipSuccess) e = hipMallocAsync((void**)&ws, 4 * arr + tmp_bytes, st);
     if (e == hipSuccess) {
-      int32_t *bins = ws, *ord = ws + n, *hist = ws + 2 * n, *offs = hist + lzq::kCostBins;
-      e = hipMemsetAsync(hist, 0, sizeof(int32_t) * lzq::kCostBins, st);
-      if (e == hipSuccess) {
-        hipLaunchKernelGGL(lzq::profile_cost_kernel, dim3((unsigned)nb), dim3(lzq::kProfBlock), 0, st, d_knots,
-                           n_shapes, n_knots, d_points, n, steps_per_radian, min_steps, (const double*)samp, bins,
-                           hist);
-        rc = lzq::launch_bin_order(bins, hist, offs, n, ord, st);
-        order = ord;
-      }
+      uint32_t* keys = (uint32_t*)ws;
+      uint32_t* keys_sorted = (uint32_t*)(ws + arr);
+      int32_t* idx = (int32_t*)(ws + 2 * arr);
+      int32_t* ord = (int32_t*)(ws + 3 * arr);
+      hipLaunchKernelGGL(lzq::profile_key_kernel, dim3((unsigned)nb), dim3(lzq::kProfBlock), 0, st, d_knots, n_shapes,
+                         n_knots, d_points, n, steps_per_radian, min_steps, (const double*)samp, keys, idx);
+      e = hipGetLastError();
+      if (e == hipSuccess)
+        e = hipcub::DeviceRadixSort::SortPairs((void*)(ws + 4 * arr), tmp_bytes, (const uint32_t*)keys, keys_sorted,
+                                               (const int32_t*)idx, ord, (int)n, 0, 31, st);
+      order = ord;
     }
   }
   if (e == hipSuccess && rc == LZQ_OK) {

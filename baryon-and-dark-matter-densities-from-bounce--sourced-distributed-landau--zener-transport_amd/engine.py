@@ -69,8 +69,9 @@ class Engine:
         return prev
 
     def tune_profile_flat(self, on: bool) -> bool:
-        """lzq_lz_propagate_profile's flattened propagation (include/lzq.h LZQ_TUNE_PROFILE_FLAT; on by
-        default, bit-identical P either way).  Returns the previous setting."""
+        """lzq_lz_propagate_profile's flattened propagation (include/lzq.h LZQ_TUNE_PROFILE_FLAT; off by
+        default -- the interval loop in keyed launch order is faster, DESIGN §6b -- bit-identical P
+        either way).  Returns the previous setting."""
         prev = self.lib.lzq_tune(_native.TUNE_PROFILE_FLAT, 1 if on else 0)
         if prev < 0:
             self._check(prev)
@@ -533,20 +534,26 @@ REUSE_MAX_BYTES = 16 << 30     # Engine.sweep(reuse=True): z-sum tables beyond t
 
 def wave_order(d_pts: torch.Tensor, d_ode: torch.Tensor, n: int):
     """A launch order (int64 permutation tensor, on the points' device) that makes points equal
-    in _native.ODE_STAGE_KEY (and deplete) contiguous, or None when the input is already grouped
-    or has no repeated keys.  d_pts / d_ode: the lzq_point / lzq_ode_params records as byte
-    tensors.  A 64-bit mix of the key fields' bits is sorted stably; a hash collision only puts
-    unequal points in one wavefront, which the kernel detects and runs per lane."""
+    in _native.ODE_COOP_KEY (and deplete) contiguous -- and within such a run, points equal in the
+    whole ODE_STAGE_KEY (same spline table) -- or None when the input is already grouped or has
+    no repeated keys.  d_pts / d_ode: the lzq_point / lzq_ode_params records as byte tensors.  A
+    64-bit mix of the key fields' bits is sorted stably; a hash collision only puts unequal
+    points in one wavefront, which the kernel detects and runs per lane."""
     if n <= 64:
         return None
     w64 = d_pts.view(n, _native.POINT_DTYPE.itemsize).view(torch.int64)
     w32 = d_pts.view(n, _native.POINT_DTYPE.itemsize).view(torch.int32)
     o32 = d_ode.view(n, _native.ODE_DTYPE.itemsize).view(torch.int32)
-    h = torch.zeros(n, dtype=torch.int64, device=d_pts.device)
-    for f in _native.ODE_STAGE_KEY:
-        off = _native.POINT_DTYPE.fields[f][1]
-        col = w64[:, off // 8] if _native.POINT_DTYPE.fields[f][0].itemsize == 8 else w32[:, off // 4].to(torch.int64)
-        h = (h * _MIX) ^ col
+
+    def mix(h, fields):
+        for f in fields:
+            off = _native.POINT_DTYPE.fields[f][1]
+            col = w64[:, off // 8] if _native.POINT_DTYPE.fields[f][0].itemsize == 8 else \
+                w32[:, off // 4].to(torch.int64)
+            h = (h * _MIX) ^ col
+        return h
+
+    h = mix(torch.zeros(n, dtype=torch.int64, device=d_pts.device), _native.ODE_COOP_KEY)
     h = (h * _MIX) ^ o32[:, _native.ODE_DTYPE.fields["deplete_DM_from_source"][1] // 4].to(torch.int64)
     breaks = int((h[1:] != h[:-1]).sum())
     if breaks == 0:
@@ -554,7 +561,9 @@ def wave_order(d_pts: torch.Tensor, d_ode: torch.Tensor, n: int):
     distinct = int(torch.unique(h).numel())
     if distinct == n or breaks <= 2 * (distinct - 1):
         return None
-    return torch.argsort(h, stable=True)
+    ht = mix(torch.zeros(n, dtype=torch.int64, device=d_pts.device), ("I_p", "v_w"))
+    by_table = torch.argsort(ht, stable=True)
+    return by_table[torch.argsort(h[by_table], stable=True)]
 
 
 _KEY_WORDS = [_native.POINT_DOUBLE_FIELDS.index(f) for f in _native.ODE_TABLE_KEY]  # 8-byte words of lzq_point

@@ -146,10 +146,11 @@ int lzq_ztables(int32_t nz, double z_max, double* z, double* gamma4, double* ome
  * ceil(max_steps / 2^value) launches (<= 65536), the per-point state carried between them in
  * stream-ordered scratch (64 B per point), so any window the reference accepts completes in
  * bounded launches.  Results are bit-identical for every value (tests/test_gpu_ode.py). */
-/* LZQ_TUNE_PROFILE_FLAT (1 = on, the default; 0 = off): lzq_lz_propagate_profile's flattened
+/* LZQ_TUNE_PROFILE_FLAT (1 = on; 0 = off, the default): lzq_lz_propagate_profile's flattened
  * propagation (the step rule for all of a point's knot intervals ahead of the propagation, then one
  * loop of Magnus steps per lane, a lane entering its next interval while the others step) or the
- * interval-by-interval loop.  P is bit-identical either way (tests/test_gpu_profile.py). */
+ * interval-by-interval loop in keyed launch order (measured faster).  P is
+ * bit-identical either way (tests/test_gpu_profile.py). */
 enum lzq_tune_key { LZQ_TUNE_EXP = 0, LZQ_TUNE_TRUNCATE = 1, LZQ_TUNE_ODE_COOP = 2, LZQ_TUNE_ODE_LAUNCH_STEPS = 3,
                     LZQ_TUNE_PROFILE_FLAT = 4 };
 enum lzq_exp_variant { LZQ_EXP_POLY11 = 0, LZQ_EXP_TABLE = 1 };

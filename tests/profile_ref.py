@@ -21,6 +21,7 @@ Blanes-Casas-Ros commutator form) on uniform steps per knot interval, started in
 on the chi-like second-order dressed (superadiabatic) state at the profile's two ends.
 """
 import math
+from fractions import Fraction
 
 import numpy as np
 
@@ -168,21 +169,40 @@ MIN_STEPS = 1
 HDOT_RATE = 4.0   # the crossing region's rate: HDOT_RATE / (LZ time), LZ time = |dH/dt|^-1/2
 
 
-def interval_steps(cphi, cPhi, yB, ychi, lam, L, v_w, spr=STEPS_PER_RADIAN, n_min=MIN_STEPS):
-    """Uniform Magnus steps on one knot interval: spr x the interval's largest local rate
-    omega = max(E, HDOT_RATE sqrt(|dH/dt|)) x its duration, at least n_min.  The rate is sampled at
-    5 points t_q = (q/4) L from the shape's samples phi(t_q), Phi(t_q), phi'(t_q), Phi'(t_q)
-    (coupling-independent: the kernel precomputes them per shape) combined with the point's
-    couplings: Delta = y_B phi - y_chi Phi, m = lambda phi (eqs.(5),(7))."""
-    w = 0.0
-    for f in (0.0, 0.25, 0.5, 0.75, 1.0):
-        t = f * L
-        a, b = pp_eval(cphi, t), pp_eval(cPhi, t)
-        da, db = pp_eval(cphi, t, 1), pp_eval(cPhi, t, 1)
-        D, m = yB * a - ychi * b, lam * a
-        Dd, md = yB * da - ychi * db, lam * da
-        w = max(w, math.sqrt(D * D + m * m), HDOT_RATE * math.sqrt(v_w * math.sqrt(Dd * Dd + md * md)))
-    return max(n_min, int(math.ceil(spr * (L / v_w) * w)))
+def fma(a, b, c):
+    """a * b + c with one rounding (exact rational arithmetic, then Python's correctly rounded
+    conversion): the restatement of the kernels' fused multiply-adds."""
+    return float(Fraction(a) * Fraction(b) + Fraction(c))
+
+
+def _samples(c, L):
+    """The shape's samples at t_q = (q/4) L, q = 0..4 (profile_samples_kernel): (phi, Phi, phi', Phi')."""
+    cphi, cPhi = c
+    return [(pp_eval(cphi, (0.25 * q) * L), pp_eval(cPhi, (0.25 * q) * L),
+             pp_eval(cphi, (0.25 * q) * L, 1), pp_eval(cPhi, (0.25 * q) * L, 1)) for q in range(5)]
+
+
+def interval_steps(knots, cphi, cPhi, j, yB, ychi, lam, v_w, spr=STEPS_PER_RADIAN, n_min=MIN_STEPS):
+    """Uniform Magnus steps on knot interval j: spr x the interval's largest local rate
+    omega = max(E, HDOT_RATE sqrt(v_w |dH/dt|)) x its duration (L / v_w), at least n_min.  The rate
+    is sampled at t_q = (q/4) L, q = 0..3, from the interval's own cubic and at its end from the
+    next interval's q = 0 sample (the last interval: its own q = 4), with the shape's samples
+    phi, Phi, phi', Phi' (coupling-independent: the kernel precomputes them per shape) combined
+    with the point's couplings: Delta = y_B phi - y_chi Phi, m = lambda phi (eqs.(5),(7)).  The
+    kernel's operations: fused products per sample, the maxima of E^2 and |dH/dt|^2, then
+    W2 = max(e2, HDOT_RATE^2 (v_w sqrt(h2))), S = ceil((spr (L (1 / v_w))) sqrt(W2))."""
+    L = knots[j + 1] - knots[j]
+    own = _samples((cphi[j], cPhi[j]), L)
+    nI = len(knots) - 1
+    end = _samples((cphi[j + 1], cPhi[j + 1]), knots[j + 2] - knots[j + 1])[0] if j + 1 < nI else own[4]
+    e2 = h2 = 0.0
+    for a, b, da, db in own[:4] + [end]:
+        D, m = fma(yB, a, -(ychi * b)), lam * a
+        Dd, md = fma(yB, da, -(ychi * db)), lam * da
+        e2 = max(e2, fma(D, D, m * m))
+        h2 = max(h2, fma(Dd, Dd, md * md))
+    W2 = max(e2, (HDOT_RATE * HDOT_RATE) * (v_w * math.sqrt(h2)))
+    return max(n_min, int(math.ceil((spr * (L * (1.0 / v_w))) * math.sqrt(W2))))
 
 
 def magnus6_vector(a1, a2, a3, dt):
@@ -224,7 +244,7 @@ def propagate_profile(knots, cphi, cPhi, yB, ychi, lam, v_w, spr=STEPS_PER_RADIA
     p = _edge(cD[0], cM[0], 0.0, v_w)
     for j in range(nI):
         L = knots[j + 1] - knots[j]
-        S = interval_steps(cphi[j], cPhi[j], yB, ychi, lam, L, v_w, spr, n_min)
+        S = interval_steps(knots, cphi, cPhi, j, yB, ychi, lam, v_w, spr, n_min)
         h = L / S
         dt = h / v_w
         for i in range(S):

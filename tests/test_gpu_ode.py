@@ -517,6 +517,60 @@ def test_ode_cooperative_subgroups_bit_identical(gpu_engine):
         assert torch_equal(a, c) and torch_equal(sa, sc), method
 
 
+def test_ode_cooperative_table_varying_bit_identical(gpu_engine):
+    """Cooperative segments whose points differ in the A/V kernel (I_p, v_w: a spline table each):
+    the shared stage rows carry a / Av and the spline location, each lane forms a from its own
+    table (ode_integrate_kernel tab_vary).  A table per point (128 distinct kernels, share_tables
+    finds nothing to share) and 8 shared tables interleaved (every wavefront spans 8 tables) give
+    the per-lane mode's bits, for Radau and the quadrature method, also as continuation launches;
+    and the C restatement's values."""
+    rng = np.random.default_rng(91)
+
+    def cfg(I_p, v_w):
+        c = full_cfg(BASE_CFG)
+        c.update(NARROW, m_chi_GeV=40.0, I_p=I_p, v_w=v_w, P_chi_to_B=float(rng.uniform(0.05, 1.0)),
+                 incident_flux_scale=float(10 ** rng.uniform(-10, -8)),
+                 Gamma_wash_over_H=float(rng.choice([0.0, 0.5, 2.0])),
+                 sigma_v_chi_GeV_m2=float(rng.choice([0.0, 1e-16, 1e-12])),
+                 deplete_DM_from_source=bool(rng.uniform() < 0.3))
+        if c["Gamma_wash_over_H"] == 0.0 and c["sigma_v_chi_GeV_m2"] == 0.0:
+            c["deplete_DM_from_source"] = True
+        return c
+
+    per_point = [cfg(float(rng.uniform(0.1, 1.0)), float(rng.uniform(0.1, 0.9))) for _ in range(128)]
+    kern = [(float(rng.uniform(0.1, 1.0)), float(rng.uniform(0.1, 0.9))) for _ in range(8)]
+    shared8 = [cfg(*kern[i % 8]) for i in range(128)]
+    for cfgs, share in ((per_point, False), (per_point, True), (shared8, True)):
+        p, o = recs(cfgs)
+        for method in ("radau", "quadrature"):
+            a, sa = gpu_engine.ode(p, o, share_tables=share, method=method, group_waves=False)
+            prev = gpu_engine.tune_ode_coop(False)
+            try:
+                b, sb = gpu_engine.ode(p, o, share_tables=share, method=method, group_waves=False)
+            finally:
+                gpu_engine.tune_ode_coop(prev)
+            assert torch_equal(sa, sb) and torch_equal(a, b), (share, method)
+            g, sg = gpu_engine.ode(p, o, share_tables=share, method=method)   # regrouped by table
+            assert torch_equal(a, g) and torch_equal(sa, sg), (share, method)
+            prev = gpu_engine.tune_ode_launch_steps(11)
+            try:
+                c, sc = gpu_engine.ode(p, o, share_tables=share, method=method, group_waves=False)
+            finally:
+                gpu_engine.tune_ode_launch_steps(prev)
+            assert torch_equal(a, c) and torch_equal(sa, sc), (share, method)
+            if method == "radau":
+                radau = (a.cpu().numpy(), sa.cpu().numpy(), dict(gpu_engine.last_ode_tables))
+        if share:
+            continue
+        t, st, tables = radau
+        assert tables["mode"] == "per_point"
+        ref, sr = O.ode_batch(cfgs[::8], nthreads=16)
+        for row, rr, s1, s2 in zip(t[::8], ref, st[::8], sr):
+            assert s1 == 0 and s2 == 0
+            for v, w in zip(row[:5], rr[:5]):
+                assert rel_err(v, w) < 1e-10, (v, w)
+
+
 def test_ode_linear_waves_degenerate_step(gpu_engine):
     """A window so narrow that a step is below x's rounding (T_max / T_min - 1 = 2e-12: h ~ 1e-16 x,
     so xk + h == xk on many steps and the general path skips them): the linear integrator

@@ -262,11 +262,12 @@ def test_batch_invariance_and_bad_inputs(gpu_engine):
 
 
 def test_flat_propagation_bit_identical_to_interval_loop(gpu_engine):
-    """The flattened propagation (LZQ_TUNE_PROFILE_FLAT, default: the step rule ahead of the
+    """The flattened propagation (LZQ_TUNE_PROFILE_FLAT, opt-in: the step rule ahead of the
     propagation, one Magnus loop per lane crossing knot intervals on its own) performs each lane's
-    interval-loop operations: P bit-identical on mixed shapes, index-ordered and cost-ordered batches
-    (>= 16384 points), NaN inputs, and steps that do not fit the uint16 step record (huge
-    steps_per_radian on a long interval: recomputed from the samples)."""
+    interval-loop operations: P bit-identical on mixed shapes, index-ordered and ordered batches
+    (>= 16384 points: the flat path's cost bins, the loop's keyed radix order), NaN inputs, and steps
+    that do not fit the uint16 step record (huge steps_per_radian on a long interval: recomputed from
+    the samples)."""
     shapes = [wiggly(40, s, span=5.0) for s in range(3)]
     sh = gpu_engine.profile_shapes(*(np.stack(a) for a in zip(*shapes)))
     rng = np.random.default_rng(11)
@@ -275,19 +276,19 @@ def test_flat_propagation_bit_identical_to_interval_loop(gpu_engine):
                 rng.uniform(0.05, 0.9, n))
         shp = rng.integers(0, 3, n)
         pts = gpu_engine.profile_points(*args, shp)
-        flat = gpu_engine.lz_propagate_profile(sh, pts).cpu().numpy()
-        prev = gpu_engine.tune_profile_flat(False)
+        loop = gpu_engine.lz_propagate_profile(sh, pts).cpu().numpy()
+        prev = gpu_engine.tune_profile_flat(True)
         try:
-            loop = gpu_engine.lz_propagate_profile(sh, pts).cpu().numpy()
+            flat = gpu_engine.lz_propagate_profile(sh, pts).cpu().numpy()
         finally:
             gpu_engine.tune_profile_flat(prev)
-        assert prev is True and np.array_equal(flat, loop) and np.isfinite(flat).all(), n
+        assert prev is False and np.array_equal(flat, loop) and np.isfinite(flat).all(), n
     # > 65534 steps in one interval (the record's overflow path) and bad inputs
     pts = gpu_engine.profile_points(1.0, 1.0, 0.1, [0.3, 0.0, 0.3, 0.0005], [0, 0, 3, 1])
-    flat = gpu_engine.lz_propagate_profile(sh, pts, 900.0).cpu().numpy()
-    prev = gpu_engine.tune_profile_flat(False)
+    loop = gpu_engine.lz_propagate_profile(sh, pts, 900.0).cpu().numpy()
+    prev = gpu_engine.tune_profile_flat(True)
     try:
-        loop = gpu_engine.lz_propagate_profile(sh, pts, 900.0).cpu().numpy()
+        flat = gpu_engine.lz_propagate_profile(sh, pts, 900.0).cpu().numpy()
     finally:
         gpu_engine.tune_profile_flat(prev)
     assert np.array_equal(flat, loop, equal_nan=True) and np.isnan(flat[1:3]).all() and np.isfinite(flat[[0, 3]]).all()

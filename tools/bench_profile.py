@@ -51,7 +51,7 @@ def main():
     ap.add_argument("--only", default=None, help="propagate | crossings: time that stage alone (profiling)")
     ap.add_argument("--sort-vw", action="store_true", help="launch the points ordered by (shape, v_w): the "
                     "cost-ordered launch's upper bound (a lane's step count scales as 1/v_w)")
-    ap.add_argument("--ab", action="store_true", help="also time the interval-by-interval loop (same process)")
+    ap.add_argument("--ab", action="store_true", help="also time the flattened propagation (same process)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     B = importlib.import_module(PKG + ".bounce")
@@ -70,13 +70,13 @@ def main():
         P = P.cpu().numpy()
         rec["propagate"] = {"seconds": t_p, "points_per_s": a.n / t_p, "finite": bool(np.isfinite(P).all()),
                             "P_mean": float(P.mean()), "P_min": float(P.min()), "P_max": float(P.max())}
-        if a.ab:   # the interval-by-interval loop in the same process (LZQ_TUNE_PROFILE_FLAT = 0)
-            prev = eng.tune_profile_flat(False)
+        if a.ab:   # the flattened propagation in the same process (LZQ_TUNE_PROFILE_FLAT = 1)
+            prev = eng.tune_profile_flat(True)
             try:
                 t_i, Pi = timed(lambda: eng.lz_propagate_profile(sh, pts, a.spr, a.min_steps), a.reps)
             finally:
                 eng.tune_profile_flat(prev)
-            rec["propagate"]["interval_loop"] = {"seconds": t_i, "points_per_s": a.n / t_i,
+            rec["propagate"]["flat"] = {"seconds": t_i, "points_per_s": a.n / t_i,
                                                  "bit_identical": bool(np.array_equal(Pi.cpu().numpy(), P,
                                                                                       equal_nan=True))}
     if a.only in (None, "crossings"):

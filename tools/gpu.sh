@@ -6,6 +6,7 @@
 #                                                         bench command, the PMC passes of the headline
 #                                                         kernel, profiles/ROUND summary, then the bench
 #   gpurun -- bash tools/gpu.sh ode-pmc                   ODE integrator PMC + kernel trace (tools/ode_pmc_run.py)
+#   gpurun -- bash tools/gpu.sh prop-pmc [N]              bounce-profile propagation PMC + kernel trace
 #   gpurun -- bash tools/gpu.sh bench [bench args ...]    one bench line
 #   gpurun -- bash tools/gpu.sh py SCRIPT [args ...]      any tools/ script (ablations, ODE / profile benches)
 #
@@ -67,6 +68,20 @@ case "$cmd" in
     timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
       python3 tools/ode_pmc_run.py > "$OUT/trace.jsonl" 2> "$OUT/trace.err" || { tail -5 "$OUT/trace.err"; exit 2; }
     cat "$OUT/trace.jsonl"
+    ;;
+  prop-pmc)  # the bounce-profile propagation (tools/bench_profile.py): instruction mix per kernel + kernel trace;
+             # summarise with: python tools/summarize_profile_pmc.py gpurun_out/prop-pmc ROUND
+    N=${1:-1000000}
+    rm -rf "$OUT"; mkdir -p "$OUT"
+    timeout -k 10 300 python3 tools/bench_profile.py "$N" 3 --ab --json "$OUT/bench_traced.json" > "$OUT/bench.log" 2>&1 \
+      || { tail -20 "$OUT/bench.log"; exit 1; }
+    cat "$OUT/bench_traced.json"
+    timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 \
+      SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_SALU --output-format csv -d "$OUT/pmc" -o run -- \
+      python3 tools/bench_profile.py "$N" 1 --only propagate --ab > "$OUT/pmc.json" 2> "$OUT/pmc.err" || { tail -5 "$OUT/pmc.err"; exit 2; }
+    timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
+      python3 tools/bench_profile.py "$N" 3 --only propagate --ab > "$OUT/trace.json" 2> "$OUT/trace.err" || { tail -5 "$OUT/trace.err"; exit 3; }
+    echo done
     ;;
   bench)
     timeout -k 10 600 python3 -u bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 3; }

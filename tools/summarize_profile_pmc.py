@@ -1,10 +1,13 @@
 #!/usr/bin/env python3
-"""Summarise the bounce-profile path's GPU runs (tools/gpu_prof_r3b.sh / tools/gpu_r3c.sh output in
-gpurun_out/profprop) into profiles/<round>/: profile_pmc.json (per-dispatch VALU / FP64
-instruction counts of profile_propagate_kernel, its rocprofv3 average duration, the executed
-FP64 rate against the 78.6 TFLOP/s peak), profile_kernel_stats.csv and the bench lines.
+"""Summarise the bounce-profile path's GPU runs (`tools/gpu.sh prop-pmc`, output in
+gpurun_out/prop-pmc) into profiles/<round>/: profile_pmc.json (per-dispatch VALU / FP64
+instruction counts of each propagation kernel, its rocprofv3 average duration, the executed FP64
+rate against the 78.6 TFLOP/s peak, and per path -- flattened (profile_steps_kernel +
+profile_flat_kernel) and the interval loop (profile_key_kernel + the radix sort +
+profile_propagate_kernel, the default) -- wave VALU x 64 per useful lane-step), profile_kernel_stats.csv and
+the bench line.
 
-    python tools/summarize_profile_pmc.py [gpurun_out/profprop] [round3]
+    python tools/summarize_profile_pmc.py [gpurun_out/prop-pmc] [round4]
 """
 import collections
 import csv
@@ -15,60 +18,80 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PEAK = 78.6
+KERNELS = ("profile_steps_kernel", "profile_flat_kernel", "profile_key_kernel", "profile_propagate_kernel",
+           "profile_samples_kernel")
+PATHS = {"flat": ("profile_steps_kernel", "profile_flat_kernel"),
+         "interval_loop": ("profile_key_kernel", "profile_propagate_kernel")}
+
+
+def short(name):
+    return next((k for k in KERNELS if k in name), None)
 
 
 def main():
-    src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "profprop")
-    rnd = sys.argv[2] if len(sys.argv) > 2 else "round3"
+    src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "prop-pmc")
+    rnd = sys.argv[2] if len(sys.argv) > 2 else "round4"
     dst = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(dst, exist_ok=True)
-    agg, disp = collections.defaultdict(float), set()
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    disp = collections.defaultdict(set)
     for r in csv.DictReader(open(os.path.join(src, "pmc", "run_counter_collection.csv"))):
-        if "profile_propagate_kernel" in r["Kernel_Name"]:
-            agg[r["Counter_Name"]] += float(r["Counter_Value"])
-            disp.add(r["Dispatch_Id"])
-    per = {c: v / len(disp) for c, v in agg.items()}
-    stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv")))}
+        k = short(r["Kernel_Name"])
+        if k:
+            agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            disp[k].add(r["Dispatch_Id"])
+    per = {k: {c: v / len(disp[k]) for c, v in cs.items()} for k, cs in agg.items()}
+    stats, sort_ns = {}, 0.0
+    rows = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
+    for r in rows:
+        k = short(r["Name"])
+        if k:
+            stats[k] = float(r["AverageNs"]) * 1e-9
+        elif "rocprim" in r["Name"] or "hipcub" in r["Name"]:
+            sort_ns += float(r["TotalDurationNs"])
+    calls = next((float(r["Calls"]) for r in rows if "profile_key_kernel" in r["Name"]), 0.0)
+    sort_s = sort_ns * 1e-9 / calls if calls else 0.0   # the radix sort's kernels, per keyed launch
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "profile_kernel_stats.csv"))
-    ks = float(next(v for n, v in stats.items() if "profile_propagate_kernel" in n)["AverageNs"]) * 1e-9
     bench = json.load(open(os.path.join(src, "bench_traced.json")))
     n = bench["points"]
     steps = bench["magnus_steps_per_point"]["total"]
-    f64 = per["SQ_INSTS_VALU_FMA_F64"] + per["SQ_INSTS_VALU_MUL_F64"] + per["SQ_INSTS_VALU_ADD_F64"]
-    flop = 64 * (2 * per["SQ_INSTS_VALU_FMA_F64"] + per["SQ_INSTS_VALU_MUL_F64"] + per["SQ_INSTS_VALU_ADD_F64"])
+    kern = {}
+    for k, c in per.items():
+        f64 = c.get("SQ_INSTS_VALU_FMA_F64", 0) + c.get("SQ_INSTS_VALU_MUL_F64", 0) + c.get("SQ_INSTS_VALU_ADD_F64", 0)
+        flop = 64 * (2 * c.get("SQ_INSTS_VALU_FMA_F64", 0) + c.get("SQ_INSTS_VALU_MUL_F64", 0)
+                     + c.get("SQ_INSTS_VALU_ADD_F64", 0))
+        ks = stats.get(k)
+        kern[k] = {"dispatches_counted": len(disp[k]), "kernel_s": ks, "valu_per_dispatch": c["SQ_INSTS_VALU"],
+                   "salu_per_dispatch": c.get("SQ_INSTS_SALU"), "trans_f64_per_dispatch": c.get("SQ_INSTS_VALU_TRANS_F64"),
+                   "fp64_share_of_valu": f64 / c["SQ_INSTS_VALU"], "waves": c["SQ_WAVES"],
+                   "wave_valu_per_lane_step": 64 * c["SQ_INSTS_VALU"] / steps,
+                   "executed_fp64_tflops": flop / ks / 1e12 if ks else None,
+                   "valu_per_simd_cycle": c["SQ_INSTS_VALU"] / (1024 * ks * 2.4e9) if ks else None}
+    paths = {}
+    for name, ks in PATHS.items():
+        if all(k in kern and kern[k]["kernel_s"] for k in ks):
+            t = sum(kern[k]["kernel_s"] for k in ks) + (sort_s if name == "interval_loop" else 0.0)
+            paths[name] = {"kernels": list(ks) + (["radix sort"] if name == "interval_loop" else []), "kernel_s": t, "points_per_s": n / t, "magnus_steps_per_s": steps / t,
+                           "wave_valu_per_lane_step": sum(kern[k]["wave_valu_per_lane_step"] for k in ks)}
     out = {
-        "source": "rocprofv3 --pmc on tools/bench_profile.py 1000000 1 --only propagate; separate --kernel-trace "
-                  "--stats pass on tools/bench_profile.py 1000000 3 (tools/gpu_r3c.sh) + tools/summarize_profile_pmc.py",
-        "kernel": "profile_propagate_kernel",
+        "source": "tools/gpu.sh prop-pmc: rocprofv3 --pmc on tools/bench_profile.py N 1 --only propagate --ab; a "
+                  "separate --kernel-trace --stats pass on tools/bench_profile.py N 3 --only propagate --ab; "
+                  "tools/summarize_profile_pmc.py",
         "config": f"{n} points, {bench['shapes']} synthetic bounce shapes x {bench['knots']} knots "
                   f"(bounce.synthetic_shapes / synthetic_couplings), {bench['steps_per_radian']} steps per radian, "
-                  "cost-ordered launch",
-        "dispatches_counted": len(disp),
-        "kernel_s": ks,
-        "points_per_s": n / ks,
+                  "keyed launch order",
         "magnus_steps_per_point": bench["magnus_steps_per_point"],
-        "magnus_steps_per_s": steps / ks,
-        "valu_per_dispatch": per["SQ_INSTS_VALU"],
-        "fp64_fma_mul_add_per_dispatch": f64,
-        "fp64_share_of_valu": f64 / per["SQ_INSTS_VALU"],
-        "waves": per["SQ_WAVES"],
-        "wave_valu_per_lane_step": 64 * per["SQ_INSTS_VALU"] / steps,
-        "executed_fp64_tflops": flop / ks / 1e12,
-        "frac_of_fp64_peak": flop / ks / 1e12 / PEAK,
-        "valu_per_simd_cycle": per["SQ_INSTS_VALU"] / (1024 * ks * 2.4e9),
-        "note": "executed FP64 counts every lane of a wave instruction (FMA = 2 FLOP); lanes idle while a "
-                "wave waits for its longest lane in a knot interval count too, which wave_valu_per_lane_step "
-                "(wave VALU x 64 / useful lane-steps) exposes. valu_per_simd_cycle: an FP64 wave64 instruction "
-                "occupies a SIMD for 4 cycles, so 0.25 is the issue ceiling.",
-        "other_kernels_us": {n.split("(")[0]: float(v["AverageNs"]) * 1e-3 for n, v in stats.items()
-                             if "profile_propagate_kernel" not in n and n.startswith("lzq::")},
+        "paths": paths,
+        "kernels": kern,
+        "bench": bench.get("propagate"),
+        "note": "wave_valu_per_lane_step = 64 x wave VALU instructions / useful Magnus lane-steps; it counts the "
+                "step rule (profile_steps_kernel / profile_key_kernel + the loop's per-interval rule), entering "
+                "intervals and idle lanes. valu_per_simd_cycle: an FP64 wave64 instruction occupies a SIMD for 4 "
+                "cycles, so 0.25 is the issue ceiling.",
     }
     with open(os.path.join(dst, "profile_pmc.json"), "w") as f:
         json.dump(out, f, indent=1)
-    for name in ("bench.json", "bench_sorted.json", "bench_1e6.json", "bench_1e6_sorted.json", "ablate.json"):
-        p = os.path.join(src, name)
-        if os.path.exists(p):
-            shutil.copy(p, os.path.join(dst, "profile_" + name))
+    shutil.copy(os.path.join(src, "bench_traced.json"), os.path.join(dst, "profile_bench.json"))
     print(json.dumps(out, indent=1))
 
 

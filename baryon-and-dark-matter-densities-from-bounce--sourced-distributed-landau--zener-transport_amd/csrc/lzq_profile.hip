@@ -341,9 +341,9 @@ __device__ __forceinline__ void cos_sinc_short(double x2, double& cs, double& sc
   if (LZQ_PROF_SHORTSC && x2 <= 0.25) {
     double ps = kSincC[6], pc = kCosC[7];
 #pragma unroll
-    for (int k = 5; k >= 0; --k) ps = __builtin_fma(ps, x2, kSincC[k]);
+    for (int k = 5; k >= 0; --k) ps = fma3s(ps, x2, kSincC[k]);
 #pragma unroll
-    for (int k = 6; k >= 0; --k) pc = __builtin_fma(pc, x2, kCosC[k]);
+    for (int k = 6; k >= 0; --k) pc = fma3s(pc, x2, kCosC[k]);
     sc = ps;
     cs = pc;
   } else {

@@ -38,13 +38,23 @@ __device__ __forceinline__ double fma3(double a, double b, double c) {
   return r;
 }
 
+// The same with a wave-uniform addend (a Horner coefficient) pinned to an SGPR pair: v_fma_f64 reads
+// one scalar operand for free, so the constants need neither VGPRs nor the per-step v_mov copies the
+// register allocator otherwise inserts to rebuild them (round 4: ~17 VALU per profile Magnus step).
+__device__ __forceinline__ double fma3s(double a, double b, double c) {
+  if (!LZQ_SU2_FMA3) return __builtin_fma(a, b, c);
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+  return r;
+}
+
 __device__ __forceinline__ void cos_sinc(double x2, double& cs, double& sc) {
   if (x2 <= 1.0) {
     double ps = kSincC[8], pc = kCosC[9];
 #pragma unroll
-    for (int k = 7; k >= 0; --k) ps = fma3(ps, x2, kSincC[k]);
+    for (int k = 7; k >= 0; --k) ps = fma3s(ps, x2, kSincC[k]);
 #pragma unroll
-    for (int k = 8; k >= 0; --k) pc = fma3(pc, x2, kCosC[k]);
+    for (int k = 8; k >= 0; --k) pc = fma3s(pc, x2, kCosC[k]);
     sc = ps;
     cs = pc;
   } else {

@@ -310,9 +310,9 @@ class Engine:
                 if share_tables and c1 - c0 >= 4096:
                     _log.warning(
                         "lzq ODE: %d of %d points differ in the A/V kernel or window (ODE_TABLE_KEY: %s): a spline "
-                        "table per point, and waves whose points differ in them integrate per lane (no shared stage "
-                        "rows) -- on long windows ~40x the cost per point of a shared-table sweep (DESIGN §5.3)",
-                        c1 - c0, c1 - c0, ", ".join(_native.ODE_TABLE_KEY))
+                        "table per point (an A/V z-sum table build each; the integration still shares stage rows "
+                        "across tables) -- ~2.4x the cost per point of a shared-table sweep on a 20000-step "
+                        "window (DESIGN §5.3)", c1 - c0, c1 - c0, ", ".join(_native.ODE_TABLE_KEY))
             if work is None or work.numel() < n_tab * _native.ODE_WS_PER_POINT:
                 work = self.ode_workspace(max(n_tab, min(n, chunk) if rep is None else n_tab))
             with torch.cuda.device(self.device):

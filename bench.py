@@ -102,7 +102,7 @@ def roofline(points_per_launch: int, kern_ms: float) -> dict:
         out.update(achieved=None, frac=None, fp64_pipe_busy_frac=None, traffic=None,
                    profile_code_object_sha256=d.get("code_object_sha256"),
                    note=f"stale profile: {os.path.relpath(PMC_SUMMARY, ROOT)} was measured on code object "
-                        f"{d.get('code_object_sha256')}, this run timed {sha}; re-run tools/gpu_profile.sh")
+                        f"{d.get('code_object_sha256')}, this run timed {sha}; re-run tools/gpu.sh profile ROUND")
         return out
     mix = d["valu_mix_per_wave_node"]
     flop_wn = 64.0 * (2.0 * mix["fma_f64"] + mix["mul_f64"] + mix["add_f64"])

@@ -29,7 +29,7 @@ def test_executed_flop_from_committed_csv():
     if not os.path.exists(os.path.join(PROF, "pmc_mix.csv")):
         pytest.skip(f"{os.path.relpath(PROF, ROOT)} holds no PMC pass yet")
     c = counters(os.path.join(PROF, "pmc_mix.csv"))
-    points = 200_000                                     # tools/gpu_profile.sh PMC launch size
+    points = 200_000                                     # tools/gpu.sh profile: the PMC launch size
     flop_pt = 64 * (2 * c["SQ_INSTS_VALU_FMA_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + c["SQ_INSTS_VALU_ADD_F64"]) / points
     stats = [r for r in csv.DictReader(open(os.path.join(PROF, "kernel_stats.csv"))) if "yields_grid_kernel" in r["Name"]]
     assert len(stats) == 1 and int(stats[0]["Calls"]) == 25     # bench.py --steps 20 --warmup 5

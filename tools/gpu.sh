@@ -7,6 +7,8 @@
 #                                                         kernel, profiles/ROUND summary, then the bench
 #   gpurun -- bash tools/gpu.sh ode-pmc                   ODE integrator PMC + kernel trace (tools/ode_pmc_run.py)
 #   gpurun -- bash tools/gpu.sh prop-pmc [N]              bounce-profile propagation PMC + kernel trace
+#   gpurun -- bash tools/gpu.sh lzprop-pmc                LZ propagator PMC + kernel trace (C5 slice)
+#   gpurun -- [REUSE=1] bash tools/gpu.sh sweeps [SPECS]  full grids through the sweep CLI (+ reuse bitwise)
 #   gpurun -- bash tools/gpu.sh bench [bench args ...]    one bench line
 #   gpurun -- bash tools/gpu.sh py SCRIPT [args ...]      any tools/ script (ablations, ODE / profile benches)
 #
@@ -83,6 +85,43 @@ case "$cmd" in
       python3 tools/bench_profile.py "$N" 3 --only propagate --ab > "$OUT/trace.json" 2> "$OUT/trace.err" || { tail -5 "$OUT/trace.err"; exit 3; }
     echo done
     ;;
+  lzprop-pmc)  # the LZ propagator (lz_propagate / lz_follow kernels) on a 4e5-point C5 slice: PMC + trace;
+               # summarise with: python tools/summarize_prop_pmc.py gpurun_out/lzprop-pmc ROUND
+    rm -rf "$OUT"; mkdir -p "$OUT"
+    timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 \
+      SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 --output-format csv -d "$OUT/pmc" -o run -- \
+      python3 tools/prop_only.py 400000 8 1 > "$OUT/pmc.json" 2> "$OUT/pmc.err" || { tail -5 "$OUT/pmc.err"; exit 1; }
+    timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
+      python3 tools/prop_only.py 400000 8 3 > "$OUT/trace.json" 2> "$OUT/trace.err" || { tail -5 "$OUT/trace.err"; exit 2; }
+    cat "$OUT/trace.json"
+    ;;
+  sweeps)  # full grids through the sweep CLI on one GPU (default C3 C4), dense and, with REUSE=1, also
+           # --reuse-zsums with the two tables compared bit for bit; summaries -> gpurun_out/sweeps/
+    PKG=baryon-and-dark-matter-densities-from-bounce--sourced-distributed-landau--zener-transport_amd
+    for S in ${@:-C3 C4}; do
+      rm -rf "/tmp/sw_d_$S" "/tmp/sw_r_$S"
+      timeout -k 10 500 python3 -u -m $PKG.sweep --spec "$S" --out "/tmp/sw_d_$S" > "$OUT/${S}_dense.log" 2>&1 \
+        || { tail -5 "$OUT/${S}_dense.log"; exit 1; }
+      tail -1 "$OUT/${S}_dense.log"
+      python3 -c "import json; d = json.load(open('/tmp/sw_d_$S/summary.json')); d.pop('spec_def', None); \
+json.dump(d, open('$OUT/${S}_summary.json', 'w'), indent=1)" || exit 2
+      if [ "${REUSE:-0}" = 1 ]; then
+        timeout -k 10 300 python3 -u -m $PKG.sweep --spec "$S" --out "/tmp/sw_r_$S" --reuse-zsums > "$OUT/${S}_reuse.log" 2>&1 \
+          || { tail -5 "$OUT/${S}_reuse.log"; exit 3; }
+        timeout -k 10 300 python3 -c "
+import json, numpy as np
+a = np.load('/tmp/sw_d_$S/table.npy', mmap_mode='r'); b = np.load('/tmp/sw_r_$S/table.npy', mmap_mode='r')
+same = a.shape == b.shape and all(np.array_equal(a[i:i + 10**7].view(np.uint64), b[i:i + 10**7].view(np.uint64))
+                                  for i in range(0, a.shape[0], 10**7))
+d = json.loads(open('$OUT/${S}_dense.log').read().strip().splitlines()[-1])
+r = json.loads(open('$OUT/${S}_reuse.log').read().strip().splitlines()[-1])
+rec = {'spec': '$S', 'points': int(a.shape[0]), 'bit_identical_tables': bool(same),
+       'dense_elapsed_s': d['elapsed_s'], 'reuse_elapsed_s': r['elapsed_s']}
+print(json.dumps(rec)); open('$OUT/${S}_reuse_bitwise.json', 'w').write(json.dumps(rec))" || exit 4
+      fi
+      rm -rf "/tmp/sw_d_$S" "/tmp/sw_r_$S"
+    done
+    ;;
   bench)
     timeout -k 10 600 python3 -u bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 3; }
     cut -c1-800 "$OUT/bench.json"
@@ -95,6 +134,6 @@ case "$cmd" in
     tail -40 "$OUT/$(basename "$script" .py).log"
     ;;
   *)
-    echo "usage: tools/gpu.sh tests|final|profile ROUND|bench|py SCRIPT ..."; exit 64
+    echo "usage: tools/gpu.sh tests|final|profile ROUND|ode-pmc|prop-pmc|lzprop-pmc|sweeps|bench|py SCRIPT ..."; exit 64
     ;;
 esac

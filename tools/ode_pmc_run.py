@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""The workload of the ODE PMC passes (tools/gpu_ode_pmc3.sh): three 262,144-point batches of
+"""The workload of the ODE PMC passes (`tools/gpu.sh ode-pmc`): three 262,144-point batches of
 the Radau fallback (fpy:385-417), each ONE integrator launch (ode_integrate_kernel<false, kLin>, both variants) after a
 64-point warm-up, in this order:
 

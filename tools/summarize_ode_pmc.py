@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""profiles/<round>/ode_pmc.json from a tools/gpu_ode_pmc.sh run: per config, the
+"""profiles/<round>/ode_pmc.json from a `tools/gpu.sh ode-pmc` run: per config, the
 ode_integrate_kernel's VALU and FP64 instructions per wave-step (PMC pass) and its duration
 (kernel-trace pass), hence executed FP64 TFLOP/s against the 78.6 TFLOP/s FP64 vector peak.
 bench_ode.py runs, per config, the shared-table and the per-point-table path: two
@@ -16,7 +16,7 @@ CONFIGS = [("narrow_wash", 262144, 20000), ("stiff_thermal", 262144, 25385), ("f
 
 
 def main_cases(src: str, tag: str, fname: str = "ode_pmc.json") -> None:
-    """tools/gpu_ode_pmc3.sh layout: tools/ode_pmc_run.py's three cases, one 262,144-point
+    """`tools/gpu.sh ode-pmc` layout: tools/ode_pmc_run.py's three cases, one 262,144-point
     ode_integrate_kernel<false> dispatch each (after a 64-point warm-up), in CASES order."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from ode_pmc_run import CASES, N
@@ -47,7 +47,7 @@ def main_cases(src: str, tag: str, fname: str = "ode_pmc.json") -> None:
             if ln.startswith("{"):
                 j = json.loads(ln)
                 lines.setdefault(j["config"], j)
-    out = {"source": "tools/gpu_ode_pmc3.sh (tools/ode_pmc_run.py) + tools/summarize_ode_pmc.py " + tag,
+    out = {"source": "tools/gpu.sh ode-pmc (tools/ode_pmc_run.py) + tools/summarize_ode_pmc.py " + tag,
            "kernel": "ode_integrate_kernel<false>" if per == 1 else "ode_integrate_kernel<false, kLin> (both variants)",
            "peak_tflops": 78.6,
            "note": "executed FP64 FLOP = 64 x (2 FMA + MUL + ADD) instructions; cooperative waves evaluate a "
@@ -90,7 +90,7 @@ def main():
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9 for r in tr]
     pmc = [disp[k] for k in sorted(disp)]
     # skip the warm-up dispatches (64 points each, 2 per config): keep dispatches with the config's wave count
-    out = {"source": "tools/gpu_ode_pmc.sh + tools/summarize_ode_pmc.py", "kernel": "ode_integrate_kernel",
+    out = {"source": "tools/gpu.sh ode-pmc + tools/summarize_ode_pmc.py", "kernel": "ode_integrate_kernel",
            "peak_tflops": 78.6, "configs": {}}
     big_p = [c for c in pmc if c.get("SQ_WAVES", 0) >= 256]
     big_t = [d for d, r in zip(durs, tr) if int(r["Grid_Size_X"]) >= 256 * 64]

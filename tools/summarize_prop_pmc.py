@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
-"""Summarise tools/gpu_prop_pmc.sh's output (gpurun_out/proppmc) into profiles/<round>/prop_pmc.json:
+"""Summarise `tools/gpu.sh lzprop-pmc` output (gpurun_out/lzprop-pmc) into profiles/<round>/prop_pmc.json:
 per-dispatch VALU / FP64 instruction counts of lz_propagate_kernel, its rocprofv3 average
 duration, the executed FP64 rate (FMA = 2 FLOP, x 64 lanes) against the 78.6 TFLOP/s peak, and
 the durations of the launch-order kernels.
 
-    python tools/summarize_prop_pmc.py [gpurun_out/proppmc] [round2]
+    python tools/summarize_prop_pmc.py [gpurun_out/lzprop-pmc] [round4]
 """
 import collections
 import csv
@@ -37,12 +37,12 @@ def kernel_summary(src, name, n_points):
 
 
 def main():
-    src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "proppmc")
-    rnd = sys.argv[2] if len(sys.argv) > 2 else "round2"
+    src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "lzprop-pmc")
+    rnd = sys.argv[2] if len(sys.argv) > 2 else "round4"
     n_points = 4e5
     stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv")))}
     out = {
-        "source": "tools/gpu_prop_pmc.sh (rocprofv3 --pmc on tools/prop_only.py 400000 8 1; separate "
+        "source": "tools/gpu.sh lzprop-pmc (rocprofv3 --pmc on tools/prop_only.py 400000 8 1; separate "
                   "--kernel-trace --stats pass) + tools/summarize_prop_pmc.py",
         "config": "C5 slice: 4e5 points x 8 crossings (sweep.builtin_specs()['C5']), longest-first launch order",
         "kernels": {k: kernel_summary(src, k, n_points) for k in ("lz_propagate_kernel", "lz_follow_kernel")},

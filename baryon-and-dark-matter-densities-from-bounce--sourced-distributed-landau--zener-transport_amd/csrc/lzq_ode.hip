@@ -508,6 +508,16 @@ __constant__ double kRadauAinv[3][3] = {
 __constant__ double kRadauAinvP[9] = {-0x1.fbb0962b0c0cap+2, 0x1.e8360f1027593p+0, 0x1.3adf0cf78af17p+0,
                                       0x1.74e16b2ae518ap+2,  -0x1.6692fca92522fp+0, 0x1.ce862a552e616p-1,
                                       0x1.adf74aa6f6bf3p+4,  0x1.9d782ab97a58ap+2,  -0x1.0aaaaaaaaaaabp+2};
+// fma(k, -a, p) for two constants a, p: a (wave-uniform) as the one SGPR operand with its negate
+// modifier, p in a VGPR, three-address.  Written as __builtin_fma the compiler picks v_fmac_f64,
+// which overwrites its addend, and copies p into the destination first (a v_mov_b64 per entry per
+// Newton iteration); the value is the same fma.
+__device__ __forceinline__ double fma_neg_s(double k, double a, double p) {
+  double r;
+  asm("v_fma_f64 %0, %1, -%2, %3" : "=v"(r) : "v"(k), "s"(a), "v"(p));
+  return r;
+}
+
 #ifndef LZQ_ODE_TNEWTON
 #define LZQ_ODE_TNEWTON 1  // the Riccati Newton iteration in the transformed form (constant off-diagonals)
 #endif
@@ -577,10 +587,10 @@ __device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st
     for (int i = 0; i < 3; ++i)
       r[i] = FMA(-kRadauAinv[i][2], d[2], FMA(-kRadauAinv[i][1], d[1], FMA(-kRadauAinv[i][0], d[0], r[i])));
     // adjugate of [[k0, a01, a02], [a10, k1, a12], [a20, a21, k2]] (a_ij = A^-1_ij, products constant)
-    const double b00 = FMA(k[1], k[2], -kRadauAinvP[0]), b01 = FMA(-kRadauAinv[0][1], k[2], kRadauAinvP[1]);
-    const double b02 = FMA(-kRadauAinv[0][2], k[1], kRadauAinvP[2]), b10 = FMA(-kRadauAinv[1][0], k[2], kRadauAinvP[3]);
-    const double b11 = FMA(k[0], k[2], -kRadauAinvP[4]), b12 = FMA(-kRadauAinv[1][2], k[0], kRadauAinvP[5]);
-    const double b20 = FMA(-kRadauAinv[2][0], k[1], kRadauAinvP[6]), b21 = FMA(-kRadauAinv[2][1], k[0], kRadauAinvP[7]);
+    const double b00 = FMA(k[1], k[2], -kRadauAinvP[0]), b01 = fma_neg_s(k[2], kRadauAinv[0][1], kRadauAinvP[1]);
+    const double b02 = fma_neg_s(k[1], kRadauAinv[0][2], kRadauAinvP[2]), b10 = fma_neg_s(k[2], kRadauAinv[1][0], kRadauAinvP[3]);
+    const double b11 = FMA(k[0], k[2], -kRadauAinvP[4]), b12 = fma_neg_s(k[0], kRadauAinv[1][2], kRadauAinvP[5]);
+    const double b20 = fma_neg_s(k[1], kRadauAinv[2][0], kRadauAinvP[6]), b21 = fma_neg_s(k[0], kRadauAinv[2][1], kRadauAinvP[7]);
     const double b22 = FMA(k[0], k[1], -kRadauAinvP[8]);
     // 1/det only scales the correction: a reciprocal within 1 ulp leaves the fixed point (the
     // stage equations) as it is and changes the iterates by rounding

@@ -292,17 +292,20 @@ class Engine:
         rp, ro = _native.POINT_DTYPE.itemsize, _native.ODE_DTYPE.itemsize
         out = torch.empty((n, 6), dtype=torch.float64, device=self.device)
         status = torch.zeros(n, dtype=torch.int32, device=self.device)
-        work = None
         keep = []
         tables = {"points": n, "tables": 0, "per_point_chunks": 0, "chunks": 0}
+        # plan every chunk first (the table grouping synchronises with the host), then launch
+        plan = []
         for c0 in range(0, n, chunk):
             c1 = min(n, c0 + chunk)
             d_pts = d_pts_all[c0 * rp:c1 * rp]
             d_ode = d_ode_all[c0 * ro:c1 * ro]
             rep = table_groups(d_pts, c1 - c0) if share_tables else None
+            d_rep = d_idx = None
             if rep is not None:
-                rep, inv = rep
-            n_tab = (c1 - c0) if rep is None else rep.numel()
+                d_rep = d_pts.view(c1 - c0, rp)[rep[0]].contiguous()
+                d_idx = rep[1].to(torch.int32)
+            n_tab = (c1 - c0) if rep is None else d_rep.shape[0]
             tables["tables"] += n_tab
             tables["chunks"] += 1
             if rep is None and c1 - c0 > 1:
@@ -313,40 +316,61 @@ class Engine:
                         "table per point (an A/V z-sum table build each; the integration still shares stage rows "
                         "across tables) -- ~2.4x the cost per point of a shared-table sweep on a 20000-step "
                         "window (DESIGN §5.3)", c1 - c0, c1 - c0, ", ".join(_native.ODE_TABLE_KEY))
-            if work is None or work.numel() < n_tab * _native.ODE_WS_PER_POINT:
-                work = self.ode_workspace(max(n_tab, min(n, chunk) if rep is None else n_tab))
-            with torch.cuda.device(self.device):
+            plan.append((c0, c1, d_pts, d_ode, d_rep, d_idx, n_tab))
+            keep.append((d_pts, d_ode, d_rep, d_idx))
+        # Two or more chunks: chunk c + 1's spline tables are built on a side stream into the other
+        # of two workspaces while chunk c integrates (the table kernels fill the SIMDs the
+        # integrator's tail leaves idle); events order each workspace's reuse.  One chunk: one stream.
+        main = torch.cuda.current_stream(self.device)
+        piped = len(plan) > 1 and getattr(self, "ode_pipeline", True)
+        side = torch.cuda.Stream(self.device) if piped else main
+        ws_n = max(p[6] for p in plan) if plan else 0
+        works = [self.ode_workspace(ws_n) for _ in range(2 if piped else 1)] if plan else []
+        if piped:
+            side.wait_stream(main)          # the records and the grouping above are on the main stream
+            for w in works:
+                w.record_stream(side)
+            for item in keep:
+                for t in item:
+                    if t is not None:
+                        t.record_stream(side)
+        freed = [None] * len(works)
+        nt = _native.ODE_NT
+        with torch.cuda.device(self.device):
+            for ci, (c0, c1, d_pts, d_ode, d_rep, d_idx, n_tab) in enumerate(plan):
+                b = ci % len(works)
+                work = works[b]
+                with torch.cuda.stream(side):
+                    if freed[b] is not None:
+                        side.wait_event(freed[b])
+                    src = d_pts if d_rep is None else d_rep
+                    self._check(self.lib.lzq_ode_tables(_vp(src), n_tab, None, None, nt, nz, z_max, _vp(work),
+                                                        work.numel(),
+                                                        _vp(status[c0:c1]) if d_rep is None and method == "radau"
+                                                        else None,
+                                                        self._stream()))
+                    built = torch.cuda.Event() if piped else None
+                    if piped:
+                        built.record(side)
+                if piped:
+                    main.wait_event(built)
                 if method == "quadrature":
-                    nt = _native.ODE_NT
-                    if rep is None:
-                        self._check(self.lib.lzq_ode_tables(_vp(d_pts), c1 - c0, None, None, nt, nz, z_max, _vp(work),
-                                                            work.numel(), None, self._stream()))
-                        d_idx = None
-                    else:
-                        d_rep = d_pts.view(c1 - c0, _native.POINT_DTYPE.itemsize)[rep].contiguous()
-                        d_idx = inv.to(torch.int32)
-                        self._check(self.lib.lzq_ode_tables(_vp(d_rep), n_tab, None, None, nt, nz, z_max, _vp(work),
-                                                            work.numel(), None, self._stream()))
-                        keep.append((d_rep, d_idx))
                     self._check(self.lib.lzq_ode_quadrature(_vp(d_pts), _vp(d_ode), c1 - c0, _vp(d_idx), n_tab,
                                                             _vp(work), work.numel(), int(max_steps), _vp(out[c0:c1]),
                                                             _vp(status[c0:c1]), self._stream()))
-                elif rep is None:
-                    self._check(self.lib.lzq_ode_batch(_vp(d_pts), _vp(d_ode), c1 - c0, nz, z_max, _vp(work),
-                                                       work.numel(), int(max_steps), _vp(out[c0:c1]),
-                                                       _vp(status[c0:c1]), self._stream()))
+                elif d_rep is None:   # lzq_ode_batch's second half (its tables are built above)
+                    self._check(self.lib.lzq_ode_integrate(_vp(d_pts), _vp(d_ode), c1 - c0, _vp(work), work.numel(),
+                                                           int(max_steps), _vp(out[c0:c1]), _vp(status[c0:c1]),
+                                                           self._stream()))
                 else:
-                    rec = _native.POINT_DTYPE.itemsize
-                    d_rep = d_pts.view(c1 - c0, rec)[rep].contiguous()
-                    d_idx = inv.to(torch.int32)
-                    self._check(self.lib.lzq_ode_tables(_vp(d_rep), n_tab, None, None, _native.ODE_NT, nz, z_max,
-                                                        _vp(work), work.numel(), None, self._stream()))
                     self._check(self.lib.lzq_ode_integrate_shared(_vp(d_pts), _vp(d_ode), c1 - c0, _vp(d_idx),
                                                                   n_tab, _vp(work), work.numel(), int(max_steps),
                                                                   _vp(out[c0:c1]), _vp(status[c0:c1]),
                                                                   self._stream()))
-                    keep.append((d_rep, d_idx))
-            keep.append((d_pts, d_ode))
+                if piped:
+                    freed[b] = torch.cuda.Event()
+                    freed[b].record(main)
+        work = works
         keep.append((d_pts_all, d_ode_all))
         self._keepalive = (keep, work)
         tables["mode"] = "shared" if tables["per_point_chunks"] == 0 else (

@@ -558,6 +558,9 @@ def test_ode_cooperative_table_varying_bit_identical(gpu_engine):
             finally:
                 gpu_engine.tune_ode_launch_steps(prev)
             assert torch_equal(a, c) and torch_equal(sa, sc), (share, method)
+            # chunks of 48 points: the next chunk's tables built on a side stream while one integrates
+            d, sd = gpu_engine.ode(p, o, share_tables=share, method=method, group_waves=False, chunk=48)
+            assert torch_equal(a, d) and torch_equal(sa, sd), (share, method, "chunked")
             if method == "radau":
                 radau = (a.cpu().numpy(), sa.cpu().numpy(), dict(gpu_engine.last_ode_tables))
         if share:

@@ -149,10 +149,21 @@ def kernels_sweep(eng, cfgm, n: int = 262144, chunk: int = 1 << 18):
     (tab, st), dt = timed(lambda: eng.ode(pts, ods, chunk=chunk))
     shared = dict(eng.last_ode_tables)
     (tab_u, st_u), dt_u = timed(lambda: eng.ode(pts, ods, chunk=chunk, share_tables=False), reps=1)
+    unshared = dict(eng.last_ode_tables)
+    # a table per point in 4 chunks: the next chunk's tables built on a side stream while one integrates
+    (tab_p, st_p), dt_p = timed(lambda: eng.ode(pts, ods, chunk=chunk // 4, share_tables=False), reps=1)
+    eng.ode_pipeline = False
+    try:
+        (tab_s, st_s), dt_s = timed(lambda: eng.ode(pts, ods, chunk=chunk // 4, share_tables=False), reps=1)
+    finally:
+        eng.ode_pipeline = True
     print(json.dumps({"config": "riccati_4096_kernels", "points": n, "kernels": 4096, "gpu_points_per_s": n / dt,
                       "ode_tables": shared, "gpu_points_per_s_table_per_point": n / dt_u,
-                      "ode_tables_unshared": eng.last_ode_tables,
-                      "bit_identical": bool(torch.equal(tab, tab_u)),
+                      "ode_tables_unshared": unshared,
+                      "gpu_points_per_s_table_per_point_4_chunks_pipelined": n / dt_p,
+                      "gpu_points_per_s_table_per_point_4_chunks_serial": n / dt_s,
+                      "bit_identical": bool(torch.equal(tab, tab_u)) and bool(torch.equal(tab, tab_p))
+                      and bool(torch.equal(tab, tab_s)),
                       "all_ok": bool((st == 0).all()) and bool((st_u == 0).all())}), flush=True)
 
 

@@ -50,7 +50,8 @@ def interval_steps(knots, coef, yB, ychi, lam, vw, spr: float = 4.0, n_min: int 
     """Magnus steps per point of lzq_lz_propagate_profile (its per-interval rule, vectorised over
     points; knots [n_knots], coef [n_knots - 1, 8] of ONE shape): the launch's work model.  The
     kernel's rule (tests/profile_ref.py interval_steps restates it exactly): rates at t = (q/4) L,
-    q = 0..3, and at the interval's end from the next interval's cubic (the last: its own),
+    q = 0..3, and at the interval's end from the next interval's cubic (the last: its own), E^2 and
+    |dH/dt|^2 as quadratic forms in the shape's samples,
     W2 = max(max E^2, hdot_rate^2 v_w sqrt(max |dH/dt|^2)), S = ceil(spr L / v_w sqrt(W2)).  numpy
     has no fused multiply-add, so a count can differ from the kernel's where spr L / v_w sqrt(W2)
     lies within rounding of an integer (reporting only).  per_interval: the [point, interval]
@@ -59,15 +60,14 @@ def interval_steps(knots, coef, yB, ychi, lam, vw, spr: float = 4.0, n_min: int 
     cols = []
     ivw = 1.0 / np.asarray(vw, dtype=float)
     nI = len(knots) - 1
+    A, B, C = yB * yB + lam * lam, (-2.0 * yB) * ychi, ychi * ychi   # the kernel's quadratic forms
 
     def rates(j, t):
         a = coef[j, 0] + t * (coef[j, 1] + t * (coef[j, 2] + t * coef[j, 3]))
         b = coef[j, 4] + t * (coef[j, 5] + t * (coef[j, 6] + t * coef[j, 7]))
         da = coef[j, 1] + t * (2.0 * coef[j, 2] + t * 3.0 * coef[j, 3])
         db = coef[j, 5] + t * (2.0 * coef[j, 6] + t * 3.0 * coef[j, 7])
-        D, m = yB * a - ychi * b, lam * a
-        Dd, md = yB * da - ychi * db, lam * da
-        return D * D + m * m, Dd * Dd + md * md
+        return A * (a * a) + B * (a * b) + C * (b * b), A * (da * da) + B * (da * db) + C * (db * db)
 
     for j in range(nI):
         L = knots[j + 1] - knots[j]

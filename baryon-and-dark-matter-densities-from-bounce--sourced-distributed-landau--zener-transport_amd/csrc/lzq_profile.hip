@@ -31,10 +31,10 @@
 //                               4 sqrt(|dH/dt|) (4 / the LZ time) at 5 points of the interval
 //                               (from per-shape samples, profile_samples_kernel).  A lane keeps
 //                               its interval's Delta and m coefficients, the state and the step
-//                               in registers; the shape's rows are read once per interval, and
-//                               the lanes of a wave read the same rows (L1/L2 hits: staging them
-//                               in LDS per block, LZQ_PROF_LDS=1, measured 5% slower).  Large
-//                               batches launch in (shape, cost, coupling angle) order
+//                               in registers; the shape's rows are read once per interval, by a
+//                               wave whose points share the shape through the scalar cache
+//                               (round 3 measured staging them in LDS per block 5% slower).
+//                               Large batches launch in (shape, cost, coupling angle) order
 //                               (profile_key_kernel + a radix sort).
 // tests/profile_ref.py restates all three in numpy; tests/test_gpu_profile.py checks them.
 #include <hip/hip_runtime.h>
@@ -53,18 +53,14 @@ int lzq_set_error(int code, const char* msg);
 namespace lzq {
 
 constexpr int kProfBlock = 256;
-#ifndef LZQ_PROF_LDS
-#define LZQ_PROF_LDS 0  // 1: stage the block's shape in LDS (A/B, 1e6 points: 5% slower -- 57 KB per block
-                        // caps the CU at 2 blocks, while every wave's row reads hit L1/L2 anyway)
-#endif
-#ifndef LZQ_PROF_LDS_KNOTS
-#define LZQ_PROF_LDS_KNOTS (LZQ_PROF_LDS ? 256 : 4)  // shapes up to this many knots are staged (LZQ_PROF_LDS)
-#endif
 #ifndef LZQ_PROF_MIN_WAVES
 #define LZQ_PROF_MIN_WAVES 2
 #endif
 #ifndef LZQ_PROF_UNROLL
 #define LZQ_PROF_UNROLL 1  // Magnus steps per loop iteration (A/B: 2 is 4% slower, tools/ablate_profile.py)
+#endif
+#ifndef LZQ_PROF_UNIFORM
+#define LZQ_PROF_UNIFORM 1  // waves whose points share one shape read its rows through the scalar cache
 #endif
 #ifndef LZQ_PROF_SORT
 #define LZQ_PROF_SORT 1  // keyed launch order for batches of >= kProfSortMin points (0: index order)
@@ -416,7 +412,11 @@ __device__ __forceinline__ void magnus6_step(const double (&cD)[4], const double
 // -- phi, Phi, phi', Phi' -- do not depend on the point, so they are evaluated once per launch
 // per (shape, interval) (profile_samples_kernel, stream-ordered scratch, staged in LDS next to the
 // coefficients); a point only combines them with its couplings.
-constexpr int kProfSamp = 20;  // doubles per interval: [q][phi, Phi, phi', Phi'], q = 0..4
+// Stored as the products the rule's quadratic forms need (round 4): per sample
+// [phi^2, phi Phi, Phi^2, phi'^2, phi' Phi', Phi'^2], so a point's E^2 = D^2 + m^2 =
+// (y_B^2 + lambda^2) phi^2 - 2 y_B y_chi phi Phi + y_chi^2 Phi^2 is three operations per sample.
+constexpr int kSampD = 6;                 // doubles per sample
+constexpr int kProfSamp = 5 * kSampD;     // doubles per interval, q = 0..4
 
 __global__ __launch_bounds__(kProfBlock) void profile_samples_kernel(const double* __restrict__ knots,
                                                                      const double* __restrict__ coef, int64_t n_rows,
@@ -430,10 +430,13 @@ __global__ __launch_bounds__(kProfBlock) void profile_samples_kernel(const doubl
 #pragma unroll
   for (int q = 0; q < 5; ++q) {
     const double t = (0.25 * q) * L;
-    o[4 * q + 0] = pp0(c, t);
-    o[4 * q + 1] = pp0(c + 4, t);
-    o[4 * q + 2] = pp1(c, t);
-    o[4 * q + 3] = pp1(c + 4, t);
+    const double a = pp0(c, t), b = pp0(c + 4, t), da = pp1(c, t), db = pp1(c + 4, t);
+    o[kSampD * q + 0] = a * a;
+    o[kSampD * q + 1] = a * b;
+    o[kSampD * q + 2] = b * b;
+    o[kSampD * q + 3] = da * da;
+    o[kSampD * q + 4] = da * db;
+    o[kSampD * q + 5] = db * db;
   }
 }
 
@@ -442,37 +445,44 @@ __global__ __launch_bounds__(kProfBlock) void profile_samples_kernel(const doubl
 // interval's q = 0 sample (the same knot, whose spline value every interval but the last takes
 // from the next piece; the last takes its own q = 4): a lane walking the intervals in order carries
 // that end sample over as the next interval's start, 4 new samples per interval instead of 5.
-// Per sample E^2 = D^2 + m^2 and |dH/dt|^2 = D'^2 + m'^2 (D = y_B phi - y_chi Phi, m = lambda phi,
-// fused multiply-adds); over the interval their maxima e2, h2, then in squares
+// Per sample E^2 = D^2 + m^2 and |dH/dt|^2 = D'^2 + m'^2 (D = y_B phi - y_chi Phi, m = lambda phi)
+// as the quadratic forms A phi^2 + B phi Phi + C Phi^2 (and the same in phi', Phi') of the point's
+// RuleForm; over the interval their maxima e2, h2, then in squares
 //   W2 = max(e2, kHdotRate^2 v_w sqrt(h2)),  S = max(n_min, ceil(spr (L (1/v_w)) sqrt(W2)))
 // -- max(E, kHdotRate sqrt(v_w |dH/dt|)) squared: two correctly rounded square roots, no division.
+struct RuleForm {
+  double A, B, C;  // y_B^2 + lambda^2, -2 y_B y_chi, y_chi^2
+};
+
+__device__ __forceinline__ RuleForm rule_form(const ProfPt& p) {
+  return {__builtin_fma(p.yB, p.yB, p.lam * p.lam), (-2.0 * p.yB) * p.ychi, p.ychi * p.ychi};
+}
+
 struct Rates {
   double e2, h2;
 };
 
-__device__ __forceinline__ Rates sample_rates(const double* __restrict__ sr, const ProfPt& p) {
-  const double a = sr[0], b = sr[1], da = sr[2], db = sr[3];
-  const double D = __builtin_fma(p.yB, a, -(p.ychi * b)), m = p.lam * a;
-  const double Dd = __builtin_fma(p.yB, da, -(p.ychi * db)), md = p.lam * da;
-  return {__builtin_fma(D, D, m * m), __builtin_fma(Dd, Dd, md * md)};
+__device__ __forceinline__ Rates sample_rates(const double* __restrict__ sr, const RuleForm& f) {
+  return {__builtin_fma(f.A, sr[0], __builtin_fma(f.B, sr[1], f.C * sr[2])),
+          __builtin_fma(f.A, sr[3], __builtin_fma(f.B, sr[4], f.C * sr[5]))};
 }
 
 __device__ __forceinline__ Rates rates_max(Rates u, Rates v) { return {fmax(u.e2, v.e2), fmax(u.h2, v.h2)}; }
 
 // the end sample of interval j (of K - 1): the next interval's q = 0, or the last interval's own q = 4
 __device__ __forceinline__ const double* end_sample(const double* __restrict__ sm, int j, int K) {
-  return j + 2 < K ? sm + (j + 1) * kProfSamp : sm + j * kProfSamp + 16;
+  return j + 2 < K ? sm + (j + 1) * kProfSamp : sm + j * kProfSamp + 4 * kSampD;
 }
 
 // interval j's rates from its start sample's (`start`, carried) and its q = 1..3 and end samples;
 // `end` returns the end sample's rates (the next interval's start)
-__device__ __forceinline__ Rates interval_rates(const double* __restrict__ sm, int j, int K, const ProfPt& p,
+__device__ __forceinline__ Rates interval_rates(const double* __restrict__ sm, int j, int K, const RuleForm& f,
                                                 Rates start, Rates& end) {
   const double* sr = sm + j * kProfSamp;
   Rates r = start;
 #pragma unroll
-  for (int q = 1; q < 4; ++q) r = rates_max(r, sample_rates(sr + 4 * q, p));
-  end = sample_rates(end_sample(sm, j, K), p);
+  for (int q = 1; q < 4; ++q) r = rates_max(r, sample_rates(sr + kSampD * q, f));
+  end = sample_rates(end_sample(sm, j, K), f);
   return rates_max(r, end);
 }
 
@@ -484,8 +494,9 @@ __device__ __forceinline__ double steps_of(Rates r, double L, const ProfPt& p, d
 // interval j on its own (no carried start): the same samples and operations, the same count
 __device__ __forceinline__ double interval_steps(const double* __restrict__ sm, int j, int K, const ProfPt& p,
                                                  double L, double ivw, double spr, int32_t n_min) {
+  const RuleForm f = rule_form(p);
   Rates end;
-  const Rates r = interval_rates(sm, j, K, p, sample_rates(sm + j * kProfSamp, p), end);
+  const Rates r = interval_rates(sm, j, K, f, sample_rates(sm + j * kProfSamp, f), end);
   return steps_of(r, L, p, ivw, spr, n_min);
 }
 
@@ -514,11 +525,15 @@ __global__ __launch_bounds__(kProfBlock) void profile_key_kernel(const double* _
   double st = 0.0;
   const bool valid = p.vw > 0.0 && p.shape >= 0 && p.shape < n_shapes;
   if (valid) {
-    const double* x = knots + (int64_t)p.shape * K;
-    const double* sm = samp + (int64_t)p.shape * (K - 1) * kProfSamp;
-    const double ivw = 1.0 / p.vw;
-    for (int j = 0; j + 1 < K; j += kProfCostStride) st += interval_steps(sm, j, K, p, x[j + 1] - x[j], ivw, spr, n_min);
-    st *= kProfCostStride;
+    auto cost = [&](const double* __restrict__ x, const double* __restrict__ sm) {
+      const double ivw = 1.0 / p.vw;
+      double c = 0.0;
+      for (int j = 0; j + 1 < K; j += kProfCostStride) c += interval_steps(sm, j, K, p, x[j + 1] - x[j], ivw, spr, n_min);
+      return c * kProfCostStride;
+    };
+    const int64_t s0 = __builtin_amdgcn_readfirstlane(p.shape), sl = p.shape;  // scalar loads when uniform
+    st = (LZQ_PROF_UNIFORM && __all(p.shape == s0)) ? cost(knots + s0 * K, samp + s0 * (K - 1) * kProfSamp)
+                                                    : cost(knots + sl * K, samp + sl * (K - 1) * kProfSamp);
   }
   const double cb = st == st ? fmin(fmax(4.0 * log2(1.0 + st), 0.0), (double)(kCostBins - 1)) : 0.0;
   const uint32_t cost = (uint32_t)((kCostBins - 1) - (int32_t)cb);  // 0 = costliest
@@ -530,56 +545,26 @@ __global__ __launch_bounds__(kProfBlock) void profile_key_kernel(const double* _
   idx[i] = (int32_t)i;
 }
 
-__global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_propagate_kernel(
-    const double* __restrict__ knots, const double* __restrict__ coef, int32_t n_shapes, int32_t K,
-    const lzq_profile_point* __restrict__ pts, int64_t n, double spr, int32_t n_min, const int32_t* __restrict__ order,
-    const double* __restrict__ samp, double* __restrict__ P_out) {
-  __shared__ double s_knots[LZQ_PROF_LDS_KNOTS];
-  __shared__ double s_coef[(LZQ_PROF_LDS_KNOTS - 1) * kProfCoef];
-  __shared__ double s_samp[(LZQ_PROF_LDS_KNOTS - 1) * kProfSamp];
-  const int64_t tid = (int64_t)blockIdx.x * kProfBlock + threadIdx.x;
-  // stage the shape of the block's first point (block-uniform)
-  const int64_t first = (int64_t)blockIdx.x * kProfBlock;
-  const int32_t s0 = pts[order ? (int64_t)order[first] : first].shape;
-  const bool staged = LZQ_PROF_LDS && K <= LZQ_PROF_LDS_KNOTS && s0 >= 0 && s0 < n_shapes;
-  if (staged) {
-    const double* gk = knots + (int64_t)s0 * K;
-    const double* gc = coef + (int64_t)s0 * (K - 1) * kProfCoef;
-    for (int q = threadIdx.x; q < K; q += kProfBlock) s_knots[q] = gk[q];
-    for (int q = threadIdx.x; q < (K - 1) * kProfCoef; q += kProfBlock) s_coef[q] = gc[q];
-    const double* gs = samp + (int64_t)s0 * (K - 1) * kProfSamp;
-    for (int q = threadIdx.x; q < (K - 1) * kProfSamp; q += kProfBlock) s_samp[q] = gs[q];
-  }
-  __syncthreads();
-  if (tid >= n) return;
-  const int64_t i = order ? (int64_t)order[tid] : tid;
-  const ProfPt p = load_point(pts + i);
-  if (!(p.vw > 0.0) || p.shape < 0 || p.shape >= n_shapes) {  // bad wall speed or shape index
-    P_out[i] = __builtin_nan("");
-    return;
-  }
-  const bool mine = staged && p.shape == s0;
-  const double* x = mine ? s_knots : knots + (int64_t)p.shape * K;
-  const double* cf = mine ? s_coef : coef + (int64_t)p.shape * (K - 1) * kProfCoef;
-  const double* sm = mine ? s_samp : samp + (int64_t)p.shape * (K - 1) * kProfSamp;
+// One point through the whole profile (x, cf, sm: its shape's knots, coefficient rows, samples).
+// Returns P, NaN for a non-finite or absurd step count.
+__device__ __forceinline__ double propagate_point(const double* __restrict__ x, const double* __restrict__ cf,
+                                                  const double* __restrict__ sm, int32_t K, const ProfPt& p,
+                                                  double spr, int32_t n_min) {
   const double ivw = 1.0 / p.vw;
-
   double cD[4], cM[4];
   interval_coefs_fma(cf, p, cD, cM);
   Cplx p0, p1;
   edge_state(cD, cM, 0.0, p.vw, p0, p1);
   double L = 0.0;
-  Rates start = sample_rates(sm, p);  // interval 0's q = 0; then each interval's end is the next one's start
+  const RuleForm rf = rule_form(p);
+  Rates start = sample_rates(sm, rf);  // interval 0's q = 0; then each interval's end is the next one's start
   for (int j = 0; j + 1 < K; ++j) {
     if (j > 0) interval_coefs_fma(cf + j * kProfCoef, p, cD, cM);
     L = x[j + 1] - x[j];
     Rates end;
-    const double Sd = steps_of(interval_rates(sm, j, K, p, start, end), L, p, ivw, spr, n_min);
+    const double Sd = steps_of(interval_rates(sm, j, K, rf, start, end), L, p, ivw, spr, n_min);
     start = end;
-    if (!(Sd <= kMaxIntervalSteps)) {  // non-finite or absurd input
-      P_out[i] = __builtin_nan("");
-      return;
-    }
+    if (!(Sd <= kMaxIntervalSteps)) return __builtin_nan("");  // non-finite or absurd input
     const int S = (int)Sd;
     const StepGeom g = step_geom(L, Sd, ivw);
 #pragma unroll LZQ_PROF_UNROLL
@@ -589,7 +574,39 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_propag
   edge_state(cD, cM, L, p.vw, u0, u1);
   const Cplx a = inner(u0, u1, p0, p1);
   const double norm = p0.re * p0.re + p0.im * p0.im + p1.re * p1.re + p1.im * p1.im;
-  P_out[i] = 1.0 - (a.re * a.re + a.im * a.im) / norm;
+  return 1.0 - (a.re * a.re + a.im * a.im) / norm;
+}
+
+// The interval loop walks every lane of a wave through the same knot interval j, so when the wave's
+// points share one shape (the keyed launch order makes that the rule) the interval's rows are the
+// same addresses for all lanes: the shape index is taken from the first lane (readfirstlane) and
+// the rows are read through the scalar cache into SGPRs (s_load; v_fma_f64 takes one SGPR operand
+// for free), not as 64 identical vector loads.  Mixed-shape waves take the per-lane path; both
+// run propagate_point on the same values, so P does not depend on the path.
+__global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_propagate_kernel(
+    const double* __restrict__ knots, const double* __restrict__ coef, int32_t n_shapes, int32_t K,
+    const lzq_profile_point* __restrict__ pts, int64_t n, double spr, int32_t n_min, const int32_t* __restrict__ order,
+    const double* __restrict__ samp, double* __restrict__ P_out) {
+  const int64_t tid = (int64_t)blockIdx.x * kProfBlock + threadIdx.x;
+  if (tid >= n) return;
+  const int64_t i = order ? (int64_t)order[tid] : tid;
+  const ProfPt p = load_point(pts + i);
+  if (!(p.vw > 0.0) || p.shape < 0 || p.shape >= n_shapes) {  // bad wall speed or shape index
+    P_out[i] = __builtin_nan("");
+    return;
+  }
+  const int32_t sh0 = __builtin_amdgcn_readfirstlane(p.shape);
+  double P;
+  if (LZQ_PROF_UNIFORM && __all(p.shape == sh0)) {
+    const int64_t su = sh0;
+    P = propagate_point(knots + su * K, coef + su * (K - 1) * kProfCoef, samp + su * (K - 1) * kProfSamp, K, p, spr,
+                        n_min);
+  } else {
+    const int64_t sl = p.shape;
+    P = propagate_point(knots + sl * K, coef + sl * (K - 1) * kProfCoef, samp + sl * (K - 1) * kProfSamp, K, p, spr,
+                        n_min);
+  }
+  P_out[i] = P;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -629,10 +646,11 @@ __global__ __launch_bounds__(kProfBlock) void profile_steps_kernel(const double*
       const double* sm = samp + (int64_t)p.shape * (K - 1) * kProfSamp;
       uint16_t* row = steps + i * (int64_t)(K - 1);
       const double ivw = 1.0 / p.vw;
-      Rates start = sample_rates(sm, p);
+      const RuleForm rf = rule_form(p);
+      Rates start = sample_rates(sm, rf);
       for (int j = 0; j + 1 < K; ++j) {
         Rates end;
-        const double Sd = steps_of(interval_rates(sm, j, K, p, start, end), x[j + 1] - x[j], p, ivw, spr, n_min);
+        const double Sd = steps_of(interval_rates(sm, j, K, rf, start, end), x[j + 1] - x[j], p, ivw, spr, n_min);
         start = end;
         row[j] = !(Sd <= kMaxIntervalSteps) ? (uint16_t)0 : (Sd < (double)kStepsRecompute ? (uint16_t)Sd : kStepsRecompute);
         tot += Sd;

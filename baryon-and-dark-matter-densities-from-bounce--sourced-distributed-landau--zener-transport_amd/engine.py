@@ -314,7 +314,7 @@ class Engine:
                     _log.warning(
                         "lzq ODE: %d of %d points differ in the A/V kernel or window (ODE_TABLE_KEY: %s): a spline "
                         "table per point (an A/V z-sum table build each; the integration still shares stage rows "
-                        "across tables) -- ~2.4x the cost per point of a shared-table sweep on a 20000-step "
+                        "across tables) -- ~2.6x the cost per point of a shared-table sweep on a 20000-step "
                         "window (DESIGN §5.3)", c1 - c0, c1 - c0, ", ".join(_native.ODE_TABLE_KEY))
             plan.append((c0, c1, d_pts, d_ode, d_rep, d_idx, n_tab))
             keep.append((d_pts, d_ode, d_rep, d_idx))

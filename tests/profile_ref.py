@@ -176,31 +176,37 @@ def fma(a, b, c):
 
 
 def _samples(c, L):
-    """The shape's samples at t_q = (q/4) L, q = 0..4 (profile_samples_kernel): (phi, Phi, phi', Phi')."""
+    """The shape's samples at t_q = (q/4) L, q = 0..4 (profile_samples_kernel), as the products the
+    rule's quadratic forms take: (phi^2, phi Phi, Phi^2, phi'^2, phi' Phi', Phi'^2)."""
     cphi, cPhi = c
-    return [(pp_eval(cphi, (0.25 * q) * L), pp_eval(cPhi, (0.25 * q) * L),
-             pp_eval(cphi, (0.25 * q) * L, 1), pp_eval(cPhi, (0.25 * q) * L, 1)) for q in range(5)]
+    out = []
+    for q in range(5):
+        t = (0.25 * q) * L
+        a, b = pp_eval(cphi, t), pp_eval(cPhi, t)
+        da, db = pp_eval(cphi, t, 1), pp_eval(cPhi, t, 1)
+        out.append((a * a, a * b, b * b, da * da, da * db, db * db))
+    return out
 
 
 def interval_steps(knots, cphi, cPhi, j, yB, ychi, lam, v_w, spr=STEPS_PER_RADIAN, n_min=MIN_STEPS):
     """Uniform Magnus steps on knot interval j: spr x the interval's largest local rate
     omega = max(E, HDOT_RATE sqrt(v_w |dH/dt|)) x its duration (L / v_w), at least n_min.  The rate
     is sampled at t_q = (q/4) L, q = 0..3, from the interval's own cubic and at its end from the
-    next interval's q = 0 sample (the last interval: its own q = 4), with the shape's samples
-    phi, Phi, phi', Phi' (coupling-independent: the kernel precomputes them per shape) combined
-    with the point's couplings: Delta = y_B phi - y_chi Phi, m = lambda phi (eqs.(5),(7)).  The
-    kernel's operations: fused products per sample, the maxima of E^2 and |dH/dt|^2, then
+    next interval's q = 0 sample (the last interval: its own q = 4).  E^2 = D^2 + m^2 with
+    Delta = y_B phi - y_chi Phi, m = lambda phi (eqs.(5),(7)) is the quadratic form
+    A phi^2 + B phi Phi + C Phi^2, A = y_B^2 + lambda^2, B = -2 y_B y_chi, C = y_chi^2, over the
+    shape's (coupling-independent, precomputed) sample products; |dH/dt|^2 the same in phi', Phi'.
+    The kernel's operations: the maxima e2, h2 over the samples, then
     W2 = max(e2, HDOT_RATE^2 (v_w sqrt(h2))), S = ceil((spr (L (1 / v_w))) sqrt(W2))."""
     L = knots[j + 1] - knots[j]
     own = _samples((cphi[j], cPhi[j]), L)
     nI = len(knots) - 1
     end = _samples((cphi[j + 1], cPhi[j + 1]), knots[j + 2] - knots[j + 1])[0] if j + 1 < nI else own[4]
+    A, B, C = fma(yB, yB, lam * lam), (-2.0 * yB) * ychi, ychi * ychi
     e2 = h2 = 0.0
-    for a, b, da, db in own[:4] + [end]:
-        D, m = fma(yB, a, -(ychi * b)), lam * a
-        Dd, md = fma(yB, da, -(ychi * db)), lam * da
-        e2 = max(e2, fma(D, D, m * m))
-        h2 = max(h2, fma(Dd, Dd, md * md))
+    for aa, ab, bb, dada, dadb, dbdb in own[:4] + [end]:
+        e2 = max(e2, fma(A, aa, fma(B, ab, C * bb)))
+        h2 = max(h2, fma(A, dada, fma(B, dadb, C * dbdb)))
     W2 = max(e2, (HDOT_RATE * HDOT_RATE) * (v_w * math.sqrt(h2)))
     return max(n_min, int(math.ceil((spr * (L * (1.0 / v_w))) * math.sqrt(W2))))
 

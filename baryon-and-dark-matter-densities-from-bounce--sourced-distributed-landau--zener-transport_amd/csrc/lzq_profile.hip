@@ -66,7 +66,7 @@ constexpr int kProfBlock = 256;
 #define LZQ_PROF_SORT 1  // keyed launch order for batches of >= kProfSortMin points (0: index order)
 #endif
 constexpr int64_t kProfSortMin = 16384;
-constexpr int kProfCostStride = 4;  // the launch-order cost model samples every 4th knot interval
+constexpr int kProfCostStride = 16;  // the launch-order cost model samples every 16th knot interval
 constexpr double kMaxIntervalSteps = 16777216.0;  // per knot interval; beyond: P = NaN (absurd input)
 constexpr int kProfCoef = 8;                      // doubles per interval row
 constexpr double kHdotRate = 4.0;  // crossing-region rate: kHdotRate / (LZ time), LZ time = |dH/dt|^-1/2
@@ -348,17 +348,38 @@ __device__ __forceinline__ void cos_sinc_short(double x2, double& cs, double& sc
 }
 
 // One sixth-order Magnus step of H = Delta sz + m sx on [t0, t0 + h] of the current knot interval
-// (cD, cM its cubics in t = xi - xi_j; dt = h / v_w the step in time): H at the three Gauss nodes,
-// the Blanes-Casas-Ros commutator form (the alphas lie in the x-z plane, so the commutators are
-// cross products), the exact SU(2) exponential.  ~90 VALU.
+// (cD, cM its cubics in t = xi - xi_j; dt = h / v_w the step in time): H at the three Gauss nodes
+// s -+ delta, s (s = t0 + h/2 the step's midpoint, delta = sqrt(15)/10 h), the Blanes-Casas-Ros
+// commutator form (the alphas lie in the x-z plane, so the commutators are cross products), the
+// exact SU(2) exponential.
+// For a cubic P the three alphas are exact polynomials in the midpoint (round 4; the node values
+// and their differences before):
+//   alpha1 = dt P(s)
+//   alpha2 = sqrt15/3 dt (P(s + delta) - P(s - delta)) = dt h (P'(s) + 0.15 h^2 c3)
+//   alpha3 = 10/3 dt (P(s - delta) - 2 P(s) + P(s + delta)) = 0.5 dt h^2 P''(s) = dt h^2 (c2 + 3 c3 s),
+// so an interval's MagnusPoly holds their coefficients and a step evaluates 3 + 2 + 1 fmas per
+// axis (35 VALU before), with no cancellation in the differences.
 constexpr double kSq15 = 3.872983346207416885;  // sqrt(15)
-struct StepGeom {
-  double h, dt, k2, k3, gh1, gh2, gh3;
+struct MagnusPoly {
+  double ex[4], fx[3], gx[2];  // x: alpha1, alpha2, alpha3 of m as polynomials in s
+  double ez[4], fz[3], gz[2];  // z: the same of Delta
+  double h, hh;                // step, half step
 };
 
-__device__ __forceinline__ StepGeom step_geom(double L, double Sd, double ivw) {
-  constexpr double g1 = 0.5 - kSq15 / 10.0, g3 = 0.5 + kSq15 / 10.0;
-  StepGeom g;
+__device__ __forceinline__ void axis_poly(const double (&c)[4], double dt, double dth, double dth2, double q, double (&e)[4],
+                                          double (&f)[3], double (&g)[2]) {
+#pragma unroll
+  for (int m = 0; m < 4; ++m) e[m] = dt * c[m];
+  f[0] = dth * __builtin_fma(q, c[3], c[1]);
+  f[1] = (2.0 * dth) * c[2];
+  f[2] = (3.0 * dth) * c[3];
+  g[0] = dth2 * c[2];
+  g[1] = (3.0 * dth2) * c[3];
+}
+
+__device__ __forceinline__ MagnusPoly magnus_poly(const double (&cD)[4], const double (&cM)[4], double L, double Sd,
+                                                  double ivw) {
+  MagnusPoly mp;
   // h = L / S by a refined reciprocal (<= 1 ulp from the quotient; the restatement divides): S is
   // an integer >= 1, so v_rcp_f64 + two Newton steps
   double r = __builtin_amdgcn_rcp(Sd);
@@ -366,32 +387,23 @@ __device__ __forceinline__ StepGeom step_geom(double L, double Sd, double ivw) {
   r = __builtin_fma(r, e, r);
   e = __builtin_fma(-Sd, r, 1.0);
   r = __builtin_fma(r, e, r);
-  g.h = L * r;
-  g.dt = g.h * ivw;
-  g.k2 = (kSq15 / 3.0) * g.dt;
-  g.k3 = (10.0 / 3.0) * g.dt;
-  g.gh1 = g1 * g.h;
-  g.gh2 = 0.5 * g.h;
-  g.gh3 = g3 * g.h;
-  return g;
+  mp.h = L * r;
+  mp.hh = 0.5 * mp.h;
+  const double dt = mp.h * ivw, dth = dt * mp.h, dth2 = dth * mp.h, q = 0.15 * (mp.h * mp.h);
+  axis_poly(cM, dt, dth, dth2, q, mp.ex, mp.fx, mp.gx);
+  axis_poly(cD, dt, dth, dth2, q, mp.ez, mp.fz, mp.gz);
+  return mp;
 }
 
-__device__ __forceinline__ void magnus6_step(const double (&cD)[4], const double (&cM)[4], double t0, const StepGeom& g,
-                                             Cplx& p0, Cplx& p1) {
+__device__ __forceinline__ void magnus6_step(const MagnusPoly& mp, double st, Cplx& p0, Cplx& p1) {
 #define FMA __builtin_fma
-  const double dt = g.dt, k2 = g.k2, k3 = g.k3;
-  const double t1 = t0 + g.gh1, t2 = t0 + g.gh2, t3 = t0 + g.gh3;
-  // H at the three Gauss nodes: (x, z) = (m, Delta)
-  const double X1 = FMA(FMA(FMA(cM[3], t1, cM[2]), t1, cM[1]), t1, cM[0]);
-  const double X2 = FMA(FMA(FMA(cM[3], t2, cM[2]), t2, cM[1]), t2, cM[0]);
-  const double X3 = FMA(FMA(FMA(cM[3], t3, cM[2]), t3, cM[1]), t3, cM[0]);
-  const double Z1 = FMA(FMA(FMA(cD[3], t1, cD[2]), t1, cD[1]), t1, cD[0]);
-  const double Z2 = FMA(FMA(FMA(cD[3], t2, cD[2]), t2, cD[1]), t2, cD[0]);
-  const double Z3 = FMA(FMA(FMA(cD[3], t3, cD[2]), t3, cD[1]), t3, cD[0]);
-  // alpha1 = dt A2, alpha2 = sqrt15/3 dt (A3 - A1), alpha3 = 10/3 dt (A3 - 2 A2 + A1)
-  const double x1 = dt * X2, z1 = dt * Z2;
-  const double x2 = k2 * (X3 - X1), z2 = k2 * (Z3 - Z1);
-  const double x3 = k3 * FMA(-2.0, X2, X1 + X3), z3 = k3 * FMA(-2.0, Z2, Z1 + Z3);
+  const double s = FMA(st, mp.h, mp.hh);
+  const double x1 = FMA(FMA(FMA(mp.ex[3], s, mp.ex[2]), s, mp.ex[1]), s, mp.ex[0]);
+  const double z1 = FMA(FMA(FMA(mp.ez[3], s, mp.ez[2]), s, mp.ez[1]), s, mp.ez[0]);
+  const double x2 = FMA(FMA(mp.fx[2], s, mp.fx[1]), s, mp.fx[0]);
+  const double z2 = FMA(FMA(mp.fz[2], s, mp.fz[1]), s, mp.fz[0]);
+  const double x3 = FMA(mp.gx[1], s, mp.gx[0]);
+  const double z3 = FMA(mp.gz[1], s, mp.gz[0]);
   // Lie bracket of -i a.sigma, -i b.sigma is -i (2 a x b).sigma; the alphas lie in the x-z plane
   const double c = 2.0 * FMA(z1, x2, -(x1 * z2));                 // C1 = [alpha1, alpha2]  (y only)
   const double C2x = z1 * c * (1.0 / 30.0);                         // C2 = -[alpha1, 2 alpha3 + C1]/60
@@ -540,8 +552,8 @@ __global__ __launch_bounds__(kProfBlock) void profile_key_kernel(const double* _
   const double ang = atan(p.ychi / p.yB);                            // (-pi/2, pi/2); NaN for 0/0
   const double af = ang == ang ? (ang * (1.0 / 3.141592653589793) + 0.5) * kAngleBins : 0.0;
   const uint32_t ab = (uint32_t)fmin(fmax(af, 0.0), (double)(kAngleBins - 1));
-  const uint32_t sh = valid ? (uint32_t)min(p.shape, 65535) : 65535u;
-  keys[i] = (sh << 15) | (cost << 8) | ab;  // 16 + 7 + 8 bits
+  const uint32_t sh = valid ? (uint32_t)min(p.shape, 65534) : (uint32_t)min(n_shapes, 65535);  // invalid: last
+  keys[i] = (sh << 15) | (cost << 8) | ab;  // shape, 7 + 8 bits
   idx[i] = (int32_t)i;
 }
 
@@ -555,23 +567,25 @@ __device__ __forceinline__ double propagate_point(const double* __restrict__ x, 
   interval_coefs_fma(cf, p, cD, cM);
   Cplx p0, p1;
   edge_state(cD, cM, 0.0, p.vw, p0, p1);
-  double L = 0.0;
   const RuleForm rf = rule_form(p);
   Rates start = sample_rates(sm, rf);  // interval 0's q = 0; then each interval's end is the next one's start
   for (int j = 0; j + 1 < K; ++j) {
-    if (j > 0) interval_coefs_fma(cf + j * kProfCoef, p, cD, cM);
-    L = x[j + 1] - x[j];
+    interval_coefs_fma(cf + j * kProfCoef, p, cD, cM);
+    const double L = x[j + 1] - x[j];
     Rates end;
     const double Sd = steps_of(interval_rates(sm, j, K, rf, start, end), L, p, ivw, spr, n_min);
     start = end;
     if (!(Sd <= kMaxIntervalSteps)) return __builtin_nan("");  // non-finite or absurd input
     const int S = (int)Sd;
-    const StepGeom g = step_geom(L, Sd, ivw);
+    const MagnusPoly mp = magnus_poly(cD, cM, L, Sd, ivw);
+    double sd = 0.0;
 #pragma unroll LZQ_PROF_UNROLL
-    for (int st = 0; st < S; ++st) magnus6_step(cD, cM, (double)st * g.h, g, p0, p1);
+    for (int st = 0; st < S; ++st, sd += 1.0) magnus6_step(mp, sd, p0, p1);
   }
+  // the last interval's rows again for the end state (not kept live across the step loop)
+  interval_coefs_fma(cf + (K - 2) * kProfCoef, p, cD, cM);
   Cplx u0, u1;
-  edge_state(cD, cM, L, p.vw, u0, u1);
+  edge_state(cD, cM, x[K - 1] - x[K - 2], p.vw, u0, u1);
   const Cplx a = inner(u0, u1, p0, p1);
   const double norm = p0.re * p0.re + p0.im * p0.im + p1.re * p1.re + p1.im * p1.im;
   return 1.0 - (a.re * a.re + a.im * a.im) / norm;
@@ -690,17 +704,16 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_flat_k
   interval_coefs_fma(cf, p, cD, cM);
   Cplx p0, p1;
   edge_state(cD, cM, 0.0, p.vw, p0, p1);
-  // interval j's step count and geometry; false for a non-finite / absurd count (P = NaN)
-  double L = 0.0;
+  // interval j's step count and Magnus polynomials; false for a non-finite / absurd count (P = NaN)
   int S = 0;
-  StepGeom g;
+  MagnusPoly mp;
   auto enter = [&](int j) -> bool {
-    L = x[j + 1] - x[j];
+    const double L = x[j + 1] - x[j];
     const uint16_t sr = srow[j];
     const double Sd = sr == kStepsRecompute ? interval_steps(sm, j, K, p, L, ivw, spr, n_min) : (double)sr;
     if (sr == 0 || !(Sd <= kMaxIntervalSteps)) return false;
     S = (int)Sd;
-    g = step_geom(L, Sd, ivw);
+    mp = magnus_poly(cD, cM, L, Sd, ivw);
     return true;
   };
   bool ok = enter(0);
@@ -713,7 +726,7 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_flat_k
       if (!ok) break;
       st = 0;
     }
-    magnus6_step(cD, cM, (double)st * g.h, g, p0, p1);
+    magnus6_step(mp, (double)st, p0, p1);
     ++st;
   }
   if (!ok) {
@@ -721,7 +734,7 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_flat_k
     return;
   }
   Cplx u0, u1;
-  edge_state(cD, cM, L, p.vw, u0, u1);
+  edge_state(cD, cM, x[K - 1] - x[K - 2], p.vw, u0, u1);
   const Cplx a = inner(u0, u1, p0, p1);
   const double norm = p0.re * p0.re + p0.im * p0.im + p1.re * p1.re + p1.im * p1.im;
   P_out[i] = 1.0 - (a.re * a.re + a.im * a.im) / norm;
@@ -845,8 +858,11 @@ extern "C" int lzq_lz_propagate_profile(const double* d_knots, const double* d_c
   int rc = LZQ_OK;
   if (LZQ_PROF_SORT && n >= lzq::kProfSortMin) {
     size_t tmp_bytes = 0;
+    // sort only the key bits in use: the shape field needs bits for n_shapes + 1 values (invalid last)
+    int end_bit = 15;
+    while (end_bit < 31 && (int64_t(1) << (end_bit - 15)) <= std::min<int64_t>(n_shapes, 65535)) ++end_bit;
     e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                           (const int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, 31, st);
+                                           (const int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, end_bit, st);
     const size_t arr = ((size_t)n * 4 + 255) & ~(size_t)255;
     if (e == hipSuccess) e = hipMallocAsync((void**)&ws, 4 * arr + tmp_bytes, st);
     if (e == hipSuccess) {
@@ -859,7 +875,7 @@ extern "C" int lzq_lz_propagate_profile(const double* d_knots, const double* d_c
       e = hipGetLastError();
       if (e == hipSuccess)
         e = hipcub::DeviceRadixSort::SortPairs((void*)(ws + 4 * arr), tmp_bytes, (const uint32_t*)keys, keys_sorted,
-                                               (const int32_t*)idx, ord, (int)n, 0, 31, st);
+                                               (const int32_t*)idx, ord, (int)n, 0, end_bit, st);
       order = ord;
     }
   }

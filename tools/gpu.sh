@@ -81,6 +81,10 @@ case "$cmd" in
     timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 \
       SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_SALU --output-format csv -d "$OUT/pmc" -o run -- \
       python3 tools/bench_profile.py "$N" 1 --only propagate --ab > "$OUT/pmc.json" 2> "$OUT/pmc.err" || { tail -5 "$OUT/pmc.err"; exit 2; }
+    timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+      SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS --output-format csv -d "$OUT/pmc_stall" -o run -- \
+      python3 tools/bench_profile.py "$N" 1 --only propagate > "$OUT/pmc_stall.json" 2> "$OUT/pmc_stall.err" \
+      || { tail -5 "$OUT/pmc_stall.err"; exit 2; }
     timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
       python3 tools/bench_profile.py "$N" 3 --only propagate --ab > "$OUT/trace.json" 2> "$OUT/trace.err" || { tail -5 "$OUT/trace.err"; exit 3; }
     echo done

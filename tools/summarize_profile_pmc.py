@@ -41,6 +41,22 @@ def main():
             agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
             disp[k].add(r["Dispatch_Id"])
     per = {k: {c: v / len(disp[k]) for c, v in cs.items()} for k, cs in agg.items()}
+    stall = {}
+    sp = os.path.join(src, "pmc_stall", "run_counter_collection.csv")
+    if os.path.exists(sp):   # wave-time split of the propagation kernel (its own PMC pass)
+        sa, sd = collections.defaultdict(float), set()
+        for r in csv.DictReader(open(sp)):
+            if "profile_propagate_kernel" in r["Kernel_Name"]:
+                sa[r["Counter_Name"]] += float(r["Counter_Value"])
+                sd.add(r["Dispatch_Id"])
+        if sa.get("SQ_WAVE_CYCLES"):
+            wc = sa["SQ_WAVE_CYCLES"]
+            stall = {"kernel": "profile_propagate_kernel", "dispatches": len(sd),
+                     **{c: sa[c] / wc for c in ("SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_LDS",
+                                                 "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY") if c in sa},
+                     "note": "fractions of the waves' cycles (SQ_WAVE_CYCLES): ACTIVE_INST_* = a wave had an "
+                             "instruction of that kind in flight, WAIT_INST_ANY = waiting for an instruction's "
+                             "dependency (issue/latency), WAIT_ANY = waiting on anything (memory included)"}
     stats, sort_ns = {}, 0.0
     rows = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
     for r in rows:
@@ -82,6 +98,7 @@ def main():
                   "keyed launch order",
         "magnus_steps_per_point": bench["magnus_steps_per_point"],
         "paths": paths,
+        "wave_time_split": stall or None,
         "kernels": kern,
         "bench": bench.get("propagate"),
         "note": "wave_valu_per_lane_step = 64 x wave VALU instructions / useful Magnus lane-steps; it counts the "

@@ -395,25 +395,28 @@ __device__ __forceinline__ MagnusPoly magnus_poly(const double (&cD)[4], const d
   return mp;
 }
 
-__device__ __forceinline__ void magnus6_step(const MagnusPoly& mp, double st, Cplx& p0, Cplx& p1) {
+// s: the step's midpoint, advanced by h per step from h/2 (the interval's steps are few, so the
+// running sum stays within a few ulp of (st + 1/2) h)
+__device__ __forceinline__ void magnus6_step(const MagnusPoly& mp, double s, Cplx& p0, Cplx& p1) {
 #define FMA __builtin_fma
-  const double s = FMA(st, mp.h, mp.hh);
   const double x1 = FMA(FMA(FMA(mp.ex[3], s, mp.ex[2]), s, mp.ex[1]), s, mp.ex[0]);
   const double z1 = FMA(FMA(FMA(mp.ez[3], s, mp.ez[2]), s, mp.ez[1]), s, mp.ez[0]);
   const double x2 = FMA(FMA(mp.fx[2], s, mp.fx[1]), s, mp.fx[0]);
   const double z2 = FMA(FMA(mp.fz[2], s, mp.fz[1]), s, mp.fz[0]);
   const double x3 = FMA(mp.gx[1], s, mp.gx[0]);
   const double z3 = FMA(mp.gz[1], s, mp.gz[0]);
-  // Lie bracket of -i a.sigma, -i b.sigma is -i (2 a x b).sigma; the alphas lie in the x-z plane
-  const double c = 2.0 * FMA(z1, x2, -(x1 * z2));                 // C1 = [alpha1, alpha2]  (y only)
-  const double C2x = z1 * c * (1.0 / 30.0);                         // C2 = -[alpha1, 2 alpha3 + C1]/60
-  const double C2y = FMA(x1, z3, -(z1 * x3)) * (1.0 / 15.0);
-  const double C2z = -(x1 * c) * (1.0 / 30.0);
-  const double Lx = FMA(-20.0, x1, -x3), Lz = FMA(-20.0, z1, -z3);  // -20 alpha1 - alpha3 + C1
-  const double Rx = x2 + C2x, Rz = z2 + C2z;                        // alpha2 + C2  (Ry = C2y)
-  const double nx = FMA(FMA(c, Rz, -(Lz * C2y)), 1.0 / 120.0, FMA(x3, 1.0 / 12.0, x1));
+  // Lie bracket of -i a.sigma, -i b.sigma is -i (2 a x b).sigma; the alphas lie in the x-z plane.
+  // C1 = [alpha1, alpha2] = (0, c, 0), c = 2 ch; C2 = -[alpha1, 2 alpha3 + C1]/60 = (z1 c/30,
+  // 2 C2h, -x1 c/30); Omega = alpha1 + alpha3/12 + (L x R)/240 with L = -20 alpha1 - alpha3 + C1,
+  // R = alpha2 + C2 -- carried with the factors 2 of c and C2_y folded into the constants.
+  const double ch = FMA(z1, x2, -(x1 * z2));
+  const double c15 = ch * (1.0 / 15.0);
+  const double C2h = FMA(x1, z3, -(z1 * x3)) * (1.0 / 30.0);        // C2_y / 2
+  const double Lx = FMA(-20.0, x1, -x3), Lz = FMA(-20.0, z1, -z3);  // L = (Lx, c, Lz)
+  const double Rx = FMA(z1, c15, x2), Rz = FMA(-x1, c15, z2);       // R = (Rx, 2 C2h, Rz)
+  const double nx = FMA(FMA(ch, Rz, -(Lz * C2h)), 1.0 / 60.0, FMA(x3, 1.0 / 12.0, x1));
   const double ny = FMA(Lz, Rx, -(Lx * Rz)) * (1.0 / 120.0);
-  const double nz = FMA(FMA(Lx, C2y, -(c * Rx)), 1.0 / 120.0, FMA(z3, 1.0 / 12.0, z1));
+  const double nz = FMA(FMA(Lx, C2h, -(ch * Rx)), 1.0 / 60.0, FMA(z3, 1.0 / 12.0, z1));
   double cs, sc;
   cos_sinc_short(FMA(nx, nx, FMA(ny, ny, nz * nz)), cs, sc);
   su2_apply(cs, sc * nx, sc * ny, sc * nz, p0, p1);
@@ -578,9 +581,9 @@ __device__ __forceinline__ double propagate_point(const double* __restrict__ x, 
     if (!(Sd <= kMaxIntervalSteps)) return __builtin_nan("");  // non-finite or absurd input
     const int S = (int)Sd;
     const MagnusPoly mp = magnus_poly(cD, cM, L, Sd, ivw);
-    double sd = 0.0;
+    double smid = mp.hh;
 #pragma unroll LZQ_PROF_UNROLL
-    for (int st = 0; st < S; ++st, sd += 1.0) magnus6_step(mp, sd, p0, p1);
+    for (int st = 0; st < S; ++st, smid += mp.h) magnus6_step(mp, smid, p0, p1);
   }
   // the last interval's rows again for the end state (not kept live across the step loop)
   interval_coefs_fma(cf + (K - 2) * kProfCoef, p, cD, cM);
@@ -707,6 +710,7 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_flat_k
   // interval j's step count and Magnus polynomials; false for a non-finite / absurd count (P = NaN)
   int S = 0;
   MagnusPoly mp;
+  double smid = 0.0;  // the current step's midpoint
   auto enter = [&](int j) -> bool {
     const double L = x[j + 1] - x[j];
     const uint16_t sr = srow[j];
@@ -714,6 +718,7 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_flat_k
     if (sr == 0 || !(Sd <= kMaxIntervalSteps)) return false;
     S = (int)Sd;
     mp = magnus_poly(cD, cM, L, Sd, ivw);
+    smid = mp.hh;
     return true;
   };
   bool ok = enter(0);
@@ -726,7 +731,8 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_flat_k
       if (!ok) break;
       st = 0;
     }
-    magnus6_step(mp, (double)st, p0, p1);
+    magnus6_step(mp, smid, p0, p1);
+    smid += mp.h;
     ++st;
   }
   if (!ok) {

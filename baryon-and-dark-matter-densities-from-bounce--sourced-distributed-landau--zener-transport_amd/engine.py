@@ -328,7 +328,7 @@ class Engine:
         works = [self.ode_workspace(ws_n) for _ in range(2 if piped else 1)] if plan else []
         if piped:
             side.wait_stream(main)          # the records and the grouping above are on the main stream
-            for w in works:
+            for w in works + [status]:     # the table kernels write bad-grid statuses on the side stream
                 w.record_stream(side)
             for item in keep:
                 for t in item:

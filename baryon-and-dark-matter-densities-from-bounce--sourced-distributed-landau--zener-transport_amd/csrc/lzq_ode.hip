@@ -123,17 +123,22 @@ __device__ __forceinline__ SplineLoc spline_loc(const OdePoint& o, double T, int
   return {Tq - linspace_at(o.T_lo, o.T_hi, o.stepT, k, nt), k};
 }
 
+// the cubic of one interval, c = (c0, c1, c2, c3) of the PPoly row
+__device__ __forceinline__ double spline_cubic(const double (&c)[4], double s) {
+  if (LZQ_ODE_FMA) return __builtin_fma(__builtin_fma(__builtin_fma(c[0], s, c[1]), s, c[2]), s, c[3]);  // Horner
+  double z = s, res = c[3];
+  res = res + c[2] * z;
+  z = z * s;
+  res = res + c[1] * z;
+  z = z * s;
+  res = res + c[0] * z;
+  return res;
+}
+
 __device__ __forceinline__ double spline_at(const double* __restrict__ w, double s, int k) {
   const double* c = w + 4 * k;
-  const double c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3];
-  if (LZQ_ODE_FMA) return __builtin_fma(__builtin_fma(__builtin_fma(c0, s, c1), s, c2), s, c3);  // Horner, 3 fma
-  double z = s, res = c3;
-  res = res + c2 * z;
-  z = z * s;
-  res = res + c1 * z;
-  z = z * s;
-  res = res + c0 * z;
-  return res;
+  const double cc[4] = {c[0], c[1], c[2], c[3]};
+  return spline_cubic(cc, s);
 }
 
 __device__ __forceinline__ double spline_eval(const OdePoint& o, const double* __restrict__ w, double T,
@@ -453,11 +458,17 @@ __device__ __forceinline__ void solve3_adj(const double (&M)[3][3], double (&b)[
 // and the stage bases, so a cooperative segment with one Gamma_wash forms them once per step
 // for all its lanes; every mode forms them with these operations, so the result does not depend
 // on the mode.
-struct YbRec {
-  double c, d;
+struct YbW {
   double W[3], id;  // d = (sum_j W_j a_j) id: a lane whose a_j differ from the segment's forms its own d (yb_d)
 };
-__device__ __forceinline__ double yb_d(const YbRec& r, const double (&a)[3]) {
+struct YbCD {
+  double c, d;
+};
+struct YbRec {
+  double c, d;
+  double W[3], id;
+};
+__device__ __forceinline__ double yb_d(const YbW& r, const double (&a)[3]) {
   double d = 0.0;
 #pragma unroll
   for (int j = 0; j < 3; ++j) d = __builtin_fma(r.W[j], a[j], d);
@@ -479,7 +490,7 @@ __device__ __forceinline__ YbRec yb_rec(const RadauH& hA, const double (&beta)[3
 #pragma unroll
   for (int j = 0; j < 3; ++j) r.W[j] = __builtin_fma(w2, hA.a[2][j], __builtin_fma(w1, hA.a[1][j], w0 * hA.a[0][j]));
   r.c = ((w0 + w1) + w2) * r.id;
-  r.d = yb_d(r, a);
+  r.d = yb_d(YbW{{r.W[0], r.W[1], r.W[2]}, r.id}, a);
   return r;
 }
 __device__ __forceinline__ YbRec yb_rec(const RadauH& hA, const OdeStage (&st)[3]) {
@@ -822,7 +833,10 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
                                                                   int64_t k_lo, int64_t k_cnt,
                                                                   OdeState* __restrict__ state) {
   __shared__ StageBase s_base[kOdeBlock / 64][64][3];  // cooperative mode
-  __shared__ YbRec s_rec[LZQ_ODE_YBREC && !kChiOnly ? kOdeBlock / 64 : 1][64];  // shared Y_B step maps
+  // shared Y_B step maps, (c, d) and the cofactor weights in separate arrays: the linear waves'
+  // tight loop streams 16-B (c, d) rows
+  __shared__ YbCD s_rcd[LZQ_ODE_YBREC && !kChiOnly ? kOdeBlock / 64 : 1][64];
+  __shared__ YbW s_rw[LZQ_ODE_YBREC && !kChiOnly ? kOdeBlock / 64 : 1][64];
   // Lanes past the end of the batch are clones of their wavefront's first point (they compute
   // it again and write nothing), so a partial wavefront -- a single CLI point included -- is
   // still full and can run cooperatively.
@@ -1003,7 +1017,9 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
             // is this lane's; a table-varying segment's lanes form theirs from W and id)
             const double beta[3] = {o.gamma_w * bs[0].beta, o.gamma_w * bs[1].beta, o.gamma_w * bs[2].beta};
             const double a[3] = {bs[0].a, bs[1].a, bs[2].a};
-            s_rec[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][lane] = yb_rec(hA, beta, a);
+            const YbRec yr = yb_rec(hA, beta, a);
+            s_rcd[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][lane] = {yr.c, yr.d};
+            s_rw[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][lane] = {{yr.W[0], yr.W[1], yr.W[2]}, yr.id};
           }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1018,13 +1034,27 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
           const int nf = (int)(kg - k);
           if (nf > 0) {
             const int r0 = seg + (int)(k - kb);
-            const YbRec* rr = &s_rec[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][r0];
+            const YbCD* rr = &s_rcd[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][r0];
+            const YbW* rw = &s_rw[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][r0];
             if (tab_vary) {  // each step's a_j from this lane's table, then its own d
+              // T falls with x, so the rows' spline intervals run from the first row's stage 0
+              // down to the last row's stage 2; when they are one interval (the rule on long
+              // windows), this lane's four coefficients are read once for the run instead of per
+              // stage (spline_at's operations on the same values)
+              const int k_hi = s_base[wv][r0][0].k, k_lo = s_base[wv][r0 + nf - 1][2].k;
+              double cc[4] = {0.0, 0.0, 0.0, 0.0};
+              if (k_hi == k_lo) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) cc[q] = w[4 * k_hi + q];
+              }
               for (int jj = 0; jj < nf; ++jj) {
                 double a[3];
 #pragma unroll
-                for (int j = 0; j < 3; ++j) a[j] = row_a(s_base[wv][r0 + jj][j]);
-                YB = __builtin_fma(rr[jj].c, YB, o.Pf * yb_d(rr[jj], a));
+                for (int j = 0; j < 3; ++j) {
+                  const StageBase& b = s_base[wv][r0 + jj][j];
+                  a[j] = (k_hi == k_lo ? spline_cubic(cc, b.s) : spline_at(w, b.s, b.k)) * b.ap;
+                }
+                YB = __builtin_fma(rr[jj].c, YB, o.Pf * yb_d(rw[jj], a));
                 if (o.deplete) {
                   double acc = Ychi;
 #pragma unroll
@@ -1041,8 +1071,17 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
                 Ychi = acc;
               }
             } else {
-#pragma unroll 4
-              for (int jj = 0; jj < nf; ++jj) YB = __builtin_fma(rr[jj].c, YB, o.Pf * rr[jj].d);
+              // the rows in batches of 8: their LDS reads are independent of Y_B, so all eight are
+              // issued before the chain of fmas needs the first
+              int jj = 0;
+              for (; jj + 8 <= nf; jj += 8) {
+                YbCD q[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) q[u] = rr[jj + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) YB = __builtin_fma(q[u].c, YB, o.Pf * q[u].d);
+              }
+              for (; jj < nf; ++jj) YB = __builtin_fma(rr[jj].c, YB, o.Pf * rr[jj].d);
             }
             k = kg;
           }
@@ -1087,15 +1126,16 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
               sg[j] = (kChiOnly && !o.deplete) ? ode_stage_chi(o, xk + R.c[j] * hs) : ode_stage(o, w, xk + R.c[j] * hs);
           }
           if (LZQ_ODE_YBREC && !kChiOnly) {  // Y_B by its step map, then Y_chi alone
-            YbRec r;
+            YbCD r;
             if (rec_shared && !split) {
-              r = s_rec[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][seg + (k - kb)];
+              r = s_rcd[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][seg + (k - kb)];
               if (tab_vary) {
                 const double a[3] = {sg[0].a, sg[1].a, sg[2].a};
-                r.d = yb_d(r, a);
+                r.d = yb_d(s_rw[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][seg + (k - kb)], a);
               }
             } else {
-              r = yb_rec(split ? radau_h(R, hs) : hA, sg);
+              const YbRec yr = yb_rec(split ? radau_h(R, hs) : hA, sg);
+              r = {yr.c, yr.d};
             }
             YB = __builtin_fma(r.c, YB, o.Pf * r.d);
             ok = radau_step<false>(split ? radau_h(R, hs) : hA, sg, Ychi, YB, Zs, use_guess);
@@ -1111,7 +1151,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
           for (int j = 0; j < 3; ++j)
             sg[j] = (kChiOnly && !o.deplete) ? ode_stage_chi(o, xb + R.c[j] * hs) : ode_stage(o, w, xb + R.c[j] * hs);
           if (LZQ_ODE_YBREC && !kChiOnly) {
-            const YbRec r = yb_rec(radau_h(R, hs), sg);
+            const YbRec r = yb_rec(radau_h(R, hs), sg);  // the split step's second part
             YB = __builtin_fma(r.c, YB, o.Pf * r.d);
             ok = radau_step<false>(radau_h(R, hs), sg, Ychi, YB, Zs, false);
           } else {

@@ -574,6 +574,40 @@ def test_ode_cooperative_table_varying_bit_identical(gpu_engine):
                 assert rel_err(v, w) < 1e-10, (v, w)
 
 
+def test_ode_linear_waves_table_varying_bit_identical(gpu_engine):
+    """Linear cooperative waves (sigma_v = 0, one Gamma_wash per segment) whose points each have
+    their own A/V kernel (I_p): the tight loop forms a_j from each lane's table, reading the lane's
+    spline row once per run of steps inside one knot interval (a window with ~60 steps per interval
+    takes both branches).  Bits equal the per-lane mode's, also as continuation launches."""
+    rng = np.random.default_rng(5)
+    cfgs = []
+    for _ in range(128):
+        c = full_cfg(BASE_CFG)
+        c.update(T_max_over_Tp=1.6, T_min_over_Tp=0.3, I_p=float(rng.uniform(0.1, 1.0)), Gamma_wash_over_H=1.0,
+                 sigma_v_chi_GeV_m2=0.0, P_chi_to_B=float(rng.uniform(0.05, 1.0)),
+                 deplete_DM_from_source=bool(rng.uniform() < 0.5))
+        cfgs.append(c)
+    p, o = recs(cfgs)
+    a, sa = gpu_engine.ode(p, o, group_waves=False)
+    assert gpu_engine.last_ode_tables["mode"] == "per_point" and bool((sa == 0).all())
+    prev = gpu_engine.tune_ode_coop(False)
+    try:
+        b, sb = gpu_engine.ode(p, o, group_waves=False)
+    finally:
+        gpu_engine.tune_ode_coop(prev)
+    assert torch_equal(a, b) and torch_equal(sa, sb)
+    prev = gpu_engine.tune_ode_launch_steps(12)
+    try:
+        c, sc = gpu_engine.ode(p, o, group_waves=False)
+    finally:
+        gpu_engine.tune_ode_launch_steps(prev)
+    assert torch_equal(a, c) and torch_equal(sa, sc)
+    ref, sr = O.ode_batch(cfgs[::32], nthreads=16)
+    for row, rr in zip(a.cpu().numpy()[::32], ref):
+        for v, w in zip(row[:5], rr[:5]):
+            assert rel_err(v, w) < 1e-10, (v, w)
+
+
 def test_ode_linear_waves_degenerate_step(gpu_engine):
     """A window so narrow that a step is below x's rounding (T_max / T_min - 1 = 2e-12: h ~ 1e-16 x,
     so xk + h == xk on many steps and the general path skips them): the linear integrator

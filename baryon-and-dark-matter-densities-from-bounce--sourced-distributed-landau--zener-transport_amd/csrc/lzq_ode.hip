@@ -519,6 +519,13 @@ __constant__ double kRadauAinv[3][3] = {
 __constant__ double kRadauAinvP[9] = {-0x1.fbb0962b0c0cap+2, 0x1.e8360f1027593p+0, 0x1.3adf0cf78af17p+0,
                                       0x1.74e16b2ae518ap+2,  -0x1.6692fca92522fp+0, 0x1.ce862a552e616p-1,
                                       0x1.adf74aa6f6bf3p+4,  0x1.9d782ab97a58ap+2,  -0x1.0aaaaaaaaaaabp+2};
+// fma(z, a, c) with the constant a as the SGPR operand, three-address (no copy of the addend)
+__device__ __forceinline__ double fma_s(double z, double a, double c) {
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(z), "s"(a), "v"(c));
+  return r;
+}
+
 // fma(k, -a, p) for two constants a, p: a (wave-uniform) as the one SGPR operand with its negate
 // modifier, p in a VGPR, three-address.  Written as __builtin_fma the compiler picks v_fmac_f64,
 // which overwrites its addend, and copies p into the destination first (a v_mov_b64 per entry per
@@ -1102,9 +1109,8 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
           use_guess = true;
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
-            g[j] = __builtin_fma(kRadauPred[j][3], Zs[2],
-                                 __builtin_fma(kRadauPred[j][2], Zs[1],
-                                               __builtin_fma(kRadauPred[j][1], Zs[0], kRadauPred[j][0] * Yp)));
+            g[j] = fma_s(Zs[2], kRadauPred[j][3], fma_s(Zs[1], kRadauPred[j][2],
+                                                        fma_s(Zs[0], kRadauPred[j][1], kRadauPred[j][0] * Yp)));
             use_guess = use_guess && fabs(g[j] - Ychi) <= 0.25 * fabs(Ychi);
           }
 #pragma unroll

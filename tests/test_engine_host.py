@@ -66,6 +66,27 @@ def test_wave_order_no_repeats_or_small():
     assert int(np.count_nonzero(d[1:] != d[:-1])) == 1
 
 
+def test_wave_order_groups_across_tables():
+    """Points that differ only in the A/V kernel (I_p, v_w: their own spline tables) share a
+    cooperative key (_native.ODE_COOP_KEY) and are grouped together; within a group, points of
+    one table are contiguous (ODE_STAGE_KEY runs)."""
+    rng = np.random.default_rng(8)
+    cfgs = []
+    for i in range(400):
+        c = full_cfg(BASE_CFG)
+        c.update(m_chi_GeV=(0.95, 40.0)[i % 2], I_p=(0.2, 0.5, 0.8, 0.3)[(i // 2) % 4], Gamma_wash_over_H=1.0,
+                 P_chi_to_B=float(rng.uniform(0.1, 1.0)))
+        cfgs.append(c)
+    p, o = _recs(cfgs)
+    order = _order(p, o)
+    assert order is not None and sorted(order.tolist()) == list(range(len(cfgs)))
+    m, ip = p["m_chi_GeV"][order], p["I_p"][order]
+    assert int(np.count_nonzero(m[1:] != m[:-1])) == 1          # two cooperative groups
+    runs = int(np.count_nonzero((ip[1:] != ip[:-1]) | (m[1:] != m[:-1])))
+    assert runs == 7                                             # 2 groups x 4 tables, each contiguous
+    assert set(pkg("_native").ODE_COOP_KEY) == set(pkg("_native").ODE_STAGE_KEY) - {"I_p", "v_w"}
+
+
 def test_ode_step_counts_device_equals_host():
     """Engine.ode sizes its continuation launches from ode_step_counts_device (torch ops on the
     device records); it must give the numpy ode_step_counts' values exactly, edge cases included

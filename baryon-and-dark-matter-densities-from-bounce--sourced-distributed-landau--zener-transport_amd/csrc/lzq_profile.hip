@@ -359,7 +359,6 @@ __device__ __forceinline__ void cos_sinc_short(double x2, double& cs, double& sc
 //   alpha3 = 10/3 dt (P(s - delta) - 2 P(s) + P(s + delta)) = 0.5 dt h^2 P''(s) = dt h^2 (c2 + 3 c3 s),
 // so an interval's MagnusPoly holds their coefficients and a step evaluates 3 + 2 + 1 fmas per
 // axis (35 VALU before), with no cancellation in the differences.
-constexpr double kSq15 = 3.872983346207416885;  // sqrt(15)
 struct MagnusPoly {
   double ex[4], fx[3], gx[2];  // x: alpha1, alpha2, alpha3 of m as polynomials in s
   double ez[4], fz[3], gz[2];  // z: the same of Delta

@@ -549,6 +549,9 @@ __device__ __forceinline__ double fma_neg_s(double k, double a, double p) {
 #ifndef LZQ_ODE_PEEL
 #define LZQ_ODE_PEEL 1  // the first two Newton iterations (and the Y_B solve) as one straight-line block
 #endif
+#ifndef LZQ_ODE_NEWTON2
+#define LZQ_ODE_NEWTON2 1  // the peeled pair of Newton iterations always both applied (no iterate selects)
+#endif
 #ifndef LZQ_ODE_LINFAST
 #define LZQ_ODE_LINFAST 1  // one fma per regular step on linear cooperative waves (sigma_v = 0, no depletion)
 #endif
@@ -688,6 +691,16 @@ __device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st
       // scheduler interleaves their dependent chains; the second is applied only if the first
       // did not converge -- the same iterates as the loop below, bit for bit
       if (kWithYB) YB = yb_step();
+#if LZQ_ODE_NEWTON2
+      // both iterations always apply: a step that converged at the first takes the second's
+      // (below 1e-15 relative) correction too, so no selects between the two iterates are needed
+      const bool c1 = newton(Z);
+      const bool c2 = newton(Z);
+      if (c1 || c2) {
+        accept(Z);
+        return true;
+      }
+#else
       double Z2[3];
       const bool c1 = newton(Z);
       Z2[0] = Z[0];
@@ -705,6 +718,7 @@ __device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st
       Z[0] = Z2[0];
       Z[1] = Z2[1];
       Z[2] = Z2[2];
+#endif
       it = 2;
     }
 #else

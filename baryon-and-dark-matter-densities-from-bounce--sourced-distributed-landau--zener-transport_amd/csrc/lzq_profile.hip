@@ -327,26 +327,6 @@ __device__ __forceinline__ void edge_state(const double* cD, const double* cM, d
                    u1);
 }
 
-// cos|n| and sin|n|/|n| from |n|^2: at >= 3 steps per radian |n|^2 <~ 0.12, where the Taylor
-// series need only 7 (sinc) and 8 (cos) terms for < 1e-16 at |n|^2 <= 1/4 (lzq_su2.h cos_sinc,
-// 9 and 10 terms up to 1, beyond it).
-#ifndef LZQ_PROF_SHORTSC
-#define LZQ_PROF_SHORTSC 1
-#endif
-__device__ __forceinline__ void cos_sinc_short(double x2, double& cs, double& sc) {
-  if (LZQ_PROF_SHORTSC && x2 <= 0.25) {
-    double ps = kSincC[6], pc = kCosC[7];
-#pragma unroll
-    for (int k = 5; k >= 0; --k) ps = fma3s(ps, x2, kSincC[k]);
-#pragma unroll
-    for (int k = 6; k >= 0; --k) pc = fma3s(pc, x2, kCosC[k]);
-    sc = ps;
-    cs = pc;
-  } else {
-    cos_sinc(x2, cs, sc);
-  }
-}
-
 // One sixth-order Magnus step of H = Delta sz + m sx on [t0, t0 + h] of the current knot interval
 // (cD, cM its cubics in t = xi - xi_j; dt = h / v_w the step in time): H at the three Gauss nodes
 // s -+ delta, s (s = t0 + h/2 the step's midpoint, delta = sqrt(15)/10 h), the Blanes-Casas-Ros
@@ -358,22 +338,26 @@ __device__ __forceinline__ void cos_sinc_short(double x2, double& cs, double& sc
 //   alpha2 = sqrt15/3 dt (P(s + delta) - P(s - delta)) = dt h (P'(s) + 0.15 h^2 c3)
 //   alpha3 = 10/3 dt (P(s - delta) - 2 P(s) + P(s + delta)) = 0.5 dt h^2 P''(s) = dt h^2 (c2 + 3 c3 s),
 // so an interval's MagnusPoly holds their coefficients and a step evaluates 3 + 2 + 1 fmas per
-// axis (35 VALU before), with no cancellation in the differences.
+// axis (35 VALU before), with no cancellation in the differences.  The polynomials are written in
+// u = s / h = st + 1/2 (coefficient of u^m = that of s^m times h^m): u is exact in a double, so the
+// step's midpoint does not drift however many steps an interval takes (a running s += h drifted by
+// up to ~2^-53 S relative, ~1.6e-10 at S = 1.4e6, which moved the long Weber fixtures 1.6e-10 -> 4.9e-10).
 struct MagnusPoly {
-  double ex[4], fx[3], gx[2];  // x: alpha1, alpha2, alpha3 of m as polynomials in s
+  double ex[4], fx[3], gx[2];  // x: alpha1, alpha2, alpha3 of m as polynomials in u
   double ez[4], fz[3], gz[2];  // z: the same of Delta
-  double h, hh;                // step, half step
 };
 
-__device__ __forceinline__ void axis_poly(const double (&c)[4], double dt, double dth, double dth2, double q, double (&e)[4],
-                                          double (&f)[3], double (&g)[2]) {
+// dk[m] = dt h^m: the coefficient of u^m in alpha1 is dk[m] c_m, and 3 dk[3] c3 is both alpha2's u^2
+// and alpha3's u coefficient, so an interval costs what the polynomials in s did
+__device__ __forceinline__ void axis_poly(const double (&c)[4], const double (&dk)[4], double q, double dk2x2,
+                                          double dk3x3, double (&e)[4], double (&f)[3], double (&g)[2]) {
 #pragma unroll
-  for (int m = 0; m < 4; ++m) e[m] = dt * c[m];
-  f[0] = dth * __builtin_fma(q, c[3], c[1]);
-  f[1] = (2.0 * dth) * c[2];
-  f[2] = (3.0 * dth) * c[3];
-  g[0] = dth2 * c[2];
-  g[1] = (3.0 * dth2) * c[3];
+  for (int m = 0; m < 4; ++m) e[m] = dk[m] * c[m];
+  f[0] = dk[1] * __builtin_fma(q, c[3], c[1]);
+  f[1] = dk2x2 * c[2];
+  f[2] = dk3x3 * c[3];
+  g[0] = dk[2] * c[2];
+  g[1] = f[2];
 }
 
 __device__ __forceinline__ MagnusPoly magnus_poly(const double (&cD)[4], const double (&cM)[4], double L, double Sd,
@@ -386,24 +370,24 @@ __device__ __forceinline__ MagnusPoly magnus_poly(const double (&cD)[4], const d
   r = __builtin_fma(r, e, r);
   e = __builtin_fma(-Sd, r, 1.0);
   r = __builtin_fma(r, e, r);
-  mp.h = L * r;
-  mp.hh = 0.5 * mp.h;
-  const double dt = mp.h * ivw, dth = dt * mp.h, dth2 = dth * mp.h, q = 0.15 * (mp.h * mp.h);
-  axis_poly(cM, dt, dth, dth2, q, mp.ex, mp.fx, mp.gx);
-  axis_poly(cD, dt, dth, dth2, q, mp.ez, mp.fz, mp.gz);
+  const double h = L * r;
+  const double dt = h * ivw, dth = dt * h, dth2 = dth * h;
+  const double dk[4] = {dt, dth, dth2, dth2 * h};
+  const double q = 0.15 * (h * h), dk2x2 = 2.0 * dk[2], dk3x3 = 3.0 * dk[3];
+  axis_poly(cM, dk, q, dk2x2, dk3x3, mp.ex, mp.fx, mp.gx);
+  axis_poly(cD, dk, q, dk2x2, dk3x3, mp.ez, mp.fz, mp.gz);
   return mp;
 }
 
-// s: the step's midpoint, advanced by h per step from h/2 (the interval's steps are few, so the
-// running sum stays within a few ulp of (st + 1/2) h)
-__device__ __forceinline__ void magnus6_step(const MagnusPoly& mp, double s, Cplx& p0, Cplx& p1) {
+// u: the step's midpoint in units of the step, st + 1/2 (exact)
+__device__ __forceinline__ void magnus6_step(const MagnusPoly& mp, double u, Cplx& p0, Cplx& p1) {
 #define FMA __builtin_fma
-  const double x1 = FMA(FMA(FMA(mp.ex[3], s, mp.ex[2]), s, mp.ex[1]), s, mp.ex[0]);
-  const double z1 = FMA(FMA(FMA(mp.ez[3], s, mp.ez[2]), s, mp.ez[1]), s, mp.ez[0]);
-  const double x2 = FMA(FMA(mp.fx[2], s, mp.fx[1]), s, mp.fx[0]);
-  const double z2 = FMA(FMA(mp.fz[2], s, mp.fz[1]), s, mp.fz[0]);
-  const double x3 = FMA(mp.gx[1], s, mp.gx[0]);
-  const double z3 = FMA(mp.gz[1], s, mp.gz[0]);
+  const double x1 = FMA(FMA(FMA(mp.ex[3], u, mp.ex[2]), u, mp.ex[1]), u, mp.ex[0]);
+  const double z1 = FMA(FMA(FMA(mp.ez[3], u, mp.ez[2]), u, mp.ez[1]), u, mp.ez[0]);
+  const double x2 = FMA(FMA(mp.fx[2], u, mp.fx[1]), u, mp.fx[0]);
+  const double z2 = FMA(FMA(mp.fz[2], u, mp.fz[1]), u, mp.fz[0]);
+  const double x3 = FMA(mp.gx[1], u, mp.gx[0]);
+  const double z3 = FMA(mp.gz[1], u, mp.gz[0]);
   // Lie bracket of -i a.sigma, -i b.sigma is -i (2 a x b).sigma; the alphas lie in the x-z plane.
   // C1 = [alpha1, alpha2] = (0, c, 0), c = 2 ch; C2 = -[alpha1, 2 alpha3 + C1]/60 = (z1 c/30,
   // 2 C2h, -x1 c/30); Omega = alpha1 + alpha3/12 + (L x R)/240 with L = -20 alpha1 - alpha3 + C1,
@@ -580,9 +564,9 @@ __device__ __forceinline__ double propagate_point(const double* __restrict__ x, 
     if (!(Sd <= kMaxIntervalSteps)) return __builtin_nan("");  // non-finite or absurd input
     const int S = (int)Sd;
     const MagnusPoly mp = magnus_poly(cD, cM, L, Sd, ivw);
-    double smid = mp.hh;
+    double smid = 0.5;
 #pragma unroll LZQ_PROF_UNROLL
-    for (int st = 0; st < S; ++st, smid += mp.h) magnus6_step(mp, smid, p0, p1);
+    for (int st = 0; st < S; ++st, smid += 1.0) magnus6_step(mp, smid, p0, p1);
   }
   // the last interval's rows again for the end state (not kept live across the step loop)
   interval_coefs_fma(cf + (K - 2) * kProfCoef, p, cD, cM);
@@ -709,7 +693,7 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_flat_k
   // interval j's step count and Magnus polynomials; false for a non-finite / absurd count (P = NaN)
   int S = 0;
   MagnusPoly mp;
-  double smid = 0.0;  // the current step's midpoint
+  double smid = 0.0;  // the current step's midpoint, in steps
   auto enter = [&](int j) -> bool {
     const double L = x[j + 1] - x[j];
     const uint16_t sr = srow[j];
@@ -717,7 +701,7 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_flat_k
     if (sr == 0 || !(Sd <= kMaxIntervalSteps)) return false;
     S = (int)Sd;
     mp = magnus_poly(cD, cM, L, Sd, ivw);
-    smid = mp.hh;
+    smid = 0.5;
     return true;
   };
   bool ok = enter(0);
@@ -731,7 +715,7 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_flat_k
       st = 0;
     }
     magnus6_step(mp, smid, p0, p1);
-    smid += mp.h;
+    smid += 1.0;
     ++st;
   }
   if (!ok) {

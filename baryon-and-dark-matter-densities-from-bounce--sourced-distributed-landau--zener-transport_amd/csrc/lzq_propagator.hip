@@ -119,6 +119,10 @@ __device__ __forceinline__ void chi_like_dressed(double d, double ddot, double m
   u1 = plus ? b.p1 : b.q1;
 }
 
+#ifndef LZQ_PROP_POLY
+#define LZQ_PROP_POLY 1  // 0: the Magnus vector from D and E^2 per step (round 3; tools/ablate_prop.py)
+#endif
+
 #ifndef LZQ_PROP_CORE
 #define LZQ_PROP_CORE 1  // 0: Magnus over every whole cell (round-1 scheme; tools/ablate_prop.py)
 #endif
@@ -375,6 +379,26 @@ __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_k
       // oracle-matching kernels, so contraction is spelled out): 63 VALU per step where the
       // separate products and sums took 84.
 #define FMA __builtin_fma
+#if LZQ_PROP_POLY
+      // Round 4: n as polynomials in the step's midpoint D = D0 + i dD (D linear in xi):
+      //   n_x = kx0 + kx2 D^2,  n_y = ky0 + ky2 D^2 + ky4 D^4,  n_z = cz D
+      // (the header's coefficients expanded in E^2 = D^2 + m^2 once per cell), 7 VALU for the
+      // Magnus vector where the expressions above take 15.
+      const double D0 = slope * ((cl - xcc) + 0.5 * h), dD = slope * h;
+      const double kx0 = cxm * FMA(-bx, m2x4, ax), kx2 = -3.0 * cxm * bx;
+      const double ky0 = cy * FMA(ey2, FMA(8.0 * m2, m2, -dd2x9), FMA(ey1, m2, 1.0 / 6.0));
+      const double ky2 = cy * FMA(16.0 * ey2, m2, ey1), ky4 = 8.0 * cy * ey2;
+      auto step = [&](int i) {
+        const double D = FMA((double)i, dD, D0);
+        const double D2 = D * D;
+        const double nx = FMA(kx2, D2, kx0);
+        const double ny = FMA(FMA(ky4, D2, ky2), D2, ky0);
+        const double nz = cz * D;
+        double cs, sc;  // cos|n| and sin|n|/|n|, both functions of |n|^2
+        cos_sinc_short(FMA(nx, nx, FMA(ny, ny, nz * nz)), cs, sc);
+        su2_apply(cs, sc * nx, sc * ny, sc * nz, p0, p1);
+      };
+#else
       auto step = [&](int i) {
         const double xm = FMA((double)i + 0.5, h, cl);
         const double D = slope * (xm - xcc);
@@ -386,6 +410,7 @@ __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_k
         cos_sinc(FMA(nx, nx, FMA(ny, ny, nz * nz)), cs, sc);
         su2_apply(cs, sc * nx, sc * ny, sc * nz, p0, p1);
       };
+#endif
       // unrolled by hand: the polynomial's inline asm (fma3) is convergent, which rules out
       // the compiler's runtime unrolling
       int i = 0;

@@ -65,6 +65,26 @@ __device__ __forceinline__ void cos_sinc(double x2, double& cs, double& sc) {
   }
 }
 
+// The same for |n|^2 <= 1/4 with the Taylor series cut at 7 (sinc) and 8 (cos) terms (< 1e-16
+// there); both propagators step at >= 3 steps per radian, where |n|^2 <~ 0.12.  Beyond 1/4 the
+// full series (and sincos beyond 1).
+#ifndef LZQ_SU2_SHORTSC
+#define LZQ_SU2_SHORTSC 1
+#endif
+__device__ __forceinline__ void cos_sinc_short(double x2, double& cs, double& sc) {
+  if (LZQ_SU2_SHORTSC && x2 <= 0.25) {
+    double ps = kSincC[6], pc = kCosC[7];
+#pragma unroll
+    for (int k = 5; k >= 0; --k) ps = fma3s(ps, x2, kSincC[k]);
+#pragma unroll
+    for (int k = 6; k >= 0; --k) pc = fma3s(pc, x2, kCosC[k]);
+    sc = ps;
+    cs = pc;
+  } else {
+    cos_sinc(x2, cs, sc);
+  }
+}
+
 // psi <- exp(-i n.sigma) psi, with cs = cos|n| and (sx, sy, sz) = sin|n|/|n| * n:
 // U11 = cs - i sz ; U12 = -sy - i sx ; U21 = sy - i sx ; U22 = cs + i sz
 __device__ __forceinline__ void su2_apply(double cs, double sx, double sy, double sz, Cplx& p0, Cplx& p1) {

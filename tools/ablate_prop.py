@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Time the LZ propagator (lz_propagate_kernel) of every library variant under
 <package>/_build/variants/ in ONE process, interleaved rounds, on the C5 crossing arrays
-(sweep.builtin_specs()["C5"]); checks that every variant returns the same P bit for bit."""
+(sweep.builtin_specs()["C5"]); reports whether every variant returns the same P bit for bit, and the largest |dP|."""
 import glob
 import importlib
 import json
@@ -28,11 +28,12 @@ def main():
     dev = next(iter(engs.values())).device
     m, dp, xi, v_w = spec.crossing_arrays(start, n, dev)
     args = (m, dp, xi, float(v_w[0]), spec.crossings.window_lz, spec.crossings.steps)
-    ref, same = None, True
+    ref, same, dmax = None, True, 0.0
     for e in engs.values():
         p = e.lz_propagate(*args)
         ref = p if ref is None else ref
         same = same and bool(torch.equal(p, ref))
+        dmax = max(dmax, float((p - ref).abs().max()))
     res = {k: [] for k in engs}
     for _ in range(rounds):
         for k, e in engs.items():
@@ -41,7 +42,7 @@ def main():
             e.lz_propagate(*args)
             torch.cuda.synchronize()
             res[k].append(time.perf_counter() - t0)
-    print(json.dumps({"points": n, "bit_identical": same, "seconds_min": {k: min(v) for k, v in res.items()}}, indent=1))
+    print(json.dumps({"points": n, "bit_identical": same, "max_abs_dP": dmax, "seconds_min": {k: min(v) for k, v in res.items()}}, indent=1))
 
 
 if __name__ == "__main__":

@@ -71,6 +71,9 @@ constexpr int kPropBlock = 256;
 #ifndef LZQ_PROP_MIN_WAVES
 #define LZQ_PROP_MIN_WAVES 2  // 217 VGPRs with the 3-step unroll, no spills (3 waves/SIMD: 168 VGPRs, spills; same time)
 #endif
+#ifndef LZQ_FOLLOW_MIN_WAVES
+#define LZQ_FOLLOW_MIN_WAVES 1  // lz_follow_kernel's occupancy floor (tools/ablate_prop.py)
+#endif
 constexpr double kDeltaAdiabatic = 16.0;              // e^{-2 pi 16} = 2e-44
 constexpr double kStepsPerRadian = 6.0;              // Magnus steps per radian of adiabatic phase in a core
 constexpr double kMaxCellSteps = 16777216.0;         // per-cell Magnus steps beyond this: P = NaN (bad input)
@@ -139,8 +142,8 @@ __device__ __forceinline__ double core_halfwidth(double m, double a, double v_w)
 // ~170-280 steps per delta <= 16 cell, none in the closed-form cells; round 2's 40-LZ-length
 // cores took 1000-1200 for delta <= 1 and up to ~6e4 for 1 < delta <= 16).  In index order
 // a wave waits on its slowest lane in every cell and the launch ends on a few long waves.  So,
-// for large batches, the points are first binned by their step count (the kernel's own cell
-// geometry, point_steps), the bins laid out longest-first (a counting sort: LDS histograms, one
+// for large batches, the points are first binned by their step count (the per-cell counts
+// lz_follow_kernel stores), the bins laid out longest-first (a counting sort: LDS histograms, one
 // scan, a scatter), and the kernel reads its point index from that order.  Every point is still
 // computed by one lane from its own inputs, so P is bit-identical to index order; only the
 // order within a bin depends on the scatter's atomics.
@@ -150,40 +153,14 @@ __device__ __forceinline__ double core_halfwidth(double m, double a, double v_w)
 #endif
 constexpr int64_t kSortMinPoints = 16384;  // below this the three extra launches do not pay
 
-// Magnus steps of one point: the cell loop of lz_propagate_kernel without the propagation.
-__device__ double point_steps(const double* mm, const double* dp, const double* xc, int32_t n_cross, double v_w,
-                              double K, int32_t S) {
-  double left = xc[0] - K * lz_length(mm[0], fabs(dp[0]), v_w);
-  double total = 0.0;
-  for (int c = 0; c < n_cross; ++c) {
-    const double ac = fabs(dp[c]), mc = mm[c], xcc = xc[c];
-    double right;
-    if (c + 1 < n_cross) {
-      const double an = fabs(dp[c + 1]);
-      right = (ac * xcc + an * xc[c + 1]) / (ac + an);
-    } else {
-      right = xcc + K * lz_length(mc, ac, v_w);
-    }
-    const double delta = mc * mc / (2.0 * v_w * ac);
-    if (delta > kDeltaAdiabatic) {
-      total += 4.0;  // closed-form cell: a few steps' worth of work
-    } else {
-      const double W = core_halfwidth(mc, ac, v_w);
-      const double cl = fmax(left, xcc - W), cr = fmin(right, xcc + W);
-      const double Phic = (wkb_G(ac * (cr - xcc), mc) - wkb_G(ac * (cl - xcc), mc)) / (ac * v_w);
-      total += fmax((double)S, ceil(Phic * kStepsPerRadian));
-    }
-    left = right;
-  }
-  return total;
-}
+constexpr int kFollowDoubles = 11;  // per (point, cell): two SU(2) matrices, the core's edges, its steps
 
-// bin (0 = costliest) of every point + the histogram of bins
-__global__ __launch_bounds__(kPropBlock) void lz_cost_kernel(const double* __restrict__ m_mix,
-                                                             const double* __restrict__ dprime,
-                                                             const double* __restrict__ xi,
-                                                             const double* __restrict__ vw, int64_t n, int32_t n_cross,
-                                                             double v_w0, double K, int32_t S,
+// bin (0 = costliest) of every point + the histogram of bins.  A point's cost is the sum of its
+// cells' Magnus step counts, which lz_follow_kernel (launched first) has stored per cell at + 10
+// (a closed-form cell, -1 there, counts as a few steps' work; NaN: the point is returned as NaN).
+__global__ __launch_bounds__(kPropBlock) void lz_cost_kernel(const double* __restrict__ vw, int64_t n,
+                                                             int32_t n_cross, double v_w0,
+                                                             const double* __restrict__ follow,
                                                              int32_t* __restrict__ bins, int32_t* __restrict__ hist) {
   __shared__ int32_t lh[kCostBins];
   for (int t = threadIdx.x; t < kCostBins; t += kPropBlock) lh[t] = 0;
@@ -191,7 +168,15 @@ __global__ __launch_bounds__(kPropBlock) void lz_cost_kernel(const double* __res
   const int64_t p = (int64_t)blockIdx.x * kPropBlock + threadIdx.x;
   if (p < n) {
     const double v_w = vw ? vw[p] : v_w0;
-    const double st = point_steps(m_mix + p * n_cross, dprime + p * n_cross, xi + p * n_cross, n_cross, v_w, K, S);
+    double st = __builtin_nan("");  // a bad wall speed: the follow kernel wrote nothing for this point
+    if (v_w > 0.0) {
+      st = 0.0;
+      const double* f = follow + p * n_cross * kFollowDoubles + 10;
+      for (int c = 0; c < n_cross; ++c) {
+        const double Sd = f[c * kFollowDoubles];
+        st += Sd < 0.0 ? 4.0 : Sd;
+      }
+    }
     // non-finite or absurd inputs (the kernel returns NaN at once) go with the cheapest
     const double key = st == st ? fmin(fmax(4.0 * log2(1.0 + st), 0.0), (double)(kCostBins - 1)) : 0.0;
     const int32_t b = (kCostBins - 1) - (int32_t)key;
@@ -234,7 +219,6 @@ __global__ __launch_bounds__(kPropBlock) void lz_scatter_kernel(const int32_t* _
   if (p < n) order[base[b] + r] = (int32_t)p;
 }
 
-constexpr int kFollowDoubles = 11;  // per (point, cell): two SU(2) matrices, the core's edges, its steps
 
 // Per-cell data of every (point, cell), one thread each: everything about a cell that does not
 // depend on the state.  Cell c's edges are computed with the propagate kernel's own expressions
@@ -243,7 +227,7 @@ constexpr int kFollowDoubles = 11;  // per (point, cell): two SU(2) matrices, th
 // a.im, b.re, b.im), the core's edges cl, cr at + 8, 9 and its Magnus step count at + 10 (NaN for
 // an absurd count).  A delta > 16 cell gets its closed-form adiabatic transfer matrix (dressed
 // bases, WKB + Stokes phase, header) at + 0..3 and -1 at + 10.
-__global__ __launch_bounds__(kPropBlock) void lz_follow_kernel(const double* __restrict__ m_mix,
+__global__ __launch_bounds__(kPropBlock, LZQ_FOLLOW_MIN_WAVES) void lz_follow_kernel(const double* __restrict__ m_mix,
                                                                const double* __restrict__ dprime,
                                                                const double* __restrict__ xi,
                                                                const double* __restrict__ vw, int64_t n,
@@ -473,8 +457,8 @@ int propagate_slice(const double* d_m_mix, const double* d_dprime, const double*
     int32_t *bins = iw, *ord = iw + n, *hist = iw + 2 * n, *offs = hist + lzq::kCostBins;
     e = hipMemsetAsync(hist, 0, lzq::kCostBins * sizeof(int32_t), st);
     if (e == hipSuccess) {
-      hipLaunchKernelGGL(lzq::lz_cost_kernel, dim3((unsigned)nb), dim3(lzq::kPropBlock), 0, st, d_m_mix, d_dprime,
-                         d_xi, d_v_w, n, n_cross, v_w, window_lz, steps_per_crossing, bins, hist);
+      hipLaunchKernelGGL(lzq::lz_cost_kernel, dim3((unsigned)nb), dim3(lzq::kPropBlock), 0, st, d_v_w, n, n_cross, v_w,
+                         follow, bins, hist);
       hipLaunchKernelGGL(lzq::lz_bin_scan_kernel, dim3(1), dim3(64), 0, st, hist, offs);
       hipLaunchKernelGGL(lzq::lz_scatter_kernel, dim3((unsigned)nb), dim3(lzq::kPropBlock), 0, st, bins, n, offs,
                          ord);

@@ -30,15 +30,34 @@ constexpr double kSAC = 3.2e5;     // |theta_10| <= kSAC mh / E^21 (fitted; cons
 constexpr int kSAFarLevels = 6;    // the outer end of a follow stretch, when that order is enough:
 constexpr double kSAFarC = 80.0;   //   |theta_6| <= kSAFarC mh / E^13 (fitted) <= kSATol / 10
 
+// 1/x for the frame and phase algebra (x: energies, their squares and the like, normal doubles far
+// from the range limits).  On the device v_rcp_f64 + two Newton steps (<= 1 ulp from the
+// quotient, ~4 VALU where the IEEE division takes ~10; the follow kernel divides ~130 times per
+// cell); the host build (tests/test_superadiabatic_host.py) divides.
+#ifndef LZQ_SA_FASTDIV
+#define LZQ_SA_FASTDIV 1
+#endif
+__host__ __device__ __forceinline__ double sa_rcp(double x) {
+#if defined(__HIP_DEVICE_COMPILE__) && LZQ_SA_FASTDIV
+  double r = __builtin_amdgcn_rcp(x);
+  double e = __builtin_fma(-x, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-x, r, 1.0);
+  return __builtin_fma(r, e, r);
+#else
+  return 1.0 / x;
+#endif
+}
+
 // cos theta, sin theta from cos 2theta = c2, sin 2theta = s2 >= 0 (theta in [0, pi/2]) or any
 // s2 with c2 > 0, without cancellation
 __host__ __device__ __forceinline__ void half_angle(double c2, double s2, bool pos, double& c, double& s) {
   if (pos) {
     c = sqrt(0.5 * (1.0 + c2));
-    s = s2 / (2.0 * c);
+    s = s2 * (0.5 * sa_rcp(c));
   } else {
     s = sqrt(0.5 * (1.0 - c2));
-    c = s2 / (2.0 * s);
+    c = s2 * (0.5 * sa_rcp(s));
   }
 }
 
@@ -81,8 +100,8 @@ __host__ __device__ __forceinline__ void sa_chain(double (&e)[M], double (&g)[M]
       q[l] = acc;
     }
     const double r0 = sqrt(q[0]);
+    const double ir = sa_rcp(r0);
     if constexpr (kRot) {
-      const double ir = 1.0 / r0;
       double c, s;
       half_angle(e[0] * ir, g[0] * ir, e[0] >= 0.0, c, s);
       su2_right_mul<lev % 2 == 0>(u, c, s);
@@ -93,7 +112,7 @@ __host__ __device__ __forceinline__ void sa_chain(double (&e)[M], double (&g)[M]
     }
     if constexpr (n > 1) {
       // theta' = (e g' - g e') / (2 q): w = num / q, g_next = -+ w / 2
-      const double iq = 1.0 / q[0];
+      const double iq = sa_rcp(q[0]);
       double w[n - 1];
 #pragma unroll
       for (int l = 0; l < n - 1; ++l) {
@@ -110,7 +129,7 @@ __host__ __device__ __forceinline__ void sa_chain(double (&e)[M], double (&g)[M]
         w[l] = acc * iq;
       }
       // sqrt(q) in place: r_l = (q_l - sum_{i=1}^{l-1} r_i r_{l-i}) / (2 r_0)
-      const double h0 = 0.5 / r0;
+      const double h0 = 0.5 * ir;
       q[0] = r0;
 #pragma unroll
       for (int l = 1; l < n - 1; ++l) {
@@ -140,7 +159,7 @@ __host__ __device__ __forceinline__ void sa_levels_linear(double Dh, double sg, 
   // q = (Dh + sg h)^2 + mh^2 = [E^2, 2 sg Dh, 1]
   const double q0 = __builtin_fma(Dh, Dh, mh * mh), q1 = 2.0 * sg * Dh;
   const double E = sqrt(q0);
-  const double iE = 1.0 / E;
+  const double iE = sa_rcp(E);
   if constexpr (kRot) {
     double c, s;
     half_angle(Dh * iE, mh * iE, Dh >= 0.0, c, s);
@@ -167,7 +186,7 @@ __host__ __device__ __forceinline__ void sa_levels_linear(double Dh, double sg, 
       if (l % 2 == 0) acc = __builtin_fma(e[l / 2], e[l / 2], acc);
       e[l] = ((l == 2 ? 1.0 : 0.0) - acc) * h0;
     }
-    const double iq = 1.0 / q0;
+    const double iq = sa_rcp(q0);
     double w[M];
     w[0] = -mh * sg * iq;
 #pragma unroll
@@ -267,16 +286,18 @@ __host__ __device__ __forceinline__ double sa_phase(double ta, double tb, double
 #pragma nounroll
   for (int k = 0; k < 4; ++k) {
     const double u = __builtin_fma(half, gx[k], mid);
+    const double iu = sa_rcp(u);
     SU2 unused;
     double ev[4], gv[4];
-    sa_levels_linear<4, false, true>(1.0 / u, 1.0, mh, unused, ev, gv);
+    sa_levels_linear<4, false, true>(iu, 1.0, mh, unused, ev, gv);
     const double E = ev[0];
-    const double d1 = gv[1] * gv[1] / (E + ev[1]);
-    const double d2 = gv[2] * gv[2] / (ev[1] + ev[2]);
-    const double d3 = gv[3] * gv[3] / (ev[2] + ev[3]);
+    const double i01 = sa_rcp(E + ev[1]);
+    const double d1 = gv[1] * gv[1] * i01;
+    const double d2 = gv[2] * gv[2] * sa_rcp(ev[1] + ev[2]);
+    const double d3 = gv[3] * gv[3] * sa_rcp(ev[2] + ev[3]);
     const double E5 = E * E * E * E * E;
-    const double f = d3 + d2 - mh * mh * d1 / (8.0 * E5 * (E + ev[1]));
-    acc = __builtin_fma(gw[k], f / (u * u), acc);
+    const double f = d3 + d2 - mh * mh * d1 * (0.125 * sa_rcp(E5) * i01);
+    acc = __builtin_fma(gw[k], f * (iu * iu), acc);
   }
   return base + lead + half * acc;
 }

@@ -552,6 +552,9 @@ __device__ __forceinline__ double fma_neg_s(double k, double a, double p) {
 #ifndef LZQ_ODE_NEWTON2
 #define LZQ_ODE_NEWTON2 1  // the peeled pair of Newton iterations always both applied (no iterate selects)
 #endif
+#ifndef LZQ_ODE_SIMPLIFIED
+#define LZQ_ODE_SIMPLIFIED 1  // the peeled pair's second iteration reuses the first one's adjugate and 1/det
+#endif
 #ifndef LZQ_ODE_LINFAST
 #define LZQ_ODE_LINFAST 1  // one fma per regular step on linear cooperative waves (sigma_v = 0, no depletion)
 #endif
@@ -595,7 +598,11 @@ __device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st
     hl2[j] = 2.0 * hl[j];
     hS[j] = hA.h * st[j].S;
   }
-  auto newton = [&](double (&Z)[3]) {
+  // the iteration matrix's adjugate and 1/det, kept for a simplified iteration (LZQ_ODE_SIMPLIFIED)
+  struct NewtonJ {
+    double b[3][3], id;
+  };
+  auto newton_j = [&](double (&Z)[3], NewtonJ& J, const bool reuse, bool& near) {
 #define FMA __builtin_fma
     double d[3], r[3], k[3];
 #pragma unroll
@@ -607,20 +614,21 @@ __device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st
 #pragma unroll
     for (int i = 0; i < 3; ++i)
       r[i] = FMA(-kRadauAinv[i][2], d[2], FMA(-kRadauAinv[i][1], d[1], FMA(-kRadauAinv[i][0], d[0], r[i])));
-    // adjugate of [[k0, a01, a02], [a10, k1, a12], [a20, a21, k2]] (a_ij = A^-1_ij, products constant)
-    const double b00 = FMA(k[1], k[2], -kRadauAinvP[0]), b01 = fma_neg_s(k[2], kRadauAinv[0][1], kRadauAinvP[1]);
-    const double b02 = fma_neg_s(k[1], kRadauAinv[0][2], kRadauAinvP[2]), b10 = fma_neg_s(k[2], kRadauAinv[1][0], kRadauAinvP[3]);
-    const double b11 = FMA(k[0], k[2], -kRadauAinvP[4]), b12 = fma_neg_s(k[0], kRadauAinv[1][2], kRadauAinvP[5]);
-    const double b20 = fma_neg_s(k[1], kRadauAinv[2][0], kRadauAinvP[6]), b21 = fma_neg_s(k[0], kRadauAinv[2][1], kRadauAinvP[7]);
-    const double b22 = FMA(k[0], k[1], -kRadauAinvP[8]);
-    // 1/det only scales the correction: a reciprocal within 1 ulp leaves the fixed point (the
-    // stage equations) as it is and changes the iterates by rounding
-    const double den = FMA(k[0], b00, FMA(kRadauAinv[0][1], b10, kRadauAinv[0][2] * b20));
-    const double id = LZQ_ODE_NEWTON_RCP ? rcp_pos(den) : 1.0 / den;
+    if (!reuse) {
+      // adjugate of [[k0, a01, a02], [a10, k1, a12], [a20, a21, k2]] (a_ij = A^-1_ij, products constant)
+      J.b[0][0] = FMA(k[1], k[2], -kRadauAinvP[0]), J.b[0][1] = fma_neg_s(k[2], kRadauAinv[0][1], kRadauAinvP[1]);
+      J.b[0][2] = fma_neg_s(k[1], kRadauAinv[0][2], kRadauAinvP[2]), J.b[1][0] = fma_neg_s(k[2], kRadauAinv[1][0], kRadauAinvP[3]);
+      J.b[1][1] = FMA(k[0], k[2], -kRadauAinvP[4]), J.b[1][2] = fma_neg_s(k[0], kRadauAinv[1][2], kRadauAinvP[5]);
+      J.b[2][0] = fma_neg_s(k[1], kRadauAinv[2][0], kRadauAinvP[6]), J.b[2][1] = fma_neg_s(k[0], kRadauAinv[2][1], kRadauAinvP[7]);
+      J.b[2][2] = FMA(k[0], k[1], -kRadauAinvP[8]);
+      // 1/det only scales the correction: a reciprocal within 1 ulp leaves the fixed point (the
+      // stage equations) as it is and changes the iterates by rounding
+      const double den = FMA(k[0], J.b[0][0], FMA(kRadauAinv[0][1], J.b[1][0], kRadauAinv[0][2] * J.b[2][0]));
+      J.id = LZQ_ODE_NEWTON_RCP ? rcp_pos(den) : 1.0 / den;
+    }
     double g[3];
-    g[0] = FMA(b00, r[0], FMA(b01, r[1], b02 * r[2])) * id;
-    g[1] = FMA(b10, r[0], FMA(b11, r[1], b12 * r[2])) * id;
-    g[2] = FMA(b20, r[0], FMA(b21, r[1], b22 * r[2])) * id;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) g[i] = FMA(J.b[i][0], r[0], FMA(J.b[i][1], r[1], J.b[i][2] * r[2])) * J.id;
 #undef FMA
     // running maxima from +0 of |.| (never NaN on the left): fmax is pymax here, one v_max_f64
     double dmax = 0.0, zmax = 0.0;
@@ -630,8 +638,12 @@ __device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st
       dmax = fmax(dmax, fabs(g[i]));
       zmax = fmax(zmax, fabs(Z[i]));
     }
+    near = !(dmax > 1e-3 * zmax);
     return !(dmax > 1e-15 * zmax);
   };
+  NewtonJ J;
+  bool near = false;
+  auto newton = [&](double (&Z)[3]) { return newton_j(Z, J, false, near); };
 #else
   auto newton = [&](double (&Z)[3]) {
     double M[3][3], g[3];
@@ -695,7 +707,21 @@ __device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st
       // both iterations always apply: a step that converged at the first takes the second's
       // (below 1e-15 relative) correction too, so no selects between the two iterates are needed
       const bool c1 = newton(Z);
+#if LZQ_ODE_SIMPLIFIED && LZQ_ODE_TNEWTON && LZQ_ODE_FASTMATH
+      // Once the first correction is below 1e-3 of the stages (the predicted start, almost every
+      // step), the second iteration reuses the first one's matrix (simplified Newton): its
+      // correction is then the first one's residual error to first order either way, so the
+      // acceptance test reads the same quantity, and the accepted iterate differs by
+      // O(1e-3 x that error), far below rounding when the test passes.  A large first correction
+      // (a start far from the solution) keeps the full iteration: a stale matrix there can carry
+      // the iterate into the other, unstable root's basin.  Per lane, so a point's iterates do not
+      // depend on its wavefront.
+      bool c2;
+      if (near) c2 = newton_j(Z, J, true, near);
+      else c2 = newton(Z);
+#else
       const bool c2 = newton(Z);
+#endif
       if (c1 || c2) {
         accept(Z);
         return true;

@@ -69,6 +69,10 @@ case "$cmd" in
       python3 tools/ode_pmc_run.py > "$OUT/pmc.jsonl" 2> "$OUT/pmc.err" || { tail -5 "$OUT/pmc.err"; exit 1; }
     timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
       python3 tools/ode_pmc_run.py > "$OUT/trace.jsonl" 2> "$OUT/trace.err" || { tail -5 "$OUT/trace.err"; exit 2; }
+    # the non-FP64 rest of the mix (integer, conversions, scalar, LDS), its own pass
+    timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 \
+      SQ_INSTS_VALU_CVT SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VALU_TRANS_F64 --output-format csv -d "$OUT/mix" -o run -- \
+      python3 tools/ode_pmc_run.py > "$OUT/mix.jsonl" 2> "$OUT/mix.err" || { tail -5 "$OUT/mix.err"; exit 3; }
     cat "$OUT/trace.jsonl"
     ;;
   prop-pmc)  # the bounce-profile propagation (tools/bench_profile.py): instruction mix per kernel + kernel trace;

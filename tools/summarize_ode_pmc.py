@@ -23,19 +23,26 @@ def main_cases(src: str, tag: str, fname: str = "ode_pmc.json") -> None:
     # ode_integrate_kernel<false> (one dispatch per case), or since the linear-wave variant
     # <false, false> + <false, true> (two per case, each stepping its own wavefronts: summed)
     per = 1
-    rows = list(csv.DictReader(open(os.path.join(src, "pmc", "run_counter_collection.csv"))))
-    disp = defaultdict(dict)
-    for r in rows:
-        if "ode_integrate_kernel<false" in r["Kernel_Name"]:
-            per = 2 if "ode_integrate_kernel<false, " in r["Kernel_Name"] else per
-            d = disp[int(r["Dispatch_Id"])]
-            d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-    big = [disp[k] for k in sorted(disp) if disp[k].get("SQ_WAVES", 0) >= N // 64]
-    big_p = []
-    for j in range(0, len(big), per):
-        c = {k: sum(d.get(k, 0.0) for d in big[j:j + per]) for k in big[j]}
-        c["SQ_WAVES"] = big[j]["SQ_WAVES"]  # every variant launches every wavefront
-        big_p.append(c)
+    def passes(sub):
+        nonlocal per
+        rows = list(csv.DictReader(open(os.path.join(src, sub, "run_counter_collection.csv"))))
+        disp = defaultdict(dict)
+        for r in rows:
+            if "ode_integrate_kernel<false" in r["Kernel_Name"]:
+                per = 2 if "ode_integrate_kernel<false, " in r["Kernel_Name"] else per
+                d = disp[int(r["Dispatch_Id"])]
+                d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        big = [disp[k] for k in sorted(disp) if disp[k].get("SQ_WAVES", 0) >= N // 64]
+        out = []
+        for j in range(0, len(big), per):
+            c = {k: sum(d.get(k, 0.0) for d in big[j:j + per]) for k in big[j]}
+            c["SQ_WAVES"] = big[j]["SQ_WAVES"]  # every variant launches every wavefront
+            out.append(c)
+        return out
+
+    big_p = passes("pmc")
+    # the optional third pass (integer / conversion / scalar / LDS instructions)
+    mix = passes("mix") if os.path.exists(os.path.join(src, "mix", "run_counter_collection.csv")) else None
     tr = [r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv")))
           if "ode_integrate_kernel<false" in r["Kernel_Name"] and int(r["Grid_Size_X"]) >= N]
     d1 = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9 for r in tr]
@@ -67,6 +74,13 @@ def main_cases(src: str, tag: str, fname: str = "ode_pmc.json") -> None:
             "executed_fp64_tflops": flop / t / 1e12, "frac_of_fp64_peak": flop / t / 1e12 / 78.6,
             # 1024 SIMDs x clock: FP64 instructions take 4 issue cycles of a SIMD (16 lanes/cycle)
             "fp64_pipe_busy_frac": f64 * 4.0 / (t * 1024 * 2.4e9)}
+        if mix:
+            m = mix[[n for n, _o, _s in CASES].index(name)]
+            wm = m["SQ_WAVES"] * steps
+            out["configs"][name]["mix_per_wave_step"] = {
+                k.replace("SQ_INSTS_", "").lower(): m[k] / wm for k in
+                ("SQ_INSTS_VALU", "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64", "SQ_INSTS_VALU_CVT",
+                 "SQ_INSTS_VALU_TRANS_F64", "SQ_INSTS_SALU", "SQ_INSTS_LDS") if k in m}
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
     with open(os.path.join(dst, fname), "w") as f:

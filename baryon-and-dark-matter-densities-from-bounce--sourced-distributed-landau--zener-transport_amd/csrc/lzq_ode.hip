@@ -716,9 +716,8 @@ __device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st
       // (a start far from the solution) keeps the full iteration: a stale matrix there can carry
       // the iterate into the other, unstable root's basin.  Per lane, so a point's iterates do not
       // depend on its wavefront.
-      bool c2;
-      if (near) c2 = newton_j(Z, J, true, near);
-      else c2 = newton(Z);
+      const bool reuse = near;
+      const bool c2 = newton_j(Z, J, reuse, near);
 #else
       const bool c2 = newton(Z);
 #endif

@@ -555,6 +555,9 @@ __device__ __forceinline__ double fma_neg_s(double k, double a, double p) {
 #ifndef LZQ_ODE_SIMPLIFIED
 #define LZQ_ODE_SIMPLIFIED 1  // the peeled pair's second iteration reuses the first one's adjugate and 1/det
 #endif
+#ifndef LZQ_ODE_KD
+#define LZQ_ODE_KD 1  // the step index as a carried exact double (no 64-bit integer conversion per step)
+#endif
 #ifndef LZQ_ODE_LINFAST
 #define LZQ_ODE_LINFAST 1  // one fma per regular step on linear cooperative waves (sigma_v = 0, no depletion)
 #endif
@@ -1073,6 +1076,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
       int64_t k = kb;
+      double kd = (double)kb;  // (double)k, carried: an exact double counter instead of a 64-bit conversion per step
       while (k < kend && !done) {
         if (lin_fast && !prev_split) {
           // the block's regular steps up to its next split step in one tight loop
@@ -1130,10 +1134,11 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
               for (; jj < nf; ++jj) YB = __builtin_fma(rr[jj].c, YB, o.Pf * rr[jj].d);
             }
             k = kg;
+            kd = (double)kg;
           }
           if (k >= kend) break;
         }
-        const double xk = x0 + (double)k * h;
+        const double xk = x0 + (LZQ_ODE_KD ? kd : (double)k) * h;
         const bool split = xk < xb && xb <= xk + h;  // the last stage (x = xk + h) would see the other branch
         const double xa = split ? xb_below : xk + h;
         double YB_prev = YB;
@@ -1212,6 +1217,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
           done = true;
         }
         ++k;
+        kd += 1.0;
       }
       if (coop) __builtin_amdgcn_wave_barrier();  // every lane is done with this block's table
     }

@@ -48,7 +48,8 @@ def main():
             t = e.ode(pts[:256], ods[:256], method=method)[0].cpu().numpy()
             if ref is None:
                 ref = t
-            assert np.max(np.abs(t - ref) / np.maximum(np.abs(ref), 1e-300)) < 1e-11, k
+            if not os.environ.get("ABLATE_NOCHECK"):  # diagnostic variants that change results
+                assert np.max(np.abs(t - ref) / np.maximum(np.abs(ref), 1e-300)) < 1e-11, k
         res = {k: [] for k in engs}
         for _ in range(rounds):
             for k, e in engs.items():

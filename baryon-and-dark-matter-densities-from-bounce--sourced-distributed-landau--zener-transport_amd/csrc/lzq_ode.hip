@@ -558,6 +558,9 @@ __device__ __forceinline__ double fma_neg_s(double k, double a, double p) {
 #ifndef LZQ_ODE_KD
 #define LZQ_ODE_KD 1  // the step index as a carried exact double (no 64-bit integer conversion per step)
 #endif
+#ifndef LZQ_ODE_NOSPLITVAR
+#define LZQ_ODE_NOSPLITVAR 1  // waves with no split step in the launch run an integrator variant without the split paths
+#endif
 #ifndef LZQ_ODE_LINFAST
 #define LZQ_ODE_LINFAST 1  // one fma per regular step on linear cooperative waves (sigma_v = 0, no depletion)
 #endif
@@ -872,7 +875,7 @@ constexpr int32_t kOdeInProgress = 64;
 // kLin: the variant for linear cooperative waves (see lin_wave below); every launch runs both
 // variants, each stepping only its own wavefronts (the other variant's return at once), so the
 // linear waves' tight loop does not share a register allocation with the Riccati Newton path.
-template <bool kChiOnly, bool kLin = false>
+template <bool kChiOnly, bool kLin = false, bool kNoSplit = false>
 __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_kernel(const lzq_point* __restrict__ pts,
                                                                   const lzq_ode_params* __restrict__ ode, int64_t n,
                                                                   const int32_t* __restrict__ tidx,
@@ -931,7 +934,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
     }
   }
   bool finished = true;  // this launch ends the point (continuation: else its state is saved)
-  if (kLin && st != LZQ_ODE_OK) return;  // the general variant reports it (its wave is not linear)
+  if ((kLin || kNoSplit) && st != LZQ_ODE_OK) return;  // the general variant reports it (its wave is not linear)
   if (st == LZQ_ODE_OK) {
     const int64_t N = (int64_t)steps;
     const int64_t k_begin = cont ? k_lo : 0;
@@ -1029,7 +1032,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
       const double xq = x0 + (double)(k_begin - 1) * h;
       prev_split = xq < xb && xb <= xq + h;
     }
-    if (lin_fast && xb < INFINITY) {  // branch_x: +inf when no step splits
+    if ((lin_fast || LZQ_ODE_NOSPLITVAR) && xb < INFINITY) {  // branch_x: +inf when no step splits
       const double kf = floor((xb - x0) / h);
       const double margin = 2.0 + floor(8.0 * __DBL_EPSILON__ * (fabs(x0) + fabs(x1)) / h);
       if (!(margin <= 16.0)) {
@@ -1046,6 +1049,15 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
           }
         }
       }
+    }
+    // Split-free waves (LZQ_ODE_NOSPLITVAR): when no lane of the wave has a split step in this
+    // launch's range (the window does not reach T = m/3, or the split lies in another
+    // continuation launch), the <kNoSplit> variant steps the wave: the same operations with the
+    // split paths compiled out, whose mere presence costs ~11% of a stiff / Riccati step
+    // (register pressure).  Both variants evaluate the same wave-uniform predicate.
+    if (!kLin && LZQ_ODE_NOSPLITVAR) {
+      const bool lane_ns = k_split == INT64_MAX || (k_split >= 0 && (k_split + 1 < k_begin || k_split >= k_stop));
+      if (__all(lane_ns) != kNoSplit) return;
     }
     const int64_t block = coop ? G : N;
     for (int64_t kb = k_begin; kb < k_stop; kb += block) {
@@ -1139,7 +1151,8 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
           if (k >= kend) break;
         }
         const double xk = x0 + (LZQ_ODE_KD ? kd : (double)k) * h;
-        const bool split = xk < xb && xb <= xk + h;  // the last stage (x = xk + h) would see the other branch
+        // (kNoSplit: no step of this launch splits on any lane of the wave -- the split paths compile away)
+        const bool split = !kNoSplit && xk < xb && xb <= xk + h;  // the last stage (x = xk + h) would see the other branch
         const double xa = split ? xb_below : xk + h;
         double YB_prev = YB;
         bool ok = true;
@@ -1472,12 +1485,20 @@ int launch_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int
              (long long)max_steps, lzq::g_ode_launch_log2);
     return lzq_set_error(LZQ_EINVAL, buf);
   }
-  // both variants (ode_integrate_kernel's kLin) per launch; none for kChiOnly (no linear waves)
+  // every variant (ode_integrate_kernel's kLin, kNoSplit) per launch, each stepping its own
+  // wavefronts; no kLin for kChiOnly (no linear waves)
   auto launch = [&](int64_t k_lo, int64_t k_cnt, lzq::OdeState* st) {
     hipLaunchKernelGGL(lzq::ode_integrate_kernel<kChiOnly>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, s,
                        d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, lzq::g_ode_coop, k_lo, k_cnt,
                        st);
     int rc = hip_check(hipGetLastError(), fn);
+    if constexpr (LZQ_ODE_NOSPLITVAR) {
+      if (rc != LZQ_OK) return rc;
+      hipLaunchKernelGGL((lzq::ode_integrate_kernel<kChiOnly, false, true>), dim3((unsigned)ode_blocks(n)),
+                         dim3(lzq::kOdeBlock), 0, s, d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status,
+                         lzq::g_ode_coop, k_lo, k_cnt, st);
+      rc = hip_check(hipGetLastError(), fn);
+    }
     if constexpr (LZQ_ODE_LINFAST && LZQ_ODE_YBREC && !kChiOnly) {
       if (rc != LZQ_OK) return rc;
       hipLaunchKernelGGL((lzq::ode_integrate_kernel<kChiOnly, true>), dim3((unsigned)ode_blocks(n)),

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """The workload of the ODE PMC passes (`tools/gpu.sh ode-pmc`): three 262,144-point batches of
-the Radau fallback (fpy:385-417), each ONE integrator launch (ode_integrate_kernel<false, kLin>, both variants) after a
+the Radau fallback (fpy:385-417), each ONE integrator launch (ode_integrate_kernel<false, kLin, kNoSplit>, every variant) after a
 64-point warm-up, in this order:
 
   narrow_wash      equal-mass config, Gamma_wash/H = 1, T in [0.6, 1.6] T_p (20000 steps/point);

@@ -21,15 +21,19 @@ def main_cases(src: str, tag: str, fname: str = "ode_pmc.json") -> None:
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from ode_pmc_run import CASES, N
     # ode_integrate_kernel<false> (one dispatch per case), or since the linear-wave variant
-    # <false, false> + <false, true> (two per case, each stepping its own wavefronts: summed)
+    # <false, false> + <false, true>, and since the split-free variant <false, false, false> +
+    # <false, false, true> + <false, true, false>: one dispatch per variant and case, each stepping
+    # its own wavefronts (summed)
     per = 1
     def passes(sub):
         nonlocal per
         rows = list(csv.DictReader(open(os.path.join(src, sub, "run_counter_collection.csv"))))
         disp = defaultdict(dict)
+        names = set()
         for r in rows:
             if "ode_integrate_kernel<false" in r["Kernel_Name"]:
-                per = 2 if "ode_integrate_kernel<false, " in r["Kernel_Name"] else per
+                names.add(r["Kernel_Name"])
+                per = max(per, len(names))
                 d = disp[int(r["Dispatch_Id"])]
                 d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
         big = [disp[k] for k in sorted(disp) if disp[k].get("SQ_WAVES", 0) >= N // 64]
@@ -55,7 +59,8 @@ def main_cases(src: str, tag: str, fname: str = "ode_pmc.json") -> None:
                 j = json.loads(ln)
                 lines.setdefault(j["config"], j)
     out = {"source": "tools/gpu.sh ode-pmc (tools/ode_pmc_run.py) + tools/summarize_ode_pmc.py " + tag,
-           "kernel": "ode_integrate_kernel<false>" if per == 1 else "ode_integrate_kernel<false, kLin> (both variants)",
+           "kernel": "ode_integrate_kernel<false>" if per == 1 else
+                     f"ode_integrate_kernel<false, ...> ({per} variants per launch, summed)",
            "peak_tflops": 78.6,
            "note": "executed FP64 FLOP = 64 x (2 FMA + MUL + ADD) instructions; cooperative waves evaluate a "
                    "step's stage ingredients once per wave (or per 32/16/8-lane segment), so executed FLOP "

@@ -66,13 +66,24 @@ __device__ __forceinline__ void cos_sinc(double x2, double& cs, double& sc) {
 }
 
 // The same for |n|^2 <= 1/4 with the Taylor series cut at 7 (sinc) and 8 (cos) terms (< 1e-16
-// there); both propagators step at >= 3 steps per radian, where |n|^2 <~ 0.12.  Beyond 1/4 the
-// full series (and sincos beyond 1).
+// there), and at 7 + 7 for |n|^2 <= 1/8 (< 6e-18); both propagators step at >= 3 steps per
+// radian, where |n|^2 <~ 0.12.  Beyond 1/4 the full series (and sincos beyond 1).
 #ifndef LZQ_SU2_SHORTSC
 #define LZQ_SU2_SHORTSC 1
 #endif
+#ifndef LZQ_SU2_SHORT8
+#define LZQ_SU2_SHORT8 1  // |n|^2 <= 1/8 (the usual step): 7 + 7 terms (< 6e-18)
+#endif
 __device__ __forceinline__ void cos_sinc_short(double x2, double& cs, double& sc) {
-  if (LZQ_SU2_SHORTSC && x2 <= 0.25) {
+  if (LZQ_SU2_SHORT8 && x2 <= 0.125) {
+    double ps = kSincC[6], pc = kCosC[6];
+#pragma unroll
+    for (int k = 5; k >= 0; --k) ps = fma3s(ps, x2, kSincC[k]);
+#pragma unroll
+    for (int k = 5; k >= 0; --k) pc = fma3s(pc, x2, kCosC[k]);
+    sc = ps;
+    cs = pc;
+  } else if (LZQ_SU2_SHORTSC && x2 <= 0.25) {
     double ps = kSincC[6], pc = kCosC[7];
 #pragma unroll
     for (int k = 5; k >= 0; --k) ps = fma3s(ps, x2, kSincC[k]);

@@ -36,6 +36,17 @@ class LzqAxis(ctypes.Structure):
     _fields_ = [("field", ctypes.c_int32), ("n", ctypes.c_int32), ("values", ctypes.c_void_p)]
 
 
+AOV_FIELDS = ("I_p", "beta_over_H", "T_p_GeV", "v_w", "g_star")
+
+
+class LzqAovParams(ctypes.Structure):  # struct lzq_aov_params: AoverVKernel's own fields (fpy:141-151)
+    _fields_ = [(n, ctypes.c_double) for n in AOV_FIELDS]
+
+
+AOV_DTYPE = np.dtype([(n, "<f8") for n in AOV_FIELDS])
+assert ctypes.sizeof(LzqAovParams) == 40 == AOV_DTYPE.itemsize
+
+
 class LzqOdeParams(ctypes.Structure):
     _fields_ = [("sigma_v_chi_GeV_m2", ctypes.c_double), ("Gamma_wash_over_H", ctypes.c_double),
                 ("deplete_DM_from_source", ctypes.c_int32), ("reserved", ctypes.c_int32)]
@@ -102,7 +113,7 @@ def library_id(path: str | None = None) -> str | None:
     return h.hexdigest()[:16]
 EXP_POLY11, EXP_TABLE = 0, 1  # enum lzq_exp_variant
 LZQ_MAX_AXES = 8
-ABI_VERSION = 2  # LZQ_ABI_VERSION (tests/test_capi.py checks it against the library)
+ABI_VERSION = 3  # LZQ_ABI_VERSION (tests/test_capi.py checks it against the library)
 
 # Symbols declared in include/lzq.h (checked by tests/test_capi.py against the header).
 EXPORTS = ("lzq_abi_version", "lzq_last_error", "lzq_init", "lzq_zgrid_init", "lzq_ztables", "lzq_tune", "lzq_aov_batch",
@@ -157,9 +168,9 @@ def load(path: str | None = None):
     L.lzq_zgrid_init.argtypes = [ctypes.c_int, i32, d]
     L.lzq_ztables.argtypes = [i32, d, P(d), P(d), P(d)]
     L.lzq_tune.argtypes = [i32, i32]
-    L.lzq_aov_batch.argtypes = [P(LzqPoint), vp, i64, i32, d, vp, vp]
+    L.lzq_aov_batch.argtypes = [P(LzqPoint), P(LzqAovParams), vp, i64, i32, d, vp, vp]
     L.lzq_jchi_batch.argtypes = [P(LzqPoint), vp, i64, vp, vp]
-    L.lzq_yields_batch.argtypes = [vp, i64, i32, i32, d, vp, vp, vp, vp, vp]
+    L.lzq_yields_batch.argtypes = [vp, i64, i32, i32, d, vp, vp, vp, vp, vp, vp]
     L.lzq_sweep_grid.argtypes = [P(LzqPoint), P(LzqAxis), i32, i64, i64, i32, i32, d, vp, vp, vp]
     L.lzq_sweep_grid_reuse_workspace.argtypes = [P(LzqAxis), i32, i32]
     L.lzq_sweep_grid_reuse.argtypes = [P(LzqPoint), P(LzqAxis), i32, i64, i64, i32, i32, d, vp, vp, i64, vp, vp]
@@ -170,11 +181,11 @@ def load(path: str | None = None):
     L.lzq_p_closed_form.argtypes = [vp, i64, vp, vp]
     L.lzq_lz_propagate.argtypes = [vp, vp, vp, i64, i32, d, d, i32, vp, vp]
     L.lzq_lz_propagate_v.argtypes = [vp, vp, vp, vp, i64, i32, d, i32, vp, vp]
-    L.lzq_ode_tables.argtypes = [vp, i64, vp, vp, i32, i32, d, vp, i64, vp, vp]
+    L.lzq_ode_tables.argtypes = [vp, i64, vp, vp, i32, i32, d, vp, vp, i64, vp, vp]
     L.lzq_ode_integrate.argtypes = [vp, vp, i64, vp, i64, i64, vp, vp, vp]
     L.lzq_ode_integrate_shared.argtypes = [vp, vp, i64, vp, i64, vp, i64, i64, vp, vp, vp]
     L.lzq_ode_quadrature.argtypes = [vp, vp, i64, vp, i64, vp, i64, i64, vp, vp, vp]
-    L.lzq_ode_batch.argtypes = [vp, vp, i64, i32, d, vp, i64, i64, vp, vp, vp]
+    L.lzq_ode_batch.argtypes = [vp, vp, i64, i32, d, vp, vp, i64, i64, vp, vp, vp]
     L.lzq_ode_aov_T.argtypes = [P(LzqPoint), d, d, i32, vp, vp, i64, vp, vp]
     L.lzq_ode_rhs.argtypes = [P(LzqPoint), P(LzqOdeParams), d, d, i32, vp, vp, vp, i64, vp, vp]
     L.lzq_profile_splines.argtypes = [vp, vp, vp, i32, i32, vp, vp, vp]

@@ -34,8 +34,6 @@ class AoverVKernel:
         self.g_star = g_star
         self.H_p = H_std(T_p, g_star)                   # fpy:150-151
         self.beta = self.beta_over_H * self.H_p
-        self._cfg = {**Config().__dict__, "I_p": I_p, "beta_over_H": beta_over_H, "T_p_GeV": T_p,
-                     "v_w": v_w, "g_star": g_star, "P_chi_to_B": 0.0}
         self._tables = None
 
     @property
@@ -57,12 +55,18 @@ class AoverVKernel:
         return float(self.A_over_V_ys([y])[0])
 
     def A_over_V_ys(self, ys) -> np.ndarray:
-        """Batched fpy:158-165 (one GPU lane per y)."""
-        return default_engine().aov(self._cfg, ys, nz=self.nz, z_max=self.z_max).cpu().numpy()
+        """Batched fpy:158-165 (one GPU lane per y), with this kernel's own I_p, beta_over_H, T_p,
+        v_w and g_star (lzq_aov_batch's lzq_aov_params block)."""
+        return default_engine().aov(self, ys, nz=self.nz, z_max=self.z_max).cpu().numpy()
 
 
 class BoltzmannSystem:
-    """fpy:192-267 direct-quadrature path."""
+    """fpy:192-267 direct-quadrature path.
+
+    As in the reference, self.aov is an independent public object (fpy:197): the integrand's
+    y-grid, T(y), H, s, J and window come from self.cfg, A/V from self.aov's own parameters and z
+    grid (fpy:211, 228, 261).  Replacing bs.aov with another AoverVKernel changes A/V only; every
+    operator below passes its parameters through the C ABI (lzq_aov_params)."""
 
     def __init__(self, cfg: Config, P_chi_to_B: float):
         self.cfg = cfg
@@ -97,7 +101,7 @@ class BoltzmannSystem:
         """fpy:231-267 on the GPU (one wavefront)."""
         rec = to_point(self.cfg, P=self.P)
         out = default_engine().yields(rec, n_y=int(n_y), T_lo=[float(T_lo)], T_hi=[float(T_hi)], P=[self.P],
-                                      nz=self.aov.nz, z_max=self.aov.z_max)
+                                      nz=self.aov.nz, z_max=self.aov.z_max, aov=self.aov)
         return float(out[0, 0].item())
 
     # ---- ODE fallback operators (fpy:207-219, 270-286) --------------------------------------
@@ -116,7 +120,7 @@ class BoltzmannSystem:
         self._nt = int(n)
         self._rec = to_point(self.cfg, P=self.P)
         self._work, status = eng.ode_tables(self._rec, [self._T_lo], [self._T_hi], nt=self._nt, nz=self.aov.nz,
-                                            z_max=self.aov.z_max)
+                                            z_max=self.aov.z_max, aov=self.aov)
         if int(status[0].item()) != 0:
             raise ValueError("`x` must be strictly increasing sequence.")
 

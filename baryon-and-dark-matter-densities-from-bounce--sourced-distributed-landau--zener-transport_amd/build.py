@@ -16,7 +16,7 @@ CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.normpath(os.path.join(HERE, "..", "include"))
 BUILD_DIR = os.path.join(HERE, "_build")
 LIB_PATH = os.path.join(BUILD_DIR, "liblzq.so")
-SOURCES = ["lzq_kernels.hip", "lzq_propagator.hip", "lzq_ode.hip", "lzq_profile.hip"]
+SOURCES = ["lzq_kernels.hip", "lzq_aov.hip", "lzq_propagator.hip", "lzq_ode.hip", "lzq_profile.hip"]
 # every header next to the sources (tests/test_engine_host.py checks each #include "..." of the
 # sources resolves to one of the build inputs)
 HEADERS = sorted(os.path.basename(h) for h in glob.glob(os.path.join(CSRC, "*.h")))
@@ -79,10 +79,27 @@ def build(force: bool = False, verbose: bool = False, defines: dict | None = Non
     os.makedirs(os.path.dirname(target), exist_ok=True)
     tmp = target + ".tmp"
     dflags = [f"-D{k}={v}" for k, v in (defines or {}).items()]
-    cmd = [hipcc(), *FLAGS, *dflags, "-I", INCLUDE, "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+    # one hipcc per translation unit, in parallel, then one link (each object embeds its own
+    # gfx950 code object, exactly as the single-command build does)
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+    with tempfile.TemporaryDirectory(prefix="lzq_build_") as objdir:
+        objs = [os.path.join(objdir, os.path.splitext(s)[0] + ".o") for s in SOURCES]
+        cflags = [f for f in FLAGS if f != "-shared"]
+        cmds = [[hipcc(), *cflags, *dflags, "-I", INCLUDE, "-c", os.path.join(CSRC, s), "-o", o]
+                for s, o in zip(SOURCES, objs)]
+        if verbose:
+            for c in cmds:
+                print(" ".join(c))
+        jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
+        with ThreadPoolExecutor(jobs) as ex:
+            for r in list(ex.map(lambda c: subprocess.run(c), cmds)):
+                if r.returncode:
+                    raise subprocess.CalledProcessError(r.returncode, r.args)
+        link = [hipcc(), *FLAGS, "-o", tmp, *objs]
+        if verbose:
+            print(" ".join(link))
+        subprocess.run(link, check=True)
     os.replace(tmp, target)
     with open(stamp_path(target), "w") as f:
         f.write(inputs_hash(defines) + "\n")

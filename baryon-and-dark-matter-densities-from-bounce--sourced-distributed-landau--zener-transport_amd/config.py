@@ -136,6 +136,28 @@ def to_ctypes_ode(rec: np.ndarray) -> "_native.LzqOdeParams":
     return o
 
 
+def to_aov(obj) -> np.ndarray:
+    """An A/V kernel's own parameters (fpy:141-151) -> one lzq_aov_params record.  obj: an
+    AoverVKernel (reference or boltzmann.AoverVKernel: attributes I_p, beta_over_H, T_p, v_w,
+    g_star), a dict with those keys (T_p or T_p_GeV), or a Config / fpy-schema dict (its own
+    kernel, fpy:197)."""
+    get = (lambda k: obj[k]) if isinstance(obj, dict) else (lambda k: getattr(obj, k))
+    def has(k):
+        return (k in obj) if isinstance(obj, dict) else hasattr(obj, k)
+    rec = np.zeros(1, dtype=_native.AOV_DTYPE)
+    for n in ("I_p", "beta_over_H", "v_w", "g_star"):
+        rec[n] = float(get(n))
+    rec["T_p_GeV"] = float(get("T_p") if has("T_p") else get("T_p_GeV"))
+    return rec
+
+
+def to_ctypes_aov(rec: np.ndarray) -> "_native.LzqAovParams":
+    a = _native.LzqAovParams()
+    for n in _native.AOV_FIELDS:
+        setattr(a, n, float(rec[n].item() if hasattr(rec[n], "item") else rec[n]))
+    return a
+
+
 def to_ctypes_point(rec: np.ndarray) -> "_native.LzqPoint":
     p = _native.LzqPoint()
     for n in _native.POINT_DOUBLE_FIELDS + _native.POINT_INT_FIELDS:

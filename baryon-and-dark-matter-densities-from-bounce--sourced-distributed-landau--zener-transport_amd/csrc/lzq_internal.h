@@ -17,8 +17,22 @@ constexpr int kOdeWS = LZQ_ODE_WS_PER_POINT;  // workspace doubles per point
 // A/V at the nt T-knots of every point (z grid (nz, z_max)) into w[4k + 3] / w[4 nt - 1] of its
 // 4 nt doubles (lzq_kernels.hip: the quadrature kernels' z-sum, one wavefront per point).
 // Host-side launch; sets lzq_last_error.
+// d_aov (optional, [n]): the A/V kernel's own parameters per point (lzq_aov.hip).
 int launch_ode_aov_tables(const lzq_point* d_points, int64_t n, const double* d_T_lo, const double* d_T_hi,
-                          int32_t nt, int32_t nz, double z_max, double* d_work, hipStream_t stream);
+                          int32_t nt, int32_t nz, double z_max, const lzq_aov_params* d_aov, double* d_work,
+                          hipStream_t stream);
+
+// lzq_aov.hip: the quadrature / build_tables kernels with the A/V constants of a per-point
+// lzq_aov_params block (fpy:141-151, 197, 211, 261), on a resolved z grid (zt, nzp; default_grid:
+// the compile-time LZQ_NZ kernels) and exp table gtab.  Set lzq_last_error on failure.
+struct ZNode;  // lzq_quad.h
+int launch_yields_points_aov(int exp_variant, bool default_grid, const lzq_point* d_points,
+                             const lzq_aov_params* d_aov, int64_t n, int32_t n_y, const double* d_T_lo,
+                             const double* d_T_hi, const double* d_P, const ZNode* zt, int32_t nzp, const double* gtab,
+                             lzq_yield* d_out, int truncate, hipStream_t s);
+int launch_ode_aov_tables_aov(int exp_variant, const lzq_point* d_points, const lzq_aov_params* d_aov, int64_t n,
+                              int32_t nt, const ZNode* zt, int32_t nzp, const double* gtab, const double* d_T_lo,
+                              const double* d_T_hi, double* d_work, int truncate, hipStream_t s);
 
 // Longest-first launch order (lzq_propagator.hip): cost bins per point (0 = costliest, kCostBins
 // of them) and their histogram -> offs (kCostBins scratch) and order[n] (a counting sort: one

@@ -32,710 +32,9 @@
 #include "lzq_internal.h"
 #include "lzq_physics.h"
 
+#include "lzq_quad.h"
+
 namespace lzq {
-
-constexpr int kNZ = LZQ_NZ;
-constexpr int kWaveSize = 64;
-// The block is sized so that the LDS copies of the exp table that fit in a CU's 160 KB carry
-// the waves: 64-KB table (default) -> two 1024-thread blocks per CU = 8 waves per SIMD, with
-// LZQ_MIN_WAVES = 8 capping the kernel at 64 VGPRs (its few spills sit outside the z-loop;
-// +2.2% over 4 waves/SIMD, tools/ablate_builds.py).
-#ifndef LZQ_BLOCK
-#define LZQ_BLOCK ((8 << LZQ_TABBITS) > 81920 ? 1024 : (8 << LZQ_TABBITS) > 40960 ? 1024 : 256)
-#endif
-constexpr int kBlock = LZQ_BLOCK;
-constexpr int kWavesPerBlock = kBlock / kWaveSize;
-#ifndef LZQ_KUNROLL
-#define LZQ_KUNROLL 8
-#endif
-#ifndef LZQ_YB
-#define LZQ_YB 1
-#endif
-// __launch_bounds__ second argument = minimum waves per SIMD (8: <= 64 VGPRs; see LZQ_BLOCK)
-#ifndef LZQ_MIN_WAVES
-#define LZQ_MIN_WAVES 8
-#endif
-// z-table source: 0 = wave-uniform scalar loads (SGPR operands), 1 = staged in LDS and read
-// with broadcast ds_read_b128 (keeps every LGKM operation of the loop in order, so the
-// compiler can use counted lgkmcnt waits instead of draining behind SMEM)
-#ifndef LZQ_ZLDS
-#define LZQ_ZLDS 0
-#endif
-#ifndef LZQ_YFACT_EARLY
-#define LZQ_YFACT_EARLY 0
-#endif
-// re-form y / e^y / weight after the z-loop instead of keeping them live across it
-#ifndef LZQ_Y_RECOMPUTE
-#define LZQ_Y_RECOMPUTE 1
-#endif
-// keep yb_wave's per-lane running sum in the wave's LDS slot instead of a VGPR pair
-#ifndef LZQ_ACC_LDS
-#define LZQ_ACC_LDS 1
-#endif
-constexpr int kKUnroll = LZQ_KUNROLL;  // z-nodes per scalar-load batch (must divide 1200)
-constexpr int kYB = LZQ_YB;            // y-nodes per lane per pass (independent chains)
-static_assert(kNZ % kKUnroll == 0, "z unroll must divide nz");
-
-struct ZNode {
-  double g4;     // fpy:156 gamma4(z_k), verbatim cancelling form
-  double omega;  // z_k^2 e^{-z_k} * trapezoid weight of node k
-};
-
-// ---------------------------------------------------------------------------------------
-// per-point quadrature setup (wave-uniform values)
-// ---------------------------------------------------------------------------------------
-struct QuadSetup {
-  double y_lo, y_hi, step, delta;  // ys = linspace(y_lo, y_hi, n)    fpy:247
-  int64_t n;
-  bool empty;                      // y_hi <= y_lo -> Y_B = 0         fpy:242-243
-  double pref0;                    // (I_p/2)(beta/v_w)               fpy:162
-  double cneg;                     // -(I_p/6)                        fpy:163
-  double Bc, Tp, dT0, sig, m, m3, flux, P, g_star, g_star_s;
-  double H0;      // 1.66 sqrt(g*) / M_Pl             fpy:85
-  double s0;      // (2 pi^2/45) g*s                   fpy:88
-  double c_rel;   // g * 3 zeta3/(4 pi^2) | g zeta3/pi^2   fpy:96-99
-  double c_nr;    // g (m/2pi)^1.5                     fpy:104
-  double v0;      // pi * max(m, 1e-20)                fpy:117
-  double isig;    // 1/sig: y_factors multiplies instead of dividing
-};
-
-// Move a wave-uniform double into SGPRs (two v_readfirstlane_b32): the per-point constants
-// then occupy scalar registers instead of ~44 VGPRs across the z-loop.
-__device__ __forceinline__ double uniform(double x) {
-  const uint64_t b = __builtin_bit_cast(uint64_t, x);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
-  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-}
-
-// x**1.5 as x*sqrt(x) (<= 2 ulp from pow; the device pow is ~100 VALU and ~40 VGPRs)
-__device__ __forceinline__ double pow15(double x) { return x * sqrt(x); }
-
-__device__ __forceinline__ QuadSetup quad_setup(const lzq_point& pt, double P, double T_lo, double T_hi,
-                                                int32_t n_y) {
-  QuadSetup s;
-  const double B = pt.beta_over_H, Tp = pt.T_p_GeV;
-  // fpy:234-243
-  double y_lo = pymax(y_of_T(T_hi, Tp, B), -80.0);
-  double y_hi = pymin(y_of_T(T_lo, Tp, B), +50.0);
-  s.empty = !(y_hi > y_lo);
-  s.y_lo = y_lo;
-  s.y_hi = y_hi;
-  s.n = n_y > LZQ_NY_MIN ? n_y : LZQ_NY_MIN;  // fpy:246
-  s.delta = y_hi - y_lo;
-  s.step = s.delta / (double)(s.n - 1);
-  // AoverVKernel constants fpy:146-151
-  double v_w = pymax(pt.v_w, 1e-12);
-  double H_p = H_std(Tp, pt.g_star);
-  double beta = B * H_p;
-  s.pref0 = (pt.I_p / 2.0) * (beta / v_w);
-  s.cneg = -(pt.I_p / 6.0);
-  // fpy:250-262
-  s.Bc = pymax(B, 1e-30);
-  s.Tp = Tp;
-  s.dT0 = -(Tp / s.Bc);
-  s.sig = pymax(pt.source_shape_sigma_y, 1e-6);
-  s.m = pt.m_chi_GeV;
-  s.m3 = pt.m_chi_GeV / 3.0;
-  s.flux = pt.incident_flux_scale;
-  s.P = P;
-  s.g_star = pt.g_star;
-  s.g_star_s = pt.g_star_s;
-  s.H0 = 1.66 * sqrt(pt.g_star);
-  s.s0 = (2.0 * (kPi * kPi) / 45.0) * pt.g_star_s;
-  s.c_rel = (pt.stats == 0) ? pt.g_chi * (3.0 * kZeta3 / (4.0 * (kPi * kPi))) : pt.g_chi * (kZeta3 / (kPi * kPi));
-  s.c_nr = pt.g_chi * pow15(pt.m_chi_GeV / (2.0 * kPi));
-  s.v0 = kPi * pymax(pt.m_chi_GeV, 1e-20);
-  s.isig = 1.0 / s.sig;
-  double* f[] = {&s.y_lo, &s.y_hi, &s.step, &s.delta, &s.pref0, &s.cneg, &s.Bc, &s.Tp, &s.dT0, &s.sig, &s.m,
-                 &s.m3, &s.flux, &s.P, &s.g_star, &s.g_star_s, &s.H0, &s.s0, &s.c_rel, &s.c_nr, &s.v0,
-                 &s.isig};
-#pragma unroll
-  for (double* v : f) *v = uniform(*v);
-  return s;
-}
-
-// A loop-invariant double materialised once in a VGPR (opaque to re-materialisation).
-__device__ __forceinline__ double vgpr_const(double x) {
-  double v;
-  asm volatile("v_mov_b64 %0, %1" : "=v"(v) : "s"(x));
-  return v;
-}
-
-// e^x for the per-y factors (<= 1 ulp, like the device libm exp).  Cody-Waite reduction
-// x = k ln2 + r, |r| <= ln2/2, Taylor series to r^13 (truncation < 5e-18), ldexp.  The 15
-// constants are read from constant memory through an offset made opaque per call, so they
-// come in by scalar loads where needed: the libm exp's coefficients were hoisted out of the
-// y-loop into VGPRs and spilled to scratch across the z-loop (which needs ~60 of 64 VGPRs).
-#ifndef LZQ_YFAST
-#define LZQ_YFAST 7  // bit mask (A/B builds): 1 SGPR Horner steps, 2 rsqrt, 4 1/sigma product
-#endif
-
-__constant__ double kExpC[15] = {
-    0x1.6124613a86d09p-33, 0x1.1eed8eff8d898p-29, 0x1.ae64567f544e4p-26, 0x1.27e4fb7789f5cp-22,
-    0x1.71de3a556c734p-19, 0x1.a01a01a01a01ap-16, 0x1.a01a01a01a01ap-13, 0x1.6c16c16c16c17p-10,
-    0x1.1111111111111p-7,  0x1.5555555555555p-5,  0x1.5555555555555p-3,  0x1.0p-1,  // 1/13! .. 1/2!
-    0x1.71547652b82fep+0,                                                           // 1/ln2
-    0x1.62e42fefa39efp-1,  0x1.abc9e3b39803fp-56};                                  // ln2 hi, lo
-__device__ __forceinline__ double exp_sc(double x) {
-  int o = 0;
-  asm volatile("" : "+s"(o));
-  const double* c = kExpC + o;
-  x = x < -1100.0 ? -1100.0 : x;  // NaN passes through both
-  x = x > 710.0 ? 710.0 : x;
-  const double k = __builtin_rint(x * c[12]);
-  double r = __builtin_fma(-k, c[13], x);
-  r = __builtin_fma(-k, c[14], r);
-  double p = c[0];
-#pragma unroll
-  for (int i = 1; i < 12; ++i) p = (LZQ_YFAST & 1) ? fma_vvs(p, r, c[i]) : __builtin_fma(p, r, c[i]);
-  p = __builtin_fma(p, r, 1.0);  // (e^r - 1) / r
-  p = __builtin_fma(p, r, 1.0);  // e^r
-  return __builtin_ldexp(p, (int)k);
-}
-
-// numpy.linspace element (handles numpy's step == 0 branch as well)
-__device__ __forceinline__ double y_node(const QuadSetup& s, int j) {  // n_y is int32
-  const int n = (int)s.n;
-  if (j == n - 1) return s.y_hi;
-  if (s.step == 0.0) return ((double)j / (double)(n - 1)) * s.delta + s.y_lo;
-  return (double)j * s.step + s.y_lo;
-}
-
-// Per-y factors of the integrand of fpy:264-265 that do not depend on F, computed BEFORE the
-// z-loop so that only these 7 doubles (not the whole QuadSetup) stay live across it.  The
-// post-loop combination keeps the reference's rounding order:
-//   SB = ((P*J)*Av)*W,  integrand = SB/((s*H)*T)*|dT/dy|,  Av = (pref0*expy)*F.
-struct YFactors {
-  double PJ;     // P * J(T)                        fpy:260,264
-  double W;      // window                          fpy:262
-  double sHT;    // (s*H)*T                         fpy:258-259,265
-  double adTdy;  // |dT/dy|                         fpy:255,265
-  double pexp;   // pref0 * expy  (A/V prefactor)   fpy:162
-  double w;      // trapezoid weight of the node    fpy:267
-  double live;   // 1 if y <= 50 (fpy:159), else 0
-};
-
-// 1/sqrt(d) for a positive normal d: v_rsq_f64, then the Goldschmidt iteration that the
-// compiler's correctly rounded sqrt uses (g -> sqrt(d), h -> 1/(2 sqrt(d))); <= 2 ulp.
-__device__ __forceinline__ double rsqrt_pos(double d) {
-  const double r = __builtin_amdgcn_rsq(d);
-  double g = d * r, h = 0.5 * r;
-  double e = __builtin_fma(-g, h, 0.5);
-  g = __builtin_fma(g, e, g);
-  h = __builtin_fma(h, e, h);
-  e = __builtin_fma(-g, h, 0.5);
-  h = __builtin_fma(h, e, h);
-  return 2.0 * h;
-}
-
-// The fixed-exponent powers of numpy's `**` (SVML pow, <= 1 ulp) are evaluated with products
-// (<= 3 ulp): denom**-0.5 and denom**-1.5 from one reciprocal square root, T**3 = (T*T)*T,
-// T**1.5 = T sqrt T; the quotients by per-point constants (y/sigma, H's 1/M_Pl) are products
-// with their reciprocals.  This keeps the per-y work small (the device pow(double) is
-// ~100 VALU and ~40 VGPRs; a division or a sqrt ~10-16) and moves results by ~1e-16 relative
-// (tests: worst golden error unchanged at 1e-13).
-__device__ __forceinline__ YFactors y_factors(const QuadSetup& s, double y, double expy, double wt) {
-  YFactors f;
-  double T, dTdy, H;
-  if (LZQ_YFAST & 2) {
-    // 2y/B stays a correctly rounded division: near y = -B/2 (T_max/T_p large) 1 + 2y/B cancels,
-    // and the product with a rounded 2/B moved Y_B by 6.7e-13 on a golden point (diag_golden.py)
-    const double denom = pymax(1.0 + 2.0 * y / s.Bc, 1e-12);  // fpy:252-253
-    const double rs = rsqrt_pos(denom);
-    T = s.Tp * rs;                                           // fpy:254
-    dTdy = s.dT0 * ((rs * rs) * rs);                         // fpy:255  denom**(-1.5)
-    H = s.H0 * T * T * (1.0 / kMplGeV);                      // fpy:258 via fpy:85
-  } else {
-    const double denom = pymax(1.0 + 2.0 * y / s.Bc, 1e-12);
-    const double sd = sqrt(denom);
-    T = s.Tp / sd;
-    dTdy = s.dT0 * (1.0 / (denom * sd));
-    H = s.H0 * T * T / kMplGeV;
-  }
-  double T3 = (T * T) * T;
-  double sE = s.s0 * T3;                                  // fpy:259 via fpy:88
-  double n_eq, vbar;                                      // fpy:90-120, strict T > m/3 branch
-  if (T > s.m3) {
-    n_eq = s.c_rel * T3;
-    vbar = 1.0;
-  } else {
-    n_eq = s.c_nr * (T * sqrt(T)) * exp_sc(-s.m / pymax(T, 1e-30));
-    vbar = sqrt(pymax(8.0 * T / s.v0, 0.0));
-  }
-  double J = s.flux * 0.25 * n_eq * vbar;                 // fpy:260
-  double q = (LZQ_YFAST & 4) ? y * s.isig : y / s.sig;
-  f.W = exp_sc(-0.5 * (q * q));                              // fpy:262
-  f.PJ = s.P * J;
-  f.sHT = sE * H * T;
-  f.adTdy = fabs(dTdy);
-  f.pexp = s.pref0 * expy;
-  f.w = wt;
-  f.live = (y > 50.0) ? 0.0 : 1.0;
-  return f;
-}
-
-__device__ __forceinline__ double integrand_from(const YFactors& f, double F) {
-  double Av = f.live != 0.0 ? f.pexp * F : 0.0;           // fpy:159-165
-  double SB = f.PJ * Av * f.W;                            // fpy:264
-  return SB / f.sHT * f.adTdy;                            // fpy:265
-}
-
-// trapezoid weight of y-node j: (d_{j-1} + d_j)/2 with d = diff(ys)      fpy:267
-__device__ __forceinline__ double y_weight(const QuadSetup& s, int j, double y) {
-  double dl = (j > 0) ? y - y_node(s, j - 1) : 0.0;
-  double dr = (j + 1 < (int)s.n) ? y_node(s, j + 1) - y : 0.0;
-  return 0.5 * (dl + dr);
-}
-
-// exp variants of the inner loop (lzq_tune(LZQ_TUNE_EXP, ...))
-enum ExpVariant { kExpPoly11 = 0, kExpTable = 1 };
-
-// Scale of c2 expected by the variant (2^(c2*g) for poly11, 2^(c2N*g/256) for the table).
-template <int EXPV>
-__device__ __forceinline__ double c2_scale() { return EXPV == kExpTable ? (double)kTabN : 1.0; }
-
-// F(c2) = sum_k omega_k 2^(c2 g4_k) for YB independent y-nodes per lane.
-//
-// The loop is VALU-issue bound: an FP64 instruction costs 4.4 cycles per wave64 on gfx950 and an
-// integer / FP32 one ~2.5 (tools/ubench_valu.hip, pure streams); in this kernel a node's 8.48
-// VALU instructions take 30.9 SIMD-cycles, 79% of them in the 6.1 FP64 FMA/MUL/ADD
-// (profiles/round2/pmc_summary.json).  So the loop is built to minimise the instruction count,
-// FP64 first.  Table variant, per (y, z) node:
-//
-//   t  = fma(c2, g, M)          M = 1.5*2^52: t = M + round(u), u = c2*g in 1/N-octave units
-//   kd = t - M                  exact
-//   r  = fma(c2, g, -kd)        u - round(u) in [-1/2, 1/2], one rounding
-//   tc = max(t, M + KMIN)       clamp to e >= -1534 octaves (also keeps lo32 in int range)
-//   a  = (lo32(tc) & (N-1))*8   LDS byte address: ONE v_lshlrev_b16 for N = 8192
-//   T' = lds[a]                 T'.hi = hi(2^(j/N)) - (j << S) + (512 << 20), S = 20 - BITS
-//   T'.hi += lo32(tc) << S      ONE v_lshl_add_u32: T' = 2^(j/N) * 2^(e+512), e = floor(k/N)
-//   q  = r*(B1 + r*B2)          2 FP64
-//   v  = fma(T', q, T')         = 2^(u/N) * 2^512, always a normal double (e+512 >= -1022)
-//   F  = fma(omega', v, F)      omega' = omega * 2^-512 (z table), so omega'*v = omega*2^u
-//
-// = 10 VALU per node (round-1 kernel: 12.5).  The default completed-square form (kSqForm,
-// lzq_exp2.h) replaces kd, r, q and the T*(1+q) fma by
-//   w  = (M + A) - t            exact (M + A an integer below 2^53)
-//   s  = fma(c2, g, w)          r + A, one rounding
-//   v  = T'' * fma(s, s, beta)  T'' = C * 2^(j/N) * 2^(e+512) from the same lookup + insert
-// = 9 VALU per node, 8 on clamp-free passes.  The last fma rounds the exact product omega*2^u
-// once, so gradual underflow is exact; clamped nodes (u < -1534 octaves) contribute
-// omega*2^-1534*(...) which rounds away exactly like the underflowed 0 it stands for.
-// For |u| < 2^51 (every non-dead lane, checked on the host) t is exact; dead lanes (whose
-// every node k >= 1 underflows) run with c2 = 0 and are zeroed, so no input reaches the
-// loop with |u| >= 2^51.
-//
-// CLAMP = false drops the max (9 VALU/node) on passes whose lanes all satisfy |c2N|*g_max <=
-// N*1534 (no node can leave the clamp range); zsum_dispatch picks it per pass.
-template <int YB, int EXPV, bool CLAMP = true>
-__device__ __forceinline__ void zsum(const ZNode* __restrict__ zt, const double* tab, const double (&c2)[YB],
-                                     double (&F)[YB], int kend) {
-#pragma unroll
-  for (int b = 0; b < YB; ++b) F[b] = 0.0;
-  if constexpr (EXPV == kExpTable) {
-    constexpr double kMagic = 0x1.8p52;
-    constexpr double kTClamp = kMagic + (double)kTabKMin;  // exact
-    const double Mv = vgpr_const(kMagic);
-    const double MAv = kMagic + kSqA;  // exact (an integer below 2^53)
-    // plain form: polynomial coefficients, B1 pinned in a VGPR for the whole loop (see tab_q_with)
-    double Bv[kPolyDeg];
-#pragma unroll
-    for (int i = 0; i < kPolyDeg; ++i) Bv[i] = TabPoly<kTabBits, kPolyDeg>::B[i];
-    if constexpr (!kSqForm) Bv[0] = vgpr_const(Bv[0]);
-    const char* tabb = reinterpret_cast<const char*>(tab);
-    for (int k = 0; k < kend; k += kKUnroll) {
-      double g4[kKUnroll], om[kKUnroll];
-#pragma unroll
-      for (int kk = 0; kk < kKUnroll; ++kk) {
-        g4[kk] = zt[k + kk].g4;
-        om[kk] = zt[k + kk].omega;
-      }
-      // phases: reduction + addresses for the whole batch, then the lookups (in flight
-      // together), then polynomial + accumulate
-      double r[YB][kKUnroll], T[YB][kKUnroll];
-      uint32_t kc[YB][kKUnroll], a[YB][kKUnroll];
-#pragma unroll
-      for (int kk = 0; kk < kKUnroll; ++kk)
-#pragma unroll
-        for (int b = 0; b < YB; ++b) {
-          const double t = __builtin_fma(c2[b], g4[kk], Mv);
-          if constexpr (kSqForm) {
-            r[b][kk] = __builtin_fma(c2[b], g4[kk], MAv - t);  // s = r + A (lzq_exp2.h)
-          } else {
-            const double kd = t - Mv;
-            r[b][kk] = __builtin_fma(c2[b], g4[kk], -kd);
-          }
-          const double tc = CLAMP ? __builtin_fmax(t, kTClamp) : t;
-          kc[b][kk] = (uint32_t)__builtin_bit_cast(uint64_t, tc);
-          a[b][kk] = tab_byte_addr(kc[b][kk]);
-        }
-#pragma unroll
-      for (int kk = 0; kk < kKUnroll; ++kk)
-#pragma unroll
-        for (int b = 0; b < YB; ++b) T[b][kk] = *reinterpret_cast<const double*>(tabb + a[b][kk]);
-#pragma unroll
-      for (int kk = 0; kk < kKUnroll; ++kk)
-#pragma unroll
-        for (int b = 0; b < YB; ++b) {
-          const double Ts = tab_scale(T[b][kk], kc[b][kk]);
-          if constexpr (kSqForm) {
-            F[b] = __builtin_fma(om[kk], Ts * __builtin_fma(r[b][kk], r[b][kk], kSqBeta), F[b]);
-          } else {
-            const double q = tab_q_with<kPolyDeg>(r[b][kk], Bv);
-            F[b] = __builtin_fma(om[kk], __builtin_fma(Ts, q, Ts), F[b]);
-          }
-        }
-    }
-  } else {
-    for (int k = 0; k < kend; k += kKUnroll) {
-#pragma unroll
-      for (int kk = 0; kk < kKUnroll; ++kk) {
-        const double g = zt[k + kk].g4, om = zt[k + kk].omega;
-#pragma unroll
-        for (int b = 0; b < YB; ++b) F[b] = __builtin_fma(om, exp2_nonpos(c2[b], g, kOmegaBias), F[b]);
-      }
-    }
-  }
-}
-
-// Pass-level wrapper: "dead" lanes, c2 * g4_1 <= -N*1077 (every node k >= 1 underflows to
-// exactly 0: g4 is increasing and omega_0 = 0), run the loop with c2 = 0 and are zeroed
-// afterwards -- the same instruction stream, the exact zero.
-//
-// The z grid: NZ > 0 is the compile-time node count of the reference's default grid
-// (fpy:142, LZQ_NZ = 1200: the headline kernels); NZ = 0 reads the padded node count nzp of a
-// runtime (nz, z_max) grid (AoverVKernel(..., z_max, nz), fpy:141-156).  Padding nodes repeat the
-// last g4 with omega = 0: each adds an exact +0, so F is the sum over the nz real nodes.  On a
-// fine grid (small g4_1) a live lane can reach |u| >= 2^51 at later nodes, where the magic-
-// constant reduction is inexact; every such node has u < KMIN, takes the clamped path (the
-// clamp-free test below sees it), and its term omega' * T''(KMIN) * ((A + O(|u| 2^-52))^2 + beta)
-// stays below 2^-1074 for |u| < 2^200, so it rounds away exactly like the underflow it stands
-// for (tests/test_exp2_host.py); build_ztable bounds |u| by that on the host.
-//
-// truncate != 0 (lzq_tune LZQ_TUNE_TRUNCATE; NOT used by the headline bench, which is dense
-// per SURVEY §8d): the pass stops at kend, the first z-node (rounded up to the unroll) beyond
-// which every live lane has c2*g4_k < -1080 octaves.  Those nodes add omega*2^u < 2^-1080 to
-// F, which the accumulate's rounding discards exactly, so F is bit-identical to the dense sum.
-// (Needs g4 non-decreasing over the grid: the host passes truncate = 0 for a grid whose
-// rounded g4 is not.)
-template <int YB, int EXPV, int NZ = 0>
-__device__ __forceinline__ void zsum_dispatch(const ZNode* __restrict__ zt, int nzp, const double* tab,
-                                              const double (&c2)[YB], double (&F)[YB], int truncate = 0) {
-  const int nz = NZ > 0 ? NZ : nzp;
-  const double g_1 = zt[1].g4, g_max = zt[nz - 1].g4;
-  bool dead[YB], small = true;
-  double c2e[YB];
-#pragma unroll
-  for (int b = 0; b < YB; ++b) {
-    dead[b] = c2[b] * g_1 <= -c2_scale<EXPV>() * 1077.0;
-    c2e[b] = dead[b] ? 0.0 : c2[b];
-    small = small && c2e[b] * g_max >= (double)kTabKMin;  // every node stays >= KMIN
-  }
-  int kend = nz;
-  if (truncate) {
-    // largest per-lane threshold g_thr = -1080 N / c2 (live lanes; dead lanes impose none,
-    // c2 = 0 lanes never underflow)
-    double thr = 0.0;
-#pragma unroll
-    for (int b = 0; b < YB; ++b) {
-      const double tb = dead[b] ? 0.0 : (c2e[b] < 0.0 ? (-1080.0 * c2_scale<EXPV>()) / c2e[b] : __builtin_inf());
-      thr = pymax(thr, tb);
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) thr = pymax(thr, __shfl_xor(thr, off, kWaveSize));
-    thr = uniform(thr);
-    // first k with g4_k > thr (g4 increasing): scalar binary search over the z table
-    int lo = 0, hi = nz;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (zt[mid].g4 > thr) hi = mid;
-      else lo = mid + 1;
-    }
-    kend = (lo + kKUnroll - 1) / kKUnroll * kKUnroll;
-  }
-  if (EXPV == kExpTable && __all(small))
-    zsum<YB, EXPV, false>(zt, tab, c2e, F, kend);
-  else
-    zsum<YB, EXPV, true>(zt, tab, c2e, F, kend);
-#pragma unroll
-  for (int b = 0; b < YB; ++b) F[b] = dead[b] ? 0.0 : F[b];
-}
-
-// Stage the exp table (N doubles, see lzq_exp2.h) in LDS (every thread of the block must call this).
-template <int EXPV>
-__device__ __forceinline__ const double* stage_table(const double* __restrict__ gtab, double* lds) {
-  if (EXPV != kExpTable) return nullptr;
-  for (int i = threadIdx.x; i < kTabN; i += blockDim.x) lds[i] = gtab[i];
-  __syncthreads();
-  return lds;
-}
-
-// LDS image of the per-block tables: z nodes (19.2 KB) followed by the exp table.
-struct LdsTables {
-  ZNode z[kNZ];
-  double t[kTabN];
-};
-
-// Stage both tables (global layout: ZNode[kNZ] then double[kTabN], see ensure_device).
-template <int EXPV>
-__device__ __forceinline__ void stage_tables(const ZNode* __restrict__ gz, LdsTables* lds) {
-  const double* src = reinterpret_cast<const double*>(gz);
-  double* dst = reinterpret_cast<double*>(lds);
-  constexpr int n = 2 * kNZ + (EXPV == kExpTable ? kTabN : 0);
-  for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
-  __syncthreads();
-}
-
-// Fixed-order xor butterfly over the 64 lanes (every lane ends with the same sum).
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWaveSize);
-  return v;
-}
-
-// Lane index 0..63, re-derived where it is used (v_mbcnt; volatile, so it is not kept live).
-__device__ __forceinline__ int lane_id() {
-  int l;
-  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-  return l;
-}
-
-// Y_B of one point by one wavefront.  fpy:231-267
-//
-// Nothing but the z-loop's own state is held in registers across the z-loop (which needs ~60
-// of the 64 VGPRs at 8 waves/SIMD):
-//   * the point's QuadSetup lives in the wave's LDS slot (~44 SGPRs otherwise); each pass
-//     re-reads the fields it needs with broadcast ds_reads, through a slot index made opaque
-//     per pass so that the reads are not hoisted back out of the y-loop;
-//   * y, e^y and the weight are re-formed after the z-loop (same operations, same bits);
-//   * the lane's running sum over its y-nodes sits in the slot (LZQ_ACC_LDS).
-// Without this the kernel spilled ~200 B/lane to scratch around every z-loop.
-// MODE (see lzq_sweep_grid_reuse): kYbDense computes every F(y_j) = sum_k omega_k 2^(c2_j g_k)
-// itself (the headline); kYbTable computes them the same way and stores them to Fout instead of
-// integrating; kYbReuse reads them from Fin (a table written by kYbTable for a point with the
-// same y-grid and A/V kernel) and integrates.  The F values and the integration are the same
-// operations in the same lane order in every mode, so Y_B is bit-identical.
-enum YbMode { kYbDense = 0, kYbReuse = 1, kYbTable = 2 };
-
-template <int YB, int EXPV, int MODE = kYbDense, int NZ = 0, typename Slot>
-__device__ double yb_wave(Slot* slots, int w, const ZNode* __restrict__ zt, int nzp, const double* tab, int truncate,
-                          const double* __restrict__ Fin = nullptr, double* __restrict__ Fout = nullptr) {
-  static_assert(MODE == kYbDense || !LZQ_YFACT_EARLY, "table modes re-form the y-factors after the z-loop");
-  if (slots[w].s.empty) return 0.0;
-  // y-node counts are int32 (n_y of the C ABI): 32-bit loop bounds save the SGPRs that
-  // would otherwise spill around the z-loop
-  const int n = (int)__builtin_bit_cast(int64_t, uniform(__builtin_bit_cast(double, slots[w].s.n)));  // SGPR
-  const int per_pass = kWaveSize * YB;
-#if LZQ_ACC_LDS
-  slots[w].acc[lane_id()] = 0.0;
-#else
-  double acc = 0.0;
-#endif
-  for (int base = 0; base < n; base += per_pass) {
-    // only y, e^y and the weight stay live across the z-loop (LZQ_YFACT_EARLY=1: the 7
-    // y-factors instead); the y-factors are formed after it
-    double yv[YB], ey[YB], wt[YB];
-#if LZQ_YFACT_EARLY
-    YFactors fy[YB];
-#endif
-    double F[YB];
-    if constexpr (MODE == kYbReuse) {
-      const int lane = lane_id();
-#pragma unroll
-      for (int b = 0; b < YB; ++b) {
-        const int j = base + b * kWaveSize + lane;
-        F[b] = Fin[j < n ? j : n - 1];
-      }
-    } else {
-      const int lane = lane_id();
-      int wo = w;
-      asm volatile("" : "+s"(wo));
-      const QuadSetup& s = slots[wo].s;
-      double c2[YB];
-#pragma unroll
-      for (int b = 0; b < YB; ++b) {
-        const int j = base + b * kWaveSize + lane;
-        const int jj = j < n ? j : n - 1;  // tail lanes recompute the last node with weight 0
-        yv[b] = y_node(s, jj);
-        ey[b] = exp_sc(pymax(pymin(yv[b], 50.0), -50.0));                          // fpy:161
-        c2[b] = ((s.cneg * ey[b]) * kLog2E) * c2_scale<EXPV>();                 // fpy:163 c, log2 units
-        wt[b] = j < n ? y_weight(s, jj, yv[b]) : 0.0;
-#if LZQ_YFACT_EARLY
-        fy[b] = y_factors(s, yv[b], ey[b], wt[b]);
-#endif
-      }
-      zsum_dispatch<YB, EXPV, NZ>(zt, nzp, tab, c2, F, truncate);
-      if constexpr (MODE == kYbTable) {
-#pragma unroll
-        for (int b = 0; b < YB; ++b) {
-          const int j = base + b * kWaveSize + lane;
-          if (j < n) Fout[j] = F[b];
-        }
-        continue;
-      }
-    }
-    int wr = w;
-    asm volatile("" : "+s"(wr));
-    const int lane2 = lane_id();
-    if (MODE == kYbReuse || (LZQ_Y_RECOMPUTE && !LZQ_YFACT_EARLY)) {
-      const QuadSetup& sr = slots[wr].s;
-#pragma unroll
-      for (int b = 0; b < YB; ++b) {
-        const int j = base + b * kWaveSize + lane2;
-        const int jj = j < n ? j : n - 1;
-        yv[b] = y_node(sr, jj);
-        ey[b] = exp_sc(pymax(pymin(yv[b], 50.0), -50.0));
-        wt[b] = j < n ? y_weight(sr, jj, yv[b]) : 0.0;
-      }
-    }
-#if LZQ_ACC_LDS
-    double acc = slots[wr].acc[lane2];
-#endif
-#pragma unroll
-    for (int b = 0; b < YB; ++b) {
-#if !LZQ_YFACT_EARLY
-      const YFactors f = y_factors(slots[wr].s, yv[b], ey[b], wt[b]);
-#else
-      const YFactors& f = fy[b];
-#endif
-      acc = __builtin_fma(f.w, integrand_from(f, F[b]), acc);
-    }
-#if LZQ_ACC_LDS
-    slots[wr].acc[lane2] = acc;
-#endif
-  }
-#if LZQ_ACC_LDS
-  return wave_sum(slots[w].acc[lane_id()]);
-#else
-  return wave_sum(acc);
-#endif
-}
-
-// fpy:372-384 (fast path) + fpy:413-417, split around the quadrature: epilogue_pre forms every
-// field that does not depend on Y_B before the z-loops (so the point record need not stay live
-// across them), epilogue_finish adds Y_B with the same operations and rounding order.
-struct EpiPre {
-  lzq_yield o;  // Y_chi, rho_DM_kg_m3, P_used set
-  int valid;    // regime is thermal / nonthermal
-};
-
-__device__ __forceinline__ EpiPre epilogue_pre(const lzq_point& pt, double P) {
-  const double T_p = pt.T_p_GeV;
-  const double T_hi = pt.T_max_over_Tp * T_p;
-  double Ychi;
-  if (pt.regime == LZQ_THERMAL) {
-    Ychi = n_chi_eq(T_hi, pt.m_chi_GeV, pt.g_chi, pt.stats) / s_entropy(T_hi, pt.g_star_s);
-  } else if (pt.regime == LZQ_NONTHERMAL) {
-    if (pt.has_Y_chi_init) Ychi = pt.Y_chi_init;
-    else if (pt.has_n_chi_at_Tp) Ychi = pt.n_chi_at_Tp_GeV3 / pymax(s_entropy(T_p, pt.g_star_s), 1e-300);
-    else Ychi = 1.0e-12;
-  } else {
-    Ychi = __builtin_nan("");  // reference: UnboundLocalError
-  }
-  EpiPre e;
-  const double nDM0 = Ychi * kS0M3;
-  e.o.Y_B = 0.0;
-  e.o.rho_B_kg_m3 = 0.0;
-  e.o.DM_over_B = 0.0;
-  e.o.Y_chi = Ychi;
-  e.o.rho_DM_kg_m3 = nDM0 * (pt.m_chi_GeV * kGeVToKg);
-  e.o.P_used = P;
-  e.valid = pt.regime == LZQ_THERMAL || pt.regime == LZQ_NONTHERMAL;
-  return e;
-}
-
-__device__ __forceinline__ lzq_yield epilogue_finish(const EpiPre& e, double YB) {
-  lzq_yield o = e.o;
-  const double nB0 = YB * kS0M3;
-  o.Y_B = YB;
-  o.rho_B_kg_m3 = nB0 * kMProtonKg;
-  o.DM_over_B = o.rho_DM_kg_m3 / pymax(o.rho_B_kg_m3, 1e-300);
-  if (!e.valid) o.Y_B = o.rho_B_kg_m3 = o.rho_DM_kg_m3 = o.DM_over_B = __builtin_nan("");
-  return o;
-}
-
-// Per-wave LDS slot of the quadrature kernels (one point per wavefront).
-struct WaveSlot {
-  QuadSetup s;
-  EpiPre e;
-#if LZQ_ACC_LDS
-  double acc[kWaveSize];  // per-lane running sums of yb_wave
-#endif
-};
-
-// Park the (wave-uniform) setup and epilogue inputs in the wave's slot.  Lane 0 writes; LDS
-// operations of one wavefront complete in order, the fence makes that formal for the compiler.
-__device__ __forceinline__ void park(WaveSlot& slot, const QuadSetup& s, const EpiPre& e, int lane) {
-  if (lane == 0) {
-    slot.s = s;
-    slot.e = e;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
-// Quadrature of the parked point, then lane 0 stores its yields.
-template <int YB, int EXPV, int NZ>
-__device__ __forceinline__ void point_yields(WaveSlot* slots, int w, const ZNode* __restrict__ zt, int nzp,
-                                             const double* tab, int lane, int truncate, lzq_yield* out) {
-  const double Y_B = yb_wave<YB, EXPV, kYbDense, NZ>(slots, w, zt, nzp, tab, truncate);
-  if (lane == 0) *out = epilogue_finish(slots[w].e, Y_B);
-}
-
-// ---------------------------------------------------------------------------------------
-// point sources
-// ---------------------------------------------------------------------------------------
-struct GridSpec {
-  int32_t n_axes;
-  int32_t field[LZQ_MAX_AXES];
-  int64_t n[LZQ_MAX_AXES];
-  int64_t stride[LZQ_MAX_AXES];
-  const double* values[LZQ_MAX_AXES];
-  int64_t tstride[LZQ_MAX_AXES];  // lzq_sweep_grid_reuse: stride in the z-sum table index (0: axis not in it)
-};
-
-__device__ __forceinline__ void set_field(lzq_point& p, int32_t f, double v, double& delta, double& m_mix,
-                                          double& dprime) {
-  switch (f) {  // explicit switch: a runtime-indexed store would push the struct to scratch
-    case LZQ_F_M_CHI: p.m_chi_GeV = v; break;
-    case LZQ_F_G_CHI: p.g_chi = v; break;
-    case LZQ_F_T_P: p.T_p_GeV = v; break;
-    case LZQ_F_BETA_OVER_H: p.beta_over_H = v; break;
-    case LZQ_F_V_W: p.v_w = v; break;
-    case LZQ_F_I_P: p.I_p = v; break;
-    case LZQ_F_G_STAR: p.g_star = v; break;
-    case LZQ_F_G_STAR_S: p.g_star_s = v; break;
-    case LZQ_F_P: p.P_chi_to_B = v; break;
-    case LZQ_F_SIGMA_Y: p.source_shape_sigma_y = v; break;
-    case LZQ_F_FLUX: p.incident_flux_scale = v; break;
-    case LZQ_F_T_MAX_OVER_TP: p.T_max_over_Tp = v; break;
-    case LZQ_F_T_MIN_OVER_TP: p.T_min_over_Tp = v; break;
-    case LZQ_F_Y_CHI_INIT: p.Y_chi_init = v; p.has_Y_chi_init = 1; break;
-    case LZQ_F_N_CHI_AT_TP: p.n_chi_at_Tp_GeV3 = v; p.has_n_chi_at_Tp = 1; break;
-    case LZQ_F_DELTA_LZ: delta = v; break;
-    case LZQ_F_M_MIX: m_mix = v; break;
-    case LZQ_F_DPRIME: dprime = v; break;
-    default: break;
-  }
-}
-
-// Materialise grid point `idx`; returns P after the LZ closed form if an LZ axis is swept.
-__device__ __forceinline__ double grid_point(const lzq_point& base, const GridSpec& g, int64_t idx, lzq_point& p) {
-  p = base;
-  double delta = __builtin_nan(""), m_mix = __builtin_nan(""), dprime = __builtin_nan("");
-  bool has_delta = false, has_mix = false;
-  for (int a = 0; a < g.n_axes; ++a) {
-    int64_t c = (idx / g.stride[a]) % g.n[a];
-    double v = g.values[a][c];
-    set_field(p, g.field[a], v, delta, m_mix, dprime);
-    has_delta |= g.field[a] == LZQ_F_DELTA_LZ;
-    has_mix |= g.field[a] == LZQ_F_M_MIX;
-  }
-  if (has_mix) delta = m_mix * m_mix / (2.0 * pymax(p.v_w, 1e-12) * fabs(dprime));  // PAPER eq.(8)
-  if (has_mix || has_delta) p.P_chi_to_B = p_closed_form(delta);                     // fpy:183-184
-  return p.P_chi_to_B;
-}
 
 // ---------------------------------------------------------------------------------------
 // kernels
@@ -1099,6 +398,13 @@ int build_ztable(int32_t nz, double z_max, HostZGrid& h) {
                   "below 0 on this grid", k, h.g4[k], nz, z_max);
     if (k > 0 && h.g4[k] < h.g4[k - 1]) h.monotone = false;
   }
+  // zsum_dispatch zeroes a lane whose term at node 1 underflows (c2 g4_1 <= -1077 N), which is
+  // exact only if g4_1 is the smallest g4 over k >= 1: a grid whose rounded gamma4 decreases
+  // anywhere (only the finest grids, where the cancelling form is noise at its first nodes) is
+  // refused like the negative one above
+  if (!h.monotone)
+    return fail(LZQ_EINVAL, "z grid (nz = %d, z_max = %g): the cancelling gamma4 of fpy:156 is not non-decreasing on "
+                "this grid (rounding noise at its first nodes)", nz, z_max);
   for (int k = 0; k < nz; ++k) {
     const double dl = k > 0 ? h.z[k] - h.z[k - 1] : 0.0;
     const double dr = k + 1 < nz ? h.z[k + 1] - h.z[k] : 0.0;
@@ -1240,7 +546,8 @@ constexpr int64_t kMaxGrid = 2147483647LL;
 int lzq_set_error(int code, const char* msg) { return fail(code, "%s", msg); }
 
 int lzq::launch_ode_aov_tables(const lzq_point* d_points, int64_t n, const double* d_T_lo, const double* d_T_hi,
-                               int32_t nt, int32_t nz, double z_max, double* d_work, hipStream_t stream) {
+                               int32_t nt, int32_t nz, double z_max, const lzq_aov_params* d_aov, double* d_work,
+                               hipStream_t stream) {
   if (n == 0) return LZQ_OK;
   int dev;
   DevZGrid g;
@@ -1252,6 +559,9 @@ int lzq::launch_ode_aov_tables(const lzq_point* d_points, int64_t n, const doubl
   // to the dense sum (tests/test_gpu_parity.py::test_truncation_is_bit_identical) and this path
   // is not the dense headline benchmark, so there is nothing to keep dense for.
   const int truncate = g.monotone ? 1 : 0;
+  if (d_aov)  // the A/V kernel's own parameters (lzq_aov.hip)
+    return lzq::launch_ode_aov_tables_aov(g_exp_variant, d_points, d_aov, n, nt, g.zt, g.nzp, exp_table(dev), d_T_lo,
+                                          d_T_hi, d_work, truncate, stream);
   if (g_exp_variant == lzq::kExpTable)
     hipLaunchKernelGGL(lzq::ode_aov_table_kernel<lzq::kExpTable>, dim3((unsigned)nb), dim3(lzq::kBlock), 0, stream,
                        d_points, n, nt, g.zt, g.nzp, exp_table(dev), d_T_lo, d_T_hi, d_work, truncate);
@@ -1333,10 +643,22 @@ int lzq_ztables(int32_t nz, double z_max, double* z, double* gamma4, double* ome
   return LZQ_OK;
 }
 
-int lzq_aov_batch(const lzq_point* pt, const double* d_y, int64_t n, int32_t nz, double z_max, double* d_out,
-                  void* stream) {
-  if (!pt || n < 0 || (n > 0 && (!d_y || !d_out))) return fail(LZQ_EINVAL, "lzq_aov_batch: bad arguments");
+int lzq_aov_batch(const lzq_point* pt_in, const lzq_aov_params* aov, const double* d_y, int64_t n, int32_t nz,
+                  double z_max, double* d_out, void* stream) {
+  if ((!pt_in && !aov) || n < 0 || (n > 0 && (!d_y || !d_out))) return fail(LZQ_EINVAL, "lzq_aov_batch: bad arguments");
   if (n == 0) return LZQ_OK;
+  // aov_kernel reads only the A/V kernel's fields of its point (quad_setup's pref0 / c)
+  lzq_point own;
+  if (pt_in) own = *pt_in;
+  else memset(&own, 0, sizeof(own));
+  if (aov) {
+    own.I_p = aov->I_p;
+    own.beta_over_H = aov->beta_over_H;
+    own.T_p_GeV = aov->T_p_GeV;
+    own.v_w = aov->v_w;
+    own.g_star = aov->g_star;
+  }
+  const lzq_point* pt = &own;
   int dev;
   DevZGrid g;
   int rc = zgrid_for(nz, z_max, g, &dev);
@@ -1365,7 +687,8 @@ int lzq_jchi_batch(const lzq_point* pt, const double* d_T, int64_t n, double* d_
 }
 
 int lzq_yields_batch(const lzq_point* d_points, int64_t n, int32_t n_y, int32_t nz, double z_max,
-                     const double* d_T_lo, const double* d_T_hi, const double* d_P, lzq_yield* d_out, void* stream) {
+                     const double* d_T_lo, const double* d_T_hi, const double* d_P, const lzq_aov_params* d_aov,
+                     lzq_yield* d_out, void* stream) {
   if (n < 0 || (n > 0 && (!d_points || !d_out))) return fail(LZQ_EINVAL, "lzq_yields_batch: bad arguments");
   if ((d_T_lo == nullptr) != (d_T_hi == nullptr))
     return fail(LZQ_EINVAL, "lzq_yields_batch: T_lo and T_hi must both be given or both be NULL");
@@ -1378,6 +701,9 @@ int lzq_yields_batch(const lzq_point* d_points, int64_t n, int32_t n_y, int32_t 
   if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_yields_batch: n too large");
   const int trunc = g.monotone ? g_truncate : 0;
   const hipStream_t s = (hipStream_t)stream;
+  if (d_aov)  // the A/V kernel's own parameters (lzq_aov.hip)
+    return lzq::launch_yields_points_aov(g_exp_variant, g.is_default, d_points, d_aov, n, n_y, d_T_lo, d_T_hi, d_P,
+                                         g.zt, g.nzp, exp_table(dev), d_out, trunc, s);
 #define LZQ_POINTS(EXPV, NZ)                                                                                        \
   hipLaunchKernelGGL((lzq::yields_points_kernel<lzq::kYB, EXPV, NZ>), dim3((unsigned)nb), dim3(lzq::kBlock), 0, s, \
                      d_points, n, n_y, d_T_lo, d_T_hi, d_P, g.zt, g.nzp, exp_table(dev), d_out, trunc)

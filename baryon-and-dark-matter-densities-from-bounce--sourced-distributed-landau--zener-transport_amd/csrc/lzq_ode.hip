@@ -1548,7 +1548,8 @@ int check_ws(int64_t n, const double* d_work, int64_t work_doubles, const char* 
 extern "C" {
 
 int lzq_ode_tables(const lzq_point* d_points, int64_t n, const double* d_T_lo, const double* d_T_hi, int32_t nt,
-                   int32_t nz, double z_max, double* d_work, int64_t work_doubles, int32_t* d_status, void* stream) {
+                   int32_t nz, double z_max, const lzq_aov_params* d_aov, double* d_work, int64_t work_doubles,
+                   int32_t* d_status, void* stream) {
   if (nt < 4 || nt > LZQ_ODE_NT_MAX) {
     char buf[128];
     snprintf(buf, sizeof(buf), "lzq_ode_tables: nt = %d knots outside [4, %d]", nt, LZQ_ODE_NT_MAX);
@@ -1561,7 +1562,7 @@ int lzq_ode_tables(const lzq_point* d_points, int64_t n, const double* d_T_lo, c
     return lzq_set_error(LZQ_EINVAL, "lzq_ode_tables: T_lo and T_hi must both be given or both be NULL");
   if (n == 0) return LZQ_OK;
   hipStream_t s = (hipStream_t)stream;
-  rc = lzq::launch_ode_aov_tables(d_points, n, d_T_lo, d_T_hi, nt, nz, z_max, d_work, s);
+  rc = lzq::launch_ode_aov_tables(d_points, n, d_T_lo, d_T_hi, nt, nz, z_max, d_aov, d_work, s);
   if (rc) return rc;
   hipLaunchKernelGGL(lzq::ode_spline_kernel, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, s, d_points, n,
                      nt, d_T_lo, d_T_hi, d_work, d_status);
@@ -1615,9 +1616,10 @@ int lzq_ode_quadrature(const lzq_point* d_points, const lzq_ode_params* d_ode, i
 }
 
 int lzq_ode_batch(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, int32_t nz, double z_max,
-                  double* d_work, int64_t work_doubles, int64_t max_steps, lzq_yield* d_out, int32_t* d_status,
-                  void* stream) {
-  int rc = lzq_ode_tables(d_points, n, nullptr, nullptr, LZQ_ODE_NT, nz, z_max, d_work, work_doubles, d_status, stream);
+                  const lzq_aov_params* d_aov, double* d_work, int64_t work_doubles, int64_t max_steps,
+                  lzq_yield* d_out, int32_t* d_status, void* stream) {
+  int rc = lzq_ode_tables(d_points, n, nullptr, nullptr, LZQ_ODE_NT, nz, z_max, d_aov, d_work, work_doubles, d_status,
+                          stream);
   if (rc) return rc;
   return lzq_ode_integrate(d_points, d_ode, n, d_work, work_doubles, max_steps, d_out, d_status, stream);
 }

@@ -14,7 +14,7 @@ import torch
 import logging
 
 from . import _native
-from .config import to_ctypes_ode, to_ctypes_point, to_point
+from .config import to_aov, to_ctypes_aov, to_ctypes_ode, to_ctypes_point, to_point
 
 _log = logging.getLogger("lzq")
 
@@ -101,15 +101,35 @@ class Engine:
         """lzq_point records (numpy POINT_DTYPE array) -> device byte tensor."""
         return _to_device_bytes(np.ascontiguousarray(recs, dtype=_native.POINT_DTYPE), self.device)
 
+    def aov_to_device(self, aov, n: int) -> Optional[torch.Tensor]:
+        """The A/V kernels of n points (include/lzq.h lzq_aov_params) as a device byte tensor, or
+        None.  aov: None (each point's own fields, fpy:197), one kernel for every point (an
+        AoverVKernel, a dict or Config, or a 1-record AOV_DTYPE array), or n AOV_DTYPE records."""
+        if aov is None:
+            return None
+        if isinstance(aov, torch.Tensor):
+            if aov.numel() != n * _native.AOV_DTYPE.itemsize:
+                raise ValueError("aov: need one lzq_aov_params record per point")
+            return aov
+        rec = aov if isinstance(aov, np.ndarray) and aov.dtype == _native.AOV_DTYPE else to_aov(aov)
+        rec = np.ascontiguousarray(rec, dtype=_native.AOV_DTYPE).reshape(-1)
+        if rec.size == 1 and n != 1:
+            rec = np.repeat(rec, n)
+        if rec.size != n:
+            raise ValueError(f"aov: {rec.size} records for {n} points")
+        return _to_device_bytes(rec, self.device)
+
     # -- fpy:158-165 -----------------------------------------------------------------------
-    def aov(self, cfg, ys, nz: int = _native.LZQ_NZ, z_max: float = _native.LZQ_Z_MAX) -> torch.Tensor:
-        """A_over_V_y at every y for the kernel AoverVKernel(..., z_max, nz) of cfg (fpy:141-165)."""
+    def aov(self, kernel, ys, nz: int = _native.LZQ_NZ, z_max: float = _native.LZQ_Z_MAX) -> torch.Tensor:
+        """A_over_V_y at every y for the kernel AoverVKernel(I_p, beta_over_H, T_p, v_w, g_star, z_max, nz)
+        (fpy:141-165); kernel: an AoverVKernel, or a Config / fpy-schema dict (the kernel main() builds
+        from it, fpy:197)."""
         nz, z_max = _native.zgrid(nz, z_max)
         y = self._f64(ys).reshape(-1)
         out = torch.empty_like(y)
-        p = to_ctypes_point(to_point(cfg, P=0.0))
+        a = to_ctypes_aov(to_aov(kernel))
         with torch.cuda.device(self.device):
-            self._check(self.lib.lzq_aov_batch(ctypes.byref(p), _vp(y), y.numel(), nz, z_max, _vp(out),
+            self._check(self.lib.lzq_aov_batch(None, ctypes.byref(a), _vp(y), y.numel(), nz, z_max, _vp(out),
                                                self._stream()))
         return out
 
@@ -124,22 +144,26 @@ class Engine:
 
     # -- fpy:231-267 + epilogue ----------------------------------------------------------------
     def yields(self, points, n_y: int = 8000, T_lo=None, T_hi=None, P=None, reuse: bool = False,
-               nz: int = _native.LZQ_NZ, z_max: float = _native.LZQ_Z_MAX) -> torch.Tensor:
+               nz: int = _native.LZQ_NZ, z_max: float = _native.LZQ_Z_MAX, aov=None) -> torch.Tensor:
         """points: POINT_DTYPE numpy array or a device byte tensor from points_to_device.
         Returns (n, 6) float64 device tensor in YIELD_FIELDS order.
         reuse: lzq_yields_batch_reuse -- points equal in _native.ZSUM_KEY share one table of
         z-sums (bit-identical; not the dense headline path).  Used only with main()'s window
         and when points do share; otherwise the dense path.
-        nz, z_max: the A/V kernel's z grid (AoverVKernel(..., z_max, nz), fpy:141-156)."""
+        nz, z_max: the A/V kernel's z grid (AoverVKernel(..., z_max, nz), fpy:141-156).
+        aov: the A/V kernel's own parameters when it is not the points' own (bs.aov replaced,
+        fpy:261; see aov_to_device); such batches run the dense kernels (no reuse)."""
         nz, z_max = _native.zgrid(nz, z_max)
         d_pts = points if isinstance(points, torch.Tensor) else self.points_to_device(points)
         n = d_pts.numel() // _native.POINT_DTYPE.itemsize
+        d_aov = self.aov_to_device(aov, n)
         out = torch.empty((n, 6), dtype=torch.float64, device=self.device)
         tl = None if T_lo is None else self._f64(T_lo)
         th = None if T_hi is None else self._f64(T_hi)
         Pv = None if P is None else self._f64(P)
         with torch.cuda.device(self.device):
-            groups = table_groups(d_pts, n, _ZSUM_WORDS) if reuse and tl is None and th is None else None
+            groups = table_groups(d_pts, n, _ZSUM_WORDS) if reuse and tl is None and th is None and d_aov is None \
+                else None
             stride = max(int(n_y), 2000) + _native.REUSE_TABLE_HEADER
             if groups is not None and groups[0].numel() * stride * 8 <= REUSE_MAX_BYTES:
                 rep, inv = groups
@@ -154,7 +178,8 @@ class Engine:
                 self._keepalive_reuse = (rep, idx, d_pts)
             else:
                 self._check(self.lib.lzq_yields_batch(_vp(d_pts), n, int(n_y), nz, z_max, _vp(tl), _vp(th), _vp(Pv),
-                                                        _vp(out), self._stream()))
+                                                        _vp(d_aov), _vp(out), self._stream()))
+                self._keepalive_aov = d_aov
         return out
 
     # -- grid sweep ----------------------------------------------------------------------------
@@ -229,25 +254,28 @@ class Engine:
         return torch.empty(n * 4 * int(nt), dtype=torch.float64, device=self.device)
 
     def ode_tables(self, points, T_lo=None, T_hi=None, work: Optional[torch.Tensor] = None, nt: int = _native.ODE_NT,
-                   nz: int = _native.LZQ_NZ, z_max: float = _native.LZQ_Z_MAX) -> tuple:
+                   nz: int = _native.LZQ_NZ, z_max: float = _native.LZQ_Z_MAX, aov=None) -> tuple:
         """BoltzmannSystem.build_tables(T_lo, T_hi, n=nt) for each point (window T_lo/T_hi per
-        point, or main()'s window) with the A/V kernel's z grid (nz, z_max): returns the (n * 4 nt)
+        point, or main()'s window) with the A/V kernel's z grid (nz, z_max) and, if given, its own
+        parameters `aov` (aov_to_device; y(T) stays the point's, fpy:211): returns the (n * 4 nt)
         spline workspace and the int32 status."""
         nz, z_max = _native.zgrid(nz, z_max)
         d_pts = points if isinstance(points, torch.Tensor) else self.points_to_device(points)
         n = d_pts.numel() // _native.POINT_DTYPE.itemsize
+        d_aov = self.aov_to_device(aov, n)
         work = self.ode_workspace(n, nt) if work is None else work
         tl = None if T_lo is None else self._f64(T_lo).reshape(-1)
         th = None if T_hi is None else self._f64(T_hi).reshape(-1)
         status = torch.zeros(n, dtype=torch.int32, device=self.device)
         with torch.cuda.device(self.device):
-            self._check(self.lib.lzq_ode_tables(_vp(d_pts), n, _vp(tl), _vp(th), int(nt), nz, z_max, _vp(work),
-                                                work.numel(), _vp(status), self._stream()))
+            self._check(self.lib.lzq_ode_tables(_vp(d_pts), n, _vp(tl), _vp(th), int(nt), nz, z_max, _vp(d_aov),
+                                                _vp(work), work.numel(), _vp(status), self._stream()))
+        self._keepalive_aov = d_aov
         return work, status
 
     def ode(self, points, ode_params, max_steps: Optional[int] = None, chunk: int = 1 << 18,
             share_tables: bool = True, method: str = "radau", group_waves: bool = True, nz: int = _native.LZQ_NZ,
-            z_max: float = _native.LZQ_Z_MAX) -> tuple:
+            z_max: float = _native.LZQ_Z_MAX, aov=None) -> tuple:
         """fpy:385-417 for n points (POINT_DTYPE records + ODE_DTYPE records): (n, 6) yields
         table and (n,) int32 status (enum lzq_ode_status), both on the device.  Points are
         processed in chunks so that the spline workspace stays <= chunk * 25.6 KB (6.7 GB at the
@@ -267,7 +295,10 @@ class Engine:
         sweeps pass sweep.ODE_MAX_STEPS).  None (default): the batch's own largest step count
         (ode_step_counts), i.e. every window the reference accepts is integrated, however long
         (fpy:403-407): the library runs it as continuation launches of <= 2^24 steps.
-        nz, z_max: the z grid of the A/V kernel behind the spline tables (fpy:141-156, 207-212)."""
+        nz, z_max: the z grid of the A/V kernel behind the spline tables (fpy:141-156, 207-212).
+        aov: the A/V kernel's own parameters behind each point's spline table when it is not the
+        point's own (bs.aov replaced before build_tables, fpy:211; see aov_to_device); the tables are
+        then built per point (no sharing)."""
         nz, z_max = _native.zgrid(nz, z_max)
         if method not in ("radau", "quadrature"):
             raise ValueError(f"method must be 'radau' or 'quadrature', got {method!r}")
@@ -278,6 +309,9 @@ class Engine:
         n = pts.size
         d_pts_all = self.points_to_device(pts)
         d_ode_all = _to_device_bytes(ods, self.device)
+        d_aov_all = self.aov_to_device(aov, n)
+        if d_aov_all is not None:
+            share_tables = False   # a table's key now includes the block (ODE_TABLE_KEY does not)
         # the launches cover the batch's own largest step count (or the cap, when a point needs more:
         # those points come back LZQ_ODE_TOO_MANY_STEPS), not the cap itself
         need = ode_step_counts_device(d_pts_all, n)   # same values as ode_step_counts, on the device
@@ -289,6 +323,8 @@ class Engine:
         if order is not None:
             d_pts_all = d_pts_all.view(n, -1)[order].contiguous().view(-1)
             d_ode_all = d_ode_all.view(n, -1)[order].contiguous().view(-1)
+            if d_aov_all is not None:
+                d_aov_all = d_aov_all.view(n, -1)[order].contiguous().view(-1)
         rp, ro = _native.POINT_DTYPE.itemsize, _native.ODE_DTYPE.itemsize
         out = torch.empty((n, 6), dtype=torch.float64, device=self.device)
         status = torch.zeros(n, dtype=torch.int32, device=self.device)
@@ -300,6 +336,8 @@ class Engine:
             c1 = min(n, c0 + chunk)
             d_pts = d_pts_all[c0 * rp:c1 * rp]
             d_ode = d_ode_all[c0 * ro:c1 * ro]
+            ra = _native.AOV_DTYPE.itemsize
+            d_aov = None if d_aov_all is None else d_aov_all[c0 * ra:c1 * ra]
             rep = table_groups(d_pts, c1 - c0) if share_tables else None
             d_rep = d_idx = None
             if rep is not None:
@@ -316,8 +354,8 @@ class Engine:
                         "table per point (an A/V z-sum table build each; the integration still shares stage rows "
                         "across tables) -- ~2.6x the cost per point of a shared-table sweep on a 20000-step "
                         "window (DESIGN §5.3)", c1 - c0, c1 - c0, ", ".join(_native.ODE_TABLE_KEY))
-            plan.append((c0, c1, d_pts, d_ode, d_rep, d_idx, n_tab))
-            keep.append((d_pts, d_ode, d_rep, d_idx))
+            plan.append((c0, c1, d_pts, d_ode, d_rep, d_idx, n_tab, d_aov))
+            keep.append((d_pts, d_ode, d_rep, d_idx, d_aov))
         # Two or more chunks: chunk c + 1's spline tables are built on a side stream into the other
         # of two workspaces while chunk c integrates (the table kernels fill the SIMDs the
         # integrator's tail leaves idle); events order each workspace's reuse.  One chunk: one stream.
@@ -337,15 +375,15 @@ class Engine:
         freed = [None] * len(works)
         nt = _native.ODE_NT
         with torch.cuda.device(self.device):
-            for ci, (c0, c1, d_pts, d_ode, d_rep, d_idx, n_tab) in enumerate(plan):
+            for ci, (c0, c1, d_pts, d_ode, d_rep, d_idx, n_tab, d_aov) in enumerate(plan):
                 b = ci % len(works)
                 work = works[b]
                 with torch.cuda.stream(side):
                     if freed[b] is not None:
                         side.wait_event(freed[b])
                     src = d_pts if d_rep is None else d_rep
-                    self._check(self.lib.lzq_ode_tables(_vp(src), n_tab, None, None, nt, nz, z_max, _vp(work),
-                                                        work.numel(),
+                    self._check(self.lib.lzq_ode_tables(_vp(src), n_tab, None, None, nt, nz, z_max,
+                                                        _vp(d_aov if d_rep is None else None), _vp(work), work.numel(),
                                                         _vp(status[c0:c1]) if d_rep is None and method == "radau"
                                                         else None,
                                                         self._stream()))

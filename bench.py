@@ -14,7 +14,7 @@ all-gathered over RCCL at the end of every step (north_star (3)).
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 Prints one JSON line (rank 0).  `roofline` = the kernel's executed FP64 FLOP (PMC
-instruction mix of profiles/round4, used only if that profile's code-object sha256 is the timed
+instruction mix of profiles/round4, used only if that profile's kernel code hash is the timed
 library's) over its HIP-event time in this run, against the 78.6 TFLOP/s FP64 vector peak, with
 the FP64-pipe and VALU issue fractions beside it; `kernel_ms` / `allgather_ms` decompose a step
 per rank (min / max / mean); `parity_spot` checks 64 rows of the last timed step's table against
@@ -66,11 +66,15 @@ def _pmc():
         return None
 
 
-def timed_code_object() -> str | None:
-    """sha256 of the gfx950 code object holding yields_grid_kernel in the library this process
-    loaded (the one being timed)."""
+def timed_code_object() -> tuple[str | None, str | None]:
+    """(kernel code sha256, whole code object sha256) of the gfx950 code object holding
+    yields_grid_kernel in the library this process loaded (the one being timed).  The first hashes
+    what the GPU executes (.text, kernel descriptors, metadata note: codeobj.kernel_code_sha256), so
+    it survives a rebuild with another command line; the second also covers clang's per-build
+    __hip_cuid symbol."""
     native = importlib.import_module(PKG + "._native")
-    return importlib.import_module(PKG + ".codeobj").kernel_object_sha256(native.LIB_PATH)
+    co = importlib.import_module(PKG + ".codeobj")
+    return co.kernel_code_sha256(native.LIB_PATH), co.kernel_object_sha256(native.LIB_PATH)
 
 
 def roofline(points_per_launch: int, kern_ms: float) -> dict:
@@ -84,7 +88,7 @@ def roofline(points_per_launch: int, kern_ms: float) -> dict:
     cycles each -- the issue rate the peak is defined by -- over the SIMD cycles of this run at
     the profile's clock), and SURVEY §8d's 30-FLOP stock-exp pricing as a secondary figure."""
     d = _pmc()
-    sha = timed_code_object()
+    code, sha = timed_code_object()
     stock = FLOP_PER_POINT * points_per_launch / (kern_ms / 1e3) / 1e12
     out = {"bound": "fp64-valu", "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s", "kernel": "yields_grid_kernel",
            "kernel_ms": kern_ms, "algorithmic_bytes": 48.0 * points_per_launch,
@@ -93,16 +97,20 @@ def roofline(points_per_launch: int, kern_ms: float) -> dict:
                                             "the table exponential does the node in ~10 executed FLOP, so this "
                                             "figure exceeds the peak and is NOT a roofline fraction"}}
     out["code_object_sha256"] = sha
+    out["kernel_code_sha256"] = code
     if d is None or "valu_mix_per_wave_node" not in d:
         out.update(achieved=None, frac=None, traffic=None,
                    note=f"no PMC summary at {os.path.relpath(PMC_SUMMARY, ROOT)}: executed FLOP unknown")
         return out
-    if d.get("code_object_sha256") != sha:
+    same = d.get("kernel_code_sha256") == code if d.get("kernel_code_sha256") else d.get("code_object_sha256") == sha
+    if not same:
         # the counters describe another build of the kernel: no fraction rather than a stale one
         out.update(achieved=None, frac=None, fp64_pipe_busy_frac=None, traffic=None,
                    profile_code_object_sha256=d.get("code_object_sha256"),
-                   note=f"stale profile: {os.path.relpath(PMC_SUMMARY, ROOT)} was measured on code object "
-                        f"{d.get('code_object_sha256')}, this run timed {sha}; re-run tools/gpu.sh profile ROUND")
+                   profile_kernel_code_sha256=d.get("kernel_code_sha256"),
+                   note=f"stale profile: {os.path.relpath(PMC_SUMMARY, ROOT)} was measured on kernel code "
+                        f"{d.get('kernel_code_sha256') or d.get('code_object_sha256')}, this run timed {code}; "
+                        f"re-run tools/gpu.sh profile ROUND")
         return out
     mix = d["valu_mix_per_wave_node"]
     flop_wn = 64.0 * (2.0 * mix["fma_f64"] + mix["mul_f64"] + mix["add_f64"])
@@ -119,6 +127,7 @@ def roofline(points_per_launch: int, kern_ms: float) -> dict:
         "fp64_pipe_busy_frac": 4.0 * fp64_wn / cyc_wn,
         "valu_issue_busy_frac": (4.0 * fp64_wn + 2.0 * other_wn) / cyc_wn,
         "profile_code_object_sha256": d["code_object_sha256"],
+        "profile_kernel_code_sha256": d.get("kernel_code_sha256"),
         "flop_per_point_executed": flop_pt,
         "traffic": d["hbm_bytes_per_point"]["total_upper"] * points_per_launch, "traffic_unit": "bytes/launch",
         # north_star: "achieved HBM GB/s for the grid I/O" -- the path is FP64-bound, so this is small
@@ -136,7 +145,8 @@ def roofline(points_per_launch: int, kern_ms: float) -> dict:
                 "(DESIGN.md §5.1). fp64_pipe_busy_frac counts every FP64 instruction as a full slot; "
                 "valu_issue_busy_frac adds the other VALU instructions at 2 cycles: the kernel is at its "
                 "formulation's issue ceiling, so the lever left is instruction count. The counters are "
-                "used only when their profile's code-object hash equals the timed library's"})
+                "used only when their profile's kernel code hash (machine code + descriptors + metadata "
+                "of the code object, codeobj.kernel_code_sha256) equals the timed library's"})
     return out
 
 

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define LZQ_ABI_VERSION 2
+#define LZQ_ABI_VERSION 3   /* 3: optional lzq_aov_params on the A/V-evaluating entry points */
 #define LZQ_NZ 1200          /* fpy:142 nz default, used unchanged at fpy:197 */
 #define LZQ_Z_MAX 30.0       /* fpy:142 z_max default */
 #define LZQ_NZ_MAX (1 << 22) /* largest z grid accepted (64 MB of device nodes) */
@@ -79,6 +79,21 @@ typedef struct lzq_point {
   int32_t has_n_chi_at_Tp;
 } lzq_point;
 
+/* The A/V kernel's own parameters: AoverVKernel(I_p, beta_over_H, T_p, v_w, g_star, z_max, nz)
+ * (fpy:141-151).  BoltzmannSystem builds self.aov from cfg (fpy:197), but it is a separate public
+ * object: integrate_YB_by_quadrature (fpy:261), build_tables (fpy:211) and S_B_T (fpy:228) take
+ * A/V from self.aov while the y-grid, T(y), H, s, J and window come from self.cfg (fpy:234-262).
+ * Entry points that take an optional lzq_aov_params block use it for the A/V constants
+ * pref0 = (I_p/2)(beta/max(v_w, 1e-12)), beta = beta_over_H H_std(T_p, g_star), and c = -I_p/6
+ * (fpy:146-151, 162-163); NULL = the point's own fields (self.aov built from cfg).  40 bytes. */
+typedef struct lzq_aov_params {
+  double I_p;          /* fpy:143 */
+  double beta_over_H;  /* fpy:144 */
+  double T_p_GeV;      /* fpy:145 (AoverVKernel's T_p) */
+  double v_w;          /* fpy:146 (max(., 1e-12) applied) */
+  double g_star;       /* fpy:147 */
+} lzq_aov_params;
+
 /* Per-point yield record: the `final` block of yields_out.json (fpy:425-427) + P_used
  * (fpy:424).  48 bytes; tables of these are what the multi-GPU all-gather moves. */
 typedef struct lzq_yield {
@@ -114,10 +129,13 @@ const char* lzq_last_error(void);
  * of fpy:156 verbatim, the trapezoid of fpy:164.  (LZQ_NZ, LZQ_Z_MAX) is the grid main() uses
  * (fpy:197) and runs the compile-time-sized headline kernels; any other grid is built on the
  * host and uploaded once per (device, nz, z_max) on first use (a synchronous copy), then kept.
- * 0 <= nz <= LZQ_NZ_MAX and 0 <= z_max < inf (numpy accepts the same; nz < 0 is its ValueError);
- * nz <= 1 or z_max = 0 give A/V = 0 exactly, as numpy's trapezoid of <= 1 node / zero width does.
- * A grid so fine that the cancelling gamma4 rounds below 0 (z_1 below ~3e-4, i.e. nz > ~1e5 on
- * [0, 30]) is refused with LZQ_EINVAL: the reference then exponentiates positive arguments. */
+ * 0 <= nz <= LZQ_NZ_MAX (nz < 0 is numpy's ValueError) and 0 <= z_max < inf; nz <= 1 or z_max = 0
+ * give A/V = 0 exactly, as numpy's trapezoid of <= 1 node / zero width does.  Refused with
+ * LZQ_EINVAL although numpy accepts them (documented parity gaps):
+ *   - z_max < 0: linspace(0, z_max, nz) runs backwards and the trapezoid of fpy:164 changes sign;
+ *   - a grid so fine that the cancelling gamma4 of fpy:156 rounds below 0 (the reference then
+ *     exponentiates positive arguments) or stops being non-decreasing (rounding noise of a few ulp
+ *     of 6.0 at the first nodes): z_1 below ~1e-3, i.e. nz >~ 2e4 on [0, 1] or >~ 1e5 on [0, 30]. */
 /* Builds and uploads the default z tables (fpy:154-156) and the exp table for `device`.  Called
  * lazily by every entry point; call it up front before capturing launches into a graph. */
 int lzq_init(int device);
@@ -157,10 +175,11 @@ enum lzq_exp_variant { LZQ_EXP_POLY11 = 0, LZQ_EXP_TABLE = 1 };
 int lzq_tune(int32_t key, int32_t value);
 
 /* ---- hot path -------------------------------------------------------------------------- */
-/* fpy:158-165: out[i] = A_over_V_y(y[i]) for the kernel AoverVKernel(I_p, beta_over_H, T_p_GeV, v_w,
- * g_star, z_max, nz) of point *pt (host struct). */
-int lzq_aov_batch(const lzq_point* pt, const double* d_y, int64_t n, int32_t nz, double z_max, double* d_out,
-                  void* stream);
+/* fpy:158-165: out[i] = A_over_V_y(y[i]) for the kernel AoverVKernel(I_p, beta_over_H, T_p, v_w,
+ * g_star, z_max, nz): aov (host struct) if non-NULL, else point *pt's fields (pt may then be NULL
+ * only if aov is not; no other field of *pt is read). */
+int lzq_aov_batch(const lzq_point* pt, const lzq_aov_params* aov, const double* d_y, int64_t n, int32_t nz,
+                  double z_max, double* d_out, void* stream);
 
 /* fpy:222-223: out[i] = BoltzmannSystem.J_chi(T[i]) for point *pt (diagnostics table). */
 int lzq_jchi_batch(const lzq_point* pt, const double* d_T, int64_t n, double* d_out, void* stream);
@@ -171,9 +190,10 @@ int lzq_jchi_batch(const lzq_point* pt, const double* d_T, int64_t n, double* d_
  * d_P: optional per-point P override (NULL: point.P_chi_to_B), e.g. lzq_lz_propagate output.
  * n_y: y-grid size as passed to integrate_YB_by_quadrature (fpy:374 uses 8000; raised to
  * LZQ_NY_MIN as fpy:246).  (nz, z_max): the A/V kernel's z grid (fpy:141-142; main(): LZQ_NZ,
- * LZQ_Z_MAX). */
+ * LZQ_Z_MAX).  d_aov: optional [n] device lzq_aov_params, point i's A/V kernel (bs.aov replaced,
+ * fpy:261); NULL = each point's own fields (fpy:197), the headline kernels. */
 int lzq_yields_batch(const lzq_point* d_points, int64_t n, int32_t n_y, int32_t nz, double z_max,
-                     const double* d_T_lo, const double* d_T_hi, const double* d_P,
+                     const double* d_T_lo, const double* d_T_hi, const double* d_P, const lzq_aov_params* d_aov,
                      lzq_yield* d_out, void* stream);
 
 /* Cartesian sweep: points [start, start+count) of the grid base x axes[0] x ... x
@@ -257,9 +277,12 @@ enum lzq_ode_status {
  * and its not-a-knot cubic spline (scipy CubicSpline), into d_work[i * 4 nt ...] (work_doubles >=
  * n * 4 nt; 4 <= nt <= LZQ_ODE_NT_MAX).  The integrators (lzq_ode_integrate*, lzq_ode_quadrature)
  * read tables of nt = LZQ_ODE_NT knots, main()'s build_tables (fpy:387), on any z grid.
- * d_status (optional, [n] int32): LZQ_ODE_BAD_GRID for a window CubicSpline rejects. */
+ * d_status (optional, [n] int32): LZQ_ODE_BAD_GRID for a window CubicSpline rejects.  d_aov:
+ * optional [n] device lzq_aov_params, the A/V kernel of each point's table (bs.aov replaced:
+ * y(T) from the point, A/V from the block, fpy:211); NULL = the point's own fields. */
 int lzq_ode_tables(const lzq_point* d_points, int64_t n, const double* d_T_lo, const double* d_T_hi, int32_t nt,
-                   int32_t nz, double z_max, double* d_work, int64_t work_doubles, int32_t* d_status, void* stream);
+                   int32_t nz, double z_max, const lzq_aov_params* d_aov, double* d_work, int64_t work_doubles,
+                   int32_t* d_status, void* stream);
 
 /* fpy:385-417 on built tables: Y_chi(x1), Y_B(x1) of rhs (fpy:270-286) from x0 = m/T_hi to
  * x1 = m/max(T_lo, 1e-30), Y(x0) = (Y_chi0 of fpy:389-399, 0), by the reference's method
@@ -303,11 +326,11 @@ int lzq_ode_quadrature(const lzq_point* d_points, const lzq_ode_params* d_ode, i
                        const int32_t* d_table_index, int64_t n_tables, const double* d_work, int64_t work_doubles,
                        int64_t max_steps, lzq_yield* d_out, int32_t* d_status, void* stream);
 
-/* lzq_ode_tables (nt = LZQ_ODE_NT, main()'s window, the z grid (nz, z_max)) + lzq_ode_integrate
- * (d_status may be NULL). */
+/* lzq_ode_tables (nt = LZQ_ODE_NT, main()'s window, the z grid (nz, z_max), d_aov as there) +
+ * lzq_ode_integrate (d_status may be NULL). */
 int lzq_ode_batch(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, int32_t nz, double z_max,
-                  double* d_work, int64_t work_doubles, int64_t max_steps, lzq_yield* d_out, int32_t* d_status,
-                  void* stream);
+                  const lzq_aov_params* d_aov, double* d_work, int64_t work_doubles, int64_t max_steps,
+                  lzq_yield* d_out, int32_t* d_status, void* stream);
 
 /* BoltzmannSystem.A_over_V_T (fpy:214-218) and .rhs (fpy:270-286) of ONE point (host structs)
  * whose nt-knot tables for the window (T_lo, T_hi) are at d_work_point (4 nt doubles, from

@@ -149,13 +149,15 @@ static void ztab_free(ztab_t* t) {
   free(t->g4);
 }
 
+/* Double-checked initialisation with acquire/release on the flag: a thread that sees it set
+ * also sees the table's pointers and contents (oracle_points_batch calls this from OpenMP). */
 static void ztab_init(void) {
-  if (g_ztab_ready) return;
+  if (__atomic_load_n(&g_ztab_ready, __ATOMIC_ACQUIRE)) return;
 #pragma omp critical(lzq_oracle_ztab)
   {
-    if (!g_ztab_ready) {
+    if (!__atomic_load_n(&g_ztab_ready, __ATOMIC_ACQUIRE)) {
       ztab_build(&g_ztab, ORACLE_NZ, ORACLE_ZMAX);
-      g_ztab_ready = 1;
+      __atomic_store_n(&g_ztab_ready, 1, __ATOMIC_RELEASE);
     }
   }
 }
@@ -184,6 +186,13 @@ static aov_t aov_make(double I_p, double B, double T_p, double v_w, double g_sta
   double H_p = H_std(T_p, g_star);
   a.beta = B * H_p;
   return a;
+}
+
+/* The kernel of BoltzmannSystem.aov: its own parameters if given (bs.aov replaced, fpy:141-151),
+ * else the one fpy:197 builds from the point (cfg). */
+static aov_t aov_of(const oracle_point* p, const oracle_aov_params* av) {
+  if (av) return aov_make(av->I_p, av->beta_over_H, av->T_p_GeV, av->v_w, av->g_star);
+  return aov_make(p->I_p, p->beta_over_H, p->T_p_GeV, p->v_w, p->g_star);
 }
 
 /* f, scratch: >= max(nz, 1) doubles.  np.trapezoid of fewer than 2 nodes is 0.0. */
@@ -217,7 +226,8 @@ double oracle_aov(double I_p, double B, double T_p, double v_w, double g_star, d
 }
 
 /* fpy:231-267 integrate_YB_by_quadrature, A/V on the grid zt */
-static double yb_quadrature(const oracle_point* p, const ztab_t* zt, double T_lo, double T_hi, int32_t n_y) {
+static double yb_quadrature(const oracle_point* p, const oracle_aov_params* av, const ztab_t* zt, double T_lo, double T_hi,
+                            int32_t n_y) {
   double B = p->beta_over_H, Tp = p->T_p_GeV, m = p->m_chi_GeV;
   double y_lo_raw = y_of_T(T_hi, Tp, B);
   double y_hi_raw = y_of_T(T_lo, Tp, B);
@@ -232,7 +242,7 @@ static double yb_quadrature(const oracle_point* p, const ztab_t* zt, double T_lo
   double* f = (double*)malloc(sizeof(double) * (size_t)(zt->nz > 1 ? zt->nz : 1));
   oracle_linspace(y_lo, y_hi, n, ys);
 
-  aov_t a = aov_make(p->I_p, B, Tp, p->v_w, p->g_star);
+  aov_t a = aov_of(p, av); /* fpy:261: self.aov; everything else from self.cfg (fpy:250-262) */
   double Bc = pymax(B, 1e-30);
   double sig = pymax(p->source_shape_sigma_y, 1e-6);
   double sqrtg = sqrt(p->g_star);
@@ -263,7 +273,16 @@ double oracle_yb_quadrature_z(const oracle_point* p, double T_lo, double T_hi, i
                               double z_max) {
   ztab_t own;
   const ztab_t* zt = ztab_get(nz, z_max, &own);
-  double r = yb_quadrature(p, zt, T_lo, T_hi, n_y);
+  double r = yb_quadrature(p, NULL, zt, T_lo, T_hi, n_y);
+  ztab_put(zt);
+  return r;
+}
+
+double oracle_yb_quadrature_a(const oracle_point* p, const oracle_aov_params* av, double T_lo, double T_hi, int32_t n_y,
+                              int64_t nz, double z_max) {
+  ztab_t own;
+  const ztab_t* zt = ztab_get(nz, z_max, &own);
+  double r = yb_quadrature(p, av, zt, T_lo, T_hi, n_y);
   ztab_put(zt);
   return r;
 }
@@ -273,11 +292,11 @@ double oracle_yb_quadrature(const oracle_point* p, double T_lo, double T_hi, int
 }
 
 /* fpy:361-417 (fast path only: the callers gate on fpy:372). */
-static int point_yields(const oracle_point* p, const ztab_t* zt, oracle_yield* o) {
+static int point_yields(const oracle_point* p, const oracle_aov_params* av, const ztab_t* zt, oracle_yield* o) {
   double T_p = p->T_p_GeV;
   double T_hi = p->T_max_over_Tp * T_p;
   double T_lo = p->T_min_over_Tp * T_p;
-  double YB = yb_quadrature(p, zt, T_lo, T_hi, 8000);
+  double YB = yb_quadrature(p, av, zt, T_lo, T_hi, 8000);
   double Ychi;
   if (p->regime == 0) {
     Ychi = n_chi_eq(T_hi, p->m_chi_GeV, p->g_chi, p->stats) / s_entropy(T_hi, p->g_star_s);
@@ -303,7 +322,15 @@ static int point_yields(const oracle_point* p, const ztab_t* zt, oracle_yield* o
 int oracle_point_yields_z(const oracle_point* p, int64_t nz, double z_max, oracle_yield* o) {
   ztab_t own;
   const ztab_t* zt = ztab_get(nz, z_max, &own);
-  int r = point_yields(p, zt, o);
+  int r = point_yields(p, NULL, zt, o);
+  ztab_put(zt);
+  return r;
+}
+
+int oracle_point_yields_a(const oracle_point* p, const oracle_aov_params* av, int64_t nz, double z_max, oracle_yield* o) {
+  ztab_t own;
+  const ztab_t* zt = ztab_get(nz, z_max, &own);
+  int r = point_yields(p, av, zt, o);
   ztab_put(zt);
   return r;
 }
@@ -324,7 +351,7 @@ int64_t oracle_points_batch_z(const oracle_point* p, int64_t n, int64_t nz, doub
 #endif
 #pragma omp parallel for schedule(dynamic, 1) reduction(+ : bad)
   for (int64_t i = 0; i < n; i++) {
-    if (point_yields(&p[i], zt, &out[i]) != 0) {
+    if (point_yields(&p[i], NULL, zt, &out[i]) != 0) {
       bad++;
       memset(&out[i], 0xff, sizeof(oracle_yield)); /* NaN pattern */
     }
@@ -404,7 +431,8 @@ static void spline_notaknot(const double* x, const double* y, int n, double* coe
 }
 
 /* build_tables(T_lo, T_hi, n=nt) with self.aov on the grid zt. */
-static int ode_tables(const oracle_point* p, const ztab_t* zt, double T_lo, double T_hi, int nt, double* coef) {
+static int ode_tables(const oracle_point* p, const oracle_aov_params* av, const ztab_t* zt, double T_lo, double T_hi, int nt,
+                      double* coef) {
   size_t nzb = (size_t)(zt->nz > 1 ? zt->nz : 1);
   double* Ts = (double*)malloc(sizeof(double) * 2 * (size_t)nt);
   double* Av = Ts + nt;
@@ -415,7 +443,7 @@ static int ode_tables(const oracle_point* p, const ztab_t* zt, double T_lo, doub
   for (int k = 0; k + 1 < nt; k++)
     if (!(Ts[k + 1] > Ts[k])) rc = -1; /* CubicSpline: `x` must be strictly increasing */
   if (rc == 0) {
-    aov_t a = aov_make(p->I_p, p->beta_over_H, p->T_p_GeV, p->v_w, p->g_star);
+    aov_t a = aov_of(p, av); /* fpy:211: A/V from self.aov, y(T) from self.cfg */
     for (int k = 0; k < nt; k++) {
       double y = y_of_T(Ts[k], p->T_p_GeV, p->beta_over_H);
       Av[k] = pymax(aov_eval(&a, zt, y, f, scratch), 0.0); /* np.maximum(Av, 0.0) */
@@ -432,7 +460,17 @@ int oracle_ode_tables_z(const oracle_point* p, double T_lo, double T_hi, int32_t
   if (nt < 4) return -2;
   ztab_t own;
   const ztab_t* zt = ztab_get(nz, z_max, &own);
-  int rc = ode_tables(p, zt, T_lo, T_hi, nt, coef);
+  int rc = ode_tables(p, NULL, zt, T_lo, T_hi, nt, coef);
+  ztab_put(zt);
+  return rc;
+}
+
+int oracle_ode_tables_a(const oracle_point* p, const oracle_aov_params* av, double T_lo, double T_hi, int32_t nt, int64_t nz,
+                        double z_max, double* coef) {
+  if (nt < 4) return -2;
+  ztab_t own;
+  const ztab_t* zt = ztab_get(nz, z_max, &own);
+  int rc = ode_tables(p, av, zt, T_lo, T_hi, nt, coef);
   ztab_put(zt);
   return rc;
 }
@@ -599,15 +637,15 @@ static int radau_step(const ode_ctx* c, const double C[3], const double A[3][3],
 
 /* fpy:361-417 for a point on the ODE path; status 0 ok, 1 bad T grid (CubicSpline raises),
  * 2 max_step <= 0 (solve_ivp raises), 3 more than max_steps steps, 4 Newton failure. */
-static int ode_point(const oracle_point* p, const oracle_ode* o, const ztab_t* zt, int64_t max_steps,
-                     oracle_yield* out, int64_t* n_steps) {
+static int ode_point(const oracle_point* p, const oracle_ode* o, const oracle_aov_params* av, const ztab_t* zt,
+                     int64_t max_steps, oracle_yield* out, int64_t* n_steps) {
   double T_p = p->T_p_GeV, m = p->m_chi_GeV;
   double T_hi = p->T_max_over_Tp * T_p, T_lo = p->T_min_over_Tp * T_p;
   double* coef = (double*)malloc(sizeof(double) * 4 * ODE_NT);
   int st = 0;
   *n_steps = 0;
   memset(out, 0xff, sizeof(*out)); /* NaN unless filled */
-  if (ode_tables(p, zt, T_lo, T_hi, ODE_NT, coef) != 0) {
+  if (ode_tables(p, av, zt, T_lo, T_hi, ODE_NT, coef) != 0) {
     free(coef);
     return 1;
   }
@@ -683,7 +721,16 @@ int oracle_ode_point_z(const oracle_point* p, const oracle_ode* o, int64_t nz, d
                        oracle_yield* out, int64_t* n_steps) {
   ztab_t own;
   const ztab_t* zt = ztab_get(nz, z_max, &own);
-  int r = ode_point(p, o, zt, max_steps, out, n_steps);
+  int r = ode_point(p, o, NULL, zt, max_steps, out, n_steps);
+  ztab_put(zt);
+  return r;
+}
+
+int oracle_ode_point_a(const oracle_point* p, const oracle_ode* o, const oracle_aov_params* av, int64_t nz, double z_max,
+                       int64_t max_steps, oracle_yield* out, int64_t* n_steps) {
+  ztab_t own;
+  const ztab_t* zt = ztab_get(nz, z_max, &own);
+  int r = ode_point(p, o, av, zt, max_steps, out, n_steps);
   ztab_put(zt);
   return r;
 }

@@ -27,6 +27,23 @@ class OraclePoint(ctypes.Structure):
         (n, ctypes.c_int32) for n in ("stats", "regime", "has_Y_chi_init", "has_n_chi_at_Tp")]
 
 
+class OracleAov(ctypes.Structure):  # oracle_aov_params: AoverVKernel's own parameters (fpy:141-151)
+    _fields_ = [(n, ctypes.c_double) for n in ("I_p", "beta_over_H", "T_p_GeV", "v_w", "g_star")]
+
+
+def aov_from(a) -> "OracleAov | None":
+    """An A/V kernel's parameters (dict with I_p, beta_over_H, T_p (or T_p_GeV), v_w, g_star) ->
+    OracleAov; None stays None (the point's own kernel, fpy:197)."""
+    if a is None:
+        return None
+    return OracleAov(float(a["I_p"]), float(a["beta_over_H"]), float(a["T_p"] if "T_p" in a else a["T_p_GeV"]),
+                     float(a["v_w"]), float(a["g_star"]))
+
+
+def _ref(o):
+    return None if o is None else ctypes.byref(o)
+
+
 YIELD_FIELDS = ("Y_B", "Y_chi", "rho_B_kg_m3", "rho_DM_kg_m3", "DM_over_B", "P_used")
 
 
@@ -74,6 +91,10 @@ def lib():
         L.oracle_point_yields_z.argtypes = [P(OraclePoint), i64, d, P(OracleYield)]
         L.oracle_points_batch_z.restype = i64
         L.oracle_points_batch_z.argtypes = [P(OraclePoint), i64, i64, d, P(OracleYield), i32]
+        L.oracle_yb_quadrature_a.restype = d
+        L.oracle_yb_quadrature_a.argtypes = [P(OraclePoint), P(OracleAov), d, d, i32, i64, d]
+        L.oracle_point_yields_a.restype = ctypes.c_int
+        L.oracle_point_yields_a.argtypes = [P(OraclePoint), P(OracleAov), i64, d, P(OracleYield)]
         _lib = L
     return _lib
 
@@ -98,11 +119,12 @@ def point_from_config(cfg: dict) -> OraclePoint:
 NZ, Z_MAX = 1200, 30.0   # fpy:142 defaults, main()'s grid (fpy:197)
 
 
-def point_yields(cfg: dict, nz: int = NZ, z_max: float = Z_MAX) -> dict:
-    """main()'s fast path (fpy:361-417) for one config, A/V on AoverVKernel(..., z_max, nz)."""
+def point_yields(cfg: dict, nz: int = NZ, z_max: float = Z_MAX, aov: dict | None = None) -> dict:
+    """main()'s fast path (fpy:361-417) for one config, A/V on AoverVKernel(..., z_max, nz) with the
+    kernel's own parameters `aov` (None: cfg's, fpy:197)."""
     p = point_from_config(cfg)
     o = OracleYield()
-    rc = lib().oracle_point_yields_z(ctypes.byref(p), int(nz), float(z_max), ctypes.byref(o))
+    rc = lib().oracle_point_yields_a(ctypes.byref(p), _ref(aov_from(aov)), int(nz), float(z_max), ctypes.byref(o))
     if rc != 0:
         raise UnboundLocalError("local variable 'Ychi_fin' referenced before assignment")
     return {n: getattr(o, n) for n in YIELD_FIELDS}
@@ -117,10 +139,13 @@ def points_batch(cfgs: list[dict], nthreads: int = 0, nz: int = NZ, z_max: float
     return np.frombuffer(out, dtype=np.float64).reshape(n, 6).copy()
 
 
-def yb_quadrature(cfg: dict, T_lo: float, T_hi: float, n_y: int = 8000, nz: int = NZ, z_max: float = Z_MAX) -> float:
-    """BoltzmannSystem.integrate_YB_by_quadrature (fpy:231-267) with bs.aov on (nz, z_max)."""
+def yb_quadrature(cfg: dict, T_lo: float, T_hi: float, n_y: int = 8000, nz: int = NZ, z_max: float = Z_MAX,
+                  aov: dict | None = None) -> float:
+    """BoltzmannSystem.integrate_YB_by_quadrature (fpy:231-267) with bs.aov on (nz, z_max) and, if
+    given, its own parameters `aov` (fpy:141-151)."""
     p = point_from_config(cfg)
-    return lib().oracle_yb_quadrature_z(ctypes.byref(p), float(T_lo), float(T_hi), int(n_y), int(nz), float(z_max))
+    return lib().oracle_yb_quadrature_a(ctypes.byref(p), _ref(aov_from(aov)), float(T_lo), float(T_hi), int(n_y),
+                                        int(nz), float(z_max))
 
 
 def aov(I_p, beta_over_H, T_p, v_w, g_star, y, nz: int = NZ, z_max: float = Z_MAX) -> float:
@@ -180,6 +205,11 @@ def _ode_lib():
         L.oracle_ode_rhs_n.argtypes = [P(OraclePoint), P(OracleOde), P(d), i32, d, d, d, P(d), P(d)]
         L.oracle_ode_point_z.restype = ctypes.c_int
         L.oracle_ode_point_z.argtypes = [P(OraclePoint), P(OracleOde), i64, d, i64, P(OracleYield), P(i64)]
+        L.oracle_ode_tables_a.restype = ctypes.c_int
+        L.oracle_ode_tables_a.argtypes = [P(OraclePoint), P(OracleAov), d, d, i32, i64, d, P(d)]
+        L.oracle_ode_point_a.restype = ctypes.c_int
+        L.oracle_ode_point_a.argtypes = [P(OraclePoint), P(OracleOde), P(OracleAov), i64, d, i64, P(OracleYield),
+                                         P(i64)]
         L._ode_ready = True
     return L
 
@@ -236,12 +266,13 @@ class OdeTables:
     """build_tables(T_lo, T_hi, n=nt) with bs.aov on (nz, z_max) (fpy:207-212), then A_over_V_T
     (fpy:214-218) and rhs (fpy:270-286) on them."""
 
-    def __init__(self, cfg: dict, T_lo: float, T_hi: float, nt: int = ODE_NT, nz: int = NZ, z_max: float = Z_MAX):
+    def __init__(self, cfg: dict, T_lo: float, T_hi: float, nt: int = ODE_NT, nz: int = NZ, z_max: float = Z_MAX,
+                 aov: dict | None = None):
         self.p, self.o = point_from_config(cfg), ode_from_config(cfg)
         self.T_lo, self.T_hi, self.nt = float(T_lo), float(T_hi), int(nt)
         self.coef = np.zeros(4 * self.nt)
-        rc = _ode_lib().oracle_ode_tables_z(ctypes.byref(self.p), self.T_lo, self.T_hi, self.nt, int(nz), float(z_max),
-                                            self.coef.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+        rc = _ode_lib().oracle_ode_tables_a(ctypes.byref(self.p), _ref(aov_from(aov)), self.T_lo, self.T_hi, self.nt,
+                                            int(nz), float(z_max), self.coef.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
         if rc != 0:
             raise ValueError("`x` must be strictly increasing sequence.")
 
@@ -258,10 +289,10 @@ class OdeTables:
         return float(dY[0]), float(dY[1])
 
 
-def ode_point(cfg: dict, max_steps: int = 1 << 26, nz: int = NZ, z_max: float = Z_MAX) -> dict:
+def ode_point(cfg: dict, max_steps: int = 1 << 26, nz: int = NZ, z_max: float = Z_MAX, aov: dict | None = None) -> dict:
     p, o, out, ns = point_from_config(cfg), ode_from_config(cfg), OracleYield(), ctypes.c_int64()
-    st = _ode_lib().oracle_ode_point_z(ctypes.byref(p), ctypes.byref(o), int(nz), float(z_max), int(max_steps),
-                                       ctypes.byref(out), ctypes.byref(ns))
+    st = _ode_lib().oracle_ode_point_a(ctypes.byref(p), ctypes.byref(o), _ref(aov_from(aov)), int(nz), float(z_max),
+                                       int(max_steps), ctypes.byref(out), ctypes.byref(ns))
     r = {n: getattr(out, n) for n in YIELD_FIELDS}
     r["status"], r["n_steps"] = st, ns.value
     return r

@@ -8,9 +8,13 @@ buffers come from hipMalloc through ctypes, and every number is computed by libl
     lzq_binding.install(first_principles_yields)   # BoltzmannSystem.integrate_YB_by_quadrature -> GPU
 
 Entry points (each cites the fpy code it replaces):
-  integrate_YB_by_quadrature(self, T_lo, T_hi, n_y=6000)  fpy:231-267 (method replacement; self.aov's z grid)
+  integrate_YB_by_quadrature(self, T_lo, T_hi, n_y=6000)  fpy:231-267 (method replacement; A/V from self.aov:
+                                                          its own I_p, beta_over_H, T_p, v_w, g_star and z grid)
+  build_tables(self, T_lo, T_hi, n=800)                   fpy:207-212 (method replacement: the n A/V knots in
+                                                          one lzq_aov_batch call, the spline by fpy's CubicSpline)
   A_over_V_y(self, y)                                     fpy:158-165 (AoverVKernel method replacement, any z grid)
-  yields(cfg, P, T_lo=None, T_hi=None, n_y=8000, nz=1200, z_max=30.0)
+  aov_batch(aov, ys)                                      fpy:158-165 for many y in one call
+  yields(cfg, P, T_lo=None, T_hi=None, n_y=8000, nz=1200, z_max=30.0, aov=None)
                                                           fpy:231-267 + fpy:372-384 + fpy:413-417
   p_closed_form(lams)                                     fpy:183-184
   lz_propagate(m_mix, dprime, xi, v_w, window_lz, steps)  no fpy counterpart (north_star (1))
@@ -41,6 +45,10 @@ class lzq_point(ctypes.Structure):  # include/lzq.h: struct lzq_point (136 B)
         [(n, ctypes.c_int32) for n in ("stats", "regime", "has_Y_chi_init", "has_n_chi_at_Tp")]
 
 
+class lzq_aov_params(ctypes.Structure):  # include/lzq.h: struct lzq_aov_params (40 B)
+    _fields_ = [(n, ctypes.c_double) for n in ("I_p", "beta_over_H", "T_p_GeV", "v_w", "g_star")]
+
+
 class lzq_yield(ctypes.Structure):  # include/lzq.h: struct lzq_yield (48 B)
     _fields_ = [(n, ctypes.c_double) for n in ("Y_B", "Y_chi", "rho_B_kg_m3", "rho_DM_kg_m3", "DM_over_B",
                                                 "P_used")]
@@ -52,6 +60,8 @@ class lzq_profile_point(ctypes.Structure):  # include/lzq.h: struct lzq_profile_
 
 
 assert ctypes.sizeof(lzq_point) == 136 and ctypes.sizeof(lzq_yield) == 48 and ctypes.sizeof(lzq_profile_point) == 40
+assert ctypes.sizeof(lzq_aov_params) == 40
+ABI_VERSION = 3  # include/lzq.h LZQ_ABI_VERSION this binding is written against
 
 _hip = None
 _lzq = None
@@ -71,14 +81,18 @@ def _libs():
         hip.hipMemcpy.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int]
         hip.hipGetDevice.argtypes = [ctypes.POINTER(ctypes.c_int)]
         L.lzq_last_error.restype = ctypes.c_char_p
+        L.lzq_abi_version.restype = ctypes.c_int
         L.lzq_init.argtypes = [ctypes.c_int]
-        L.lzq_yields_batch.argtypes = [vp, i64, i32, i32, d, vp, vp, vp, vp, vp]
-        L.lzq_aov_batch.argtypes = [ctypes.POINTER(lzq_point), vp, i64, i32, d, vp, vp]
+        L.lzq_yields_batch.argtypes = [vp, i64, i32, i32, d, vp, vp, vp, vp, vp, vp]
+        L.lzq_aov_batch.argtypes = [ctypes.POINTER(lzq_point), ctypes.POINTER(lzq_aov_params), vp, i64, i32, d, vp,
+                                    vp]
         L.lzq_p_closed_form.argtypes = [vp, i64, vp, vp]
         L.lzq_lz_propagate.argtypes = [vp, vp, vp, i64, i32, d, d, i32, vp, vp]
         L.lzq_profile_splines.argtypes = [vp, vp, vp, i32, i32, vp, vp, vp]
         L.lzq_profile_crossings.argtypes = [vp, vp, i32, i32, vp, i64, i32, vp, vp, vp, vp, vp, vp]
         L.lzq_lz_propagate_profile.argtypes = [vp, vp, i32, i32, vp, i64, d, i32, vp, vp]
+        _ok(L.lzq_abi_version() == ABI_VERSION,
+            f"liblzq.so ABI {L.lzq_abi_version()} != {ABI_VERSION} (rebuild the library or update the binding)")
         dev = ctypes.c_int(0)
         _ok(hip.hipGetDevice(ctypes.byref(dev)) == 0, "hipGetDevice failed (no GPU?)")
         _hip = hip
@@ -138,17 +152,27 @@ def point_from_cfg(c, P: float) -> lzq_point:
                      int(c.Y_chi_init is not None), int(c.n_chi_at_Tp_GeV3 is not None))
 
 
-def yields(cfg, P: float, T_lo=None, T_hi=None, n_y: int = 8000, nz: int = 1200, z_max: float = 30.0) -> dict:
+def aov_params(aov) -> lzq_aov_params:
+    """A reference AoverVKernel (fpy:141-151: attributes I_p, beta_over_H, T_p, v_w, g_star) ->
+    lzq_aov_params."""
+    return lzq_aov_params(float(aov.I_p), float(aov.beta_over_H), float(aov.T_p), float(aov.v_w), float(aov.g_star))
+
+
+def yields(cfg, P: float, T_lo=None, T_hi=None, n_y: int = 8000, nz: int = 1200, z_max: float = 30.0,
+           aov=None) -> dict:
     """fpy:231-267 (Y_B) + fpy:372-384, 413-417 (Y_chi, densities) for one config on the GPU
     (T_lo/T_hi default to main()'s window, fpy:367-369), A/V on the z grid linspace(0, z_max, nz)
-    (fpy:141-156)."""
+    (fpy:141-156) with the A/V kernel's own parameters `aov` (an AoverVKernel; None: cfg's own,
+    fpy:197)."""
     _, L = _libs()
     pt = point_from_cfg(cfg, P)
     out = lzq_yield()
     tl, th = ctypes.c_double(T_lo or 0.0), ctypes.c_double(T_hi or 0.0)
-    with _Dev(136, pt) as d_pt, _Dev(8, tl) as d_tl, _Dev(8, th) as d_th, _Dev(48) as d_out:
+    ap = aov_params(aov) if aov is not None else lzq_aov_params()
+    with _Dev(136, pt) as d_pt, _Dev(8, tl) as d_tl, _Dev(8, th) as d_th, _Dev(40, ap) as d_aov, _Dev(48) as d_out:
         _check(L.lzq_yields_batch(d_pt.p, 1, int(n_y), int(nz), float(z_max), d_tl.p if T_lo is not None else None,
-                                  d_th.p if T_hi is not None else None, None, d_out.p, None))
+                                  d_th.p if T_hi is not None else None, None, d_aov.p if aov is not None else None,
+                                  d_out.p, None))
         d_out.read(out)
     return {n: getattr(out, n) for n, _ in lzq_yield._fields_}
 
@@ -166,21 +190,47 @@ def integrate_YB_by_quadrature(self, T_lo: float, T_hi: float, n_y: int = 6000) 
     same result (north_star tolerance 1e-8; measured ~1e-13), computed by lzq_yields_batch on
     self.aov's z grid (any AoverVKernel(..., z_max, nz))."""
     nz, z_max = zgrid_of(self.aov)
-    return yields(self.cfg, self.P, T_lo, T_hi, n_y, nz, z_max)["Y_B"]
+    return yields(self.cfg, self.P, T_lo, T_hi, n_y, nz, z_max, aov=self.aov)["Y_B"]
+
+
+def aov_batch(aov, ys) -> list:
+    """A_over_V_y (fpy:158-165) of the AoverVKernel `aov` (its own parameters and z grid) at every
+    y, in one lzq_aov_batch launch."""
+    _, L = _libs()
+    nz, z_max = zgrid_of(aov)
+    h = _doubles(ys)
+    n = len(h)
+    out = (ctypes.c_double * max(n, 1))()
+    ap = aov_params(aov)
+    if n == 0:
+        return []
+    with _Dev(8 * n, h) as d_y, _Dev(8 * n) as d_out:
+        _check(L.lzq_aov_batch(None, ctypes.byref(ap), d_y.p, n, nz, z_max, d_out.p, None))
+        d_out.read(out)
+    return list(out)[:n]
 
 
 def A_over_V_y(self, y: float) -> float:
     """Drop-in for AoverVKernel.A_over_V_y (fpy:158-165) on the kernel's own z grid
-    (lzq_aov_batch).  Reads I_p, beta_over_H, T_p, v_w and g_star from the kernel object."""
-    _, L = _libs()
-    nz, z_max = zgrid_of(self)
-    pt = lzq_point()
-    pt.I_p, pt.beta_over_H, pt.T_p_GeV, pt.v_w, pt.g_star = self.I_p, self.beta_over_H, self.T_p, self.v_w, self.g_star
-    yv, out = ctypes.c_double(float(y)), ctypes.c_double()
-    with _Dev(8, yv) as d_y, _Dev(8) as d_out:
-        _check(L.lzq_aov_batch(ctypes.byref(pt), d_y.p, 1, nz, z_max, d_out.p, None))
-        d_out.read(out)
-    return out.value
+    (lzq_aov_batch).  Reads I_p, beta_over_H, T_p, v_w and g_star from the kernel object.  One
+    launch per call: batch callers (build_tables below) use aov_batch."""
+    return aov_batch(self, [y])[0]
+
+
+def make_build_tables(fpy_module):
+    """Drop-in for BoltzmannSystem.build_tables (fpy:207-212) of `fpy_module`: the same Ts
+    (np.linspace) and y(T) (fpy's y_of_T, from self.cfg), A/V of self.aov at all n knots in one
+    lzq_aov_batch launch (instead of n scalar A_over_V_y round trips), and fpy's own
+    CubicSpline(Ts, np.maximum(Av, 0.0), extrapolate=True)."""
+    def build_tables(self, T_lo: float, T_hi: float, n: int = 800):
+        np = fpy_module.np
+        self._T_lo, self._T_hi = float(T_lo), float(T_hi)
+        Ts = np.linspace(self._T_lo, self._T_hi, n)
+        ys = [fpy_module.y_of_T(T, self.cfg.T_p_GeV, self.cfg.beta_over_H) for T in Ts]
+        Av = np.array(aov_batch(self.aov, ys), float)
+        self._A_spline = fpy_module.CubicSpline(Ts, np.maximum(Av, 0.0), extrapolate=True)
+
+    return build_tables
 
 
 def p_closed_form(lams) -> list:
@@ -274,7 +324,8 @@ def lz_propagate_profile(knots, phi, Phi, y_B, y_chi, lambda_tr_eff, v_w, steps_
 
 
 def install(fpy_module) -> None:
-    """Route the reference's quadrature operator and its A/V kernel through the GPU
+    """Route the reference's quadrature operator, its ODE tables and its A/V kernel through the GPU
     (INTEGRATION.md §2)."""
     fpy_module.BoltzmannSystem.integrate_YB_by_quadrature = integrate_YB_by_quadrature
+    fpy_module.BoltzmannSystem.build_tables = make_build_tables(fpy_module)
     fpy_module.AoverVKernel.A_over_V_y = A_over_V_y

@@ -30,7 +30,7 @@ def test_library_builds_and_exports_header_symbols():
 def test_abi_version_and_struct_layout():
     n = pkg("_native")
     L = n.load()
-    assert L.lzq_abi_version() == pkg("_native").ABI_VERSION == 2
+    assert L.lzq_abi_version() == pkg("_native").ABI_VERSION == 3
     assert ctypes.sizeof(n.LzqPoint) == 136 and ctypes.sizeof(n.LzqYield) == 48
 
 
@@ -70,13 +70,15 @@ def test_ztables_runtime_grids():
 
 def test_ztables_refuse_bad_grids():
     """nz < 0 is numpy's ValueError; non-finite / negative z_max and grids so fine that the
-    cancelling gamma4 of fpy:156 rounds below 0 are refused (LZQ_EINVAL) before any GPU work."""
+    cancelling gamma4 of fpy:156 rounds below 0, or stops being non-decreasing (the exact-underflow
+    lane test of zsum_dispatch reads gamma4_1 as the smallest node), are refused (LZQ_EINVAL) before
+    any GPU work."""
     import pytest
     nat = pkg("_native")
     L = nat.load()
     for nz, zmax, msg in ((-1, 30.0, b"non-negative"), (1200, float("nan"), b"finite"), (1200, -1.0, b"finite"),
                           (1200, float("inf"), b"finite"), (nat.LZQ_NZ_MAX + 1, 30.0, b"LZQ_NZ_MAX"),
-                          (2_000_000, 30.0, b"gamma4")):
+                          (2_000_000, 30.0, b"gamma4"), (20000, 1.0, b"non-decreasing"), (100000, 10.0, b"non-decreasing")):
         assert L.lzq_ztables(nz, zmax, None, None, None) == -1, (nz, zmax)
         assert msg in L.lzq_last_error(), (nz, zmax, L.lzq_last_error())
     with pytest.raises(ValueError, match="non-negative"):
@@ -89,13 +91,13 @@ def test_ztables_refuse_bad_grids():
 def test_host_side_argument_validation():
     n = pkg("_native")
     L = n.load()
-    rc = L.lzq_yields_batch(None, -1, 8000, 1200, 30.0, None, None, None, None, None)
+    rc = L.lzq_yields_batch(None, -1, 8000, 1200, 30.0, None, None, None, None, None, None)
     assert rc == -1 and b"bad arguments" in L.lzq_last_error()
-    rc = L.lzq_aov_batch(None, None, 1, 1200, 30.0, None, None)
+    rc = L.lzq_aov_batch(None, None, None, 1, 1200, 30.0, None, None)   # neither point nor block
     assert rc == -1 and b"bad arguments" in L.lzq_last_error()
-    assert L.lzq_ode_tables(8, 1, None, None, 3, 1200, 30.0, 8, 12, None, None) == -1   # nt < 4
+    assert L.lzq_ode_tables(8, 1, None, None, 3, 1200, 30.0, None, 8, 12, None, None) == -1   # nt < 4
     assert b"nt = 3" in L.lzq_last_error()
-    assert L.lzq_ode_tables(8, 2, None, None, 100, 1200, 30.0, 8, 799, None, None) == -1  # < 2 x 4 nt
+    assert L.lzq_ode_tables(8, 2, None, None, 100, 1200, 30.0, None, 8, 799, None, None) == -1  # < 2 x 4 nt
     assert b"workspace" in L.lzq_last_error()
     assert L.lzq_ode_aov_T(None, 1.0, 2.0, 800, None, None, 1, None, None) == -1
     rc = L.lzq_p_closed_form(None, 0, None, None)  # n == 0 is a no-op

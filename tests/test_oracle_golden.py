@@ -155,3 +155,57 @@ def test_golden_zgrid_ode():
         assert o["status"] == 0
         assert rel_err(o["Y_B"], r["Y_B"]) < 1e-10, (o["Y_B"], r["Y_B"])
         assert rel_err(o["Y_chi"], r["Y_chi"]) < 1e-10, (o["Y_chi"], r["Y_chi"])
+
+
+# ---- bs.aov replaced by a kernel of other parameters (fpy:141-151, 197, 211, 228, 261) -------------
+def _aov_cases():
+    return golden("golden_aov_params.json")
+
+
+def test_golden_aov_params_yields():
+    """Y_B of bs.integrate_YB_by_quadrature with bs.aov = AoverVKernel(I_p', beta_over_H', T_p', v_w',
+    g_star', z_max, nz) != cfg's kernel (tests/golden/make_golden_aov.py ran the reference): A/V from
+    the kernel's own parameters, the rest of the integrand from cfg.  Also A_over_V_y of the kernel,
+    and every case differs from the answer with cfg's own kernel (the fixture exercises the split)."""
+    worst = 0.0
+    for r in _aov_cases()["yields"]:
+        cfg, a = full_cfg(r["config"]), r["aov"]
+        T_p = cfg["T_p_GeV"]
+        win = (cfg["T_min_over_Tp"] * T_p, cfg["T_max_over_Tp"] * T_p)
+        got = O.yb_quadrature(cfg, *win, 8000, r["nz"], r["z_max"], aov=a)
+        own = O.yb_quadrature(cfg, *win, 8000, r["nz"], r["z_max"])
+        worst = max(worst, rel_err(got, r["Y_B"]))
+        assert rel_err(own, r["Y_B"]) > 1e-6, r["aov"]
+        for y, ref in zip(r["y"], r["Av"]):
+            g = O.aov(a["I_p"], a["beta_over_H"], a["T_p"], a["v_w"], a["g_star"], y, r["nz"], r["z_max"])
+            assert (g == ref == 0.0) or rel_err(g, ref) < TOL_AOV * max(1.0, r["nz"] / 1200), (a, y, g, ref)
+        o = O.point_yields(cfg, r["nz"], r["z_max"], aov=a)
+        assert o["Y_B"] == got
+    assert worst < 1e-11, worst
+
+
+def test_golden_aov_params_tables_and_ode():
+    """build_tables (fpy:211: y(T) from cfg, A/V from bs.aov) + A_over_V_T + rhs, and main()'s ODE
+    fallback (the reference's own solve_ivp on bs.rhs) with the replaced kernel."""
+    d = _aov_cases()
+    for t in d["tables"]:
+        c = full_cfg(t["config"])
+        T_p = c["T_p_GeV"]
+        tab = O.OdeTables(c, c["T_min_over_Tp"] * T_p, c["T_max_over_Tp"] * T_p, t["nt"], t["nz"], t["z_max"],
+                          aov=t["aov"])
+        scale = max(abs(v) for v in t["Av"])
+        for T, ref in zip(t["T"], t["Av"]):
+            assert abs(tab.aov_T(T) - ref) <= 1e-11 * abs(ref) + 1e-13 * scale, (T, tab.aov_T(T), ref)
+        k = 0
+        for x in t["x"]:
+            for Y in t["Y"]:
+                got, ref = tab.rhs(x, Y), t["rhs"][k]
+                k += 1
+                for g, r in zip(got, ref):
+                    assert abs(g - r) <= 1e-10 * abs(r) + 1e-300, (x, Y, got, ref)
+    for r in d["ode"]:
+        assert r["success"]
+        o = O.ode_point(full_cfg(r["config"]), nz=r["nz"], z_max=r["z_max"], aov=r["aov"])
+        assert o["status"] == 0
+        assert rel_err(o["Y_B"], r["Y_B"]) < 1e-10, (o["Y_B"], r["Y_B"])
+        assert rel_err(o["Y_chi"], r["Y_chi"]) < 1e-10, (o["Y_chi"], r["Y_chi"])

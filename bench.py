@@ -13,6 +13,12 @@ all-gathered over RCCL at the end of every step (north_star (3)).
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
+`python bench.py --gpus N` with N > 1 and no launcher (no WORLD_SIZE in the environment) starts
+the N ranks itself: the parent touches no GPU, runs this same script under
+`python -m torch.distributed.run --nproc-per-node N` (one process per GPU, RCCL), lets rank 0's
+line through and exits with the launcher's status.  A rank count that disagrees with --gpus, or
+more RCCL ranks than the node has GPUs, is an error (exit status 2), never a 1-GPU line.
+
 Prints one JSON line (rank 0).  `roofline` = the kernel's executed FP64 FLOP (PMC
 instruction mix of profiles/round4, used only if that profile's kernel code hash is the timed
 library's) over its HIP-event time in this run, against the 78.6 TFLOP/s FP64 vector peak, with
@@ -29,6 +35,8 @@ import argparse
 import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -282,6 +290,32 @@ def spread(vals) -> dict:
     return {"min": min(v), "max": max(v), "mean": float(np.mean(v)), "per_rank": v}
 
 
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(argv: list, n: int) -> int:
+    """--gpus N > 1 without a launcher: N ranks of this same script (sys.argv[0]: bench.py, or a
+    test's stand-in) under torch.distributed.run on this node, master 127.0.0.1.  Nothing here
+    touches a GPU (the ranks do); the children inherit stdout, so rank 0's JSON line is the only
+    line.  Returns the launcher's exit status (non-zero if any rank failed)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(sys.argv[0]), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # RCCL needs dmabuf IPC on this pool
+    print(f"[bench] --gpus {n} without a launcher: starting {n} ranks ({' '.join(cmd[1:8])} ...)", file=sys.stderr,
+          flush=True)
+    try:
+        return subprocess.run(cmd, env=env).returncode
+    except OSError as e:
+        print(f"[bench] could not start the ranks: {e}", file=sys.stderr)
+        return 2
+
+
 def main(argv=None, engine=None) -> int:
     """The bench (one JSON line on rank 0).  engine: a stand-in with Engine.sweep's signature and a
     torch `device` (tests only: the CPU rehearsal of the timing / evidence order); None = the HIP
@@ -302,16 +336,28 @@ def main(argv=None, engine=None) -> int:
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI, default) | gloo (rehearsal of the N>1 path on one GPU)")
+    argv = list(sys.argv[1:] if argv is None else argv)
     args = ap.parse_args(argv)
+    if args.gpus < 1:
+        print(f"[bench] --gpus {args.gpus}: need at least 1", file=sys.stderr)
+        return 2
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(argv, args.gpus)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        print(f"[bench] WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE", file=sys.stderr)
+        print(f"[bench] WORLD_SIZE={world} but --gpus={args.gpus}: the line would not measure --gpus GPUs",
+              file=sys.stderr)
+        return 2
     cuda = engine is None
     if cuda:
-        local = local % max(1, torch.cuda.device_count())  # gloo rehearsal: several ranks may share a GPU
+        ndev = torch.cuda.device_count()   # counts devices without initialising HIP
+        if args.dist_backend == "nccl" and world > ndev:
+            print(f"[bench] --gpus {world} over RCCL needs {world} GPUs; this node has {ndev}", file=sys.stderr)
+            return 2
+        local = local % max(1, ndev)  # gloo rehearsal: several ranks may share a GPU
         torch.cuda.set_device(local)
     # a process group whenever a launcher started us (torchrun sets MASTER_ADDR/PORT), so a
     # 1-rank torchrun runs the same RCCL all-gather as N ranks; plain `python bench.py` has none
@@ -465,7 +511,9 @@ def main(argv=None, engine=None) -> int:
             rec["truncated"] = trunc
         if reuse is not None:
             rec["reuse_zsums"] = reuse
-        if world == 1 and not args.no_cpu_baseline:
+        if not args.no_cpu_baseline:
+            # after every collective of the run (the other ranks are done), at every N (north_star:
+            # the CPU path beside the throughput at 1/2/4/8 GPUs); the sample is the same grid's
             rec["cpu_baseline"] = cpu_baseline(axes, grid_total, args.cpu_seconds)
         print(json.dumps(rec), flush=True)
         if status:

@@ -113,3 +113,26 @@ def test_two_rank_line_is_decomposed():
         assert len(rec[k]["per_rank"]) == 2 and rec[k]["max"] >= rec[k]["mean"] >= rec[k]["min"] >= 0.0, rec[k]
     assert rec["evidence"]["all_finite_and_placed"]
     assert abs(rec["value"] - 128 / (rec["ms_per_step"] / 1e3)) <= 1e-6 * rec["value"]
+
+
+def test_gpus_n_without_launcher_spawns_the_ranks():
+    """`bench.py --gpus 2` with no launcher: the parent starts the 2 ranks itself
+    (torch.distributed.run of the same script), and the one line it lets through measured both:
+    n_gpus 2, the all-gather timed on both ranks, and the CPU baseline beside it (north_star: at
+    every N)."""
+    r = _run([sys.executable, FAKE, "--gpus", "2", "--points", "64", "--steps", "2", "--warmup", "1", "--no-reuse",
+              "--no-parity-spot", "--dist-backend", "gloo", "--cpu-seconds", "0.5"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _line(r.stdout)
+    assert rec["n_gpus"] == 2 and rec["config"]["global_points_per_step"] == 128
+    assert rec["allgather_ms"] is not None and len(rec["allgather_ms"]["per_rank"]) == 2
+    assert rec["cpu_baseline"]["value"] > 0 and rec["cpu_baseline"]["kind"] == "port"
+    assert "starting 2 ranks" in r.stderr
+
+
+def test_rank_count_mismatch_is_an_error():
+    """A launcher's WORLD_SIZE that disagrees with --gpus exits 2 and prints no line (it would not
+    measure --gpus GPUs)."""
+    r = _run([sys.executable, FAKE, "--gpus", "4", *SMALL], env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert "WORLD_SIZE=1 but --gpus=4" in r.stderr

@@ -56,11 +56,13 @@ ODE_DTYPE = np.dtype([("sigma_v_chi_GeV_m2", "<f8"), ("Gamma_wash_over_H", "<f8"
                       ("deplete_DM_from_source", "<i4"), ("reserved", "<i4")])
 assert ctypes.sizeof(LzqOdeParams) == 24 == ODE_DTYPE.itemsize
 ODE_NT, ODE_WS_PER_POINT = 800, 3200  # LZQ_ODE_NT, LZQ_ODE_WS_PER_POINT
-ODE_OK, ODE_BAD_GRID, ODE_BAD_STEP, ODE_TOO_MANY_STEPS, ODE_NEWTON, ODE_NOT_LINEAR, ODE_UNRESOLVED = range(7)  # enum lzq_ode_status
+ODE_OK, ODE_BAD_GRID, ODE_BAD_STEP, ODE_TOO_MANY_STEPS, ODE_NEWTON, ODE_NOT_LINEAR, ODE_UNRESOLVED, ODE_BAD_TABLE = \
+    range(8)  # enum lzq_ode_status
 ODE_STATUS = {0: "ok", 1: "`x` must be strictly increasing sequence.", 2: "`max_step` must be positive.",
               3: "more than max_steps integration steps", 4: "Radau stage Newton iteration did not converge",
               5: "sigma_v != 0: the quadrature form needs a linear Y_chi equation",
-              6: "quadrature form: a knot interval needs more than 4096 sub-intervals"}
+              6: "quadrature form: a knot interval needs more than 4096 sub-intervals",
+              7: "spline table not built for LZQ_ODE_NT knots"}
 
 # struct lzq_profile_point (40 B): a bounce-profile shape + the couplings of PAPER eqs.(5)-(8)
 PROFILE_POINT_DTYPE = np.dtype([("y_B", "<f8"), ("y_chi", "<f8"), ("lambda_tr_eff", "<f8"), ("v_w", "<f8"),

@@ -312,6 +312,11 @@ __device__ __forceinline__ bool ode_grid_ok(double T_lo, double T_hi, double ste
   return ok;
 }
 
+// The integrators read tables of kOdeNT knots at a fixed stride: ode_spline_kernel records the
+// table's knot count in its last 4 doubles (spare: the cubics use 4 (nt - 1)), and a table built
+// for another nt (lzq_ode_tables takes any) is refused per point instead of read as wrong rows.
+__device__ __forceinline__ bool ode_table_ok(const double* __restrict__ w) { return w[kOdeWS - 4] == (double)kOdeNT; }
+
 // Radau IIA, 3 stages (the method of scipy's Radau): nodes C, matrix A (row 3 = weights).
 struct Radau {
   double c[3], a[3][3];
@@ -566,6 +571,12 @@ __device__ __forceinline__ double fma_neg_s(double k, double a, double p) {
 #endif
 #ifndef LZQ_ODE_YBREC
 #define LZQ_ODE_YBREC 1  // Y_B by its affine step map (yb_rec), shared per cooperative segment
+#endif
+#ifndef LZQ_ODE_RICVAR
+#define LZQ_ODE_RICVAR 1  // whole-wave cooperative split-free waves run ode_riccati_kernel (compact rows, uniform constants)
+#endif
+#ifndef LZQ_RIC_MIN_WAVES
+#define LZQ_RIC_MIN_WAVES 4  // ode_riccati_kernel: minimum waves per SIMD (its VGPR cap = 512 / this)
 #endif
 
 template <bool kWithYB = true>
@@ -836,6 +847,7 @@ __global__ __launch_bounds__(kOdeBlock) void ode_spline_kernel(const lzq_point* 
     w[4 * k + 2] = sk;
     s_next = sk;
   }
+  w[ws_pt - 4] = (double)N;  // the table's knot count, in its spare doubles (ode_table_ok)
   if (status) status[i] = LZQ_ODE_OK;
 }
 
@@ -908,7 +920,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
   const double* w = ws + (tidx ? (int64_t)tidx[i] : i) * (int64_t)kOdeWS;
   const double nan = __builtin_nan("");
   lzq_yield r = {nan, nan, nan, nan, nan, pt.P_chi_to_B};
-  int st = ode_grid_ok(o.T_lo, o.T_hi, o.stepT) ? LZQ_ODE_OK : LZQ_ODE_BAD_GRID;
+  int st = ode_grid_ok(o.T_lo, o.T_hi, o.stepT) ? (ode_table_ok(w) ? LZQ_ODE_OK : LZQ_ODE_BAD_TABLE) : LZQ_ODE_BAD_GRID;
   const double m = o.m, T_p = o.Tp;
   const double x0 = m / o.T_hi, x1 = m / pymax(o.T_lo, 1e-30);  // fpy:387-388
   double Ychi;                                                   // fpy:389-399
@@ -1058,6 +1070,10 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
     if (!kLin && LZQ_ODE_NOSPLITVAR) {
       const bool lane_ns = k_split == INT64_MAX || (k_split >= 0 && (k_split + 1 < k_begin || k_split >= k_stop));
       if (__all(lane_ns) != kNoSplit) return;
+      // whole-wave cooperative, one table, one Gamma_wash: ode_riccati_kernel steps it, split steps
+      // included unless the x rounding makes the split search unreliable (k_split = -1: every step
+      // takes the general path here) -- LZQ_ODE_RICVAR; the same predicate there, on the same values
+      if (LZQ_ODE_RICVAR && !kChiOnly && G == 64 && !tab_vary && rec_shared && __all(k_split != -1)) return;
     }
     const int64_t block = coop ? G : N;
     for (int64_t kb = k_begin; kb < k_stop; kb += block) {
@@ -1268,6 +1284,311 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
 }
 
 // ---------------------------------------------------------------------------------------
+// ode_riccati_kernel (LZQ_ODE_RICVAR): the <kNoSplit> variant's steps for its most common wave,
+// a whole 64-lane cooperative segment (G = 64) on one spline table with one Gamma_wash and no
+// split step in the launch -- the Riccati sweeps over sigma_v, P, flux, deplete (and m_chi
+// once grouped).  Every lane of such a wave agrees in everything ode_stage_base reads, so those
+// per-point constants, the window, N, h, hA and the table pointer are wave-uniform and live in
+// SGPRs (readfirstlane); the LDS rows hold only what a lane's step reads (lam, E2, a per stage
+// and the Y_B step map: 88 B instead of 216 B per step); and the per-lane and split paths are
+// not compiled in.  That is what keeps the kernel at LZQ_RIC_MIN_WAVES waves per SIMD against the
+// general variant's 2 (VGPRs and LDS both): a step is a serial Newton chain, and more waves hide
+// its latency.  The operations are the general path's, in the same order (ode_stage_base,
+// stage_scale's products, yb_rec, radau_step<false>), so the bits are the same
+// (tests/test_gpu_ode.py mode-independence tests).  Every launch runs every variant; each steps
+// only its own waves.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ double ode_uniform(double x) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, x);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+struct RicRow {
+  double lam[3], E2[3], a[3];  // StageBase lam, E2, a of the step's three stages
+};
+
+// kPhase: a wave whose split step (the T = m/3 branch) lies in this launch's range runs in three
+// passes -- 0: the regular steps before it, 1: the split step and the next (ode_integrate_kernel's
+// split-step code, each lane forming its own stages: two steps, so registers do not matter),
+// 2: the regular steps after it -- with its state handed on in OdeState; so the regular-step
+// kernels (0, 2) carry no split code.  A wave with no split in range runs in pass 0 alone.
+template <int kPhase>
+__global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) void ode_riccati_kernel(
+    const lzq_point* __restrict__ pts, const lzq_ode_params* __restrict__ ode, int64_t n,
+    const int32_t* __restrict__ tidx, const double* __restrict__ ws, int64_t max_steps, lzq_yield* __restrict__ out,
+    int32_t* __restrict__ status, int coop_on, int64_t k_lo, int64_t k_cnt, OdeState* __restrict__ state) {
+  __shared__ RicRow s_row[kOdeBlock / 64][64];
+  __shared__ YbCD s_rcd[kOdeBlock / 64][64];
+  __shared__ OdePoint s_pt[kOdeBlock / 64];
+  __shared__ double s_beta[kOdeBlock / 64][64][3];  // the fill's beta_j (Gamma_wash * base)
+
+  if (!LZQ_ODE_RICVAR || !LZQ_ODE_COOP || !coop_on) return;
+  // --- the classification of ode_integrate_kernel<false, false, true>, on the same values ---
+  const int64_t wave0 = (int64_t)blockIdx.x * kOdeBlock + (threadIdx.x & ~63);
+  if (wave0 >= n) return;
+  const int64_t i_self = (int64_t)blockIdx.x * kOdeBlock + threadIdx.x;
+  const bool real = i_self < n;
+  const int64_t i = real ? i_self : wave0;
+  const bool cont = state != nullptr, first = kPhase == 0 && (!cont || k_lo == 0);
+  if (kPhase > 0 && !cont) return;  // passes 1 and 2 continue from pass 0's state
+  if (cont && !first && state[i].status != kOdeInProgress) return;
+  const lzq_point pt = pts[i];
+  const OdePoint o = ode_point(pt, ode[i]);
+  const double* w = ws + (tidx ? (int64_t)tidx[i] : i) * (int64_t)kOdeWS;
+  if (!ode_grid_ok(o.T_lo, o.T_hi, o.stepT) || !ode_table_ok(w)) return;  // the general variant reports it
+  const double m = o.m, T_p = o.Tp;
+  const double x0 = m / o.T_hi, x1 = m / pymax(o.T_lo, 1e-30);
+  const double x_p = m / pymax(T_p, 1e-30);
+  const double max_step = pymin(pymin(fabs(x1 - x0) / 20000.0, x_p / 1000.0), 5e-4);
+  if (!(max_step > 0.0)) return;
+  const double steps = ceil(fabs(x1 - x0) / max_step);
+  if (!(steps <= (double)max_steps)) return;
+  if (__ballot(1) != ~0ull) return;  // a lane returned above: not a whole cooperative wave
+  auto same = [](double v) { return __builtin_bit_cast(uint64_t, v) == __builtin_bit_cast(uint64_t, __shfl(v, 0, 64)); };
+  const bool eq = same(o.m) && same(o.Tp) && same(o.B) && same(o.sig) && same(o.H0) && same(o.s0) && same(o.c_rel) &&
+                  same(o.c_nr) && same(o.v0) && same(o.T_lo) && same(o.T_hi);
+  if (!__all(eq)) return;                                                    // G < 64
+  if (!__all(same(__builtin_bit_cast(double, w)))) return;                   // tab_vary
+  if (!__all(same(o.gamma_w))) return;                                       // !rec_shared
+  if (LZQ_ODE_LINFAST && __all(o.sigmav == 0.0)) return;                     // lin_wave
+  const int64_t N = (int64_t)steps;
+  const int64_t k_begin = cont ? k_lo : 0;
+  const int64_t k_stop = cont ? (k_lo + k_cnt < N ? k_lo + k_cnt : N) : N;
+  const double h = (x1 - x0) / (double)N;
+  const double xb = branch_x(o, x0, x1);
+  int64_t k_split = INT64_MAX;
+  if (xb < INFINITY) {  // ode_integrate_kernel's search, verbatim
+    const double kf = floor((xb - x0) / h);
+    const double margin = 2.0 + floor(8.0 * __DBL_EPSILON__ * (fabs(x0) + fabs(x1)) / h);
+    if (!(margin <= 16.0)) {
+      k_split = -1;
+    } else if (kf - margin < (double)N && kf + margin >= 0.0) {
+      const int64_t c0 = kf - margin > 0.0 ? (int64_t)(kf - margin) : 0;
+      const int64_t c1 = kf + margin < (double)(N - 1) ? (int64_t)(kf + margin) : N - 1;
+#pragma nounroll
+      for (int64_t c = c0; c <= c1; ++c) {
+        const double xc = x0 + (double)c * h;
+        if (xc < xb && xb <= xc + h) {
+          k_split = c;
+          break;
+        }
+      }
+    }
+  }
+  if (!__all(k_split != -1)) return;  // x rounding comparable to h: the general variant's every-step test
+  // the split step (xk < xb <= xk + h) of this wave: k_split, and k_split + 1 when a rounding splits
+  // that one too (wave-uniform: x0, h and xb are); every other step is a regular one
+  const int64_t ks = (int64_t)__builtin_bit_cast(uint64_t, ode_uniform(__builtin_bit_cast(double, k_split)));
+  const double xbu = ode_uniform(xb), xb_below = nextafter(xbu, -INFINITY);
+  // this pass's steps [pk_begin, pk_stop)
+  const bool in_range = ks != INT64_MAX && !(ks + 1 < k_begin || ks >= k_stop);
+  if (kPhase > 0 && !in_range) return;
+  const int64_t ks_lo = ks > k_begin ? ks : k_begin, ks_hi = ks + 2 < k_stop ? ks + 2 : k_stop;
+  const int64_t pk_begin = kPhase == 0 ? k_begin : (kPhase == 1 ? ks_lo : ks_hi);
+  const int64_t pk_stop = kPhase == 0 ? (in_range ? ks_lo : k_stop) : (kPhase == 1 ? ks_hi : k_stop);
+  // --- this wave is ours: the wave-uniform point constants in the wave's LDS slot (read by the
+  // fill phase only), the window, h, hA and the table pointer in SGPRs ---
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) s_pt[wv] = o;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const OdePoint& ou = s_pt[wv];
+  const double* wu = reinterpret_cast<const double*>(
+      (uintptr_t)__builtin_bit_cast(uint64_t, ode_uniform(__builtin_bit_cast(double, (uint64_t)(uintptr_t)w))));
+  const double x0u = ode_uniform(x0), hu = ode_uniform(h);
+  const Radau R = radau_tableau();
+  RadauH hA = radau_h(R, hu);
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) hA.a[a][b] = ode_uniform(hA.a[a][b]);
+  // --- per-lane state (ode_integrate_kernel's) ---
+  const double Pf = o.Pf, sigmav = o.sigmav;
+  const int deplete = o.deplete;
+  int st = LZQ_ODE_OK;
+  double Ychi;
+  if (pt.regime == LZQ_NONTHERMAL) {
+    if (pt.has_Y_chi_init) Ychi = pt.Y_chi_init;
+    else if (pt.has_n_chi_at_Tp) Ychi = pt.n_chi_at_Tp_GeV3 / pymax(s_entropy(T_p, pt.g_star_s), 1e-300);
+    else Ychi = 1.0e-12;
+  } else {
+    Ychi = n_chi_eq(o.T_hi, m, pt.g_chi, pt.stats) / s_entropy(o.T_hi, pt.g_star_s);
+  }
+  double YB = 0.0;
+  const bool riccati = LZQ_ODE_PREDICT && sigmav != 0.0;
+  double Zs[3] = {Ychi, Ychi, Ychi}, Yp = Ychi;
+  bool have = false, done = false;
+  if (!first) {
+    const OdeState sv = state[i];
+    Ychi = sv.Ychi;
+    YB = sv.YB;
+    Yp = sv.Yp;
+    Zs[0] = sv.Z[0];
+    Zs[1] = sv.Z[1];
+    Zs[2] = sv.Z[2];
+    have = sv.have != 0;
+  }
+  const bool finished_here = pk_stop >= N;
+  if (kPhase == 1) {
+    // ode_integrate_kernel's steps, each lane on its own stages (ode_stage: the shared base and its
+    // products; the same values the cooperative rows hold): the split step in two parts around the
+    // branch point without the predictor, a regular step with it
+    for (int64_t k = pk_begin; k < pk_stop && !done; ++k) {
+      const double xk = x0u + (double)k * hu;
+      const bool split = xk < xbu && xbu <= xk + hu;
+      const double xa = split ? xb_below : xk + hu;
+      double YB_prev = YB;
+      bool ok = true;
+      const double Ystart = Ychi;
+      bool use_guess = false;
+      if (riccati && have && !split) {
+        double g[3];
+        use_guess = true;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          g[j] = fma_s(Zs[2], kRadauPred[j][3], fma_s(Zs[1], kRadauPred[j][2],
+                                                      fma_s(Zs[0], kRadauPred[j][1], kRadauPred[j][0] * Yp)));
+          use_guess = use_guess && fabs(g[j] - Ychi) <= 0.25 * fabs(Ychi);
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) Zs[j] = g[j];
+      }
+      auto part = [&](double xs, double hs, bool guess) {
+        const RadauH hAs = radau_h(R, hs);
+        OdeStage sg[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const StageBase b = ode_stage_base(ou, wu, xs + R.c[j] * hs);
+          sg[j].alpha = Pf * b.a;
+          sg[j].S = deplete ? sg[j].alpha : 0.0;
+          sg[j].lam = sigmav * b.lam;
+          sg[j].E2 = b.E2;
+          sg[j].beta = ou.gamma_w * b.beta;
+          sg[j].a = b.a;
+        }
+        const YbRec yr = yb_rec(hAs, sg);
+        YB = __builtin_fma(yr.c, YB, Pf * yr.d);
+        return radau_step<false>(hAs, sg, Ychi, YB, Zs, guess);
+      };
+      if (xa > xk) ok = part(xk, split ? xa - xk : hu, use_guess);
+      if (ok && split && xk + hu > xbu) {
+        YB_prev = YB;
+        ok = part(xbu, (xk + hu) - xbu, false);
+      }
+      have = !split;
+      Yp = Ystart;
+      if (!ok) {
+        YB = YB_prev;
+        st = LZQ_ODE_NEWTON;
+        done = true;
+      }
+    }
+  }
+  for (int64_t kb = pk_begin; kPhase != 1 && kb < pk_stop; kb += 64) {
+    const int64_t kend = kb + 64 < pk_stop ? kb + 64 : pk_stop;
+    {  // lane l: the stage ingredients and Y_B step map of step kb + l (the cooperative fill)
+      const int64_t kl = kb + lane;
+      if (kl < kend) {
+        const double xk = x0u + (double)kl * hu;
+        RicRow& row = s_row[wv][lane];
+        double* bt = s_beta[wv][lane];
+#pragma unroll 1
+        for (int j = 0; j < 3; ++j) {  // one stage at a time (the fill's register peak), parked in LDS
+          const double cj = j == 0 ? R.c[0] : (j == 1 ? R.c[1] : R.c[2]);  // (a dynamic index would go to scratch)
+          const StageBase bs = ode_stage_base(ou, wu, xk + cj * hu);
+          row.lam[j] = bs.lam;
+          row.E2[j] = bs.E2;
+          row.a[j] = bs.a;
+          bt[j] = ou.gamma_w * bs.beta;
+        }
+        const double beta[3] = {bt[0], bt[1], bt[2]}, a[3] = {row.a[0], row.a[1], row.a[2]};
+        const YbRec yr = yb_rec(hA, beta, a);
+        s_rcd[wv][lane] = {yr.c, yr.d};
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    double kd = (double)kb;
+    for (int r = 0; r < (int)(kend - kb) && !done; ++r) {
+      const double xk = x0u + kd * hu;
+      kd += 1.0;
+      const double YB_prev = YB;
+      const double Ystart = Ychi;
+      bool use_guess = false;
+      if (riccati && have) {  // the Radau5 predictor, as ode_integrate_kernel
+        double g[3];
+        use_guess = true;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          g[j] = fma_s(Zs[2], kRadauPred[j][3], fma_s(Zs[1], kRadauPred[j][2],
+                                                      fma_s(Zs[0], kRadauPred[j][1], kRadauPred[j][0] * Yp)));
+          use_guess = use_guess && fabs(g[j] - Ychi) <= 0.25 * fabs(Ychi);
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) Zs[j] = g[j];
+      }
+      bool ok = true;
+      if (xk + hu > xk) {
+        const RicRow& row = s_row[wv][r];
+        OdeStage sg[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {  // stage_scale's products (beta is not read by radau_step<false>)
+          sg[j].alpha = Pf * row.a[j];
+          sg[j].S = deplete ? sg[j].alpha : 0.0;
+          sg[j].lam = sigmav * row.lam[j];
+          sg[j].E2 = row.E2[j];
+          sg[j].beta = 0.0;
+          sg[j].a = row.a[j];
+        }
+        const YbCD rc = s_rcd[wv][r];
+        YB = __builtin_fma(rc.c, YB, Pf * rc.d);
+        ok = radau_step<false>(hA, sg, Ychi, YB, Zs, use_guess);
+      }
+      have = true;
+      Yp = Ystart;
+      if (!ok) {
+        YB = YB_prev;
+        st = LZQ_ODE_NEWTON;
+        done = true;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // every lane is done with this block's rows
+  }
+  const bool finished = finished_here || done;
+  if (!finished) {
+    if (real) {
+      OdeState sv;
+      sv.Ychi = Ychi;
+      sv.YB = YB;
+      sv.Yp = Yp;
+      sv.Z[0] = Zs[0];
+      sv.Z[1] = Zs[1];
+      sv.Z[2] = Zs[2];
+      sv.status = kOdeInProgress;
+      sv.have = have ? 1 : 0;
+      state[i] = sv;
+    }
+    return;
+  }
+  if (cont && real) state[i].status = st;
+  const double nan = __builtin_nan("");
+  lzq_yield res = {nan, nan, nan, nan, nan, pt.P_chi_to_B};
+  const double nB0 = YB * kS0M3, nDM0 = Ychi * kS0M3;  // fpy:412-417 (st is OK or NEWTON here)
+  res.Y_B = YB;
+  res.Y_chi = Ychi;
+  res.rho_B_kg_m3 = nB0 * kMProtonKg;
+  res.rho_DM_kg_m3 = nDM0 * (m * kGeVToKg);
+  res.DM_over_B = res.rho_DM_kg_m3 / pymax(res.rho_B_kg_m3, 1e-300);
+  if (!real) return;
+  out[i] = res;
+  if (status) status[i] = st;
+}
+
+// ---------------------------------------------------------------------------------------
 // Converged quadrature form of the sigma_v = 0 fallback (opt-in; lzq_ode_quadrature).
 // With sigma_v = 0 both equations of rhs (fpy:270-286) are linear with known integrating
 // factors: beta = gamma_w H / (H x) = gamma_w / x, so
@@ -1347,7 +1668,8 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_QUAD_MIN_WAVES) void ode_quad_kernel
   bool ok = true;
   for (int k = lane + 1; k < kOdeNT; k += kW)
     ok = ok && linspace_at(o.T_lo, o.T_hi, o.stepT, k, kOdeNT) > linspace_at(o.T_lo, o.T_hi, o.stepT, k - 1, kOdeNT);
-  int st = __any(!ok) ? LZQ_ODE_BAD_GRID : (o.sigmav != 0.0 ? LZQ_ODE_NOT_LINEAR : LZQ_OK);
+  int st = __any(!ok) ? LZQ_ODE_BAD_GRID
+                      : (!ode_table_ok(w) ? LZQ_ODE_BAD_TABLE : (o.sigmav != 0.0 ? LZQ_ODE_NOT_LINEAR : LZQ_OK));
   const double m = o.m, T_p = o.Tp;
   const double x1 = m / pymax(o.T_lo, 1e-30);  // fpy:388
   const double ix1 = 1.0 / x1;
@@ -1498,6 +1820,23 @@ int launch_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int
                          dim3(lzq::kOdeBlock), 0, s, d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status,
                          lzq::g_ode_coop, k_lo, k_cnt, st);
       rc = hip_check(hipGetLastError(), fn);
+      if constexpr (LZQ_ODE_RICVAR && !kChiOnly) {  // the three passes (ode_riccati_kernel)
+        if (rc != LZQ_OK) return rc;
+        hipLaunchKernelGGL(lzq::ode_riccati_kernel<0>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, s,
+                           d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, lzq::g_ode_coop, k_lo,
+                           k_cnt, st);
+        rc = hip_check(hipGetLastError(), fn);
+        if (rc != LZQ_OK) return rc;
+        hipLaunchKernelGGL(lzq::ode_riccati_kernel<1>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, s,
+                           d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, lzq::g_ode_coop, k_lo,
+                           k_cnt, st);
+        rc = hip_check(hipGetLastError(), fn);
+        if (rc != LZQ_OK) return rc;
+        hipLaunchKernelGGL(lzq::ode_riccati_kernel<2>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, s,
+                           d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, lzq::g_ode_coop, k_lo,
+                           k_cnt, st);
+        rc = hip_check(hipGetLastError(), fn);
+      }
     }
     if constexpr (LZQ_ODE_LINFAST && LZQ_ODE_YBREC && !kChiOnly) {
       if (rc != LZQ_OK) return rc;
@@ -1508,7 +1847,9 @@ int launch_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int
     }
     return rc;
   };
-  if (launches == 1) return launch(0, 0, nullptr);
+  // one launch needs no carried state, unless the Riccati passes (ode_riccati_kernel) hand a
+  // wave's state from pass to pass
+  if (launches == 1 && !(LZQ_ODE_RICVAR && !kChiOnly)) return launch(0, 0, nullptr);
   lzq::OdeState* st = nullptr;
   int rc = hip_check(hipMallocAsync((void**)&st, sizeof(lzq::OdeState) * (size_t)n, s), fn);
   if (rc) return rc;

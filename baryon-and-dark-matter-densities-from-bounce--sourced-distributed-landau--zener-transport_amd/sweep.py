@@ -268,9 +268,10 @@ def spec_from_json(d: dict) -> SweepSpec:
     nz, z_max = _native.zgrid(d.get("nz", _native.LZQ_NZ), d.get("z_max", _native.LZQ_Z_MAX))
     ms = d.get("ode_max_steps", ODE_MAX_STEPS)
     if ms is not None and int(ms) < 0:
-        raise ValueError("ode_max_steps must be >= 0 or null")
+        raise ValueError("ode_max_steps must be >= 0 (0 or null: no cap)")
+    # 0 means "no cap", as --ode-max-steps 0 on the command line does (one meaning in both places)
     return SweepSpec(d.get("name", "custom"), base, axes, int(d.get("n_y", 8000)), d.get("notes", ""), cr, method, prof,
-                     nz, z_max, None if ms is None else int(ms))
+                     nz, z_max, None if ms is None or int(ms) == 0 else int(ms))
 
 
 def builtin_specs() -> dict:
@@ -535,7 +536,8 @@ def ode_status_summary(counts, group=None, device=None) -> Optional[dict]:
     c = c.cpu().numpy()
     names = {_native.ODE_OK: "ok", _native.ODE_BAD_GRID: "bad_grid", _native.ODE_BAD_STEP: "bad_step",
              _native.ODE_TOO_MANY_STEPS: "too_many_steps", _native.ODE_NEWTON: "newton_failed",
-             _native.ODE_NOT_LINEAR: "not_linear", _native.ODE_UNRESOLVED: "quadrature_unresolved"}
+             _native.ODE_NOT_LINEAR: "not_linear", _native.ODE_UNRESOLVED: "quadrature_unresolved",
+             _native.ODE_BAD_TABLE: "bad_table"}
     return {names.get(k, str(k)): int(v) for k, v in enumerate(c) if v}
 
 

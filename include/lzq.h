@@ -263,6 +263,8 @@ enum lzq_ode_status {
   LZQ_ODE_BAD_STEP = 2,       /* max_step <= 0 (zero-width x range): solve_ivp raises ValueError */
   LZQ_ODE_TOO_MANY_STEPS = 3, /* more than max_steps integration steps: not attempted */
   LZQ_ODE_NOT_LINEAR = 5,     /* internal to lzq_ode_quadrature: Y_chi still to be stepped */
+  LZQ_ODE_BAD_TABLE = 7,      /* the point's spline table was not built by lzq_ode_tables with
+                                 nt = LZQ_ODE_NT (the integrators' knot count; NaN yields) */
   LZQ_ODE_UNRESOLVED = 6,     /* lzq_ode_quadrature: a knot interval needs more than 4096
                                  Gauss sub-intervals to resolve its scales (NaN yields) */
   LZQ_ODE_NEWTON = 4          /* a Radau stage system did not converge: the yields are the
@@ -276,7 +278,9 @@ enum lzq_ode_status {
  * needs): A/V at linspace(T_lo, T_hi, nt) (the quadrature kernels' z-sum on the grid (nz, z_max))
  * and its not-a-knot cubic spline (scipy CubicSpline), into d_work[i * 4 nt ...] (work_doubles >=
  * n * 4 nt; 4 <= nt <= LZQ_ODE_NT_MAX).  The integrators (lzq_ode_integrate*, lzq_ode_quadrature)
- * read tables of nt = LZQ_ODE_NT knots, main()'s build_tables (fpy:387), on any z grid.
+ * read tables of nt = LZQ_ODE_NT knots, main()'s build_tables (fpy:387), on any z grid: a table
+ * records its nt in its last 4 (spare) doubles, and a point whose table holds another nt gets
+ * LZQ_ODE_BAD_TABLE (NaN yields) from them.
  * d_status (optional, [n] int32): LZQ_ODE_BAD_GRID for a window CubicSpline rejects.  d_aov:
  * optional [n] device lzq_aov_params, the A/V kernel of each point's table (bs.aov replaced:
  * y(T) from the point, A/V from the block, fpy:211); NULL = the point's own fields. */

@@ -5,6 +5,7 @@ import os
 
 import numpy as np
 import pytest
+import torch
 
 from conftest import BASE_CFG, GOLDEN, full_cfg, golden, pkg, rel_err
 from oracle import oracle as O
@@ -136,6 +137,36 @@ def test_ode_status_and_step_cap(gpu_engine):
     assert st.cpu().numpy().tolist() == [0, 1, 1, 3]
     t = t.cpu().numpy()
     assert np.isfinite(t[0]).all() and np.isnan(t[1:, :5]).all()
+
+
+def test_ode_table_of_another_knot_count_is_refused(gpu_engine):
+    """lzq_ode_tables builds any nt (build_tables(n=nt)), the integrators read LZQ_ODE_NT-knot tables:
+    tables of another nt are refused per point (LZQ_ODE_BAD_TABLE, NaN yields) by the knot count each
+    table records, in every integrator kernel; main()'s tables still integrate."""
+    import ctypes
+    nat = pkg("_native")
+    cfgs = [full_cfg({**BASE_CFG, "Gamma_wash_over_H": 1.0, **NARROW}),
+            full_cfg({**BASE_CFG, "sigma_v_chi_GeV_m2": 1e-12, **NARROW})]
+    p, o = recs(cfgs)
+    d_p = gpu_engine.points_to_device(p)
+    d_o = torch.from_numpy(np.ascontiguousarray(o).view(np.uint8).copy()).to(gpu_engine.device)
+    for nt, want in ((1600, nat.ODE_BAD_TABLE), (nat.ODE_NT, nat.ODE_OK)):
+        work, st = gpu_engine.ode_tables(d_p, nt=nt)
+        assert (st.cpu().numpy() == 0).all()
+        out = torch.empty((2, 6), dtype=torch.float64, device=gpu_engine.device)
+        status = torch.full((2,), -1, dtype=torch.int32, device=gpu_engine.device)
+        vp = lambda t: ctypes.c_void_p(t.data_ptr())
+        for fn in ("lzq_ode_integrate", "lzq_ode_quadrature"):
+            if fn == "lzq_ode_integrate":
+                rc = gpu_engine.lib.lzq_ode_integrate(vp(d_p), vp(d_o), 2, vp(work), work.numel(), 10**6, vp(out),
+                                                      vp(status), None)
+            else:
+                rc = gpu_engine.lib.lzq_ode_quadrature(vp(d_p), vp(d_o), 2, None, 0, vp(work), work.numel(), 10**6,
+                                                       vp(out), vp(status), None)
+            assert rc == 0
+            torch.cuda.synchronize()
+            assert status.cpu().numpy().tolist() == [want, want], (nt, fn, status)
+            assert np.isnan(out.cpu().numpy()[:, 0]).all() == (want != nat.ODE_OK), (nt, fn)
 
 
 def test_ode_deterministic_and_batch_independent(gpu_engine):

@@ -98,6 +98,13 @@ def test_spec_json_roundtrip():
     assert again.total == 6 and np.array_equal(again.axes[0][1], spec.axes[0][1])
     with pytest.raises(ValueError):
         sw.spec_from_json({"axes": [{"field": "nope", "values": [1]}]})
+    # ode_max_steps: 0 and null both mean "no cap" (as --ode-max-steps 0 does), < 0 is refused
+    ax = [{"field": "I_p", "values": [0.3]}]
+    for ms, want in ((0, None), (None, None), (5000, 5000)):
+        assert sw.spec_from_json({"axes": ax, "ode_max_steps": ms}).ode_max_steps == want, ms
+    assert sw.spec_from_json({"axes": ax}).ode_max_steps == sw.ODE_MAX_STEPS
+    with pytest.raises(ValueError):
+        sw.spec_from_json({"axes": ax, "ode_max_steps": -1})
 
 
 def test_summary_fixed_order():

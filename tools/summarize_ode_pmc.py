@@ -12,6 +12,15 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def integrator(name: str) -> bool:
+    """A dispatch of the Radau integrator: every ode_integrate_kernel<false, ...> variant and, since
+    round 5, the three ode_riccati_kernel passes (each launch runs all of them; each steps its own
+    waves)."""
+    return "ode_integrate_kernel<false" in name or "ode_riccati_kernel" in name
+
+
 CONFIGS = [("narrow_wash", 262144, 20000), ("stiff_thermal", 262144, 25385), ("full_window_wash", 16384, 999800)]
 
 
@@ -31,7 +40,7 @@ def main_cases(src: str, tag: str, fname: str = "ode_pmc.json") -> None:
         disp = defaultdict(dict)
         names = set()
         for r in rows:
-            if "ode_integrate_kernel<false" in r["Kernel_Name"]:
+            if integrator(r["Kernel_Name"]):
                 names.add(r["Kernel_Name"])
                 per = max(per, len(names))
                 d = disp[int(r["Dispatch_Id"])]
@@ -48,7 +57,7 @@ def main_cases(src: str, tag: str, fname: str = "ode_pmc.json") -> None:
     # the optional third pass (integer / conversion / scalar / LDS instructions)
     mix = passes("mix") if os.path.exists(os.path.join(src, "mix", "run_counter_collection.csv")) else None
     tr = [r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv")))
-          if "ode_integrate_kernel<false" in r["Kernel_Name"] and int(r["Grid_Size_X"]) >= N]
+          if integrator(r["Kernel_Name"]) and int(r["Grid_Size_X"]) >= N]
     d1 = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9 for r in tr]
     durs = [sum(d1[j:j + per]) for j in range(0, len(d1), per)]
     assert len(big_p) == len(CASES) and len(durs) == len(CASES), (len(big_p), len(durs))

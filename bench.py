@@ -20,7 +20,7 @@ line through and exits with the launcher's status.  A rank count that disagrees 
 more RCCL ranks than the node has GPUs, is an error (exit status 2), never a 1-GPU line.
 
 Prints one JSON line (rank 0).  `roofline` = the kernel's executed FP64 FLOP (PMC
-instruction mix of profiles/round4, used only if that profile's kernel code hash is the timed
+instruction mix of profiles/round5, used only if that profile's kernel code hash is the timed
 library's) over its HIP-event time in this run, against the 78.6 TFLOP/s FP64 vector peak, with
 the FP64-pipe and VALU issue fractions beside it; `kernel_ms` / `allgather_ms` decompose a step
 per rank (min / max / mean); `parity_spot` checks 64 rows of the last timed step's table against
@@ -62,7 +62,7 @@ BASE = {  # /root/reference/yields_config_equal_mass.json
 }
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "round4", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "round5", "pmc_summary.json")
 WAVE_NODES_PER_POINT = 8000 * 1200 // 64
 
 
@@ -89,7 +89,7 @@ def roofline(points_per_launch: int, kern_ms: float) -> dict:
     """FP64 VALU roofline of yields_grid_kernel for this run.
 
     achieved = EXECUTED FP64 FLOP per launch / this run's HIP-event kernel time.  The executed
-    FLOP per point come from the rocprofv3 PMC pass of the same build (profiles/round4, tools/
+    FLOP per point come from the rocprofv3 PMC pass of the same build (profiles/round5, tools/
     gpu_profile.sh): (2 x SQ_INSTS_VALU_FMA_F64 + SQ_INSTS_VALU_MUL_F64 + SQ_INSTS_VALU_ADD_F64)
     x 64 lanes / points; peak = 78.6 TFLOP/s (256 CU x 2.4 GHz x 128 FP64 FLOP/clk/CU, every
     issue slot an FMA).  Also reported: the FP64 pipe's busy fraction (FP64 instructions x 4

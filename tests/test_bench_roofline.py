@@ -14,7 +14,7 @@ from conftest import ROOT
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
-PROF = os.path.dirname(bench.PMC_SUMMARY)   # this round's committed profile (profiles/round4)
+PROF = os.path.dirname(bench.PMC_SUMMARY)   # this round's committed profile (profiles/round5)
 
 
 def counters(path, kernel="yields_grid_kernel"):

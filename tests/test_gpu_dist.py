@@ -72,7 +72,7 @@ def test_bench_multi_rank_gloo(world):
     assert r["n_gpus"] == world and r["config"]["global_points_per_step"] == 20000 * world
     assert r["value"] > 0 and r["unit"] == "points/s" and r["scaling"] == "weak"
     assert abs(r["value"] - 20000 * world / (r["ms_per_step"] / 1e3)) <= 1e-6 * r["value"]
-    assert "cpu_baseline" not in r   # rank 0 at N = 1 only
+    assert r["cpu_baseline"]["value"] > 0 and r["cpu_baseline"]["kind"] == "port"   # rank 0, at every N
 
 
 def test_bench_single_rank_line():

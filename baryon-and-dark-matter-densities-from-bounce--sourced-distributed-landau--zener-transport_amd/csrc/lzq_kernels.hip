@@ -5,7 +5,7 @@
 //   A/V(y) = pref(y) * trapz_z[ z^2 e^-z exp(c(y) g4(z)) ]          fpy:158-165
 // with 8000 y-nodes x 1200 z-nodes per parameter point.
 //
-// Mapping (DESIGN.md §5.1):
+// Mapping (DESIGN.md §4.1):
 //   * one 64-lane wavefront owns one parameter point; lane l takes y-nodes l, l+64, ...;
 //     no barriers (besides staging the exp table) and no atomics; 16 independent wavefronts
 //     per 1024-thread block, two blocks per CU (8 waves per SIMD);

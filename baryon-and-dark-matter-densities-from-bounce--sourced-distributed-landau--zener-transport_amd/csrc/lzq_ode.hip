@@ -607,7 +607,7 @@ __device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st
   // A^-1_jj + 2 h lam_j Z_j: its adjugate is one fma per entry against constant products
   // (kRadauAinvP), and the h-scaled stage data h lam_j, 2 h lam_j, h S_j are formed once per step.
   // Same fixed point (the stage equations), ~20 FP64 instructions fewer per iteration than
-  // forming I - hA diag(jf) and its full adjugate (DESIGN §5.3).
+  // forming I - hA diag(jf) and its full adjugate (DESIGN §4.3).
   double hl[3], hl2[3], hS[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
@@ -1066,7 +1066,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
     // launch's range (the window does not reach T = m/3, or the split lies in another
     // continuation launch), the <kNoSplit> variant steps the wave: the same operations with the
     // split paths compiled out, whose mere presence costs ~11% of a stiff / Riccati step
-    // (register pressure; DESIGN §5.3).  Both variants evaluate the same wave-uniform predicate.
+    // (register pressure; DESIGN §4.3).  Both variants evaluate the same wave-uniform predicate.
     if (!kLin && LZQ_ODE_NOSPLITVAR) {
       const bool lane_ns = k_split == INT64_MAX || (k_split >= 0 && (k_split + 1 < k_begin || k_split >= k_stop));
       if (__all(lane_ns) != kNoSplit) return;

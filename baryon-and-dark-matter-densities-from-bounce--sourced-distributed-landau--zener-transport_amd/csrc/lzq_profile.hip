@@ -729,7 +729,7 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_flat_k
   P_out[i] = 1.0 - (a.re * a.re + a.im * a.im) / norm;
 }
 
-int g_profile_flat = 0;  // lzq_tune(LZQ_TUNE_PROFILE_FLAT): the interval loop is the default (DESIGN §6b)
+int g_profile_flat = 0;  // lzq_tune(LZQ_TUNE_PROFILE_FLAT): the interval loop is the default (DESIGN §4.5)
 
 }  // namespace lzq
 

@@ -2,7 +2,7 @@
 // per-point setup, the z-sum inner loop, the one-wavefront-per-point y-loop and the epilogue,
 // shared by the translation units that launch it (lzq_kernels.hip: the headline kernels;
 // lzq_aov.hip: the kernels whose A/V kernel has parameters of its own, fpy:141-151, 197).
-// Not ABI.  The design notes are in lzq_kernels.hip's header comment and DESIGN.md §5.1.
+// Not ABI.  The design notes are in lzq_kernels.hip's header comment and DESIGN.md §4.1.
 #pragma once
 #include <hip/hip_runtime.h>
 

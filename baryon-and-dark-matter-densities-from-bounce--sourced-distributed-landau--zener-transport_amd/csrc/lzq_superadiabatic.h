@@ -1,4 +1,4 @@
-// lzq_superadiabatic.h -- superadiabatic frames of a two-level crossing (DESIGN.md §6), shared
+// lzq_superadiabatic.h -- superadiabatic frames of a two-level crossing (DESIGN.md §4.4), shared
 // device code of the LZ propagator.  Not ABI.  tests/lz_ref.py (sa_levels, sa_to_frame,
 // sa_from_frame, sa_phase, sa_core_tau) restates every function here.
 //

@@ -70,7 +70,7 @@ class Engine:
 
     def tune_profile_flat(self, on: bool) -> bool:
         """lzq_lz_propagate_profile's flattened propagation (include/lzq.h LZQ_TUNE_PROFILE_FLAT; off by
-        default -- the interval loop in keyed launch order is faster, DESIGN §6b -- bit-identical P
+        default -- the interval loop in keyed launch order is faster, DESIGN §4.5 -- bit-identical P
         either way).  Returns the previous setting."""
         prev = self.lib.lzq_tune(_native.TUNE_PROFILE_FLAT, 1 if on else 0)
         if prev < 0:
@@ -353,7 +353,7 @@ class Engine:
                         "lzq ODE: %d of %d points differ in the A/V kernel or window (ODE_TABLE_KEY: %s): a spline "
                         "table per point (an A/V z-sum table build each; the integration still shares stage rows "
                         "across tables) -- ~2.6x the cost per point of a shared-table sweep on a 20000-step "
-                        "window (DESIGN §5.3)", c1 - c0, c1 - c0, ", ".join(_native.ODE_TABLE_KEY))
+                        "window (DESIGN §4.3)", c1 - c0, c1 - c0, ", ".join(_native.ODE_TABLE_KEY))
             plan.append((c0, c1, d_pts, d_ode, d_rep, d_idx, n_tab, d_aov))
             keep.append((d_pts, d_ode, d_rep, d_idx, d_aov))
         # Two or more chunks: chunk c + 1's spline tables are built on a side stream into the other

@@ -50,7 +50,7 @@ EQUAL_MASS = {  # /root/reference/yields_config_equal_mass.json
 @dataclass
 class CrossingSpec:
     """Multi-crossing bounce profile per grid point (BASELINE config C5; no reference
-    counterpart, DESIGN.md §6).  Crossing c of the point with grid values (m_mix, |Delta'|)
+    counterpart, DESIGN.md §4.4).  Crossing c of the point with grid values (m_mix, |Delta'|)
     has m_c = m_mix (1 + jitter a_c), |Delta'_c| = |Delta'| (1 + jitter b_c) and position
     xi_c = L (spacing_lz c + jitter d_c), L = sqrt(v_w/|Delta'|) max(1, sqrt(delta)), with
     (a, b, d) ~ U(-1, 1) drawn once from numpy default_rng(seed).  P is the coherent
@@ -59,7 +59,7 @@ class CrossingSpec:
     spacing_lz: float = 40.0
     jitter: float = 0.1
     window_lz: float = 20.0
-    steps: int = 64        # Magnus steps per crossing core (floor): <= 1e-10 from the exact solution (DESIGN.md §6)
+    steps: int = 64        # Magnus steps per crossing core (floor): <= 1e-10 from the exact solution (DESIGN.md §4.4)
     seed: int = 5
 
     def pattern(self) -> np.ndarray:

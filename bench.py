@@ -150,7 +150,7 @@ def roofline(points_per_launch: int, kern_ms: float) -> dict:
         "note": "frac = executed FP64 FLOP (PMC instruction mix, FMA = 2) / kernel time / FP64 vector peak. "
                 "It is below 1 because MUL/ADD fill a 2-FLOP slot with 1 FLOP and the per-node integer "
                 "table address / exponent insert (and the range clamp) take VALU issue slots "
-                "(DESIGN.md §5.1). fp64_pipe_busy_frac counts every FP64 instruction as a full slot; "
+                "(DESIGN.md §4.1). fp64_pipe_busy_frac counts every FP64 instruction as a full slot; "
                 "valu_issue_busy_frac adds the other VALU instructions at 2 cycles: the kernel is at its "
                 "formulation's issue ceiling, so the lever left is instruction count. The counters are "
                 "used only when their profile's kernel code hash (machine code + descriptors + metadata "

@@ -167,7 +167,7 @@ int lzq_ztables(int32_t nz, double z_max, double* z, double* gamma4, double* ome
 /* LZQ_TUNE_PROFILE_FLAT (1 = on; 0 = off, the default): lzq_lz_propagate_profile's flattened
  * propagation (the step rule for all of a point's knot intervals ahead of the propagation, then one
  * loop of Magnus steps per lane, a lane entering its next interval while the others step) or the
- * interval-by-interval loop in keyed launch order (measured faster, DESIGN §6b).  P is
+ * interval-by-interval loop in keyed launch order (measured faster, DESIGN §4.5).  P is
  * bit-identical either way (tests/test_gpu_profile.py). */
 enum lzq_tune_key { LZQ_TUNE_EXP = 0, LZQ_TUNE_TRUNCATE = 1, LZQ_TUNE_ODE_COOP = 2, LZQ_TUNE_ODE_LAUNCH_STEPS = 3,
                     LZQ_TUNE_PROFILE_FLAT = 4 };
@@ -362,7 +362,7 @@ int lzq_ode_rhs(const lzq_point* pt, const lzq_ode_params* ode, double T_lo, dou
  * where "dressed" = second-order superadiabatic state of the outer cell (the adiabatic state
  * carried in from / out to infinity).  For one crossing this is 1 - exp(-2 pi delta)
  * (fpy:183-184, PAPER eq.(9)) to <= 1e-8 relative at window_lz = 20 for any steps_per_crossing;
- * DESIGN.md §6 states the window / step tolerances (the C5 default is steps_per_crossing = 64).
+ * DESIGN.md §4.4 states the window / step tolerances (the C5 default is steps_per_crossing = 64).
  * Scratch from hipMallocAsync on `stream`, freed stream-ordered: 80 bytes per (point, crossing)
  * for the follow matrices (lz_follow_kernel; batches beyond 2^23 pairs run in slices) and, for
  * n >= 16384 points, 8n bytes for the longest-first launch order (points binned by their step
@@ -423,7 +423,7 @@ int lzq_profile_crossings(const double* d_knots, const double* d_coef, int32_t n
  * max(min_steps, ceil(steps_per_radian x duration x max(E, 4 sqrt|dH/dt|))) uniform steps.
  * 0.5 <= steps_per_radian <= 1000 and 1 <= min_steps <= 1e6 (else LZQ_EINVAL); a point with
  * v_w <= 0, a bad shape index or more than 2^24 steps in one interval gets P = NaN.  For one
- * linear crossing in a wide window P -> eq.(9).  Accuracy (DESIGN.md §6b): the error falls as
+ * linear crossing in a wide window P -> eq.(9).  Accuracy (DESIGN.md §4.5): the error falls as
  * steps_per_radian^-6; at 3 it is within 9.2e-10 of the exact (Weber) solutions of
  * lzq_lz_propagate's piecewise-linear model and up to ~1e-8 on coarse smooth profiles, at 4 (the
  * package default) <= ~1e-9. 

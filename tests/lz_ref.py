@@ -3,7 +3,7 @@ csrc/lzq_propagator.hip (TEST INFRASTRUCTURE).
 
 The reference has no propagator, so parity is UNPINNED beyond the single-
 crossing limit, which must reproduce the reference's closed form P = 1 - exp(-2 pi delta)
-(fpy:183-184, PAPER eqs.(8)-(9)).  This module restates the same model (DESIGN.md §6) with
+(fpy:183-184, PAPER eqs.(8)-(9)).  This module restates the same model (DESIGN.md §4.4) with
 the same eighth-order Magnus scheme, step by step, so the GPU kernel can be checked against
 it to rounding, and the scheme itself against the closed form.  Start state and final
 projection are the second-order dressed (superadiabatic) chi-like states of the outer cells.

@@ -104,7 +104,7 @@ def test_host_side_argument_validation():
     assert rc == 0
     rc = L.lzq_lz_propagate(None, None, None, 4, 0, 0.3, 1.0, 10, None, None)
     assert rc == -1
-    # bounded windows / steps (a cell's step count is bounded by its core; DESIGN.md §6)
+    # bounded windows / steps (a cell's step count is bounded by its core; DESIGN.md §4.4)
     for K, S in ((300.0, 1000), (20.0, 2_000_000), (float("nan"), 1000)):
         rc = L.lzq_lz_propagate(8, 8, 8, 1, 1, 0.3, K, S, 8, None)
         assert rc == -1 and b"window_lz <= 200" in L.lzq_last_error(), (K, S)

@@ -51,7 +51,7 @@ def test_cli_stiff_cases_documented_divergence(case, tmp_path, gpu_engine):
     Radau gives up at the T = m/3 jump: the reference CLI prints `[warn] ODE solver reported
     failure: ...` (fpy:408-409) and reports the state where it stopped (fpy:410), Y_B ~68x below
     the converged one.  lzq splits the straddling fixed step at the branch point and integrates
-    through (DESIGN §5.3, INTEGRATION.md): its stdout is the reference's without the [warn] line,
+    through (DESIGN §4.3, INTEGRATION.md): its stdout is the reference's without the [warn] line,
     with the same result block layout, and its finals are the converged solution of the
     reference's own equations (golden_ode_stiff.json, two-piece rtol-1e-12 solve)."""
     import re

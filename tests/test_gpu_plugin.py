@@ -100,7 +100,7 @@ def test_shipped_module_multi_crossing_and_profile(tmp_path, plugin_path, gpu_en
     # them (slopes +0.5, -0.3, +0.7), m_mix constant per crossing neighbourhood
     xs = np.linspace(-40.0, 150.0, 3801)
     D = np.where(xs < 22.5, 0.5 * (xs - 0.0), np.where(xs < 95.0, -0.3 * (xs - 60.0), 0.7 * (xs - 110.0)))
-    # Delta is continuous at the joins, which are the model's turning points (DESIGN.md §6)
+    # Delta is continuous at the joins, which are the model's turning points (DESIGN.md §4.4)
     assert abs(0.5 * 22.5 - (-0.3) * (22.5 - 60.0)) < 1e-12 and abs(-0.3 * (95.0 - 60.0) - 0.7 * (95.0 - 110.0)) < 1e-12
     mm = np.where(xs < 22.5, 0.05, np.where(xs < 95.0, 0.08, 0.04))
     body = "xi,Delta,m_mix\n" + "".join(f"{float(a)!r},{float(b)!r},{float(c)!r}\n" for a, b, c in zip(xs, D, mm))

@@ -202,7 +202,7 @@ def test_piecewise_linear_profile_matches_lz_propagate(gpu_engine):
 def test_weber_fixtures_default_steps(gpu_engine):
     """All 53 exact Weber-function solutions at 3 steps per radian: <= 2e-9 (measured 9.2e-10;
     lzq_lz_propagate at the C5 default: 7.2e-10); at the default 4: <= 2.5e-10 (measured 1.64e-10;
-    4.9e-10 while the step midpoint was a running sum, DESIGN §6b)."""
+    4.9e-10 while the step midpoint was a running sum, DESIGN §4.5)."""
     worst, worst4 = 0.0, 0.0
     for c in WEBER["cases"]:
         P4 = float(_profile_P(gpu_engine, c, 4.0).cpu().numpy()[0])

@@ -148,7 +148,7 @@ def test_golden_zgrid_tables_and_rhs():
 def test_golden_zgrid_ode():
     """main()'s ODE fallback with bs.aov on non-default grids: the reference's adaptive Radau vs the
     oracle's fixed-step Radau (narrow wash-out windows, where the reference sits ~1e-13 from its
-    converged solution, DESIGN §5.3)."""
+    converged solution, DESIGN §4.3)."""
     for r in _zgrid_cases()["ode"]:
         assert r["success"]
         o = O.ode_point(full_cfg(r["config"]), nz=r["nz"], z_max=r["z_max"])

@@ -1,4 +1,4 @@
-"""The Magnus scheme of the LZ propagator (DESIGN.md §6) against the reference's closed form
+"""The Magnus scheme of the LZ propagator (DESIGN.md §4.4) against the reference's closed form
 in the single-crossing limit, on CPU (numpy restatement tests/lz_ref.py).  With the
 second-order dressed edge states the finite window costs ~2e-9 relative at K = 20 LZ lengths
 (falling as ~K^-7), inside north_star's 1e-8 on P_LZ."""

@@ -36,7 +36,7 @@ def _worker(rank, world, port, total, chunk, out_dir, res_path, rows_per_round=1
     s, e = sw.shard_range(total, rank, world)
     local = sw.run_local(fake_compute, s, e, lambda n: torch.empty((n, 6), dtype=torch.float64), chunk, out_dir)
     table = sw.gather_table(local, total, rank, world, rows_per_round=rows_per_round)
-    # every rank holds the whole table (DESIGN.md §7)
+    # every rank holds the whole table (DESIGN.md §6)
     np.save(res_path + f".{rank}.npy", table.numpy())
     dist.destroy_process_group()
 

@@ -2,7 +2,7 @@
 Weber (parabolic-cylinder) functions, in mpmath (TEST INFRASTRUCTURE; SURVEY §8f(2)
 "validation ... against the exact finite-time Weber-function solution").
 
-Model (DESIGN.md §6): i dpsi/dt = H psi, t = xi / v_w, H = Delta(xi) sigma_z + m_c sigma_x with
+Model (DESIGN.md §4.4): i dpsi/dt = H psi, t = xi / v_w, H = Delta(xi) sigma_z + m_c sigma_x with
 Delta = s_c |Delta'_c| (xi - xi_c) on cell c.  On one cell, with tau = t - t_c and
 alpha = s_c |Delta'_c| v_w, the lower component obeys
 

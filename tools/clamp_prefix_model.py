@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""What a clamp-free prefix would save in the headline kernel (VERDICT r3 item 5; DESIGN §8.1).
+"""What a clamp-free prefix would save in the headline kernel (VERDICT r3 item 5; DESIGN §8).
 
 The z-loop's range clamp (one v_max_f64 per node) runs on the passes where some lane's exponent
 can leave the table's range, c2 g4_max < KMIN (KMIN = -1506 octaves x N).  Since c2 g4_k falls

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Symbolic derivation of the Magnus vector used by csrc/lzq_propagator.hip (DESIGN.md §6).
+"""Symbolic derivation of the Magnus vector used by csrc/lzq_propagator.hip (DESIGN.md §4.4).
 
 H(t) = m sx + (D + Dd t) sz on a step t in [-h/2, h/2] (D at the midpoint, Dd = dD/dt).  The
 Dyson series of U is built to h^8, then the SU(2) logarithm U = exp(-i n.sigma) is taken as a

@@ -83,7 +83,7 @@ LZQ_NZ, LZQ_Z_MAX = 1200, 30.0  # fpy:142 AoverVKernel defaults, main()'s grid (
 LZQ_NZ_MAX = 1 << 22
 ODE_NT_MAX = 1 << 20
 REUSE_TABLE_HEADER = 6  # LZQ_REUSE_TABLE_HEADER
-TUNE_EXP, TUNE_TRUNCATE, TUNE_ODE_COOP, TUNE_ODE_LAUNCH_STEPS, TUNE_PROFILE_FLAT = 0, 1, 2, 3, 4  # enum lzq_tune_key
+TUNE_EXP, TUNE_TRUNCATE, TUNE_ODE_COOP, TUNE_ODE_LAUNCH_STEPS, TUNE_PROFILE_FLAT, TUNE_ODE_TP_INTERVAL = 0, 1, 2, 3, 4, 5  # enum lzq_tune_key
 ODE_MAX_LAUNCHES = 65536  # lzq_ode_*: max_steps <= 65536 x 2^(launch log2)
 # tuning state that changes result bits (the inner-loop exponential, ~1e-14): part of the
 # sweep checkpoint key (sweep.spec_key); Engine.tune_exp keeps it current
@@ -122,7 +122,7 @@ EXPORTS = ("lzq_abi_version", "lzq_last_error", "lzq_init", "lzq_zgrid_init", "l
            "lzq_jchi_batch", "lzq_yields_batch", "lzq_sweep_grid", "lzq_sweep_grid_reuse_workspace",
            "lzq_sweep_grid_reuse", "lzq_sweep_grid_ztables", "lzq_sweep_grid_from_ztables",
            "lzq_yields_batch_reuse", "lzq_p_closed_form",
-           "lzq_lz_propagate", "lzq_lz_propagate_v", "lzq_ode_tables", "lzq_ode_integrate", "lzq_ode_integrate_shared", "lzq_ode_quadrature", "lzq_ode_batch",
+           "lzq_lz_propagate", "lzq_lz_propagate_v", "lzq_ode_tables", "lzq_ode_integrate", "lzq_ode_integrate_shared", "lzq_ode_integrate_tp", "lzq_ode_quadrature", "lzq_ode_batch",
            "lzq_ode_aov_T", "lzq_ode_rhs", "lzq_profile_splines", "lzq_profile_crossings",
            "lzq_lz_propagate_profile")
 # the lzq_point fields an ODE spline table depends on (A/V kernel fpy:141-156 + window fpy:368-369)
@@ -186,6 +186,7 @@ def load(path: str | None = None):
     L.lzq_ode_tables.argtypes = [vp, i64, vp, vp, i32, i32, d, vp, vp, i64, vp, vp]
     L.lzq_ode_integrate.argtypes = [vp, vp, i64, vp, i64, i64, vp, vp, vp]
     L.lzq_ode_integrate_shared.argtypes = [vp, vp, i64, vp, i64, vp, i64, i64, vp, vp, vp]
+    L.lzq_ode_integrate_tp.argtypes = [vp, vp, i64, vp, i64, vp, i64, i64, vp, vp, vp, vp]
     L.lzq_ode_quadrature.argtypes = [vp, vp, i64, vp, i64, vp, i64, i64, vp, vp, vp]
     L.lzq_ode_batch.argtypes = [vp, vp, i64, i32, d, vp, vp, i64, i64, vp, vp, vp]
     L.lzq_ode_aov_T.argtypes = [P(LzqPoint), d, d, i32, vp, vp, i64, vp, vp]

@@ -44,6 +44,7 @@ int launch_bin_order(const int32_t* bins, const int32_t* hist, int32_t* offs, in
 // lzq_tune(LZQ_TUNE_ODE_COOP) / (LZQ_TUNE_ODE_LAUNCH_STEPS) state, read by lzq_ode.hip's launches
 extern int g_ode_coop;
 extern int g_ode_launch_log2;
+extern int g_ode_tp_interval;  // lzq_tune(LZQ_TUNE_ODE_TP_INTERVAL): steps per lzq_ode_integrate_tp interval
 // lzq_tune(LZQ_TUNE_PROFILE_FLAT) state, read by lzq_profile.hip's launch
 extern int g_profile_flat;
 

@@ -619,6 +619,13 @@ int lzq_tune(int32_t key, int32_t value) {
     lzq::g_profile_flat = value;
     return prev;
   }
+  if (key == LZQ_TUNE_ODE_TP_INTERVAL) {
+    if (value < 8 || value > (1 << 20))
+      return fail(LZQ_EINVAL, "lzq_tune: ode_tp_interval must be in [8, 2^20] steps, got %d", value);
+    int prev = lzq::g_ode_tp_interval;
+    lzq::g_ode_tp_interval = value;
+    return prev;
+  }
   if (key == LZQ_TUNE_ODE_COOP) {
     if (value != 0 && value != 1) return fail(LZQ_EINVAL, "lzq_tune: ode_coop must be 0 or 1, got %d", value);
     int prev = lzq::g_ode_coop;

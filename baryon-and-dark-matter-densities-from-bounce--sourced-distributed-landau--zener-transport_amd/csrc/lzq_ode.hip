@@ -32,6 +32,7 @@ namespace lzq {
 constexpr int kOdeBlock = 256;
 int g_ode_coop = 1;          // lzq_tune(LZQ_TUNE_ODE_COOP)
 int g_ode_launch_log2 = 24;  // lzq_tune(LZQ_TUNE_ODE_LAUNCH_STEPS): <= 2^24 Radau steps per launch
+int g_ode_tp_interval = 64;  // lzq_tune(LZQ_TUNE_ODE_TP_INTERVAL): steps per lzq_ode_integrate_tp interval
 constexpr double kInvMplGeV = 1.0 / kMplGeV;
 
 // ---------------------------------------------------------------------------------------
@@ -895,7 +896,8 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
                                                                   lzq_yield* __restrict__ out,
                                                                   int32_t* __restrict__ status, int coop_on,
                                                                   int64_t k_lo, int64_t k_cnt,
-                                                                  OdeState* __restrict__ state) {
+                                                                  OdeState* __restrict__ state,
+                                                                  const int32_t* __restrict__ skip) {
   __shared__ StageBase s_base[kOdeBlock / 64][64][3];  // cooperative mode
   // shared Y_B step maps, (c, d) and the cofactor weights in separate arrays: the linear waves'
   // tight loop streams 16-B (c, d) rows
@@ -909,6 +911,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
   const int64_t i_self = (int64_t)blockIdx.x * kOdeBlock + threadIdx.x;
   const bool real = i_self < n;
   const int64_t i = real ? i_self : wave0;
+  if (skip && skip[i]) return;  // integrated by lzq_ode_integrate_tp's iteration
   const bool cont = state != nullptr, first = !cont || k_lo == 0;
   if (cont && !first && state[i].status != kOdeInProgress) return;  // finished in an earlier launch
   const lzq_point pt = pts[i];
@@ -1318,7 +1321,8 @@ template <int kPhase>
 __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) void ode_riccati_kernel(
     const lzq_point* __restrict__ pts, const lzq_ode_params* __restrict__ ode, int64_t n,
     const int32_t* __restrict__ tidx, const double* __restrict__ ws, int64_t max_steps, lzq_yield* __restrict__ out,
-    int32_t* __restrict__ status, int coop_on, int64_t k_lo, int64_t k_cnt, OdeState* __restrict__ state) {
+    int32_t* __restrict__ status, int coop_on, int64_t k_lo, int64_t k_cnt, OdeState* __restrict__ state,
+    const int32_t* __restrict__ skip) {
   __shared__ RicRow s_row[kOdeBlock / 64][64];
   __shared__ YbCD s_rcd[kOdeBlock / 64][64];
   __shared__ OdePoint s_pt[kOdeBlock / 64];
@@ -1331,6 +1335,7 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
   const int64_t i_self = (int64_t)blockIdx.x * kOdeBlock + threadIdx.x;
   const bool real = i_self < n;
   const int64_t i = real ? i_self : wave0;
+  if (skip && skip[i]) return;
   const bool cont = state != nullptr, first = kPhase == 0 && (!cont || k_lo == 0);
   if (kPhase > 0 && !cont) return;  // passes 1 and 2 continue from pass 0's state
   if (cont && !first && state[i].status != kOdeInProgress) return;
@@ -1589,6 +1594,361 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
 }
 
 // ---------------------------------------------------------------------------------------
+// Time-parallel integration of a few points (lzq_ode_integrate_tp): multiple shooting.
+// A point's N fixed steps are cut into M intervals of L steps; node m holds the integrator's
+// state at the start of interval m (Y_chi, Y_B and the predictor's data).  Each iteration
+// (1) integrates every interval from its node, one lane per interval, with the per-lane steps
+// of ode_integrate_kernel (same stages, Y_B step map, Radau step, split step, predictor), and
+// records the end state F_m and its derivatives D_m = dY_chi_end/dY_chi_start (the product of
+// the steps' dZ_3/dY_0, the implicit function theorem on the converged stage system) and
+// C_m = dY_B_end/dY_B_start (the product of the Y_B step maps' c); (2) applies Newton's update to
+// the nodes: with residuals r_m = F_m - s_{m+1}, the corrections solve the linear recurrence
+// d_{m+1} = D_m d_m + r_m, d_0 = 0 -- a block scan of affine maps.  Node M is the point's final
+// state.  Y_B's recurrence is affine (one update makes it exact up to rounding); Y_chi's is the
+// Riccati map, for which Newton converges quadratically once the nodes are close.  The fixed
+// point is the sequential trajectory: at convergence every node is its interval predecessor's
+// end state, so the result differs from ode_integrate_kernel's only by rounding (the nodes are
+// formed as s + d instead of being carried), which the contractive or neutral dynamics keep at
+// the ~1e-14 level (tests/test_gpu_ode_tp.py).  A point whose iteration does not converge within
+// the budget, or one whose interval hits a Newton failure, is integrated sequentially instead.
+// ---------------------------------------------------------------------------------------
+struct TpNode {  // the integrator's state at the start of an interval
+  double Ychi, YB, Yp, Z[3];
+  int32_t have, pad;
+};
+struct TpEnd {  // an interval's end state from its start node, and its derivatives
+  double Ychi, YB, Yp, Z[3];
+  double D;  // dY_chi(end) / dY_chi(start)
+  double C;  // dY_B(end) / dY_B(start)
+  int32_t have;
+  int32_t exact;  // every step took the Radau step (0: a Newton failure was bridged, see tp_bridge)
+};
+struct TpCtl {
+  int64_t N, M;     // the point's steps and intervals
+  double err;       // the last update's largest relative correction
+  int32_t phase;    // kTpIter, kTpDone (converged; node M is the result), kTpFallback (sequential path)
+  int32_t iters;    // Newton updates applied
+  int32_t riccati;  // sigma_v != 0: Y_chi's map is nonlinear (the update is safeguarded)
+  int32_t pad;
+};
+constexpr int32_t kTpIter = 0, kTpDone = 1, kTpFallback = 2;
+
+// ode_integrate_kernel's prologue, in its order: status, window, step count, h, initial Y_chi.
+struct OdeSetup {
+  OdePoint o;
+  double x0, x1, h, Ychi0;
+  int64_t N;
+  int st;
+};
+__device__ __forceinline__ OdeSetup ode_setup(const lzq_point& pt, const lzq_ode_params& od, const double* w,
+                                              int64_t max_steps) {
+  OdeSetup S;
+  S.o = ode_point(pt, od);
+  const OdePoint& o = S.o;
+  S.st = ode_grid_ok(o.T_lo, o.T_hi, o.stepT) ? (ode_table_ok(w) ? LZQ_ODE_OK : LZQ_ODE_BAD_TABLE) : LZQ_ODE_BAD_GRID;
+  const double m = o.m, T_p = o.Tp;
+  S.x0 = m / o.T_hi;
+  S.x1 = m / pymax(o.T_lo, 1e-30);
+  if (pt.regime == LZQ_NONTHERMAL) {
+    if (pt.has_Y_chi_init) S.Ychi0 = pt.Y_chi_init;
+    else if (pt.has_n_chi_at_Tp) S.Ychi0 = pt.n_chi_at_Tp_GeV3 / pymax(s_entropy(T_p, pt.g_star_s), 1e-300);
+    else S.Ychi0 = 1.0e-12;
+  } else {
+    S.Ychi0 = n_chi_eq(o.T_hi, m, pt.g_chi, pt.stats) / s_entropy(o.T_hi, pt.g_star_s);
+  }
+  const double x_p = m / pymax(T_p, 1e-30);
+  const double max_step = pymin(pymin(fabs(S.x1 - S.x0) / 20000.0, x_p / 1000.0), 5e-4);
+  double steps = 0.0;
+  if (S.st == LZQ_ODE_OK) {
+    if (!(max_step > 0.0)) S.st = LZQ_ODE_BAD_STEP;
+    else {
+      steps = ceil(fabs(S.x1 - S.x0) / max_step);
+      if (!(steps <= (double)max_steps)) S.st = LZQ_ODE_TOO_MANY_STEPS;
+    }
+  }
+  S.N = S.st == LZQ_ODE_OK ? (int64_t)steps : 0;
+  S.h = S.N > 0 ? (S.x1 - S.x0) / (double)S.N : 0.0;
+  return S;
+}
+
+// dZ_3/dY_0 of a converged Riccati stage system Z = Y_0 1 + hA f(Z), f_j = -lam_j (Z_j^2 - E2_j) - S_j:
+// (A^-1 + diag(2 h lam_j Z_j)) dZ = A^-1 1, the transformed Newton matrix of radau_step.
+__device__ __forceinline__ double tp_dz3(double h, const OdeStage (&sg)[3], const double (&Z)[3]) {
+  double k[3], q[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    k[j] = kRadauAinv[j][j] + 2.0 * (h * sg[j].lam) * Z[j];
+    q[j] = (kRadauAinv[j][0] + kRadauAinv[j][1]) + kRadauAinv[j][2];
+  }
+  const double a01 = kRadauAinv[0][1], a02 = kRadauAinv[0][2], a10 = kRadauAinv[1][0];
+  const double a12 = kRadauAinv[1][2], a20 = kRadauAinv[2][0], a21 = kRadauAinv[2][1];
+  const double b20 = a10 * a21 - k[1] * a20, b21 = a01 * a20 - k[0] * a21, b22 = k[0] * k[1] - a01 * a10;
+  const double b00 = k[1] * k[2] - a12 * a21, b10 = a12 * a20 - a10 * k[2];
+  const double det = k[0] * b00 + a01 * b10 + a02 * b20;
+  const double dz = (b20 * q[0] + b21 * q[1] + b22 * q[2]) / det;
+  return isfinite(dz) ? dz : 0.0;  // overflowing stiff stages: the map contracts there
+}
+
+// One block per point: ctl, and every node at the initial state (node 0 is ode_integrate_kernel's
+// start; the others are the first guess).  Points the iteration does not take (a status other
+// than OK, fewer than two intervals) go to the fallback.
+__global__ __launch_bounds__(256) void ode_tp_init_kernel(const lzq_point* __restrict__ pts,
+                                                          const lzq_ode_params* __restrict__ ode,
+                                                          const int32_t* __restrict__ tidx,
+                                                          const double* __restrict__ ws, int64_t max_steps, int64_t L,
+                                                          int64_t Mmax, TpNode* __restrict__ nodes,
+                                                          TpCtl* __restrict__ ctl) {
+  const int64_t p = blockIdx.x;
+  const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
+  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
+  const int64_t M = S.st == LZQ_ODE_OK ? (S.N + L - 1) / L : 0;
+  const bool go = S.st == LZQ_ODE_OK && M >= 2 && M <= Mmax;
+  if (threadIdx.x == 0) ctl[p] = TpCtl{S.N, M, 0.0, go ? kTpIter : kTpFallback, 0, S.o.sigmav != 0.0 ? 1 : 0, 0};
+  if (!go) return;
+  TpNode* nd = nodes + p * (Mmax + 1);
+  for (int64_t m = threadIdx.x; m <= M; m += blockDim.x)
+    nd[m] = TpNode{S.Ychi0, 0.0, S.Ychi0, {S.Ychi0, S.Ychi0, S.Ychi0}, 0, 0};
+}
+
+// A Riccati step whose Newton iteration fails -- possible only from a start far above the
+// trajectory, as in the first iterations -- is bridged by backward Euler at the step's end,
+// Y1 = Y0 - h lam (Y1^2 - E2) - h S, whose positive root 2c / (1 + sqrt(1 + 4 h lam c)),
+// c = Y0 + h lam E2 - h S, exists for every start (unconditionally stable, no iteration): the
+// interval still returns an end state and a derivative to improve the nodes with, and is marked
+// inexact, so the iteration cannot converge while any interval needs the bridge.
+__device__ __forceinline__ double tp_bridge(double Y0, double h, const OdeStage& s3, double& dY1) {
+  const double hl = h * s3.lam;
+  const double c = Y0 + hl * s3.E2 - h * s3.S;
+  const double q = sqrt(pymax(1.0 + 4.0 * hl * c, 0.0));
+  dY1 = 1.0 / pymax(q, 1e-300);
+  return 2.0 * c / (1.0 + q);
+}
+
+// One lane per (point, interval): F_m, D_m, C_m from node m (ode_integrate_kernel's per-lane steps).
+__global__ __launch_bounds__(64) void ode_tp_interval_kernel(const lzq_point* __restrict__ pts,
+                                                             const lzq_ode_params* __restrict__ ode, int64_t n,
+                                                             const int32_t* __restrict__ tidx,
+                                                             const double* __restrict__ ws, int64_t max_steps,
+                                                             int64_t L, int64_t Mmax, const TpNode* __restrict__ nodes,
+                                                             TpEnd* __restrict__ ends, const TpCtl* __restrict__ ctl) {
+  const int64_t g = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  const int64_t p = g / Mmax, m = g - p * Mmax;
+  if (p >= n) return;
+  const TpCtl c = ctl[p];
+  if (c.phase != kTpIter || m >= c.M) return;
+  const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
+  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
+  const OdePoint& o = S.o;
+  const double x0 = S.x0, h = S.h;
+  const int64_t k0 = m * L, k1 = k0 + L < S.N ? k0 + L : S.N;
+  const double xb = branch_x(o, x0, S.x1);
+  const double xb_below = nextafter(xb, -INFINITY);
+  const Radau R = radau_tableau();
+  const RadauH hA = radau_h(R, h);
+  const bool riccati = LZQ_ODE_PREDICT && o.sigmav != 0.0;
+  const TpNode nd = nodes[p * (Mmax + 1) + m];
+  double Ychi = nd.Ychi, YB = nd.YB, Yp = nd.Yp;
+  double Zs[3] = {nd.Z[0], nd.Z[1], nd.Z[2]};
+  bool have = nd.have != 0, exact = true;
+  double D = 1.0, C = 1.0;
+  double kd = (double)k0;
+  for (int64_t k = k0; k < k1; ++k, kd += 1.0) {
+    const double xk = x0 + kd * h;
+    const bool split = xk < xb && xb <= xk + h;
+    const double xa = split ? xb_below : xk + h;
+    const double Ystart = Ychi;
+    bool use_guess = false;
+    if (riccati && have && !split) {  // the Radau5 predictor, as ode_integrate_kernel
+      double gs[3];
+      use_guess = true;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        gs[j] = fma_s(Zs[2], kRadauPred[j][3],
+                      fma_s(Zs[1], kRadauPred[j][2], fma_s(Zs[0], kRadauPred[j][1], kRadauPred[j][0] * Yp)));
+        use_guess = use_guess && fabs(gs[j] - Ychi) <= 0.25 * fabs(Ychi);
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) Zs[j] = gs[j];
+    }
+    auto part = [&](double xs, double hs, bool guess, bool own_h) {
+      const RadauH hAs = own_h ? radau_h(R, hs) : hA;
+      OdeStage sg[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) sg[j] = ode_stage(o, w, xs + R.c[j] * hs);
+      const YbRec yr = yb_rec(hAs, sg);
+      YB = __builtin_fma(yr.c, YB, o.Pf * yr.d);
+      C *= yr.c;
+      const double Y0 = Ychi;
+      // (radau_step's convergence test reads NaN corrections as converged -- it never meets one on
+      // the sequential trajectory, but a start far from it can diverge: a non-finite result, or a
+      // sign change of a source-free positive Y_chi (the stage system's other root), is a failure)
+      const bool src = sg[0].S != 0.0 || sg[1].S != 0.0 || sg[2].S != 0.0;
+      if (radau_step<false>(hAs, sg, Ychi, YB, Zs, guess) && isfinite(Ychi) && (src || !(Y0 > 0.0) || Ychi > 0.0)) {
+        const bool nonlinear = sg[0].lam != 0.0 || sg[1].lam != 0.0 || sg[2].lam != 0.0;
+        if (nonlinear) D *= tp_dz3(hs, sg, Zs);
+        return true;
+      }
+      double dY1;
+      Ychi = tp_bridge(Y0, hs, sg[2], dY1);
+      Zs[0] = Zs[1] = Zs[2] = Ychi;
+      D *= dY1;
+      return false;
+    };
+    bool ok = true;
+    if (xa > xk) ok = part(xk, split ? xa - xk : h, use_guess, split);
+    if (split && xk + h > xb) ok = part(xb, (xk + h) - xb, false, true) && ok;
+    exact = exact && ok;
+    have = !split && ok;  // after a bridge the predictor has no collocation polynomial behind it
+    Yp = Ystart;
+  }
+  ends[p * Mmax + m] = TpEnd{Ychi, YB, Yp, {Zs[0], Zs[1], Zs[2]}, D, C, have ? 1 : 0, exact ? 1 : 0};
+}
+
+// One 1024-thread block per point: Newton's update of the nodes.  Thread t takes a contiguous run
+// of intervals, composes their affine maps d -> D d + r, the block scans the 1024 maps (Hillis-
+// Steele in LDS), and each thread re-walks its run from its carry-in, updating nodes m + 1.
+constexpr int kTpScan = 1024;
+__global__ __launch_bounds__(kTpScan) void ode_tp_update_kernel(int64_t Mmax, TpNode* __restrict__ nodes,
+                                                                const TpEnd* __restrict__ ends,
+                                                                TpCtl* __restrict__ ctl, int32_t max_iters,
+                                                                double tol) {
+  __shared__ double sA[kTpScan], sB[kTpScan], sAb[kTpScan], sBb[kTpScan];
+  __shared__ double s_err[kTpScan / 64];
+  __shared__ int s_fail;
+  const int64_t p = blockIdx.x;
+  const TpCtl c = ctl[p];
+  if (c.phase != kTpIter) return;  // block-uniform
+  const int t = threadIdx.x;
+  if (t == 0) s_fail = 0;
+  const int64_t M = c.M;
+  TpNode* nd = nodes + p * (Mmax + 1);
+  const TpEnd* en = ends + p * Mmax;
+  const int64_t per = (M + kTpScan - 1) / kTpScan;
+  const int64_t m0 = (int64_t)t * per < M ? (int64_t)t * per : M, m1 = m0 + per < M ? m0 + per : M;
+  double A = 1.0, B = 0.0, Ab = 1.0, Bb = 0.0;
+  bool fail = false;
+  for (int64_t m = m0; m < m1; ++m) {  // this run's map: d_{m1} = A d_{m0} + B
+    const TpEnd& e = en[m];
+    const double sy = nd[m + 1].Ychi, sb = nd[m + 1].YB;
+    const bool fin = isfinite(e.Ychi) && isfinite(e.D) && isfinite(e.YB) && isfinite(e.C);
+    fail = fail || e.exact == 0 || !fin;
+    // a non-finite end (a start far from the trajectory) moves nothing downstream this update
+    B = fin ? __builtin_fma(e.D, B, e.Ychi - sy) : 0.0;
+    A = fin ? e.D * A : 0.0;
+    Bb = fin ? __builtin_fma(e.C, Bb, e.YB - sb) : 0.0;
+    Ab = fin ? e.C * Ab : 0.0;
+  }
+  sA[t] = A, sB[t] = B, sAb[t] = Ab, sBb[t] = Bb;
+  __syncthreads();
+  if (fail) s_fail = 1;
+  for (int off = 1; off < kTpScan; off <<= 1) {  // inclusive scan: map(t) = map(t) o map(t - off)
+    double pA = 1.0, pB = 0.0, pAb = 1.0, pBb = 0.0;
+    if (t >= off) pA = sA[t - off], pB = sB[t - off], pAb = sAb[t - off], pBb = sBb[t - off];
+    __syncthreads();
+    if (t >= off) {
+      B = __builtin_fma(A, pB, B);
+      A = A * pA;
+      Bb = __builtin_fma(Ab, pBb, Bb);
+      Ab = Ab * pAb;
+      sA[t] = A, sB[t] = B, sAb[t] = Ab, sBb[t] = Bb;
+    }
+    __syncthreads();
+  }
+  double d = t > 0 ? sB[t - 1] : 0.0, db = t > 0 ? sBb[t - 1] : 0.0;  // d_{m0}: the runs before this one
+  double err = 0.0;
+#ifdef LZQ_ODE_TP_DEBUG
+  __shared__ int s_dbg[4];  // non-finite end Y_chi / D / Y_B, non-finite correction
+  if (t < 4) s_dbg[t] = 0;
+  __syncthreads();
+#endif
+  {
+    for (int64_t m = m0; m < m1; ++m) {
+      const TpEnd& e = en[m];
+      TpNode q = nd[m + 1];
+      const bool fin = isfinite(e.Ychi) && isfinite(e.D) && isfinite(e.YB) && isfinite(e.C);
+#ifdef LZQ_ODE_TP_DEBUG
+      if (!isfinite(e.Ychi)) atomicAdd(&s_dbg[0], 1);
+      if (!isfinite(e.D)) atomicAdd(&s_dbg[1], 1);
+      if (!isfinite(e.YB)) atomicAdd(&s_dbg[2], 1);
+      if (m == 0 || m == M - 1 || (m % 50) == 0)
+        printf("  p %lld m %lld node %.6e end %.6e D %.3e exact %d\n", (long long)p, (long long)m, q.Ychi, e.Ychi, e.D, e.exact);
+#endif
+      d = fin ? __builtin_fma(e.D, d, e.Ychi - q.Ychi) : 0.0;
+      db = fin ? __builtin_fma(e.C, db, e.YB - q.YB) : 0.0;
+      const double old = q.Ychi;
+      double nv = old + d;
+      // the Riccati stage system has a second root below zero: a correction never takes a
+      // positive node below a quarter of the smaller of its value and its predecessor interval's
+      // (positive) end (far from the solution only).  Y_chi's map is affine without annihilation
+      // (depletion may take it through zero): no safeguard there.
+      const double lo = 0.25 * pymin(old, fin && e.Ychi > 0.0 ? e.Ychi : old);
+      if (c.riccati && old > 0.0 && !(nv >= lo)) nv = lo;
+      q.Ychi = nv;
+      q.YB = q.YB + db;
+      if (fin) {
+        q.Yp = e.Yp;
+        q.Z[0] = e.Z[0], q.Z[1] = e.Z[1], q.Z[2] = e.Z[2];
+        q.have = e.have;
+      } else {
+        q.have = 0;
+      }
+      nd[m + 1] = q;
+      // relative to the node, floored at 1e-290: below it the doubles approach the subnormal range,
+      // whose coarser spacing no correction could resolve to the tolerance
+      const double ec = fabs(d) / pymax(fabs(nv), 1e-290), eb = fabs(db) / pymax(fabs(q.YB), 1e-290);
+      err = pymax(err, pymax(ec, eb));  // pymax keeps a NaN on the right: a NaN correction fails the test below
+      if (!(ec == ec) || !(eb == eb)) err = INFINITY;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) err = pymax(err, __shfl_xor(err, off, 64));
+  if ((t & 63) == 0) s_err[t >> 6] = err;
+  __syncthreads();
+  if (t != 0) return;
+  double e_all = 0.0;
+  for (int k = 0; k < kTpScan / 64; ++k) e_all = pymax(e_all, s_err[k]);
+  TpCtl cn = c;
+  cn.iters = c.iters + 1;
+  cn.err = e_all;
+#ifdef LZQ_ODE_TP_DEBUG
+  printf("tp point %lld update %d: M %lld err %.3e fail %d nonfinite end Ychi %d D %d YB %d\n", (long long)p, cn.iters,
+         (long long)M, e_all, s_fail, s_dbg[0], s_dbg[1], s_dbg[2]);
+#endif
+  // converged: the corrections are below the tolerance and every interval took only Radau steps
+  if (e_all <= tol && !s_fail) cn.phase = kTpDone;
+  else if (cn.iters >= max_iters) cn.phase = kTpFallback;
+  ctl[p] = cn;
+}
+
+// Converged points: node M is the final state -> the yields (fpy:412-417) and skip[p] = 1 (the
+// sequential launches pass them by); the others: skip[p] = 0.
+__global__ __launch_bounds__(64) void ode_tp_finish_kernel(const lzq_point* __restrict__ pts, int64_t n, int64_t Mmax,
+                                                           const TpNode* __restrict__ nodes,
+                                                           const TpCtl* __restrict__ ctl, lzq_yield* __restrict__ out,
+                                                           int32_t* __restrict__ status, int32_t* __restrict__ skip,
+                                                           int32_t* __restrict__ iters) {
+  const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (p >= n) return;
+  const TpCtl c = ctl[p];
+  const bool done = c.phase == kTpDone;
+  skip[p] = done ? 1 : 0;
+  if (iters) iters[p] = done ? c.iters : -c.iters;  // < 0: iterated, abandoned, integrated sequentially
+  if (!done) return;
+  const TpNode f = nodes[p * (Mmax + 1) + c.M];
+  const double m = pts[p].m_chi_GeV;
+  lzq_yield r;
+  const double nB0 = f.YB * kS0M3, nDM0 = f.Ychi * kS0M3;
+  r.Y_B = f.YB;
+  r.Y_chi = f.Ychi;
+  r.rho_B_kg_m3 = nB0 * kMProtonKg;
+  r.rho_DM_kg_m3 = nDM0 * (m * kGeVToKg);
+  r.DM_over_B = r.rho_DM_kg_m3 / pymax(r.rho_B_kg_m3, 1e-300);
+  r.P_used = pts[p].P_chi_to_B;
+  out[p] = r;
+  if (status) status[p] = LZQ_ODE_OK;
+}
+
+// ---------------------------------------------------------------------------------------
 // Converged quadrature form of the sigma_v = 0 fallback (opt-in; lzq_ode_quadrature).
 // With sigma_v = 0 both equations of rhs (fpy:270-286) are linear with known integrating
 // factors: beta = gamma_w H / (H x) = gamma_w / x, so
@@ -1798,7 +2158,7 @@ int hip_check(hipError_t e, const char* what);
 template <bool kChiOnly>
 int launch_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, const int32_t* d_tidx,
                      const double* d_work, int64_t max_steps, lzq_yield* d_out, int32_t* d_status, hipStream_t s,
-                     const char* fn) {
+                     const char* fn, const int32_t* d_skip = nullptr) {
   const int64_t per = (int64_t)1 << lzq::g_ode_launch_log2;
   const int64_t launches = max_steps <= per ? 1 : (max_steps + per - 1) / per;
   if (launches > 65536) {
@@ -1812,29 +2172,29 @@ int launch_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int
   auto launch = [&](int64_t k_lo, int64_t k_cnt, lzq::OdeState* st) {
     hipLaunchKernelGGL(lzq::ode_integrate_kernel<kChiOnly>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, s,
                        d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, lzq::g_ode_coop, k_lo, k_cnt,
-                       st);
+                       st, d_skip);
     int rc = hip_check(hipGetLastError(), fn);
     if constexpr (LZQ_ODE_NOSPLITVAR) {
       if (rc != LZQ_OK) return rc;
       hipLaunchKernelGGL((lzq::ode_integrate_kernel<kChiOnly, false, true>), dim3((unsigned)ode_blocks(n)),
                          dim3(lzq::kOdeBlock), 0, s, d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status,
-                         lzq::g_ode_coop, k_lo, k_cnt, st);
+                         lzq::g_ode_coop, k_lo, k_cnt, st, d_skip);
       rc = hip_check(hipGetLastError(), fn);
       if constexpr (LZQ_ODE_RICVAR && !kChiOnly) {  // the three passes (ode_riccati_kernel)
         if (rc != LZQ_OK) return rc;
         hipLaunchKernelGGL(lzq::ode_riccati_kernel<0>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, s,
                            d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, lzq::g_ode_coop, k_lo,
-                           k_cnt, st);
+                           k_cnt, st, d_skip);
         rc = hip_check(hipGetLastError(), fn);
         if (rc != LZQ_OK) return rc;
         hipLaunchKernelGGL(lzq::ode_riccati_kernel<1>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, s,
                            d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, lzq::g_ode_coop, k_lo,
-                           k_cnt, st);
+                           k_cnt, st, d_skip);
         rc = hip_check(hipGetLastError(), fn);
         if (rc != LZQ_OK) return rc;
         hipLaunchKernelGGL(lzq::ode_riccati_kernel<2>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, s,
                            d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, lzq::g_ode_coop, k_lo,
-                           k_cnt, st);
+                           k_cnt, st, d_skip);
         rc = hip_check(hipGetLastError(), fn);
       }
     }
@@ -1842,7 +2202,7 @@ int launch_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int
       if (rc != LZQ_OK) return rc;
       hipLaunchKernelGGL((lzq::ode_integrate_kernel<kChiOnly, true>), dim3((unsigned)ode_blocks(n)),
                          dim3(lzq::kOdeBlock), 0, s, d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status,
-                         lzq::g_ode_coop, k_lo, k_cnt, st);
+                         lzq::g_ode_coop, k_lo, k_cnt, st, d_skip);
       rc = hip_check(hipGetLastError(), fn);
     }
     return rc;
@@ -1855,6 +2215,62 @@ int launch_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int
   if (rc) return rc;
   for (int64_t j = 0; j < launches && rc == LZQ_OK; ++j) rc = launch(j * per, per, st);
   const int rf = hip_check(hipFreeAsync(st, s), fn);
+  return rc ? rc : rf;
+}
+
+// lzq_ode_integrate_tp: the time-parallel iteration (ode_tp_*_kernel) for batches of <= kTpMaxPoints
+// points, then the sequential launches for the points it did not finish (skip mask).  Intervals
+// of g_ode_tp_interval steps, more when max_steps would need over kTpMaxIntervals of them.
+constexpr int64_t kTpMaxPoints = 64;
+constexpr int64_t kTpMaxIntervals = 1 << 16;
+constexpr int32_t kTpMaxIters = 48;
+constexpr double kTpTol = 1e-14;  // largest relative node correction of a converged iteration
+int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, const int32_t* d_tidx,
+                        const double* d_work, int64_t max_steps, lzq_yield* d_out, int32_t* d_status,
+                        int32_t* d_iters, hipStream_t s, const char* fn) {
+  const int64_t L0 = lzq::g_ode_tp_interval;
+  const int64_t L = max_steps > L0 * kTpMaxIntervals ? (max_steps + kTpMaxIntervals - 1) / kTpMaxIntervals : L0;
+  const int64_t Mmax = (max_steps + L - 1) / L;
+  if (n > kTpMaxPoints || Mmax < 2) {  // nothing to cut: the sequential path alone
+    if (d_iters) {
+      int rc = hip_check(hipMemsetAsync(d_iters, 0, sizeof(int32_t) * (size_t)n, s), fn);
+      if (rc) return rc;
+    }
+    return launch_integrate<false>(d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, s, fn);
+  }
+  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t b_nodes = up(sizeof(lzq::TpNode) * (size_t)n * (size_t)(Mmax + 1));
+  const size_t b_ends = up(sizeof(lzq::TpEnd) * (size_t)n * (size_t)Mmax);
+  const size_t b_ctl = up(sizeof(lzq::TpCtl) * (size_t)n);
+  const size_t b_skip = up(sizeof(int32_t) * (size_t)n);
+  char* buf = nullptr;
+  int rc = hip_check(hipMallocAsync((void**)&buf, b_nodes + b_ends + b_ctl + b_skip, s), fn);
+  if (rc) return rc;
+  auto* nodes = reinterpret_cast<lzq::TpNode*>(buf);
+  auto* ends = reinterpret_cast<lzq::TpEnd*>(buf + b_nodes);
+  auto* ctl = reinterpret_cast<lzq::TpCtl*>(buf + b_nodes + b_ends);
+  auto* skip = reinterpret_cast<int32_t*>(buf + b_nodes + b_ends + b_ctl);
+  hipLaunchKernelGGL(lzq::ode_tp_init_kernel, dim3((unsigned)n), dim3(256), 0, s, d_points, d_ode, d_tidx, d_work,
+                     max_steps, L, Mmax, nodes, ctl);
+  rc = hip_check(hipGetLastError(), fn);
+  const unsigned ib = (unsigned)((n * Mmax + 63) / 64);
+  for (int32_t it = 0; it < kTpMaxIters && rc == LZQ_OK; ++it) {
+    hipLaunchKernelGGL(lzq::ode_tp_interval_kernel, dim3(ib), dim3(64), 0, s, d_points, d_ode, n, d_tidx, d_work,
+                       max_steps, L, Mmax, nodes, ends, ctl);
+    rc = hip_check(hipGetLastError(), fn);
+    if (rc) break;
+    hipLaunchKernelGGL(lzq::ode_tp_update_kernel, dim3((unsigned)n), dim3(lzq::kTpScan), 0, s, Mmax, nodes, ends, ctl,
+                       kTpMaxIters, kTpTol);
+    rc = hip_check(hipGetLastError(), fn);
+  }
+  if (rc == LZQ_OK) {
+    hipLaunchKernelGGL(lzq::ode_tp_finish_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, d_points, n, Mmax,
+                       nodes, ctl, d_out, d_status, skip, d_iters);
+    rc = hip_check(hipGetLastError(), fn);
+  }
+  if (rc == LZQ_OK)
+    rc = launch_integrate<false>(d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, s, fn, skip);
+  const int rf = hip_check(hipFreeAsync(buf, s), fn);
   return rc ? rc : rf;
 }
 
@@ -1934,6 +2350,19 @@ int lzq_ode_integrate_shared(const lzq_point* d_points, const lzq_ode_params* d_
   if (n == 0) return LZQ_OK;
   return launch_integrate<false>(d_points, d_ode, n, d_table_index, d_work, max_steps, d_out, d_status,
                                  (hipStream_t)stream, "lzq_ode_integrate_shared");
+}
+
+int lzq_ode_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n,
+                         const int32_t* d_table_index, int64_t n_tables, const double* d_work, int64_t work_doubles,
+                         int64_t max_steps, lzq_yield* d_out, int32_t* d_status, int32_t* d_iters, void* stream) {
+  if (n < 0 || n_tables < 0 || max_steps < 0 || (n > 0 && (!d_points || !d_ode || !d_out)) ||
+      (d_table_index && n > 0 && n_tables == 0))
+    return lzq_set_error(LZQ_EINVAL, "lzq_ode_integrate_tp: bad arguments");
+  int rc = check_ws(d_table_index ? n_tables : n, d_work, work_doubles, "lzq_ode_integrate_tp");
+  if (rc) return rc;
+  if (n == 0) return LZQ_OK;
+  return launch_integrate_tp(d_points, d_ode, n, d_table_index, d_work, max_steps, d_out, d_status, d_iters,
+                             (hipStream_t)stream, "lzq_ode_integrate_tp");
 }
 
 int lzq_ode_quadrature(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n,

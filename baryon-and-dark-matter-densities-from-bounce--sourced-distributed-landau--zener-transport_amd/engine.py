@@ -275,7 +275,7 @@ class Engine:
 
     def ode(self, points, ode_params, max_steps: Optional[int] = None, chunk: int = 1 << 18,
             share_tables: bool = True, method: str = "radau", group_waves: bool = True, nz: int = _native.LZQ_NZ,
-            z_max: float = _native.LZQ_Z_MAX, aov=None) -> tuple:
+            z_max: float = _native.LZQ_Z_MAX, aov=None, time_parallel: Optional[bool] = None) -> tuple:
         """fpy:385-417 for n points (POINT_DTYPE records + ODE_DTYPE records): (n, 6) yields
         table and (n,) int32 status (enum lzq_ode_status), both on the device.  Points are
         processed in chunks so that the spline workspace stays <= chunk * 25.6 KB (6.7 GB at the
@@ -298,7 +298,13 @@ class Engine:
         nz, z_max: the z grid of the A/V kernel behind the spline tables (fpy:141-156, 207-212).
         aov: the A/V kernel's own parameters behind each point's spline table when it is not the
         point's own (bs.aov replaced before build_tables, fpy:211; see aov_to_device); the tables are
-        then built per point (no sharing)."""
+        then built per point (no sharing).
+        time_parallel: integrate by lzq_ode_integrate_tp (multiple shooting: a point's steps cut into
+        intervals integrated side by side, Newton on their boundaries) -- the latency path for a few
+        points on long windows; within ~1e-13 of the sequential integration, not bit-identical to it.
+        None (default): on for a single point (the CLI's case), off otherwise, so every multi-point
+        call keeps the batch-independent bits.  Radau only.  self.last_ode_tp_iters: the Newton
+        updates per point of the last time-parallel call (0: integrated sequentially)."""
         nz, z_max = _native.zgrid(nz, z_max)
         if method not in ("radau", "quadrature"):
             raise ValueError(f"method must be 'radau' or 'quadrature', got {method!r}")
@@ -307,6 +313,10 @@ class Engine:
         if pts.size != ods.size:
             raise ValueError("points and ode_params must have the same length")
         n = pts.size
+        if time_parallel is None:
+            time_parallel = n == 1
+        time_parallel = bool(time_parallel) and method == "radau"
+        tp_iters = torch.zeros(n, dtype=torch.int32, device=self.device) if time_parallel else None
         d_pts_all = self.points_to_device(pts)
         d_ode_all = _to_device_bytes(ods, self.device)
         d_aov_all = self.aov_to_device(aov, n)
@@ -396,6 +406,11 @@ class Engine:
                     self._check(self.lib.lzq_ode_quadrature(_vp(d_pts), _vp(d_ode), c1 - c0, _vp(d_idx), n_tab,
                                                             _vp(work), work.numel(), int(max_steps), _vp(out[c0:c1]),
                                                             _vp(status[c0:c1]), self._stream()))
+                elif time_parallel:
+                    self._check(self.lib.lzq_ode_integrate_tp(_vp(d_pts), _vp(d_ode), c1 - c0, _vp(d_idx), n_tab,
+                                                              _vp(work), work.numel(), int(max_steps),
+                                                              _vp(out[c0:c1]), _vp(status[c0:c1]),
+                                                              _vp(tp_iters[c0:c1]), self._stream()))
                 elif d_rep is None:   # lzq_ode_batch's second half (its tables are built above)
                     self._check(self.lib.lzq_ode_integrate(_vp(d_pts), _vp(d_ode), c1 - c0, _vp(work), work.numel(),
                                                            int(max_steps), _vp(out[c0:c1]), _vp(status[c0:c1]),
@@ -418,6 +433,11 @@ class Engine:
             out_in, st_in = torch.empty_like(out), torch.empty_like(status)
             out_in[order], st_in[order] = out, status
             out, status = out_in, st_in
+            if tp_iters is not None:
+                it_in = torch.empty_like(tp_iters)
+                it_in[order] = tp_iters
+                tp_iters = it_in
+        self.last_ode_tp_iters = tp_iters
         return out, status
 
     def ode_aov_T(self, point, T_lo: float, T_hi: float, work_point: torch.Tensor, Ts,

@@ -169,8 +169,10 @@ int lzq_ztables(int32_t nz, double z_max, double* z, double* gamma4, double* ome
  * loop of Magnus steps per lane, a lane entering its next interval while the others step) or the
  * interval-by-interval loop in keyed launch order (measured faster).  P is
  * bit-identical either way (tests/test_gpu_profile.py). */
+/* LZQ_TUNE_ODE_TP_INTERVAL (steps, 8..2^20; default 64): the interval length of lzq_ode_integrate_tp's
+ * multiple shooting (more when max_steps would need over 65536 intervals). */
 enum lzq_tune_key { LZQ_TUNE_EXP = 0, LZQ_TUNE_TRUNCATE = 1, LZQ_TUNE_ODE_COOP = 2, LZQ_TUNE_ODE_LAUNCH_STEPS = 3,
-                    LZQ_TUNE_PROFILE_FLAT = 4 };
+                    LZQ_TUNE_PROFILE_FLAT = 4, LZQ_TUNE_ODE_TP_INTERVAL = 5 };
 enum lzq_exp_variant { LZQ_EXP_POLY11 = 0, LZQ_EXP_TABLE = 1 };
 int lzq_tune(int32_t key, int32_t value);
 
@@ -313,6 +315,26 @@ int lzq_ode_integrate_shared(const lzq_point* d_points, const lzq_ode_params* d_
                              const int32_t* d_table_index, int64_t n_tables, const double* d_work,
                              int64_t work_doubles, int64_t max_steps, lzq_yield* d_out, int32_t* d_status,
                              void* stream);
+
+/* lzq_ode_integrate / lzq_ode_integrate_shared (d_table_index NULL: table i for point i) for a
+ * FEW points on long windows -- the CLI's single point -- integrated parallel in time: each
+ * point's N fixed steps are cut into intervals of LZQ_TUNE_ODE_TP_INTERVAL steps, every interval
+ * is integrated from a guess of its start state on its own lane (the same per-step operations),
+ * and Newton's method on the interval boundaries (multiple shooting; the corrections by a scan of
+ * the intervals' linearised maps) iterates the guesses to the sequential trajectory.  A point's
+ * latency drops from N serial steps to (a few iterations) x (one interval).  The result is the
+ * sequential integration's up to rounding -- the boundaries are formed as guess + correction
+ * instead of carried -- within ~1e-13 relative (tests/test_gpu_ode_tp.py), NOT bit-identical to
+ * lzq_ode_integrate.  A point whose iteration does not converge to 1e-14 within 48 updates, whose
+ * interval meets a Newton failure, or whose status is not OK, takes the sequential integration
+ * (same statuses and results as lzq_ode_integrate); so does every point of a batch of more than
+ * 64.  d_iters (optional, [n] int32): the Newton updates a point took; 0: not iterated, -k: abandoned
+ * after k updates; both then integrated sequentially.
+ * Blocks nothing: the iteration count is fixed (48 rounds of two launches; a converged point's
+ * later launches return at once), so the call is stream-ordered like lzq_ode_integrate. */
+int lzq_ode_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n,
+                         const int32_t* d_table_index, int64_t n_tables, const double* d_work, int64_t work_doubles,
+                         int64_t max_steps, lzq_yield* d_out, int32_t* d_status, int32_t* d_iters, void* stream);
 
 /* Quadrature form of the fallback (opt-in; not the reference's method).  Y_B's equation of
  * fpy:270-286 is linear with integrating factor (x/x1)^Gamma_wash for every sigma_v, so

@@ -174,6 +174,28 @@ def test_tune_ode_coop_knob():
     assert L.lzq_tune(n.TUNE_ODE_COOP, 2) < 0 and b"ode_coop" in L.lzq_last_error()
 
 
+def test_tune_ode_tp_interval_knob():
+    """lzq_tune(LZQ_TUNE_ODE_TP_INTERVAL): 64 steps by default, [8, 2^20] only, returns the previous."""
+    n = pkg("_native")
+    L = n.load()
+    assert L.lzq_tune(n.TUNE_ODE_TP_INTERVAL, 16) == 64
+    assert L.lzq_tune(n.TUNE_ODE_TP_INTERVAL, 64) == 16
+    for bad in (7, (1 << 20) + 1, -1):
+        assert L.lzq_tune(n.TUNE_ODE_TP_INTERVAL, bad) < 0 and b"ode_tp_interval" in L.lzq_last_error()
+    assert L.lzq_tune(n.TUNE_ODE_TP_INTERVAL, 64) == 64
+
+
+def test_ode_integrate_tp_argument_checks():
+    """lzq_ode_integrate_tp refuses bad arguments before any launch (no GPU needed)."""
+    n = pkg("_native")
+    L = n.load()
+    assert L.lzq_ode_integrate_tp(8, 8, -1, None, 0, 8, 1 << 20, 100, 8, None, None, None) < 0
+    assert L.lzq_ode_integrate_tp(8, 8, 4, 8, 0, 8, 1 << 20, 100, 8, None, None, None) < 0   # index, no tables
+    assert L.lzq_ode_integrate_tp(8, 8, 4, None, 0, 8, 100, 100, 8, None, None, None) < 0    # workspace < 4 tables
+    assert L.lzq_ode_integrate_tp(8, 8, 4, None, 0, 8, 1 << 20, -1, 8, None, None, None) < 0  # max_steps < 0
+    assert L.lzq_ode_integrate_tp(None, None, 0, None, 0, None, 0, 0, None, None, None, None) == 0
+
+
 def test_sweep_grid_reuse_workspace_and_validation():
     """lzq_sweep_grid_reuse_workspace: one table of max(n_y, 2000) + 6 doubles per combination of
     the grid's I_p / beta_over_H / T_p / T_min / T_max values; lzq_sweep_grid_reuse refuses a

@@ -1870,7 +1870,7 @@ __global__ __launch_bounds__(kTpScan) void ode_tp_update_kernel(int64_t Mmax, Tp
       if (!isfinite(e.Ychi)) atomicAdd(&s_dbg[0], 1);
       if (!isfinite(e.D)) atomicAdd(&s_dbg[1], 1);
       if (!isfinite(e.YB)) atomicAdd(&s_dbg[2], 1);
-      if (m == 0 || m == M - 1 || (m % 50) == 0)
+      if (m == 0 || m == M - 1 || (m % ((M + 7) / 8)) == 0)
         printf("  p %lld m %lld node %.6e end %.6e D %.3e exact %d\n", (long long)p, (long long)m, q.Ychi, e.Ychi, e.D, e.exact);
 #endif
       d = fin ? __builtin_fma(e.D, d, e.Ychi - q.Ychi) : 0.0;

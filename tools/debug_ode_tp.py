@@ -25,6 +25,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--build", action="store_true", help="build the debug library (CPU side)")
     ap.add_argument("--cases", type=int, nargs="*", default=None)
+    ap.add_argument("--over", type=str, default=None,
+                    help="JSON overrides of the shipped config to trace instead of the golden cases")
     a = ap.parse_args()
     if a.build:
         importlib.import_module(bench.PKG + ".build").build(defines={"LZQ_ODE_TP_DEBUG": 1}, out=DBG)
@@ -34,6 +36,9 @@ def main():
     from conftest import full_cfg
     eng = importlib.import_module(bench.PKG + ".engine").Engine(0, lib_path=DBG)
     pts = json.load(open(os.path.join(ROOT, "tests", "golden", "golden_ode.json")))["points"]
+    if a.over is not None:
+        from conftest import BASE_CFG
+        pts = [{"config": {**BASE_CFG, **json.loads(a.over)}}]
     for i, r in enumerate(pts):
         if a.cases is not None and i not in a.cases:
             continue

@@ -1724,33 +1724,24 @@ __device__ __forceinline__ double tp_bridge(double Y0, double h, const OdeStage&
   return 2.0 * c / (1.0 + q);
 }
 
-// One lane per (point, interval): F_m, D_m, C_m from node m (ode_integrate_kernel's per-lane steps).
-__global__ __launch_bounds__(64) void ode_tp_interval_kernel(const lzq_point* __restrict__ pts,
-                                                             const lzq_ode_params* __restrict__ ode, int64_t n,
-                                                             const int32_t* __restrict__ tidx,
-                                                             const double* __restrict__ ws, int64_t max_steps,
-                                                             int64_t L, int64_t Mmax, const TpNode* __restrict__ nodes,
-                                                             TpEnd* __restrict__ ends, const TpCtl* __restrict__ ctl) {
-  const int64_t g = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  const int64_t p = g / Mmax, m = g - p * Mmax;
-  if (p >= n) return;
-  const TpCtl c = ctl[p];
-  if (c.phase != kTpIter || m >= c.M) return;
-  const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
-  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
-  const OdePoint& o = S.o;
-  const double x0 = S.x0, h = S.h;
-  const int64_t k0 = m * L, k1 = k0 + L < S.N ? k0 + L : S.N;
-  const double xb = branch_x(o, x0, S.x1);
-  const double xb_below = nextafter(xb, -INFINITY);
+// The integrator's state between steps (ode_integrate_kernel's per-lane registers).
+struct TpState {
+  double Ychi, YB, Yp, Z[3];
+  bool have;
+};
+
+// Steps [k0, k1) of the fixed-step sequence x_k = x0 + k h from state St, with ode_integrate_kernel's
+// per-lane operations (stages, Y_B map, Radau step, the T = m/3 split step, the predictor); D and C
+// accumulate the derivatives of the end state.  Returns false when a step needed tp_bridge.
+__device__ __forceinline__ bool tp_steps(const OdePoint& o, const double* __restrict__ w, double x0, double h,
+                                         double xb, double xb_below, int64_t k0, int64_t k1, TpState& St, double& D,
+                                         double& C) {
   const Radau R = radau_tableau();
   const RadauH hA = radau_h(R, h);
   const bool riccati = LZQ_ODE_PREDICT && o.sigmav != 0.0;
-  const TpNode nd = nodes[p * (Mmax + 1) + m];
-  double Ychi = nd.Ychi, YB = nd.YB, Yp = nd.Yp;
-  double Zs[3] = {nd.Z[0], nd.Z[1], nd.Z[2]};
-  bool have = nd.have != 0, exact = true;
-  double D = 1.0, C = 1.0;
+  double Ychi = St.Ychi, YB = St.YB, Yp = St.Yp;
+  double Zs[3] = {St.Z[0], St.Z[1], St.Z[2]};
+  bool have = St.have, exact = true;
   double kd = (double)k0;
   for (int64_t k = k0; k < k1; ++k, kd += 1.0) {
     const double xk = x0 + kd * h;
@@ -1801,7 +1792,78 @@ __global__ __launch_bounds__(64) void ode_tp_interval_kernel(const lzq_point* __
     have = !split && ok;  // after a bridge the predictor has no collocation polynomial behind it
     Yp = Ystart;
   }
-  ends[p * Mmax + m] = TpEnd{Ychi, YB, Yp, {Zs[0], Zs[1], Zs[2]}, D, C, have ? 1 : 0, exact ? 1 : 0};
+  St = TpState{Ychi, YB, Yp, {Zs[0], Zs[1], Zs[2]}, have};
+  return exact;
+}
+
+// One lane per (point, interval): F_m, D_m, C_m from node m.
+__global__ __launch_bounds__(64) void ode_tp_interval_kernel(const lzq_point* __restrict__ pts,
+                                                             const lzq_ode_params* __restrict__ ode, int64_t n,
+                                                             const int32_t* __restrict__ tidx,
+                                                             const double* __restrict__ ws, int64_t max_steps,
+                                                             int64_t L, int64_t Mmax, const TpNode* __restrict__ nodes,
+                                                             TpEnd* __restrict__ ends, const TpCtl* __restrict__ ctl) {
+  const int64_t g = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  const int64_t p = g / Mmax, m = g - p * Mmax;
+  if (p >= n) return;
+  const TpCtl c = ctl[p];
+  if (c.phase != kTpIter || m >= c.M) return;
+  const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
+  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
+  const int64_t k0 = m * L, k1 = k0 + L < S.N ? k0 + L : S.N;
+  const double xb = branch_x(S.o, S.x0, S.x1);
+  const TpNode nd = nodes[p * (Mmax + 1) + m];
+  TpState St{nd.Ychi, nd.YB, nd.Yp, {nd.Z[0], nd.Z[1], nd.Z[2]}, nd.have != 0};
+  double D = 1.0, C = 1.0;
+  const bool exact = tp_steps(S.o, w, S.x0, S.h, xb, nextafter(xb, -INFINITY), k0, k1, St, D, C);
+  ends[p * Mmax + m] = TpEnd{St.Ychi, St.YB, St.Yp, {St.Z[0], St.Z[1], St.Z[2]}, D, C, St.have ? 1 : 0, exact ? 1 : 0};
+}
+
+// The first guess of long Riccati windows (M >= kTpGuessMin intervals): the same integrator on kTpGuessSteps
+// coarse steps of (x1 - x0) / kTpGuessSteps (one lane per point, sequential), each node then
+// interpolated between the coarse points around it (Y_chi geometrically when both are positive,
+// Y_B linearly).  Radau IIA is L-stable, so the coarse trajectory tracks equilibrium where the
+// fine one does and freezes out near where it does: Newton starts within reach of its quadratic
+// phase instead of from the constant initial value (14 -> ~5 updates on the shipped window).
+constexpr int64_t kTpGuessMin = 1024, kTpGuessSteps = 256;
+__global__ __launch_bounds__(256) void ode_tp_guess_kernel(const lzq_point* __restrict__ pts,
+                                                           const lzq_ode_params* __restrict__ ode,
+                                                           const int32_t* __restrict__ tidx,
+                                                           const double* __restrict__ ws, int64_t max_steps, int64_t L,
+                                                           int64_t Mmax, TpNode* __restrict__ nodes,
+                                                           const TpCtl* __restrict__ ctl) {
+  __shared__ double s_y[kTpGuessSteps + 1], s_b[kTpGuessSteps + 1];
+  const int64_t p = blockIdx.x;
+  const TpCtl c = ctl[p];
+  // block-uniform; without annihilation Y_chi's map is affine and Newton needs no first guess
+  if (c.phase != kTpIter || c.M < kTpGuessMin || !c.riccati) return;
+  const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
+  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
+  const double Hc = (S.x1 - S.x0) / (double)kTpGuessSteps;
+  if (threadIdx.x == 0) {
+    const double xb = branch_x(S.o, S.x0, S.x1);
+    TpState St{S.Ychi0, 0.0, S.Ychi0, {S.Ychi0, S.Ychi0, S.Ychi0}, false};
+    s_y[0] = S.Ychi0;
+    s_b[0] = 0.0;
+    for (int64_t k = 0; k < kTpGuessSteps; ++k) {
+      double D = 1.0, C = 1.0;
+      tp_steps(S.o, w, S.x0, Hc, xb, nextafter(xb, -INFINITY), k, k + 1, St, D, C);
+      s_y[k + 1] = St.Ychi;
+      s_b[k + 1] = St.YB;
+    }
+  }
+  __syncthreads();
+  TpNode* nd = nodes + p * (Mmax + 1);
+  for (int64_t m = 1 + threadIdx.x; m <= c.M; m += blockDim.x) {
+    const int64_t km = m * L < S.N ? m * L : S.N;  // node m's step index (node M: x1)
+    const double u = (double)km / (double)S.N * (double)kTpGuessSteps;
+    const int64_t j = u < (double)kTpGuessSteps ? (int64_t)u : kTpGuessSteps - 1;
+    const double t = u - (double)j;
+    const double y0 = s_y[j], y1 = s_y[j + 1];
+    const double y = (y0 > 0.0 && y1 > 0.0) ? y0 * exp(t * log(y1 / y0)) : y0 + t * (y1 - y0);
+    const double b = s_b[j] + t * (s_b[j + 1] - s_b[j]);
+    if (isfinite(y) && isfinite(b)) nd[m] = TpNode{y, b, y, {y, y, y}, 0, 0};
+  }
 }
 
 // One 1024-thread block per point: Newton's update of the nodes.  Thread t takes a contiguous run
@@ -2253,6 +2315,11 @@ int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, 
   hipLaunchKernelGGL(lzq::ode_tp_init_kernel, dim3((unsigned)n), dim3(256), 0, s, d_points, d_ode, d_tidx, d_work,
                      max_steps, L, Mmax, nodes, ctl);
   rc = hip_check(hipGetLastError(), fn);
+  if (rc == LZQ_OK && Mmax >= lzq::kTpGuessMin) {
+    hipLaunchKernelGGL(lzq::ode_tp_guess_kernel, dim3((unsigned)n), dim3(256), 0, s, d_points, d_ode, d_tidx, d_work,
+                       max_steps, L, Mmax, nodes, ctl);
+    rc = hip_check(hipGetLastError(), fn);
+  }
   const unsigned ib = (unsigned)((n * Mmax + 63) / 64);
   for (int32_t it = 0; it < kTpMaxIters && rc == LZQ_OK; ++it) {
     hipLaunchKernelGGL(lzq::ode_tp_interval_kernel, dim3(ib), dim3(64), 0, s, d_points, d_ode, n, d_tidx, d_work,

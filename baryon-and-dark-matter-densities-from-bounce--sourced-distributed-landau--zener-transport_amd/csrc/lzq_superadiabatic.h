@@ -49,9 +49,35 @@ __host__ __device__ __forceinline__ double sa_rcp(double x) {
 #endif
 }
 
+// 1/sqrt(x) for the same quantities: v_rsq_f64 + two Newton steps r += r (1 - x r^2) / 2 (~1 ulp).
+// A square root and a reciprocal of the same number then cost one such chain (sqrt(x) = x rsqrt(x),
+// 1/x = rsqrt(x)^2) instead of the IEEE square root's refinement followed by sa_rcp's: the frame
+// levels are a dependent chain of these, so their latency is the follow kernel's (LZQ_SA_RSQRT).
+#ifndef LZQ_SA_RSQRT
+#define LZQ_SA_RSQRT 1
+#endif
+__host__ __device__ __forceinline__ double sa_rsqrt(double x) {
+#if defined(__HIP_DEVICE_COMPILE__) && LZQ_SA_FASTDIV
+  double r = __builtin_amdgcn_rsq(x);
+  double e = __builtin_fma(-(x * r), r, 1.0);
+  r = __builtin_fma(0.5 * r, e, r);
+  e = __builtin_fma(-(x * r), r, 1.0);
+  return __builtin_fma(0.5 * r, e, r);
+#else
+  return 1.0 / sqrt(x);
+#endif
+}
+
 // cos theta, sin theta from cos 2theta = c2, sin 2theta = s2 >= 0 (theta in [0, pi/2]) or any
 // s2 with c2 > 0, without cancellation
 __host__ __device__ __forceinline__ void half_angle(double c2, double s2, bool pos, double& c, double& s) {
+#if LZQ_SA_RSQRT
+  const double x = 0.5 * (pos ? 1.0 + c2 : 1.0 - c2);  // in [1/2, 1]
+  const double rr = sa_rsqrt(x);
+  const double big = x * rr, small = s2 * (0.5 * rr);
+  c = pos ? big : small;
+  s = pos ? small : big;
+#else
   if (pos) {
     c = sqrt(0.5 * (1.0 + c2));
     s = s2 * (0.5 * sa_rcp(c));
@@ -59,6 +85,7 @@ __host__ __device__ __forceinline__ void half_angle(double c2, double s2, bool p
     s = sqrt(0.5 * (1.0 - c2));
     c = s2 * (0.5 * sa_rcp(s));
   }
+#endif
 }
 
 // The frame rotation U = V_0 V_1 .. V_{N-1} accumulated as it is built: an SU(2) element
@@ -99,8 +126,13 @@ __host__ __device__ __forceinline__ void sa_chain(double (&e)[M], double (&g)[M]
       if (l % 2 == 0) acc = __builtin_fma(e[l / 2], e[l / 2], __builtin_fma(g[l / 2], g[l / 2], acc));
       q[l] = acc;
     }
+#if LZQ_SA_RSQRT
+    const double ir = sa_rsqrt(q[0]);
+    const double r0 = q[0] * ir;
+#else
     const double r0 = sqrt(q[0]);
     const double ir = sa_rcp(r0);
+#endif
     if constexpr (kRot) {
       double c, s;
       half_angle(e[0] * ir, g[0] * ir, e[0] >= 0.0, c, s);
@@ -112,7 +144,11 @@ __host__ __device__ __forceinline__ void sa_chain(double (&e)[M], double (&g)[M]
     }
     if constexpr (n > 1) {
       // theta' = (e g' - g e') / (2 q): w = num / q, g_next = -+ w / 2
+#if LZQ_SA_RSQRT
+      const double iq = ir * ir;
+#else
       const double iq = sa_rcp(q[0]);
+#endif
       double w[n - 1];
 #pragma unroll
       for (int l = 0; l < n - 1; ++l) {
@@ -158,8 +194,13 @@ template <int N, bool kRot, bool kEG>
 __host__ __device__ __forceinline__ void sa_levels_linear(double Dh, double sg, double mh, SU2& u, double* ev, double* gv) {
   // q = (Dh + sg h)^2 + mh^2 = [E^2, 2 sg Dh, 1]
   const double q0 = __builtin_fma(Dh, Dh, mh * mh), q1 = 2.0 * sg * Dh;
+#if LZQ_SA_RSQRT
+  const double iE = sa_rsqrt(q0);
+  const double E = q0 * iE;
+#else
   const double E = sqrt(q0);
   const double iE = sa_rcp(E);
+#endif
   if constexpr (kRot) {
     double c, s;
     half_angle(Dh * iE, mh * iE, Dh >= 0.0, c, s);
@@ -186,7 +227,11 @@ __host__ __device__ __forceinline__ void sa_levels_linear(double Dh, double sg, 
       if (l % 2 == 0) acc = __builtin_fma(e[l / 2], e[l / 2], acc);
       e[l] = ((l == 2 ? 1.0 : 0.0) - acc) * h0;
     }
+#if LZQ_SA_RSQRT
+    const double iq = iE * iE;
+#else
     const double iq = sa_rcp(q0);
+#endif
     double w[M];
     w[0] = -mh * sg * iq;
 #pragma unroll
@@ -283,7 +328,10 @@ __host__ __device__ __forceinline__ double sa_phase(double ta, double tb, double
   const double ulo = fmin(u1, u2), uhi = fmax(u1, u2);
   const double half = 0.5 * (uhi - ulo), mid = 0.5 * (uhi + ulo);
   double acc = 0.0;
-#pragma nounroll
+#ifndef LZQ_SA_PHASE_UNROLL
+#define LZQ_SA_PHASE_UNROLL 1  // the 4 Gauss points one after another (2, 4: side by side, tools/ablate_prop.py)
+#endif
+#pragma unroll LZQ_SA_PHASE_UNROLL
   for (int k = 0; k < 4; ++k) {
     const double u = __builtin_fma(half, gx[k], mid);
     const double iu = sa_rcp(u);
@@ -320,8 +368,32 @@ __host__ __device__ __forceinline__ SU2 sa_reflect(const SU2& u) {
 // state, so lz_follow_kernel computes them ahead of the propagation.  The core-edge frame is
 // computed once (the one at -tau_c by sa_reflect), and one frame per loop iteration: two side by
 // side (they are independent) would need ~250 VGPRs.
+#ifndef LZQ_FOLLOW_PAIR
+#define LZQ_FOLLOW_PAIR 0  // 1: the two outer frames (and phases) side by side after the core's (tools/ablate_prop.py)
+#endif
+__host__ __device__ __forceinline__ SU2 sa_frame(double tau, double sg, double mh, bool outer) {
+  const double Ef2 = tau * tau + mh * mh, Ef4 = Ef2 * Ef2, Ef12 = Ef4 * Ef4 * Ef4;
+  const bool far6 = outer && kSAFarC * fmax(mh, kSAMFloor) <= 0.1 * kSATol * Ef12 * sqrt(Ef2);
+  SU2 u;
+  if (far6)
+    sa_levels_linear<kSAFarLevels, true, false>(sg * tau, sg, mh, u, nullptr, nullptr);
+  else
+    sa_levels_linear<kSALevels, true, false>(sg * tau, sg, mh, u, nullptr, nullptr);
+  return u;
+}
 __host__ __device__ __forceinline__ void sa_cell_follow(double mh, double sg, double tl, double tr, double tau_c,
                                                         bool has_left, bool has_right, SU2& ML, SU2& MR) {
+#if LZQ_FOLLOW_PAIR
+  if (!(has_left || has_right)) return;
+  const SU2 uc = sa_frame(tau_c, sg, mh, false);
+  // both outer stretches in one straight block (the compiler interleaves the independent chains);
+  // a side that is absent evaluates the other's arguments and is not stored
+  const double ta = has_left ? tl : tr, tb = has_right ? tr : tl;
+  const SU2 ua = sa_frame(ta, sg, mh, true), ub = sa_frame(tb, sg, mh, true);
+  const double pa = sa_phase(ta, -tau_c, mh), pb = sa_phase(tau_c, tb, mh);
+  if (has_left) ML = su2_mul(sa_reflect(uc), su2_phase_adj(pa, ua));
+  if (has_right) MR = su2_mul(ub, su2_phase_adj(pb, uc));
+#else
   SU2 uc;
 #pragma nounroll
   for (int job = 0; job < 3; ++job) {
@@ -341,6 +413,7 @@ __host__ __device__ __forceinline__ void sa_cell_follow(double mh, double sg, do
     else
       MR = su2_mul(u, su2_phase_adj(sa_phase(tau_c, tr, mh), uc));               // U(tr) P U(tau_c)^+
   }
+#endif
 }
 
 }  // namespace lzq

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Run lz_propagate_kernel alone on a C5 slice (for rocprofv3 PMC / kernel-trace passes):
-    python tools/prop_only.py [n_points] [n_cross] [repeats]"""
+    python tools/prop_only.py [n_points] [n_cross] [repeats] [library path (default: the in-tree build)]"""
 import importlib
 import json
 import os
@@ -20,7 +20,8 @@ def main():
     nc = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
     sw = importlib.import_module(PKG + ".sweep")
-    eng = importlib.import_module(PKG + ".engine").Engine(0)
+    lib = sys.argv[4] if len(sys.argv) > 4 else None
+    eng = importlib.import_module(PKG + ".engine").Engine(0, lib_path=lib)
     spec = sw.builtin_specs()["C5"]
     spec = dataclasses.replace(spec, crossings=dataclasses.replace(spec.crossings, n_cross=nc))
     start = (spec.total - n) // 2

@@ -18,6 +18,8 @@
 #include <math.h>
 #include <stdio.h>
 
+#include <algorithm>
+
 #include "../../include/lzq.h"
 #include "lzq_exp2.h"
 #include "lzq_internal.h"
@@ -1625,6 +1627,7 @@ struct TpEnd {  // an interval's end state from its start node, and its derivati
 };
 struct TpCtl {
   int64_t N, M;     // the point's steps and intervals
+  int64_t L;        // its interval length (steps)
   double err;       // the last update's largest relative correction
   int32_t phase;    // kTpIter, kTpDone (converged; node M is the result), kTpFallback (sequential path)
   int32_t iters;    // Newton updates applied
@@ -1701,9 +1704,12 @@ __global__ __launch_bounds__(256) void ode_tp_init_kernel(const lzq_point* __res
   const int64_t p = blockIdx.x;
   const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
   const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
-  const int64_t M = S.st == LZQ_ODE_OK ? (S.N + L - 1) / L : 0;
+  // the point's own interval length: L steps, more when its N would need over Mmax intervals
+  // (max_steps only sizes the node arrays)
+  const int64_t Lp = S.N > L * Mmax ? (S.N + Mmax - 1) / Mmax : L;
+  const int64_t M = S.st == LZQ_ODE_OK ? (S.N + Lp - 1) / Lp : 0;
   const bool go = S.st == LZQ_ODE_OK && M >= 2 && M <= Mmax;
-  if (threadIdx.x == 0) ctl[p] = TpCtl{S.N, M, 0.0, go ? kTpIter : kTpFallback, 0, S.o.sigmav != 0.0 ? 1 : 0, 0};
+  if (threadIdx.x == 0) ctl[p] = TpCtl{S.N, M, Lp, 0.0, go ? kTpIter : kTpFallback, 0, S.o.sigmav != 0.0 ? 1 : 0, 0};
   if (!go) return;
   TpNode* nd = nodes + p * (Mmax + 1);
   for (int64_t m = threadIdx.x; m <= M; m += blockDim.x)
@@ -1810,7 +1816,7 @@ __global__ __launch_bounds__(64) void ode_tp_interval_kernel(const lzq_point* __
   if (c.phase != kTpIter || m >= c.M) return;
   const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
   const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
-  const int64_t k0 = m * L, k1 = k0 + L < S.N ? k0 + L : S.N;
+  const int64_t k0 = m * c.L, k1 = k0 + c.L < S.N ? k0 + c.L : S.N;
   const double xb = branch_x(S.o, S.x0, S.x1);
   const TpNode nd = nodes[p * (Mmax + 1) + m];
   TpState St{nd.Ychi, nd.YB, nd.Yp, {nd.Z[0], nd.Z[1], nd.Z[2]}, nd.have != 0};
@@ -1855,7 +1861,7 @@ __global__ __launch_bounds__(256) void ode_tp_guess_kernel(const lzq_point* __re
   __syncthreads();
   TpNode* nd = nodes + p * (Mmax + 1);
   for (int64_t m = 1 + threadIdx.x; m <= c.M; m += blockDim.x) {
-    const int64_t km = m * L < S.N ? m * L : S.N;  // node m's step index (node M: x1)
+    const int64_t km = m * c.L < S.N ? m * c.L : S.N;  // node m's step index (node M: x1)
     const double u = (double)km / (double)S.N * (double)kTpGuessSteps;
     const int64_t j = u < (double)kTpGuessSteps ? (int64_t)u : kTpGuessSteps - 1;
     const double t = u - (double)j;
@@ -2290,9 +2296,10 @@ constexpr double kTpTol = 1e-14;  // largest relative node correction of a conve
 int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, const int32_t* d_tidx,
                         const double* d_work, int64_t max_steps, lzq_yield* d_out, int32_t* d_status,
                         int32_t* d_iters, hipStream_t s, const char* fn) {
-  const int64_t L0 = lzq::g_ode_tp_interval;
-  const int64_t L = max_steps > L0 * kTpMaxIntervals ? (max_steps + kTpMaxIntervals - 1) / kTpMaxIntervals : L0;
-  const int64_t Mmax = (max_steps + L - 1) / L;
+  // node arrays for max_steps at the default interval length, at most kTpMaxIntervals per point
+  // (a point whose N needs more takes longer intervals, ode_tp_init_kernel)
+  const int64_t L = lzq::g_ode_tp_interval;
+  const int64_t Mmax = std::min<int64_t>((max_steps + L - 1) / L, kTpMaxIntervals);
   if (n > kTpMaxPoints || Mmax < 2) {  // nothing to cut: the sequential path alone
     if (d_iters) {
       int rc = hip_check(hipMemsetAsync(d_iters, 0, sizeof(int32_t) * (size_t)n, s), fn);

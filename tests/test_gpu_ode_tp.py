@@ -137,3 +137,26 @@ def test_tp_is_stream_ordered_and_deterministic(gpu_engine):
         y, sy = gpu_engine.ode(p, o, time_parallel=True)
     s.synchronize()
     assert torch.equal(sx, sy) and torch.equal(x, y) and bool((sx == 0).all())
+
+
+def test_tp_raw_abi_large_step_cap(gpu_engine):
+    """The C ABI with a step cap far above the window's need (max_steps only sizes the node arrays:
+    the point takes intervals of its own length) and with d_iters / d_status NULL."""
+    import ctypes
+    cfg = full_cfg({**BASE_CFG, "Gamma_wash_over_H": 1.0, "sigma_v_chi_GeV_m2": 1e-12})
+    p, o = recs([cfg])
+    ref, sr = gpu_engine.ode(p, o, time_parallel=False)
+    d_p = gpu_engine.points_to_device(p)
+    d_o = torch.from_numpy(np.ascontiguousarray(o).view(np.uint8).copy()).to(gpu_engine.device)
+    work, st = gpu_engine.ode_tables(d_p)
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())
+    for cap, with_iters in ((1 << 40, True), (1 << 22, False)):
+        out = torch.empty((1, 6), dtype=torch.float64, device=gpu_engine.device)
+        its = torch.zeros(1, dtype=torch.int32, device=gpu_engine.device)
+        rc = gpu_engine.lib.lzq_ode_integrate_tp(vp(d_p), vp(d_o), 1, None, 0, vp(work), work.numel(), cap, vp(out),
+                                                 None, vp(its) if with_iters else None, None)
+        assert rc == 0
+        torch.cuda.synchronize()
+        if with_iters:
+            assert int(its[0]) > 0
+        close(out.cpu().numpy(), ref.cpu().numpy())

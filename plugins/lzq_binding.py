@@ -16,6 +16,10 @@ Entry points (each cites the fpy code it replaces):
   aov_batch(aov, ys)                                      fpy:158-165 for many y in one call
   yields(cfg, P, T_lo=None, T_hi=None, n_y=8000, nz=1200, z_max=30.0, aov=None)
                                                           fpy:231-267 + fpy:372-384 + fpy:413-417
+  ode_yields(cfg, P, aov=None, nz=1200, z_max=30.0, time_parallel=True)
+                                                          fpy:385-417 (build_tables + the Radau solve +
+                                                          densities) for one sigma_v / Gamma_wash /
+                                                          depletion config
   p_closed_form(lams)                                     fpy:183-184
   lz_propagate(m_mix, dprime, xi, v_w, window_lz, steps)  no fpy counterpart (north_star (1))
   profile_crossings(knots, phi, Phi, y_B, y_chi, lam, v_w)  PAPER eqs.(5)-(8) (the absent modules of fpy:173)
@@ -54,13 +58,22 @@ class lzq_yield(ctypes.Structure):  # include/lzq.h: struct lzq_yield (48 B)
                                                 "P_used")]
 
 
+class lzq_ode_params(ctypes.Structure):  # include/lzq.h: struct lzq_ode_params (24 B)
+    _fields_ = [("sigma_v_chi_GeV_m2", ctypes.c_double), ("Gamma_wash_over_H", ctypes.c_double),
+                ("deplete_DM_from_source", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
 class lzq_profile_point(ctypes.Structure):  # include/lzq.h: struct lzq_profile_point (40 B)
     _fields_ = [(n, ctypes.c_double) for n in ("y_B", "y_chi", "lambda_tr_eff", "v_w")] + \
         [(n, ctypes.c_int32) for n in ("shape", "reserved")]
 
 
 assert ctypes.sizeof(lzq_point) == 136 and ctypes.sizeof(lzq_yield) == 48 and ctypes.sizeof(lzq_profile_point) == 40
-assert ctypes.sizeof(lzq_aov_params) == 40
+assert ctypes.sizeof(lzq_aov_params) == 40 and ctypes.sizeof(lzq_ode_params) == 24
+ODE_NT = 800                # LZQ_ODE_NT: main()'s build_tables knots (fpy:387)
+ODE_WS_PER_POINT = 3200     # LZQ_ODE_WS_PER_POINT
+ODE_STATUS = {0: "ok", 1: "bad_grid", 2: "bad_step", 3: "too_many_steps", 4: "newton", 6: "unresolved",
+              7: "bad_table"}  # enum lzq_ode_status
 ABI_VERSION = 3  # include/lzq.h LZQ_ABI_VERSION this binding is written against
 
 _hip = None
@@ -87,6 +100,9 @@ def _libs():
         L.lzq_aov_batch.argtypes = [ctypes.POINTER(lzq_point), ctypes.POINTER(lzq_aov_params), vp, i64, i32, d, vp,
                                     vp]
         L.lzq_p_closed_form.argtypes = [vp, i64, vp, vp]
+        L.lzq_ode_tables.argtypes = [vp, i64, vp, vp, i32, i32, d, vp, vp, i64, vp, vp]
+        L.lzq_ode_integrate.argtypes = [vp, vp, i64, vp, i64, i64, vp, vp, vp]
+        L.lzq_ode_integrate_tp.argtypes = [vp, vp, i64, vp, i64, vp, i64, i64, vp, vp, vp, vp]
         L.lzq_lz_propagate.argtypes = [vp, vp, vp, i64, i32, d, d, i32, vp, vp]
         L.lzq_profile_splines.argtypes = [vp, vp, vp, i32, i32, vp, vp, vp]
         L.lzq_profile_crossings.argtypes = [vp, vp, i32, i32, vp, i64, i32, vp, vp, vp, vp, vp, vp]
@@ -231,6 +247,52 @@ def make_build_tables(fpy_module):
         self._A_spline = fpy_module.CubicSpline(Ts, np.maximum(Av, 0.0), extrapolate=True)
 
     return build_tables
+
+
+def ode_steps(cfg) -> int:
+    """The fixed Radau step count of fpy:403-404's window for a config: x0 = m/T_hi, x1 = m/T_lo,
+    max_step = min(|x1 - x0|/20000, x_p/1000, 5e-4), N = ceil(|x1 - x0| / max_step) -- the integrator's
+    own expression (0 when the window is degenerate; the library then reports the status)."""
+    import math
+    m, Tp = float(cfg.m_chi_GeV), float(cfg.T_p_GeV)
+    T_hi, T_lo = float(cfg.T_max_over_Tp) * Tp, float(cfg.T_min_over_Tp) * Tp
+    x0, x1 = m / T_hi, m / max(T_lo, 1e-30)
+    x_p = m / max(Tp, 1e-30)
+    ms = min(min(abs(x1 - x0) / 20000.0, x_p / 1000.0), 5e-4)
+    n = abs(x1 - x0) / ms if ms > 0.0 else float("nan")
+    return int(math.ceil(n)) if math.isfinite(n) else 0
+
+
+def ode_yields(cfg, P: float, aov=None, nz: int = 1200, z_max: float = 30.0, time_parallel: bool = True) -> dict:
+    """fpy:385-417 for one config on the GPU: build_tables(T_lo, T_hi, n=800) of the A/V kernel
+    (`aov`: an AoverVKernel with its own parameters and z grid, None: cfg's own on (nz, z_max)), the
+    reference's Radau IIA on its fixed-step window (fpy:403-404), Y_chi(x1), Y_B(x1) and the
+    densities; plus "status" (enum lzq_ode_status name).  time_parallel (default): the few-point
+    latency path lzq_ode_integrate_tp (~1e-15 from the sequential steps; the shipped window's
+    sigma_v != 0 point in milliseconds instead of ~0.75 s); False: lzq_ode_integrate."""
+    _, L = _libs()
+    if aov is not None:
+        nz, z_max = zgrid_of(aov)
+    pt = point_from_cfg(cfg, P)
+    od = lzq_ode_params(max(float(cfg.sigma_v_chi_GeV_m2), 0.0), max(float(cfg.Gamma_wash_over_H), 0.0),
+                        int(bool(cfg.deplete_DM_from_source)), 0)
+    ap = aov_params(aov) if aov is not None else lzq_aov_params()
+    out, st = lzq_yield(), ctypes.c_int32(-1)
+    max_steps = ode_steps(cfg) + 64
+    with _Dev(136, pt) as d_pt, _Dev(24, od) as d_od, _Dev(40, ap) as d_aov, _Dev(8 * ODE_WS_PER_POINT) as d_w, \
+            _Dev(48) as d_out, _Dev(4) as d_st:
+        _check(L.lzq_ode_tables(d_pt.p, 1, None, None, ODE_NT, int(nz), float(z_max),
+                                d_aov.p if aov is not None else None, d_w.p, ODE_WS_PER_POINT, d_st.p, None))
+        if time_parallel:
+            _check(L.lzq_ode_integrate_tp(d_pt.p, d_od.p, 1, None, 0, d_w.p, ODE_WS_PER_POINT, max_steps, d_out.p,
+                                          d_st.p, None, None))
+        else:
+            _check(L.lzq_ode_integrate(d_pt.p, d_od.p, 1, d_w.p, ODE_WS_PER_POINT, max_steps, d_out.p, d_st.p, None))
+        d_out.read(out)
+        d_st.read(st)
+    res = {n: getattr(out, n) for n, _ in lzq_yield._fields_}
+    res["status"] = ODE_STATUS.get(st.value, str(st.value))
+    return res
 
 
 def p_closed_form(lams) -> list:

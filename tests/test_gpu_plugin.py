@@ -264,3 +264,46 @@ def test_reference_side_binding(plugin_path, gpu_engine):
     lam = [float(s) for s in d["lambda"]]
     for l, g, r in zip(lam, B.p_closed_form(lam), d["P"]):
         assert abs(g - r) <= 1e-8 * abs(r) + 4.5e-16, (l, g, r)
+
+
+def test_reference_side_binding_ode(plugin_path, gpu_engine):
+    """plugins/lzq_binding.ode_yields (fpy:385-417 for one config, torch-free): the reference's own
+    ODE outputs (golden_ode.json) within the tolerance test_gpu_ode.py applies, the Engine's
+    sequential integration within 1e-13 (time-parallel) and bit for bit (time_parallel=False), a
+    refused window with the reference's status, and bs.aov's own parameters."""
+    B = importlib.import_module("lzq_binding")
+    cfgm = pkg("config")
+    pts = golden("golden_ode.json")["points"]
+    for r in pts[::3] + [pts[-1]]:
+        c = full_cfg(r["config"])
+        cfg = cfgm.Config(**c)
+        P = r.get("P_used", c["P_chi_to_B"])
+        got = B.ode_yields(cfg, P)
+        seq = B.ode_yields(cfg, P, time_parallel=False)
+        t, st = gpu_engine.ode(cfgm.to_point(dict(c, P_chi_to_B=P)), cfgm.to_ode_params(c), time_parallel=False)
+        row = t.cpu().numpy()[0]
+        if "error" in r:
+            assert got["status"] == seq["status"] == "bad_grid" and int(st[0]) == 1
+            continue
+        assert got["status"] == seq["status"] == "ok", (got, r["config"])
+        assert seq["Y_B"] == row[0] and seq["Y_chi"] == row[1]
+        assert rel_err(got["Y_B"], row[0]) < 1e-13 and rel_err(got["Y_chi"], row[1]) < 1e-13
+        if r["tight"]["success"]:
+            ref_acc = max(rel_err(r["final"]["Y_B"], r["tight"]["Y_B"]), rel_err(r["final"]["Y_chi"], r["tight"]["Y_chi"]))
+            assert rel_err(got["Y_B"], r["final"]["Y_B"]) < 1e-8 + 10 * ref_acc, (got, r["final"])
+    # bs.aov replaced: the A/V kernel's own parameters and z grid behind build_tables
+
+    class KernelStandIn:  # the attributes of the reference's AoverVKernel the binding reads (fpy:141-156)
+        def __init__(self, I_p, beta_over_H, T_p, v_w, g_star, z_max=30.0, nz=1200):
+            self.I_p, self.beta_over_H, self.T_p, self.v_w, self.g_star = I_p, beta_over_H, T_p, v_w, g_star
+            self.z = np.linspace(0.0, z_max, nz)
+
+    c = full_cfg({**BASE_CFG, "Gamma_wash_over_H": 1.0, "sigma_v_chi_GeV_m2": 1e-12, "T_max_over_Tp": 1.6,
+                  "T_min_over_Tp": 0.6})
+    cfg = cfgm.Config(**c)
+    kern = KernelStandIn(0.5, 60.0, cfg.T_p_GeV, 0.45, cfg.g_star, z_max=40.0, nz=1600)
+    got = B.ode_yields(cfg, cfg.P_chi_to_B, aov=kern)
+    aov = {"I_p": 0.5, "beta_over_H": 60.0, "T_p_GeV": cfg.T_p_GeV, "v_w": 0.45, "g_star": cfg.g_star}
+    t, st = gpu_engine.ode(cfgm.to_point(c), cfgm.to_ode_params(c), aov=aov, nz=1600, z_max=40.0, time_parallel=False)
+    assert got["status"] == "ok" and int(st[0]) == 0
+    assert rel_err(got["Y_B"], float(t[0, 0])) < 1e-13 and rel_err(got["Y_chi"], float(t[0, 1])) < 1e-13

@@ -620,8 +620,8 @@ int lzq_tune(int32_t key, int32_t value) {
     return prev;
   }
   if (key == LZQ_TUNE_ODE_TP_INTERVAL) {
-    if (value < 8 || value > (1 << 20))
-      return fail(LZQ_EINVAL, "lzq_tune: ode_tp_interval must be in [8, 2^20] steps, got %d", value);
+    if (value < 64 || value > (1 << 20) || value % 64 != 0)
+      return fail(LZQ_EINVAL, "lzq_tune: ode_tp_interval must be a multiple of 64 in [64, 2^20] steps, got %d", value);
     int prev = lzq::g_ode_tp_interval;
     lzq::g_ode_tp_interval = value;
     return prev;

@@ -19,6 +19,7 @@
 #include <stdio.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "../../include/lzq.h"
 #include "lzq_exp2.h"
@@ -578,6 +579,14 @@ __device__ __forceinline__ double fma_neg_s(double k, double a, double p) {
 #ifndef LZQ_ODE_RICVAR
 #define LZQ_ODE_RICVAR 1  // whole-wave cooperative split-free waves run ode_riccati_kernel (compact rows, uniform constants)
 #endif
+#ifndef LZQ_ODE_PRED_BLOCK
+// The Radau5 predictor is not used on steps k = 0 (mod LZQ_ODE_PRED_BLOCK): every block of that
+// many steps starts its Newton iteration from Y_chi, so a block's end state is a function of its
+// start (Y_chi, Y_B) alone -- what lzq_ode_integrate_tp's exact stitching needs.  Every integrator
+// applies the rule on the absolute step index, so all modes stay bit-identical.  (A power of two.)
+#define LZQ_ODE_PRED_BLOCK 64
+#endif
+__device__ __forceinline__ bool pred_step(int64_t k) { return (k & (LZQ_ODE_PRED_BLOCK - 1)) != 0; }
 #ifndef LZQ_RIC_MIN_WAVES
 #define LZQ_RIC_MIN_WAVES 4  // ode_riccati_kernel: minimum waves per SIMD (its VGPR cap = 512 / this)
 #endif
@@ -1179,7 +1188,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
         bool ok = true;
         const double Ystart = Ychi;
         bool use_guess = false;
-        if (riccati && have && !split) {
+        if (riccati && have && !split && pred_step(k)) {
           // the Riccati stage system has a second (unstable, other-sign) root: a predicted start
           // is used only when it stays within 25% of Y_chi, where Newton converges to the same
           // root as from Y_chi itself (an extrapolation across a fast transient can overshoot)
@@ -1451,7 +1460,7 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
       bool ok = true;
       const double Ystart = Ychi;
       bool use_guess = false;
-      if (riccati && have && !split) {
+      if (riccati && have && !split && pred_step(k)) {
         double g[3];
         use_guess = true;
 #pragma unroll
@@ -1526,7 +1535,7 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
       const double YB_prev = YB;
       const double Ystart = Ychi;
       bool use_guess = false;
-      if (riccati && have) {  // the Radau5 predictor, as ode_integrate_kernel
+      if (riccati && have && pred_step(kb + r)) {  // the Radau5 predictor, as ode_integrate_kernel
         double g[3];
         use_guess = true;
 #pragma unroll
@@ -1629,7 +1638,8 @@ struct TpCtl {
   int64_t N, M;     // the point's steps and intervals
   int64_t L;        // its interval length (steps)
   double err;       // the last update's largest relative correction
-  int32_t phase;    // kTpIter, kTpDone (converged; node M is the result), kTpFallback (sequential path)
+  int32_t phase;    // kTpIter, kTpDone (converged, to be stitched), kTpExact (stitched: the result is
+                    // written), kTpFallback (sequential path)
   int32_t iters;    // Newton updates applied
   int32_t riccati;  // sigma_v != 0: Y_chi's map is nonlinear (the update is safeguarded)
   int32_t pad;
@@ -1706,7 +1716,10 @@ __global__ __launch_bounds__(256) void ode_tp_init_kernel(const lzq_point* __res
   const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
   // the point's own interval length: L steps, more when its N would need over Mmax intervals
   // (max_steps only sizes the node arrays)
-  const int64_t Lp = S.N > L * Mmax ? (S.N + Mmax - 1) / Mmax : L;
+  // (a whole number of predictor blocks, LZQ_ODE_PRED_BLOCK: the exact stitching needs interval starts
+  // whose first step does not read the predictor)
+  constexpr int64_t B = LZQ_ODE_PRED_BLOCK;
+  const int64_t Lp = S.N > L * Mmax ? ((S.N + Mmax - 1) / Mmax + B - 1) / B * B : L;
   const int64_t M = S.st == LZQ_ODE_OK ? (S.N + Lp - 1) / Lp : 0;
   const bool go = S.st == LZQ_ODE_OK && M >= 2 && M <= Mmax;
   if (threadIdx.x == 0) ctl[p] = TpCtl{S.N, M, Lp, 0.0, go ? kTpIter : kTpFallback, 0, S.o.sigmav != 0.0 ? 1 : 0, 0};
@@ -1755,7 +1768,7 @@ __device__ __forceinline__ bool tp_steps(const OdePoint& o, const double* __rest
     const double xa = split ? xb_below : xk + h;
     const double Ystart = Ychi;
     bool use_guess = false;
-    if (riccati && have && !split) {  // the Radau5 predictor, as ode_integrate_kernel
+    if (riccati && have && !split && pred_step(k)) {  // the Radau5 predictor, as ode_integrate_kernel
       double gs[3];
       use_guess = true;
 #pragma unroll
@@ -1988,32 +2001,179 @@ __global__ __launch_bounds__(kTpScan) void ode_tp_update_kernel(int64_t Mmax, Tp
   ctl[p] = cn;
 }
 
-// Converged points: node M is the final state -> the yields (fpy:412-417) and skip[p] = 1 (the
-// sequential launches pass them by); the others: skip[p] = 0.
-__global__ __launch_bounds__(64) void ode_tp_finish_kernel(const lzq_point* __restrict__ pts, int64_t n, int64_t Mmax,
-                                                           const TpNode* __restrict__ nodes,
-                                                           const TpCtl* __restrict__ ctl, lzq_yield* __restrict__ out,
-                                                           int32_t* __restrict__ status, int32_t* __restrict__ skip,
-                                                           int32_t* __restrict__ iters) {
-  const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
+// Exact stitching.  At convergence the nodes sit within a few ulps of the sequential trajectory
+// but are formed as s + d, not carried, so the Newton result differs from the sequential one by
+// rounding.  Because no block of LZQ_ODE_PRED_BLOCK steps uses the predictor on its first step
+// (and the intervals are whole blocks), interval m's end state is a function of its start
+// (Y_chi, Y_B) alone: F_m for Y_chi, G_m for Y_B (independent chains: Y_B's step map does not read
+// Y_chi, Y_chi's Newton does not read Y_B).  So every interval is integrated from the 2J + 1
+// candidate starts s_m + j ulp, |j| <= J (both chains side by side in one lane), and the exact
+// chains are followed through the candidate tables: node 0 is exact, and if node m's exact value
+// is candidate j_m, node m + 1's is F_m(candidate j_m) -- a table entry, which again is a candidate
+// of node m + 1 unless the Newton node was more than J ulps off.  Following the chain is M
+// dependent look-ups, done as segments of kTpSeg intervals for every entry candidate in parallel
+// (ode_tp_seg_kernel), then one walk over the segments per point (ode_tp_stitch_kernel).  Each
+// candidate integration performs exactly the sequential kernels' operations on that start, so a
+// point whose chains stay inside the windows gets the sequential integration's bits; a point whose
+// chain leaves a window, or meets a bridged step, is integrated sequentially.  Three rounds: J = 4
+// (cheap, the usual case), then J = 32 and J = 256 for the points the previous did not finish (the
+// Newton nodes wander from the exact chain where the dynamics is neutral, e.g. a weakly annihilating
+// plateau; the last round only where its tables fit kTpCandBytes).
+constexpr int kTpSeg = 64;       // intervals per stitching segment
+constexpr int kTpJ1 = 4, kTpJ2 = 32, kTpJ3 = 256;
+constexpr size_t kTpCandBytes = size_t(1) << 30;  // candidate tables of the J = 256 round, at most
+
+// monotone integer key of a double (ordered like the values; -0 and +0 map to 0) and back
+__device__ __forceinline__ int64_t dkey(double x) {
+  const int64_t b = __builtin_bit_cast(int64_t, x);
+  return b >= 0 ? b : -(b & 0x7FFFFFFFFFFFFFFFll);
+}
+__device__ __forceinline__ double dfromkey(int64_t k) {
+  return __builtin_bit_cast(double, k >= 0 ? k : ((-k) | (int64_t)0x8000000000000000ull));
+}
+
+// One lane per (point, interval, candidate j): F_m and G_m at s_m + j ulp, b_m + j ulp (NaN for a
+// start that needed a bridge).  Points already stitched (phase kTpExact) or not converged return.
+constexpr int32_t kTpExact = 3;
+template <int J>
+__global__ __launch_bounds__(64) void ode_tp_cand_kernel(const lzq_point* __restrict__ pts,
+                                                         const lzq_ode_params* __restrict__ ode, int64_t n,
+                                                         const int32_t* __restrict__ tidx,
+                                                         const double* __restrict__ ws, int64_t max_steps, int64_t Mmax,
+                                                         const TpNode* __restrict__ nodes, const TpCtl* __restrict__ ctl,
+                                                         double* __restrict__ candF, double* __restrict__ candG) {
+  constexpr int NC = 2 * J + 1;
+  const int64_t g = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  const int64_t p = g / (Mmax * NC), rem = g - p * (Mmax * NC), m = rem / NC;
+  const int jj = (int)(rem - m * NC);
   if (p >= n) return;
   const TpCtl c = ctl[p];
-  const bool done = c.phase == kTpDone;
-  skip[p] = done ? 1 : 0;
-  if (iters) iters[p] = done ? c.iters : -c.iters;  // < 0: iterated, abandoned, integrated sequentially
-  if (!done) return;
-  const TpNode f = nodes[p * (Mmax + 1) + c.M];
+  if (c.phase != kTpDone || m >= c.M) return;
+  const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
+  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
+  const int64_t k0 = m * c.L, k1 = k0 + c.L < S.N ? k0 + c.L : S.N;
+  const TpNode nd = nodes[p * (Mmax + 1) + m];
+  const double y0 = dfromkey(dkey(nd.Ychi) + (jj - J)), b0 = dfromkey(dkey(nd.YB) + (jj - J));
+  // (k0 is a whole number of predictor blocks: the first step does not read Yp / Z / have)
+  TpState St{y0, b0, y0, {y0, y0, y0}, false};
+  double D = 1.0, C = 1.0;
+  const double xb = branch_x(S.o, S.x0, S.x1);
+  const bool exact = tp_steps(S.o, w, S.x0, S.h, xb, nextafter(xb, -INFINITY), k0, k1, St, D, C);
+  const int64_t o = (p * Mmax + m) * NC + jj;
+  candF[o] = exact ? St.Ychi : __builtin_nan("");
+  candG[o] = exact ? St.YB : __builtin_nan("");
+}
+
+// One lane per (point, segment, entry candidate of both chains): follow the chains through the
+// segment's intervals; the exit candidate index at the next segment's first node (-1: the chain
+// left the window or met a bridged start) and the value at the segment's end node.
+template <int J>
+__global__ __launch_bounds__(64) void ode_tp_seg_kernel(int64_t n, int64_t Mmax, int64_t Smax,
+                                                        const TpNode* __restrict__ nodes,
+                                                        const TpCtl* __restrict__ ctl,
+                                                        const double* __restrict__ candF,
+                                                        const double* __restrict__ candG, int32_t* __restrict__ segF,
+                                                        int32_t* __restrict__ segG, double* __restrict__ lastF,
+                                                        double* __restrict__ lastG) {
+  constexpr int NC = 2 * J + 1;
+  const int64_t g = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  const int64_t p = g / (Smax * NC), rem = g - p * (Smax * NC), sg = rem / NC;
+  const int jj = (int)(rem - sg * NC);
+  if (p >= n) return;
+  const TpCtl c = ctl[p];
+  if (c.phase != kTpDone || sg * kTpSeg >= c.M) return;
+  const int64_t m0 = sg * kTpSeg, m1 = m0 + kTpSeg < c.M ? m0 + kTpSeg : c.M;
+  const TpNode* nd = nodes + p * (Mmax + 1);
+  int jF = jj, jG = jj;
+  double vF = 0.0, vG = 0.0;
+  for (int64_t m = m0; m < m1; ++m) {
+    const int64_t o = (p * Mmax + m) * NC;
+    vF = jF >= 0 ? candF[o + jF] : __builtin_nan("");
+    vG = jG >= 0 ? candG[o + jG] : __builtin_nan("");
+    if (m + 1 < c.M) {  // the candidate index of node m + 1 (node M, the final state, needs none)
+      const int64_t dF = dkey(vF) - dkey(nd[m + 1].Ychi) + J, dG = dkey(vG) - dkey(nd[m + 1].YB) + J;
+#ifdef LZQ_ODE_TP_DEBUG
+      if (jj == J && ((jF >= 0 && !(isfinite(vF) && dF >= 0 && dF < NC)) || (jG >= 0 && !(isfinite(vG) && dG >= 0 && dG < NC))))
+        printf("  J %d seg %lld node %lld: offset F %lld G %lld (vF %.17g node %.17g)\n", J, (long long)sg,
+               (long long)(m + 1), (long long)(dF - J), (long long)(dG - J), vF, nd[m + 1].Ychi);
+#endif
+      jF = (isfinite(vF) && dF >= 0 && dF < NC) ? (int)dF : -1;
+      jG = (isfinite(vG) && dG >= 0 && dG < NC) ? (int)dG : -1;
+    }
+  }
+  const int64_t o = (p * Smax + sg) * NC + jj;
+  segF[o] = jF;
+  segG[o] = jG;
+  lastF[o] = vF;
+  lastG[o] = vG;
+}
+
+// One thread per point: the chains from node 0 (candidate J, the exact start) through the
+// segments; both inside their windows to the end -> the final state is the sequential one: the
+// yields, skip[p] = 1, phase kTpExact.  Otherwise the point waits for the next round or the
+// sequential launches.
+template <int J>
+__global__ __launch_bounds__(64) void ode_tp_stitch_kernel(const lzq_point* __restrict__ pts, int64_t n, int64_t Smax,
+                                                           TpCtl* __restrict__ ctl, const int32_t* __restrict__ segF,
+                                                           const int32_t* __restrict__ segG,
+                                                           const double* __restrict__ lastF,
+                                                           const double* __restrict__ lastG, lzq_yield* __restrict__ out,
+                                                           int32_t* __restrict__ status, int32_t* __restrict__ skip) {
+  constexpr int NC = 2 * J + 1;
+  const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (p >= n) return;
+  TpCtl c = ctl[p];
+#ifdef LZQ_ODE_TP_DEBUG
+  printf("tp point %lld: stitch round J = %d, phase %d\n", (long long)p, J, c.phase);
+#endif
+  if (c.phase != kTpDone) return;
+  const int64_t nseg = (c.M + kTpSeg - 1) / kTpSeg;
+  int jF = J, jG = J;
+  double YB = 0.0, Ychi = 0.0;
+  for (int64_t sg = 0; sg < nseg && jF >= 0 && jG >= 0; ++sg) {
+    const int64_t o = (p * Smax + sg) * NC;
+    if (sg + 1 == nseg) {
+      Ychi = lastF[o + jF];
+      YB = lastG[o + jG];
+    } else {
+      const int a = segF[o + jF], b = segG[o + jG];
+      jF = a;
+      jG = b;
+    }
+  }
+  if (jF < 0 || jG < 0 || !isfinite(Ychi) || !isfinite(YB)) {
+#ifdef LZQ_ODE_TP_DEBUG
+    printf("tp point %lld: stitching with J = %d failed (chains %d %d, %lld segments)\n", (long long)p, J, jF, jG,
+           (long long)nseg);
+#endif
+    return;
+  }
+  c.phase = kTpExact;
+  ctl[p] = c;
+  skip[p] = 1;
   const double m = pts[p].m_chi_GeV;
   lzq_yield r;
-  const double nB0 = f.YB * kS0M3, nDM0 = f.Ychi * kS0M3;
-  r.Y_B = f.YB;
-  r.Y_chi = f.Ychi;
+  const double nB0 = YB * kS0M3, nDM0 = Ychi * kS0M3;  // fpy:412-417
+  r.Y_B = YB;
+  r.Y_chi = Ychi;
   r.rho_B_kg_m3 = nB0 * kMProtonKg;
   r.rho_DM_kg_m3 = nDM0 * (m * kGeVToKg);
   r.DM_over_B = r.rho_DM_kg_m3 / pymax(r.rho_B_kg_m3, 1e-300);
   r.P_used = pts[p].P_chi_to_B;
   out[p] = r;
   if (status) status[p] = LZQ_ODE_OK;
+}
+
+// skip[p] from the phase (stitched points only), and the optional update counts (< 0: iterated,
+// not stitched, integrated sequentially).
+__global__ __launch_bounds__(64) void ode_tp_finish_kernel(int64_t n, const TpCtl* __restrict__ ctl,
+                                                           int32_t* __restrict__ skip, int32_t* __restrict__ iters) {
+  const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (p >= n) return;
+  const TpCtl c = ctl[p];
+  const bool done = c.phase == kTpExact;
+  skip[p] = done ? 1 : 0;
+  if (iters) iters[p] = done ? c.iters : -c.iters;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2308,17 +2468,36 @@ int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, 
     return launch_integrate<false>(d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, s, fn);
   }
   auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const int64_t Smax = (Mmax + lzq::kTpSeg - 1) / lzq::kTpSeg;
+  const bool round3 = 2 * sizeof(double) * (size_t)n * (size_t)Mmax * (size_t)(2 * lzq::kTpJ3 + 1) <= lzq::kTpCandBytes;
+  const int64_t NC2 = 2 * (round3 ? lzq::kTpJ3 : lzq::kTpJ2) + 1;
   const size_t b_nodes = up(sizeof(lzq::TpNode) * (size_t)n * (size_t)(Mmax + 1));
   const size_t b_ends = up(sizeof(lzq::TpEnd) * (size_t)n * (size_t)Mmax);
   const size_t b_ctl = up(sizeof(lzq::TpCtl) * (size_t)n);
   const size_t b_skip = up(sizeof(int32_t) * (size_t)n);
+  const size_t b_cand = up(sizeof(double) * (size_t)n * (size_t)Mmax * (size_t)NC2);  // per chain
+  const size_t b_segi = up(sizeof(int32_t) * (size_t)n * (size_t)Smax * (size_t)NC2);
+  const size_t b_segv = up(sizeof(double) * (size_t)n * (size_t)Smax * (size_t)NC2);
   char* buf = nullptr;
-  int rc = hip_check(hipMallocAsync((void**)&buf, b_nodes + b_ends + b_ctl + b_skip, s), fn);
+  int rc = hip_check(hipMallocAsync((void**)&buf, b_nodes + b_ends + b_ctl + b_skip + 2 * (b_cand + b_segi + b_segv), s),
+                     fn);
   if (rc) return rc;
-  auto* nodes = reinterpret_cast<lzq::TpNode*>(buf);
-  auto* ends = reinterpret_cast<lzq::TpEnd*>(buf + b_nodes);
-  auto* ctl = reinterpret_cast<lzq::TpCtl*>(buf + b_nodes + b_ends);
-  auto* skip = reinterpret_cast<int32_t*>(buf + b_nodes + b_ends + b_ctl);
+  char* q = buf;
+  auto take = [&](size_t b) {
+    char* r = q;
+    q += b;
+    return r;
+  };
+  auto* nodes = reinterpret_cast<lzq::TpNode*>(take(b_nodes));
+  auto* ends = reinterpret_cast<lzq::TpEnd*>(take(b_ends));
+  auto* ctl = reinterpret_cast<lzq::TpCtl*>(take(b_ctl));
+  auto* skip = reinterpret_cast<int32_t*>(take(b_skip));
+  auto* candF = reinterpret_cast<double*>(take(b_cand));
+  auto* candG = reinterpret_cast<double*>(take(b_cand));
+  auto* segF = reinterpret_cast<int32_t*>(take(b_segi));
+  auto* segG = reinterpret_cast<int32_t*>(take(b_segi));
+  auto* lastF = reinterpret_cast<double*>(take(b_segv));
+  auto* lastG = reinterpret_cast<double*>(take(b_segv));
   hipLaunchKernelGGL(lzq::ode_tp_init_kernel, dim3((unsigned)n), dim3(256), 0, s, d_points, d_ode, d_tidx, d_work,
                      max_steps, L, Mmax, nodes, ctl);
   rc = hip_check(hipGetLastError(), fn);
@@ -2337,9 +2516,27 @@ int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, 
                        kTpMaxIters, kTpTol);
     rc = hip_check(hipGetLastError(), fn);
   }
+  // exact stitching, J = kTpJ1 then kTpJ2 for the points the first round did not finish
+  auto stitch = [&](auto Jc) {
+    constexpr int J = decltype(Jc)::value, NC = 2 * J + 1;
+    hipLaunchKernelGGL(lzq::ode_tp_cand_kernel<J>, dim3((unsigned)((n * Mmax * NC + 63) / 64)), dim3(64), 0, s,
+                       d_points, d_ode, n, d_tidx, d_work, max_steps, Mmax, nodes, ctl, candF, candG);
+    int r = hip_check(hipGetLastError(), fn);
+    if (r) return r;
+    hipLaunchKernelGGL(lzq::ode_tp_seg_kernel<J>, dim3((unsigned)((n * Smax * NC + 63) / 64)), dim3(64), 0, s, n, Mmax,
+                       Smax, nodes, ctl, candF, candG, segF, segG, lastF, lastG);
+    r = hip_check(hipGetLastError(), fn);
+    if (r) return r;
+    hipLaunchKernelGGL(lzq::ode_tp_stitch_kernel<J>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, d_points, n, Smax,
+                       ctl, segF, segG, lastF, lastG, d_out, d_status, skip);
+    return hip_check(hipGetLastError(), fn);
+  };
+  if (rc == LZQ_OK) rc = stitch(std::integral_constant<int, lzq::kTpJ1>());
+  if (rc == LZQ_OK) rc = stitch(std::integral_constant<int, lzq::kTpJ2>());
+  if (rc == LZQ_OK && round3) rc = stitch(std::integral_constant<int, lzq::kTpJ3>());
   if (rc == LZQ_OK) {
-    hipLaunchKernelGGL(lzq::ode_tp_finish_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, d_points, n, Mmax,
-                       nodes, ctl, d_out, d_status, skip, d_iters);
+    hipLaunchKernelGGL(lzq::ode_tp_finish_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, n, ctl, skip,
+                       d_iters);
     rc = hip_check(hipGetLastError(), fn);
   }
   if (rc == LZQ_OK)

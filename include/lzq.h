@@ -169,8 +169,9 @@ int lzq_ztables(int32_t nz, double z_max, double* z, double* gamma4, double* ome
  * loop of Magnus steps per lane, a lane entering its next interval while the others step) or the
  * interval-by-interval loop in keyed launch order (measured faster).  P is
  * bit-identical either way (tests/test_gpu_profile.py). */
-/* LZQ_TUNE_ODE_TP_INTERVAL (steps, 8..2^20; default 64): the interval length of lzq_ode_integrate_tp's
- * multiple shooting (longer for a point whose window would need over 65536 intervals). */
+/* LZQ_TUNE_ODE_TP_INTERVAL (steps, a multiple of 64 in [64, 2^20]; default 64): the interval length of
+ * lzq_ode_integrate_tp's multiple shooting (longer for a point whose window would need over 65536
+ * intervals). */
 enum lzq_tune_key { LZQ_TUNE_EXP = 0, LZQ_TUNE_TRUNCATE = 1, LZQ_TUNE_ODE_COOP = 2, LZQ_TUNE_ODE_LAUNCH_STEPS = 3,
                     LZQ_TUNE_PROFILE_FLAT = 4, LZQ_TUNE_ODE_TP_INTERVAL = 5 };
 enum lzq_exp_variant { LZQ_EXP_POLY11 = 0, LZQ_EXP_TABLE = 1 };

@@ -175,12 +175,13 @@ def test_tune_ode_coop_knob():
 
 
 def test_tune_ode_tp_interval_knob():
-    """lzq_tune(LZQ_TUNE_ODE_TP_INTERVAL): 64 steps by default, [8, 2^20] only, returns the previous."""
+    """lzq_tune(LZQ_TUNE_ODE_TP_INTERVAL): 64 steps by default, multiples of 64 in [64, 2^20] only
+    (whole predictor blocks), returns the previous."""
     n = pkg("_native")
     L = n.load()
-    assert L.lzq_tune(n.TUNE_ODE_TP_INTERVAL, 16) == 64
-    assert L.lzq_tune(n.TUNE_ODE_TP_INTERVAL, 64) == 16
-    for bad in (7, (1 << 20) + 1, -1):
+    assert L.lzq_tune(n.TUNE_ODE_TP_INTERVAL, 128) == 64
+    assert L.lzq_tune(n.TUNE_ODE_TP_INTERVAL, 64) == 128
+    for bad in (7, 16, 96, (1 << 20) + 64, -64):
         assert L.lzq_tune(n.TUNE_ODE_TP_INTERVAL, bad) < 0 and b"ode_tp_interval" in L.lzq_last_error()
     assert L.lzq_tune(n.TUNE_ODE_TP_INTERVAL, 64) == 64
 

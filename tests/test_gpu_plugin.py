@@ -287,7 +287,7 @@ def test_reference_side_binding_ode(plugin_path, gpu_engine):
             continue
         assert got["status"] == seq["status"] == "ok", (got, r["config"])
         assert seq["Y_B"] == row[0] and seq["Y_chi"] == row[1]
-        assert rel_err(got["Y_B"], row[0]) < 1e-13 and rel_err(got["Y_chi"], row[1]) < 1e-13
+        assert got["Y_B"] == row[0] and got["Y_chi"] == row[1]   # time-parallel: the same bits
         if r["tight"]["success"]:
             ref_acc = max(rel_err(r["final"]["Y_B"], r["tight"]["Y_B"]), rel_err(r["final"]["Y_chi"], r["tight"]["Y_chi"]))
             assert rel_err(got["Y_B"], r["final"]["Y_B"]) < 1e-8 + 10 * ref_acc, (got, r["final"])

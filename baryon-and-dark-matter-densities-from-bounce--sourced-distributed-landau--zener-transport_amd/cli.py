@@ -53,7 +53,7 @@ def main(argv=None):
         table = eng.yields(to_point(cfg, P=P_used), n_y=8000)  # fpy:374 + fpy:376-417 on the GPU
     else:
         # fpy:385-410: build_tables + Radau, then fpy:412-417; one point: Engine.ode integrates it
-        # parallel in time (lzq_ode_integrate_tp, within ~1e-13 of the sequential steps)
+        # parallel in time (lzq_ode_integrate_tp, the sequential steps' bits)
         table, status = eng.ode(to_point(cfg, P=P_used), to_ode_params(cfg))
         st = int(status[0].item())
         if st in (_native.ODE_BAD_GRID, _native.ODE_BAD_STEP):  # scipy's ValueError (CubicSpline / solve_ivp)

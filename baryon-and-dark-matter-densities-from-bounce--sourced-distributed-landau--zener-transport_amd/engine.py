@@ -300,11 +300,11 @@ class Engine:
         point's own (bs.aov replaced before build_tables, fpy:211; see aov_to_device); the tables are
         then built per point (no sharing).
         time_parallel: integrate by lzq_ode_integrate_tp (multiple shooting: a point's steps cut into
-        intervals integrated side by side, Newton on their boundaries) -- the latency path for a few
-        points on long windows; within ~1e-13 of the sequential integration, not bit-identical to it.
-        None (default): on for a single point (the CLI's case), off otherwise, so every multi-point
-        call keeps the batch-independent bits.  Radau only.  self.last_ode_tp_iters: the Newton
-        updates per point of the last time-parallel call (0: integrated sequentially)."""
+        intervals integrated side by side, Newton on their boundaries, the exact chains stitched
+        through candidate starts) -- the latency path for a few points on long windows, with the
+        sequential integration's bits.  None (default): on for a single point (the CLI's case).
+        Radau only.  self.last_ode_tp_iters: the Newton updates per point of the last
+        time-parallel call (<= 0: integrated sequentially)."""
         nz, z_max = _native.zgrid(nz, z_max)
         if method not in ("radau", "quadrature"):
             raise ValueError(f"method must be 'radau' or 'quadrature', got {method!r}")

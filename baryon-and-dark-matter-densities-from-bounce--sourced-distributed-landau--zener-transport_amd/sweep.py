@@ -629,10 +629,9 @@ def make_compute(spec: SweepSpec, engine, reuse: bool = False) -> ComputeFn:
                   (ods["deplete_DM_from_source"] != 0)
             sel = np.nonzero(ode)[0]
             if sel.size:
-                # sequential integration even for a chunk with one ODE point: a row's bits do not
-                # depend on the chunking or sharding (Engine.ode's time-parallel default is n == 1)
+                # (a chunk with a single ODE point integrates it parallel in time: the same bits)
                 tab, status = engine.ode(pts[sel], ods[sel], method=spec.ode_method, max_steps=spec.ode_max_steps,
-                                         nz=spec.nz, z_max=spec.z_max, time_parallel=False)
+                                         nz=spec.nz, z_max=spec.z_max)
                 for k in tables:
                     tables[k] += engine.last_ode_tables[k]
                 # a point the integrator did not finish normally (a Radau Newton failure reports the

@@ -322,15 +322,17 @@ int lzq_ode_integrate_shared(const lzq_point* d_points, const lzq_ode_params* d_
  * point's N fixed steps are cut into intervals of LZQ_TUNE_ODE_TP_INTERVAL steps, every interval
  * is integrated from a guess of its start state on its own lane (the same per-step operations),
  * and Newton's method on the interval boundaries (multiple shooting; the corrections by a scan of
- * the intervals' linearised maps) iterates the guesses to the sequential trajectory.  A point's
- * latency drops from N serial steps to (a few iterations) x (one interval).  The result is the
- * sequential integration's up to rounding -- the boundaries are formed as guess + correction
- * instead of carried -- within ~1e-13 relative (tests/test_gpu_ode_tp.py), NOT bit-identical to
- * lzq_ode_integrate.  A point whose iteration does not converge to 1e-14 within 48 updates, whose
- * interval meets a Newton failure, or whose status is not OK, takes the sequential integration
- * (same statuses and results as lzq_ode_integrate); so does every point of a batch of more than
- * 64.  d_iters (optional, [n] int32): the Newton updates a point took; 0: not iterated, -k: abandoned
- * after k updates; both then integrated sequentially.
+ * the intervals' linearised maps) iterates the guesses to within a few ulps of the sequential
+ * trajectory; then every interval is integrated from the candidate starts around its converged
+ * node and the exact chains are followed through those tables from the exact initial state (no
+ * integrator uses the predictor on the first step of a 64-step block, so an interval's end is a
+ * function of its start values alone).  A point's latency drops from N serial steps to (a few
+ * iterations + the candidate pass) x (one interval), and its result is lzq_ode_integrate's, BIT FOR
+ * BIT (tests/test_gpu_ode_tp.py).  A point whose iteration does not converge to 1e-14 within 48
+ * updates, whose exact chain leaves the candidate windows (+-256 ulps), or whose status is not OK,
+ * takes the sequential integration (the same bits again, at the sequential cost); so does every
+ * point of a batch of more than 64.  d_iters (optional, [n] int32): the Newton updates of a point
+ * that was stitched; 0: not iterated, -k: iterated k updates, then integrated sequentially.
  * Blocks nothing: the iteration count is fixed (48 rounds of two launches; a converged point's
  * later launches return at once), so the call is stream-ordered like lzq_ode_integrate. */
 int lzq_ode_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n,

@@ -268,8 +268,8 @@ def ode_yields(cfg, P: float, aov=None, nz: int = 1200, z_max: float = 30.0, tim
     (`aov`: an AoverVKernel with its own parameters and z grid, None: cfg's own on (nz, z_max)), the
     reference's Radau IIA on its fixed-step window (fpy:403-404), Y_chi(x1), Y_B(x1) and the
     densities; plus "status" (enum lzq_ode_status name).  time_parallel (default): the few-point
-    latency path lzq_ode_integrate_tp (~1e-15 from the sequential steps; the shipped window's
-    sigma_v != 0 point in milliseconds instead of ~0.75 s); False: lzq_ode_integrate."""
+    latency path lzq_ode_integrate_tp (the sequential steps' bits; the shipped window's sigma_v != 0
+    point in milliseconds instead of ~0.8 s); False: lzq_ode_integrate."""
     _, L = _libs()
     if aov is not None:
         nz, z_max = zgrid_of(aov)

@@ -1623,16 +1623,17 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
 // the ~1e-14 level (tests/test_gpu_ode_tp.py).  A point whose iteration does not converge within
 // the budget, or one whose interval hits a Newton failure, is integrated sequentially instead.
 // ---------------------------------------------------------------------------------------
-struct TpNode {  // the integrator's state at the start of an interval
-  double Ychi, YB, Yp, Z[3];
-  int32_t have, pad;
+// The integrator's state at the start of an interval is (Y_chi, Y_B) alone: intervals are whole
+// predictor blocks (LZQ_ODE_PRED_BLOCK), whose first step does not read the predictor's data.
+struct TpNode {
+  double Ychi, YB;
 };
 struct TpEnd {  // an interval's end state from its start node, and its derivatives
-  double Ychi, YB, Yp, Z[3];
+  double Ychi, YB;
   double D;  // dY_chi(end) / dY_chi(start)
   double C;  // dY_B(end) / dY_B(start)
-  int32_t have;
   int32_t exact;  // every step took the Radau step (0: a Newton failure was bridged, see tp_bridge)
+  int32_t pad;
 };
 struct TpCtl {
   int64_t N, M;     // the point's steps and intervals
@@ -1726,7 +1727,7 @@ __global__ __launch_bounds__(256) void ode_tp_init_kernel(const lzq_point* __res
   if (!go) return;
   TpNode* nd = nodes + p * (Mmax + 1);
   for (int64_t m = threadIdx.x; m <= M; m += blockDim.x)
-    nd[m] = TpNode{S.Ychi0, 0.0, S.Ychi0, {S.Ychi0, S.Ychi0, S.Ychi0}, 0, 0};
+    nd[m] = TpNode{S.Ychi0, 0.0};
 }
 
 // A Riccati step whose Newton iteration fails -- possible only from a start far above the
@@ -1832,10 +1833,10 @@ __global__ __launch_bounds__(64) void ode_tp_interval_kernel(const lzq_point* __
   const int64_t k0 = m * c.L, k1 = k0 + c.L < S.N ? k0 + c.L : S.N;
   const double xb = branch_x(S.o, S.x0, S.x1);
   const TpNode nd = nodes[p * (Mmax + 1) + m];
-  TpState St{nd.Ychi, nd.YB, nd.Yp, {nd.Z[0], nd.Z[1], nd.Z[2]}, nd.have != 0};
+  TpState St{nd.Ychi, nd.YB, nd.Ychi, {nd.Ychi, nd.Ychi, nd.Ychi}, false};  // (the first step reads no predictor)
   double D = 1.0, C = 1.0;
   const bool exact = tp_steps(S.o, w, S.x0, S.h, xb, nextafter(xb, -INFINITY), k0, k1, St, D, C);
-  ends[p * Mmax + m] = TpEnd{St.Ychi, St.YB, St.Yp, {St.Z[0], St.Z[1], St.Z[2]}, D, C, St.have ? 1 : 0, exact ? 1 : 0};
+  ends[p * Mmax + m] = TpEnd{St.Ychi, St.YB, D, C, exact ? 1 : 0, 0};
 }
 
 // The first guess of long Riccati windows (M >= kTpGuessMin intervals): the same integrator on kTpGuessSteps
@@ -1881,124 +1882,164 @@ __global__ __launch_bounds__(256) void ode_tp_guess_kernel(const lzq_point* __re
     const double y0 = s_y[j], y1 = s_y[j + 1];
     const double y = (y0 > 0.0 && y1 > 0.0) ? y0 * exp(t * log(y1 / y0)) : y0 + t * (y1 - y0);
     const double b = s_b[j] + t * (s_b[j + 1] - s_b[j]);
-    if (isfinite(y) && isfinite(b)) nd[m] = TpNode{y, b, y, {y, y, y}, 0, 0};
+    if (isfinite(y) && isfinite(b)) nd[m] = TpNode{y, b};
   }
 }
 
-// One 1024-thread block per point: Newton's update of the nodes.  Thread t takes a contiguous run
-// of intervals, composes their affine maps d -> D d + r, the block scans the 1024 maps (Hillis-
-// Steele in LDS), and each thread re-walks its run from its carry-in, updating nodes m + 1.
-constexpr int kTpScan = 1024;
-__global__ __launch_bounds__(kTpScan) void ode_tp_update_kernel(int64_t Mmax, TpNode* __restrict__ nodes,
-                                                                const TpEnd* __restrict__ ends,
-                                                                TpCtl* __restrict__ ctl, int32_t max_iters,
-                                                                double tol) {
-  __shared__ double sA[kTpScan], sB[kTpScan], sAb[kTpScan], sBb[kTpScan];
-  __shared__ double s_err[kTpScan / 64];
-  __shared__ int s_fail;
-  const int64_t p = blockIdx.x;
-  const TpCtl c = ctl[p];
-  if (c.phase != kTpIter) return;  // block-uniform
+// Newton's update of the nodes: the corrections solve d_{m+1} = D_m d_m + r_m (r_m = F_m - s_{m+1},
+// d_0 = 0) for both chains, a scan of the affine maps d -> D d + r.  Three launches, kTpBlk
+// intervals per block: (1) each block scans its maps in LDS (Hillis-Steele) and stores the local
+// inclusive prefixes and its aggregate; (2) each block scans the aggregates of the blocks before it
+// (in LDS, at most Mmax / kTpBlk of them), applies the carry to its prefixes and updates its nodes;
+// (3) one thread per point folds the blocks' largest corrections and failure flags into TpCtl.
+constexpr int kTpBlk = 256;
+struct TpMap {
+  double A, B, Ab, Bb;  // d -> A d + B (Y_chi), d -> Ab d + Bb (Y_B)
+};
+__device__ __forceinline__ TpMap tp_compose(const TpMap& later, const TpMap& earlier) {  // later o earlier
+  return TpMap{later.A * earlier.A, __builtin_fma(later.A, earlier.B, later.B), later.Ab * earlier.Ab,
+               __builtin_fma(later.Ab, earlier.Bb, later.Bb)};
+}
+// inclusive block scan of kTpBlk maps (every thread of the block calls it)
+__device__ __forceinline__ TpMap tp_block_scan(TpMap v, TpMap* sm) {
   const int t = threadIdx.x;
-  if (t == 0) s_fail = 0;
-  const int64_t M = c.M;
-  TpNode* nd = nodes + p * (Mmax + 1);
-  const TpEnd* en = ends + p * Mmax;
-  const int64_t per = (M + kTpScan - 1) / kTpScan;
-  const int64_t m0 = (int64_t)t * per < M ? (int64_t)t * per : M, m1 = m0 + per < M ? m0 + per : M;
-  double A = 1.0, B = 0.0, Ab = 1.0, Bb = 0.0;
-  bool fail = false;
-  for (int64_t m = m0; m < m1; ++m) {  // this run's map: d_{m1} = A d_{m0} + B
-    const TpEnd& e = en[m];
-    const double sy = nd[m + 1].Ychi, sb = nd[m + 1].YB;
+  sm[t] = v;
+  __syncthreads();
+  for (int off = 1; off < kTpBlk; off <<= 1) {
+    const TpMap prev = t >= off ? sm[t - off] : TpMap{1.0, 0.0, 1.0, 0.0};
+    __syncthreads();
+    if (t >= off) v = tp_compose(v, prev);
+    sm[t] = v;
+    __syncthreads();
+  }
+  return v;
+}
+struct TpBlkOut {
+  double err;
+  int32_t fail, pad;
+};
+
+__global__ __launch_bounds__(kTpBlk) void ode_tp_scan_local_kernel(int64_t Mmax, int64_t Bmax,
+                                                                   const TpNode* __restrict__ nodes,
+                                                                   const TpEnd* __restrict__ ends,
+                                                                   const TpCtl* __restrict__ ctl,
+                                                                   TpMap* __restrict__ loc, TpMap* __restrict__ agg,
+                                                                   TpBlkOut* __restrict__ bout) {
+  __shared__ TpMap sm[kTpBlk];
+  const int64_t p = blockIdx.y, b = blockIdx.x;
+  const TpCtl c = ctl[p];
+  if (c.phase != kTpIter || b * kTpBlk >= c.M) return;  // block-uniform
+  const int t = threadIdx.x;
+  const int64_t m = b * kTpBlk + t;
+  TpMap v{1.0, 0.0, 1.0, 0.0};
+  int fail = 0;
+  if (m < c.M) {
+    const TpEnd e = ends[p * Mmax + m];
+    const TpNode q = nodes[p * (Mmax + 1) + m + 1];
     const bool fin = isfinite(e.Ychi) && isfinite(e.D) && isfinite(e.YB) && isfinite(e.C);
-    fail = fail || e.exact == 0 || !fin;
+    fail = e.exact == 0 || !fin;
     // a non-finite end (a start far from the trajectory) moves nothing downstream this update
-    B = fin ? __builtin_fma(e.D, B, e.Ychi - sy) : 0.0;
-    A = fin ? e.D * A : 0.0;
-    Bb = fin ? __builtin_fma(e.C, Bb, e.YB - sb) : 0.0;
-    Ab = fin ? e.C * Ab : 0.0;
+    v = fin ? TpMap{e.D, e.Ychi - q.Ychi, e.C, e.YB - q.YB} : TpMap{0.0, 0.0, 0.0, 0.0};
   }
-  sA[t] = A, sB[t] = B, sAb[t] = Ab, sBb[t] = Bb;
-  __syncthreads();
-  if (fail) s_fail = 1;
-  for (int off = 1; off < kTpScan; off <<= 1) {  // inclusive scan: map(t) = map(t) o map(t - off)
-    double pA = 1.0, pB = 0.0, pAb = 1.0, pBb = 0.0;
-    if (t >= off) pA = sA[t - off], pB = sB[t - off], pAb = sAb[t - off], pBb = sBb[t - off];
-    __syncthreads();
-    if (t >= off) {
-      B = __builtin_fma(A, pB, B);
-      A = A * pA;
-      Bb = __builtin_fma(Ab, pBb, Bb);
-      Ab = Ab * pAb;
-      sA[t] = A, sB[t] = B, sAb[t] = Ab, sBb[t] = Bb;
-    }
+  const int any_fail = __syncthreads_or(fail);
+  v = tp_block_scan(v, sm);
+  if (m < c.M) loc[p * Mmax + m] = v;
+  if (t == kTpBlk - 1) {
+    agg[p * Bmax + b] = v;
+    bout[p * Bmax + b].fail = any_fail;
+  }
+}
+
+__global__ __launch_bounds__(kTpBlk) void ode_tp_scan_apply_kernel(int64_t Mmax, int64_t Bmax,
+                                                                   TpNode* __restrict__ nodes,
+                                                                   const TpEnd* __restrict__ ends,
+                                                                   const TpCtl* __restrict__ ctl,
+                                                                   const TpMap* __restrict__ loc,
+                                                                   const TpMap* __restrict__ agg,
+                                                                   TpBlkOut* __restrict__ bout) {
+  __shared__ TpMap sm[kTpBlk];
+  __shared__ double s_err[kTpBlk / 64];
+  const int64_t p = blockIdx.y, b = blockIdx.x;
+  const TpCtl c = ctl[p];
+  if (c.phase != kTpIter || b * kTpBlk >= c.M) return;  // block-uniform
+  const int t = threadIdx.x;
+  const int64_t nb = (c.M + kTpBlk - 1) / kTpBlk;
+  // the carry into this block: the aggregates of blocks 0 .. b-1 composed (their own scan, in
+  // rounds of kTpBlk when there are more blocks than threads)
+  TpMap carry{1.0, 0.0, 1.0, 0.0};
+  for (int64_t r0 = 0; r0 < b; r0 += kTpBlk) {
+    const int64_t k = r0 + t;
+    TpMap v = k < b ? agg[p * Bmax + k] : TpMap{1.0, 0.0, 1.0, 0.0};
+    v = tp_block_scan(v, sm);
+    const int last = (int)((b - r0 < kTpBlk ? b - r0 : kTpBlk) - 1);
+    carry = tp_compose(sm[last], carry);
     __syncthreads();
   }
-  double d = t > 0 ? sB[t - 1] : 0.0, db = t > 0 ? sBb[t - 1] : 0.0;  // d_{m0}: the runs before this one
+  (void)nb;
+  const int64_t m = b * kTpBlk + t;
   double err = 0.0;
+  if (m < c.M) {
+    const TpMap v = loc[p * Mmax + m];
+    const double d = __builtin_fma(v.A, carry.B, v.B), db = __builtin_fma(v.Ab, carry.Bb, v.Bb);  // d_{m+1}
+    const TpEnd e = ends[p * Mmax + m];
+    TpNode q = nodes[p * (Mmax + 1) + m + 1];
+    const bool fin = isfinite(e.Ychi) && isfinite(e.D) && isfinite(e.YB) && isfinite(e.C);
+    const double old = q.Ychi;
+    double nv = old + d;
+    // the Riccati stage system has a second root below zero: a correction never takes a positive
+    // node below a quarter of the smaller of its value and its predecessor interval's (positive)
+    // end (far from the solution only).  Y_chi's map is affine without annihilation (depletion may
+    // take it through zero): no safeguard there.
+    const double lo = 0.25 * pymin(old, fin && e.Ychi > 0.0 ? e.Ychi : old);
+    if (c.riccati && old > 0.0 && !(nv >= lo)) nv = lo;
+    q.Ychi = nv;
+    q.YB = q.YB + db;
+    nodes[p * (Mmax + 1) + m + 1] = q;
+    // relative to the node, floored at 1e-290: below it the doubles approach the subnormal range,
+    // whose coarser spacing no correction could resolve to the tolerance
+    const double ec = fabs(d) / pymax(fabs(nv), 1e-290), eb = fabs(db) / pymax(fabs(q.YB), 1e-290);
+    err = pymax(ec, eb);  // pymax keeps a NaN on the right: checked below
+    if (!(ec == ec) || !(eb == eb)) err = INFINITY;
 #ifdef LZQ_ODE_TP_DEBUG
-  __shared__ int s_dbg[4];  // non-finite end Y_chi / D / Y_B, non-finite correction
-  if (t < 4) s_dbg[t] = 0;
-  __syncthreads();
+    if (m == 0 || m == c.M - 1 || (m % ((c.M + 7) / 8)) == 0)
+      printf("  p %lld m %lld node %.6e end %.6e D %.3e exact %d\n", (long long)p, (long long)m, old, e.Ychi, e.D,
+             e.exact);
 #endif
-  {
-    for (int64_t m = m0; m < m1; ++m) {
-      const TpEnd& e = en[m];
-      TpNode q = nd[m + 1];
-      const bool fin = isfinite(e.Ychi) && isfinite(e.D) && isfinite(e.YB) && isfinite(e.C);
-#ifdef LZQ_ODE_TP_DEBUG
-      if (!isfinite(e.Ychi)) atomicAdd(&s_dbg[0], 1);
-      if (!isfinite(e.D)) atomicAdd(&s_dbg[1], 1);
-      if (!isfinite(e.YB)) atomicAdd(&s_dbg[2], 1);
-      if (m == 0 || m == M - 1 || (m % ((M + 7) / 8)) == 0)
-        printf("  p %lld m %lld node %.6e end %.6e D %.3e exact %d\n", (long long)p, (long long)m, q.Ychi, e.Ychi, e.D, e.exact);
-#endif
-      d = fin ? __builtin_fma(e.D, d, e.Ychi - q.Ychi) : 0.0;
-      db = fin ? __builtin_fma(e.C, db, e.YB - q.YB) : 0.0;
-      const double old = q.Ychi;
-      double nv = old + d;
-      // the Riccati stage system has a second root below zero: a correction never takes a
-      // positive node below a quarter of the smaller of its value and its predecessor interval's
-      // (positive) end (far from the solution only).  Y_chi's map is affine without annihilation
-      // (depletion may take it through zero): no safeguard there.
-      const double lo = 0.25 * pymin(old, fin && e.Ychi > 0.0 ? e.Ychi : old);
-      if (c.riccati && old > 0.0 && !(nv >= lo)) nv = lo;
-      q.Ychi = nv;
-      q.YB = q.YB + db;
-      if (fin) {
-        q.Yp = e.Yp;
-        q.Z[0] = e.Z[0], q.Z[1] = e.Z[1], q.Z[2] = e.Z[2];
-        q.have = e.have;
-      } else {
-        q.have = 0;
-      }
-      nd[m + 1] = q;
-      // relative to the node, floored at 1e-290: below it the doubles approach the subnormal range,
-      // whose coarser spacing no correction could resolve to the tolerance
-      const double ec = fabs(d) / pymax(fabs(nv), 1e-290), eb = fabs(db) / pymax(fabs(q.YB), 1e-290);
-      err = pymax(err, pymax(ec, eb));  // pymax keeps a NaN on the right: a NaN correction fails the test below
-      if (!(ec == ec) || !(eb == eb)) err = INFINITY;
-    }
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) err = pymax(err, __shfl_xor(err, off, 64));
   if ((t & 63) == 0) s_err[t >> 6] = err;
   __syncthreads();
-  if (t != 0) return;
+  if (t == 0) {
+    double e_all = 0.0;
+    for (int k = 0; k < kTpBlk / 64; ++k) e_all = pymax(e_all, s_err[k]);
+    bout[p * Bmax + b].err = e_all;
+  }
+}
+
+__global__ __launch_bounds__(64) void ode_tp_scan_finish_kernel(int64_t n, int64_t Bmax, TpCtl* __restrict__ ctl,
+                                                                const TpBlkOut* __restrict__ bout, int32_t max_iters,
+                                                                double tol) {
+  const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (p >= n) return;
+  TpCtl c = ctl[p];
+  if (c.phase != kTpIter) return;
+  const int64_t nb = (c.M + kTpBlk - 1) / kTpBlk;
   double e_all = 0.0;
-  for (int k = 0; k < kTpScan / 64; ++k) e_all = pymax(e_all, s_err[k]);
-  TpCtl cn = c;
-  cn.iters = c.iters + 1;
-  cn.err = e_all;
+  bool fail = false;
+  for (int64_t b = 0; b < nb; ++b) {
+    e_all = pymax(e_all, bout[p * Bmax + b].err);
+    fail = fail || bout[p * Bmax + b].fail != 0;
+  }
+  c.iters += 1;
+  c.err = e_all;
 #ifdef LZQ_ODE_TP_DEBUG
-  printf("tp point %lld update %d: M %lld err %.3e fail %d nonfinite end Ychi %d D %d YB %d\n", (long long)p, cn.iters,
-         (long long)M, e_all, s_fail, s_dbg[0], s_dbg[1], s_dbg[2]);
+  printf("tp point %lld update %d: M %lld err %.3e fail %d\n", (long long)p, c.iters, (long long)c.M, e_all, (int)fail);
 #endif
   // converged: the corrections are below the tolerance and every interval took only Radau steps
-  if (e_all <= tol && !s_fail) cn.phase = kTpDone;
-  else if (cn.iters >= max_iters) cn.phase = kTpFallback;
-  ctl[p] = cn;
+  if (e_all <= tol && !fail) c.phase = kTpDone;
+  else if (c.iters >= max_iters) c.phase = kTpFallback;
+  ctl[p] = c;
 }
 
 // Exact stitching.  At convergence the nodes sit within a few ulps of the sequential trajectory
@@ -2035,7 +2076,28 @@ __device__ __forceinline__ double dfromkey(int64_t k) {
 // One lane per (point, interval, candidate j): F_m and G_m at s_m + j ulp, b_m + j ulp (NaN for a
 // start that needed a bridge).  Points already stitched (phase kTpExact) or not converged return.
 constexpr int32_t kTpExact = 3;
-template <int J>
+// one (interval, candidate) of one point (out of line: the grid-stride loop around it keeps no
+// values of its own live across the integration)
+__device__ __noinline__ void tp_cand_one(const lzq_point* __restrict__ pts, const lzq_ode_params* __restrict__ ode,
+                                         const int32_t* __restrict__ tidx, const double* __restrict__ ws,
+                                         int64_t max_steps, const TpNode* __restrict__ nd, const TpCtl& c, int64_t p,
+                                         int64_t m, int off, double* __restrict__ oF, double* __restrict__ oG) {
+  const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
+  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
+  const int64_t k0 = m * c.L, k1 = k0 + c.L < S.N ? k0 + c.L : S.N;
+  const double y0 = dfromkey(dkey(nd->Ychi) + off), b0 = dfromkey(dkey(nd->YB) + off);
+  // (k0 is a whole number of predictor blocks: the first step does not read Yp / Z / have)
+  TpState St{y0, b0, y0, {y0, y0, y0}, false};
+  double D = 1.0, C = 1.0;
+  const double xb = branch_x(S.o, S.x0, S.x1);
+  const bool exact = tp_steps(S.o, w, S.x0, S.h, xb, nextafter(xb, -INFINITY), k0, k1, St, D, C);
+  *oF = exact ? St.Ychi : __builtin_nan("");
+  *oG = exact ? St.YB : __builtin_nan("");
+}
+
+// kStride: a grid-stride loop around an out-of-line body (the last round, whose full grid would be
+// ~10^5 blocks that mostly return at once); else one lane per item, the body inline (2 waves/SIMD).
+template <int J, bool kStride>
 __global__ __launch_bounds__(64) void ode_tp_cand_kernel(const lzq_point* __restrict__ pts,
                                                          const lzq_ode_params* __restrict__ ode, int64_t n,
                                                          const int32_t* __restrict__ tidx,
@@ -2043,25 +2105,30 @@ __global__ __launch_bounds__(64) void ode_tp_cand_kernel(const lzq_point* __rest
                                                          const TpNode* __restrict__ nodes, const TpCtl* __restrict__ ctl,
                                                          double* __restrict__ candF, double* __restrict__ candG) {
   constexpr int NC = 2 * J + 1;
-  const int64_t g = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  const int64_t p = g / (Mmax * NC), rem = g - p * (Mmax * NC), m = rem / NC;
-  const int jj = (int)(rem - m * NC);
-  if (p >= n) return;
-  const TpCtl c = ctl[p];
-  if (c.phase != kTpDone || m >= c.M) return;
-  const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
-  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
-  const int64_t k0 = m * c.L, k1 = k0 + c.L < S.N ? k0 + c.L : S.N;
-  const TpNode nd = nodes[p * (Mmax + 1) + m];
-  const double y0 = dfromkey(dkey(nd.Ychi) + (jj - J)), b0 = dfromkey(dkey(nd.YB) + (jj - J));
-  // (k0 is a whole number of predictor blocks: the first step does not read Yp / Z / have)
-  TpState St{y0, b0, y0, {y0, y0, y0}, false};
-  double D = 1.0, C = 1.0;
-  const double xb = branch_x(S.o, S.x0, S.x1);
-  const bool exact = tp_steps(S.o, w, S.x0, S.h, xb, nextafter(xb, -INFINITY), k0, k1, St, D, C);
-  const int64_t o = (p * Mmax + m) * NC + jj;
-  candF[o] = exact ? St.Ychi : __builtin_nan("");
-  candG[o] = exact ? St.YB : __builtin_nan("");
+  for (int64_t g = (int64_t)blockIdx.x * 64 + threadIdx.x; g < n * Mmax * NC; g += (int64_t)gridDim.x * 64) {
+    const int64_t p = g / (Mmax * NC), rem = g - p * (Mmax * NC), m = rem / NC;
+    const int jj = (int)(rem - m * NC);
+    const TpCtl c = ctl[p];
+    if (c.phase == kTpDone && m < c.M) {
+      const int64_t o = (p * Mmax + m) * NC + jj;
+      if constexpr (kStride) {
+        tp_cand_one(pts, ode, tidx, ws, max_steps, nodes + p * (Mmax + 1) + m, c, p, m, jj - J, candF + o, candG + o);
+      } else {
+        const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
+        const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
+        const int64_t k0 = m * c.L, k1 = k0 + c.L < S.N ? k0 + c.L : S.N;
+        const TpNode& nd = nodes[p * (Mmax + 1) + m];
+        const double y0 = dfromkey(dkey(nd.Ychi) + (jj - J)), b0 = dfromkey(dkey(nd.YB) + (jj - J));
+        TpState St{y0, b0, y0, {y0, y0, y0}, false};
+        double D = 1.0, C = 1.0;
+        const double xb = branch_x(S.o, S.x0, S.x1);
+        const bool exact = tp_steps(S.o, w, S.x0, S.h, xb, nextafter(xb, -INFINITY), k0, k1, St, D, C);
+        candF[o] = exact ? St.Ychi : __builtin_nan("");
+        candG[o] = exact ? St.YB : __builtin_nan("");
+      }
+    }
+    if constexpr (!kStride) break;  // one item per lane
+  }
 }
 
 // One lane per (point, segment, entry candidate of both chains): follow the chains through the
@@ -2451,7 +2518,7 @@ int launch_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int
 // of g_ode_tp_interval steps, more when max_steps would need over kTpMaxIntervals of them.
 constexpr int64_t kTpMaxPoints = 64;
 constexpr int64_t kTpMaxIntervals = 1 << 16;
-constexpr int32_t kTpMaxIters = 48;
+constexpr int32_t kTpMaxIters = 32;
 constexpr double kTpTol = 1e-14;  // largest relative node correction of a converged iteration
 int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, const int32_t* d_tidx,
                         const double* d_work, int64_t max_steps, lzq_yield* d_out, int32_t* d_status,
@@ -2478,8 +2545,14 @@ int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, 
   const size_t b_cand = up(sizeof(double) * (size_t)n * (size_t)Mmax * (size_t)NC2);  // per chain
   const size_t b_segi = up(sizeof(int32_t) * (size_t)n * (size_t)Smax * (size_t)NC2);
   const size_t b_segv = up(sizeof(double) * (size_t)n * (size_t)Smax * (size_t)NC2);
+  const int64_t Bmax = (Mmax + lzq::kTpBlk - 1) / lzq::kTpBlk;
+  const size_t b_loc = up(sizeof(lzq::TpMap) * (size_t)n * (size_t)Mmax);
+  const size_t b_agg = up(sizeof(lzq::TpMap) * (size_t)n * (size_t)Bmax);
+  const size_t b_bout = up(sizeof(lzq::TpBlkOut) * (size_t)n * (size_t)Bmax);
   char* buf = nullptr;
-  int rc = hip_check(hipMallocAsync((void**)&buf, b_nodes + b_ends + b_ctl + b_skip + 2 * (b_cand + b_segi + b_segv), s),
+  int rc = hip_check(hipMallocAsync((void**)&buf, b_nodes + b_ends + b_ctl + b_skip + 2 * (b_cand + b_segi + b_segv) +
+                                                       b_loc + b_agg + b_bout,
+                                    s),
                      fn);
   if (rc) return rc;
   char* q = buf;
@@ -2498,6 +2571,9 @@ int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, 
   auto* segG = reinterpret_cast<int32_t*>(take(b_segi));
   auto* lastF = reinterpret_cast<double*>(take(b_segv));
   auto* lastG = reinterpret_cast<double*>(take(b_segv));
+  auto* loc = reinterpret_cast<lzq::TpMap*>(take(b_loc));
+  auto* agg = reinterpret_cast<lzq::TpMap*>(take(b_agg));
+  auto* bout = reinterpret_cast<lzq::TpBlkOut*>(take(b_bout));
   hipLaunchKernelGGL(lzq::ode_tp_init_kernel, dim3((unsigned)n), dim3(256), 0, s, d_points, d_ode, d_tidx, d_work,
                      max_steps, L, Mmax, nodes, ctl);
   rc = hip_check(hipGetLastError(), fn);
@@ -2512,14 +2588,25 @@ int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, 
                        max_steps, L, Mmax, nodes, ends, ctl);
     rc = hip_check(hipGetLastError(), fn);
     if (rc) break;
-    hipLaunchKernelGGL(lzq::ode_tp_update_kernel, dim3((unsigned)n), dim3(lzq::kTpScan), 0, s, Mmax, nodes, ends, ctl,
-                       kTpMaxIters, kTpTol);
+    hipLaunchKernelGGL(lzq::ode_tp_scan_local_kernel, dim3((unsigned)Bmax, (unsigned)n), dim3(lzq::kTpBlk), 0, s, Mmax,
+                       Bmax, nodes, ends, ctl, loc, agg, bout);
+    rc = hip_check(hipGetLastError(), fn);
+    if (rc) break;
+    hipLaunchKernelGGL(lzq::ode_tp_scan_apply_kernel, dim3((unsigned)Bmax, (unsigned)n), dim3(lzq::kTpBlk), 0, s, Mmax,
+                       Bmax, nodes, ends, ctl, loc, agg, bout);
+    rc = hip_check(hipGetLastError(), fn);
+    if (rc) break;
+    hipLaunchKernelGGL(lzq::ode_tp_scan_finish_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, n, Bmax, ctl,
+                       bout, kTpMaxIters, kTpTol);
     rc = hip_check(hipGetLastError(), fn);
   }
   // exact stitching, J = kTpJ1 then kTpJ2 for the points the first round did not finish
   auto stitch = [&](auto Jc) {
     constexpr int J = decltype(Jc)::value, NC = 2 * J + 1;
-    hipLaunchKernelGGL(lzq::ode_tp_cand_kernel<J>, dim3((unsigned)((n * Mmax * NC + 63) / 64)), dim3(64), 0, s,
+    constexpr bool kStride = J > 32;
+    const int64_t full = (n * Mmax * NC + 63) / 64;
+    const int64_t cb = kStride ? std::min<int64_t>(full, 4096) : full;
+    hipLaunchKernelGGL((lzq::ode_tp_cand_kernel<J, kStride>), dim3((unsigned)cb), dim3(64), 0, s,
                        d_points, d_ode, n, d_tidx, d_work, max_steps, Mmax, nodes, ctl, candF, candG);
     int r = hip_check(hipGetLastError(), fn);
     if (r) return r;

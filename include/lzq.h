@@ -328,12 +328,12 @@ int lzq_ode_integrate_shared(const lzq_point* d_points, const lzq_ode_params* d_
  * integrator uses the predictor on the first step of a 64-step block, so an interval's end is a
  * function of its start values alone).  A point's latency drops from N serial steps to (a few
  * iterations + the candidate pass) x (one interval), and its result is lzq_ode_integrate's, BIT FOR
- * BIT (tests/test_gpu_ode_tp.py).  A point whose iteration does not converge to 1e-14 within 48
+ * BIT (tests/test_gpu_ode_tp.py).  A point whose iteration does not converge to 1e-14 within 32
  * updates, whose exact chain leaves the candidate windows (+-256 ulps), or whose status is not OK,
  * takes the sequential integration (the same bits again, at the sequential cost); so does every
  * point of a batch of more than 64.  d_iters (optional, [n] int32): the Newton updates of a point
  * that was stitched; 0: not iterated, -k: iterated k updates, then integrated sequentially.
- * Blocks nothing: the iteration count is fixed (48 rounds of two launches; a converged point's
+ * Blocks nothing: the iteration count is fixed (32 rounds of two launches; a converged point's
  * later launches return at once), so the call is stream-ordered like lzq_ode_integrate. */
 int lzq_ode_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n,
                          const int32_t* d_table_index, int64_t n_tables, const double* d_work, int64_t work_doubles,

@@ -344,6 +344,33 @@ __device__ __forceinline__ Radau radau_tableau() {
   return r;
 }
 
+// The Newton start of a block's first step (LZQ_ODE_PRED_BLOCK), from Y_chi and the step's stages
+// alone: per stage one linearised backward-Euler step over c_j h,
+//   Z_j = Y0 + c_j h f_j(Y0) / (1 + 2 c_j h lam_j Y0),   f_j = -lam_j (Y0^2 - E2_j) - S_j,
+// between E and Y0 where the stage relaxes (annihilation), ~Y0 + c_j h f where it does not -- so a
+// stiff step converges in the peeled iterations as it does from the predictor, and the start stays
+// history-free (the block's end a function of its start: lzq_ode_integrate_tp's exact stitching).
+// false (start from Y0) for a non-finite guess or a sign change of a positive Y0.  Every integrator
+// calls it with the same operands.
+__device__ __forceinline__ bool block_guess(const Radau& R, double h, const OdeStage (&sg)[3], double Y0,
+                                            double (&Z)[3]) {
+  bool ok = true;
+  double g[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const double ch = (j == 0 ? R.c[0] : (j == 1 ? R.c[1] : R.c[2])) * h;  // (no dynamic index: scratch)
+    const double f = -sg[j].lam * (Y0 * Y0 - sg[j].E2) - sg[j].S;
+    const double den = 1.0 + 2.0 * (ch * sg[j].lam) * Y0;  // >= 1 for Y0 >= 0
+    g[j] = Y0 + ch * f * rcp_pos(den);
+    ok = ok && den > 0.0 && isfinite(g[j]) && (!(Y0 > 0.0) || g[j] > 0.0);
+  }
+  if (ok) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) Z[j] = g[j];
+  }
+  return ok;
+}
+
 // x = M^-1 b for the 3x3 stage matrices M = I + h A diag(d) (partial pivoting; branch-free
 // selects, so the lanes of a wave stay converged).
 __device__ __forceinline__ void solve3(double M[3][3], double b[3]) {
@@ -586,6 +613,7 @@ __device__ __forceinline__ double fma_neg_s(double k, double a, double p) {
 // applies the rule on the absolute step index, so all modes stay bit-identical.  (A power of two.)
 #define LZQ_ODE_PRED_BLOCK 64
 #endif
+
 __device__ __forceinline__ bool pred_step(int64_t k) { return (k & (LZQ_ODE_PRED_BLOCK - 1)) != 0; }
 #ifndef LZQ_RIC_MIN_WAVES
 #define LZQ_RIC_MIN_WAVES 4  // ode_riccati_kernel: minimum waves per SIMD (its VGPR cap = 512 / this)
@@ -1218,6 +1246,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
             for (int j = 0; j < 3; ++j)
               sg[j] = (kChiOnly && !o.deplete) ? ode_stage_chi(o, xk + R.c[j] * hs) : ode_stage(o, w, xk + R.c[j] * hs);
           }
+          if (riccati && !split && !pred_step(k)) use_guess = block_guess(R, hs, sg, Ychi, Zs);
           if (LZQ_ODE_YBREC && !kChiOnly) {  // Y_B by its step map, then Y_chi alone
             YbCD r;
             if (rec_shared && !split) {
@@ -1472,7 +1501,7 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
 #pragma unroll
         for (int j = 0; j < 3; ++j) Zs[j] = g[j];
       }
-      auto part = [&](double xs, double hs, bool guess) {
+      auto part = [&](double xs, double hs, bool guess, bool block_start) {
         const RadauH hAs = radau_h(R, hs);
         OdeStage sg[3];
 #pragma unroll
@@ -1487,12 +1516,13 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
         }
         const YbRec yr = yb_rec(hAs, sg);
         YB = __builtin_fma(yr.c, YB, Pf * yr.d);
+        if (block_start) guess = block_guess(R, hs, sg, Ychi, Zs);
         return radau_step<false>(hAs, sg, Ychi, YB, Zs, guess);
       };
-      if (xa > xk) ok = part(xk, split ? xa - xk : hu, use_guess);
+      if (xa > xk) ok = part(xk, split ? xa - xk : hu, use_guess, riccati && !split && !pred_step(k));
       if (ok && split && xk + hu > xbu) {
         YB_prev = YB;
-        ok = part(xbu, (xk + hu) - xbu, false);
+        ok = part(xbu, (xk + hu) - xbu, false, false);
       }
       have = !split;
       Yp = Ystart;
@@ -1529,13 +1559,18 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     double kd = (double)kb;
+    // the block's predictor-free step (k = 0 mod LZQ_ODE_PRED_BLOCK) is row rz (a row past the
+    // block when it has none: pass 2 starts after the split steps, unaligned): one wave-uniform
+    // compare per step.  (Peeling row 0 of aligned blocks, with pass 1 run on to the next block,
+    // measured slower: profiles/round5/ablate_ode_pred_block.json.)
+    const int rz = (int)((-kb) & (int64_t)(LZQ_ODE_PRED_BLOCK - 1));
     for (int r = 0; r < (int)(kend - kb) && !done; ++r) {
       const double xk = x0u + kd * hu;
       kd += 1.0;
       const double YB_prev = YB;
       const double Ystart = Ychi;
       bool use_guess = false;
-      if (riccati && have && pred_step(kb + r)) {  // the Radau5 predictor, as ode_integrate_kernel
+      if (riccati && have && r != rz) {  // the Radau5 predictor, as ode_integrate_kernel
         double g[3];
         use_guess = true;
 #pragma unroll
@@ -1562,6 +1597,7 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
         }
         const YbCD rc = s_rcd[wv][r];
         YB = __builtin_fma(rc.c, YB, Pf * rc.d);
+        if (riccati && r == rz) use_guess = block_guess(R, hu, sg, Ychi, Zs);
         ok = radau_step<false>(hA, sg, Ychi, YB, Zs, use_guess);
       }
       have = true;
@@ -1781,7 +1817,7 @@ __device__ __forceinline__ bool tp_steps(const OdePoint& o, const double* __rest
 #pragma unroll
       for (int j = 0; j < 3; ++j) Zs[j] = gs[j];
     }
-    auto part = [&](double xs, double hs, bool guess, bool own_h) {
+    auto part = [&](double xs, double hs, bool guess, bool own_h, bool block_start) {
       const RadauH hAs = own_h ? radau_h(R, hs) : hA;
       OdeStage sg[3];
 #pragma unroll
@@ -1790,6 +1826,7 @@ __device__ __forceinline__ bool tp_steps(const OdePoint& o, const double* __rest
       YB = __builtin_fma(yr.c, YB, o.Pf * yr.d);
       C *= yr.c;
       const double Y0 = Ychi;
+      if (block_start) guess = block_guess(R, hs, sg, Ychi, Zs);
       // (radau_step's convergence test reads NaN corrections as converged -- it never meets one on
       // the sequential trajectory, but a start far from it can diverge: a non-finite result, or a
       // sign change of a source-free positive Y_chi (the stage system's other root), is a failure)
@@ -1806,8 +1843,8 @@ __device__ __forceinline__ bool tp_steps(const OdePoint& o, const double* __rest
       return false;
     };
     bool ok = true;
-    if (xa > xk) ok = part(xk, split ? xa - xk : h, use_guess, split);
-    if (split && xk + h > xb) ok = part(xb, (xk + h) - xb, false, true) && ok;
+    if (xa > xk) ok = part(xk, split ? xa - xk : h, use_guess, split, riccati && !split && !pred_step(k));
+    if (split && xk + h > xb) ok = part(xb, (xk + h) - xb, false, true, false) && ok;
     exact = exact && ok;
     have = !split && ok;  // after a bridge the predictor has no collocation polynomial behind it
     Yp = Ystart;

@@ -29,11 +29,11 @@
 //                               ceil(steps_per_radian * (len_j / v_w) * omega_j)) uniform steps,
 //                               omega_j = the largest of E = sqrt(Delta^2 + m^2) and
 //                               4 sqrt(|dH/dt|) (4 / the LZ time) at 5 points of the interval
-//                               (from per-shape samples, profile_samples_kernel).  A lane keeps
-//                               its interval's Delta and m coefficients, the state and the step
-//                               in registers; the shape's rows are read once per interval, by a
-//                               wave whose points share the shape through the scalar cache
-//                               (round 3 measured staging them in LDS per block 5% slower).
+//                               (from per-shape interval records, profile_samples_kernel).  A
+//                               lane keeps its interval's Delta and m coefficients, the state and
+//                               the step in registers; a wave whose points share the shape stages
+//                               the interval records in LDS, the next one fetched while it steps
+//                               (round 5; round 3's per-block staging of whole shapes was 5% slower).
 //                               Large batches launch in (shape, cost, coupling angle) order
 //                               (profile_key_kernel + a radix sort).
 // tests/profile_ref.py restates all three in numpy; tests/test_gpu_profile.py checks them.
@@ -379,6 +379,37 @@ __device__ __forceinline__ MagnusPoly magnus_poly(const double (&cD)[4], const d
   return mp;
 }
 
+// cos|n| and sin|n|/|n| of a step (cos_sinc_short's values): the usual |n|^2 <= 1/8 inline, the
+// rest out of line, so the longer series' coefficients hold no registers in the step loop
+#ifndef LZQ_PROF_COLD_SC
+#define LZQ_PROF_COLD_SC 1
+#endif
+struct CosSinc {
+  double cs, sc;
+};
+__device__ __noinline__ CosSinc cos_sinc_cold(double x2) {
+  CosSinc r;
+  cos_sinc_short(x2, r.cs, r.sc);
+  return r;
+}
+__device__ __forceinline__ void cos_sinc_step(double x2, double& cs, double& sc) {
+  if (!LZQ_PROF_COLD_SC || !LZQ_SU2_SHORT8) {
+    cos_sinc_short(x2, cs, sc);
+  } else if (x2 <= 0.125) {
+    double ps = kSincC[6], pc = kCosC[6];
+#pragma unroll
+    for (int k = 5; k >= 0; --k) ps = fma3s(ps, x2, kSincC[k]);
+#pragma unroll
+    for (int k = 5; k >= 0; --k) pc = fma3s(pc, x2, kCosC[k]);
+    sc = ps;
+    cs = pc;
+  } else {
+    const CosSinc r = cos_sinc_cold(x2);
+    cs = r.cs;
+    sc = r.sc;
+  }
+}
+
 // u: the step's midpoint in units of the step, st + 1/2 (exact)
 __device__ __forceinline__ void magnus6_step(const MagnusPoly& mp, double u, Cplx& p0, Cplx& p1) {
 #define FMA __builtin_fma
@@ -401,7 +432,7 @@ __device__ __forceinline__ void magnus6_step(const MagnusPoly& mp, double u, Cpl
   const double ny = FMA(Lz, Rx, -(Lx * Rz)) * (1.0 / 120.0);
   const double nz = FMA(FMA(Lx, C2h, -(ch * Rx)), 1.0 / 60.0, FMA(z3, 1.0 / 12.0, z1));
   double cs, sc;
-  cos_sinc_short(FMA(nx, nx, FMA(ny, ny, nz * nz)), cs, sc);
+  cos_sinc_step(FMA(nx, nx, FMA(ny, ny, nz * nz)), cs, sc);
   su2_apply(cs, sc * nx, sc * ny, sc * nz, p0, p1);
 #undef FMA
 }
@@ -413,18 +444,34 @@ __device__ __forceinline__ void magnus6_step(const MagnusPoly& mp, double u, Cpl
 // Stored as the products the rule's quadratic forms need (round 4): per sample
 // [phi^2, phi Phi, Phi^2, phi'^2, phi' Phi', Phi'^2], so a point's E^2 = D^2 + m^2 =
 // (y_B^2 + lambda^2) phi^2 - 2 y_B y_chi phi Phi + y_chi^2 Phi^2 is three operations per sample.
-constexpr int kSampD = 6;                 // doubles per sample
-constexpr int kProfSamp = 5 * kSampD;     // doubles per interval, q = 0..4
+// With them (round 5) the interval's length and its spline row, so that everything an interval
+// entry reads is one 320-B RECORD per (shape, interval):
+//   [q0 .. q4 samples (30)] [L = x_{j+1} - x_j] [0] [phi c0..c3, Phi c0..c3]
+// and one record past the last (pad: the propagation's record fetch of the last interval reads
+// the next record's q = 0 slot, unused there).
+constexpr int kSampD = 6;                    // doubles per sample
+constexpr int kRecL = 5 * kSampD;            // the interval length
+constexpr int kRecCoef = kRecL + 2;          // the spline row (kProfCoef doubles)
+constexpr int kProfRec = kRecCoef + kProfCoef;  // doubles per interval record (40)
 
 __global__ __launch_bounds__(kProfBlock) void profile_samples_kernel(const double* __restrict__ knots,
                                                                      const double* __restrict__ coef, int64_t n_rows,
                                                                      int32_t K, double* __restrict__ samp) {
   const int64_t r = (int64_t)blockIdx.x * kProfBlock + threadIdx.x;  // row = shape * (K - 1) + interval
-  if (r >= n_rows) return;
+  if (r > n_rows) return;
+  double* o = samp + r * kProfRec;
+  if (r == n_rows) {  // the pad record
+#pragma unroll
+    for (int k = 0; k < kProfRec; ++k) o[k] = 0.0;
+    return;
+  }
   const int64_t s = r / (K - 1), j = r - s * (K - 1);
   const double L = knots[s * K + j + 1] - knots[s * K + j];
   const double* c = coef + r * kProfCoef;
-  double* o = samp + r * kProfSamp;
+  o[kRecL] = L;
+  o[kRecL + 1] = 0.0;
+#pragma unroll
+  for (int k = 0; k < kProfCoef; ++k) o[kRecCoef + k] = c[k];
 #pragma unroll
   for (int q = 0; q < 5; ++q) {
     const double t = (0.25 * q) * L;
@@ -469,14 +516,14 @@ __device__ __forceinline__ Rates rates_max(Rates u, Rates v) { return {fmax(u.e2
 
 // the end sample of interval j (of K - 1): the next interval's q = 0, or the last interval's own q = 4
 __device__ __forceinline__ const double* end_sample(const double* __restrict__ sm, int j, int K) {
-  return j + 2 < K ? sm + (j + 1) * kProfSamp : sm + j * kProfSamp + 4 * kSampD;
+  return j + 2 < K ? sm + (j + 1) * kProfRec : sm + j * kProfRec + 4 * kSampD;
 }
 
 // interval j's rates from its start sample's (`start`, carried) and its q = 1..3 and end samples;
 // `end` returns the end sample's rates (the next interval's start)
 __device__ __forceinline__ Rates interval_rates(const double* __restrict__ sm, int j, int K, const RuleForm& f,
                                                 Rates start, Rates& end) {
-  const double* sr = sm + j * kProfSamp;
+  const double* sr = sm + j * kProfRec;
   Rates r = start;
 #pragma unroll
   for (int q = 1; q < 4; ++q) r = rates_max(r, sample_rates(sr + kSampD * q, f));
@@ -484,9 +531,31 @@ __device__ __forceinline__ Rates interval_rates(const double* __restrict__ sm, i
   return rates_max(r, end);
 }
 
+// The rule's square roots: the device library's sqrt is v_rsq_f64 + two Goldschmidt / Newton
+// refinements, wrapped in range fix-ups (a 2^256 pre-scale below 2^-767, 0 / +inf passed through).
+// When every lane's argument lies in [2^-767, DBL_MAX] the fix-ups are identities, so the bare
+// sequence gives the library's bits; otherwise the wave takes the library sqrt.
+#ifndef LZQ_PROF_RULE_SQRT
+#define LZQ_PROF_RULE_SQRT 1
+#endif
+__device__ __forceinline__ double rule_sqrt(double x) {
+  if (LZQ_PROF_RULE_SQRT && __all(x >= 0x1p-767 && x <= 0x1.fffffffffffffp+1023)) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    return __builtin_fma(d, h, g);
+  }
+  return sqrt(x);
+}
+
 __device__ __forceinline__ double steps_of(Rates r, double L, const ProfPt& p, double ivw, double spr, int32_t n_min) {
-  const double W2 = fmax(r.e2, (kHdotRate * kHdotRate) * (p.vw * sqrt(r.h2)));
-  return fmax((double)n_min, ceil((spr * (L * ivw)) * sqrt(W2)));
+  const double W2 = fmax(r.e2, (kHdotRate * kHdotRate) * (p.vw * rule_sqrt(r.h2)));
+  return fmax((double)n_min, ceil((spr * (L * ivw)) * rule_sqrt(W2)));
 }
 
 // interval j on its own (no carried start): the same samples and operations, the same count
@@ -494,7 +563,7 @@ __device__ __forceinline__ double interval_steps(const double* __restrict__ sm, 
                                                  double L, double ivw, double spr, int32_t n_min) {
   const RuleForm f = rule_form(p);
   Rates end;
-  const Rates r = interval_rates(sm, j, K, f, sample_rates(sm + j * kProfSamp, f), end);
+  const Rates r = interval_rates(sm, j, K, f, sample_rates(sm + j * kProfRec, f), end);
   return steps_of(r, L, p, ivw, spr, n_min);
 }
 
@@ -530,8 +599,8 @@ __global__ __launch_bounds__(kProfBlock) void profile_key_kernel(const double* _
       return c * kProfCostStride;
     };
     const int64_t s0 = __builtin_amdgcn_readfirstlane(p.shape), sl = p.shape;  // scalar loads when uniform
-    st = (LZQ_PROF_UNIFORM && __all(p.shape == s0)) ? cost(knots + s0 * K, samp + s0 * (K - 1) * kProfSamp)
-                                                    : cost(knots + sl * K, samp + sl * (K - 1) * kProfSamp);
+    st = (LZQ_PROF_UNIFORM && __all(p.shape == s0)) ? cost(knots + s0 * K, samp + s0 * (K - 1) * kProfRec)
+                                                    : cost(knots + sl * K, samp + sl * (K - 1) * kProfRec);
   }
   const double cb = st == st ? fmin(fmax(4.0 * log2(1.0 + st), 0.0), (double)(kCostBins - 1)) : 0.0;
   const uint32_t cost = (uint32_t)((kCostBins - 1) - (int32_t)cb);  // 0 = costliest
@@ -543,50 +612,108 @@ __global__ __launch_bounds__(kProfBlock) void profile_key_kernel(const double* _
   idx[i] = (int32_t)i;
 }
 
-// One point through the whole profile (x, cf, sm: its shape's knots, coefficient rows, samples).
-// Returns P, NaN for a non-finite or absurd step count.
-__device__ __forceinline__ double propagate_point(const double* __restrict__ x, const double* __restrict__ cf,
-                                                  const double* __restrict__ sm, int32_t K, const ProfPt& p,
-                                                  double spr, int32_t n_min) {
+// An interval's entry reads the SPAN of the records from its own q = 1 sample up to the next
+// record's q = 0 (its end sample): 40 doubles, 320 B, contiguous.  Offsets in the span:
+constexpr int kSpanOff = kSampD;                   // the span starts at the record's q = 1
+constexpr int kSpan = kProfRec;                    // doubles
+constexpr int kSpQ4 = 3 * kSampD;                  // the record's own q = 4 (the last interval's end)
+constexpr int kSpL = kRecL - kSpanOff;             // L
+constexpr int kSpCoef = kRecCoef - kSpanOff;       // the spline row
+constexpr int kSpNext = kProfRec - kSpanOff;       // the next record's q = 0
+
+// Interval entry from its span s: the step rule's count (rates carried in `start`), Delta / m
+// coefficients and Magnus polynomials -- the operations of the round-4 loop in the same order, so
+// S and every bit of the polynomials are unchanged.  All of the span is read before any branch, so
+// its loads issue together.  False for a non-finite or absurd count.
+__device__ __forceinline__ bool enter_interval(const double* __restrict__ s, bool last, const ProfPt& p,
+                                               const RuleForm& rf, double ivw, double spr, int32_t n_min, Rates& start,
+                                               double (&cD)[4], double (&cM)[4], MagnusPoly& mp, int& S) {
+  interval_coefs_fma(s + kSpCoef, p, cD, cM);
+  Rates r = start;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) r = rates_max(r, sample_rates(s + kSampD * q, rf));
+  const Rates end = sample_rates(s + (last ? kSpQ4 : kSpNext), rf);
+  r = rates_max(r, end);
+  start = end;
+  const double L = s[kSpL];
+  const double Sd = steps_of(r, L, p, ivw, spr, n_min);
+  mp = magnus_poly(cD, cM, L, Sd, ivw);
+  const bool good = Sd <= kMaxIntervalSteps;
+  S = good ? (int)Sd : 0;
+  return good;
+}
+
+// The wave's LDS stage: two spans (interval j, j + 1) per wave
+struct alignas(16) ProfStage {
+  double span[2][kSpan];
+};
+
+// One point through the whole profile (rec: its shape's interval records).  Returns P, NaN for a
+// non-finite or absurd step count (that lane takes no further steps).
+//   kStaged: the wave's points share the shape and all 64 lanes are here -- the record spans go
+//   through the wave's LDS stage, interval j + 1's fetched (global_load_lds, 20 lanes x 16 B) while
+//   the wave steps interval j, so an entry waits on LDS, not on a trip to L2 (round 4: five
+//   dependent scalar loads per entry, 24% of the waves' cycles in SQ_WAIT_ANY).
+//   Otherwise each lane reads its own spans from global memory.
+template <bool kStaged>
+__device__ __forceinline__ double propagate_point(const double* __restrict__ rec, int32_t K, const ProfPt& p,
+                                                  double spr, int32_t n_min, ProfStage* stage) {
+  const int lane = (int)(threadIdx.x & 63);
+  auto fetch = [&](int j) {  // interval j's span into stage->span[j & 1]
+    if (lane < kSpan / 2)
+      __builtin_amdgcn_global_load_lds(rec + (int64_t)j * kProfRec + kSpanOff + 2 * lane, &stage->span[j & 1][0], 16,
+                                       0, 0);
+  };
+  if (kStaged) fetch(0);
   const double ivw = 1.0 / p.vw;
   double cD[4], cM[4];
-  interval_coefs_fma(cf, p, cD, cM);
+  interval_coefs_fma(rec + kRecCoef, p, cD, cM);
   Cplx p0, p1;
   edge_state(cD, cM, 0.0, p.vw, p0, p1);
   const RuleForm rf = rule_form(p);
-  Rates start = sample_rates(sm, rf);  // interval 0's q = 0; then each interval's end is the next one's start
+  Rates start = sample_rates(rec, rf);  // interval 0's q = 0; then each interval's end is the next one's start
+  bool ok = true;
   for (int j = 0; j + 1 < K; ++j) {
-    interval_coefs_fma(cf + j * kProfCoef, p, cD, cM);
-    const double L = x[j + 1] - x[j];
-    Rates end;
-    const double Sd = steps_of(interval_rates(sm, j, K, rf, start, end), L, p, ivw, spr, n_min);
-    start = end;
-    if (!(Sd <= kMaxIntervalSteps)) return __builtin_nan("");  // non-finite or absurd input
-    const int S = (int)Sd;
-    const MagnusPoly mp = magnus_poly(cD, cM, L, Sd, ivw);
+    const double* s;
+    if (kStaged) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this interval's span has landed in LDS
+      s = &stage->span[j & 1][0];
+    } else {
+      s = rec + (int64_t)j * kProfRec + kSpanOff;
+    }
+    MagnusPoly mp;
+    int S;
+    ok = enter_interval(s, j + 2 == K, p, rf, ivw, spr, n_min, start, cD, cM, mp, S) && ok;
+    if (kStaged && j + 2 < K) fetch(j + 1);
+    if (!ok) S = 0;
     double smid = 0.5;
 #pragma unroll LZQ_PROF_UNROLL
     for (int st = 0; st < S; ++st, smid += 1.0) magnus6_step(mp, smid, p0, p1);
   }
-  // the last interval's rows again for the end state (not kept live across the step loop)
-  interval_coefs_fma(cf + (K - 2) * kProfCoef, p, cD, cM);
+  if (!ok) return __builtin_nan("");
+  // the last interval's row again for the end state (not kept live across the step loop)
+  const double* s = kStaged ? &stage->span[(K - 2) & 1][0] : rec + (int64_t)(K - 2) * kProfRec + kSpanOff;
+  interval_coefs_fma(s + kSpCoef, p, cD, cM);
   Cplx u0, u1;
-  edge_state(cD, cM, x[K - 1] - x[K - 2], p.vw, u0, u1);
+  edge_state(cD, cM, s[kSpL], p.vw, u0, u1);
   const Cplx a = inner(u0, u1, p0, p1);
   const double norm = p0.re * p0.re + p0.im * p0.im + p1.re * p1.re + p1.im * p1.im;
   return 1.0 - (a.re * a.re + a.im * a.im) / norm;
 }
 
+#ifndef LZQ_PROF_STAGE
+#define LZQ_PROF_STAGE 1  // 0: every wave reads its spans from global memory
+#endif
+
 // The interval loop walks every lane of a wave through the same knot interval j, so when the wave's
-// points share one shape (the keyed launch order makes that the rule) the interval's rows are the
-// same addresses for all lanes: the shape index is taken from the first lane (readfirstlane) and
-// the rows are read through the scalar cache into SGPRs (s_load; v_fma_f64 takes one SGPR operand
-// for free), not as 64 identical vector loads.  Mixed-shape waves take the per-lane path; both
-// run propagate_point on the same values, so P does not depend on the path.
+// points share one shape (the keyed launch order makes that the rule) the interval's records are
+// the same addresses for all lanes: those waves stage them in LDS (propagate_point<true>).
+// Mixed-shape and partial waves take the per-lane path; both run the same operations on the same
+// values, so P does not depend on the path.
 __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_propagate_kernel(
-    const double* __restrict__ knots, const double* __restrict__ coef, int32_t n_shapes, int32_t K,
-    const lzq_profile_point* __restrict__ pts, int64_t n, double spr, int32_t n_min, const int32_t* __restrict__ order,
-    const double* __restrict__ samp, double* __restrict__ P_out) {
+    int32_t n_shapes, int32_t K, const lzq_profile_point* __restrict__ pts, int64_t n, double spr, int32_t n_min,
+    const int32_t* __restrict__ order, const double* __restrict__ rec, double* __restrict__ P_out) {
+  __shared__ ProfStage stage[kProfBlock / 64];
   const int64_t tid = (int64_t)blockIdx.x * kProfBlock + threadIdx.x;
   if (tid >= n) return;
   const int64_t i = order ? (int64_t)order[tid] : tid;
@@ -597,14 +724,10 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_propag
   }
   const int32_t sh0 = __builtin_amdgcn_readfirstlane(p.shape);
   double P;
-  if (LZQ_PROF_UNIFORM && __all(p.shape == sh0)) {
-    const int64_t su = sh0;
-    P = propagate_point(knots + su * K, coef + su * (K - 1) * kProfCoef, samp + su * (K - 1) * kProfSamp, K, p, spr,
-                        n_min);
+  if (LZQ_PROF_STAGE && __builtin_amdgcn_read_exec() == ~0ull && __all(p.shape == sh0)) {
+    P = propagate_point<true>(rec + (int64_t)sh0 * (K - 1) * kProfRec, K, p, spr, n_min, &stage[threadIdx.x >> 6]);
   } else {
-    const int64_t sl = p.shape;
-    P = propagate_point(knots + sl * K, coef + sl * (K - 1) * kProfCoef, samp + sl * (K - 1) * kProfSamp, K, p, spr,
-                        n_min);
+    P = propagate_point<false>(rec + (int64_t)p.shape * (K - 1) * kProfRec, K, p, spr, n_min, nullptr);
   }
   P_out[i] = P;
 }
@@ -643,7 +766,7 @@ __global__ __launch_bounds__(kProfBlock) void profile_steps_kernel(const double*
     double tot = 0.0;
     if (p.vw > 0.0 && p.shape >= 0 && p.shape < n_shapes) {
       const double* x = knots + (int64_t)p.shape * K;
-      const double* sm = samp + (int64_t)p.shape * (K - 1) * kProfSamp;
+      const double* sm = samp + (int64_t)p.shape * (K - 1) * kProfRec;
       uint16_t* row = steps + i * (int64_t)(K - 1);
       const double ivw = 1.0 / p.vw;
       const RuleForm rf = rule_form(p);
@@ -683,7 +806,7 @@ __global__ __launch_bounds__(kProfBlock, LZQ_PROF_MIN_WAVES) void profile_flat_k
   }
   const double* x = knots + (int64_t)p.shape * K;
   const double* cf = coef + (int64_t)p.shape * (K - 1) * kProfCoef;
-  const double* sm = samp + (int64_t)p.shape * (K - 1) * kProfSamp;
+  const double* sm = samp + (int64_t)p.shape * (K - 1) * kProfRec;
   const uint16_t* srow = steps + i * (int64_t)(K - 1);
   const double ivw = 1.0 / p.vw;
   double cD[4], cM[4];
@@ -827,9 +950,9 @@ extern "C" int lzq_lz_propagate_profile(const double* d_knots, const double* d_c
   // the shapes' step-rule samples: stream-ordered scratch
   const int64_t rows = (int64_t)n_shapes * (n_knots - 1);
   double* samp = nullptr;
-  hipError_t e = hipMallocAsync((void**)&samp, sizeof(double) * lzq::kProfSamp * (size_t)rows, st);
+  hipError_t e = hipMallocAsync((void**)&samp, sizeof(double) * lzq::kProfRec * (size_t)(rows + 1), st);
   if (e != hipSuccess) return lzq_set_error(LZQ_EHIP, hipGetErrorString(e));
-  hipLaunchKernelGGL(lzq::profile_samples_kernel, dim3((unsigned)((rows + lzq::kProfBlock - 1) / lzq::kProfBlock)),
+  hipLaunchKernelGGL(lzq::profile_samples_kernel, dim3((unsigned)((rows + 1 + lzq::kProfBlock - 1) / lzq::kProfBlock)),
                      dim3(lzq::kProfBlock), 0, st, d_knots, d_coef, rows, n_knots, samp);
   if (lzq::g_profile_flat) {
     const int rc2 = profile_flat_launch(d_knots, d_coef, n_shapes, n_knots, d_points, n, steps_per_radian, min_steps,
@@ -869,8 +992,8 @@ extern "C" int lzq_lz_propagate_profile(const double* d_knots, const double* d_c
     }
   }
   if (e == hipSuccess && rc == LZQ_OK) {
-    hipLaunchKernelGGL(lzq::profile_propagate_kernel, dim3((unsigned)nb), dim3(lzq::kProfBlock), 0, st, d_knots, d_coef,
-                       n_shapes, n_knots, d_points, n, steps_per_radian, min_steps, order, (const double*)samp, d_P);
+    hipLaunchKernelGGL(lzq::profile_propagate_kernel, dim3((unsigned)nb), dim3(lzq::kProfBlock), 0, st, n_shapes,
+                       n_knots, d_points, n, steps_per_radian, min_steps, order, (const double*)samp, d_P);
     e = hipGetLastError();
   }
   if (ws) {

@@ -512,7 +512,20 @@ __device__ __forceinline__ Rates sample_rates(const double* __restrict__ sr, con
           __builtin_fma(f.A, sr[3], __builtin_fma(f.B, sr[4], f.C * sr[5]))};
 }
 
-__device__ __forceinline__ Rates rates_max(Rates u, Rates v) { return {fmax(u.e2, v.e2), fmax(u.h2, v.h2)}; }
+// fmax for the rule: v_max_f64 as such.  fmax's lowering first quiets signalling NaNs of operands
+// it cannot prove canonical (a v_max_f64 x, x for each carried or loaded value, three per interval
+// entry); the rule's operands are never signalling NaNs, and for every other input v_max_f64 is
+// fmax (a quiet NaN operand yields the other).
+#ifndef LZQ_PROF_ASM_MAX
+#define LZQ_PROF_ASM_MAX 1
+#endif
+__device__ __forceinline__ double rmax(double a, double b) {
+  if (!LZQ_PROF_ASM_MAX) return fmax(a, b);
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ Rates rates_max(Rates u, Rates v) { return {rmax(u.e2, v.e2), rmax(u.h2, v.h2)}; }
 
 // the end sample of interval j (of K - 1): the next interval's q = 0, or the last interval's own q = 4
 __device__ __forceinline__ const double* end_sample(const double* __restrict__ sm, int j, int K) {
@@ -538,8 +551,20 @@ __device__ __forceinline__ Rates interval_rates(const double* __restrict__ sm, i
 #ifndef LZQ_PROF_RULE_SQRT
 #define LZQ_PROF_RULE_SQRT 1
 #endif
+// every active lane's x in [2^-767, DBL_MAX] (NaN: no): the two compares' lane masks straight into
+// SGPRs (a ballot of the C++ condition re-materialises it as a VGPR and compares that again)
+#ifndef LZQ_PROF_VOTE_ASM
+#define LZQ_PROF_VOTE_ASM 1
+#endif
+__device__ __forceinline__ bool wave_in_sqrt_range(double x) {
+  if (!LZQ_PROF_VOTE_ASM) return __all(x >= 0x1p-767 && x <= 0x1.fffffffffffffp+1023);
+  uint64_t lo, hi;
+  asm("v_cmp_le_f64_e64 %0, %1, %2" : "=s"(lo) : "s"(0x1p-767), "v"(x));
+  asm("v_cmp_ge_f64_e64 %0, %1, %2" : "=s"(hi) : "s"(0x1.fffffffffffffp+1023), "v"(x));
+  return (lo & hi) == __builtin_amdgcn_read_exec();
+}
 __device__ __forceinline__ double rule_sqrt(double x) {
-  if (LZQ_PROF_RULE_SQRT && __all(x >= 0x1p-767 && x <= 0x1.fffffffffffffp+1023)) {
+  if (LZQ_PROF_RULE_SQRT && wave_in_sqrt_range(x)) {
     const double y = __builtin_amdgcn_rsq(x);
     double g = x * y, h = y * 0.5;
     const double r = __builtin_fma(-h, g, 0.5);
@@ -554,8 +579,8 @@ __device__ __forceinline__ double rule_sqrt(double x) {
 }
 
 __device__ __forceinline__ double steps_of(Rates r, double L, const ProfPt& p, double ivw, double spr, int32_t n_min) {
-  const double W2 = fmax(r.e2, (kHdotRate * kHdotRate) * (p.vw * rule_sqrt(r.h2)));
-  return fmax((double)n_min, ceil((spr * (L * ivw)) * rule_sqrt(W2)));
+  const double W2 = rmax(r.e2, (kHdotRate * kHdotRate) * (p.vw * rule_sqrt(r.h2)));
+  return rmax((double)n_min, ceil((spr * (L * ivw)) * rule_sqrt(W2)));
 }
 
 // interval j on its own (no carried start): the same samples and operations, the same count
@@ -624,10 +649,12 @@ constexpr int kSpNext = kProfRec - kSpanOff;       // the next record's q = 0
 // Interval entry from its span s: the step rule's count (rates carried in `start`), Delta / m
 // coefficients and Magnus polynomials -- the operations of the round-4 loop in the same order, so
 // S and every bit of the polynomials are unchanged.  All of the span is read before any branch, so
-// its loads issue together.  False for a non-finite or absurd count.
+// its loads issue together.  False for a non-finite or absurd count.  S: the count as a double (an
+// integer; 0 for a bad one) -- the step loop runs on the midpoint u = 1/2, 3/2, .. < S, exact in a
+// double, without an integer counter.
 __device__ __forceinline__ bool enter_interval(const double* __restrict__ s, bool last, const ProfPt& p,
                                                const RuleForm& rf, double ivw, double spr, int32_t n_min, Rates& start,
-                                               double (&cD)[4], double (&cM)[4], MagnusPoly& mp, int& S) {
+                                               double (&cD)[4], double (&cM)[4], MagnusPoly& mp, double& S) {
   interval_coefs_fma(s + kSpCoef, p, cD, cM);
   Rates r = start;
 #pragma unroll
@@ -639,7 +666,7 @@ __device__ __forceinline__ bool enter_interval(const double* __restrict__ s, boo
   const double Sd = steps_of(r, L, p, ivw, spr, n_min);
   mp = magnus_poly(cD, cM, L, Sd, ivw);
   const bool good = Sd <= kMaxIntervalSteps;
-  S = good ? (int)Sd : 0;
+  S = good ? Sd : 0.0;
   return good;
 }
 
@@ -682,13 +709,12 @@ __device__ __forceinline__ double propagate_point(const double* __restrict__ rec
       s = rec + (int64_t)j * kProfRec + kSpanOff;
     }
     MagnusPoly mp;
-    int S;
+    double S;
     ok = enter_interval(s, j + 2 == K, p, rf, ivw, spr, n_min, start, cD, cM, mp, S) && ok;
     if (kStaged && j + 2 < K) fetch(j + 1);
-    if (!ok) S = 0;
-    double smid = 0.5;
+    if (!ok) S = 0.0;
 #pragma unroll LZQ_PROF_UNROLL
-    for (int st = 0; st < S; ++st, smid += 1.0) magnus6_step(mp, smid, p0, p1);
+    for (double u = 0.5; u < S; u += 1.0) magnus6_step(mp, u, p0, p1);
   }
   if (!ok) return __builtin_nan("");
   // the last interval's row again for the end state (not kept live across the step loop)

@@ -287,11 +287,8 @@ __global__ __launch_bounds__(kPropBlock, LZQ_FOLLOW_MIN_WAVES) void lz_follow_ke
   out[8] = cl;
   out[9] = cr;
   out[10] = Sd <= kMaxCellSteps ? Sd : __builtin_nan("");  // non-finite or absurd input: P = NaN
-  SU2 ML, MR;
   const bool has_left = left < cl, has_right = cr < right;
-  sa_cell_follow(mh, sg, sa * (left - xcc) * inv_vw, sa * (right - xcc) * inv_vw, tau_c, has_left, has_right, ML, MR);
-  if (has_left) out[0] = ML.a.re, out[1] = ML.a.im, out[2] = ML.b.re, out[3] = ML.b.im;
-  if (has_right) out[4] = MR.a.re, out[5] = MR.a.im, out[6] = MR.b.re, out[7] = MR.b.im;
+  sa_cell_follow(mh, sg, sa * (left - xcc) * inv_vw, sa * (right - xcc) * inv_vw, tau_c, has_left, has_right, out);
 }
 
 __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_kernel(const double* __restrict__ m_mix,

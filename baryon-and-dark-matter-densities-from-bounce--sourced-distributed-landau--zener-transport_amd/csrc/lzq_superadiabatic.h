@@ -24,6 +24,16 @@
 
 namespace lzq {
 
+// The frame and phase algebra below is checked against the numpy restatement at tolerances, not bit
+// for bit, so its products and sums may contract to fma (the library builds with -ffp-contract=off
+// for the oracle-matched quadrature); reset to off at the end of this header.
+#ifndef LZQ_SA_CONTRACT
+#define LZQ_SA_CONTRACT 1
+#endif
+#if LZQ_SA_CONTRACT
+#pragma clang fp contract(fast)
+#endif
+
 constexpr int kSALevels = 10;      // frame order outside a Magnus core (rotations V_0 .. V_9)
 constexpr double kSATol = 1e-11;   // core edge: first neglected angle |theta_10| <= this
 constexpr double kSAC = 3.2e5;     // |theta_10| <= kSAC mh / E^21 (fitted; conservative for mh > 1)
@@ -361,8 +371,9 @@ __host__ __device__ __forceinline__ SU2 sa_reflect(const SU2& u) {
 }
 
 // Transfer matrices of superadiabatic following (tests/lz_ref.py sa_follow) on both sides of a
-// cell's core [-tau_c, tau_c]: ML from tl (< -tau_c) to -tau_c when has_left, MR from tau_c to
-// tr (> tau_c) when has_right, each U(tb) diag(e^{-i ph}, e^{i ph}) U(ta)^+ with U the frame
+// cell's core [-tau_c, tau_c]: ML from tl (< -tau_c) to -tau_c when has_left (stored at out[0..3]
+// as (a.re, a.im, b.re, b.im) as soon as it is built, so it holds no registers while MR is), MR from
+// tau_c to tr (> tau_c) when has_right (out[4..7]), each U(tb) diag(e^{-i ph}, e^{i ph}) U(ta)^+ with U the frame
 // rotation of order kSALevels (kSAFarLevels at an outer end where that is enough) and
 // ph = int e dtau (sa_phase).  Error ~ |theta_10| at the inner end.  They do not depend on the
 // state, so lz_follow_kernel computes them ahead of the propagation.  The core-edge frame is
@@ -381,8 +392,11 @@ __host__ __device__ __forceinline__ SU2 sa_frame(double tau, double sg, double m
     sa_levels_linear<kSALevels, true, false>(sg * tau, sg, mh, u, nullptr, nullptr);
   return u;
 }
+__host__ __device__ __forceinline__ void sa_store(const SU2& m, double* out) {
+  out[0] = m.a.re, out[1] = m.a.im, out[2] = m.b.re, out[3] = m.b.im;
+}
 __host__ __device__ __forceinline__ void sa_cell_follow(double mh, double sg, double tl, double tr, double tau_c,
-                                                        bool has_left, bool has_right, SU2& ML, SU2& MR) {
+                                                        bool has_left, bool has_right, double* out) {
 #if LZQ_FOLLOW_PAIR
   if (!(has_left || has_right)) return;
   const SU2 uc = sa_frame(tau_c, sg, mh, false);
@@ -391,8 +405,8 @@ __host__ __device__ __forceinline__ void sa_cell_follow(double mh, double sg, do
   const double ta = has_left ? tl : tr, tb = has_right ? tr : tl;
   const SU2 ua = sa_frame(ta, sg, mh, true), ub = sa_frame(tb, sg, mh, true);
   const double pa = sa_phase(ta, -tau_c, mh), pb = sa_phase(tau_c, tb, mh);
-  if (has_left) ML = su2_mul(sa_reflect(uc), su2_phase_adj(pa, ua));
-  if (has_right) MR = su2_mul(ub, su2_phase_adj(pb, uc));
+  if (has_left) sa_store(su2_mul(sa_reflect(uc), su2_phase_adj(pa, ua)), out);
+  if (has_right) sa_store(su2_mul(ub, su2_phase_adj(pb, uc)), out + 4);
 #else
   SU2 uc;
 #pragma nounroll
@@ -409,11 +423,15 @@ __host__ __device__ __forceinline__ void sa_cell_follow(double mh, double sg, do
     if (job == 0)
       uc = u;
     else if (job == 1)
-      ML = su2_mul(sa_reflect(uc), su2_phase_adj(sa_phase(tl, -tau_c, mh), u));  // U(-tau_c) P U(tl)^+
+      sa_store(su2_mul(sa_reflect(uc), su2_phase_adj(sa_phase(tl, -tau_c, mh), u)), out);  // U(-tau_c) P U(tl)^+
     else
-      MR = su2_mul(u, su2_phase_adj(sa_phase(tau_c, tr, mh), uc));               // U(tr) P U(tau_c)^+
+      sa_store(su2_mul(u, su2_phase_adj(sa_phase(tau_c, tr, mh), uc)), out + 4);           // U(tr) P U(tau_c)^+
   }
 #endif
 }
+
+#if LZQ_SA_CONTRACT
+#pragma clang fp contract(off)
+#endif
 
 }  // namespace lzq

@@ -27,10 +27,8 @@ double sa_core_tau_host(double mh) { return sa_core_tau(mh); }
 // both stretches of a cell: out = ML (4), MR (4)
 void sa_cell_follow_host(double mh, double sg, double tl, double tr, double tau_c, int has_left, int has_right,
                          double* out) {
-  SU2 ML = {{1.0, 0.0}, {0.0, 0.0}}, MR = ML;
-  sa_cell_follow(mh, sg, tl, tr, tau_c, has_left != 0, has_right != 0, ML, MR);
-  out[0] = ML.a.re, out[1] = ML.a.im, out[2] = ML.b.re, out[3] = ML.b.im;
-  out[4] = MR.a.re, out[5] = MR.a.im, out[6] = MR.b.re, out[7] = MR.b.im;
+  for (int k = 0; k < 8; ++k) out[k] = (k % 4 == 0) ? 1.0 : 0.0;  // identity where a side is absent
+  sa_cell_follow(mh, sg, tl, tr, tau_c, has_left != 0, has_right != 0, out);
 }
 
 int sa_levels_count(void) { return kSALevels; }

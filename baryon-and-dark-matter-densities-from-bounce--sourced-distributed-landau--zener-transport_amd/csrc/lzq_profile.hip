@@ -686,12 +686,11 @@ template <bool kStaged>
 __device__ __forceinline__ double propagate_point(const double* __restrict__ rec, int32_t K, const ProfPt& p,
                                                   double spr, int32_t n_min, ProfStage* stage) {
   const int lane = (int)(threadIdx.x & 63);
-  auto fetch = [&](int j) {  // interval j's span into stage->span[j & 1]
+  auto fetch = [&](int j, double* dst) {  // interval j's span into the stage buffer dst
     if (lane < kSpan / 2)
-      __builtin_amdgcn_global_load_lds(rec + (int64_t)j * kProfRec + kSpanOff + 2 * lane, &stage->span[j & 1][0], 16,
-                                       0, 0);
+      __builtin_amdgcn_global_load_lds(rec + (int64_t)j * kProfRec + kSpanOff + 2 * lane, dst, 16, 0, 0);
   };
-  if (kStaged) fetch(0);
+  if (kStaged) fetch(0, &stage->span[0][0]);
   const double ivw = 1.0 / p.vw;
   double cD[4], cM[4];
   interval_coefs_fma(rec + kRecCoef, p, cD, cM);
@@ -700,21 +699,30 @@ __device__ __forceinline__ double propagate_point(const double* __restrict__ rec
   const RuleForm rf = rule_form(p);
   Rates start = sample_rates(rec, rf);  // interval 0's q = 0; then each interval's end is the next one's start
   bool ok = true;
-  for (int j = 0; j + 1 < K; ++j) {
-    const double* s;
-    if (kStaged) {
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this interval's span has landed in LDS
-      s = &stage->span[j & 1][0];
-    } else {
-      s = rec + (int64_t)j * kProfRec + kSpanOff;
-    }
+  // interval j from its span s; staged: then interval j + 1's span into `next`
+  auto interval = [&](int j, const double* s, double* next) {
     MagnusPoly mp;
     double S;
     ok = enter_interval(s, j + 2 == K, p, rf, ivw, spr, n_min, start, cD, cM, mp, S) && ok;
-    if (kStaged && j + 2 < K) fetch(j + 1);
+    if (kStaged && j + 2 < K) fetch(j + 1, next);
     if (!ok) S = 0.0;
 #pragma unroll LZQ_PROF_UNROLL
     for (double u = 0.5; u < S; u += 1.0) magnus6_step(mp, u, p0, p1);
+  };
+  if constexpr (kStaged) {
+    // two intervals per iteration, so each one's LDS buffer is a constant offset
+    double* b0 = &stage->span[0][0];
+    double* b1 = &stage->span[1][0];
+    for (int j = 0; j + 1 < K; j += 2) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this interval's span has landed in LDS
+      interval(j, b0, b1);
+      if (j + 2 < K) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        interval(j + 1, b1, b0);
+      }
+    }
+  } else {
+    for (int j = 0; j + 1 < K; ++j) interval(j, rec + (int64_t)j * kProfRec + kSpanOff, nullptr);
   }
   if (!ok) return __builtin_nan("");
   // the last interval's row again for the end state (not kept live across the step loop)

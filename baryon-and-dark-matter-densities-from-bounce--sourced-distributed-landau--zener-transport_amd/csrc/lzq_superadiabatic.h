@@ -409,7 +409,10 @@ __host__ __device__ __forceinline__ void sa_cell_follow(double mh, double sg, do
   if (has_right) sa_store(su2_mul(ub, su2_phase_adj(pb, uc)), out + 4);
 #else
   SU2 uc;
-#pragma nounroll
+#ifndef LZQ_FOLLOW_JOB_UNROLL
+#define LZQ_FOLLOW_JOB_UNROLL 1  // 3: the three frames straight-line (tools/ablate_follow.sh)
+#endif
+#pragma unroll LZQ_FOLLOW_JOB_UNROLL
   for (int job = 0; job < 3; ++job) {
     if ((job == 0 && !(has_left || has_right)) || (job == 1 && !has_left) || (job == 2 && !has_right)) continue;
     const double tau = job == 0 ? tau_c : (job == 1 ? tl : tr);

@@ -379,37 +379,6 @@ __device__ __forceinline__ MagnusPoly magnus_poly(const double (&cD)[4], const d
   return mp;
 }
 
-// cos|n| and sin|n|/|n| of a step (cos_sinc_short's values): the usual |n|^2 <= 1/8 inline, the
-// rest out of line, so the longer series' coefficients hold no registers in the step loop
-#ifndef LZQ_PROF_COLD_SC
-#define LZQ_PROF_COLD_SC 1
-#endif
-struct CosSinc {
-  double cs, sc;
-};
-__device__ __noinline__ CosSinc cos_sinc_cold(double x2) {
-  CosSinc r;
-  cos_sinc_short(x2, r.cs, r.sc);
-  return r;
-}
-__device__ __forceinline__ void cos_sinc_step(double x2, double& cs, double& sc) {
-  if (!LZQ_PROF_COLD_SC || !LZQ_SU2_SHORT8) {
-    cos_sinc_short(x2, cs, sc);
-  } else if (x2 <= 0.125) {
-    double ps = kSincC[6], pc = kCosC[6];
-#pragma unroll
-    for (int k = 5; k >= 0; --k) ps = fma3s(ps, x2, kSincC[k]);
-#pragma unroll
-    for (int k = 5; k >= 0; --k) pc = fma3s(pc, x2, kCosC[k]);
-    sc = ps;
-    cs = pc;
-  } else {
-    const CosSinc r = cos_sinc_cold(x2);
-    cs = r.cs;
-    sc = r.sc;
-  }
-}
-
 // u: the step's midpoint in units of the step, st + 1/2 (exact)
 __device__ __forceinline__ void magnus6_step(const MagnusPoly& mp, double u, Cplx& p0, Cplx& p1) {
 #define FMA __builtin_fma

@@ -96,6 +96,38 @@ __device__ __forceinline__ void cos_sinc_short(double x2, double& cs, double& sc
   }
 }
 
+// cos|n| and sin|n|/|n| of a step (cos_sinc_short's values): the usual |n|^2 <= 1/8 inline, the
+// rest out of line, so the longer series' coefficients hold no registers in the step loops
+// (lzq_profile.hip's Magnus step, lzq_propagator.hip's core steps)
+#ifndef LZQ_SU2_COLD_SC
+#define LZQ_SU2_COLD_SC 1  // 0: cos_sinc_short inline (tools/ablate_profile.py, tools/ablate_prop.py)
+#endif
+struct CosSinc {
+  double cs, sc;
+};
+static __device__ __noinline__ CosSinc cos_sinc_cold(double x2) {
+  CosSinc r;
+  cos_sinc_short(x2, r.cs, r.sc);
+  return r;
+}
+__device__ __forceinline__ void cos_sinc_step(double x2, double& cs, double& sc) {
+  if (!LZQ_SU2_COLD_SC || !LZQ_SU2_SHORT8) {
+    cos_sinc_short(x2, cs, sc);
+  } else if (x2 <= 0.125) {
+    double ps = kSincC[6], pc = kCosC[6];
+#pragma unroll
+    for (int k = 5; k >= 0; --k) ps = fma3s(ps, x2, kSincC[k]);
+#pragma unroll
+    for (int k = 5; k >= 0; --k) pc = fma3s(pc, x2, kCosC[k]);
+    sc = ps;
+    cs = pc;
+  } else {
+    const CosSinc r = cos_sinc_cold(x2);
+    cs = r.cs;
+    sc = r.sc;
+  }
+}
+
 // psi <- exp(-i n.sigma) psi, with cs = cos|n| and (sx, sy, sz) = sin|n|/|n| * n:
 // U11 = cs - i sz ; U12 = -sy - i sx ; U21 = sy - i sx ; U22 = cs + i sz
 __device__ __forceinline__ void su2_apply(double cs, double sx, double sy, double sz, Cplx& p0, Cplx& p1) {

@@ -2212,6 +2212,118 @@ __global__ __launch_bounds__(64) void ode_tp_seg_kernel(int64_t n, int64_t Mmax,
   lastG[o] = vG;
 }
 
+// The Y_B chain on its own (round 5).  Y_B's step is affine, YB <- fma(c, YB, Pf d), with c and d
+// from the step's stages alone (yb_rec): they do not depend on Y_chi.  So the Y_B candidates of an
+// interval need no Newton iteration and can share the stages: one lane steps kTpGChunk of them
+// with tp_steps' step / split structure and Y_B operations, and a window of +-kTpJG ulps costs a
+// fraction of the J = 4 round.  A point whose Y_B chain stitches here (gdone) needs only its Y_chi
+// chain in the rounds after (its Y_B chain is the one that wanders where the dynamics is neutral).
+constexpr int kTpGChunk = 22;  // 3 lanes per interval for JG = 32
+constexpr int kTpJG = 32;      // the Y_B round's window (a wider one cost more than it saved; J = 256 stays)
+template <int JG>
+__global__ __launch_bounds__(64) void ode_tp_gcand_kernel(const lzq_point* __restrict__ pts,
+                                                          const lzq_ode_params* __restrict__ ode, int64_t n,
+                                                          const int32_t* __restrict__ tidx,
+                                                          const double* __restrict__ ws, int64_t max_steps,
+                                                          int64_t Mmax, const TpNode* __restrict__ nodes,
+                                                          const TpCtl* __restrict__ ctl, double* __restrict__ candG) {
+  constexpr int NC = 2 * JG + 1, NCH = (NC + kTpGChunk - 1) / kTpGChunk;
+  const int64_t g = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  const int64_t p = g / (Mmax * NCH), rem = g - p * (Mmax * NCH), m = rem / NCH;
+  const int ch = (int)(rem - m * NCH);
+  if (p >= n) return;
+  const TpCtl c = ctl[p];
+  if (c.phase != kTpDone || m >= c.M) return;
+  const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
+  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
+  const int64_t k0 = m * c.L, k1 = k0 + c.L < S.N ? k0 + c.L : S.N;
+  const int64_t bkey = dkey(nodes[p * (Mmax + 1) + m].YB);
+  double yb[kTpGChunk];
+#pragma unroll
+  for (int i = 0; i < kTpGChunk; ++i) yb[i] = dfromkey(bkey + (ch * kTpGChunk + i - JG));
+  const Radau R = radau_tableau();
+  const RadauH hA = radau_h(R, S.h);
+  const double xb = branch_x(S.o, S.x0, S.x1), xb_below = nextafter(xb, -INFINITY);
+  auto part = [&](double xs, double hs, bool own_h) {
+    const RadauH hAs = own_h ? radau_h(R, hs) : hA;
+    OdeStage sg[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) sg[j] = ode_stage(S.o, w, xs + R.c[j] * hs);
+    const YbRec yr = yb_rec(hAs, sg);
+    const double e = S.o.Pf * yr.d;
+#pragma unroll
+    for (int i = 0; i < kTpGChunk; ++i) yb[i] = __builtin_fma(yr.c, yb[i], e);
+  };
+  double kd = (double)k0;
+  for (int64_t k = k0; k < k1; ++k, kd += 1.0) {
+    const double xk = S.x0 + kd * S.h;
+    const bool split = xk < xb && xb <= xk + S.h;
+    const double xa = split ? xb_below : xk + S.h;
+    if (xa > xk) part(xk, split ? xa - xk : S.h, split);
+    if (split && xk + S.h > xb) part(xb, (xk + S.h) - xb, true);
+  }
+  double* o = candG + (p * Mmax + m) * NC;
+#pragma unroll
+  for (int i = 0; i < kTpGChunk; ++i)
+    if (ch * kTpGChunk + i < NC) o[ch * kTpGChunk + i] = yb[i];
+}
+
+// the Y_B chain through one segment from every entry candidate (ode_tp_seg_kernel's G half)
+template <int JG>
+__global__ __launch_bounds__(64) void ode_tp_gseg_kernel(int64_t n, int64_t Mmax, int64_t Smax,
+                                                         const TpNode* __restrict__ nodes, const TpCtl* __restrict__ ctl,
+                                                         const double* __restrict__ candG, int32_t* __restrict__ segG,
+                                                         double* __restrict__ lastG) {
+  constexpr int NC = 2 * JG + 1;
+  const int64_t g = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  const int64_t p = g / (Smax * NC), rem = g - p * (Smax * NC), sg = rem / NC;
+  const int jj = (int)(rem - sg * NC);
+  if (p >= n) return;
+  const TpCtl c = ctl[p];
+  if (c.phase != kTpDone || sg * kTpSeg >= c.M) return;
+  const int64_t m0 = sg * kTpSeg, m1 = m0 + kTpSeg < c.M ? m0 + kTpSeg : c.M;
+  const TpNode* nd = nodes + p * (Mmax + 1);
+  int jG = jj;
+  double vG = 0.0;
+  for (int64_t m = m0; m < m1; ++m) {
+    vG = jG >= 0 ? candG[(p * Mmax + m) * NC + jG] : __builtin_nan("");
+    if (m + 1 < c.M) {
+      const int64_t dG = dkey(vG) - dkey(nd[m + 1].YB) + JG;
+      jG = (isfinite(vG) && dG >= 0 && dG < NC) ? (int)dG : -1;
+    }
+  }
+  segG[(p * Smax + sg) * NC + jj] = jG;
+  lastG[(p * Smax + sg) * NC + jj] = vG;
+}
+
+// the Y_B chain from node 0 through the segments: gdone[p], and its final value gyb[p]
+template <int JG>
+__global__ __launch_bounds__(64) void ode_tp_gstitch_kernel(int64_t n, int64_t Smax, const TpCtl* __restrict__ ctl,
+                                                            const int32_t* __restrict__ segG,
+                                                            const double* __restrict__ lastG,
+                                                            int32_t* __restrict__ gdone, double* __restrict__ gyb) {
+  constexpr int NC = 2 * JG + 1;
+  const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (p >= n) return;
+  const TpCtl c = ctl[p];
+  gdone[p] = 0;
+  if (c.phase != kTpDone) return;
+  const int64_t nseg = (c.M + kTpSeg - 1) / kTpSeg;
+  int jG = JG;
+  double YB = __builtin_nan("");
+  for (int64_t sg = 0; sg < nseg && jG >= 0; ++sg) {
+    const int64_t o = (p * Smax + sg) * NC;
+    if (sg + 1 == nseg)
+      YB = lastG[o + jG];
+    else
+      jG = segG[o + jG];
+  }
+  if (jG >= 0 && isfinite(YB)) {
+    gdone[p] = 1;
+    gyb[p] = YB;
+  }
+}
+
 // One thread per point: the chains from node 0 (candidate J, the exact start) through the
 // segments; both inside their windows to the end -> the final state is the sequential one: the
 // yields, skip[p] = 1, phase kTpExact.  Otherwise the point waits for the next round or the
@@ -2222,11 +2334,15 @@ __global__ __launch_bounds__(64) void ode_tp_stitch_kernel(const lzq_point* __re
                                                            const int32_t* __restrict__ segG,
                                                            const double* __restrict__ lastF,
                                                            const double* __restrict__ lastG, lzq_yield* __restrict__ out,
-                                                           int32_t* __restrict__ status, int32_t* __restrict__ skip) {
+                                                           int32_t* __restrict__ status, int32_t* __restrict__ skip,
+                                                           const int32_t* __restrict__ gdone,
+                                                           const double* __restrict__ gyb, int32_t only_gdone) {
   constexpr int NC = 2 * J + 1;
   const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (p >= n) return;
   TpCtl c = ctl[p];
+  const bool gd = gdone[p] != 0;  // the Y_B chain stitched on its own (ode_tp_gstitch_kernel)
+  if (only_gdone && !gd) return;  // a walk over tables whose Y_B half is not this round's
 #ifdef LZQ_ODE_TP_DEBUG
   printf("tp point %lld: stitch round J = %d, phase %d\n", (long long)p, J, c.phase);
 #endif
@@ -2234,18 +2350,18 @@ __global__ __launch_bounds__(64) void ode_tp_stitch_kernel(const lzq_point* __re
   const int64_t nseg = (c.M + kTpSeg - 1) / kTpSeg;
   int jF = J, jG = J;
   double YB = 0.0, Ychi = 0.0;
-  for (int64_t sg = 0; sg < nseg && jF >= 0 && jG >= 0; ++sg) {
+  for (int64_t sg = 0; sg < nseg && jF >= 0 && (gd || jG >= 0); ++sg) {
     const int64_t o = (p * Smax + sg) * NC;
     if (sg + 1 == nseg) {
       Ychi = lastF[o + jF];
-      YB = lastG[o + jG];
+      YB = gd ? gyb[p] : lastG[o + jG];
     } else {
-      const int a = segF[o + jF], b = segG[o + jG];
+      const int a = segF[o + jF], b = gd ? 0 : segG[o + jG];
       jF = a;
       jG = b;
     }
   }
-  if (jF < 0 || jG < 0 || !isfinite(Ychi) || !isfinite(YB)) {
+  if (jF < 0 || (!gd && jG < 0) || !isfinite(Ychi) || !isfinite(YB)) {
 #ifdef LZQ_ODE_TP_DEBUG
     printf("tp point %lld: stitching with J = %d failed (chains %d %d, %lld segments)\n", (long long)p, J, jF, jG,
            (long long)nseg);
@@ -2586,9 +2702,10 @@ int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, 
   const size_t b_loc = up(sizeof(lzq::TpMap) * (size_t)n * (size_t)Mmax);
   const size_t b_agg = up(sizeof(lzq::TpMap) * (size_t)n * (size_t)Bmax);
   const size_t b_bout = up(sizeof(lzq::TpBlkOut) * (size_t)n * (size_t)Bmax);
+  const size_t b_gd = up(sizeof(int32_t) * (size_t)n), b_gy = up(sizeof(double) * (size_t)n);
   char* buf = nullptr;
   int rc = hip_check(hipMallocAsync((void**)&buf, b_nodes + b_ends + b_ctl + b_skip + 2 * (b_cand + b_segi + b_segv) +
-                                                       b_loc + b_agg + b_bout,
+                                                       b_loc + b_agg + b_bout + b_gd + b_gy,
                                     s),
                      fn);
   if (rc) return rc;
@@ -2611,6 +2728,8 @@ int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, 
   auto* loc = reinterpret_cast<lzq::TpMap*>(take(b_loc));
   auto* agg = reinterpret_cast<lzq::TpMap*>(take(b_agg));
   auto* bout = reinterpret_cast<lzq::TpBlkOut*>(take(b_bout));
+  auto* gdone = reinterpret_cast<int32_t*>(take(b_gd));
+  auto* gyb = reinterpret_cast<double*>(take(b_gy));
   hipLaunchKernelGGL(lzq::ode_tp_init_kernel, dim3((unsigned)n), dim3(256), 0, s, d_points, d_ode, d_tidx, d_work,
                      max_steps, L, Mmax, nodes, ctl);
   rc = hip_check(hipGetLastError(), fn);
@@ -2638,26 +2757,52 @@ int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, 
     rc = hip_check(hipGetLastError(), fn);
   }
   // exact stitching, J = kTpJ1 then kTpJ2 for the points the first round did not finish
-  auto stitch = [&](auto Jc) {
+  auto stitch = [&](auto Jc, bool cands) {
     constexpr int J = decltype(Jc)::value, NC = 2 * J + 1;
     constexpr bool kStride = J > 32;
     const int64_t full = (n * Mmax * NC + 63) / 64;
     const int64_t cb = kStride ? std::min<int64_t>(full, 4096) : full;
-    hipLaunchKernelGGL((lzq::ode_tp_cand_kernel<J, kStride>), dim3((unsigned)cb), dim3(64), 0, s,
-                       d_points, d_ode, n, d_tidx, d_work, max_steps, Mmax, nodes, ctl, candF, candG);
-    int r = hip_check(hipGetLastError(), fn);
-    if (r) return r;
+    int r = LZQ_OK;
+    if (cands) {
+      hipLaunchKernelGGL((lzq::ode_tp_cand_kernel<J, kStride>), dim3((unsigned)cb), dim3(64), 0, s,
+                         d_points, d_ode, n, d_tidx, d_work, max_steps, Mmax, nodes, ctl, candF, candG);
+      r = hip_check(hipGetLastError(), fn);
+      if (r) return r;
+    }
     hipLaunchKernelGGL(lzq::ode_tp_seg_kernel<J>, dim3((unsigned)((n * Smax * NC + 63) / 64)), dim3(64), 0, s, n, Mmax,
                        Smax, nodes, ctl, candF, candG, segF, segG, lastF, lastG);
     r = hip_check(hipGetLastError(), fn);
     if (r) return r;
     hipLaunchKernelGGL(lzq::ode_tp_stitch_kernel<J>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, d_points, n, Smax,
-                       ctl, segF, segG, lastF, lastG, d_out, d_status, skip);
+                       ctl, segF, segG, lastF, lastG, d_out, d_status, skip, (const int32_t*)gdone, (const double*)gyb,
+                       (int32_t)!cands);
     return hip_check(hipGetLastError(), fn);
   };
-  if (rc == LZQ_OK) rc = stitch(std::integral_constant<int, lzq::kTpJ1>());
-  if (rc == LZQ_OK) rc = stitch(std::integral_constant<int, lzq::kTpJ2>());
-  if (rc == LZQ_OK && round3) rc = stitch(std::integral_constant<int, lzq::kTpJ3>());
+  // the Y_B chain on its own (its candidates fit the buffers of either last round)
+  auto gstitch = [&](auto Jc) {
+    constexpr int JG = decltype(Jc)::value, NC = 2 * JG + 1;
+    constexpr int NCH = (NC + lzq::kTpGChunk - 1) / lzq::kTpGChunk;
+    hipLaunchKernelGGL(lzq::ode_tp_gcand_kernel<JG>, dim3((unsigned)((n * Mmax * NCH + 63) / 64)), dim3(64), 0, s,
+                       d_points, d_ode, n, d_tidx, d_work, max_steps, Mmax, nodes, ctl, candG);
+    int r = hip_check(hipGetLastError(), fn);
+    if (r) return r;
+    hipLaunchKernelGGL(lzq::ode_tp_gseg_kernel<JG>, dim3((unsigned)((n * Smax * NC + 63) / 64)), dim3(64), 0, s, n, Mmax,
+                       Smax, nodes, ctl, candG, segG, lastG);
+    r = hip_check(hipGetLastError(), fn);
+    if (r) return r;
+    hipLaunchKernelGGL(lzq::ode_tp_gstitch_kernel<JG>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, n, Smax, ctl,
+                       segG, lastG, gdone, gyb);
+    return hip_check(hipGetLastError(), fn);
+  };
+  // J = 4 for both chains; then, for the points it did not finish, the Y_B chain alone at +-32
+  // ulps and the J = 4 walk again over the Y_chi candidates it has (candF is untouched); then
+  // J = 32 and J = 256 for both chains (a Y_B chain already stitched is not needed there)
+  if (rc == LZQ_OK) rc = hip_check(hipMemsetAsync(gdone, 0, sizeof(int32_t) * (size_t)n, s), fn);
+  if (rc == LZQ_OK) rc = stitch(std::integral_constant<int, lzq::kTpJ1>(), true);
+  if (rc == LZQ_OK) rc = gstitch(std::integral_constant<int, lzq::kTpJG>());
+  if (rc == LZQ_OK) rc = stitch(std::integral_constant<int, lzq::kTpJ1>(), false);
+  if (rc == LZQ_OK) rc = stitch(std::integral_constant<int, lzq::kTpJ2>(), true);
+  if (rc == LZQ_OK && round3) rc = stitch(std::integral_constant<int, lzq::kTpJ3>(), true);
   if (rc == LZQ_OK) {
     hipLaunchKernelGGL(lzq::ode_tp_finish_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, n, ctl, skip,
                        d_iters);

@@ -854,17 +854,31 @@ __global__ __launch_bounds__(kOdeBlock) void ode_spline_kernel(const lzq_point* 
     w[0] = cpm1;
     w[1] = dpm1;
   }
-  for (int k = 1; k < N - 1; ++k) {
-    const double dxk = X(k + 1) - X(k), slk = (Yk(k + 1) - Yk(k)) / dxk;
-    const double a = dxk, b = 2.0 * (dxm1 + dxk), c = dxm1;
-    const double r = 3.0 * (dxk * slm1 + dxm1 * slk);
-    const double den = b - a * cpm1;
-    cpm1 = c / den;
-    dpm1 = (r - a * dpm1) / den;
-    w[4 * k + 0] = cpm1;
-    w[4 * k + 1] = dpm1;
-    dxm1 = dxk;
-    slm1 = slk;
+  // (the sweeps read the knot values kSplCh rows ahead: one row at a time, each load waited behind
+  // the previous row's stores, ~0.3 us per row -- 0.46 ms per 800-knot table; same operations)
+  constexpr int kSplCh = 8;
+  double yk = Yk(1);
+  for (int k0 = 1; k0 < N - 1; k0 += kSplCh) {
+    double yn[kSplCh];
+#pragma unroll
+    for (int i = 0; i < kSplCh; ++i) yn[i] = k0 + i < N - 1 ? Yk(k0 + i + 1) : 0.0;
+#pragma unroll
+    for (int i = 0; i < kSplCh; ++i) {
+      const int k = k0 + i;
+      if (k < N - 1) {
+        const double dxk = X(k + 1) - X(k), slk = (yn[i] - yk) / dxk;
+        const double a = dxk, b = 2.0 * (dxm1 + dxk), c = dxm1;
+        const double r = 3.0 * (dxk * slm1 + dxm1 * slk);
+        const double den = b - a * cpm1;
+        cpm1 = c / den;
+        dpm1 = (r - a * dpm1) / den;
+        w[4 * k + 0] = cpm1;
+        w[4 * k + 1] = dpm1;
+        dxm1 = dxk;
+        slm1 = slk;
+        yk = yn[i];
+      }
+    }
   }
   // last row (not-a-knot): (x[-1]-x[-3]) s[-2] + dx[-2] s[-1] = b[-1]
   double s_next;
@@ -876,16 +890,31 @@ __global__ __launch_bounds__(kOdeBlock) void ode_spline_kernel(const lzq_point* 
   }
   // back substitution, forming the PPoly coefficients of interval k on the way
   const double y_last = w[ws_pt - 1];
-  for (int k = N - 2; k >= 0; --k) {
-    const double sk = w[4 * k + 1] - w[4 * k + 0] * s_next;
-    const double dxk = X(k + 1) - X(k);
-    const double yk = w[4 * k + 3], yk1 = (k + 1 < N - 1) ? w[4 * (k + 1) + 3] : y_last;
-    const double slk = (yk1 - yk) / dxk;
-    const double t = (sk + s_next - 2.0 * slk) / dxk;
-    w[4 * k + 0] = t / dxk;
-    w[4 * k + 1] = (slk - sk) / dxk - t;
-    w[4 * k + 2] = sk;
-    s_next = sk;
+  double yk1 = y_last;  // Y at knot k + 1
+  for (int k0 = N - 2; k0 >= 0; k0 -= kSplCh) {
+    double rc[kSplCh], rd[kSplCh], ry[kSplCh];
+#pragma unroll
+    for (int i = 0; i < kSplCh; ++i) {
+      const int k = k0 - i;
+      rc[i] = k >= 0 ? w[4 * k + 0] : 0.0;
+      rd[i] = k >= 0 ? w[4 * k + 1] : 0.0;
+      ry[i] = k >= 0 ? w[4 * k + 3] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < kSplCh; ++i) {
+      const int k = k0 - i;
+      if (k >= 0) {
+        const double sk = rd[i] - rc[i] * s_next;
+        const double dxk = X(k + 1) - X(k);
+        const double slk = (yk1 - ry[i]) / dxk;
+        const double t = (sk + s_next - 2.0 * slk) / dxk;
+        w[4 * k + 0] = t / dxk;
+        w[4 * k + 1] = (slk - sk) / dxk - t;
+        w[4 * k + 2] = sk;
+        s_next = sk;
+        yk1 = ry[i];
+      }
+    }
   }
   w[ws_pt - 4] = (double)N;  // the table's knot count, in its spare doubles (ode_table_ok)
   if (status) status[i] = LZQ_ODE_OK;

@@ -27,7 +27,9 @@ per rank (min / max / mean); `parity_spot` checks 64 rows of the last timed step
 the C oracle right after the timed region, before any secondary leg reuses the buffer (the exit
 status is non-zero if it, or the table's finiteness / shard placement, fails); `cpu_baseline`
 times the C oracle (the CPU restatement, OpenMP) on a bounded random sample of the same grid on
-every CPU of this job, and on one core.
+every CPU of this job, and on one core.  `world_size` / `dist_backend` come from the process group
+itself and `devices` holds every rank's GPU (PCI bus id, UUID, host), gathered before any timing;
+two RCCL ranks reporting one device end the run (exit status 2, no line).
 """
 from __future__ import annotations
 
@@ -290,6 +292,41 @@ def spread(vals) -> dict:
     return {"min": min(v), "max": max(v), "mean": float(np.mean(v)), "per_rank": v}
 
 
+def device_identity(eng, cuda: bool, rank: int, local: int) -> dict:
+    """This rank's device as the hardware names it: PCI domain:bus:device and the HIP UUID of the
+    GPU the engine runs on (torch device properties; no HIP call beyond the engine's own), the
+    host, and the visibility masks the launcher set.  `key` is what must differ between RCCL
+    ranks.  A stand-in engine (tests) supplies its own via eng.device_identity()."""
+    rec = {"rank": rank, "local_rank": local, "host": socket.gethostname(),
+           "visible": {k: os.environ.get(k) for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
+                                                      "CUDA_VISIBLE_DEVICES") if os.environ.get(k) is not None}}
+    if hasattr(eng, "device_identity"):
+        rec.update(eng.device_identity(rank, local))
+    elif cuda:
+        idx = eng.device.index if getattr(eng, "device", None) is not None and eng.device.index is not None \
+            else torch.cuda.current_device()
+        p = torch.cuda.get_device_properties(idx)
+        pci = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+        uuid = str(getattr(p, "uuid", ""))
+        rec.update({"device_index": idx, "name": p.name, "arch": p.gcnArchName, "pci_bus_id": pci, "uuid": uuid,
+                    "cus": p.multi_processor_count})
+    else:
+        rec.update({"device_index": None, "pci_bus_id": None, "uuid": None})
+    rec.setdefault("key", f"{rec['host']}/{rec.get('pci_bus_id')}/{rec.get('uuid')}")
+    return rec
+
+
+def duplicate_devices(ids: list) -> list:
+    """Pairs of ranks whose device keys coincide (two ranks on one GPU)."""
+    seen, dups = {}, []
+    for r in ids:
+        if r["key"] in seen:
+            dups.append((seen[r["key"]], r["rank"]))
+        else:
+            seen[r["key"]] = r["rank"]
+    return dups
+
+
 def free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -370,6 +407,28 @@ def main(argv=None, engine=None) -> int:
             dist.init_process_group("gloo")
 
     eng = engine if engine is not None else importlib.import_module(PKG + ".engine").Engine(local)
+    # every rank's device, gathered before any timing: the line names the GPUs it measured, and
+    # two RCCL ranks on one GPU (or a stand-in claiming exclusive devices) end the run here
+    me = device_identity(eng, cuda, rank, local)
+    if use_dist:
+        ids = [None] * world
+        dist.all_gather_object(ids, me)
+        pg = {"world_size": dist.get_world_size(), "backend": str(dist.get_backend())}
+    else:
+        ids, pg = [me], {"world_size": 1, "backend": None}
+    if pg["world_size"] != args.gpus:
+        print(f"[bench] process group has {pg['world_size']} ranks but --gpus={args.gpus}", file=sys.stderr)
+        if use_dist:
+            dist.destroy_process_group()
+        return 2
+    dups = duplicate_devices(ids)
+    if dups and (nccl or getattr(eng, "exclusive_devices", False)):
+        if rank == 0:
+            print(f"[bench] ranks {dups} report the same device ({[ids[a]['key'] for a, _ in dups]}): the line "
+                  f"would not measure {world} GPUs", file=sys.stderr)
+        if use_dist:
+            dist.destroy_process_group()
+        return 2
     axes = grid_axes(world)
     per = args.points
     total = per * world
@@ -483,6 +542,10 @@ def main(argv=None, engine=None) -> int:
             "value": total * args.steps / elapsed,
             "unit": "points/s",
             "n_gpus": world,
+            "world_size": pg["world_size"],
+            "dist_backend": pg["backend"],
+            "devices": ids,
+            "distinct_devices": len({r["key"] for r in ids}),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,

@@ -72,7 +72,7 @@ assert ctypes.sizeof(lzq_point) == 136 and ctypes.sizeof(lzq_yield) == 48 and ct
 assert ctypes.sizeof(lzq_aov_params) == 40 and ctypes.sizeof(lzq_ode_params) == 24
 ODE_NT = 800                # LZQ_ODE_NT: main()'s build_tables knots (fpy:387)
 ODE_WS_PER_POINT = 3200     # LZQ_ODE_WS_PER_POINT
-ODE_STATUS = {0: "ok", 1: "bad_grid", 2: "bad_step", 3: "too_many_steps", 4: "newton", 6: "unresolved",
+ODE_STATUS = {0: "ok", 1: "bad_grid", 2: "bad_step", 3: "too_many_steps", 4: "newton", 5: "not_linear", 6: "unresolved",
               7: "bad_table"}  # enum lzq_ode_status
 ABI_VERSION = 3  # include/lzq.h LZQ_ABI_VERSION this binding is written against
 

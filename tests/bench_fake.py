@@ -16,11 +16,19 @@ sys.path.insert(0, ROOT)
 
 
 class FakeEngine:
+    # the stand-in claims one device per rank, so bench.py's duplicate-device check applies to it
+    # as to RCCL ranks; FAKE_DUP_DEVICE=1 makes every rank report device 0
+    exclusive_devices = True
+
     def __init__(self, bad_dense_row: int | None = None):
         self.device = torch.device("cpu")
         self.truncate = False
         self.bad = bad_dense_row
         self._cache = {}
+
+    def device_identity(self, rank: int, local: int) -> dict:
+        dev = 0 if os.environ.get("FAKE_DUP_DEVICE") else local
+        return {"device_index": dev, "pci_bus_id": f"0000:{0x11 + dev:02x}:00", "uuid": f"fake-gpu-{dev}"}
 
     def tune_truncate(self, on: bool) -> bool:
         prev, self.truncate = self.truncate, bool(on)

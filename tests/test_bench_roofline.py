@@ -136,3 +136,36 @@ def test_rank_count_mismatch_is_an_error():
     r = _run([sys.executable, FAKE, "--gpus", "4", *SMALL], env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2 and not [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert "WORLD_SIZE=1 but --gpus=4" in r.stderr
+
+
+def test_n_rank_line_names_distinct_devices():
+    """at N > 1 the line carries the process group's own world size and backend
+    and one device record per rank (PCI bus id, UUID, host), and counts the distinct devices; the
+    CPU baseline is still there."""
+    r = _run([sys.executable, FAKE, "--gpus", "2", "--points", "64", "--steps", "2", "--warmup", "1", "--no-reuse",
+              "--no-parity-spot", "--dist-backend", "gloo", "--cpu-seconds", "0.5"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _line(r.stdout)
+    assert rec["n_gpus"] == 2 and rec["world_size"] == 2 and rec["dist_backend"] == "gloo"
+    assert [d["rank"] for d in rec["devices"]] == [0, 1]
+    assert rec["distinct_devices"] == 2 and len({d["pci_bus_id"] for d in rec["devices"]}) == 2
+    assert all(d["uuid"] and d["host"] for d in rec["devices"])
+    assert rec["cpu_baseline"]["value"] > 0
+
+
+def test_two_ranks_on_one_device_exit_nonzero():
+    """Two ranks that report the same device (a stand-in claiming exclusive devices, as RCCL ranks
+    are): exit 2 before any timing, no line."""
+    r = _run([sys.executable, FAKE, "--gpus", "2", "--points", "64", "--steps", "2", "--warmup", "1", "--no-reuse",
+              "--no-parity-spot", "--dist-backend", "gloo", "--no-cpu-baseline"], env={"FAKE_DUP_DEVICE": "1"})
+    assert r.returncode != 0
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert "report the same device" in r.stderr
+
+
+def test_single_rank_line_names_its_device():
+    r = _run([sys.executable, FAKE, *SMALL, "--no-reuse", "--no-parity-spot"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _line(r.stdout)
+    assert rec["world_size"] == 1 and rec["dist_backend"] is None and rec["distinct_devices"] == 1
+    assert len(rec["devices"]) == 1 and rec["devices"][0]["rank"] == 0

@@ -1381,6 +1381,129 @@ struct RicRow {
   double lam[3], E2[3], a[3];  // StageBase lam, E2, a of the step's three stages
 };
 
+#ifndef LZQ_RIC_LEAN
+#define LZQ_RIC_LEAN 1  // ode_riccati_kernel's regular steps through ric_step (round 6): radau_step<false>'s operations, lean registers
+#endif
+
+// ode_riccati_kernel's cooperative fill of one row (step at xk): the stage bases, beta_j and the
+// Y_B step map, with the operations of the kernel's inline fill (ode_stage_base, yb_rec on
+// radau_h(R, h)).  Out of line: the fill runs once per 64 steps, and inlined its constants (the
+// exponential's and the spline's) and temporaries were hoisted across the step loop, where they
+// took the registers the Newton iteration needs (spills in the hot loop).
+__device__ __noinline__ void ric_fill(const OdePoint* ou, const double* __restrict__ wu, double xk, double h,
+                                      RicRow* row, double* bt, YbCD* rcd) {
+  const Radau R = radau_tableau();
+#pragma unroll 1
+  for (int j = 0; j < 3; ++j) {
+    const double cj = j == 0 ? R.c[0] : (j == 1 ? R.c[1] : R.c[2]);
+    const StageBase bs = ode_stage_base(*ou, wu, xk + cj * h);
+    row->lam[j] = bs.lam;
+    row->E2[j] = bs.E2;
+    row->a[j] = bs.a;
+    bt[j] = ou->gamma_w * bs.beta;
+  }
+  const double beta[3] = {bt[0], bt[1], bt[2]}, a[3] = {row->a[0], row->a[1], row->a[2]};
+  const YbRec yr = yb_rec(radau_h(R, h), beta, a);
+  *rcd = {yr.c, yr.d};
+}
+
+// radau_step<false>'s transformed Newton iteration (newton_j) for ode_riccati_kernel: the same
+// operations in the same order, with the six off-diagonal constant products of the adjugate held in
+// VGPRs (pv, pinned once per launch) instead of copied from SGPRs into a VGPR per entry per iteration
+// (fma_neg_s takes one constant as its SGPR operand, the other must be a VGPR).
+// pv = kRadauAinvP[1, 2, 3, 5, 6, 7].
+struct RicJ {
+  double b[3][3], id;
+};
+__device__ __forceinline__ bool ric_newton(double (&Z)[3], double Y0, const double (&hl)[3], const double (&hl2)[3],
+                                           const double (&hS)[3], const double (&E2)[3], const double (&pv)[6],
+                                           RicJ& J, const bool reuse, bool& near) {
+#define FMA __builtin_fma
+  double d[3], r[3], k[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    r[j] = FMA(-hl[j], FMA(Z[j], Z[j], -E2[j]), -hS[j]);
+    d[j] = Z[j] - Y0;
+    k[j] = FMA(hl2[j], Z[j], kRadauAinv[j][j]);
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    r[i] = FMA(-kRadauAinv[i][2], d[2], FMA(-kRadauAinv[i][1], d[1], FMA(-kRadauAinv[i][0], d[0], r[i])));
+  if (!reuse) {
+    J.b[0][0] = FMA(k[1], k[2], -kRadauAinvP[0]), J.b[0][1] = fma_neg_s(k[2], kRadauAinv[0][1], pv[0]);
+    J.b[0][2] = fma_neg_s(k[1], kRadauAinv[0][2], pv[1]), J.b[1][0] = fma_neg_s(k[2], kRadauAinv[1][0], pv[2]);
+    J.b[1][1] = FMA(k[0], k[2], -kRadauAinvP[4]), J.b[1][2] = fma_neg_s(k[0], kRadauAinv[1][2], pv[3]);
+    J.b[2][0] = fma_neg_s(k[1], kRadauAinv[2][0], pv[4]), J.b[2][1] = fma_neg_s(k[0], kRadauAinv[2][1], pv[5]);
+    J.b[2][2] = FMA(k[0], k[1], -kRadauAinvP[8]);
+    const double den = FMA(k[0], J.b[0][0], FMA(kRadauAinv[0][1], J.b[1][0], kRadauAinv[0][2] * J.b[2][0]));
+    J.id = LZQ_ODE_NEWTON_RCP ? rcp_pos(den) : 1.0 / den;
+  }
+  double g[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) g[i] = FMA(J.b[i][0], r[0], FMA(J.b[i][1], r[1], J.b[i][2] * r[2])) * J.id;
+#undef FMA
+  double dmax = 0.0, zmax = 0.0;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    Z[i] = Z[i] + g[i];
+    dmax = fmax(dmax, fabs(g[i]));
+    zmax = fmax(zmax, fabs(Z[i]));
+  }
+  near = !(dmax > 1e-3 * zmax);
+  return !(dmax > 1e-15 * zmax);
+}
+
+// radau_step<false>(hA, sg, Ychi, YB, Zs, guess) for ode_riccati_kernel's regular steps, from the
+// step's scaled stage data (lam_j, E2_j, S_j) and h; hA2 = hA.a[2][*] for the linear branch.  The
+// same branches and iterates: the linear update, the peeled pair (the second simplified when the
+// first correction was small), then -- only for a lane whose pair did not converge -- full
+// iterations up to the 40th, and from Y_chi once more when the start was predicted.
+__device__ __forceinline__ bool ric_step(double h, const double (&hA2)[3], const double (&lam)[3],
+                                         const double (&E2)[3], const double (&S)[3], const double (&pv)[6],
+                                         double& Ychi, double (&Zs)[3], bool guess) {
+  const bool nonlinear = lam[0] != 0.0 || lam[1] != 0.0 || lam[2] != 0.0;
+  if (!nonlinear) {
+    double acc = Ychi;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc = __builtin_fma(-hA2[j], S[j], acc);
+    Ychi = acc;
+    return true;
+  }
+  const double Y0 = Ychi;
+  double hl[3], hl2[3], hS[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    hl[j] = h * lam[j];
+    hl2[j] = 2.0 * hl[j];
+    hS[j] = h * S[j];
+  }
+  double Z[3] = {guess ? Zs[0] : Y0, guess ? Zs[1] : Y0, guess ? Zs[2] : Y0};
+  RicJ J;
+  bool near = false;
+  const bool c1 = ric_newton(Z, Y0, hl, hl2, hS, E2, pv, J, false, near);
+  const bool reuse = near;
+  const bool c2 = ric_newton(Z, Y0, hl, hl2, hS, E2, pv, J, reuse, near);
+  bool ok = c1 || c2;
+  if (!ok) {  // rare: radau_step's loop after the peeled pair, and its second attempt from Y0
+#pragma nounroll
+    for (int it = 2; it < 40 && !ok; ++it) ok = ric_newton(Z, Y0, hl, hl2, hS, E2, pv, J, false, near);
+    if (!ok && guess) {
+      Z[0] = Y0;
+      Z[1] = Y0;
+      Z[2] = Y0;
+#pragma nounroll
+      for (int it = 0; it < 40 && !ok; ++it) ok = ric_newton(Z, Y0, hl, hl2, hS, E2, pv, J, false, near);
+    }
+  }
+  if (ok) {
+    Zs[0] = Z[0];
+    Zs[1] = Z[1];
+    Zs[2] = Z[2];
+    Ychi = Z[2];
+  }
+  return ok;
+}
+
 // kPhase: a wave whose split step (the T = m/3 branch) lies in this launch's range runs in three
 // passes -- 0: the regular steps before it, 1: the split step and the next (ode_integrate_kernel's
 // split-step code, each lane forming its own stages: two steps, so registers do not matter),
@@ -1562,11 +1685,22 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
       }
     }
   }
+  // ric_step's loop constants: hA's last row (the linear branch) and the adjugate's off-diagonal
+  // constant products, pinned in VGPRs (see ric_newton)
+  const double hA2[3] = {hA.a[2][0], hA.a[2][1], hA.a[2][2]};
+  double pv[6] = {kRadauAinvP[1], kRadauAinvP[2], kRadauAinvP[3], kRadauAinvP[5], kRadauAinvP[6], kRadauAinvP[7]};
+  if (LZQ_RIC_LEAN && kPhase != 1) {
+#pragma unroll
+    for (int q = 0; q < 6; ++q) asm volatile("" : "+v"(pv[q]));
+  }
   for (int64_t kb = pk_begin; kPhase != 1 && kb < pk_stop; kb += 64) {
     const int64_t kend = kb + 64 < pk_stop ? kb + 64 : pk_stop;
     {  // lane l: the stage ingredients and Y_B step map of step kb + l (the cooperative fill)
       const int64_t kl = kb + lane;
       if (kl < kend) {
+        if (LZQ_RIC_LEAN) {
+          ric_fill(&s_pt[wv], wu, x0u + (double)kl * hu, hu, &s_row[wv][lane], s_beta[wv][lane], &s_rcd[wv][lane]);
+        } else {
         const double xk = x0u + (double)kl * hu;
         RicRow& row = s_row[wv][lane];
         double* bt = s_beta[wv][lane];
@@ -1582,6 +1716,7 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
         const double beta[3] = {bt[0], bt[1], bt[2]}, a[3] = {row.a[0], row.a[1], row.a[2]};
         const YbRec yr = yb_rec(hA, beta, a);
         s_rcd[wv][lane] = {yr.c, yr.d};
+        }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -1627,7 +1762,13 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
         const YbCD rc = s_rcd[wv][r];
         YB = __builtin_fma(rc.c, YB, Pf * rc.d);
         if (riccati && r == rz) use_guess = block_guess(R, hu, sg, Ychi, Zs);
-        ok = radau_step<false>(hA, sg, Ychi, YB, Zs, use_guess);
+        if (LZQ_RIC_LEAN) {
+          const double lam[3] = {sg[0].lam, sg[1].lam, sg[2].lam}, E2[3] = {sg[0].E2, sg[1].E2, sg[2].E2},
+                       S[3] = {sg[0].S, sg[1].S, sg[2].S};
+          ok = ric_step(hu, hA2, lam, E2, S, pv, Ychi, Zs, use_guess);
+        } else {
+          ok = radau_step<false>(hA, sg, Ychi, YB, Zs, use_guess);
+        }
       }
       have = true;
       Yp = Ystart;

@@ -51,14 +51,20 @@ def main():
             if not os.environ.get("ABLATE_NOCHECK"):  # diagnostic variants that change results
                 assert np.max(np.abs(t - ref) / np.maximum(np.abs(ref), 1e-300)) < 1e-11, k
         res = {k: [] for k in engs}
+        last = {}
         for _ in range(rounds):
             for k, e in engs.items():
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
-                e.ode(pts, ods, chunk=1 << 18, method=method)
+                last[k] = e.ode(pts, ods, chunk=1 << 18, method=method)[0]
                 torch.cuda.synchronize()
                 res[k].append(n / (time.perf_counter() - t0))
         out[cname] = {k: round(max(v)) for k, v in res.items()}
+        first = next(iter(last))
+        # every variant's full timed table against the first variant's, bit for bit (NaN rows equal)
+        out[cname + "_bit_identical_to_" + first] = {
+            k: bool(torch.equal(torch.nan_to_num(v, nan=1.5e308), torch.nan_to_num(last[first], nan=1.5e308)))
+            for k, v in last.items()}
     print(json.dumps(out, indent=1))
 
 

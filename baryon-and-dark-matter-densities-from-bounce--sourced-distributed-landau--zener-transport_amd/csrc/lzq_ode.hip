@@ -1695,8 +1695,14 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
   }
   for (int64_t kb = pk_begin; kPhase != 1 && kb < pk_stop; kb += 64) {
     const int64_t kend = kb + 64 < pk_stop ? kb + 64 : pk_stop;
+    uint64_t xok = 0;
     {  // lane l: the stage ingredients and Y_B step map of step kb + l (the cooperative fill)
       const int64_t kl = kb + lane;
+      if (LZQ_RIC_LEAN) {
+        // the steps' x guard (xk + h > xk, wave-uniform per step) as one mask, from the fill's xk
+        const double xk = x0u + (double)kl * hu;
+        xok = __ballot(kl < kend && xk + hu > xk);
+      }
       if (kl < kend) {
         if (LZQ_RIC_LEAN) {
           ric_fill(&s_pt[wv], wu, x0u + (double)kl * hu, hu, &s_row[wv][lane], s_beta[wv][lane], &s_rcd[wv][lane]);
@@ -1728,7 +1734,58 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
     // compare per step.  (Peeling row 0 of aligned blocks, with pass 1 run on to the next block,
     // measured slower: profiles/round5/ablate_ode_pred_block.json.)
     const int rz = (int)((-kb) & (int64_t)(LZQ_ODE_PRED_BLOCK - 1));
-    for (int r = 0; r < (int)(kend - kb) && !done; ++r) {
+    for (int r = 0; LZQ_RIC_LEAN && r < (int)(kend - kb) && !done; ++r) {
+      // the same step as the loop below: the row is read first (its LDS latency under the
+      // predictor), the x guard is the fill's mask bit, the step index needs no counter
+      const RicRow row = s_row[wv][r];
+      const YbCD rc = s_rcd[wv][r];
+      const double YB_prev = YB;
+      const double Ystart = Ychi;
+      bool use_guess = false;
+      if (riccati && have && r != rz) {
+        double g[3];
+        use_guess = true;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          g[j] = fma_s(Zs[2], kRadauPred[j][3], fma_s(Zs[1], kRadauPred[j][2],
+                                                      fma_s(Zs[0], kRadauPred[j][1], kRadauPred[j][0] * Yp)));
+          use_guess = use_guess && fabs(g[j] - Ychi) <= 0.25 * fabs(Ychi);
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) Zs[j] = g[j];
+      }
+      bool ok = true;
+      if ((xok >> r) & 1) {
+        double lam[3], E2[3], S[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const double alpha = Pf * row.a[j];
+          S[j] = deplete ? alpha : 0.0;
+          lam[j] = sigmav * row.lam[j];
+          E2[j] = row.E2[j];
+        }
+        YB = __builtin_fma(rc.c, YB, Pf * rc.d);
+        if (riccati && r == rz) {
+          OdeStage sg[3];
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            sg[j].lam = lam[j];
+            sg[j].E2 = E2[j];
+            sg[j].S = S[j];
+          }
+          use_guess = block_guess(R, hu, sg, Ychi, Zs);
+        }
+        ok = ric_step(hu, hA2, lam, E2, S, pv, Ychi, Zs, use_guess);
+      }
+      have = true;
+      Yp = Ystart;
+      if (!ok) {
+        YB = YB_prev;
+        st = LZQ_ODE_NEWTON;
+        done = true;
+      }
+    }
+    for (int r = 0; !LZQ_RIC_LEAN && r < (int)(kend - kb) && !done; ++r) {
       const double xk = x0u + kd * hu;
       kd += 1.0;
       const double YB_prev = YB;

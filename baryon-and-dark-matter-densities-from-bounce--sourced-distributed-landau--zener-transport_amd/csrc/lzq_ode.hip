@@ -1415,6 +1415,7 @@ __device__ __noinline__ void ric_fill(const OdePoint* ou, const double* __restri
 struct RicJ {
   double b[3][3], id;
 };
+template <bool kDep>
 __device__ __forceinline__ bool ric_newton(double (&Z)[3], double Y0, const double (&hl)[3], const double (&hl2)[3],
                                            const double (&hS)[3], const double (&E2)[3], const double (&pv)[6],
                                            RicJ& J, const bool reuse, bool& near) {
@@ -1422,7 +1423,9 @@ __device__ __forceinline__ bool ric_newton(double (&Z)[3], double Y0, const doub
   double d[3], r[3], k[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    r[j] = FMA(-hl[j], FMA(Z[j], Z[j], -E2[j]), -hS[j]);
+    // without depletion hS_j = h * (+0) = +0, and fma(a, b, -0) rounds a * b exactly as the product
+    // does (zero products keep their sign: +0 + -0 = +0, -0 + -0 = -0): the same r_j
+    r[j] = kDep ? FMA(-hl[j], FMA(Z[j], Z[j], -E2[j]), -hS[j]) : -hl[j] * FMA(Z[j], Z[j], -E2[j]);
     d[j] = Z[j] - Y0;
     k[j] = FMA(hl2[j], Z[j], kRadauAinv[j][j]);
   }
@@ -1458,15 +1461,20 @@ __device__ __forceinline__ bool ric_newton(double (&Z)[3], double Y0, const doub
 // same branches and iterates: the linear update, the peeled pair (the second simplified when the
 // first correction was small), then -- only for a lane whose pair did not converge -- full
 // iterations up to the 40th, and from Y_chi once more when the start was predicted.
+// kDep = false: a wave with no depleting lane (S_j = +0 on every lane): the linear branch leaves
+// Y_chi as it is (fma(-hA, +0, Y) = Y + -0 = Y, exactly) and hS is not formed (ric_newton).
+template <bool kDep>
 __device__ __forceinline__ bool ric_step(double h, const double (&hA2)[3], const double (&lam)[3],
                                          const double (&E2)[3], const double (&S)[3], const double (&pv)[6],
                                          double& Ychi, double (&Zs)[3], bool guess) {
   const bool nonlinear = lam[0] != 0.0 || lam[1] != 0.0 || lam[2] != 0.0;
   if (!nonlinear) {
-    double acc = Ychi;
+    if (kDep) {
+      double acc = Ychi;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) acc = __builtin_fma(-hA2[j], S[j], acc);
-    Ychi = acc;
+      for (int j = 0; j < 3; ++j) acc = __builtin_fma(-hA2[j], S[j], acc);
+      Ychi = acc;
+    }
     return true;
   }
   const double Y0 = Ychi;
@@ -1475,24 +1483,24 @@ __device__ __forceinline__ bool ric_step(double h, const double (&hA2)[3], const
   for (int j = 0; j < 3; ++j) {
     hl[j] = h * lam[j];
     hl2[j] = 2.0 * hl[j];
-    hS[j] = h * S[j];
+    hS[j] = kDep ? h * S[j] : 0.0;
   }
   double Z[3] = {guess ? Zs[0] : Y0, guess ? Zs[1] : Y0, guess ? Zs[2] : Y0};
   RicJ J;
   bool near = false;
-  const bool c1 = ric_newton(Z, Y0, hl, hl2, hS, E2, pv, J, false, near);
+  const bool c1 = ric_newton<kDep>(Z, Y0, hl, hl2, hS, E2, pv, J, false, near);
   const bool reuse = near;
-  const bool c2 = ric_newton(Z, Y0, hl, hl2, hS, E2, pv, J, reuse, near);
+  const bool c2 = ric_newton<kDep>(Z, Y0, hl, hl2, hS, E2, pv, J, reuse, near);
   bool ok = c1 || c2;
   if (!ok) {  // rare: radau_step's loop after the peeled pair, and its second attempt from Y0
 #pragma nounroll
-    for (int it = 2; it < 40 && !ok; ++it) ok = ric_newton(Z, Y0, hl, hl2, hS, E2, pv, J, false, near);
+    for (int it = 2; it < 40 && !ok; ++it) ok = ric_newton<kDep>(Z, Y0, hl, hl2, hS, E2, pv, J, false, near);
     if (!ok && guess) {
       Z[0] = Y0;
       Z[1] = Y0;
       Z[2] = Y0;
 #pragma nounroll
-      for (int it = 0; it < 40 && !ok; ++it) ok = ric_newton(Z, Y0, hl, hl2, hS, E2, pv, J, false, near);
+      for (int it = 0; it < 40 && !ok; ++it) ok = ric_newton<kDep>(Z, Y0, hl, hl2, hS, E2, pv, J, false, near);
     }
   }
   if (ok) {
@@ -1688,6 +1696,7 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
   // ric_step's loop constants: hA's last row (the linear branch) and the adjugate's off-diagonal
   // constant products, pinned in VGPRs (see ric_newton)
   const double hA2[3] = {hA.a[2][0], hA.a[2][1], hA.a[2][2]};
+  const bool dep_any = !__all(deplete == 0);  // wave-uniform: some lane depletes its source
   double pv[6] = {kRadauAinvP[1], kRadauAinvP[2], kRadauAinvP[3], kRadauAinvP[5], kRadauAinvP[6], kRadauAinvP[7]};
   if (LZQ_RIC_LEAN && kPhase != 1) {
 #pragma unroll
@@ -1734,7 +1743,10 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
     // compare per step.  (Peeling row 0 of aligned blocks, with pass 1 run on to the next block,
     // measured slower: profiles/round5/ablate_ode_pred_block.json.)
     const int rz = (int)((-kb) & (int64_t)(LZQ_ODE_PRED_BLOCK - 1));
-    for (int r = 0; LZQ_RIC_LEAN && r < (int)(kend - kb) && !done; ++r) {
+    // a wave with no depleting lane runs the loop without the source products (ric_step<false>)
+    auto lean_steps = [&](auto dep_tag) {
+    constexpr bool kDep = decltype(dep_tag)::value;
+    for (int r = 0; r < (int)(kend - kb) && !done; ++r) {
       // the same step as the loop below: the row is read first (its LDS latency under the
       // predictor), the x guard is the fill's mask bit, the step index needs no counter
       const RicRow row = s_row[wv][r];
@@ -1759,8 +1771,7 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
         double lam[3], E2[3], S[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-          const double alpha = Pf * row.a[j];
-          S[j] = deplete ? alpha : 0.0;
+          S[j] = kDep ? (deplete ? Pf * row.a[j] : 0.0) : 0.0;
           lam[j] = sigmav * row.lam[j];
           E2[j] = row.E2[j];
         }
@@ -1775,7 +1786,7 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
           }
           use_guess = block_guess(R, hu, sg, Ychi, Zs);
         }
-        ok = ric_step(hu, hA2, lam, E2, S, pv, Ychi, Zs, use_guess);
+        ok = ric_step<kDep>(hu, hA2, lam, E2, S, pv, Ychi, Zs, use_guess);
       }
       have = true;
       Yp = Ystart;
@@ -1784,6 +1795,11 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
         st = LZQ_ODE_NEWTON;
         done = true;
       }
+    }
+    };
+    if (LZQ_RIC_LEAN) {
+      if (dep_any) lean_steps(std::true_type{});
+      else lean_steps(std::false_type{});
     }
     for (int r = 0; !LZQ_RIC_LEAN && r < (int)(kend - kb) && !done; ++r) {
       const double xk = x0u + kd * hu;
@@ -1822,7 +1838,7 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
         if (LZQ_RIC_LEAN) {
           const double lam[3] = {sg[0].lam, sg[1].lam, sg[2].lam}, E2[3] = {sg[0].E2, sg[1].E2, sg[2].E2},
                        S[3] = {sg[0].S, sg[1].S, sg[2].S};
-          ok = ric_step(hu, hA2, lam, E2, S, pv, Ychi, Zs, use_guess);
+          ok = ric_step<true>(hu, hA2, lam, E2, S, pv, Ychi, Zs, use_guess);
         } else {
           ok = radau_step<false>(hA, sg, Ychi, YB, Zs, use_guess);
         }

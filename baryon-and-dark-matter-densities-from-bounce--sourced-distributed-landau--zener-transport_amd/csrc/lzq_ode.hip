@@ -1381,6 +1381,12 @@ struct RicRow {
   double lam[3], E2[3], a[3];  // StageBase lam, E2, a of the step's three stages
 };
 
+#ifndef LZQ_RIC_KRELOAD
+#define LZQ_RIC_KRELOAD 1  // ode_riccati_kernel's lean loop reloads the predictor constants per step (SGPR room)
+#endif
+#ifndef LZQ_RIC_V4
+#define LZQ_RIC_V4 1  // ric_newton's dmax without the +0 start (same tests; see there)
+#endif
 #ifndef LZQ_RIC_LEAN
 #define LZQ_RIC_LEAN 1  // ode_riccati_kernel's regular steps through ric_step (round 6): radau_step<false>'s operations, lean registers
 #endif
@@ -1445,13 +1451,17 @@ __device__ __forceinline__ bool ric_newton(double (&Z)[3], double Y0, const doub
 #pragma unroll
   for (int i = 0; i < 3; ++i) g[i] = FMA(J.b[i][0], r[0], FMA(J.b[i][1], r[1], J.b[i][2] * r[2])) * J.id;
 #undef FMA
-  double dmax = 0.0, zmax = 0.0;
+  double zmax = 0.0;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     Z[i] = Z[i] + g[i];
-    dmax = fmax(dmax, fabs(g[i]));
     zmax = fmax(zmax, fabs(Z[i]));
   }
+  // newton_j's dmax = fmax(fmax(fmax(+0, |g0|), |g1|), |g2|) without the +0: the two differ only when
+  // all three corrections are NaN (+0 there, NaN here), and both then fail "dmax > c zmax" (zmax >= 0),
+  // so near and the convergence test are the same
+  const double dmax = LZQ_RIC_V4 ? fmax(fmax(fabs(g[0]), fabs(g[1])), fabs(g[2]))
+                                 : fmax(fmax(fmax(0.0, fabs(g[0])), fabs(g[1])), fabs(g[2]));
   near = !(dmax > 1e-3 * zmax);
   return !(dmax > 1e-15 * zmax);
 }
@@ -1746,21 +1756,29 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
     // a wave with no depleting lane runs the loop without the source products (ric_step<false>)
     auto lean_steps = [&](auto dep_tag) {
     constexpr bool kDep = decltype(dep_tag)::value;
-    for (int r = 0; r < (int)(kend - kb) && !done; ++r) {
+    // LZQ_RIC_V4: a uniform trip count, each lane's steps under !done (a lane whose Newton iteration
+    // failed stops there, as in the loop below)
+    const int nr = (int)(kend - kb);
+    for (int r = 0; r < nr && (LZQ_RIC_V4 || !done); ++r) {
       // the same step as the loop below: the row is read first (its LDS latency under the
       // predictor), the x guard is the fill's mask bit, the step index needs no counter
       const RicRow row = s_row[wv][r];
       const YbCD rc = s_rcd[wv][r];
+      if (done) continue;
       const double YB_prev = YB;
       const double Ystart = Ychi;
       bool use_guess = false;
       if (riccati && have && r != rz) {
+        // the predictor's 12 constants are read from the constant cache each step (scalar loads
+        // through an opaque pointer) instead of held in 24 SGPRs across the loop (LZQ_RIC_KRELOAD)
+        const __attribute__((address_space(4))) double* kp =
+            (const __attribute__((address_space(4))) double*)&kRadauPred[0][0];
+        if (LZQ_RIC_KRELOAD) asm volatile("" : "+s"(kp));
         double g[3];
         use_guess = true;
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-          g[j] = fma_s(Zs[2], kRadauPred[j][3], fma_s(Zs[1], kRadauPred[j][2],
-                                                      fma_s(Zs[0], kRadauPred[j][1], kRadauPred[j][0] * Yp)));
+          g[j] = fma_s(Zs[2], kp[4 * j + 3], fma_s(Zs[1], kp[4 * j + 2], fma_s(Zs[0], kp[4 * j + 1], kp[4 * j] * Yp)));
           use_guess = use_guess && fabs(g[j] - Ychi) <= 0.25 * fabs(Ychi);
         }
 #pragma unroll

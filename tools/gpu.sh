@@ -73,6 +73,11 @@ case "$cmd" in
     timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 \
       SQ_INSTS_VALU_CVT SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VALU_TRANS_F64 --output-format csv -d "$OUT/mix" -o run -- \
       python3 tools/ode_pmc_run.py > "$OUT/mix.jsonl" 2> "$OUT/mix.err" || { tail -5 "$OUT/mix.err"; exit 3; }
+    # where the wave cycles go (issue stalls vs parked vs issuing), and the clock: its own pass
+    timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+      SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv \
+      -d "$OUT/stall" -o run -- python3 tools/ode_pmc_run.py > "$OUT/stall.jsonl" 2> "$OUT/stall.err" \
+      || { tail -5 "$OUT/stall.err"; exit 4; }
     cat "$OUT/trace.jsonl"
     ;;
   prop-pmc)  # the bounce-profile propagation (tools/bench_profile.py): instruction mix per kernel + kernel trace;

@@ -54,6 +54,8 @@ def main_cases(src: str, tag: str, fname: str = "ode_pmc.json") -> None:
         return out
 
     big_p = passes("pmc")
+    # the optional stall pass (SQ_WAVE_CYCLES & co. count quad-cycles; GRBM_GUI_ACTIVE sums 8 XCDs)
+    stall = passes("stall") if os.path.exists(os.path.join(src, "stall", "run_counter_collection.csv")) else None
     # the optional third pass (integer / conversion / scalar / LDS instructions)
     mix = passes("mix") if os.path.exists(os.path.join(src, "mix", "run_counter_collection.csv")) else None
     tr = [r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv")))
@@ -95,6 +97,20 @@ def main_cases(src: str, tag: str, fname: str = "ode_pmc.json") -> None:
                 k.replace("SQ_INSTS_", "").lower(): m[k] / wm for k in
                 ("SQ_INSTS_VALU", "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64", "SQ_INSTS_VALU_CVT",
                  "SQ_INSTS_VALU_TRANS_F64", "SQ_INSTS_SALU", "SQ_INSTS_LDS") if k in m}
+        if stall:
+            m = stall[[n for n, _o, _s in CASES].index(name)]
+            wc = m.get("SQ_WAVE_CYCLES", 0.0)
+            out["configs"][name]["wave_cycles"] = {
+                "wait_any_frac": m.get("SQ_WAIT_ANY", 0.0) / wc if wc else None,
+                "wait_inst_any_frac": m.get("SQ_WAIT_INST_ANY", 0.0) / wc if wc else None,
+                "active_inst_any_frac": m.get("SQ_ACTIVE_INST_ANY", 0.0) / wc if wc else None,
+                "active_inst_valu_frac": m.get("SQ_ACTIVE_INST_VALU", 0.0) / wc if wc else None,
+                "active_inst_sca_frac": m.get("SQ_ACTIVE_INST_SCA", 0.0) / wc if wc else None,
+                "wave_quad_cycles_per_wave_step": wc / (m["SQ_WAVES"] * steps),
+                "note": "fractions of SQ_WAVE_CYCLES (summed over the launch's variants); WAIT_ANY = parked on "
+                        "s_waitcnt/barrier, WAIT_INST_ANY = issue stalls (dependency / pipe busy)"}
+            if m.get("GRBM_GUI_ACTIVE"):
+                out["configs"][name]["clock_ghz_grbm"] = m["GRBM_GUI_ACTIVE"] / 8.0 / t / 1e9
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
     with open(os.path.join(dst, fname), "w") as f:

@@ -16,7 +16,7 @@ CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.normpath(os.path.join(HERE, "..", "include"))
 BUILD_DIR = os.path.join(HERE, "_build")
 LIB_PATH = os.path.join(BUILD_DIR, "liblzq.so")
-SOURCES = ["lzq_kernels.hip", "lzq_aov.hip", "lzq_propagator.hip", "lzq_ode.hip", "lzq_profile.hip"]
+SOURCES = ["lzq_kernels.hip", "lzq_aov.hip", "lzq_propagator.hip", "lzq_ode.hip", "lzq_ode_tp.hip", "lzq_profile.hip"]
 # every header next to the sources (tests/test_engine_host.py checks each #include "..." of the
 # sources resolves to one of the build inputs)
 HEADERS = sorted(os.path.basename(h) for h in glob.glob(os.path.join(CSRC, "*.h")))

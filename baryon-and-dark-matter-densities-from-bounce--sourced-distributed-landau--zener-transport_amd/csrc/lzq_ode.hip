@@ -13,808 +13,15 @@
 //
 // The ingredients of rhs follow fpy:270-286 in the reference's operation order, with T**3 as
 // (T*T)*T and T**1.5 as T*sqrt(T) (<= 2 ulp from pow; the device pow is ~100 VALU).
-#include <hip/hip_runtime.h>
-
-#include <math.h>
-#include <stdio.h>
-
-#include <algorithm>
-#include <type_traits>
-
-#include "../../include/lzq.h"
-#include "lzq_exp2.h"
-#include "lzq_internal.h"
-#include "lzq_physics.h"
+//
+// The device helpers (per-point constants, stages, the Radau step) live in lzq_ode.h, shared with
+// lzq_ode_tp.hip (the time-parallel integration of a few points).
+#include "lzq_ode.h"
 
 namespace lzq {
-
-// ode_integrate_kernel: minimum waves per SIMD (its VGPR cap = 512 / this)
-#ifndef LZQ_ODE_MIN_WAVES
-#define LZQ_ODE_MIN_WAVES 2
-#endif
-constexpr int kOdeBlock = 256;
 int g_ode_coop = 1;          // lzq_tune(LZQ_TUNE_ODE_COOP)
 int g_ode_launch_log2 = 24;  // lzq_tune(LZQ_TUNE_ODE_LAUNCH_STEPS): <= 2^24 Radau steps per launch
 int g_ode_tp_interval = 64;  // lzq_tune(LZQ_TUNE_ODE_TP_INTERVAL): steps per lzq_ode_integrate_tp interval
-constexpr double kInvMplGeV = 1.0 / kMplGeV;
-
-// ---------------------------------------------------------------------------------------
-// per-point constants of rhs (one lane per point)
-// ---------------------------------------------------------------------------------------
-struct OdePoint {
-  double m, m3, Tp, B, sig, flux, P;
-  double H0;     // 1.66 sqrt(g*)                       fpy:85
-  double s0;     // (2 pi^2/45) g*s                      fpy:88
-  double c_rel;  // g 3 zeta3/(4 pi^2) | g zeta3/pi^2    fpy:96-99
-  double c_nr;   // g (m/2pi)^1.5                        fpy:104
-  double v0;     // pi max(m, 1e-20)                     fpy:117
-  double sigmav, gamma_w;
-  int deplete;
-  double T_lo, T_hi, stepT;
-  double inv_m, inv_sig, inv_v0, inv_stepT;  // reciprocals: ode_stage multiplies instead of dividing
-  double inv_s0, mpl_over_h0;                // 1/s0, M_Pl/H0 (1/s and 1/(H x) as products)
-  double Pf;                                 // P * flux: the source term's per-point scale
-};
-
-__device__ __forceinline__ void ode_point_recips(OdePoint& o) {
-  o.inv_m = 1.0 / o.m;
-  o.inv_sig = 1.0 / o.sig;
-  o.inv_v0 = 1.0 / o.v0;
-  o.inv_stepT = 1.0 / o.stepT;
-  o.inv_s0 = 1.0 / o.s0;
-  o.mpl_over_h0 = kMplGeV / o.H0;
-}
-
-__device__ __forceinline__ OdePoint ode_point(const lzq_point& pt, const lzq_ode_params& od) {
-  OdePoint o;
-  o.m = pt.m_chi_GeV;
-  o.m3 = pt.m_chi_GeV / 3.0;
-  o.Tp = pt.T_p_GeV;
-  o.B = pt.beta_over_H;
-  o.sig = pymax(pt.source_shape_sigma_y, 1e-6);
-  o.flux = pt.incident_flux_scale;
-  o.P = pt.P_chi_to_B;
-  o.Pf = o.P * o.flux;
-  o.H0 = 1.66 * sqrt(pt.g_star);
-  o.s0 = (2.0 * (kPi * kPi) / 45.0) * pt.g_star_s;
-  o.c_rel = (pt.stats == 0) ? pt.g_chi * (3.0 * kZeta3 / (4.0 * (kPi * kPi))) : pt.g_chi * (kZeta3 / (kPi * kPi));
-  o.c_nr = pt.g_chi * pow(pt.m_chi_GeV / (2.0 * kPi), 1.5);
-  o.v0 = kPi * pymax(pt.m_chi_GeV, 1e-20);
-  o.sigmav = pymax(od.sigma_v_chi_GeV_m2, 0.0);  // fpy:279
-  o.gamma_w = pymax(od.Gamma_wash_over_H, 0.0);  // fpy:284
-  o.deplete = od.deplete_DM_from_source != 0;
-  o.T_lo = pt.T_min_over_Tp * pt.T_p_GeV;         // fpy:369
-  o.T_hi = pt.T_max_over_Tp * pt.T_p_GeV;         // fpy:368
-  o.stepT = (o.T_hi - o.T_lo) / (double)(kOdeNT - 1);
-  ode_point_recips(o);
-  return o;
-}
-
-#ifndef LZQ_ODE_MIN_GROUP
-#define LZQ_ODE_MIN_GROUP 8  // smallest cooperative segment (64: whole wavefronts only, round 2)
-#endif
-#ifndef LZQ_ODE_PREDICT
-#define LZQ_ODE_PREDICT 1  // Radau5 collocation predictor for the Riccati Newton iteration
-#endif
-#ifndef LZQ_ODE_FASTMATH
-#define LZQ_ODE_FASTMATH 1  // 0: IEEE division and ROCm exp in the stage function (tools/ablate_ode.py);
-#endif
-#ifndef LZQ_ODE_COOP
-#define LZQ_ODE_COOP 1  // cooperative stage tables for group-uniform wavefronts (ode_integrate_kernel)
-#endif
-#ifndef LZQ_ODE_FMA
-#define LZQ_ODE_FMA LZQ_ODE_FASTMATH  // fused multiply-adds in the spline, the window exponent, Newton's f
-#endif
-
-// fpy:214-218 A_over_V_T: min(max(T, T_lo), T_hi), then the PPoly of scipy (_ppoly.pyx:
-// interval k with T_k <= T < T_{k+1}, T == T_hi in the last one; c3 + c2 s + c1 s^2 + c0 s^3
-// accumulated in that order, powers by repeated multiplication).  nt: the table's knot count
-// (the integrators read main()'s LZQ_ODE_NT tables; the operator kernel any build_tables n).
-// Split into the interval search, which depends on the point only through its window (shared by
-// the cooperative segments, whose points agree in it), and the cubic of one table.
-struct SplineLoc {
-  double s;  // T - T_k
-  int k;     // interval
-};
-
-__device__ __forceinline__ SplineLoc spline_loc(const OdePoint& o, double T, int nt = kOdeNT) {
-  const double Tq = pymin(pymax(T, o.T_lo), o.T_hi);
-  int k = (int)((Tq - o.T_lo) * o.inv_stepT);
-  k = k < 0 ? 0 : (k > nt - 2 ? nt - 2 : k);
-  // the quotient can land one knot off after rounding: settle against the knots themselves
-  if (Tq < linspace_at(o.T_lo, o.T_hi, o.stepT, k, nt) && k > 0) --k;
-  else if (k < nt - 2 && Tq >= linspace_at(o.T_lo, o.T_hi, o.stepT, k + 1, nt)) ++k;
-  return {Tq - linspace_at(o.T_lo, o.T_hi, o.stepT, k, nt), k};
-}
-
-// the cubic of one interval, c = (c0, c1, c2, c3) of the PPoly row
-__device__ __forceinline__ double spline_cubic(const double (&c)[4], double s) {
-  if (LZQ_ODE_FMA) return __builtin_fma(__builtin_fma(__builtin_fma(c[0], s, c[1]), s, c[2]), s, c[3]);  // Horner
-  double z = s, res = c[3];
-  res = res + c[2] * z;
-  z = z * s;
-  res = res + c[1] * z;
-  z = z * s;
-  res = res + c[0] * z;
-  return res;
-}
-
-__device__ __forceinline__ double spline_at(const double* __restrict__ w, double s, int k) {
-  const double* c = w + 4 * k;
-  const double cc[4] = {c[0], c[1], c[2], c[3]};
-  return spline_cubic(cc, s);
-}
-
-__device__ __forceinline__ double spline_eval(const OdePoint& o, const double* __restrict__ w, double T,
-                                              int nt = kOdeNT) {
-  const SplineLoc l = spline_loc(o, T, nt);
-  return spline_at(w, l.s, l.k);
-}
-
-
-// 1/x for a positive normal x: v_rcp_f64 + two Newton steps (5 VALU; <= 1 ulp from the
-// correctly rounded quotient, which costs ~10).
-__device__ __forceinline__ double rcp_pos(double x) {
-  if (!LZQ_ODE_FASTMATH) return 1.0 / x;
-  double r = __builtin_amdgcn_rcp(x);
-  double e = __builtin_fma(-x, r, 1.0);
-  r = __builtin_fma(r, e, r);
-  e = __builtin_fma(-x, r, 1.0);
-  return __builtin_fma(r, e, r);
-}
-
-// exp(v) for v <= 0 as 2^(v log2 e) with the degree-11 exp2 of lzq_exp2.h (0.63 ulp on the
-// reduced argument; the one rounding of v log2 e costs |v| 2^-53 relative, < 1e-13 for
-// |v| < 700, where the factor is still > 1e-304).  ~16 VALU against ~22 for ROCm's exp.
-__device__ __forceinline__ double exp_nonpos(double v) {
-  if (!LZQ_ODE_FASTMATH) return exp(v);
-  return exp2_nonpos(v * kLog2E, 1.0);
-}
-
-// The ingredients of rhs(x, .) (fpy:270-286), which do not depend on Y:
-//   dY_chi/dx = -lam (Y_chi^2 - E2) - S        lam = sigmav s/(H x), E2 = (n_eq/s)^2,
-//                                               S = (deplete ? SB/s : 0)/(H x)
-//   dY_B/dx   = alpha - beta Y_B               alpha = (SB/s)/(H x), beta = (gamma_w H)/(H x)
-struct OdeStage {
-  double lam, E2, S, alpha, beta;
-  double a;  // alpha per unit P * flux (the Y_B recurrence forms P * flux * (its coefficient of a))
-};
-
-// The same with the per-point scalars factored out: alpha (and S) per unit P * flux, lam per
-// unit sigma_v, beta per unit gamma_w.  Points that differ only in those scalars (and in their
-// initial state) share these values -- the cooperative mode of ode_integrate_kernel computes
-// them once per step for a whole wavefront.  Every stage goes through this split, so a point's
-// result does not depend on which mode its wavefront ran in.  a = Av * ap: the A/V spline value
-// times the rest of the source term, so points that differ also in the A/V kernel (I_p, v_w: their
-// own spline tables) share ap and the spline location (s, k) and form a from their own table.
-struct StageBase {
-  double a, lam, E2, beta;
-  double ap;  // a / Av
-  double s;   // spline location of the stage's T (spline_loc)
-  int k;
-};
-
-__device__ __forceinline__ StageBase ode_stage_base(const OdePoint& o, const double* __restrict__ w, double x,
-                                                    double* Av_out = nullptr, int nt = kOdeNT) {
-  // One division per call (1/x); every other quotient of fpy:270-286 is a product with a
-  // per-point reciprocal or with powers of 1/T: 1/s = (1/T)^3 / s0 and 1/(H x) =
-  // (M_Pl/H0) (1/T)^2 / x, exact rewrites of s = s0 T^3 and H = H0 T^2 / M_Pl (fpy:85, 88)
-  // wherever the max(., 1e-300) guards are inactive (T > 1e-30 GeV: always on the ODE window;
-  // the guarded branch divides).  Each product differs from the quotient by a few ulp, far
-  // inside the 1e-11 oracle gate (tests/test_gpu_ode.py).
-  const double xc = pymax(x, 1e-30);
-  const double ixc = rcp_pos(xc);
-  const double T = o.m * ixc;                                 // fpy:272  m / max(x, 1e-30)
-  const double iT = T >= 1e-30 ? xc * o.inv_m : 1e30;         // 1 / max(T, 1e-30)
-  const double H = pymax(o.H0 * T * T * kInvMplGeV, 1e-300);  // fpy:273 via fpy:85
-  const double T3 = (T * T) * T;
-  const double s = pymax(o.s0 * T3, 1e-300);                  // fpy:274 via fpy:88
-  const double qT = o.Tp * iT;                                // fpy:275 y_of_T (fpy:126-128)
-  const double y = 0.5 * o.B * (LZQ_ODE_FMA ? __builtin_fma(qT, qT, -1.0) : qT * qT - 1.0);
-  const double q = y * o.inv_sig;
-  const double window = exp_nonpos(-0.5 * (q * q));           // fpy:276
-  double n_eq, vbar;                                          // fpy:90-120
-  if (T > o.m3) {
-    n_eq = o.c_rel * T3;
-    vbar = 1.0;
-  } else {
-    n_eq = o.c_nr * (T * sqrt(T)) * exp_nonpos(-o.m * iT);
-    vbar = sqrt(pymax(8.0 * T * o.inv_v0, 0.0));
-  }
-  const double Jb = 0.25 * n_eq * vbar;                       // fpy:222-223, J / flux
-  const SplineLoc loc = spline_loc(o, T, nt);
-  const double Av = spline_at(w, loc.s, loc.k);               // fpy:214-218
-  if (Av_out) *Av_out = Av;
-  const double SBb = Jb * window;                             // fpy:277, SB / (P flux Av)
-  const bool plain = H > 1e-290 && s > 1e-290 && x == xc;     // the max() guards are inactive
-  const double iT2 = iT * iT;
-  const double is = plain ? (iT2 * iT) * o.inv_s0 : 1.0 / s;
-  const double E = n_eq * is;                                 // fpy:280
-  const double iHx = plain ? (o.mpl_over_h0 * iT2) * ixc : 1.0 / (H * x);
-  StageBase b;
-  b.ap = (SBb * is) * iHx;
-  b.a = Av * b.ap;                                            // fpy:282, 285
-  b.s = loc.s;
-  b.k = loc.k;
-  b.lam = s * iHx;                                            // fpy:279-281
-  b.E2 = E * E;
-  b.beta = H * iHx;                                           // fpy:284-285
-  return b;
-}
-
-__device__ __forceinline__ OdeStage stage_scale(const OdePoint& o, const StageBase& b) {
-  OdeStage st;
-  st.alpha = o.Pf * b.a;
-  st.S = o.deplete ? st.alpha : 0.0;
-  st.lam = o.sigmav * b.lam;
-  st.E2 = b.E2;
-  st.beta = o.gamma_w * b.beta;
-  st.a = b.a;
-  return st;
-}
-
-__device__ __forceinline__ OdeStage ode_stage(const OdePoint& o, const double* __restrict__ w, double x,
-                                              double* Av_out = nullptr, int nt = kOdeNT) {
-  return stage_scale(o, ode_stage_base(o, w, x, Av_out, nt));
-}
-
-// The Y_chi-only stage of the Riccati equation with no source term (deplete off):
-// lam = sigma_v s/(H x), E2 = (n_eq/s)^2, S = 0 -- no spline, no window (ode_stage's
-// operations otherwise).  alpha / beta are not formed (Y_B comes from the quadrature).  Split
-// like ode_stage into a shared base (lam per unit sigma_v, E2) and the per-point product.
-__device__ __forceinline__ StageBase ode_stage_chi_base(const OdePoint& o, double x) {
-  const double xc = pymax(x, 1e-30);
-  const double ixc = rcp_pos(xc);
-  const double T = o.m * ixc;
-  const double iT = T >= 1e-30 ? xc * o.inv_m : 1e30;
-  const double H = pymax(o.H0 * T * T * kInvMplGeV, 1e-300);
-  const double T3 = (T * T) * T;
-  const double s = pymax(o.s0 * T3, 1e-300);
-  double n_eq;
-  if (T > o.m3) n_eq = o.c_rel * T3;
-  else n_eq = o.c_nr * (T * sqrt(T)) * exp_nonpos(-o.m * iT);
-  const bool plain = H > 1e-290 && s > 1e-290 && x == xc;
-  const double iT2 = iT * iT;
-  const double is = plain ? (iT2 * iT) * o.inv_s0 : 1.0 / s;
-  const double E = n_eq * is;
-  const double iHx = plain ? (o.mpl_over_h0 * iT2) * ixc : 1.0 / (H * x);
-  StageBase b;
-  b.a = 0.0;
-  b.ap = 0.0;
-  b.s = 0.0;
-  b.k = 0;
-  b.lam = s * iHx;
-  b.E2 = E * E;
-  b.beta = 0.0;
-  return b;
-}
-
-__device__ __forceinline__ OdeStage chi_scale(const OdePoint& o, const StageBase& b) {
-  OdeStage st;
-  st.lam = o.sigmav * b.lam;
-  st.E2 = b.E2;
-  st.S = 0.0;
-  st.alpha = 0.0;
-  st.beta = 0.0;
-  st.a = 0.0;
-  return st;
-}
-
-__device__ __forceinline__ OdeStage ode_stage_chi(const OdePoint& o, double x) {
-  return chi_scale(o, ode_stage_chi_base(o, x));
-}
-
-// CubicSpline's check of the knots linspace(T_lo, T_hi, nt): strictly increasing.
-__device__ __forceinline__ bool ode_grid_ok(double T_lo, double T_hi, double stepT, int nt = kOdeNT) {
-  bool ok = true;
-  double prev = linspace_at(T_lo, T_hi, stepT, 0, nt);
-  for (int k = 1; k < nt; ++k) {
-    const double xk = linspace_at(T_lo, T_hi, stepT, k, nt);
-    ok = ok && (xk > prev);
-    prev = xk;
-  }
-  return ok;
-}
-
-// The integrators read tables of kOdeNT knots at a fixed stride: ode_spline_kernel records the
-// table's knot count in its last 4 doubles (spare: the cubics use 4 (nt - 1)), and a table built
-// for another nt (lzq_ode_tables takes any) is refused per point instead of read as wrong rows.
-__device__ __forceinline__ bool ode_table_ok(const double* __restrict__ w) { return w[kOdeWS - 4] == (double)kOdeNT; }
-
-// Radau IIA, 3 stages (the method of scipy's Radau): nodes C, matrix A (row 3 = weights).
-struct Radau {
-  double c[3], a[3][3];
-};
-
-__device__ __forceinline__ Radau radau_tableau() {
-  Radau r;
-  const double s6 = sqrt(6.0);
-  r.c[0] = (4.0 - s6) / 10.0;
-  r.c[1] = (4.0 + s6) / 10.0;
-  r.c[2] = 1.0;
-  r.a[0][0] = (88.0 - 7.0 * s6) / 360.0;
-  r.a[0][1] = (296.0 - 169.0 * s6) / 1800.0;
-  r.a[0][2] = (-2.0 + 3.0 * s6) / 225.0;
-  r.a[1][0] = (296.0 + 169.0 * s6) / 1800.0;
-  r.a[1][1] = (88.0 + 7.0 * s6) / 360.0;
-  r.a[1][2] = (-2.0 - 3.0 * s6) / 225.0;
-  r.a[2][0] = (16.0 - s6) / 36.0;
-  r.a[2][1] = (16.0 + s6) / 36.0;
-  r.a[2][2] = 1.0 / 9.0;
-  return r;
-}
-
-// The Newton start of a block's first step (LZQ_ODE_PRED_BLOCK), from Y_chi and the step's stages
-// alone: per stage one linearised backward-Euler step over c_j h,
-//   Z_j = Y0 + c_j h f_j(Y0) / (1 + 2 c_j h lam_j Y0),   f_j = -lam_j (Y0^2 - E2_j) - S_j,
-// between E and Y0 where the stage relaxes (annihilation), ~Y0 + c_j h f where it does not -- so a
-// stiff step converges in the peeled iterations as it does from the predictor, and the start stays
-// history-free (the block's end a function of its start: lzq_ode_integrate_tp's exact stitching).
-// false (start from Y0) for a non-finite guess or a sign change of a positive Y0.  Every integrator
-// calls it with the same operands.
-__device__ __forceinline__ bool block_guess(const Radau& R, double h, const OdeStage (&sg)[3], double Y0,
-                                            double (&Z)[3]) {
-  bool ok = true;
-  double g[3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const double ch = (j == 0 ? R.c[0] : (j == 1 ? R.c[1] : R.c[2])) * h;  // (no dynamic index: scratch)
-    const double f = -sg[j].lam * (Y0 * Y0 - sg[j].E2) - sg[j].S;
-    const double den = 1.0 + 2.0 * (ch * sg[j].lam) * Y0;  // >= 1 for Y0 >= 0
-    g[j] = Y0 + ch * f * rcp_pos(den);
-    ok = ok && den > 0.0 && isfinite(g[j]) && (!(Y0 > 0.0) || g[j] > 0.0);
-  }
-  if (ok) {
-#pragma unroll
-    for (int j = 0; j < 3; ++j) Z[j] = g[j];
-  }
-  return ok;
-}
-
-// x = M^-1 b for the 3x3 stage matrices M = I + h A diag(d) (partial pivoting; branch-free
-// selects, so the lanes of a wave stay converged).
-__device__ __forceinline__ void solve3(double M[3][3], double b[3]) {
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-#pragma unroll
-    for (int r = c + 1; r < 3; ++r) {
-      const bool sw = fabs(M[r][c]) > fabs(M[c][c]);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const double t = M[c][k];
-        M[c][k] = sw ? M[r][k] : t;
-        M[r][k] = sw ? t : M[r][k];
-      }
-      const double t = b[c];
-      b[c] = sw ? b[r] : t;
-      b[r] = sw ? t : b[r];
-    }
-#pragma unroll
-    for (int r = c + 1; r < 3; ++r) {
-      const double f = M[r][c] / M[c][c];
-#pragma unroll
-      for (int k = c; k < 3; ++k) M[r][k] = M[r][k] - f * M[c][k];
-      b[r] = b[r] - f * b[c];
-    }
-  }
-#pragma unroll
-  for (int c = 2; c >= 0; --c) {
-    double acc = b[c];
-#pragma unroll
-    for (int k = c + 1; k < 3; ++k) acc = acc - M[c][k] * b[k];
-    b[c] = acc / M[c][c];
-  }
-}
-
-// z[2] of M z = b by Cramer's rule (one division): the Y_B stage system needs only the last
-// stage.  M = I + h A diag(beta), beta >= 0, is well conditioned for every h (A of Radau IIA
-// has eigenvalues in the right half plane), so the cofactor form loses nothing against the
-// pivoted elimination of solve3 (tests/test_gpu_ode.py: oracle at 1e-11).
-__device__ __forceinline__ double solve3_last(const double (&M)[3][3], const double (&b)[3]) {
-  const double c0 = M[1][0] * M[2][1] - M[1][1] * M[2][0];
-  const double det = M[0][0] * (M[1][1] * M[2][2] - M[1][2] * M[2][1]) -
-                     M[0][1] * (M[1][0] * M[2][2] - M[1][2] * M[2][0]) + M[0][2] * c0;
-  const double num = M[0][0] * (M[1][1] * b[2] - b[1] * M[2][1]) - M[0][1] * (M[1][0] * b[2] - b[1] * M[2][0]) +
-                     b[0] * c0;
-  return num / det;
-}
-
-// h * a_ij of the Radau matrix for one step size (formed once per step size, not per step), and h.
-struct RadauH {
-  double a[3][3];
-  double h;
-};
-
-__device__ __forceinline__ RadauH radau_h(const Radau& R, double h) {
-  RadauH r;
-  r.h = h;
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) r.a[i][j] = h * R.a[i][j];
-  return r;
-}
-
-// x = M^-1 b by the adjugate (one division for all three components), for the Newton stage
-// systems M = I - hA diag(jf) of the Riccati equation: well conditioned like the Y_B system
-// (jf = -2 lam Z <= 0 near the solution), so the cofactor form loses nothing against pivoted
-// elimination (tests/test_gpu_ode.py: oracle at 1e-11, stiff cases at 1e-10 of converged).
-#ifndef LZQ_ODE_ADJFMA
-#define LZQ_ODE_ADJFMA 1  // the adjugate, determinant and products as explicit fmas (the file builds with -ffp-contract=off)
-#endif
-struct Adj3 {
-  double a[3][3];  // adjugate of M
-  double id;       // 1 / det M
-};
-__device__ __forceinline__ Adj3 adj3(const double (&M)[3][3]) {
-  Adj3 r;
-  if (LZQ_ODE_ADJFMA) {
-#define FMA __builtin_fma
-    r.a[0][0] = FMA(M[1][1], M[2][2], -(M[1][2] * M[2][1]));
-    r.a[0][1] = FMA(M[0][2], M[2][1], -(M[0][1] * M[2][2]));
-    r.a[0][2] = FMA(M[0][1], M[1][2], -(M[0][2] * M[1][1]));
-    r.a[1][0] = FMA(M[1][2], M[2][0], -(M[1][0] * M[2][2]));
-    r.a[1][1] = FMA(M[0][0], M[2][2], -(M[0][2] * M[2][0]));
-    r.a[1][2] = FMA(M[0][2], M[1][0], -(M[0][0] * M[1][2]));
-    r.a[2][0] = FMA(M[1][0], M[2][1], -(M[1][1] * M[2][0]));
-    r.a[2][1] = FMA(M[0][1], M[2][0], -(M[0][0] * M[2][1]));
-    r.a[2][2] = FMA(M[0][0], M[1][1], -(M[0][1] * M[1][0]));
-    r.id = 1.0 / FMA(M[0][0], r.a[0][0], FMA(M[0][1], r.a[1][0], M[0][2] * r.a[2][0]));
-#undef FMA
-  } else {
-    r.a[0][0] = M[1][1] * M[2][2] - M[1][2] * M[2][1];
-    r.a[0][1] = M[0][2] * M[2][1] - M[0][1] * M[2][2];
-    r.a[0][2] = M[0][1] * M[1][2] - M[0][2] * M[1][1];
-    r.a[1][0] = M[1][2] * M[2][0] - M[1][0] * M[2][2];
-    r.a[1][1] = M[0][0] * M[2][2] - M[0][2] * M[2][0];
-    r.a[1][2] = M[0][2] * M[1][0] - M[0][0] * M[1][2];
-    r.a[2][0] = M[1][0] * M[2][1] - M[1][1] * M[2][0];
-    r.a[2][1] = M[0][1] * M[2][0] - M[0][0] * M[2][1];
-    r.a[2][2] = M[0][0] * M[1][1] - M[0][1] * M[1][0];
-    r.id = 1.0 / (M[0][0] * r.a[0][0] + M[0][1] * r.a[1][0] + M[0][2] * r.a[2][0]);
-  }
-  return r;
-}
-__device__ __forceinline__ void adj3_apply(const Adj3& A, double (&b)[3]) {
-  double x[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-    x[i] = LZQ_ODE_ADJFMA ? __builtin_fma(A.a[i][0], b[0], __builtin_fma(A.a[i][1], b[1], A.a[i][2] * b[2])) * A.id
-                          : (A.a[i][0] * b[0] + A.a[i][1] * b[1] + A.a[i][2] * b[2]) * A.id;
-  b[0] = x[0];
-  b[1] = x[1];
-  b[2] = x[2];
-}
-__device__ __forceinline__ void solve3_adj(const double (&M)[3][3], double (&b)[3]) { adj3_apply(adj3(M), b); }
-
-// Y_B's Radau step as an affine map (LZQ_ODE_YBREC): the stage system (I + hA diag(beta)) Z =
-// Y_B 1 + hA alpha, alpha_j = P flux a_j, gives by Cramer's rule Z_3 = c Y_B + P flux d with
-// c = (w0 + w1 + w2)/det and d = sum_j (sum_i w_i hA_ij) a_j / det, w_i the cofactors of the last
-// column's numerator (solve3_last's).  c and d depend on the point only through Gamma_wash (beta)
-// and the stage bases, so a cooperative segment with one Gamma_wash forms them once per step
-// for all its lanes; every mode forms them with these operations, so the result does not depend
-// on the mode.
-struct YbW {
-  double W[3], id;  // d = (sum_j W_j a_j) id: a lane whose a_j differ from the segment's forms its own d (yb_d)
-};
-struct YbCD {
-  double c, d;
-};
-struct YbRec {
-  double c, d;
-  double W[3], id;
-};
-__device__ __forceinline__ double yb_d(const YbW& r, const double (&a)[3]) {
-  double d = 0.0;
-#pragma unroll
-  for (int j = 0; j < 3; ++j) d = __builtin_fma(r.W[j], a[j], d);
-  return d * r.id;
-}
-__device__ __forceinline__ YbRec yb_rec(const RadauH& hA, const double (&beta)[3], const double (&a)[3]) {
-  double M[3][3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) M[i][j] = __builtin_fma(hA.a[i][j], beta[j], i == j ? 1.0 : 0.0);
-  const double w0 = M[1][0] * M[2][1] - M[1][1] * M[2][0];
-  const double w1 = M[0][1] * M[2][0] - M[0][0] * M[2][1];
-  const double w2 = M[0][0] * M[1][1] - M[0][1] * M[1][0];
-  const double det = M[0][0] * (M[1][1] * M[2][2] - M[1][2] * M[2][1]) -
-                     M[0][1] * (M[1][0] * M[2][2] - M[1][2] * M[2][0]) + M[0][2] * w0;
-  YbRec r;
-  r.id = 1.0 / det;
-#pragma unroll
-  for (int j = 0; j < 3; ++j) r.W[j] = __builtin_fma(w2, hA.a[2][j], __builtin_fma(w1, hA.a[1][j], w0 * hA.a[0][j]));
-  r.c = ((w0 + w1) + w2) * r.id;
-  r.d = yb_d(YbW{{r.W[0], r.W[1], r.W[2]}, r.id}, a);
-  return r;
-}
-__device__ __forceinline__ YbRec yb_rec(const RadauH& hA, const OdeStage (&st)[3]) {
-  const double beta[3] = {st[0].beta, st[1].beta, st[2].beta}, a[3] = {st[0].a, st[1].a, st[2].a};
-  return yb_rec(hA, beta, a);
-}
-
-// One Radau step for both equations (hA = h * A of the step); false when the Y_chi Newton
-// iteration fails.  The stage sums are explicit fmas (hA_ij * f_j + acc); only the last stage
-// of each equation is the step's result, so the linear cases form only what they need.
-// Newton starting values for the next step's Riccati stages: the previous step's collocation
-// polynomial (through Y at its start and its three stage values, nodes 0, c1, c2, 1) evaluated
-// at 1 + c_j (Lagrange weights, mpmath): the standard Radau5 predictor.
-__constant__ double kRadauPred[3][4] = {
-    {-0x1.94f343c8b1118p-1, 0x1.6c62e7ee47cd1p+0, -0x1.98b0a4fff4ae1p+0, 0x1.f6c75ef60569bp+0},
-    {-0x1.337d989041bbbp+3, 0x1.0879f93eee39dp+4, -0x1.c2e1b2531e4efp+3, 0x1.056b586583971p+3},
-    {-0x1.9000000000000p+4, 0x1.51cdd7dde1522p+5, -0x1.07232d3336a77p+5, 0x1.0aaaaaaaaaaabp+4}};
-
-// A^-1 of the Radau IIA matrix (mpmath, rounded once) and the products of its off-diagonal pairs
-// that the transformed Newton system's adjugate needs (LZQ_ODE_TNEWTON):
-// [a12 a21, a02 a21, a01 a12, a12 a20, a02 a20, a02 a10, a10 a21, a01 a20, a01 a10].
-__constant__ double kRadauAinv[3][3] = {
-    {0x1.9cc470a049097p+1, 0x1.2af7915ab4027p+0, -0x1.034624ce046cap-2},
-    {-0x1.c8aefbe08d347p+1, 0x1.8cee3d7edbda3p-1, 0x1.0d9e56004de7fp+0},
-    {0x1.620bd700c2c3ep+2, -0x1.e20bd700c2c3ep+2, 0x1.4000000000000p+2}};
-__constant__ double kRadauAinvP[9] = {-0x1.fbb0962b0c0cap+2, 0x1.e8360f1027593p+0, 0x1.3adf0cf78af17p+0,
-                                      0x1.74e16b2ae518ap+2,  -0x1.6692fca92522fp+0, 0x1.ce862a552e616p-1,
-                                      0x1.adf74aa6f6bf3p+4,  0x1.9d782ab97a58ap+2,  -0x1.0aaaaaaaaaaabp+2};
-// fma(z, a, c) with the constant a as the SGPR operand, three-address (no copy of the addend)
-__device__ __forceinline__ double fma_s(double z, double a, double c) {
-  double r;
-  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(z), "s"(a), "v"(c));
-  return r;
-}
-
-// fma(k, -a, p) for two constants a, p: a (wave-uniform) as the one SGPR operand with its negate
-// modifier, p in a VGPR, three-address.  Written as __builtin_fma the compiler picks v_fmac_f64,
-// which overwrites its addend, and copies p into the destination first (a v_mov_b64 per entry per
-// Newton iteration); the value is the same fma.
-__device__ __forceinline__ double fma_neg_s(double k, double a, double p) {
-  double r;
-  asm("v_fma_f64 %0, %1, -%2, %3" : "=v"(r) : "v"(k), "s"(a), "v"(p));
-  return r;
-}
-
-#ifndef LZQ_ODE_TNEWTON
-#define LZQ_ODE_TNEWTON 1  // the Riccati Newton iteration in the transformed form (constant off-diagonals)
-#endif
-#ifndef LZQ_ODE_NEWTON_RCP
-#define LZQ_ODE_NEWTON_RCP 1  // the Newton solve's 1/det by rcp_pos (5 VALU) instead of the IEEE quotient (~14)
-#endif
-
-// Zs: in, Newton starting stages when `guess` (else Ychi for all three); out, the converged
-// stages (the next predictor's data).  A predicted start that does not converge is retried
-// from Ychi, so the predictor can only save iterations, never lose a step.
-#ifndef LZQ_ODE_PEEL
-#define LZQ_ODE_PEEL 1  // the first two Newton iterations (and the Y_B solve) as one straight-line block
-#endif
-#ifndef LZQ_ODE_NEWTON2
-#define LZQ_ODE_NEWTON2 1  // the peeled pair of Newton iterations always both applied (no iterate selects)
-#endif
-#ifndef LZQ_ODE_SIMPLIFIED
-#define LZQ_ODE_SIMPLIFIED 1  // the peeled pair's second iteration reuses the first one's adjugate and 1/det
-#endif
-#ifndef LZQ_ODE_KD
-#define LZQ_ODE_KD 1  // the step index as a carried exact double (no 64-bit integer conversion per step)
-#endif
-#ifndef LZQ_ODE_NOSPLITVAR
-#define LZQ_ODE_NOSPLITVAR 1  // waves with no split step in the launch run an integrator variant without the split paths
-#endif
-#ifndef LZQ_ODE_LINFAST
-#define LZQ_ODE_LINFAST 1  // one fma per regular step on linear cooperative waves (sigma_v = 0, no depletion)
-#endif
-#ifndef LZQ_ODE_YBREC
-#define LZQ_ODE_YBREC 1  // Y_B by its affine step map (yb_rec), shared per cooperative segment
-#endif
-#ifndef LZQ_ODE_RICVAR
-#define LZQ_ODE_RICVAR 1  // whole-wave cooperative split-free waves run ode_riccati_kernel (compact rows, uniform constants)
-#endif
-#ifndef LZQ_ODE_PRED_BLOCK
-// The Radau5 predictor is not used on steps k = 0 (mod LZQ_ODE_PRED_BLOCK): every block of that
-// many steps starts its Newton iteration from Y_chi, so a block's end state is a function of its
-// start (Y_chi, Y_B) alone -- what lzq_ode_integrate_tp's exact stitching needs.  Every integrator
-// applies the rule on the absolute step index, so all modes stay bit-identical.  (A power of two.)
-#define LZQ_ODE_PRED_BLOCK 64
-#endif
-
-__device__ __forceinline__ bool pred_step(int64_t k) { return (k & (LZQ_ODE_PRED_BLOCK - 1)) != 0; }
-#ifndef LZQ_RIC_MIN_WAVES
-#define LZQ_RIC_MIN_WAVES 4  // ode_riccati_kernel: minimum waves per SIMD (its VGPR cap = 512 / this)
-#endif
-
-template <bool kWithYB = true>
-__device__ __forceinline__ bool radau_step(const RadauH& hA, const OdeStage (&st)[3], double& Ychi, double& YB,
-                                           double (&Zs)[3], bool guess) {
-  // Y_B: (I + hA diag(beta)) Z = YB + hA alpha, exactly; Z_3 = Y_B(x + h)
-  auto yb_step = [&]() {
-    double M[3][3], b[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      double acc = YB;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        acc = __builtin_fma(hA.a[i][j], st[j].alpha, acc);
-        M[i][j] = __builtin_fma(hA.a[i][j], st[j].beta, i == j ? 1.0 : 0.0);
-      }
-      b[i] = acc;
-    }
-    return solve3_last(M, b);
-  };
-  // Y_chi: Z_i = Y + h sum_j a_ij f_j(Z_j), f_j(Z) = -lam_j (Z^2 - E2_j) - S_j; one Newton
-  // iteration on Z, true when its correction is below 1e-15 of the stages
-  const double Y0 = Ychi;
-#if LZQ_ODE_TNEWTON && LZQ_ODE_FASTMATH
-  // Transformed Newton system: (I - hA diag(jf)) g = -(Z - Y0 - hA f) times h (hA)^-1 is
-  //   (A^-1 - diag(h jf)) g = h f - A^-1 (Z - Y0),
-  // whose matrix keeps A^-1's constant off-diagonals (kRadauAinv) and changes only on the diagonal,
-  // A^-1_jj + 2 h lam_j Z_j: its adjugate is one fma per entry against constant products
-  // (kRadauAinvP), and the h-scaled stage data h lam_j, 2 h lam_j, h S_j are formed once per step.
-  // Same fixed point (the stage equations), ~20 FP64 instructions fewer per iteration than
-  // forming I - hA diag(jf) and its full adjugate.
-  double hl[3], hl2[3], hS[3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    hl[j] = hA.h * st[j].lam;
-    hl2[j] = 2.0 * hl[j];
-    hS[j] = hA.h * st[j].S;
-  }
-  // the iteration matrix's adjugate and 1/det, kept for a simplified iteration (LZQ_ODE_SIMPLIFIED)
-  struct NewtonJ {
-    double b[3][3], id;
-  };
-  auto newton_j = [&](double (&Z)[3], NewtonJ& J, const bool reuse, bool& near) {
-#define FMA __builtin_fma
-    double d[3], r[3], k[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      r[j] = FMA(-hl[j], FMA(Z[j], Z[j], -st[j].E2), -hS[j]);  // h f_j
-      d[j] = Z[j] - Y0;
-      k[j] = FMA(hl2[j], Z[j], kRadauAinv[j][j]);              // A^-1_jj - h jf_j
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-      r[i] = FMA(-kRadauAinv[i][2], d[2], FMA(-kRadauAinv[i][1], d[1], FMA(-kRadauAinv[i][0], d[0], r[i])));
-    if (!reuse) {
-      // adjugate of [[k0, a01, a02], [a10, k1, a12], [a20, a21, k2]] (a_ij = A^-1_ij, products constant)
-      J.b[0][0] = FMA(k[1], k[2], -kRadauAinvP[0]), J.b[0][1] = fma_neg_s(k[2], kRadauAinv[0][1], kRadauAinvP[1]);
-      J.b[0][2] = fma_neg_s(k[1], kRadauAinv[0][2], kRadauAinvP[2]), J.b[1][0] = fma_neg_s(k[2], kRadauAinv[1][0], kRadauAinvP[3]);
-      J.b[1][1] = FMA(k[0], k[2], -kRadauAinvP[4]), J.b[1][2] = fma_neg_s(k[0], kRadauAinv[1][2], kRadauAinvP[5]);
-      J.b[2][0] = fma_neg_s(k[1], kRadauAinv[2][0], kRadauAinvP[6]), J.b[2][1] = fma_neg_s(k[0], kRadauAinv[2][1], kRadauAinvP[7]);
-      J.b[2][2] = FMA(k[0], k[1], -kRadauAinvP[8]);
-      // 1/det only scales the correction: a reciprocal within 1 ulp leaves the fixed point (the
-      // stage equations) as it is and changes the iterates by rounding
-      const double den = FMA(k[0], J.b[0][0], FMA(kRadauAinv[0][1], J.b[1][0], kRadauAinv[0][2] * J.b[2][0]));
-      J.id = LZQ_ODE_NEWTON_RCP ? rcp_pos(den) : 1.0 / den;
-    }
-    double g[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) g[i] = FMA(J.b[i][0], r[0], FMA(J.b[i][1], r[1], J.b[i][2] * r[2])) * J.id;
-#undef FMA
-    // running maxima from +0 of |.| (never NaN on the left): fmax is pymax here, one v_max_f64
-    double dmax = 0.0, zmax = 0.0;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      Z[i] = Z[i] + g[i];
-      dmax = fmax(dmax, fabs(g[i]));
-      zmax = fmax(zmax, fabs(Z[i]));
-    }
-    near = !(dmax > 1e-3 * zmax);
-    return !(dmax > 1e-15 * zmax);
-  };
-  NewtonJ J;
-  bool near = false;
-  auto newton = [&](double (&Z)[3]) { return newton_j(Z, J, false, near); };
-#else
-  auto newton = [&](double (&Z)[3]) {
-    double M[3][3], g[3];
-    double f[3], jf[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      f[j] = LZQ_ODE_FMA ? __builtin_fma(-st[j].lam, __builtin_fma(Z[j], Z[j], -st[j].E2), -st[j].S)
-                         : -st[j].lam * (Z[j] * Z[j] - st[j].E2) - st[j].S;
-      jf[j] = -st[j].lam * (2.0 * Z[j]);
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      double acc = Z[i] - Y0;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        acc = __builtin_fma(-hA.a[i][j], f[j], acc);
-        M[i][j] = __builtin_fma(-hA.a[i][j], jf[j], i == j ? 1.0 : 0.0);
-      }
-      g[i] = -acc;
-    }
-#if LZQ_ODE_FASTMATH
-    solve3_adj(M, g);
-#else
-    solve3(M, g);
-#endif
-    double dmax = 0.0, zmax = 0.0;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      Z[i] = Z[i] + g[i];
-      dmax = fmax(dmax, fabs(g[i]));
-      zmax = fmax(zmax, fabs(Z[i]));
-    }
-    return !(dmax > 1e-15 * zmax);
-  };
-#endif
-  auto accept = [&](const double (&Z)[3]) {
-    Zs[0] = Z[0];
-    Zs[1] = Z[1];
-    Zs[2] = Z[2];
-    Ychi = Z[2];
-  };
-  const bool nonlinear = st[0].lam != 0.0 || st[1].lam != 0.0 || st[2].lam != 0.0;
-  if (!nonlinear) {  // f_j = -S_j: Z_3 = Y - sum_j hA_3j S_j
-    if (kWithYB) YB = yb_step();
-    double acc = Ychi;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) acc = __builtin_fma(-hA.a[2][j], st[j].S, acc);
-    Ychi = acc;
-    return true;
-  }
-  for (int attempt = guess ? 0 : 1; attempt < 2; ++attempt) {
-    double Z[3] = {attempt == 0 ? Zs[0] : Y0, attempt == 0 ? Zs[1] : Y0, attempt == 0 ? Zs[2] : Y0};
-    int it = 0;
-#if LZQ_ODE_PEEL
-    if (attempt == (guess ? 0 : 1)) {
-      // the first two iterations (and Y_B's independent solve) in one basic block, so the
-      // scheduler interleaves their dependent chains; the second is applied only if the first
-      // did not converge -- the same iterates as the loop below, bit for bit
-      if (kWithYB) YB = yb_step();
-#if LZQ_ODE_NEWTON2
-      // both iterations always apply: a step that converged at the first takes the second's
-      // (below 1e-15 relative) correction too, so no selects between the two iterates are needed
-      const bool c1 = newton(Z);
-#if LZQ_ODE_SIMPLIFIED && LZQ_ODE_TNEWTON && LZQ_ODE_FASTMATH
-      // Once the first correction is below 1e-3 of the stages (the predicted start, almost every
-      // step), the second iteration reuses the first one's matrix (simplified Newton): its
-      // correction is then the first one's residual error to first order either way, so the
-      // acceptance test reads the same quantity, and the accepted iterate differs by
-      // O(1e-3 x that error), far below rounding when the test passes.  A large first correction
-      // (a start far from the solution) keeps the full iteration: a stale matrix there can carry
-      // the iterate into the other, unstable root's basin.  Per lane, so a point's iterates do not
-      // depend on its wavefront.
-      const bool reuse = near;
-      const bool c2 = newton_j(Z, J, reuse, near);
-#else
-      const bool c2 = newton(Z);
-#endif
-      if (c1 || c2) {
-        accept(Z);
-        return true;
-      }
-#else
-      double Z2[3];
-      const bool c1 = newton(Z);
-      Z2[0] = Z[0];
-      Z2[1] = Z[1];
-      Z2[2] = Z[2];
-      const bool c2 = newton(Z2);
-      if (c1) {
-        accept(Z);
-        return true;
-      }
-      if (c2) {
-        accept(Z2);
-        return true;
-      }
-      Z[0] = Z2[0];
-      Z[1] = Z2[1];
-      Z[2] = Z2[2];
-#endif
-      it = 2;
-    }
-#else
-    if (kWithYB && attempt == (guess ? 0 : 1)) YB = yb_step();
-#endif
-    for (; it < 40; ++it) {
-      if (newton(Z)) {
-        accept(Z);
-        return true;
-      }
-    }
-  }
-  return false;
-}
 
 // ---------------------------------------------------------------------------------------
 // kernels
@@ -920,22 +127,6 @@ __global__ __launch_bounds__(kOdeBlock) void ode_spline_kernel(const lzq_point* 
   if (status) status[i] = LZQ_ODE_OK;
 }
 
-// fpy:385-417 on the ODE path, one lane per point.
-// The first x in (x0, x1) at which ode_stage's T = m * (1/x) is no longer > m/3 (the branch of
-// n_chi_eq / vbar_chi, fpy:100, 111), +inf if there is none: a few ulp steps from m/(m/3).
-__device__ __forceinline__ double branch_x(const OdePoint& o, double x0, double x1) {
-  auto rel = [&](double x) { return o.m * (1.0 / pymax(x, 1e-30)) > o.m3; };
-  double xg = o.m / o.m3;
-  if (!(xg > x0 && xg < x1 + 1.0)) return INFINITY;
-  int guard = 0;
-  if (rel(xg)) {
-    while (rel(xg) && ++guard < 64) xg = nextafter(xg, INFINITY);
-  } else {
-    while (!rel(nextafter(xg, -INFINITY)) && ++guard < 64) xg = nextafter(xg, -INFINITY);
-  }
-  return (x0 < xg && xg < x1) ? xg : INFINITY;
-}
-
 // tidx (optional): point i reads the spline table at ws[tidx[i] * kOdeWS] (tables shared by
 // points with the same A/V kernel and window, lzq_ode_integrate_shared); NULL: its own, ws[i].
 // kChiOnly (lzq_ode_quadrature, sigma_v != 0 points): Y_B is already in out[i] from the
@@ -947,11 +138,6 @@ __device__ __forceinline__ double branch_x(const OdePoint& o, double x0, double 
 // previous start and stages) between launches in HBM, so a window of any length runs as a
 // series of bounded launches (lzq_ode_launches); the arithmetic of every step is the single
 // launch's, so the result is bit-identical to one launch over [0, N).
-struct OdeState {
-  double Ychi, YB, Yp, Z[3];
-  int32_t status, have;  // status: kOdeInProgress while steps remain
-};
-constexpr int32_t kOdeInProgress = 64;
 
 // kLin: the variant for linear cooperative waves (see lin_wave below); every launch runs both
 // variants, each stepping only its own wavefronts (the other variant's return at once), so the
@@ -1370,12 +556,6 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
 // (tests/test_gpu_ode.py mode-independence tests).  Every launch runs every variant; each steps
 // only its own waves.
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ double ode_uniform(double x) {
-  const uint64_t b = __builtin_bit_cast(uint64_t, x);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
-  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-}
 
 struct RicRow {
   double lam[3], E2[3], a[3];  // StageBase lam, E2, a of the step's three stages
@@ -1902,762 +1082,6 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
 }
 
 // ---------------------------------------------------------------------------------------
-// Time-parallel integration of a few points (lzq_ode_integrate_tp): multiple shooting.
-// A point's N fixed steps are cut into M intervals of L steps; node m holds the integrator's
-// state at the start of interval m (Y_chi, Y_B and the predictor's data).  Each iteration
-// (1) integrates every interval from its node, one lane per interval, with the per-lane steps
-// of ode_integrate_kernel (same stages, Y_B step map, Radau step, split step, predictor), and
-// records the end state F_m and its derivatives D_m = dY_chi_end/dY_chi_start (the product of
-// the steps' dZ_3/dY_0, the implicit function theorem on the converged stage system) and
-// C_m = dY_B_end/dY_B_start (the product of the Y_B step maps' c); (2) applies Newton's update to
-// the nodes: with residuals r_m = F_m - s_{m+1}, the corrections solve the linear recurrence
-// d_{m+1} = D_m d_m + r_m, d_0 = 0 -- a block scan of affine maps.  Node M is the point's final
-// state.  Y_B's recurrence is affine (one update makes it exact up to rounding); Y_chi's is the
-// Riccati map, for which Newton converges quadratically once the nodes are close.  The fixed
-// point is the sequential trajectory: at convergence every node is its interval predecessor's
-// end state, so the result differs from ode_integrate_kernel's only by rounding (the nodes are
-// formed as s + d instead of being carried), which the contractive or neutral dynamics keep at
-// the ~1e-14 level (tests/test_gpu_ode_tp.py).  A point whose iteration does not converge within
-// the budget, or one whose interval hits a Newton failure, is integrated sequentially instead.
-// ---------------------------------------------------------------------------------------
-// The integrator's state at the start of an interval is (Y_chi, Y_B) alone: intervals are whole
-// predictor blocks (LZQ_ODE_PRED_BLOCK), whose first step does not read the predictor's data.
-struct TpNode {
-  double Ychi, YB;
-};
-struct TpEnd {  // an interval's end state from its start node, and its derivatives
-  double Ychi, YB;
-  double D;  // dY_chi(end) / dY_chi(start)
-  double C;  // dY_B(end) / dY_B(start)
-  int32_t exact;  // every step took the Radau step (0: a Newton failure was bridged, see tp_bridge)
-  int32_t pad;
-};
-struct TpCtl {
-  int64_t N, M;     // the point's steps and intervals
-  int64_t L;        // its interval length (steps)
-  double err;       // the last update's largest relative correction
-  int32_t phase;    // kTpIter, kTpDone (converged, to be stitched), kTpExact (stitched: the result is
-                    // written), kTpFallback (sequential path)
-  int32_t iters;    // Newton updates applied
-  int32_t riccati;  // sigma_v != 0: Y_chi's map is nonlinear (the update is safeguarded)
-  int32_t pad;
-};
-constexpr int32_t kTpIter = 0, kTpDone = 1, kTpFallback = 2;
-
-// ode_integrate_kernel's prologue, in its order: status, window, step count, h, initial Y_chi.
-struct OdeSetup {
-  OdePoint o;
-  double x0, x1, h, Ychi0;
-  int64_t N;
-  int st;
-};
-__device__ __forceinline__ OdeSetup ode_setup(const lzq_point& pt, const lzq_ode_params& od, const double* w,
-                                              int64_t max_steps) {
-  OdeSetup S;
-  S.o = ode_point(pt, od);
-  const OdePoint& o = S.o;
-  S.st = ode_grid_ok(o.T_lo, o.T_hi, o.stepT) ? (ode_table_ok(w) ? LZQ_ODE_OK : LZQ_ODE_BAD_TABLE) : LZQ_ODE_BAD_GRID;
-  const double m = o.m, T_p = o.Tp;
-  S.x0 = m / o.T_hi;
-  S.x1 = m / pymax(o.T_lo, 1e-30);
-  if (pt.regime == LZQ_NONTHERMAL) {
-    if (pt.has_Y_chi_init) S.Ychi0 = pt.Y_chi_init;
-    else if (pt.has_n_chi_at_Tp) S.Ychi0 = pt.n_chi_at_Tp_GeV3 / pymax(s_entropy(T_p, pt.g_star_s), 1e-300);
-    else S.Ychi0 = 1.0e-12;
-  } else {
-    S.Ychi0 = n_chi_eq(o.T_hi, m, pt.g_chi, pt.stats) / s_entropy(o.T_hi, pt.g_star_s);
-  }
-  const double x_p = m / pymax(T_p, 1e-30);
-  const double max_step = pymin(pymin(fabs(S.x1 - S.x0) / 20000.0, x_p / 1000.0), 5e-4);
-  double steps = 0.0;
-  if (S.st == LZQ_ODE_OK) {
-    if (!(max_step > 0.0)) S.st = LZQ_ODE_BAD_STEP;
-    else {
-      steps = ceil(fabs(S.x1 - S.x0) / max_step);
-      if (!(steps <= (double)max_steps)) S.st = LZQ_ODE_TOO_MANY_STEPS;
-    }
-  }
-  S.N = S.st == LZQ_ODE_OK ? (int64_t)steps : 0;
-  S.h = S.N > 0 ? (S.x1 - S.x0) / (double)S.N : 0.0;
-  return S;
-}
-
-// dZ_3/dY_0 of a converged Riccati stage system Z = Y_0 1 + hA f(Z), f_j = -lam_j (Z_j^2 - E2_j) - S_j:
-// (A^-1 + diag(2 h lam_j Z_j)) dZ = A^-1 1, the transformed Newton matrix of radau_step.
-__device__ __forceinline__ double tp_dz3(double h, const OdeStage (&sg)[3], const double (&Z)[3]) {
-  double k[3], q[3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    k[j] = kRadauAinv[j][j] + 2.0 * (h * sg[j].lam) * Z[j];
-    q[j] = (kRadauAinv[j][0] + kRadauAinv[j][1]) + kRadauAinv[j][2];
-  }
-  const double a01 = kRadauAinv[0][1], a02 = kRadauAinv[0][2], a10 = kRadauAinv[1][0];
-  const double a12 = kRadauAinv[1][2], a20 = kRadauAinv[2][0], a21 = kRadauAinv[2][1];
-  const double b20 = a10 * a21 - k[1] * a20, b21 = a01 * a20 - k[0] * a21, b22 = k[0] * k[1] - a01 * a10;
-  const double b00 = k[1] * k[2] - a12 * a21, b10 = a12 * a20 - a10 * k[2];
-  const double det = k[0] * b00 + a01 * b10 + a02 * b20;
-  const double dz = (b20 * q[0] + b21 * q[1] + b22 * q[2]) / det;
-  return isfinite(dz) ? dz : 0.0;  // overflowing stiff stages: the map contracts there
-}
-
-// One block per point: ctl, and every node at the initial state (node 0 is ode_integrate_kernel's
-// start; the others are the first guess).  Points the iteration does not take (a status other
-// than OK, fewer than two intervals) go to the fallback.
-__global__ __launch_bounds__(256) void ode_tp_init_kernel(const lzq_point* __restrict__ pts,
-                                                          const lzq_ode_params* __restrict__ ode,
-                                                          const int32_t* __restrict__ tidx,
-                                                          const double* __restrict__ ws, int64_t max_steps, int64_t L,
-                                                          int64_t Mmax, TpNode* __restrict__ nodes,
-                                                          TpCtl* __restrict__ ctl) {
-  const int64_t p = blockIdx.x;
-  const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
-  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
-  // the point's own interval length: L steps, more when its N would need over Mmax intervals
-  // (max_steps only sizes the node arrays)
-  // (a whole number of predictor blocks, LZQ_ODE_PRED_BLOCK: the exact stitching needs interval starts
-  // whose first step does not read the predictor)
-  constexpr int64_t B = LZQ_ODE_PRED_BLOCK;
-  const int64_t Lp = S.N > L * Mmax ? ((S.N + Mmax - 1) / Mmax + B - 1) / B * B : L;
-  const int64_t M = S.st == LZQ_ODE_OK ? (S.N + Lp - 1) / Lp : 0;
-  const bool go = S.st == LZQ_ODE_OK && M >= 2 && M <= Mmax;
-  if (threadIdx.x == 0) ctl[p] = TpCtl{S.N, M, Lp, 0.0, go ? kTpIter : kTpFallback, 0, S.o.sigmav != 0.0 ? 1 : 0, 0};
-  if (!go) return;
-  TpNode* nd = nodes + p * (Mmax + 1);
-  for (int64_t m = threadIdx.x; m <= M; m += blockDim.x)
-    nd[m] = TpNode{S.Ychi0, 0.0};
-}
-
-// A Riccati step whose Newton iteration fails -- possible only from a start far above the
-// trajectory, as in the first iterations -- is bridged by backward Euler at the step's end,
-// Y1 = Y0 - h lam (Y1^2 - E2) - h S, whose positive root 2c / (1 + sqrt(1 + 4 h lam c)),
-// c = Y0 + h lam E2 - h S, exists for every start (unconditionally stable, no iteration): the
-// interval still returns an end state and a derivative to improve the nodes with, and is marked
-// inexact, so the iteration cannot converge while any interval needs the bridge.
-__device__ __forceinline__ double tp_bridge(double Y0, double h, const OdeStage& s3, double& dY1) {
-  const double hl = h * s3.lam;
-  const double c = Y0 + hl * s3.E2 - h * s3.S;
-  const double q = sqrt(pymax(1.0 + 4.0 * hl * c, 0.0));
-  dY1 = 1.0 / pymax(q, 1e-300);
-  return 2.0 * c / (1.0 + q);
-}
-
-// The integrator's state between steps (ode_integrate_kernel's per-lane registers).
-struct TpState {
-  double Ychi, YB, Yp, Z[3];
-  bool have;
-};
-
-// Steps [k0, k1) of the fixed-step sequence x_k = x0 + k h from state St, with ode_integrate_kernel's
-// per-lane operations (stages, Y_B map, Radau step, the T = m/3 split step, the predictor); D and C
-// accumulate the derivatives of the end state.  Returns false when a step needed tp_bridge.
-__device__ __forceinline__ bool tp_steps(const OdePoint& o, const double* __restrict__ w, double x0, double h,
-                                         double xb, double xb_below, int64_t k0, int64_t k1, TpState& St, double& D,
-                                         double& C) {
-  const Radau R = radau_tableau();
-  const RadauH hA = radau_h(R, h);
-  const bool riccati = LZQ_ODE_PREDICT && o.sigmav != 0.0;
-  double Ychi = St.Ychi, YB = St.YB, Yp = St.Yp;
-  double Zs[3] = {St.Z[0], St.Z[1], St.Z[2]};
-  bool have = St.have, exact = true;
-  double kd = (double)k0;
-  for (int64_t k = k0; k < k1; ++k, kd += 1.0) {
-    const double xk = x0 + kd * h;
-    const bool split = xk < xb && xb <= xk + h;
-    const double xa = split ? xb_below : xk + h;
-    const double Ystart = Ychi;
-    bool use_guess = false;
-    if (riccati && have && !split && pred_step(k)) {  // the Radau5 predictor, as ode_integrate_kernel
-      double gs[3];
-      use_guess = true;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        gs[j] = fma_s(Zs[2], kRadauPred[j][3],
-                      fma_s(Zs[1], kRadauPred[j][2], fma_s(Zs[0], kRadauPred[j][1], kRadauPred[j][0] * Yp)));
-        use_guess = use_guess && fabs(gs[j] - Ychi) <= 0.25 * fabs(Ychi);
-      }
-#pragma unroll
-      for (int j = 0; j < 3; ++j) Zs[j] = gs[j];
-    }
-    auto part = [&](double xs, double hs, bool guess, bool own_h, bool block_start) {
-      const RadauH hAs = own_h ? radau_h(R, hs) : hA;
-      OdeStage sg[3];
-#pragma unroll
-      for (int j = 0; j < 3; ++j) sg[j] = ode_stage(o, w, xs + R.c[j] * hs);
-      const YbRec yr = yb_rec(hAs, sg);
-      YB = __builtin_fma(yr.c, YB, o.Pf * yr.d);
-      C *= yr.c;
-      const double Y0 = Ychi;
-      if (block_start) guess = block_guess(R, hs, sg, Ychi, Zs);
-      // (radau_step's convergence test reads NaN corrections as converged -- it never meets one on
-      // the sequential trajectory, but a start far from it can diverge: a non-finite result, or a
-      // sign change of a source-free positive Y_chi (the stage system's other root), is a failure)
-      const bool src = sg[0].S != 0.0 || sg[1].S != 0.0 || sg[2].S != 0.0;
-      if (radau_step<false>(hAs, sg, Ychi, YB, Zs, guess) && isfinite(Ychi) && (src || !(Y0 > 0.0) || Ychi > 0.0)) {
-        const bool nonlinear = sg[0].lam != 0.0 || sg[1].lam != 0.0 || sg[2].lam != 0.0;
-        if (nonlinear) D *= tp_dz3(hs, sg, Zs);
-        return true;
-      }
-      double dY1;
-      Ychi = tp_bridge(Y0, hs, sg[2], dY1);
-      Zs[0] = Zs[1] = Zs[2] = Ychi;
-      D *= dY1;
-      return false;
-    };
-    bool ok = true;
-    if (xa > xk) ok = part(xk, split ? xa - xk : h, use_guess, split, riccati && !split && !pred_step(k));
-    if (split && xk + h > xb) ok = part(xb, (xk + h) - xb, false, true, false) && ok;
-    exact = exact && ok;
-    have = !split && ok;  // after a bridge the predictor has no collocation polynomial behind it
-    Yp = Ystart;
-  }
-  St = TpState{Ychi, YB, Yp, {Zs[0], Zs[1], Zs[2]}, have};
-  return exact;
-}
-
-// One lane per (point, interval): F_m, D_m, C_m from node m.
-__global__ __launch_bounds__(64) void ode_tp_interval_kernel(const lzq_point* __restrict__ pts,
-                                                             const lzq_ode_params* __restrict__ ode, int64_t n,
-                                                             const int32_t* __restrict__ tidx,
-                                                             const double* __restrict__ ws, int64_t max_steps,
-                                                             int64_t L, int64_t Mmax, const TpNode* __restrict__ nodes,
-                                                             TpEnd* __restrict__ ends, const TpCtl* __restrict__ ctl) {
-  const int64_t g = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  const int64_t p = g / Mmax, m = g - p * Mmax;
-  if (p >= n) return;
-  const TpCtl c = ctl[p];
-  if (c.phase != kTpIter || m >= c.M) return;
-  const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
-  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
-  const int64_t k0 = m * c.L, k1 = k0 + c.L < S.N ? k0 + c.L : S.N;
-  const double xb = branch_x(S.o, S.x0, S.x1);
-  const TpNode nd = nodes[p * (Mmax + 1) + m];
-  TpState St{nd.Ychi, nd.YB, nd.Ychi, {nd.Ychi, nd.Ychi, nd.Ychi}, false};  // (the first step reads no predictor)
-  double D = 1.0, C = 1.0;
-  const bool exact = tp_steps(S.o, w, S.x0, S.h, xb, nextafter(xb, -INFINITY), k0, k1, St, D, C);
-  ends[p * Mmax + m] = TpEnd{St.Ychi, St.YB, D, C, exact ? 1 : 0, 0};
-}
-
-// The first guess of long Riccati windows (M >= kTpGuessMin intervals): the same integrator on kTpGuessSteps
-// coarse steps of (x1 - x0) / kTpGuessSteps (one lane per point, sequential), each node then
-// interpolated between the coarse points around it (Y_chi geometrically when both are positive,
-// Y_B linearly).  Radau IIA is L-stable, so the coarse trajectory tracks equilibrium where the
-// fine one does and freezes out near where it does: Newton starts within reach of its quadratic
-// phase instead of from the constant initial value (14 -> ~5 updates on the shipped window).
-constexpr int64_t kTpGuessMin = 1024, kTpGuessSteps = 256;
-__global__ __launch_bounds__(256) void ode_tp_guess_kernel(const lzq_point* __restrict__ pts,
-                                                           const lzq_ode_params* __restrict__ ode,
-                                                           const int32_t* __restrict__ tidx,
-                                                           const double* __restrict__ ws, int64_t max_steps, int64_t L,
-                                                           int64_t Mmax, TpNode* __restrict__ nodes,
-                                                           const TpCtl* __restrict__ ctl) {
-  __shared__ double s_y[kTpGuessSteps + 1], s_b[kTpGuessSteps + 1];
-  const int64_t p = blockIdx.x;
-  const TpCtl c = ctl[p];
-  // block-uniform; without annihilation Y_chi's map is affine and Newton needs no first guess
-  if (c.phase != kTpIter || c.M < kTpGuessMin || !c.riccati) return;
-  const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
-  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
-  const double Hc = (S.x1 - S.x0) / (double)kTpGuessSteps;
-  if (threadIdx.x == 0) {
-    const double xb = branch_x(S.o, S.x0, S.x1);
-    TpState St{S.Ychi0, 0.0, S.Ychi0, {S.Ychi0, S.Ychi0, S.Ychi0}, false};
-    s_y[0] = S.Ychi0;
-    s_b[0] = 0.0;
-    for (int64_t k = 0; k < kTpGuessSteps; ++k) {
-      double D = 1.0, C = 1.0;
-      tp_steps(S.o, w, S.x0, Hc, xb, nextafter(xb, -INFINITY), k, k + 1, St, D, C);
-      s_y[k + 1] = St.Ychi;
-      s_b[k + 1] = St.YB;
-    }
-  }
-  __syncthreads();
-  TpNode* nd = nodes + p * (Mmax + 1);
-  for (int64_t m = 1 + threadIdx.x; m <= c.M; m += blockDim.x) {
-    const int64_t km = m * c.L < S.N ? m * c.L : S.N;  // node m's step index (node M: x1)
-    const double u = (double)km / (double)S.N * (double)kTpGuessSteps;
-    const int64_t j = u < (double)kTpGuessSteps ? (int64_t)u : kTpGuessSteps - 1;
-    const double t = u - (double)j;
-    const double y0 = s_y[j], y1 = s_y[j + 1];
-    const double y = (y0 > 0.0 && y1 > 0.0) ? y0 * exp(t * log(y1 / y0)) : y0 + t * (y1 - y0);
-    const double b = s_b[j] + t * (s_b[j + 1] - s_b[j]);
-    if (isfinite(y) && isfinite(b)) nd[m] = TpNode{y, b};
-  }
-}
-
-// Newton's update of the nodes: the corrections solve d_{m+1} = D_m d_m + r_m (r_m = F_m - s_{m+1},
-// d_0 = 0) for both chains, a scan of the affine maps d -> D d + r.  Three launches, kTpBlk
-// intervals per block: (1) each block scans its maps in LDS (Hillis-Steele) and stores the local
-// inclusive prefixes and its aggregate; (2) each block scans the aggregates of the blocks before it
-// (in LDS, at most Mmax / kTpBlk of them), applies the carry to its prefixes and updates its nodes;
-// (3) one thread per point folds the blocks' largest corrections and failure flags into TpCtl.
-constexpr int kTpBlk = 256;
-struct TpMap {
-  double A, B, Ab, Bb;  // d -> A d + B (Y_chi), d -> Ab d + Bb (Y_B)
-};
-__device__ __forceinline__ TpMap tp_compose(const TpMap& later, const TpMap& earlier) {  // later o earlier
-  return TpMap{later.A * earlier.A, __builtin_fma(later.A, earlier.B, later.B), later.Ab * earlier.Ab,
-               __builtin_fma(later.Ab, earlier.Bb, later.Bb)};
-}
-// inclusive block scan of kTpBlk maps (every thread of the block calls it)
-__device__ __forceinline__ TpMap tp_block_scan(TpMap v, TpMap* sm) {
-  const int t = threadIdx.x;
-  sm[t] = v;
-  __syncthreads();
-  for (int off = 1; off < kTpBlk; off <<= 1) {
-    const TpMap prev = t >= off ? sm[t - off] : TpMap{1.0, 0.0, 1.0, 0.0};
-    __syncthreads();
-    if (t >= off) v = tp_compose(v, prev);
-    sm[t] = v;
-    __syncthreads();
-  }
-  return v;
-}
-struct TpBlkOut {
-  double err;
-  int32_t fail, pad;
-};
-
-__global__ __launch_bounds__(kTpBlk) void ode_tp_scan_local_kernel(int64_t Mmax, int64_t Bmax,
-                                                                   const TpNode* __restrict__ nodes,
-                                                                   const TpEnd* __restrict__ ends,
-                                                                   const TpCtl* __restrict__ ctl,
-                                                                   TpMap* __restrict__ loc, TpMap* __restrict__ agg,
-                                                                   TpBlkOut* __restrict__ bout) {
-  __shared__ TpMap sm[kTpBlk];
-  const int64_t p = blockIdx.y, b = blockIdx.x;
-  const TpCtl c = ctl[p];
-  if (c.phase != kTpIter || b * kTpBlk >= c.M) return;  // block-uniform
-  const int t = threadIdx.x;
-  const int64_t m = b * kTpBlk + t;
-  TpMap v{1.0, 0.0, 1.0, 0.0};
-  int fail = 0;
-  if (m < c.M) {
-    const TpEnd e = ends[p * Mmax + m];
-    const TpNode q = nodes[p * (Mmax + 1) + m + 1];
-    const bool fin = isfinite(e.Ychi) && isfinite(e.D) && isfinite(e.YB) && isfinite(e.C);
-    fail = e.exact == 0 || !fin;
-    // a non-finite end (a start far from the trajectory) moves nothing downstream this update
-    v = fin ? TpMap{e.D, e.Ychi - q.Ychi, e.C, e.YB - q.YB} : TpMap{0.0, 0.0, 0.0, 0.0};
-  }
-  const int any_fail = __syncthreads_or(fail);
-  v = tp_block_scan(v, sm);
-  if (m < c.M) loc[p * Mmax + m] = v;
-  if (t == kTpBlk - 1) {
-    agg[p * Bmax + b] = v;
-    bout[p * Bmax + b].fail = any_fail;
-  }
-}
-
-__global__ __launch_bounds__(kTpBlk) void ode_tp_scan_apply_kernel(int64_t Mmax, int64_t Bmax,
-                                                                   TpNode* __restrict__ nodes,
-                                                                   const TpEnd* __restrict__ ends,
-                                                                   const TpCtl* __restrict__ ctl,
-                                                                   const TpMap* __restrict__ loc,
-                                                                   const TpMap* __restrict__ agg,
-                                                                   TpBlkOut* __restrict__ bout) {
-  __shared__ TpMap sm[kTpBlk];
-  __shared__ double s_err[kTpBlk / 64];
-  const int64_t p = blockIdx.y, b = blockIdx.x;
-  const TpCtl c = ctl[p];
-  if (c.phase != kTpIter || b * kTpBlk >= c.M) return;  // block-uniform
-  const int t = threadIdx.x;
-  const int64_t nb = (c.M + kTpBlk - 1) / kTpBlk;
-  // the carry into this block: the aggregates of blocks 0 .. b-1 composed (their own scan, in
-  // rounds of kTpBlk when there are more blocks than threads)
-  TpMap carry{1.0, 0.0, 1.0, 0.0};
-  for (int64_t r0 = 0; r0 < b; r0 += kTpBlk) {
-    const int64_t k = r0 + t;
-    TpMap v = k < b ? agg[p * Bmax + k] : TpMap{1.0, 0.0, 1.0, 0.0};
-    v = tp_block_scan(v, sm);
-    const int last = (int)((b - r0 < kTpBlk ? b - r0 : kTpBlk) - 1);
-    carry = tp_compose(sm[last], carry);
-    __syncthreads();
-  }
-  (void)nb;
-  const int64_t m = b * kTpBlk + t;
-  double err = 0.0;
-  if (m < c.M) {
-    const TpMap v = loc[p * Mmax + m];
-    const double d = __builtin_fma(v.A, carry.B, v.B), db = __builtin_fma(v.Ab, carry.Bb, v.Bb);  // d_{m+1}
-    const TpEnd e = ends[p * Mmax + m];
-    TpNode q = nodes[p * (Mmax + 1) + m + 1];
-    const bool fin = isfinite(e.Ychi) && isfinite(e.D) && isfinite(e.YB) && isfinite(e.C);
-    const double old = q.Ychi;
-    double nv = old + d;
-    // the Riccati stage system has a second root below zero: a correction never takes a positive
-    // node below a quarter of the smaller of its value and its predecessor interval's (positive)
-    // end (far from the solution only).  Y_chi's map is affine without annihilation (depletion may
-    // take it through zero): no safeguard there.
-    const double lo = 0.25 * pymin(old, fin && e.Ychi > 0.0 ? e.Ychi : old);
-    if (c.riccati && old > 0.0 && !(nv >= lo)) nv = lo;
-    q.Ychi = nv;
-    q.YB = q.YB + db;
-    nodes[p * (Mmax + 1) + m + 1] = q;
-    // relative to the node, floored at 1e-290: below it the doubles approach the subnormal range,
-    // whose coarser spacing no correction could resolve to the tolerance
-    const double ec = fabs(d) / pymax(fabs(nv), 1e-290), eb = fabs(db) / pymax(fabs(q.YB), 1e-290);
-    err = pymax(ec, eb);  // pymax keeps a NaN on the right: checked below
-    if (!(ec == ec) || !(eb == eb)) err = INFINITY;
-#ifdef LZQ_ODE_TP_DEBUG
-    if (m == 0 || m == c.M - 1 || (m % ((c.M + 7) / 8)) == 0)
-      printf("  p %lld m %lld node %.6e end %.6e D %.3e exact %d\n", (long long)p, (long long)m, old, e.Ychi, e.D,
-             e.exact);
-#endif
-  }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) err = pymax(err, __shfl_xor(err, off, 64));
-  if ((t & 63) == 0) s_err[t >> 6] = err;
-  __syncthreads();
-  if (t == 0) {
-    double e_all = 0.0;
-    for (int k = 0; k < kTpBlk / 64; ++k) e_all = pymax(e_all, s_err[k]);
-    bout[p * Bmax + b].err = e_all;
-  }
-}
-
-__global__ __launch_bounds__(64) void ode_tp_scan_finish_kernel(int64_t n, int64_t Bmax, TpCtl* __restrict__ ctl,
-                                                                const TpBlkOut* __restrict__ bout, int32_t max_iters,
-                                                                double tol) {
-  const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  if (p >= n) return;
-  TpCtl c = ctl[p];
-  if (c.phase != kTpIter) return;
-  const int64_t nb = (c.M + kTpBlk - 1) / kTpBlk;
-  double e_all = 0.0;
-  bool fail = false;
-  for (int64_t b = 0; b < nb; ++b) {
-    e_all = pymax(e_all, bout[p * Bmax + b].err);
-    fail = fail || bout[p * Bmax + b].fail != 0;
-  }
-  c.iters += 1;
-  c.err = e_all;
-#ifdef LZQ_ODE_TP_DEBUG
-  printf("tp point %lld update %d: M %lld err %.3e fail %d\n", (long long)p, c.iters, (long long)c.M, e_all, (int)fail);
-#endif
-  // converged: the corrections are below the tolerance and every interval took only Radau steps
-  if (e_all <= tol && !fail) c.phase = kTpDone;
-  else if (c.iters >= max_iters) c.phase = kTpFallback;
-  ctl[p] = c;
-}
-
-// Exact stitching.  At convergence the nodes sit within a few ulps of the sequential trajectory
-// but are formed as s + d, not carried, so the Newton result differs from the sequential one by
-// rounding.  Because no block of LZQ_ODE_PRED_BLOCK steps uses the predictor on its first step
-// (and the intervals are whole blocks), interval m's end state is a function of its start
-// (Y_chi, Y_B) alone: F_m for Y_chi, G_m for Y_B (independent chains: Y_B's step map does not read
-// Y_chi, Y_chi's Newton does not read Y_B).  So every interval is integrated from the 2J + 1
-// candidate starts s_m + j ulp, |j| <= J (both chains side by side in one lane), and the exact
-// chains are followed through the candidate tables: node 0 is exact, and if node m's exact value
-// is candidate j_m, node m + 1's is F_m(candidate j_m) -- a table entry, which again is a candidate
-// of node m + 1 unless the Newton node was more than J ulps off.  Following the chain is M
-// dependent look-ups, done as segments of kTpSeg intervals for every entry candidate in parallel
-// (ode_tp_seg_kernel), then one walk over the segments per point (ode_tp_stitch_kernel).  Each
-// candidate integration performs exactly the sequential kernels' operations on that start, so a
-// point whose chains stay inside the windows gets the sequential integration's bits; a point whose
-// chain leaves a window, or meets a bridged step, is integrated sequentially.  Three rounds: J = 4
-// (cheap, the usual case), then J = 32 and J = 256 for the points the previous did not finish (the
-// Newton nodes wander from the exact chain where the dynamics is neutral, e.g. a weakly annihilating
-// plateau; the last round only where its tables fit kTpCandBytes).
-constexpr int kTpSeg = 64;       // intervals per stitching segment
-constexpr int kTpJ1 = 4, kTpJ2 = 32, kTpJ3 = 256;
-constexpr size_t kTpCandBytes = size_t(1) << 30;  // candidate tables of the J = 256 round, at most
-
-// monotone integer key of a double (ordered like the values; -0 and +0 map to 0) and back
-__device__ __forceinline__ int64_t dkey(double x) {
-  const int64_t b = __builtin_bit_cast(int64_t, x);
-  return b >= 0 ? b : -(b & 0x7FFFFFFFFFFFFFFFll);
-}
-__device__ __forceinline__ double dfromkey(int64_t k) {
-  return __builtin_bit_cast(double, k >= 0 ? k : ((-k) | (int64_t)0x8000000000000000ull));
-}
-
-// One lane per (point, interval, candidate j): F_m and G_m at s_m + j ulp, b_m + j ulp (NaN for a
-// start that needed a bridge).  Points already stitched (phase kTpExact) or not converged return.
-constexpr int32_t kTpExact = 3;
-// one (interval, candidate) of one point (out of line: the grid-stride loop around it keeps no
-// values of its own live across the integration)
-__device__ __noinline__ void tp_cand_one(const lzq_point* __restrict__ pts, const lzq_ode_params* __restrict__ ode,
-                                         const int32_t* __restrict__ tidx, const double* __restrict__ ws,
-                                         int64_t max_steps, const TpNode* __restrict__ nd, const TpCtl& c, int64_t p,
-                                         int64_t m, int off, double* __restrict__ oF, double* __restrict__ oG) {
-  const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
-  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
-  const int64_t k0 = m * c.L, k1 = k0 + c.L < S.N ? k0 + c.L : S.N;
-  const double y0 = dfromkey(dkey(nd->Ychi) + off), b0 = dfromkey(dkey(nd->YB) + off);
-  // (k0 is a whole number of predictor blocks: the first step does not read Yp / Z / have)
-  TpState St{y0, b0, y0, {y0, y0, y0}, false};
-  double D = 1.0, C = 1.0;
-  const double xb = branch_x(S.o, S.x0, S.x1);
-  const bool exact = tp_steps(S.o, w, S.x0, S.h, xb, nextafter(xb, -INFINITY), k0, k1, St, D, C);
-  *oF = exact ? St.Ychi : __builtin_nan("");
-  *oG = exact ? St.YB : __builtin_nan("");
-}
-
-// kStride: a grid-stride loop around an out-of-line body (the last round, whose full grid would be
-// ~10^5 blocks that mostly return at once); else one lane per item, the body inline (2 waves/SIMD).
-template <int J, bool kStride>
-__global__ __launch_bounds__(64) void ode_tp_cand_kernel(const lzq_point* __restrict__ pts,
-                                                         const lzq_ode_params* __restrict__ ode, int64_t n,
-                                                         const int32_t* __restrict__ tidx,
-                                                         const double* __restrict__ ws, int64_t max_steps, int64_t Mmax,
-                                                         const TpNode* __restrict__ nodes, const TpCtl* __restrict__ ctl,
-                                                         double* __restrict__ candF, double* __restrict__ candG) {
-  constexpr int NC = 2 * J + 1;
-  for (int64_t g = (int64_t)blockIdx.x * 64 + threadIdx.x; g < n * Mmax * NC; g += (int64_t)gridDim.x * 64) {
-    const int64_t p = g / (Mmax * NC), rem = g - p * (Mmax * NC), m = rem / NC;
-    const int jj = (int)(rem - m * NC);
-    const TpCtl c = ctl[p];
-    if (c.phase == kTpDone && m < c.M) {
-      const int64_t o = (p * Mmax + m) * NC + jj;
-      if constexpr (kStride) {
-        tp_cand_one(pts, ode, tidx, ws, max_steps, nodes + p * (Mmax + 1) + m, c, p, m, jj - J, candF + o, candG + o);
-      } else {
-        const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
-        const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
-        const int64_t k0 = m * c.L, k1 = k0 + c.L < S.N ? k0 + c.L : S.N;
-        const TpNode& nd = nodes[p * (Mmax + 1) + m];
-        const double y0 = dfromkey(dkey(nd.Ychi) + (jj - J)), b0 = dfromkey(dkey(nd.YB) + (jj - J));
-        TpState St{y0, b0, y0, {y0, y0, y0}, false};
-        double D = 1.0, C = 1.0;
-        const double xb = branch_x(S.o, S.x0, S.x1);
-        const bool exact = tp_steps(S.o, w, S.x0, S.h, xb, nextafter(xb, -INFINITY), k0, k1, St, D, C);
-        candF[o] = exact ? St.Ychi : __builtin_nan("");
-        candG[o] = exact ? St.YB : __builtin_nan("");
-      }
-    }
-    if constexpr (!kStride) break;  // one item per lane
-  }
-}
-
-// One lane per (point, segment, entry candidate of both chains): follow the chains through the
-// segment's intervals; the exit candidate index at the next segment's first node (-1: the chain
-// left the window or met a bridged start) and the value at the segment's end node.
-template <int J>
-__global__ __launch_bounds__(64) void ode_tp_seg_kernel(int64_t n, int64_t Mmax, int64_t Smax,
-                                                        const TpNode* __restrict__ nodes,
-                                                        const TpCtl* __restrict__ ctl,
-                                                        const double* __restrict__ candF,
-                                                        const double* __restrict__ candG, int32_t* __restrict__ segF,
-                                                        int32_t* __restrict__ segG, double* __restrict__ lastF,
-                                                        double* __restrict__ lastG) {
-  constexpr int NC = 2 * J + 1;
-  const int64_t g = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  const int64_t p = g / (Smax * NC), rem = g - p * (Smax * NC), sg = rem / NC;
-  const int jj = (int)(rem - sg * NC);
-  if (p >= n) return;
-  const TpCtl c = ctl[p];
-  if (c.phase != kTpDone || sg * kTpSeg >= c.M) return;
-  const int64_t m0 = sg * kTpSeg, m1 = m0 + kTpSeg < c.M ? m0 + kTpSeg : c.M;
-  const TpNode* nd = nodes + p * (Mmax + 1);
-  int jF = jj, jG = jj;
-  double vF = 0.0, vG = 0.0;
-  for (int64_t m = m0; m < m1; ++m) {
-    const int64_t o = (p * Mmax + m) * NC;
-    vF = jF >= 0 ? candF[o + jF] : __builtin_nan("");
-    vG = jG >= 0 ? candG[o + jG] : __builtin_nan("");
-    if (m + 1 < c.M) {  // the candidate index of node m + 1 (node M, the final state, needs none)
-      const int64_t dF = dkey(vF) - dkey(nd[m + 1].Ychi) + J, dG = dkey(vG) - dkey(nd[m + 1].YB) + J;
-#ifdef LZQ_ODE_TP_DEBUG
-      if (jj == J && ((jF >= 0 && !(isfinite(vF) && dF >= 0 && dF < NC)) || (jG >= 0 && !(isfinite(vG) && dG >= 0 && dG < NC))))
-        printf("  J %d seg %lld node %lld: offset F %lld G %lld (vF %.17g node %.17g)\n", J, (long long)sg,
-               (long long)(m + 1), (long long)(dF - J), (long long)(dG - J), vF, nd[m + 1].Ychi);
-#endif
-      jF = (isfinite(vF) && dF >= 0 && dF < NC) ? (int)dF : -1;
-      jG = (isfinite(vG) && dG >= 0 && dG < NC) ? (int)dG : -1;
-    }
-  }
-  const int64_t o = (p * Smax + sg) * NC + jj;
-  segF[o] = jF;
-  segG[o] = jG;
-  lastF[o] = vF;
-  lastG[o] = vG;
-}
-
-// The Y_B chain on its own (round 5).  Y_B's step is affine, YB <- fma(c, YB, Pf d), with c and d
-// from the step's stages alone (yb_rec): they do not depend on Y_chi.  So the Y_B candidates of an
-// interval need no Newton iteration and can share the stages: one lane steps kTpGChunk of them
-// with tp_steps' step / split structure and Y_B operations, and a window of +-kTpJG ulps costs a
-// fraction of the J = 4 round.  A point whose Y_B chain stitches here (gdone) needs only its Y_chi
-// chain in the rounds after (its Y_B chain is the one that wanders where the dynamics is neutral).
-constexpr int kTpGChunk = 22;  // 3 lanes per interval for JG = 32
-constexpr int kTpJG = 32;      // the Y_B round's window (a wider one cost more than it saved; J = 256 stays)
-template <int JG>
-__global__ __launch_bounds__(64) void ode_tp_gcand_kernel(const lzq_point* __restrict__ pts,
-                                                          const lzq_ode_params* __restrict__ ode, int64_t n,
-                                                          const int32_t* __restrict__ tidx,
-                                                          const double* __restrict__ ws, int64_t max_steps,
-                                                          int64_t Mmax, const TpNode* __restrict__ nodes,
-                                                          const TpCtl* __restrict__ ctl, double* __restrict__ candG) {
-  constexpr int NC = 2 * JG + 1, NCH = (NC + kTpGChunk - 1) / kTpGChunk;
-  const int64_t g = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  const int64_t p = g / (Mmax * NCH), rem = g - p * (Mmax * NCH), m = rem / NCH;
-  const int ch = (int)(rem - m * NCH);
-  if (p >= n) return;
-  const TpCtl c = ctl[p];
-  if (c.phase != kTpDone || m >= c.M) return;
-  const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
-  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
-  const int64_t k0 = m * c.L, k1 = k0 + c.L < S.N ? k0 + c.L : S.N;
-  const int64_t bkey = dkey(nodes[p * (Mmax + 1) + m].YB);
-  double yb[kTpGChunk];
-#pragma unroll
-  for (int i = 0; i < kTpGChunk; ++i) yb[i] = dfromkey(bkey + (ch * kTpGChunk + i - JG));
-  const Radau R = radau_tableau();
-  const RadauH hA = radau_h(R, S.h);
-  const double xb = branch_x(S.o, S.x0, S.x1), xb_below = nextafter(xb, -INFINITY);
-  auto part = [&](double xs, double hs, bool own_h) {
-    const RadauH hAs = own_h ? radau_h(R, hs) : hA;
-    OdeStage sg[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) sg[j] = ode_stage(S.o, w, xs + R.c[j] * hs);
-    const YbRec yr = yb_rec(hAs, sg);
-    const double e = S.o.Pf * yr.d;
-#pragma unroll
-    for (int i = 0; i < kTpGChunk; ++i) yb[i] = __builtin_fma(yr.c, yb[i], e);
-  };
-  double kd = (double)k0;
-  for (int64_t k = k0; k < k1; ++k, kd += 1.0) {
-    const double xk = S.x0 + kd * S.h;
-    const bool split = xk < xb && xb <= xk + S.h;
-    const double xa = split ? xb_below : xk + S.h;
-    if (xa > xk) part(xk, split ? xa - xk : S.h, split);
-    if (split && xk + S.h > xb) part(xb, (xk + S.h) - xb, true);
-  }
-  double* o = candG + (p * Mmax + m) * NC;
-#pragma unroll
-  for (int i = 0; i < kTpGChunk; ++i)
-    if (ch * kTpGChunk + i < NC) o[ch * kTpGChunk + i] = yb[i];
-}
-
-// the Y_B chain through one segment from every entry candidate (ode_tp_seg_kernel's G half)
-template <int JG>
-__global__ __launch_bounds__(64) void ode_tp_gseg_kernel(int64_t n, int64_t Mmax, int64_t Smax,
-                                                         const TpNode* __restrict__ nodes, const TpCtl* __restrict__ ctl,
-                                                         const double* __restrict__ candG, int32_t* __restrict__ segG,
-                                                         double* __restrict__ lastG) {
-  constexpr int NC = 2 * JG + 1;
-  const int64_t g = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  const int64_t p = g / (Smax * NC), rem = g - p * (Smax * NC), sg = rem / NC;
-  const int jj = (int)(rem - sg * NC);
-  if (p >= n) return;
-  const TpCtl c = ctl[p];
-  if (c.phase != kTpDone || sg * kTpSeg >= c.M) return;
-  const int64_t m0 = sg * kTpSeg, m1 = m0 + kTpSeg < c.M ? m0 + kTpSeg : c.M;
-  const TpNode* nd = nodes + p * (Mmax + 1);
-  int jG = jj;
-  double vG = 0.0;
-  for (int64_t m = m0; m < m1; ++m) {
-    vG = jG >= 0 ? candG[(p * Mmax + m) * NC + jG] : __builtin_nan("");
-    if (m + 1 < c.M) {
-      const int64_t dG = dkey(vG) - dkey(nd[m + 1].YB) + JG;
-      jG = (isfinite(vG) && dG >= 0 && dG < NC) ? (int)dG : -1;
-    }
-  }
-  segG[(p * Smax + sg) * NC + jj] = jG;
-  lastG[(p * Smax + sg) * NC + jj] = vG;
-}
-
-// the Y_B chain from node 0 through the segments: gdone[p], and its final value gyb[p]
-template <int JG>
-__global__ __launch_bounds__(64) void ode_tp_gstitch_kernel(int64_t n, int64_t Smax, const TpCtl* __restrict__ ctl,
-                                                            const int32_t* __restrict__ segG,
-                                                            const double* __restrict__ lastG,
-                                                            int32_t* __restrict__ gdone, double* __restrict__ gyb) {
-  constexpr int NC = 2 * JG + 1;
-  const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  if (p >= n) return;
-  const TpCtl c = ctl[p];
-  gdone[p] = 0;
-  if (c.phase != kTpDone) return;
-  const int64_t nseg = (c.M + kTpSeg - 1) / kTpSeg;
-  int jG = JG;
-  double YB = __builtin_nan("");
-  for (int64_t sg = 0; sg < nseg && jG >= 0; ++sg) {
-    const int64_t o = (p * Smax + sg) * NC;
-    if (sg + 1 == nseg)
-      YB = lastG[o + jG];
-    else
-      jG = segG[o + jG];
-  }
-  if (jG >= 0 && isfinite(YB)) {
-    gdone[p] = 1;
-    gyb[p] = YB;
-  }
-}
-
-// One thread per point: the chains from node 0 (candidate J, the exact start) through the
-// segments; both inside their windows to the end -> the final state is the sequential one: the
-// yields, skip[p] = 1, phase kTpExact.  Otherwise the point waits for the next round or the
-// sequential launches.
-template <int J>
-__global__ __launch_bounds__(64) void ode_tp_stitch_kernel(const lzq_point* __restrict__ pts, int64_t n, int64_t Smax,
-                                                           TpCtl* __restrict__ ctl, const int32_t* __restrict__ segF,
-                                                           const int32_t* __restrict__ segG,
-                                                           const double* __restrict__ lastF,
-                                                           const double* __restrict__ lastG, lzq_yield* __restrict__ out,
-                                                           int32_t* __restrict__ status, int32_t* __restrict__ skip,
-                                                           const int32_t* __restrict__ gdone,
-                                                           const double* __restrict__ gyb, int32_t only_gdone) {
-  constexpr int NC = 2 * J + 1;
-  const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  if (p >= n) return;
-  TpCtl c = ctl[p];
-  const bool gd = gdone[p] != 0;  // the Y_B chain stitched on its own (ode_tp_gstitch_kernel)
-  if (only_gdone && !gd) return;  // a walk over tables whose Y_B half is not this round's
-#ifdef LZQ_ODE_TP_DEBUG
-  printf("tp point %lld: stitch round J = %d, phase %d\n", (long long)p, J, c.phase);
-#endif
-  if (c.phase != kTpDone) return;
-  const int64_t nseg = (c.M + kTpSeg - 1) / kTpSeg;
-  int jF = J, jG = J;
-  double YB = 0.0, Ychi = 0.0;
-  for (int64_t sg = 0; sg < nseg && jF >= 0 && (gd || jG >= 0); ++sg) {
-    const int64_t o = (p * Smax + sg) * NC;
-    if (sg + 1 == nseg) {
-      Ychi = lastF[o + jF];
-      YB = gd ? gyb[p] : lastG[o + jG];
-    } else {
-      const int a = segF[o + jF], b = gd ? 0 : segG[o + jG];
-      jF = a;
-      jG = b;
-    }
-  }
-  if (jF < 0 || (!gd && jG < 0) || !isfinite(Ychi) || !isfinite(YB)) {
-#ifdef LZQ_ODE_TP_DEBUG
-    printf("tp point %lld: stitching with J = %d failed (chains %d %d, %lld segments)\n", (long long)p, J, jF, jG,
-           (long long)nseg);
-#endif
-    return;
-  }
-  c.phase = kTpExact;
-  ctl[p] = c;
-  skip[p] = 1;
-  const double m = pts[p].m_chi_GeV;
-  lzq_yield r;
-  const double nB0 = YB * kS0M3, nDM0 = Ychi * kS0M3;  // fpy:412-417
-  r.Y_B = YB;
-  r.Y_chi = Ychi;
-  r.rho_B_kg_m3 = nB0 * kMProtonKg;
-  r.rho_DM_kg_m3 = nDM0 * (m * kGeVToKg);
-  r.DM_over_B = r.rho_DM_kg_m3 / pymax(r.rho_B_kg_m3, 1e-300);
-  r.P_used = pts[p].P_chi_to_B;
-  out[p] = r;
-  if (status) status[p] = LZQ_ODE_OK;
-}
-
-// skip[p] from the phase (stitched points only), and the optional update counts (< 0: iterated,
-// not stitched, integrated sequentially).
-__global__ __launch_bounds__(64) void ode_tp_finish_kernel(int64_t n, const TpCtl* __restrict__ ctl,
-                                                           int32_t* __restrict__ skip, int32_t* __restrict__ iters) {
-  const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  if (p >= n) return;
-  const TpCtl c = ctl[p];
-  const bool done = c.phase == kTpExact;
-  skip[p] = done ? 1 : 0;
-  if (iters) iters[p] = done ? c.iters : -c.iters;
-}
-
-// ---------------------------------------------------------------------------------------
 // Converged quadrature form of the sigma_v = 0 fallback (opt-in; lzq_ode_quadrature).
 // With sigma_v = 0 both equations of rhs (fpy:270-286) are linear with known integrating
 // factors: beta = gamma_w H / (H x) = gamma_w / x, so
@@ -2927,154 +1351,6 @@ int launch_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int
   return rc ? rc : rf;
 }
 
-// lzq_ode_integrate_tp: the time-parallel iteration (ode_tp_*_kernel) for batches of <= kTpMaxPoints
-// points, then the sequential launches for the points it did not finish (skip mask).  Intervals
-// of g_ode_tp_interval steps, more when max_steps would need over kTpMaxIntervals of them.
-constexpr int64_t kTpMaxPoints = 64;
-constexpr int64_t kTpMaxIntervals = 1 << 16;
-constexpr int32_t kTpMaxIters = 32;
-constexpr double kTpTol = 1e-14;  // largest relative node correction of a converged iteration
-int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, const int32_t* d_tidx,
-                        const double* d_work, int64_t max_steps, lzq_yield* d_out, int32_t* d_status,
-                        int32_t* d_iters, hipStream_t s, const char* fn) {
-  // node arrays for max_steps at the default interval length, at most kTpMaxIntervals per point
-  // (a point whose N needs more takes longer intervals, ode_tp_init_kernel)
-  const int64_t L = lzq::g_ode_tp_interval;
-  const int64_t Mmax = std::min<int64_t>((max_steps + L - 1) / L, kTpMaxIntervals);
-  if (n > kTpMaxPoints || Mmax < 2) {  // nothing to cut: the sequential path alone
-    if (d_iters) {
-      int rc = hip_check(hipMemsetAsync(d_iters, 0, sizeof(int32_t) * (size_t)n, s), fn);
-      if (rc) return rc;
-    }
-    return launch_integrate<false>(d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, s, fn);
-  }
-  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  const int64_t Smax = (Mmax + lzq::kTpSeg - 1) / lzq::kTpSeg;
-  const bool round3 = 2 * sizeof(double) * (size_t)n * (size_t)Mmax * (size_t)(2 * lzq::kTpJ3 + 1) <= lzq::kTpCandBytes;
-  const int64_t NC2 = 2 * (round3 ? lzq::kTpJ3 : lzq::kTpJ2) + 1;
-  const size_t b_nodes = up(sizeof(lzq::TpNode) * (size_t)n * (size_t)(Mmax + 1));
-  const size_t b_ends = up(sizeof(lzq::TpEnd) * (size_t)n * (size_t)Mmax);
-  const size_t b_ctl = up(sizeof(lzq::TpCtl) * (size_t)n);
-  const size_t b_skip = up(sizeof(int32_t) * (size_t)n);
-  const size_t b_cand = up(sizeof(double) * (size_t)n * (size_t)Mmax * (size_t)NC2);  // per chain
-  const size_t b_segi = up(sizeof(int32_t) * (size_t)n * (size_t)Smax * (size_t)NC2);
-  const size_t b_segv = up(sizeof(double) * (size_t)n * (size_t)Smax * (size_t)NC2);
-  const int64_t Bmax = (Mmax + lzq::kTpBlk - 1) / lzq::kTpBlk;
-  const size_t b_loc = up(sizeof(lzq::TpMap) * (size_t)n * (size_t)Mmax);
-  const size_t b_agg = up(sizeof(lzq::TpMap) * (size_t)n * (size_t)Bmax);
-  const size_t b_bout = up(sizeof(lzq::TpBlkOut) * (size_t)n * (size_t)Bmax);
-  const size_t b_gd = up(sizeof(int32_t) * (size_t)n), b_gy = up(sizeof(double) * (size_t)n);
-  char* buf = nullptr;
-  int rc = hip_check(hipMallocAsync((void**)&buf, b_nodes + b_ends + b_ctl + b_skip + 2 * (b_cand + b_segi + b_segv) +
-                                                       b_loc + b_agg + b_bout + b_gd + b_gy,
-                                    s),
-                     fn);
-  if (rc) return rc;
-  char* q = buf;
-  auto take = [&](size_t b) {
-    char* r = q;
-    q += b;
-    return r;
-  };
-  auto* nodes = reinterpret_cast<lzq::TpNode*>(take(b_nodes));
-  auto* ends = reinterpret_cast<lzq::TpEnd*>(take(b_ends));
-  auto* ctl = reinterpret_cast<lzq::TpCtl*>(take(b_ctl));
-  auto* skip = reinterpret_cast<int32_t*>(take(b_skip));
-  auto* candF = reinterpret_cast<double*>(take(b_cand));
-  auto* candG = reinterpret_cast<double*>(take(b_cand));
-  auto* segF = reinterpret_cast<int32_t*>(take(b_segi));
-  auto* segG = reinterpret_cast<int32_t*>(take(b_segi));
-  auto* lastF = reinterpret_cast<double*>(take(b_segv));
-  auto* lastG = reinterpret_cast<double*>(take(b_segv));
-  auto* loc = reinterpret_cast<lzq::TpMap*>(take(b_loc));
-  auto* agg = reinterpret_cast<lzq::TpMap*>(take(b_agg));
-  auto* bout = reinterpret_cast<lzq::TpBlkOut*>(take(b_bout));
-  auto* gdone = reinterpret_cast<int32_t*>(take(b_gd));
-  auto* gyb = reinterpret_cast<double*>(take(b_gy));
-  hipLaunchKernelGGL(lzq::ode_tp_init_kernel, dim3((unsigned)n), dim3(256), 0, s, d_points, d_ode, d_tidx, d_work,
-                     max_steps, L, Mmax, nodes, ctl);
-  rc = hip_check(hipGetLastError(), fn);
-  if (rc == LZQ_OK && Mmax >= lzq::kTpGuessMin) {
-    hipLaunchKernelGGL(lzq::ode_tp_guess_kernel, dim3((unsigned)n), dim3(256), 0, s, d_points, d_ode, d_tidx, d_work,
-                       max_steps, L, Mmax, nodes, ctl);
-    rc = hip_check(hipGetLastError(), fn);
-  }
-  const unsigned ib = (unsigned)((n * Mmax + 63) / 64);
-  for (int32_t it = 0; it < kTpMaxIters && rc == LZQ_OK; ++it) {
-    hipLaunchKernelGGL(lzq::ode_tp_interval_kernel, dim3(ib), dim3(64), 0, s, d_points, d_ode, n, d_tidx, d_work,
-                       max_steps, L, Mmax, nodes, ends, ctl);
-    rc = hip_check(hipGetLastError(), fn);
-    if (rc) break;
-    hipLaunchKernelGGL(lzq::ode_tp_scan_local_kernel, dim3((unsigned)Bmax, (unsigned)n), dim3(lzq::kTpBlk), 0, s, Mmax,
-                       Bmax, nodes, ends, ctl, loc, agg, bout);
-    rc = hip_check(hipGetLastError(), fn);
-    if (rc) break;
-    hipLaunchKernelGGL(lzq::ode_tp_scan_apply_kernel, dim3((unsigned)Bmax, (unsigned)n), dim3(lzq::kTpBlk), 0, s, Mmax,
-                       Bmax, nodes, ends, ctl, loc, agg, bout);
-    rc = hip_check(hipGetLastError(), fn);
-    if (rc) break;
-    hipLaunchKernelGGL(lzq::ode_tp_scan_finish_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, n, Bmax, ctl,
-                       bout, kTpMaxIters, kTpTol);
-    rc = hip_check(hipGetLastError(), fn);
-  }
-  // exact stitching, J = kTpJ1 then kTpJ2 for the points the first round did not finish
-  auto stitch = [&](auto Jc, bool cands) {
-    constexpr int J = decltype(Jc)::value, NC = 2 * J + 1;
-    constexpr bool kStride = J > 32;
-    const int64_t full = (n * Mmax * NC + 63) / 64;
-    const int64_t cb = kStride ? std::min<int64_t>(full, 4096) : full;
-    int r = LZQ_OK;
-    if (cands) {
-      hipLaunchKernelGGL((lzq::ode_tp_cand_kernel<J, kStride>), dim3((unsigned)cb), dim3(64), 0, s,
-                         d_points, d_ode, n, d_tidx, d_work, max_steps, Mmax, nodes, ctl, candF, candG);
-      r = hip_check(hipGetLastError(), fn);
-      if (r) return r;
-    }
-    hipLaunchKernelGGL(lzq::ode_tp_seg_kernel<J>, dim3((unsigned)((n * Smax * NC + 63) / 64)), dim3(64), 0, s, n, Mmax,
-                       Smax, nodes, ctl, candF, candG, segF, segG, lastF, lastG);
-    r = hip_check(hipGetLastError(), fn);
-    if (r) return r;
-    hipLaunchKernelGGL(lzq::ode_tp_stitch_kernel<J>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, d_points, n, Smax,
-                       ctl, segF, segG, lastF, lastG, d_out, d_status, skip, (const int32_t*)gdone, (const double*)gyb,
-                       (int32_t)!cands);
-    return hip_check(hipGetLastError(), fn);
-  };
-  // the Y_B chain on its own (its candidates fit the buffers of either last round)
-  auto gstitch = [&](auto Jc) {
-    constexpr int JG = decltype(Jc)::value, NC = 2 * JG + 1;
-    constexpr int NCH = (NC + lzq::kTpGChunk - 1) / lzq::kTpGChunk;
-    hipLaunchKernelGGL(lzq::ode_tp_gcand_kernel<JG>, dim3((unsigned)((n * Mmax * NCH + 63) / 64)), dim3(64), 0, s,
-                       d_points, d_ode, n, d_tidx, d_work, max_steps, Mmax, nodes, ctl, candG);
-    int r = hip_check(hipGetLastError(), fn);
-    if (r) return r;
-    hipLaunchKernelGGL(lzq::ode_tp_gseg_kernel<JG>, dim3((unsigned)((n * Smax * NC + 63) / 64)), dim3(64), 0, s, n, Mmax,
-                       Smax, nodes, ctl, candG, segG, lastG);
-    r = hip_check(hipGetLastError(), fn);
-    if (r) return r;
-    hipLaunchKernelGGL(lzq::ode_tp_gstitch_kernel<JG>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, n, Smax, ctl,
-                       segG, lastG, gdone, gyb);
-    return hip_check(hipGetLastError(), fn);
-  };
-  // J = 4 for both chains; then, for the points it did not finish, the Y_B chain alone at +-32
-  // ulps and the J = 4 walk again over the Y_chi candidates it has (candF is untouched); then
-  // J = 32 and J = 256 for both chains (a Y_B chain already stitched is not needed there)
-  if (rc == LZQ_OK) rc = hip_check(hipMemsetAsync(gdone, 0, sizeof(int32_t) * (size_t)n, s), fn);
-  if (rc == LZQ_OK) rc = stitch(std::integral_constant<int, lzq::kTpJ1>(), true);
-  if (rc == LZQ_OK) rc = gstitch(std::integral_constant<int, lzq::kTpJG>());
-  if (rc == LZQ_OK) rc = stitch(std::integral_constant<int, lzq::kTpJ1>(), false);
-  if (rc == LZQ_OK) rc = stitch(std::integral_constant<int, lzq::kTpJ2>(), true);
-  if (rc == LZQ_OK && round3) rc = stitch(std::integral_constant<int, lzq::kTpJ3>(), true);
-  if (rc == LZQ_OK) {
-    hipLaunchKernelGGL(lzq::ode_tp_finish_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, n, ctl, skip,
-                       d_iters);
-    rc = hip_check(hipGetLastError(), fn);
-  }
-  if (rc == LZQ_OK)
-    rc = launch_integrate<false>(d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, s, fn, skip);
-  const int rf = hip_check(hipFreeAsync(buf, s), fn);
-  return rc ? rc : rf;
-}
-
 int hip_check(hipError_t e, const char* what) {
   if (e == hipSuccess) return LZQ_OK;
   char buf[256];
@@ -3102,6 +1378,16 @@ int check_ws(int64_t n, const double* d_work, int64_t work_doubles, const char* 
 }
 
 }  // namespace
+
+int lzq_ode_launch_sequential(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n,
+                              const int32_t* d_tidx, const double* d_work, int64_t max_steps, lzq_yield* d_out,
+                              int32_t* d_status, hipStream_t s, const char* fn, const int32_t* d_skip) {
+  return launch_integrate<false>(d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, s, fn, d_skip);
+}
+int lzq_ode_hip_check(hipError_t e, const char* what) { return hip_check(e, what); }
+int lzq_ode_check_ws(int64_t n, const double* d_work, int64_t work_doubles, const char* fn, int64_t per_table) {
+  return check_ws(n, d_work, work_doubles, fn, per_table);
+}
 
 extern "C" {
 
@@ -3151,19 +1437,6 @@ int lzq_ode_integrate_shared(const lzq_point* d_points, const lzq_ode_params* d_
   if (n == 0) return LZQ_OK;
   return launch_integrate<false>(d_points, d_ode, n, d_table_index, d_work, max_steps, d_out, d_status,
                                  (hipStream_t)stream, "lzq_ode_integrate_shared");
-}
-
-int lzq_ode_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n,
-                         const int32_t* d_table_index, int64_t n_tables, const double* d_work, int64_t work_doubles,
-                         int64_t max_steps, lzq_yield* d_out, int32_t* d_status, int32_t* d_iters, void* stream) {
-  if (n < 0 || n_tables < 0 || max_steps < 0 || (n > 0 && (!d_points || !d_ode || !d_out)) ||
-      (d_table_index && n > 0 && n_tables == 0))
-    return lzq_set_error(LZQ_EINVAL, "lzq_ode_integrate_tp: bad arguments");
-  int rc = check_ws(d_table_index ? n_tables : n, d_work, work_doubles, "lzq_ode_integrate_tp");
-  if (rc) return rc;
-  if (n == 0) return LZQ_OK;
-  return launch_integrate_tp(d_points, d_ode, n, d_table_index, d_work, max_steps, d_out, d_status, d_iters,
-                             (hipStream_t)stream, "lzq_ode_integrate_tp");
 }
 
 int lzq_ode_quadrature(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n,

@@ -666,7 +666,7 @@ def test_ode_linear_waves_degenerate_step(gpu_engine):
 
 
 def _split_step(m, T_lo, T_hi, T_p):
-    """Host restatement of the integrator's first split step (lzq_ode.hip branch_x and the linear
+    """Host restatement of the integrator's first split step (lzq_ode.h branch_x and the linear
     waves' k_split): the step k with x_k < x_b <= x_k + h, x_b the first x whose T = m (1/x) is no
     longer > m/3 (same IEEE operations)."""
     x0, x1 = m / T_hi, m / max(T_lo, 1e-30)

@@ -11,7 +11,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = "baryon-and-dark-matter-densities-from-bounce--sourced-distributed-landau--zener-transport_amd"
-SOURCES = ["lzq_kernels.hip", "lzq_aov.hip", "lzq_ode.hip", "lzq_propagator.hip", "lzq_profile.hip"]
+SOURCES = ["lzq_kernels.hip", "lzq_aov.hip", "lzq_ode.hip", "lzq_ode_tp.hip", "lzq_propagator.hip", "lzq_profile.hip"]
 KEYS = ("VGPRs", "AGPRs", "TotalSGPRs", "ScratchSize [bytes/lane]", "Occupancy [waves/SIMD]", "SGPRs Spill",
         "VGPRs Spill", "LDS Size [bytes/block]")
 

@@ -83,7 +83,8 @@ LZQ_NZ, LZQ_Z_MAX = 1200, 30.0  # fpy:142 AoverVKernel defaults, main()'s grid (
 LZQ_NZ_MAX = 1 << 22
 ODE_NT_MAX = 1 << 20
 REUSE_TABLE_HEADER = 6  # LZQ_REUSE_TABLE_HEADER
-TUNE_EXP, TUNE_TRUNCATE, TUNE_ODE_COOP, TUNE_ODE_LAUNCH_STEPS, TUNE_PROFILE_FLAT, TUNE_ODE_TP_INTERVAL = 0, 1, 2, 3, 4, 5  # enum lzq_tune_key
+(TUNE_EXP, TUNE_TRUNCATE, TUNE_ODE_COOP, TUNE_ODE_LAUNCH_STEPS, TUNE_PROFILE_FLAT, TUNE_ODE_TP_INTERVAL,
+ TUNE_ODE_TABLE_WIDE) = 0, 1, 2, 3, 4, 5, 6  # enum lzq_tune_key
 ODE_MAX_LAUNCHES = 65536  # lzq_ode_*: max_steps <= 65536 x 2^(launch log2)
 # tuning state that changes result bits (the inner-loop exponential, ~1e-14): part of the
 # sweep checkpoint key (sweep.spec_key); Engine.tune_exp keeps it current

@@ -63,11 +63,16 @@ template <int EXPV>
 __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void ode_aov_table_aov_kernel(
     const lzq_point* __restrict__ pts, const lzq_aov_params* __restrict__ aov, int64_t n, int32_t nt,
     const ZNode* __restrict__ zt, int32_t nzp, const double* __restrict__ gtab, const double* __restrict__ Tlo,
-    const double* __restrict__ Thi, double* __restrict__ ws, int truncate) {
+    const double* __restrict__ Thi, double* __restrict__ ws, int truncate,
+    int chunks) {
   __shared__ double lds_tab[kTabN];
   const double* tab = stage_table<EXPV>(gtab, lds_tab);
   const int lane = threadIdx.x & (kWaveSize - 1);
-  const int64_t idx = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  // chunks > 1 (few tables, LZQ_TUNE_ODE_TABLE_WIDE): the point's 64-knot groups spread over
+  // `chunks` wavefronts (group g on wave g mod chunks) -- each group's operations as with one wave
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int64_t idx = wave / chunks;
+  const int chunk = (int)(wave - idx * chunks);
   if (idx >= n) return;  // wave-uniform
   const lzq_point pt = pts[idx];
   const double Tp = uniform(pt.T_p_GeV), B = uniform(pt.beta_over_H);  // fpy:211 y_of_T(T, cfg.T_p, cfg.beta/H)
@@ -79,7 +84,7 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void ode_aov_table_aov_kerne
   const double pref0 = s.pref0, cneg = s.cneg;
   const int64_t ws_pt = 4 * (int64_t)nt;
   double* w = ws + idx * ws_pt;
-  for (int base = 0; base < nt; base += kWaveSize) {
+  for (int base = chunk * kWaveSize; base < nt; base += kWaveSize * chunks) {
     const int i = base + lane;
     const int ii = i < nt ? i : nt - 1;
     const double T = linspace_at(T_lo, T_hi, stepT, ii, nt);
@@ -117,14 +122,14 @@ int lzq::launch_yields_points_aov(int exp_variant, bool default_grid, const lzq_
 int lzq::launch_ode_aov_tables_aov(int exp_variant, const lzq_point* d_points, const lzq_aov_params* d_aov,
                                    int64_t n, int32_t nt, const ZNode* zt, int32_t nzp, const double* gtab,
                                    const double* d_T_lo, const double* d_T_hi, double* d_work, int truncate,
-                                   hipStream_t s) {
-  const int64_t nb = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+                                   hipStream_t s, int chunks) {
+  const int64_t nb = (n * chunks + kWavesPerBlock - 1) / kWavesPerBlock;
   if (exp_variant == kExpTable)
     hipLaunchKernelGGL(ode_aov_table_aov_kernel<kExpTable>, dim3((unsigned)nb), dim3(kBlock), 0, s, d_points, d_aov,
-                       n, nt, zt, nzp, gtab, d_T_lo, d_T_hi, d_work, truncate);
+                       n, nt, zt, nzp, gtab, d_T_lo, d_T_hi, d_work, truncate, chunks);
   else
     hipLaunchKernelGGL(ode_aov_table_aov_kernel<kExpPoly11>, dim3((unsigned)nb), dim3(kBlock), 0, s, d_points, d_aov,
-                       n, nt, zt, nzp, gtab, d_T_lo, d_T_hi, d_work, truncate);
+                       n, nt, zt, nzp, gtab, d_T_lo, d_T_hi, d_work, truncate, chunks);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? LZQ_OK : lzq_set_error(LZQ_EHIP, hipGetErrorString(e));
 }

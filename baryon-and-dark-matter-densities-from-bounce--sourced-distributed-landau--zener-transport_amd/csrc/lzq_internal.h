@@ -32,7 +32,7 @@ int launch_yields_points_aov(int exp_variant, bool default_grid, const lzq_point
                              lzq_yield* d_out, int truncate, hipStream_t s);
 int launch_ode_aov_tables_aov(int exp_variant, const lzq_point* d_points, const lzq_aov_params* d_aov, int64_t n,
                               int32_t nt, const ZNode* zt, int32_t nzp, const double* gtab, const double* d_T_lo,
-                              const double* d_T_hi, double* d_work, int truncate, hipStream_t s);
+                              const double* d_T_hi, double* d_work, int truncate, hipStream_t s, int chunks = 1);
 
 // Longest-first launch order (lzq_propagator.hip): cost bins per point (0 = costliest, kCostBins
 // of them) and their histogram -> offs (kCostBins scratch) and order[n] (a counting sort: one
@@ -45,6 +45,7 @@ int launch_bin_order(const int32_t* bins, const int32_t* hist, int32_t* offs, in
 extern int g_ode_coop;
 extern int g_ode_launch_log2;
 extern int g_ode_tp_interval;  // lzq_tune(LZQ_TUNE_ODE_TP_INTERVAL): steps per lzq_ode_integrate_tp interval
+extern int g_ode_table_wide;   // lzq_tune(LZQ_TUNE_ODE_TABLE_WIDE): few ODE tables built a wavefront wide
 // lzq_tune(LZQ_TUNE_PROFILE_FLAT) state, read by lzq_profile.hip's launch
 extern int g_profile_flat;
 

@@ -277,11 +277,16 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void ode_aov_table_kernel(co
                                                                                const double* __restrict__ gtab,
                                                                                const double* __restrict__ Tlo,
                                                                                const double* __restrict__ Thi,
-                                                                               double* __restrict__ ws, int truncate) {
+                                                                               double* __restrict__ ws, int truncate,
+    int chunks) {
   __shared__ double lds_tab[kTabN];
   const double* tab = stage_table<EXPV>(gtab, lds_tab);
   const int lane = threadIdx.x & (kWaveSize - 1);
-  const int64_t idx = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  // chunks > 1 (few tables, LZQ_TUNE_ODE_TABLE_WIDE): the point's 64-knot groups spread over
+  // `chunks` wavefronts (group g on wave g mod chunks) -- each group's operations as with one wave
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int64_t idx = wave / chunks;
+  const int chunk = (int)(wave - idx * chunks);
   if (idx >= n) return;  // wave-uniform
   const lzq_point pt = pts[idx];
   // every per-point value is wave-uniform: pinned in SGPRs (readfirstlane) so that the z-loop
@@ -294,7 +299,7 @@ __global__ __launch_bounds__(kBlock, LZQ_MIN_WAVES) void ode_aov_table_kernel(co
   const double pref0 = uniform(s.pref0), cneg = uniform(s.cneg);
   const int64_t ws_pt = 4 * (int64_t)nt;
   double* w = ws + idx * ws_pt;
-  for (int base = 0; base < nt; base += kWaveSize) {
+  for (int base = chunk * kWaveSize; base < nt; base += kWaveSize * chunks) {
     const int i = base + lane;
     const int ii = i < nt ? i : nt - 1;
     const double T = linspace_at(T_lo, T_hi, stepT, ii, nt);
@@ -553,7 +558,9 @@ int lzq::launch_ode_aov_tables(const lzq_point* d_points, int64_t n, const doubl
   DevZGrid g;
   int rc = zgrid_for(nz, z_max, g, &dev);
   if (rc) return rc;
-  const int64_t nb = blocks_for(n, lzq::kWavesPerBlock);
+  // few tables: one wavefront per 64 knots (LZQ_TUNE_ODE_TABLE_WIDE; the same bits), else one per table
+  const int chunks = ((lzq::g_ode_table_wide & 1) && n <= 4096) ? (int)((nt + lzq::kWaveSize - 1) / lzq::kWaveSize) : 1;
+  const int64_t nb = blocks_for(n * chunks, lzq::kWavesPerBlock);
   if (nb > kMaxGrid) return fail(LZQ_EINVAL, "lzq_ode_tables: n too large");
   // The ODE tables always use the exact-underflow truncation of the z-sums: it is bit-identical
   // to the dense sum (tests/test_gpu_parity.py::test_truncation_is_bit_identical) and this path
@@ -561,13 +568,13 @@ int lzq::launch_ode_aov_tables(const lzq_point* d_points, int64_t n, const doubl
   const int truncate = g.monotone ? 1 : 0;
   if (d_aov)  // the A/V kernel's own parameters (lzq_aov.hip)
     return lzq::launch_ode_aov_tables_aov(g_exp_variant, d_points, d_aov, n, nt, g.zt, g.nzp, exp_table(dev), d_T_lo,
-                                          d_T_hi, d_work, truncate, stream);
+                                          d_T_hi, d_work, truncate, stream, chunks);
   if (g_exp_variant == lzq::kExpTable)
     hipLaunchKernelGGL(lzq::ode_aov_table_kernel<lzq::kExpTable>, dim3((unsigned)nb), dim3(lzq::kBlock), 0, stream,
-                       d_points, n, nt, g.zt, g.nzp, exp_table(dev), d_T_lo, d_T_hi, d_work, truncate);
+                       d_points, n, nt, g.zt, g.nzp, exp_table(dev), d_T_lo, d_T_hi, d_work, truncate, chunks);
   else
     hipLaunchKernelGGL(lzq::ode_aov_table_kernel<lzq::kExpPoly11>, dim3((unsigned)nb), dim3(lzq::kBlock), 0, stream,
-                       d_points, n, nt, g.zt, g.nzp, exp_table(dev), d_T_lo, d_T_hi, d_work, truncate);
+                       d_points, n, nt, g.zt, g.nzp, exp_table(dev), d_T_lo, d_T_hi, d_work, truncate, chunks);
   LZQ_HIP(hipGetLastError());
   return LZQ_OK;
 }
@@ -617,6 +624,12 @@ int lzq_tune(int32_t key, int32_t value) {
     if (value != 0 && value != 1) return fail(LZQ_EINVAL, "lzq_tune: profile_flat must be 0 or 1, got %d", value);
     int prev = lzq::g_profile_flat;
     lzq::g_profile_flat = value;
+    return prev;
+  }
+  if (key == LZQ_TUNE_ODE_TABLE_WIDE) {
+    if (value < 0 || value > 3) return fail(LZQ_EINVAL, "lzq_tune: ode_table_wide must be in 0..3, got %d", value);
+    int prev = lzq::g_ode_table_wide;
+    lzq::g_ode_table_wide = value;
     return prev;
   }
   if (key == LZQ_TUNE_ODE_TP_INTERVAL) {

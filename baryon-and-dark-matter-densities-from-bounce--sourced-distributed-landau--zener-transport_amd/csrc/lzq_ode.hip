@@ -22,6 +22,7 @@ namespace lzq {
 int g_ode_coop = 1;          // lzq_tune(LZQ_TUNE_ODE_COOP)
 int g_ode_launch_log2 = 24;  // lzq_tune(LZQ_TUNE_ODE_LAUNCH_STEPS): <= 2^24 Radau steps per launch
 int g_ode_tp_interval = 64;  // lzq_tune(LZQ_TUNE_ODE_TP_INTERVAL): steps per lzq_ode_integrate_tp interval
+int g_ode_table_wide = 3;    // lzq_tune(LZQ_TUNE_ODE_TABLE_WIDE): few tables built wide (1: A/V, 2: spline)
 
 // ---------------------------------------------------------------------------------------
 // kernels
@@ -125,6 +126,132 @@ __global__ __launch_bounds__(kOdeBlock) void ode_spline_kernel(const lzq_point* 
   }
   w[ws_pt - 4] = (double)N;  // the table's knot count, in its spare doubles (ode_table_ok)
   if (status) status[i] = LZQ_ODE_OK;
+}
+
+// ode_spline_kernel's table, one wavefront per point (round 6): for batches of few tables (the
+// CLI's single point, a sweep's shared tables), where one lane per point leaves the table build a
+// serial chain of ~800 global-memory rows.  Per knot, everything but the two short recurrences is
+// independent: the lanes form 64 knots' (a, b, c, r) of the slope system (and, going back, their
+// PPoly coefficients) side by side; lane 0 runs only the forward elimination (den, c', d') and the
+// back substitution (s_k = d'_k - c'_k s_{k+1}).  Every value is formed by the same operations on
+// the same operands as in ode_spline_kernel (dx[k-1] and slope[k-1] recomputed from the knots, as
+// that kernel computed them one row earlier), so the table is the same, bit for bit.
+constexpr int kSplWaves = 4;  // points (wavefronts) per block
+__global__ __launch_bounds__(64 * kSplWaves) void ode_spline_wave_kernel(const lzq_point* __restrict__ pts, int64_t n,
+                                                                         int32_t nt, const double* __restrict__ Tlo,
+                                                                         const double* __restrict__ Thi,
+                                                                         double* __restrict__ ws,
+                                                                         int32_t* __restrict__ status) {
+  __shared__ double s_abcr[kSplWaves][4][64];
+  __shared__ double s_s[kSplWaves][65];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * kSplWaves + wv;
+  if (i >= n) return;  // wave-uniform
+  const lzq_point pt = pts[i];
+  const double T_lo = Tlo ? Tlo[i] : pt.T_min_over_Tp * pt.T_p_GeV;
+  const double T_hi = Thi ? Thi[i] : pt.T_max_over_Tp * pt.T_p_GeV;
+  const int N = nt;
+  const int64_t ws_pt = 4 * (int64_t)N;
+  const double stepT = (T_hi - T_lo) / (double)(N - 1);
+  double* w = ws + i * ws_pt;
+  auto X = [&](int k) { return linspace_at(T_lo, T_hi, stepT, k, N); };
+  auto Yk = [&](int k) { return k < N - 1 ? w[4 * k + 3] : w[ws_pt - 1]; };
+  // ode_grid_ok, its comparisons spread over the lanes
+  bool ok = true;
+  for (int k = 1 + lane; k < N; k += 64) ok = ok && (X(k) > X(k - 1));
+  if (!__all(ok)) {
+    if (lane == 0 && status) status[i] = LZQ_ODE_BAD_GRID;
+    return;
+  }
+  auto sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  double* A = s_abcr[wv][0];
+  double* Bv = s_abcr[wv][1];
+  double* Cv = s_abcr[wv][2];
+  double* Rv = s_abcr[wv][3];
+  // first row (lane 0, as ode_spline_kernel)
+  double cpm1 = 0.0, dpm1 = 0.0;
+  if (lane == 0) {
+    const double dxm1 = X(1) - X(0), slm1 = (Yk(1) - Yk(0)) / dxm1;
+    const double dx1 = X(2) - X(1), sl1 = (Yk(2) - Yk(1)) / dx1;
+    const double d = X(2) - X(0);
+    const double r = ((dxm1 + 2.0 * d) * dx1 * slm1 + (dxm1 * dxm1) * sl1) / d;
+    cpm1 = d / dx1;
+    dpm1 = r / dx1;
+    w[0] = cpm1;
+    w[1] = dpm1;
+  }
+  // forward sweep over rows 1 .. N-2, 64 at a time
+  for (int k0 = 1; k0 < N - 1; k0 += 64) {
+    const int k = k0 + lane;
+    if (k < N - 1) {
+      const double dxm1 = X(k) - X(k - 1), slm1 = (Yk(k) - Yk(k - 1)) / dxm1;
+      const double dxk = X(k + 1) - X(k), slk = (Yk(k + 1) - Yk(k)) / dxk;
+      A[lane] = dxk;
+      Bv[lane] = 2.0 * (dxm1 + dxk);
+      Cv[lane] = dxm1;
+      Rv[lane] = 3.0 * (dxk * slm1 + dxm1 * slk);
+    }
+    sync();
+    if (lane == 0) {
+      const int nk = N - 1 - k0 < 64 ? N - 1 - k0 : 64;
+      for (int j = 0; j < nk; ++j) {
+        const double a = A[j];
+        const double den = Bv[j] - a * cpm1;
+        cpm1 = Cv[j] / den;
+        dpm1 = (Rv[j] - a * dpm1) / den;
+        w[4 * (k0 + j) + 0] = cpm1;
+        w[4 * (k0 + j) + 1] = dpm1;
+      }
+    }
+    sync();
+  }
+  // last row (not-a-knot) and back substitution (lane 0), the coefficients of 64 intervals at a
+  // time (all lanes)
+  double s_next = 0.0;
+  if (lane == 0) {
+    const double dxm1 = X(N - 1) - X(N - 2), slm1 = (Yk(N - 1) - Yk(N - 2)) / dxm1;  // dx[-1], slope[-1]
+    const double dx2 = X(N - 2) - X(N - 3), sl2 = (Yk(N - 2) - Yk(N - 3)) / dx2;    // dx[-2], slope[-2]
+    const double d = X(N - 1) - X(N - 3);
+    const double r = ((dxm1 * dxm1) * sl2 + (2.0 * d + dxm1) * dx2 * slm1) / d;
+    s_next = (r - d * dpm1) / (dx2 - d * cpm1);
+    s_s[wv][64] = s_next;
+  }
+  double* Sv = s_s[wv];
+  for (int top = N - 2; top >= 0; top -= 64) {
+    const int nk = top + 1 < 64 ? top + 1 : 64;  // knots top, top-1, ..., top-nk+1 (slot j: knot top - j)
+    if (lane == 0) {
+      // Sv[64] holds s of knot top + 1
+      double sn = Sv[64];
+      for (int j = 0; j < nk; ++j) {
+        const int k = top - j;
+        const double sk = w[4 * k + 1] - w[4 * k + 0] * sn;
+        Sv[j] = sk;
+        sn = sk;
+      }
+    }
+    sync();
+    if (lane < nk) {
+      const int k = top - lane;
+      const double sk = Sv[lane], sn = lane == 0 ? Sv[64] : Sv[lane - 1];
+      const double dxk = X(k + 1) - X(k);
+      const double slk = (Yk(k + 1) - w[4 * k + 3]) / dxk;
+      const double t = (sk + sn - 2.0 * slk) / dxk;
+      w[4 * k + 0] = t / dxk;
+      w[4 * k + 1] = (slk - sk) / dxk - t;
+      w[4 * k + 2] = sk;
+    }
+    sync();
+    if (lane == 0) Sv[64] = Sv[nk - 1];
+    sync();
+  }
+  if (lane == 0) {
+    w[ws_pt - 4] = (double)N;
+    if (status) status[i] = LZQ_ODE_OK;
+  }
 }
 
 // tidx (optional): point i reads the spline table at ws[tidx[i] * kOdeWS] (tables shared by
@@ -1280,6 +1407,9 @@ __global__ __launch_bounds__(kOdeBlock) void ode_eval_kernel(lzq_point pt, lzq_o
 namespace {
 
 int64_t ode_blocks(int64_t n) { return (n + lzq::kOdeBlock - 1) / lzq::kOdeBlock; }
+// lzq_ode_tables: up to this many tables take ode_spline_wave_kernel (a wavefront each); more, one
+// lane each (ode_spline_kernel: the serial chains of 64 tables share a wavefront's issue)
+constexpr int64_t kSplineWaveMax = 4096;
 
 int hip_check(hipError_t e, const char* what);
 
@@ -1408,8 +1538,12 @@ int lzq_ode_tables(const lzq_point* d_points, int64_t n, const double* d_T_lo, c
   hipStream_t s = (hipStream_t)stream;
   rc = lzq::launch_ode_aov_tables(d_points, n, d_T_lo, d_T_hi, nt, nz, z_max, d_aov, d_work, s);
   if (rc) return rc;
-  hipLaunchKernelGGL(lzq::ode_spline_kernel, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, s, d_points, n,
-                     nt, d_T_lo, d_T_hi, d_work, d_status);
+  if (n <= kSplineWaveMax && (lzq::g_ode_table_wide & 2))  // few tables: a wavefront per table (same bits)
+    hipLaunchKernelGGL(lzq::ode_spline_wave_kernel, dim3((unsigned)((n + lzq::kSplWaves - 1) / lzq::kSplWaves)),
+                       dim3(64 * lzq::kSplWaves), 0, s, d_points, n, nt, d_T_lo, d_T_hi, d_work, d_status);
+  else
+    hipLaunchKernelGGL(lzq::ode_spline_kernel, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, s, d_points, n,
+                       nt, d_T_lo, d_T_hi, d_work, d_status);
   return hip_check(hipGetLastError(), "lzq_ode_tables");
 }
 

@@ -152,12 +152,62 @@ struct TpState {
   bool have;
 };
 
+// A regular step's stage data for one point (round 6): what tp_steps reads of its three stages
+// (ode_stage: lam, E2, S) and of Y_B's step map (yb_rec: c, d), formed by ode_tp_rows_kernel once per
+// call -- the stages depend on the point and x only, not on the state -- instead of in every
+// interval integration, candidate and update.  The same functions on the same x, so the same bits.
+// Layout per point: step k at (k mod L) * Mmax + k / L (the lanes of an interval launch, one
+// interval each, read consecutive rows); only points whose interval length is L (ctl.L) use them.
+struct TpRow {
+  double lam[3], E2[3], S[3], c, d;
+};
+constexpr size_t kTpRowBytes = size_t(1) << 31;  // row tables of one call, at most (else stages inline)
+#ifndef LZQ_ODE_TP_ROWS
+#define LZQ_ODE_TP_ROWS 1  // 0: every step forms its stages inline (the round-5 path; same bits)
+#endif
+
+__global__ __launch_bounds__(256) void ode_tp_rows_kernel(const lzq_point* __restrict__ pts,
+                                                          const lzq_ode_params* __restrict__ ode, int64_t n,
+                                                          const int32_t* __restrict__ tidx,
+                                                          const double* __restrict__ ws, int64_t max_steps, int64_t L,
+                                                          int64_t Mmax, const TpCtl* __restrict__ ctl,
+                                                          TpRow* __restrict__ rows) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t per = Mmax * L;
+  const int64_t p = g / per, rem = g - p * per;
+  if (p >= n) return;
+  const TpCtl c = ctl[p];
+  const int64_t r = rem / Mmax, m = rem - r * Mmax, k = m * L + r;  // lanes: consecutive intervals
+  if (c.phase != kTpIter || c.L != L || k >= c.N) return;
+  const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
+  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
+  const Radau R = radau_tableau();
+  const RadauH hA = radau_h(R, S.h);
+  const double xk = S.x0 + (double)k * S.h;  // tp_steps' x_k (its step counter is an exact double)
+  OdeStage sg[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) sg[j] = ode_stage(S.o, w, xk + R.c[j] * S.h);
+  const YbRec yr = yb_rec(hA, sg);
+  TpRow row;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    row.lam[j] = sg[j].lam;
+    row.E2[j] = sg[j].E2;
+    row.S[j] = sg[j].S;
+  }
+  row.c = yr.c;
+  row.d = yr.d;
+  rows[p * per + rem] = row;  // (a split step's row is formed too, and not read: tp_steps splits it)
+}
+
 // Steps [k0, k1) of the fixed-step sequence x_k = x0 + k h from state St, with ode_integrate_kernel's
 // per-lane operations (stages, Y_B map, Radau step, the T = m/3 split step, the predictor); D and C
 // accumulate the derivatives of the end state.  Returns false when a step needed tp_bridge.
+// rows (optional): the TpRow of step k0 of an interval, the next steps' rows `stride` apart (the
+// point's table at (k mod L) * Mmax + k / L: stride Mmax), for the regular steps.
 __device__ __forceinline__ bool tp_steps(const OdePoint& o, const double* __restrict__ w, double x0, double h,
                                          double xb, double xb_below, int64_t k0, int64_t k1, TpState& St, double& D,
-                                         double& C) {
+                                         double& C, const TpRow* __restrict__ rows = nullptr, int64_t stride = 0) {
   const Radau R = radau_tableau();
   const RadauH hA = radau_h(R, h);
   const bool riccati = LZQ_ODE_PREDICT && o.sigmav != 0.0;
@@ -186,11 +236,26 @@ __device__ __forceinline__ bool tp_steps(const OdePoint& o, const double* __rest
     auto part = [&](double xs, double hs, bool guess, bool own_h, bool block_start) {
       const RadauH hAs = own_h ? radau_h(R, hs) : hA;
       OdeStage sg[3];
+      double yc, yd;
+      if (rows && !own_h) {  // a regular step: its stage data from the row table
+        const TpRow& rw = rows[(k - k0) * stride];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) sg[j] = ode_stage(o, w, xs + R.c[j] * hs);
-      const YbRec yr = yb_rec(hAs, sg);
-      YB = __builtin_fma(yr.c, YB, o.Pf * yr.d);
-      C *= yr.c;
+        for (int j = 0; j < 3; ++j) {
+          sg[j].lam = rw.lam[j];
+          sg[j].E2 = rw.E2[j];
+          sg[j].S = rw.S[j];
+        }
+        yc = rw.c;
+        yd = rw.d;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) sg[j] = ode_stage(o, w, xs + R.c[j] * hs);
+        const YbRec yr = yb_rec(hAs, sg);
+        yc = yr.c;
+        yd = yr.d;
+      }
+      YB = __builtin_fma(yc, YB, o.Pf * yd);
+      C *= yc;
       const double Y0 = Ychi;
       if (block_start) guess = block_guess(R, hs, sg, Ychi, Zs);
       // (radau_step's convergence test reads NaN corrections as converged -- it never meets one on
@@ -225,7 +290,8 @@ __global__ __launch_bounds__(64) void ode_tp_interval_kernel(const lzq_point* __
                                                              const int32_t* __restrict__ tidx,
                                                              const double* __restrict__ ws, int64_t max_steps,
                                                              int64_t L, int64_t Mmax, const TpNode* __restrict__ nodes,
-                                                             TpEnd* __restrict__ ends, const TpCtl* __restrict__ ctl) {
+                                                             TpEnd* __restrict__ ends, const TpCtl* __restrict__ ctl,
+                                                             const TpRow* __restrict__ rows) {
   const int64_t g = (int64_t)blockIdx.x * 64 + threadIdx.x;
   const int64_t p = g / Mmax, m = g - p * Mmax;
   if (p >= n) return;
@@ -238,7 +304,8 @@ __global__ __launch_bounds__(64) void ode_tp_interval_kernel(const lzq_point* __
   const TpNode nd = nodes[p * (Mmax + 1) + m];
   TpState St{nd.Ychi, nd.YB, nd.Ychi, {nd.Ychi, nd.Ychi, nd.Ychi}, false};  // (the first step reads no predictor)
   double D = 1.0, C = 1.0;
-  const bool exact = tp_steps(S.o, w, S.x0, S.h, xb, nextafter(xb, -INFINITY), k0, k1, St, D, C);
+  const TpRow* rp = rows && c.L == L ? rows + p * Mmax * L + m : nullptr;  // interval m's first row
+  const bool exact = tp_steps(S.o, w, S.x0, S.h, xb, nextafter(xb, -INFINITY), k0, k1, St, D, C, rp, Mmax);
   ends[p * Mmax + m] = TpEnd{St.Ychi, St.YB, D, C, exact ? 1 : 0, 0};
 }
 
@@ -484,7 +551,8 @@ constexpr int32_t kTpExact = 3;
 __device__ __noinline__ void tp_cand_one(const lzq_point* __restrict__ pts, const lzq_ode_params* __restrict__ ode,
                                          const int32_t* __restrict__ tidx, const double* __restrict__ ws,
                                          int64_t max_steps, const TpNode* __restrict__ nd, const TpCtl& c, int64_t p,
-                                         int64_t m, int off, double* __restrict__ oF, double* __restrict__ oG) {
+                                         int64_t m, int off, double* __restrict__ oF, double* __restrict__ oG,
+                                         const TpRow* __restrict__ rp, int64_t stride) {
   const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
   const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
   const int64_t k0 = m * c.L, k1 = k0 + c.L < S.N ? k0 + c.L : S.N;
@@ -493,7 +561,7 @@ __device__ __noinline__ void tp_cand_one(const lzq_point* __restrict__ pts, cons
   TpState St{y0, b0, y0, {y0, y0, y0}, false};
   double D = 1.0, C = 1.0;
   const double xb = branch_x(S.o, S.x0, S.x1);
-  const bool exact = tp_steps(S.o, w, S.x0, S.h, xb, nextafter(xb, -INFINITY), k0, k1, St, D, C);
+  const bool exact = tp_steps(S.o, w, S.x0, S.h, xb, nextafter(xb, -INFINITY), k0, k1, St, D, C, rp, stride);
   *oF = exact ? St.Ychi : __builtin_nan("");
   *oG = exact ? St.YB : __builtin_nan("");
 }
@@ -506,7 +574,8 @@ __global__ __launch_bounds__(64) void ode_tp_cand_kernel(const lzq_point* __rest
                                                          const int32_t* __restrict__ tidx,
                                                          const double* __restrict__ ws, int64_t max_steps, int64_t Mmax,
                                                          const TpNode* __restrict__ nodes, const TpCtl* __restrict__ ctl,
-                                                         double* __restrict__ candF, double* __restrict__ candG) {
+                                                         double* __restrict__ candF, double* __restrict__ candG,
+                                                         const TpRow* __restrict__ rows, int64_t L) {
   constexpr int NC = 2 * J + 1;
   for (int64_t g = (int64_t)blockIdx.x * 64 + threadIdx.x; g < n * Mmax * NC; g += (int64_t)gridDim.x * 64) {
     const int64_t p = g / (Mmax * NC), rem = g - p * (Mmax * NC), m = rem / NC;
@@ -514,8 +583,10 @@ __global__ __launch_bounds__(64) void ode_tp_cand_kernel(const lzq_point* __rest
     const TpCtl c = ctl[p];
     if (c.phase == kTpDone && m < c.M) {
       const int64_t o = (p * Mmax + m) * NC + jj;
+      const TpRow* rp = rows && c.L == L ? rows + p * Mmax * L + m : nullptr;  // interval m's first row
       if constexpr (kStride) {
-        tp_cand_one(pts, ode, tidx, ws, max_steps, nodes + p * (Mmax + 1) + m, c, p, m, jj - J, candF + o, candG + o);
+        tp_cand_one(pts, ode, tidx, ws, max_steps, nodes + p * (Mmax + 1) + m, c, p, m, jj - J, candF + o, candG + o, rp,
+                    Mmax);
       } else {
         const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
         const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
@@ -525,7 +596,7 @@ __global__ __launch_bounds__(64) void ode_tp_cand_kernel(const lzq_point* __rest
         TpState St{y0, b0, y0, {y0, y0, y0}, false};
         double D = 1.0, C = 1.0;
         const double xb = branch_x(S.o, S.x0, S.x1);
-        const bool exact = tp_steps(S.o, w, S.x0, S.h, xb, nextafter(xb, -INFINITY), k0, k1, St, D, C);
+        const bool exact = tp_steps(S.o, w, S.x0, S.h, xb, nextafter(xb, -INFINITY), k0, k1, St, D, C, rp, Mmax);
         candF[o] = exact ? St.Ychi : __builtin_nan("");
         candG[o] = exact ? St.YB : __builtin_nan("");
       }
@@ -592,7 +663,8 @@ __global__ __launch_bounds__(64) void ode_tp_gcand_kernel(const lzq_point* __res
                                                           const int32_t* __restrict__ tidx,
                                                           const double* __restrict__ ws, int64_t max_steps,
                                                           int64_t Mmax, const TpNode* __restrict__ nodes,
-                                                          const TpCtl* __restrict__ ctl, double* __restrict__ candG) {
+                                                          const TpCtl* __restrict__ ctl, double* __restrict__ candG,
+                                                          const TpRow* __restrict__ rows, int64_t L) {
   constexpr int NC = 2 * JG + 1, NCH = (NC + kTpGChunk - 1) / kTpGChunk;
   const int64_t g = (int64_t)blockIdx.x * 64 + threadIdx.x;
   const int64_t p = g / (Mmax * NCH), rem = g - p * (Mmax * NCH), m = rem / NCH;
@@ -610,18 +682,29 @@ __global__ __launch_bounds__(64) void ode_tp_gcand_kernel(const lzq_point* __res
   const Radau R = radau_tableau();
   const RadauH hA = radau_h(R, S.h);
   const double xb = branch_x(S.o, S.x0, S.x1), xb_below = nextafter(xb, -INFINITY);
+  const TpRow* rp = rows && c.L == L ? rows + p * Mmax * L + m : nullptr;  // interval m's first row
+  int64_t k = k0;
   auto part = [&](double xs, double hs, bool own_h) {
-    const RadauH hAs = own_h ? radau_h(R, hs) : hA;
-    OdeStage sg[3];
+    double yc, yd;
+    if (rp && !own_h) {  // a regular step: Y_B's map from the row table
+      const TpRow& rw = rp[(k - k0) * Mmax];
+      yc = rw.c;
+      yd = rw.d;
+    } else {
+      const RadauH hAs = own_h ? radau_h(R, hs) : hA;
+      OdeStage sg[3];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) sg[j] = ode_stage(S.o, w, xs + R.c[j] * hs);
-    const YbRec yr = yb_rec(hAs, sg);
-    const double e = S.o.Pf * yr.d;
+      for (int j = 0; j < 3; ++j) sg[j] = ode_stage(S.o, w, xs + R.c[j] * hs);
+      const YbRec yr = yb_rec(hAs, sg);
+      yc = yr.c;
+      yd = yr.d;
+    }
+    const double e = S.o.Pf * yd;
 #pragma unroll
-    for (int i = 0; i < kTpGChunk; ++i) yb[i] = __builtin_fma(yr.c, yb[i], e);
+    for (int i = 0; i < kTpGChunk; ++i) yb[i] = __builtin_fma(yc, yb[i], e);
   };
   double kd = (double)k0;
-  for (int64_t k = k0; k < k1; ++k, kd += 1.0) {
+  for (; k < k1; ++k, kd += 1.0) {
     const double xk = S.x0 + kd * S.h;
     const bool split = xk < xb && xb <= xk + S.h;
     const double xa = split ? xb_below : xk + S.h;
@@ -816,9 +899,13 @@ int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, 
   const size_t b_agg = up(sizeof(lzq::TpMap) * (size_t)n * (size_t)Bmax);
   const size_t b_bout = up(sizeof(lzq::TpBlkOut) * (size_t)n * (size_t)Bmax);
   const size_t b_gd = up(sizeof(int32_t) * (size_t)n), b_gy = up(sizeof(double) * (size_t)n);
+  // the regular steps' stage rows (TpRow), when the tables of the call fit kTpRowBytes
+  const size_t rows_raw = sizeof(lzq::TpRow) * (size_t)n * (size_t)Mmax * (size_t)L;
+  const bool use_rows = LZQ_ODE_TP_ROWS && rows_raw <= lzq::kTpRowBytes;
+  const size_t b_rows = use_rows ? up(rows_raw) : 0;
   char* buf = nullptr;
   int rc = hip_check(hipMallocAsync((void**)&buf, b_nodes + b_ends + b_ctl + b_skip + 2 * (b_cand + b_segi + b_segv) +
-                                                       b_loc + b_agg + b_bout + b_gd + b_gy,
+                                                       b_loc + b_agg + b_bout + b_gd + b_gy + b_rows,
                                     s),
                      fn);
   if (rc) return rc;
@@ -843,6 +930,7 @@ int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, 
   auto* bout = reinterpret_cast<lzq::TpBlkOut*>(take(b_bout));
   auto* gdone = reinterpret_cast<int32_t*>(take(b_gd));
   auto* gyb = reinterpret_cast<double*>(take(b_gy));
+  auto* rows = use_rows ? reinterpret_cast<lzq::TpRow*>(take(b_rows)) : nullptr;
   hipLaunchKernelGGL(lzq::ode_tp_init_kernel, dim3((unsigned)n), dim3(256), 0, s, d_points, d_ode, d_tidx, d_work,
                      max_steps, L, Mmax, nodes, ctl);
   rc = hip_check(hipGetLastError(), fn);
@@ -851,10 +939,15 @@ int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, 
                        max_steps, L, Mmax, nodes, ctl);
     rc = hip_check(hipGetLastError(), fn);
   }
+  if (rc == LZQ_OK && use_rows) {
+    hipLaunchKernelGGL(lzq::ode_tp_rows_kernel, dim3((unsigned)((n * Mmax * L + 255) / 256)), dim3(256), 0, s,
+                       d_points, d_ode, n, d_tidx, d_work, max_steps, L, Mmax, ctl, rows);
+    rc = hip_check(hipGetLastError(), fn);
+  }
   const unsigned ib = (unsigned)((n * Mmax + 63) / 64);
   for (int32_t it = 0; it < kTpMaxIters && rc == LZQ_OK; ++it) {
     hipLaunchKernelGGL(lzq::ode_tp_interval_kernel, dim3(ib), dim3(64), 0, s, d_points, d_ode, n, d_tidx, d_work,
-                       max_steps, L, Mmax, nodes, ends, ctl);
+                       max_steps, L, Mmax, nodes, ends, ctl, rows);
     rc = hip_check(hipGetLastError(), fn);
     if (rc) break;
     hipLaunchKernelGGL(lzq::ode_tp_scan_local_kernel, dim3((unsigned)Bmax, (unsigned)n), dim3(lzq::kTpBlk), 0, s, Mmax,
@@ -878,7 +971,7 @@ int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, 
     int r = LZQ_OK;
     if (cands) {
       hipLaunchKernelGGL((lzq::ode_tp_cand_kernel<J, kStride>), dim3((unsigned)cb), dim3(64), 0, s,
-                         d_points, d_ode, n, d_tidx, d_work, max_steps, Mmax, nodes, ctl, candF, candG);
+                         d_points, d_ode, n, d_tidx, d_work, max_steps, Mmax, nodes, ctl, candF, candG, rows, L);
       r = hip_check(hipGetLastError(), fn);
       if (r) return r;
     }
@@ -896,7 +989,7 @@ int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, 
     constexpr int JG = decltype(Jc)::value, NC = 2 * JG + 1;
     constexpr int NCH = (NC + lzq::kTpGChunk - 1) / lzq::kTpGChunk;
     hipLaunchKernelGGL(lzq::ode_tp_gcand_kernel<JG>, dim3((unsigned)((n * Mmax * NCH + 63) / 64)), dim3(64), 0, s,
-                       d_points, d_ode, n, d_tidx, d_work, max_steps, Mmax, nodes, ctl, candG);
+                       d_points, d_ode, n, d_tidx, d_work, max_steps, Mmax, nodes, ctl, candG, rows, L);
     int r = hip_check(hipGetLastError(), fn);
     if (r) return r;
     hipLaunchKernelGGL(lzq::ode_tp_gseg_kernel<JG>, dim3((unsigned)((n * Smax * NC + 63) / 64)), dim3(64), 0, s, n, Mmax,

@@ -59,6 +59,16 @@ class Engine:
             self._check(prev)
         return bool(prev)
 
+    def tune_ode_table_wide(self, on) -> int:
+        """Few ODE tables (<= 4096) built wide (include/lzq.h LZQ_TUNE_ODE_TABLE_WIDE): True / 3 both,
+        1 the A/V knots over 64-knot wavefronts, 2 the spline around its two recurrences over a
+        wavefront, False / 0 neither; bit-identical tables either way.  Returns the previous mask."""
+        v = 3 if on is True else (0 if on is False else int(on))
+        prev = self.lib.lzq_tune(_native.TUNE_ODE_TABLE_WIDE, v)
+        if prev < 0:
+            self._check(prev)
+        return prev
+
     def tune_ode_launch_steps(self, log2: int) -> int:
         """Fixed Radau steps per ODE continuation launch, as a power of two (include/lzq.h
         LZQ_TUNE_ODE_LAUNCH_STEPS, default 24; bit-identical results).  Returns the previous."""

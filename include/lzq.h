@@ -172,8 +172,13 @@ int lzq_ztables(int32_t nz, double z_max, double* z, double* gamma4, double* ome
 /* LZQ_TUNE_ODE_TP_INTERVAL (steps, a multiple of 64 in [64, 2^20]; default 64): the interval length of
  * lzq_ode_integrate_tp's multiple shooting (longer for a point whose window would need over 65536
  * intervals). */
+/* LZQ_TUNE_ODE_TABLE_WIDE (bit mask, default 3 = both; 0 = off): lzq_ode_tables for few tables
+ * (<= 4096) spreads each table wide -- bit 0: the A/V knots over 64-knot wavefronts instead of one
+ * wavefront per table; bit 1: the spline's per-knot work over a wavefront's lanes around its two
+ * recurrences instead of one lane per table.  The tables are bit-identical either way
+ * (tests/test_gpu_ode_tp.py). */
 enum lzq_tune_key { LZQ_TUNE_EXP = 0, LZQ_TUNE_TRUNCATE = 1, LZQ_TUNE_ODE_COOP = 2, LZQ_TUNE_ODE_LAUNCH_STEPS = 3,
-                    LZQ_TUNE_PROFILE_FLAT = 4, LZQ_TUNE_ODE_TP_INTERVAL = 5 };
+                    LZQ_TUNE_PROFILE_FLAT = 4, LZQ_TUNE_ODE_TP_INTERVAL = 5, LZQ_TUNE_ODE_TABLE_WIDE = 6 };
 enum lzq_exp_variant { LZQ_EXP_POLY11 = 0, LZQ_EXP_TABLE = 1 };
 int lzq_tune(int32_t key, int32_t value);
 

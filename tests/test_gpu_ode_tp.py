@@ -156,3 +156,43 @@ def test_tp_raw_abi_large_step_cap(gpu_engine):
         if with_iters:
             assert int(its[0]) > 0
         close(out.cpu().numpy(), ref.cpu().numpy())
+
+
+def test_wide_tables_bit_identical(gpu_engine):
+    """LZQ_TUNE_ODE_TABLE_WIDE (round 6): few tables built a wavefront wide -- the spline's per-knot
+    work spread over the lanes around its two recurrences (ode_spline_wave_kernel), the A/V knots
+    over 64-knot wavefronts -- give the one-lane / one-wave tables bit for bit: main()'s 800 knots,
+    knot counts around the 64-lane chunk edges and the smallest, own windows, the A/V kernel's own
+    parameters, and a batch above the wide path's 4096-table limit (which takes the narrow kernels)."""
+    rng = np.random.default_rng(11)
+    cfgs = seeded_cfgs(7, seed=11)
+    p, _ = recs(cfgs)
+    n = len(cfgs)
+    Tp = np.array([c["T_p_GeV"] for c in cfgs])
+    T_lo = torch.tensor(Tp * rng.uniform(0.05, 0.6, n), dtype=torch.float64, device=gpu_engine.device)
+    T_hi = torch.tensor(Tp * rng.uniform(1.1, 4.0, n), dtype=torch.float64, device=gpu_engine.device)
+    aov = {"I_p": 0.27, "beta_over_H": 63.0, "T_p_GeV": 81.0, "v_w": 0.41, "g_star": 100.5}
+    try:
+        for kw in ({}, {"T_lo": T_lo, "T_hi": T_hi}, {"aov": aov}):
+            for nt in (800, 4, 5, 63, 64, 65, 127, 129, 1000):
+                tabs = []
+                for wide in (False, True):
+                    gpu_engine.tune_ode_table_wide(wide)
+                    # a zeroed workspace: a table leaves two spare doubles of its last knot unwritten
+                    work = torch.zeros(n * 4 * nt, dtype=torch.float64, device=gpu_engine.device)
+                    w, st = gpu_engine.ode_tables(p, nt=nt, work=work, **kw)
+                    tabs.append((w.cpu().numpy(), st.cpu().numpy()))
+                assert np.array_equal(tabs[0][1], tabs[1][1]), (kw.keys(), nt)
+                assert np.array_equal(tabs[0][0], tabs[1][0], equal_nan=True), (list(kw), nt)
+        # one point (the CLI's case) and a batch past the wide limit
+        for cf in ([cfgs[0]], [cfgs[k % n] for k in range(4100)]):
+            pp, _ = recs(cf)
+            tabs = []
+            for wide in (False, True):
+                gpu_engine.tune_ode_table_wide(wide)
+                work = torch.zeros(len(cf) * 4 * 800, dtype=torch.float64, device=gpu_engine.device)
+                w, st = gpu_engine.ode_tables(pp, work=work)
+                tabs.append(w.cpu().numpy())
+            assert np.array_equal(tabs[0], tabs[1], equal_nan=True)
+    finally:
+        gpu_engine.tune_ode_table_wide(True)

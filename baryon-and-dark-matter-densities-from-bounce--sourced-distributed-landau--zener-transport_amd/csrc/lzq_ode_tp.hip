@@ -56,12 +56,17 @@ struct OdeSetup {
   int64_t N;
   int st;
 };
+// verified: the point's window and table already passed these checks (ode_tp_init_kernel took it:
+// ctl.phase != kTpFallback), so the knot-by-knot grid check (~800 comparisons per lane) is skipped;
+// every other value is formed as in the checked call.
 __device__ __forceinline__ OdeSetup ode_setup(const lzq_point& pt, const lzq_ode_params& od, const double* w,
-                                              int64_t max_steps) {
+                                              int64_t max_steps, bool verified = false) {
   OdeSetup S;
   S.o = ode_point(pt, od);
   const OdePoint& o = S.o;
-  S.st = ode_grid_ok(o.T_lo, o.T_hi, o.stepT) ? (ode_table_ok(w) ? LZQ_ODE_OK : LZQ_ODE_BAD_TABLE) : LZQ_ODE_BAD_GRID;
+  S.st = verified ? LZQ_ODE_OK
+                  : (ode_grid_ok(o.T_lo, o.T_hi, o.stepT) ? (ode_table_ok(w) ? LZQ_ODE_OK : LZQ_ODE_BAD_TABLE)
+                                                          : LZQ_ODE_BAD_GRID);
   const double m = o.m, T_p = o.Tp;
   S.x0 = m / o.T_hi;
   S.x1 = m / pymax(o.T_lo, 1e-30);
@@ -162,6 +167,9 @@ struct TpRow {
   double lam[3], E2[3], S[3], c, d;
 };
 constexpr size_t kTpRowBytes = size_t(1) << 31;  // row tables of one call, at most (else stages inline)
+#ifndef LZQ_ODE_TP_FUSE
+#define LZQ_ODE_TP_FUSE 1  // a Newton update in two launches instead of four (same operations)
+#endif
 #ifndef LZQ_ODE_TP_ROWS
 #define LZQ_ODE_TP_ROWS 1  // 0: every step forms its stages inline (the round-5 path; same bits)
 #endif
@@ -180,7 +188,7 @@ __global__ __launch_bounds__(256) void ode_tp_rows_kernel(const lzq_point* __res
   const int64_t r = rem / Mmax, m = rem - r * Mmax, k = m * L + r;  // lanes: consecutive intervals
   if (c.phase != kTpIter || c.L != L || k >= c.N) return;
   const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
-  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
+  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps, true);
   const Radau R = radau_tableau();
   const RadauH hA = radau_h(R, S.h);
   const double xk = S.x0 + (double)k * S.h;  // tp_steps' x_k (its step counter is an exact double)
@@ -298,7 +306,7 @@ __global__ __launch_bounds__(64) void ode_tp_interval_kernel(const lzq_point* __
   const TpCtl c = ctl[p];
   if (c.phase != kTpIter || m >= c.M) return;
   const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
-  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
+  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps, true);
   const int64_t k0 = m * c.L, k1 = k0 + c.L < S.N ? k0 + c.L : S.N;
   const double xb = branch_x(S.o, S.x0, S.x1);
   const TpNode nd = nodes[p * (Mmax + 1) + m];
@@ -328,7 +336,7 @@ __global__ __launch_bounds__(256) void ode_tp_guess_kernel(const lzq_point* __re
   // block-uniform; without annihilation Y_chi's map is affine and Newton needs no first guess
   if (c.phase != kTpIter || c.M < kTpGuessMin || !c.riccati) return;
   const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
-  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
+  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps, true);
   const double Hc = (S.x1 - S.x0) / (double)kTpGuessSteps;
   if (threadIdx.x == 0) {
     const double xb = branch_x(S.o, S.x0, S.x1);
@@ -389,6 +397,50 @@ struct TpBlkOut {
   int32_t fail, pad;
 };
 
+// (LZQ_ODE_TP_FUSE) the interval integration and the block-local scan in one launch: thread t of
+// block b integrates interval b kTpBlk + t (ode_tp_interval_kernel's body), then the block scans.
+__global__ __launch_bounds__(kTpBlk) void ode_tp_interval_scan_kernel(
+    const lzq_point* __restrict__ pts, const lzq_ode_params* __restrict__ ode, const int32_t* __restrict__ tidx,
+    const double* __restrict__ ws, int64_t max_steps, int64_t L, int64_t Mmax, int64_t Bmax,
+    const TpNode* __restrict__ nodes, TpEnd* __restrict__ ends, const TpCtl* __restrict__ ctl,
+    const TpRow* __restrict__ rows, TpMap* __restrict__ loc, TpMap* __restrict__ agg, TpBlkOut* __restrict__ bout) {
+  __shared__ TpMap sm[kTpBlk];
+  const int64_t p = blockIdx.y, b = blockIdx.x;
+  const TpCtl c = ctl[p];
+  if (c.phase != kTpIter || b * kTpBlk >= c.M) return;  // block-uniform
+  const int t = threadIdx.x;
+  const int64_t m = b * kTpBlk + t;
+  TpEnd e{0.0, 0.0, 0.0, 0.0, 0, 0};
+  if (m < c.M) {
+    const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
+    const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps, true);
+    const int64_t k0 = m * c.L, k1 = k0 + c.L < S.N ? k0 + c.L : S.N;
+    const double xb = branch_x(S.o, S.x0, S.x1);
+    const TpNode nd = nodes[p * (Mmax + 1) + m];
+    TpState St{nd.Ychi, nd.YB, nd.Ychi, {nd.Ychi, nd.Ychi, nd.Ychi}, false};
+    double D = 1.0, C = 1.0;
+    const TpRow* rp = rows && c.L == L ? rows + p * Mmax * L + m : nullptr;
+    const bool exact = tp_steps(S.o, w, S.x0, S.h, xb, nextafter(xb, -INFINITY), k0, k1, St, D, C, rp, Mmax);
+    e = TpEnd{St.Ychi, St.YB, D, C, exact ? 1 : 0, 0};
+    ends[p * Mmax + m] = e;
+  }
+  TpMap v{1.0, 0.0, 1.0, 0.0};
+  int fail = 0;
+  if (m < c.M) {
+    const TpNode q = nodes[p * (Mmax + 1) + m + 1];
+    const bool fin = isfinite(e.Ychi) && isfinite(e.D) && isfinite(e.YB) && isfinite(e.C);
+    fail = e.exact == 0 || !fin;
+    v = fin ? TpMap{e.D, e.Ychi - q.Ychi, e.C, e.YB - q.YB} : TpMap{0.0, 0.0, 0.0, 0.0};
+  }
+  const int any_fail = __syncthreads_or(fail);
+  v = tp_block_scan(v, sm);
+  if (m < c.M) loc[p * Mmax + m] = v;
+  if (t == kTpBlk - 1) {
+    agg[p * Bmax + b] = v;
+    bout[p * Bmax + b].fail = any_fail;
+  }
+}
+
 __global__ __launch_bounds__(kTpBlk) void ode_tp_scan_local_kernel(int64_t Mmax, int64_t Bmax,
                                                                    const TpNode* __restrict__ nodes,
                                                                    const TpEnd* __restrict__ ends,
@@ -420,13 +472,20 @@ __global__ __launch_bounds__(kTpBlk) void ode_tp_scan_local_kernel(int64_t Mmax,
   }
 }
 
+// ticket (LZQ_ODE_TP_FUSE, else nullptr): per point, the blocks of this update that are done; the
+// last one folds the point's block results into TpCtl (tp_finish_update, what
+// ode_tp_scan_finish_kernel does in its own launch) and resets the count for the next update.
+__device__ __forceinline__ void tp_finish_update(int64_t p, int64_t Bmax, TpCtl* __restrict__ ctl,
+                                                 const TpBlkOut* __restrict__ bout, int32_t max_iters, double tol);
 __global__ __launch_bounds__(kTpBlk) void ode_tp_scan_apply_kernel(int64_t Mmax, int64_t Bmax,
                                                                    TpNode* __restrict__ nodes,
                                                                    const TpEnd* __restrict__ ends,
-                                                                   const TpCtl* __restrict__ ctl,
+                                                                   TpCtl* __restrict__ ctl,
                                                                    const TpMap* __restrict__ loc,
                                                                    const TpMap* __restrict__ agg,
-                                                                   TpBlkOut* __restrict__ bout) {
+                                                                   TpBlkOut* __restrict__ bout,
+                                                                   int32_t* __restrict__ ticket, int32_t max_iters,
+                                                                   double tol) {
   __shared__ TpMap sm[kTpBlk];
   __shared__ double s_err[kTpBlk / 64];
   const int64_t p = blockIdx.y, b = blockIdx.x;
@@ -445,7 +504,6 @@ __global__ __launch_bounds__(kTpBlk) void ode_tp_scan_apply_kernel(int64_t Mmax,
     carry = tp_compose(sm[last], carry);
     __syncthreads();
   }
-  (void)nb;
   const int64_t m = b * kTpBlk + t;
   double err = 0.0;
   if (m < c.M) {
@@ -484,16 +542,32 @@ __global__ __launch_bounds__(kTpBlk) void ode_tp_scan_apply_kernel(int64_t Mmax,
     double e_all = 0.0;
     for (int k = 0; k < kTpBlk / 64; ++k) e_all = pymax(e_all, s_err[k]);
     bout[p * Bmax + b].err = e_all;
+    if (ticket) {
+      // release this block's bout store, count it; the last block acquires the others' and folds
+      const int32_t done = __hip_atomic_fetch_add(&ticket[p], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (done == (int32_t)(nb - 1)) {
+        tp_finish_update(p, Bmax, ctl, bout, max_iters, tol);
+        __hip_atomic_store(&ticket[p], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
 }
 
+__device__ __forceinline__ void tp_finish_update(int64_t p, int64_t Bmax, TpCtl* __restrict__ ctl,
+                                                 const TpBlkOut* __restrict__ bout, int32_t max_iters, double tol);
 __global__ __launch_bounds__(64) void ode_tp_scan_finish_kernel(int64_t n, int64_t Bmax, TpCtl* __restrict__ ctl,
                                                                 const TpBlkOut* __restrict__ bout, int32_t max_iters,
                                                                 double tol) {
   const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (p >= n) return;
+  if (ctl[p].phase != kTpIter) return;
+  tp_finish_update(p, Bmax, ctl, bout, max_iters, tol);
+}
+// fold point p's block errors and failure flags into its TpCtl (the update count, converged ->
+// kTpDone, out of updates -> kTpFallback)
+__device__ __forceinline__ void tp_finish_update(int64_t p, int64_t Bmax, TpCtl* __restrict__ ctl,
+                                                 const TpBlkOut* __restrict__ bout, int32_t max_iters, double tol) {
   TpCtl c = ctl[p];
-  if (c.phase != kTpIter) return;
   const int64_t nb = (c.M + kTpBlk - 1) / kTpBlk;
   double e_all = 0.0;
   bool fail = false;
@@ -554,7 +628,7 @@ __device__ __noinline__ void tp_cand_one(const lzq_point* __restrict__ pts, cons
                                          int64_t m, int off, double* __restrict__ oF, double* __restrict__ oG,
                                          const TpRow* __restrict__ rp, int64_t stride) {
   const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
-  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
+  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps, true);
   const int64_t k0 = m * c.L, k1 = k0 + c.L < S.N ? k0 + c.L : S.N;
   const double y0 = dfromkey(dkey(nd->Ychi) + off), b0 = dfromkey(dkey(nd->YB) + off);
   // (k0 is a whole number of predictor blocks: the first step does not read Yp / Z / have)
@@ -589,7 +663,7 @@ __global__ __launch_bounds__(64) void ode_tp_cand_kernel(const lzq_point* __rest
                     Mmax);
       } else {
         const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
-        const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
+        const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps, true);
         const int64_t k0 = m * c.L, k1 = k0 + c.L < S.N ? k0 + c.L : S.N;
         const TpNode& nd = nodes[p * (Mmax + 1) + m];
         const double y0 = dfromkey(dkey(nd.Ychi) + (jj - J)), b0 = dfromkey(dkey(nd.YB) + (jj - J));
@@ -673,7 +747,7 @@ __global__ __launch_bounds__(64) void ode_tp_gcand_kernel(const lzq_point* __res
   const TpCtl c = ctl[p];
   if (c.phase != kTpDone || m >= c.M) return;
   const double* w = ws + (tidx ? (int64_t)tidx[p] : p) * (int64_t)kOdeWS;
-  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps);
+  const OdeSetup S = ode_setup(pts[p], ode[p], w, max_steps, true);
   const int64_t k0 = m * c.L, k1 = k0 + c.L < S.N ? k0 + c.L : S.N;
   const int64_t bkey = dkey(nodes[p * (Mmax + 1) + m].YB);
   double yb[kTpGChunk];
@@ -903,9 +977,10 @@ int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, 
   const size_t rows_raw = sizeof(lzq::TpRow) * (size_t)n * (size_t)Mmax * (size_t)L;
   const bool use_rows = LZQ_ODE_TP_ROWS && rows_raw <= lzq::kTpRowBytes;
   const size_t b_rows = use_rows ? up(rows_raw) : 0;
+  const size_t b_tk = up(sizeof(int32_t) * (size_t)n);
   char* buf = nullptr;
   int rc = hip_check(hipMallocAsync((void**)&buf, b_nodes + b_ends + b_ctl + b_skip + 2 * (b_cand + b_segi + b_segv) +
-                                                       b_loc + b_agg + b_bout + b_gd + b_gy + b_rows,
+                                                       b_loc + b_agg + b_bout + b_gd + b_gy + b_rows + b_tk,
                                     s),
                      fn);
   if (rc) return rc;
@@ -931,6 +1006,7 @@ int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, 
   auto* gdone = reinterpret_cast<int32_t*>(take(b_gd));
   auto* gyb = reinterpret_cast<double*>(take(b_gy));
   auto* rows = use_rows ? reinterpret_cast<lzq::TpRow*>(take(b_rows)) : nullptr;
+  auto* ticket = reinterpret_cast<int32_t*>(take(b_tk));
   hipLaunchKernelGGL(lzq::ode_tp_init_kernel, dim3((unsigned)n), dim3(256), 0, s, d_points, d_ode, d_tidx, d_work,
                      max_steps, L, Mmax, nodes, ctl);
   rc = hip_check(hipGetLastError(), fn);
@@ -945,7 +1021,21 @@ int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, 
     rc = hip_check(hipGetLastError(), fn);
   }
   const unsigned ib = (unsigned)((n * Mmax + 63) / 64);
+  // one Newton update: LZQ_ODE_TP_FUSE, two launches (intervals + local scans, then the carries,
+  // the node update and -- in the point's last block -- the convergence fold); else four
+  if (rc == LZQ_OK && LZQ_ODE_TP_FUSE) rc = hip_check(hipMemsetAsync(ticket, 0, sizeof(int32_t) * (size_t)n, s), fn);
   for (int32_t it = 0; it < kTpMaxIters && rc == LZQ_OK; ++it) {
+    if (LZQ_ODE_TP_FUSE) {
+      hipLaunchKernelGGL(lzq::ode_tp_interval_scan_kernel, dim3((unsigned)Bmax, (unsigned)n), dim3(lzq::kTpBlk), 0, s,
+                         d_points, d_ode, d_tidx, d_work, max_steps, L, Mmax, Bmax, nodes, ends, ctl, rows, loc, agg,
+                         bout);
+      rc = hip_check(hipGetLastError(), fn);
+      if (rc) break;
+      hipLaunchKernelGGL(lzq::ode_tp_scan_apply_kernel, dim3((unsigned)Bmax, (unsigned)n), dim3(lzq::kTpBlk), 0, s,
+                         Mmax, Bmax, nodes, ends, ctl, loc, agg, bout, ticket, kTpMaxIters, kTpTol);
+      rc = hip_check(hipGetLastError(), fn);
+      continue;
+    }
     hipLaunchKernelGGL(lzq::ode_tp_interval_kernel, dim3(ib), dim3(64), 0, s, d_points, d_ode, n, d_tidx, d_work,
                        max_steps, L, Mmax, nodes, ends, ctl, rows);
     rc = hip_check(hipGetLastError(), fn);
@@ -955,7 +1045,7 @@ int launch_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, 
     rc = hip_check(hipGetLastError(), fn);
     if (rc) break;
     hipLaunchKernelGGL(lzq::ode_tp_scan_apply_kernel, dim3((unsigned)Bmax, (unsigned)n), dim3(lzq::kTpBlk), 0, s, Mmax,
-                       Bmax, nodes, ends, ctl, loc, agg, bout);
+                       Bmax, nodes, ends, ctl, loc, agg, bout, (int32_t*)nullptr, kTpMaxIters, kTpTol);
     rc = hip_check(hipGetLastError(), fn);
     if (rc) break;
     hipLaunchKernelGGL(lzq::ode_tp_scan_finish_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, n, Bmax, ctl,

@@ -79,3 +79,99 @@ def kernel_code_sha256(lib_path: str, kernel: str = "yields_grid_kernel", arch: 
                 h.update(name.encode() + b"\0" + struct.pack("<Q", len(data)) + data)
             return h.hexdigest()
     return None
+
+
+def elf_symbols(obj: bytes) -> list[tuple[str, int, int, int]]:
+    """(name, value, size, section index) of every .symtab entry of a little-endian ELF64 object."""
+    (shoff,) = struct.unpack_from("<Q", obj, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", obj, 0x3A)
+    hdrs = [struct.unpack_from("<IIQQQQIIQQ", obj, shoff + i * shentsize) for i in range(shnum)]
+    str_off = hdrs[shstrndx][4]
+
+    def sec_name(h):
+        end = obj.index(b"\0", str_off + h[0])
+        return obj[str_off + h[0]:end].decode("ascii", "replace")
+    names = [sec_name(h) for h in hdrs]
+    if ".symtab" not in names:
+        return []
+    sym = hdrs[names.index(".symtab")]
+    strtab = hdrs[sym[6]]  # sh_link: the symbol names' string table
+    out = []
+    for k in range(sym[5] // 24):
+        st_name, _info, _other, shndx, value, size = struct.unpack_from("<IBBHQQ", obj, sym[4] + 24 * k)
+        end = obj.index(b"\0", strtab[4] + st_name)
+        out.append((obj[strtab[4] + st_name:end].decode("ascii", "replace"), value, size, shndx))
+    return out
+
+
+OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+
+
+def kernel_isa_sha256(lib_path: str, kernel: str = "yields_grid_kernel", arch: str = "gfx950") -> str | None:
+    """sha256 of the disassembly of the kernels whose mangled names contain `kernel` (every template
+    instantiation, in name order), with what depends on where the code object lays them out masked:
+    the literal of each s_add_u32 / s_addc_u32 that forms a PC-relative address after s_getpc_b64.
+    The identity of a PMC profile of those kernels that survives changes to the other kernels of the
+    same translation unit (kernel_code_sha256 hashes the whole object's .text, and the raw bytes of
+    a kernel change with the placement of the data it addresses).  None if the kernel or
+    llvm-objdump (ROCm's) is absent."""
+    import os
+    import re
+    import subprocess
+    import tempfile
+    if not os.path.exists(OBJDUMP):
+        return None
+    for obj in device_objects(lib_path, arch):
+        if kernel.encode() not in obj:
+            continue
+        with tempfile.NamedTemporaryFile(suffix=".co") as f:
+            f.write(obj)
+            f.flush()
+            r = subprocess.run([OBJDUMP, "-d", "--no-show-raw-insn", "--no-leading-addr", f.name],
+                               capture_output=True, text=True)
+        if r.returncode:
+            return None
+        funcs, cur = {}, None
+        for line in r.stdout.splitlines():
+            m = re.match(r"^<(\S+)>:$", line.strip())
+            if m:
+                cur = m.group(1) if kernel in m.group(1) else None
+                if cur:
+                    funcs[cur] = []
+                continue
+            if cur is None:
+                continue
+            t = line.split("//")[0].strip()
+            if t:
+                funcs[cur].append(t)
+        if not funcs:
+            return None
+        h = hashlib.sha256()
+        for name in sorted(funcs):
+            pcrel = set()
+            out = []
+            for t in funcs[name]:
+                op = t.split()[0]
+                args = t[len(op):].replace(" ", "").split(",")
+                if op == "s_getpc_b64":
+                    m = re.match(r"s\[(\d+):(\d+)\]", args[0])
+                    if m:
+                        pcrel = {f"s{m.group(1)}", f"s{m.group(2)}"}
+                elif op in ("s_add_u32", "s_addc_u32") and args and args[0] in pcrel and len(args) == 3:
+                    t = f"{op} {args[0]}, {args[1]}, PCREL"
+                elif args and args[0] in pcrel:
+                    pcrel.discard(args[0])  # the register is redefined: no longer a PC-relative base
+                out.append(t)
+            h.update(name.encode() + b"\0" + "\n".join(out).encode() + b"\0")
+        # and their kernel descriptors (registers, LDS, scratch), less the code entry offset
+        (shoff,) = struct.unpack_from("<Q", obj, 0x28)
+        shentsize, shnum, _ = struct.unpack_from("<HHH", obj, 0x3A)
+        hdrs = [struct.unpack_from("<IIQQQQIIQQ", obj, shoff + i * shentsize) for i in range(shnum)]
+        for name, value, size, shndx in sorted(elf_symbols(obj)):
+            if kernel in name and name.endswith(".kd") and size == 64 and 0 < shndx < shnum:
+                sec = hdrs[shndx]
+                kd = bytearray(obj[sec[4] + (value - sec[3]):sec[4] + (value - sec[3]) + 64])
+                kd[16:24] = bytes(8)  # kernel_code_entry_byte_offset: where the code sits, not what it is
+                h.update(name.encode() + b"\0" + bytes(kd))
+        return h.hexdigest()
+    return None

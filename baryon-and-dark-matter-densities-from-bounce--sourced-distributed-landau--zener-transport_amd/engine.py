@@ -334,10 +334,17 @@ class Engine:
             share_tables = False   # a table's key now includes the block (ODE_TABLE_KEY does not)
         # the launches cover the batch's own largest step count (or the cap, when a point needs more:
         # those points come back LZQ_ODE_TOO_MANY_STEPS), not the cap itself
-        need = ode_step_counts_device(d_pts_all, n)   # same values as ode_step_counts, on the device
-        need = need[torch.isfinite(need)]
         per = 1 << getattr(self, "_ode_launch_log2", 24)
-        longest = int(min(float(need.max()) + 64 if need.numel() else 0, _native.ODE_MAX_LAUNCHES * per))
+        if n <= 4096:
+            # few points (the CLI's one): on the host, no device round trip (the same values)
+            need_h = ode_step_counts(pts)
+            need_h = need_h[np.isfinite(need_h)]
+            top = float(need_h.max()) + 64 if need_h.size else 0
+        else:
+            need = ode_step_counts_device(d_pts_all, n)   # same values as ode_step_counts, on the device
+            need = need[torch.isfinite(need)]
+            top = float(need.max()) + 64 if need.numel() else 0
+        longest = int(min(top, _native.ODE_MAX_LAUNCHES * per))
         max_steps = longest if max_steps is None else min(int(max_steps), longest)
         order = wave_order(d_pts_all, d_ode_all, n) if group_waves else None
         if order is not None:

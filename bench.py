@@ -20,7 +20,7 @@ line through and exits with the launcher's status.  A rank count that disagrees 
 more RCCL ranks than the node has GPUs, is an error (exit status 2), never a 1-GPU line.
 
 Prints one JSON line (rank 0).  `roofline` = the kernel's executed FP64 FLOP (PMC
-instruction mix of profiles/round5, used only if that profile's kernel code hash is the timed
+instruction mix of profiles/round6, used only if that profile's kernel ISA hash is the timed
 library's) over its HIP-event time in this run, against the 78.6 TFLOP/s FP64 vector peak, with
 the FP64-pipe and VALU issue fractions beside it; `kernel_ms` / `allgather_ms` decompose a step
 per rank (min / max / mean); `parity_spot` checks 64 rows of the last timed step's table against
@@ -64,7 +64,7 @@ BASE = {  # /root/reference/yields_config_equal_mass.json
 }
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "round5", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "round6", "pmc_summary.json")
 WAVE_NODES_PER_POINT = 8000 * 1200 // 64
 
 
@@ -74,6 +74,14 @@ def _pmc():
             return json.load(f)
     except (OSError, ValueError):
         return None
+
+
+def timed_kernel_isa() -> str | None:
+    """codeobj.kernel_isa_sha256 of yields_grid_kernel in the library this process loaded: its
+    disassembly and descriptors with the layout-dependent PC-relative literals masked, so a
+    profile stays tied to the kernel, not to the other kernels of its translation unit."""
+    native = importlib.import_module(PKG + "._native")
+    return importlib.import_module(PKG + ".codeobj").kernel_isa_sha256(native.LIB_PATH)
 
 
 def timed_code_object() -> tuple[str | None, str | None]:
@@ -91,7 +99,7 @@ def roofline(points_per_launch: int, kern_ms: float) -> dict:
     """FP64 VALU roofline of yields_grid_kernel for this run.
 
     achieved = EXECUTED FP64 FLOP per launch / this run's HIP-event kernel time.  The executed
-    FLOP per point come from the rocprofv3 PMC pass of the same build (profiles/round5, tools/
+    FLOP per point come from the rocprofv3 PMC pass of the same kernel (profiles/round6, tools/
     gpu_profile.sh): (2 x SQ_INSTS_VALU_FMA_F64 + SQ_INSTS_VALU_MUL_F64 + SQ_INSTS_VALU_ADD_F64)
     x 64 lanes / points; peak = 78.6 TFLOP/s (256 CU x 2.4 GHz x 128 FP64 FLOP/clk/CU, every
     issue slot an FMA).  Also reported: the FP64 pipe's busy fraction (FP64 instructions x 4
@@ -112,12 +120,18 @@ def roofline(points_per_launch: int, kern_ms: float) -> dict:
         out.update(achieved=None, frac=None, traffic=None,
                    note=f"no PMC summary at {os.path.relpath(PMC_SUMMARY, ROOT)}: executed FLOP unknown")
         return out
-    same = d.get("kernel_code_sha256") == code if d.get("kernel_code_sha256") else d.get("code_object_sha256") == sha
+    isa = timed_kernel_isa() if d and d.get("kernel_isa_sha256") else None
+    out["kernel_isa_sha256"] = isa
+    if d and d.get("kernel_isa_sha256") and isa:
+        same = d["kernel_isa_sha256"] == isa   # the kernel's own machine code and descriptors (round 6)
+    else:
+        same = d.get("kernel_code_sha256") == code if d.get("kernel_code_sha256") else d.get("code_object_sha256") == sha
     if not same:
         # the counters describe another build of the kernel: no fraction rather than a stale one
         out.update(achieved=None, frac=None, fp64_pipe_busy_frac=None, traffic=None,
                    profile_code_object_sha256=d.get("code_object_sha256"),
                    profile_kernel_code_sha256=d.get("kernel_code_sha256"),
+                   profile_kernel_isa_sha256=d.get("kernel_isa_sha256"),
                    note=f"stale profile: {os.path.relpath(PMC_SUMMARY, ROOT)} was measured on kernel code "
                         f"{d.get('kernel_code_sha256') or d.get('code_object_sha256')}, this run timed {code}; "
                         f"re-run tools/gpu.sh profile ROUND")
@@ -138,6 +152,7 @@ def roofline(points_per_launch: int, kern_ms: float) -> dict:
         "valu_issue_busy_frac": (4.0 * fp64_wn + 2.0 * other_wn) / cyc_wn,
         "profile_code_object_sha256": d["code_object_sha256"],
         "profile_kernel_code_sha256": d.get("kernel_code_sha256"),
+        "profile_kernel_isa_sha256": d.get("kernel_isa_sha256"),
         "flop_per_point_executed": flop_pt,
         "traffic": d["hbm_bytes_per_point"]["total_upper"] * points_per_launch, "traffic_unit": "bytes/launch",
         # north_star: "achieved HBM GB/s for the grid I/O" -- the path is FP64-bound, so this is small
@@ -155,8 +170,9 @@ def roofline(points_per_launch: int, kern_ms: float) -> dict:
                 "(DESIGN.md §4.1). fp64_pipe_busy_frac counts every FP64 instruction as a full slot; "
                 "valu_issue_busy_frac adds the other VALU instructions at 2 cycles: the kernel is at its "
                 "formulation's issue ceiling, so the lever left is instruction count. The counters are "
-                "used only when their profile's kernel code hash (machine code + descriptors + metadata "
-                "of the code object, codeobj.kernel_code_sha256) equals the timed library's"})
+                "used only when their profile's kernel ISA hash (the kernel's disassembly and descriptors, "
+                "layout-dependent PC-relative literals masked: codeobj.kernel_isa_sha256) equals the timed "
+                "library's"})
     return out
 
 

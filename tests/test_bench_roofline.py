@@ -14,7 +14,7 @@ from conftest import ROOT
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
-PROF = os.path.dirname(bench.PMC_SUMMARY)   # this round's committed profile (profiles/round5)
+PROF = os.path.dirname(bench.PMC_SUMMARY)   # this round's committed profile (profiles/round6)
 
 
 def counters(path, kernel="yields_grid_kernel"):
@@ -38,7 +38,9 @@ def test_executed_flop_from_committed_csv():
     rf = bench.roofline(1_000_000, kern_ms)
     import json
     summ = json.load(open(os.path.join(PROF, "pmc_summary.json")))
-    if rf["kernel_code_sha256"] != summ.get("kernel_code_sha256"):
+    same = (rf.get("kernel_isa_sha256") == summ["kernel_isa_sha256"]) if summ.get("kernel_isa_sha256") and \
+        rf.get("kernel_isa_sha256") else rf["kernel_code_sha256"] == summ.get("kernel_code_sha256")
+    if not same:
         # the library here is another build of the kernel than the profiled one
         assert rf["frac"] is None and rf["note"].startswith("stale profile"), rf
         return

@@ -80,6 +80,19 @@ case "$cmd" in
       || { tail -5 "$OUT/stall.err"; exit 4; }
     cat "$OUT/trace.jsonl"
     ;;
+  configs)   # per-config throughput (tools/bench_configs.py, all configs in one process), then one PMC pass per
+             # config for its executed FP64; summarise with: python tools/summarize_configs.py gpurun_out/configs ROUND
+    rm -rf "$OUT"; mkdir -p "$OUT"
+    timeout -k 10 400 python3 tools/bench_configs.py > "$OUT/timed.jsonl" 2> "$OUT/timed.err" \
+      || { tail -5 "$OUT/timed.err"; exit 1; }
+    for c in C2 C3 C4 C5 C5_N16 C5_N32 P1 O_narrow_wash O_stiff_thermal O_riccati_mchi_sv; do
+      timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 \
+        SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 --output-format csv -d "$OUT/pmc_$c" -o run -- \
+        python3 tools/bench_configs.py --pmc --only $c --points 100000 --ode-points 65536 > "$OUT/pmc_$c.jsonl" \
+        2> "$OUT/pmc_$c.err" || { tail -5 "$OUT/pmc_$c.err"; exit 2; }
+    done
+    cat "$OUT/timed.jsonl" | cut -c1-300
+    ;;
   prop-pmc)  # the bounce-profile propagation (tools/bench_profile.py): instruction mix per kernel + kernel trace;
              # summarise with: python tools/summarize_profile_pmc.py gpurun_out/prop-pmc ROUND
     N=${1:-1000000}
@@ -147,6 +160,6 @@ print(json.dumps(rec)); open('$OUT/${S}_reuse_bitwise.json', 'w').write(json.dum
     tail -40 "$OUT/$(basename "$script" .py).log"
     ;;
   *)
-    echo "usage: tools/gpu.sh tests|final|profile ROUND|ode-pmc|prop-pmc|lzprop-pmc|sweeps|bench|py SCRIPT ..."; exit 64
+    echo "usage: tools/gpu.sh tests|final|profile ROUND|ode-pmc|configs|prop-pmc|lzprop-pmc|sweeps|bench|py SCRIPT ..."; exit 64
     ;;
 esac

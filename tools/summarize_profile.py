@@ -47,7 +47,8 @@ def main():
     # the build the counters were taken on (bench.py reports a fraction only for this code object)
     out = {"pmc_points_per_launch": points, "counters": {},
            "code_object_sha256": importlib.import_module(pkg + ".codeobj").kernel_object_sha256(lib),
-           "kernel_code_sha256": importlib.import_module(pkg + ".codeobj").kernel_code_sha256(lib)}
+           "kernel_code_sha256": importlib.import_module(pkg + ".codeobj").kernel_code_sha256(lib),
+           "kernel_isa_sha256": importlib.import_module(pkg + ".codeobj").kernel_isa_sha256(lib)}
     for g in ("fetch", "write", "sq", "inst", "mix"):
         p = os.path.join(src, f"pmc_{g}", "run_counter_collection.csv")
         if not os.path.exists(p):

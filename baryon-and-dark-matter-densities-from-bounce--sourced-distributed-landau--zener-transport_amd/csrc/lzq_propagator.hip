@@ -71,6 +71,9 @@ constexpr int kPropBlock = 256;
 #ifndef LZQ_PROP_MIN_WAVES
 #define LZQ_PROP_MIN_WAVES 2  // 217 VGPRs with the 3-step unroll, no spills (3 waves/SIMD: 168 VGPRs, spills; same time)
 #endif
+#ifndef LZQ_FOLLOW_SPLIT
+#define LZQ_FOLLOW_SPLIT 0  // 1: lz_follow_split_kernel (three frame jobs on three wavefronts; measured slower)
+#endif
 #ifndef LZQ_FOLLOW_MIN_WAVES
 #define LZQ_FOLLOW_MIN_WAVES 1  // lz_follow_kernel's occupancy floor (tools/ablate_prop.py)
 #endif
@@ -291,6 +294,111 @@ __global__ __launch_bounds__(kPropBlock, LZQ_FOLLOW_MIN_WAVES) void lz_follow_ke
   sa_cell_follow(mh, sg, sa * (left - xcc) * inv_vw, sa * (right - xcc) * inv_vw, tau_c, has_left, has_right, out);
 }
 
+// lz_follow_kernel with a cell's three frame jobs on three wavefronts (round 6, LZQ_FOLLOW_SPLIT):
+// a block takes 64 cells; wave 0 forms each cell's core-edge frame U(tau_c) (and the header:
+// edges, step count, or the closed form of an adiabatic cell), wave 1 the left stretch's outer
+// frame and phase, wave 2 the right one's; after a block barrier waves 1 and 2 combine them with
+// the core frame from LDS and store ML / MR.  sa_cell_follow's operations per job, so the same
+// matrices; what changes is that a lane carries one frame chain at a time instead of three
+// (its registers: more waves per SIMD to hide the chains' latency) and a wave runs one kind of
+// job (no has_left / has_right predication across the three).
+constexpr int kFollowCells = 64;
+#ifndef LZQ_FOLLOW_SPLIT_WAVES
+#define LZQ_FOLLOW_SPLIT_WAVES 4  // lz_follow_split_kernel's waves per SIMD (its VGPR cap = 512 / this)
+#endif
+__global__ __launch_bounds__(3 * kFollowCells) __attribute__((amdgpu_waves_per_eu(LZQ_FOLLOW_SPLIT_WAVES)))
+void lz_follow_split_kernel(
+    const double* __restrict__ m_mix, const double* __restrict__ dprime, const double* __restrict__ xi,
+    const double* __restrict__ vw, int64_t n, int32_t n_cross, double v_w0, double K, int32_t S,
+    double* __restrict__ follow) {
+  struct Geo {
+    double tl, tr, tau_c, mh;
+    int32_t sides;  // bit 0: the left stretch, bit 1: the right one
+  };
+  __shared__ SU2 s_uc[kFollowCells];
+  __shared__ Geo s_geo[kFollowCells];
+  const int lane = threadIdx.x & 63, job = threadIdx.x >> 6;  // job: wave-uniform
+  const int64_t t = (int64_t)blockIdx.x * kFollowCells + lane;
+  const int c = t < n * n_cross ? (int)(t % n_cross) : 0;
+  const double sg = (c % 2 == 0) ? 1.0 : -1.0;
+  double* out = follow + t * kFollowDoubles;
+  if (job == 0) {  // the cell's geometry (lz_follow_kernel's, verbatim), the header and the core frame
+    Geo geo{0.0, 0.0, 0.0, 0.0, 0};
+    const int64_t p = t / n_cross;
+    const double v_w = t < n * n_cross ? (vw ? vw[p] : v_w0) : 0.0;
+    if (t < n * n_cross && v_w > 0.0) {  // (the propagate kernel writes NaN for a bad wall speed)
+      const double* mm = m_mix + p * n_cross;
+      const double* dp = dprime + p * n_cross;
+      const double* xc = xi + p * n_cross;
+      const double ac = fabs(dp[c]), mc = mm[c], xcc = xc[c];
+      double left, right;
+      if (c == 0) {
+        left = xc[0] - K * lz_length(mm[0], fabs(dp[0]), v_w);
+      } else {
+        const double ap = fabs(dp[c - 1]);
+        left = (ap * xc[c - 1] + ac * xcc) / (ap + ac);
+      }
+      if (c + 1 < n_cross) {
+        const double an = fabs(dp[c + 1]);
+        right = (ac * xcc + an * xc[c + 1]) / (ac + an);
+      } else {
+        right = xcc + K * lz_length(mc, ac, v_w);
+      }
+      const double delta = mc * mc / (2.0 * v_w * ac);
+      if (delta > kDeltaAdiabatic) {
+        const double slope = sg * ac;
+        const double Phi = (wkb_G(ac * (right - xcc), mc) - wkb_G(ac * (left - xcc), mc)) / (ac * v_w);
+        const double DL = slope * (left - xcc), DR = slope * (right - xcc);
+        const double ddot = slope * v_w;
+        const Dressed L = dressed_basis(DL, ddot, mc), R = dressed_basis(DR, ddot, mc);
+        const double id = 1.0 / delta, id2 = id * id;
+        const double phiS = id * (1.0 / 12.0 + id2 * (1.0 / 360.0 + id2 * (1.0 / 1260.0 + id2 * (1.0 / 1680.0))));
+        const double tails = 0.125 * mc * mc * ac * v_w * (tail_T(DL, mc) + tail_T(DR, mc));
+        const SU2 m = su2_mul({R.p0, R.p1}, su2_phase_adj(Phi + phiS - tails, {L.p0, L.p1}));
+        out[0] = m.a.re, out[1] = m.a.im, out[2] = m.b.re, out[3] = m.b.im;
+        out[10] = -1.0;
+      } else {
+        const double W = core_halfwidth(mc, ac, v_w);
+        const double cl = fmax(left, xcc - W), cr = fmin(right, xcc + W);
+        const double Phic = (wkb_G(ac * (cr - xcc), mc) - wkb_G(ac * (cl - xcc), mc)) / (ac * v_w);
+        const double Sd = fmax((double)S, ceil(Phic * kStepsPerRadian));
+        const double inv_vw = 1.0 / v_w;
+        const double sa = sqrt(ac * v_w);
+        geo.mh = mc / sa;
+        geo.tau_c = W * sa * inv_vw;
+        geo.tl = sa * (left - xcc) * inv_vw;
+        geo.tr = sa * (right - xcc) * inv_vw;
+        geo.sides = (left < cl ? 1 : 0) | (cr < right ? 2 : 0);
+        out[8] = cl;
+        out[9] = cr;
+        out[10] = Sd <= kMaxCellSteps ? Sd : __builtin_nan("");
+      }
+    }
+    s_geo[lane] = geo;
+  }
+  __syncthreads();
+  const Geo geo = s_geo[lane];
+  // wave 0: the core frame; waves 1, 2: the outer frame and the phase of their stretch
+  const bool mine = job == 0 ? geo.sides != 0 : ((geo.sides >> (job - 1)) & 1) != 0;
+  SU2 u{};
+  double ph = 0.0;
+  if (mine) {
+    if (job == 0) {
+      s_uc[lane] = sa_frame(geo.tau_c, sg, geo.mh, false);
+    } else {
+      const double tau = job == 1 ? geo.tl : geo.tr;
+      u = sa_frame(tau, sg, geo.mh, true);
+      ph = job == 1 ? sa_phase(geo.tl, -geo.tau_c, geo.mh) : sa_phase(geo.tau_c, geo.tr, geo.mh);
+    }
+  }
+  __syncthreads();
+  if (mine && job > 0) {
+    const SU2 uc = s_uc[lane];
+    if (job == 1) sa_store(su2_mul(sa_reflect(uc), su2_phase_adj(ph, u)), out);  // U(-tau_c) P U(tl)^+
+    else sa_store(su2_mul(u, su2_phase_adj(ph, uc)), out + 4);                   // U(tr) P U(tau_c)^+
+  }
+}
+
 __global__ __launch_bounds__(kPropBlock, LZQ_PROP_MIN_WAVES) void lz_propagate_kernel(const double* __restrict__ m_mix,
                                                                   const double* __restrict__ dprime,
                                                                   const double* __restrict__ xi,
@@ -445,9 +553,15 @@ int propagate_slice(const double* d_m_mix, const double* d_dprime, const double*
   const int32_t* order = nullptr;
   hipError_t e = hipSuccess;
   {
-    const int64_t nf = (n * n_cross + lzq::kPropBlock - 1) / lzq::kPropBlock;
-    hipLaunchKernelGGL(lzq::lz_follow_kernel, dim3((unsigned)nf), dim3(lzq::kPropBlock), 0, st, d_m_mix, d_dprime,
-                       d_xi, d_v_w, n, n_cross, v_w, window_lz, steps_per_crossing, follow);
+    if (LZQ_FOLLOW_SPLIT) {
+      const int64_t nf = (n * n_cross + lzq::kFollowCells - 1) / lzq::kFollowCells;
+      hipLaunchKernelGGL(lzq::lz_follow_split_kernel, dim3((unsigned)nf), dim3(3 * lzq::kFollowCells), 0, st, d_m_mix,
+                         d_dprime, d_xi, d_v_w, n, n_cross, v_w, window_lz, steps_per_crossing, follow);
+    } else {
+      const int64_t nf = (n * n_cross + lzq::kPropBlock - 1) / lzq::kPropBlock;
+      hipLaunchKernelGGL(lzq::lz_follow_kernel, dim3((unsigned)nf), dim3(lzq::kPropBlock), 0, st, d_m_mix, d_dprime,
+                         d_xi, d_v_w, n, n_cross, v_w, window_lz, steps_per_crossing, follow);
+    }
   }
   if (sort) {
     int32_t* iw = (int32_t*)(ws + follow_bytes);

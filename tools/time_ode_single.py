@@ -32,10 +32,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--interval", type=int, nargs="*", default=[],
                     help="LZQ_TUNE_ODE_TP_INTERVAL values to time as well (default: the library's 64)")
+    ap.add_argument("--lib", default=None, help="a liblzq.so variant to time instead of the in-tree build")
     a = ap.parse_args()
     cfgm = importlib.import_module(bench.PKG + ".config")
     nat = importlib.import_module(bench.PKG + "._native")
-    eng = importlib.import_module(bench.PKG + ".engine").Engine(0)
+    eng = importlib.import_module(bench.PKG + ".engine").Engine(0, **({"lib_path": a.lib} if a.lib else {}))
     cases = {"narrow_wash": {"Gamma_wash_over_H": 1.0, "T_max_over_Tp": 1.6, "T_min_over_Tp": 0.6},
              "narrow_riccati": {"Gamma_wash_over_H": 1.0, "sigma_v_chi_GeV_m2": 1e-12, "T_max_over_Tp": 1.6,
                                 "T_min_over_Tp": 0.6},

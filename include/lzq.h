@@ -339,7 +339,13 @@ int lzq_ode_integrate_shared(const lzq_point* d_points, const lzq_ode_params* d_
  * point of a batch of more than 64.  d_iters (optional, [n] int32): the Newton updates of a point
  * that was stitched; 0: not iterated, -k: iterated k updates, then integrated sequentially.
  * Blocks nothing: the iteration count is fixed (32 rounds of two launches; a converged point's
- * later launches return at once), so the call is stream-ordered like lzq_ode_integrate. */
+ * later launches return at once), so the call is stream-ordered like lzq_ode_integrate.
+ * Scratch (stream-ordered, hipMallocAsync, freed by the call): with L = LZQ_TUNE_ODE_TP_INTERVAL
+ * and M = min(ceil(max_steps / L), 65536) intervals per point, about n M (72 + 32 (2J + 1)) bytes
+ * for the nodes, ends, scans and the two chains' candidate tables, J = 256 when those fit 1 GiB
+ * (else 32), plus n M L 88 bytes of the regular steps' stage rows when they fit 2 GiB (else the
+ * stages are formed inline).  max_steps only sizes it: pass the batch's longest step count
+ * (Engine.ode does), not a generous cap -- e.g. n = 64 with max_steps = 2^22 asks ~4.7 GB. */
 int lzq_ode_integrate_tp(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n,
                          const int32_t* d_table_index, int64_t n_tables, const double* d_work, int64_t work_doubles,
                          int64_t max_steps, lzq_yield* d_out, int32_t* d_status, int32_t* d_iters, void* stream);

@@ -56,8 +56,8 @@ constexpr int kProfBlock = 256;
 #ifndef LZQ_PROF_MIN_WAVES
 #define LZQ_PROF_MIN_WAVES 2
 #endif
-#ifndef LZQ_PROF_UNROLL
-#define LZQ_PROF_UNROLL 1  // Magnus steps per loop iteration (A/B: 2 is 4% slower, tools/ablate_profile.py)
+#ifndef LZQ_PROF_PAIR
+#define LZQ_PROF_PAIR 0  // the interval loop's Magnus steps two per iteration (state in alternating registers)
 #endif
 #ifndef LZQ_PROF_UNIFORM
 #define LZQ_PROF_UNIFORM 1  // waves whose points share one shape read its rows through the scalar cache
@@ -574,7 +574,17 @@ __device__ __forceinline__ double interval_steps(const double* __restrict__ sm, 
 // atan(y_chi / y_B)) have nearly the same S_j, so the key is (shape, cost bin, angle bin), radix
 // sorted (stable) -- tools/profile_order_model.py: executed / useful lane-steps 1.31 with the cost
 // bins alone, 1.16 with this key, on tools/bench_profile.py's workload.
+// Round 6: 6 cost bins per octave, and the angle bins walked up in one cost bin and down in the
+// next (boustrophedon), so a wave that straddles two cost bins holds neighbouring angles, not
+// the two ends of the range: the model's 1.131 -> 1.102 (tools/profile_order_model.py).
 constexpr int kAngleBins = 256;
+#ifndef LZQ_PROF_KEY_SERP
+#define LZQ_PROF_KEY_SERP 1
+#endif
+#ifndef LZQ_PROF_KEY_BINS
+#define LZQ_PROF_KEY_BINS 6
+#endif
+constexpr double kKeyBinsPerOctave = LZQ_PROF_KEY_BINS;  // 128 bins: saturate at 2^21 steps per point
 __global__ __launch_bounds__(kProfBlock) void profile_key_kernel(const double* __restrict__ knots, int32_t n_shapes,
                                                                  int32_t K, const lzq_profile_point* __restrict__ pts,
                                                                  int64_t n, double spr, int32_t n_min,
@@ -596,11 +606,12 @@ __global__ __launch_bounds__(kProfBlock) void profile_key_kernel(const double* _
     st = (LZQ_PROF_UNIFORM && __all(p.shape == s0)) ? cost(knots + s0 * K, samp + s0 * (K - 1) * kProfRec)
                                                     : cost(knots + sl * K, samp + sl * (K - 1) * kProfRec);
   }
-  const double cb = st == st ? fmin(fmax(4.0 * log2(1.0 + st), 0.0), (double)(kCostBins - 1)) : 0.0;
+  const double cb = st == st ? fmin(fmax(kKeyBinsPerOctave * log2(1.0 + st), 0.0), (double)(kCostBins - 1)) : 0.0;
   const uint32_t cost = (uint32_t)((kCostBins - 1) - (int32_t)cb);  // 0 = costliest
   const double ang = atan(p.ychi / p.yB);                            // (-pi/2, pi/2); NaN for 0/0
   const double af = ang == ang ? (ang * (1.0 / 3.141592653589793) + 0.5) * kAngleBins : 0.0;
-  const uint32_t ab = (uint32_t)fmin(fmax(af, 0.0), (double)(kAngleBins - 1));
+  uint32_t ab = (uint32_t)fmin(fmax(af, 0.0), (double)(kAngleBins - 1));
+  if (LZQ_PROF_KEY_SERP && (cost & 1)) ab = (kAngleBins - 1) - ab;  // boustrophedon: see kKeyBinsPerOctave
   const uint32_t sh = valid ? (uint32_t)min(p.shape, 65534) : (uint32_t)min(n_shapes, 65535);  // invalid: last
   keys[i] = (sh << 15) | (cost << 8) | ab;  // shape, 7 + 8 bits
   idx[i] = (int32_t)i;
@@ -675,8 +686,16 @@ __device__ __forceinline__ double propagate_point(const double* __restrict__ rec
     ok = enter_interval(s, j + 2 == K, p, rf, ivw, spr, n_min, start, cD, cM, mp, S) && ok;
     if (kStaged && j + 2 < K) fetch(j + 1, next);
     if (!ok) S = 0.0;
-#pragma unroll LZQ_PROF_UNROLL
-    for (double u = 0.5; u < S; u += 1.0) magnus6_step(mp, u, p0, p1);
+    if (LZQ_PROF_PAIR) {
+      double u = 0.5;
+      for (; u + 1.0 < S; u += 2.0) {
+        magnus6_step(mp, u, p0, p1);
+        magnus6_step(mp, u + 1.0, p0, p1);
+      }
+      if (u < S) magnus6_step(mp, u, p0, p1);
+    } else {
+      for (double u = 0.5; u < S; u += 1.0) magnus6_step(mp, u, p0, p1);
+    }
   };
   if constexpr (kStaged) {
     // two intervals per iteration, so each one's LDS buffer is a constant offset

@@ -5,7 +5,7 @@ ONE process, interleaved rounds, on the synthetic bounce batch of tools/bench_pr
 first variant's bit for bit (variants that change the arithmetic, e.g. polynomial degree, are
 compared at 1e-12 instead).  One JSON line.
 
-    python tools/build_variants.py LZQ_PROF_UNROLL=1 LZQ_PROF_UNROLL=2 ... && python tools/ablate_profile.py
+    python tools/build_variants.py LZQ_PROF_PAIR=0 LZQ_PROF_PAIR=1 ... && python tools/ablate_profile.py [n] [rounds]
 """
 import glob
 import importlib

@@ -691,6 +691,12 @@ struct RicRow {
 #ifndef LZQ_RIC_KRELOAD
 #define LZQ_RIC_KRELOAD 1  // ode_riccati_kernel's lean loop reloads the predictor constants per step (SGPR room)
 #endif
+#ifndef LZQ_RIC_IP
+#define LZQ_RIC_IP 1  // ode_riccati_kernel's lean steps through ric_step_ip (round 6; see there)
+#endif
+#ifndef LZQ_RIC_KPTR
+#define LZQ_RIC_KPTR 1  // the predictor table's address hoisted out of the step loop (see there)
+#endif
 #ifndef LZQ_RIC_V4
 #define LZQ_RIC_V4 1  // ric_newton's dmax without the +0 start (same tests; see there)
 #endif
@@ -826,6 +832,57 @@ __device__ __forceinline__ bool ric_step(double h, const double (&hA2)[3], const
     Zs[2] = Z[2];
     Ychi = Z[2];
   }
+  return ok;
+}
+
+// ric_step with the iterate kept in Zs itself (LZQ_RIC_IP): the start is guess ? g : Y0 (g: the
+// predictor's or block_guess's stages), Newton updates Zs in place, and on success Ychi = Zs[2] --
+// the values ric_step leaves in Zs and Ychi.  A failed step leaves Zs holding the last iterate
+// where ric_step kept g, but its lane is done (no later step or saved state reads Zs), so every
+// value that is read is the same.  The linear branch takes g as ric_step's Zs = g did.
+template <bool kDep>
+__device__ __forceinline__ bool ric_step_ip(double h, const double (&hA2)[3], const double (&lam)[3],
+                                            const double (&E2)[3], const double (&S)[3], const double (&pv)[6],
+                                            double& Ychi, double (&Zs)[3], const double (&g)[3], bool guess) {
+  const bool nonlinear = lam[0] != 0.0 || lam[1] != 0.0 || lam[2] != 0.0;
+  if (!nonlinear) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) Zs[j] = g[j];
+    if (kDep) {
+      double acc = Ychi;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc = __builtin_fma(-hA2[j], S[j], acc);
+      Ychi = acc;
+    }
+    return true;
+  }
+  const double Y0 = Ychi;
+  double hl[3], hl2[3], hS[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    hl[j] = h * lam[j];
+    hl2[j] = 2.0 * hl[j];
+    hS[j] = kDep ? h * S[j] : 0.0;
+    Zs[j] = guess ? g[j] : Y0;
+  }
+  RicJ J;
+  bool near = false;
+  const bool c1 = ric_newton<kDep>(Zs, Y0, hl, hl2, hS, E2, pv, J, false, near);
+  const bool reuse = near;
+  const bool c2 = ric_newton<kDep>(Zs, Y0, hl, hl2, hS, E2, pv, J, reuse, near);
+  bool ok = c1 || c2;
+  if (!ok) {
+#pragma nounroll
+    for (int it = 2; it < 40 && !ok; ++it) ok = ric_newton<kDep>(Zs, Y0, hl, hl2, hS, E2, pv, J, false, near);
+    if (!ok && guess) {
+      Zs[0] = Y0;
+      Zs[1] = Y0;
+      Zs[2] = Y0;
+#pragma nounroll
+      for (int it = 0; it < 40 && !ok; ++it) ok = ric_newton<kDep>(Zs, Y0, hl, hl2, hS, E2, pv, J, false, near);
+    }
+  }
+  if (ok) Ychi = Zs[2];
   return ok;
 }
 
@@ -1060,12 +1117,73 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
     // compare per step.  (Peeling row 0 of aligned blocks, with pass 1 run on to the next block,
     // measured slower: profiles/round5/ablate_ode_pred_block.json.)
     const int rz = (int)((-kb) & (int64_t)(LZQ_ODE_PRED_BLOCK - 1));
+    // LZQ_RIC_KPTR: the predictor table's address formed once per block of steps (two SGPRs), so a
+    // step's reload is the constants' own scalar loads, not a GOT load and then them
+    const __attribute__((address_space(4))) double* kp_loop =
+        (const __attribute__((address_space(4))) double*)&kRadauPred[0][0];
+    if (LZQ_RIC_KPTR) asm volatile("" : "+s"(kp_loop));  // opaque: not re-formed in the loop
     // a wave with no depleting lane runs the loop without the source products (ric_step<false>)
     auto lean_steps = [&](auto dep_tag) {
     constexpr bool kDep = decltype(dep_tag)::value;
     // LZQ_RIC_V4: a uniform trip count, each lane's steps under !done (a lane whose Newton iteration
     // failed stops there, as in the loop below)
     const int nr = (int)(kend - kb);
+    if (LZQ_RIC_IP) {
+      // the same steps with the loop-carried values written once each (ric_step_ip): the predictor
+      // and block_guess fill g, the iterate lives in Zs, Y_B is committed only on success and the
+      // status once after the loop (a lane done here failed here) -- the loop below copied Y_chi,
+      // Y_B, the stages and the status between registers at every step's joins
+      const bool done0 = done;
+      for (int r = 0; r < nr; ++r) {
+        const RicRow row = s_row[wv][r];
+        const YbCD rc = s_rcd[wv][r];
+        if (done) continue;
+        const double Ystart = Ychi;
+        bool use_guess = false;
+        double g[3] = {Zs[0], Zs[1], Zs[2]};  // Zs as it stands unless a guess replaces it
+        if (riccati && have && r != rz) {
+          const __attribute__((address_space(4))) double* kp = kp_loop;
+          if (LZQ_RIC_KRELOAD) asm volatile("" : "+s"(kp));
+          use_guess = true;
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            g[j] = fma_s(Zs[2], kp[4 * j + 3], fma_s(Zs[1], kp[4 * j + 2], fma_s(Zs[0], kp[4 * j + 1], kp[4 * j] * Yp)));
+            use_guess = use_guess && fabs(g[j] - Ychi) <= 0.25 * fabs(Ychi);
+          }
+        }
+        bool ok = true;
+        if ((xok >> r) & 1) {
+          double lam[3], E2[3], S[3];
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            S[j] = kDep ? (deplete ? Pf * row.a[j] : 0.0) : 0.0;
+            lam[j] = sigmav * row.lam[j];
+            E2[j] = row.E2[j];
+          }
+          const double YBn = __builtin_fma(rc.c, YB, Pf * rc.d);
+          if (riccati && r == rz) {
+            OdeStage sg[3];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+              sg[j].lam = lam[j];
+              sg[j].E2 = E2[j];
+              sg[j].S = S[j];
+            }
+            use_guess = block_guess(R, hu, sg, Ychi, g);
+          }
+          ok = ric_step_ip<kDep>(hu, hA2, lam, E2, S, pv, Ychi, Zs, g, use_guess);
+          if (ok) YB = YBn;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 3; ++j) Zs[j] = g[j];
+        }
+        have = true;
+        Yp = Ystart;
+        done = !ok;
+      }
+      if (done && !done0) st = LZQ_ODE_NEWTON;
+      return;
+    }
     for (int r = 0; r < nr && (LZQ_RIC_V4 || !done); ++r) {
       // the same step as the loop below: the row is read first (its LDS latency under the
       // predictor), the x guard is the fill's mask bit, the step index needs no counter
@@ -1078,8 +1196,8 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
       if (riccati && have && r != rz) {
         // the predictor's 12 constants are read from the constant cache each step (scalar loads
         // through an opaque pointer) instead of held in 24 SGPRs across the loop (LZQ_RIC_KRELOAD)
-        const __attribute__((address_space(4))) double* kp =
-            (const __attribute__((address_space(4))) double*)&kRadauPred[0][0];
+        const __attribute__((address_space(4))) double* kp = LZQ_RIC_KPTR ? kp_loop
+            : (const __attribute__((address_space(4))) double*)&kRadauPred[0][0];
         if (LZQ_RIC_KRELOAD) asm volatile("" : "+s"(kp));
         double g[3];
         use_guess = true;

@@ -692,7 +692,7 @@ struct RicRow {
 #define LZQ_RIC_KRELOAD 1  // ode_riccati_kernel's lean loop reloads the predictor constants per step (SGPR room)
 #endif
 #ifndef LZQ_RIC_IP
-#define LZQ_RIC_IP 1  // ode_riccati_kernel's lean steps through ric_step_ip (round 6; see there)
+#define LZQ_RIC_IP 2  // ode_riccati_kernel's lean steps through ric_step_ip (round 6; see there); 2: have / Yp outside the joins
 #endif
 #ifndef LZQ_RIC_KPTR
 #define LZQ_RIC_KPTR 1  // the predictor table's address hoisted out of the step loop (see there)
@@ -1138,10 +1138,10 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
         const RicRow row = s_row[wv][r];
         const YbCD rc = s_rcd[wv][r];
         if (done) continue;
-        const double Ystart = Ychi;
         bool use_guess = false;
         double g[3] = {Zs[0], Zs[1], Zs[2]};  // Zs as it stands unless a guess replaces it
-        if (riccati && have && r != rz) {
+        // a lane that is not done has taken steps 0 .. r - 1 of this block, so have = have || r > 0
+        if (riccati && (LZQ_RIC_IP < 2 || r > 0 || have) && (LZQ_RIC_IP >= 2 || have) && r != rz) {
           const __attribute__((address_space(4))) double* kp = kp_loop;
           if (LZQ_RIC_KRELOAD) asm volatile("" : "+s"(kp));
           use_guess = true;
@@ -1151,6 +1151,8 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
             use_guess = use_guess && fabs(g[j] - Ychi) <= 0.25 * fabs(Ychi);
           }
         }
+        const double Ystart = Ychi;
+        if (LZQ_RIC_IP >= 2) Yp = Ystart;  // the predictor has read the previous one
         bool ok = true;
         if ((xok >> r) & 1) {
           double lam[3], E2[3], S[3];
@@ -1177,10 +1179,13 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
 #pragma unroll
           for (int j = 0; j < 3; ++j) Zs[j] = g[j];
         }
-        have = true;
-        Yp = Ystart;
+        if (LZQ_RIC_IP < 2) {
+          have = true;
+          Yp = Ystart;
+        }
         done = !ok;
       }
+      if (LZQ_RIC_IP >= 2 && nr > 0 && !done0) have = true;
       if (done && !done0) st = LZQ_ODE_NEWTON;
       return;
     }

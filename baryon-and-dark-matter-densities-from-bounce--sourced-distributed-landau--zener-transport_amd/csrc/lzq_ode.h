@@ -594,6 +594,9 @@ __device__ __forceinline__ double fma_neg_s(double k, double a, double p) {
 #ifndef LZQ_ODE_RICVAR
 #define LZQ_ODE_RICVAR 1  // whole-wave cooperative split-free waves run ode_riccati_kernel (compact rows, uniform constants)
 #endif
+#ifndef LZQ_ODE_RICTAB
+#define LZQ_ODE_RICTAB 1  // table-varying whole waves too, through ode_riccati_kernel<., true> (round 6; RicRowT)
+#endif
 #ifndef LZQ_ODE_PRED_BLOCK
 // The Radau5 predictor is not used on steps k = 0 (mod LZQ_ODE_PRED_BLOCK): every block of that
 // many steps starts its Newton iteration from Y_chi, so a block's end state is a function of its

@@ -457,7 +457,9 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
       // whole-wave cooperative, one table, one Gamma_wash: ode_riccati_kernel steps it, split steps
       // included unless the x rounding makes the split search unreliable (k_split = -1: every step
       // takes the general path here) -- LZQ_ODE_RICVAR; the same predicate there, on the same values
-      if (LZQ_ODE_RICVAR && !kChiOnly && G == 64 && !tab_vary && rec_shared && __all(k_split != -1)) return;
+      if (LZQ_ODE_RICVAR && !kChiOnly && G == 64 && (!tab_vary || LZQ_ODE_RICTAB) && rec_shared &&
+          __all(k_split != -1))
+        return;
     }
     const int64_t block = coop ? G : N;
     for (int64_t kb = k_begin; kb < k_stop; kb += block) {
@@ -691,6 +693,9 @@ struct RicRow {
 #ifndef LZQ_RIC_KRELOAD
 #define LZQ_RIC_KRELOAD 1  // ode_riccati_kernel's lean loop reloads the predictor constants per step (SGPR room)
 #endif
+#ifndef LZQ_RIC_TAB_MIN_WAVES
+#define LZQ_RIC_TAB_MIN_WAVES 3  // its rows take 38 KB of LDS per 4-wave block: 3 blocks per CU
+#endif
 #ifndef LZQ_RIC_IP
 #define LZQ_RIC_IP 2  // ode_riccati_kernel's lean steps through ric_step_ip (round 6; see there); 2: have / Yp outside the joins
 #endif
@@ -724,6 +729,41 @@ __device__ __noinline__ void ric_fill(const OdePoint* ou, const double* __restri
   const double beta[3] = {bt[0], bt[1], bt[2]}, a[3] = {row->a[0], row->a[1], row->a[2]};
   const YbRec yr = yb_rec(radau_h(R, h), beta, a);
   *rcd = {yr.c, yr.d};
+}
+
+// ode_riccati_kernel<., kTab = true> (LZQ_ODE_RICTAB, round 6): whole waves whose points agree in
+// everything but the A/V kernel (I_p, v_w: a spline table each), the table-varying waves the
+// general variant stepped.  A row then holds what every lane shares -- lam, E2, the spline location
+// (s, k) and a / Av (ap) of each stage, and the Y_B step map's c, W, id (which do not depend on a)
+// -- and each lane forms a_j = Av(own table; s_j, k_j) * ap_j and d = yb_d(W, a) itself: the
+// general variant's row_a / stage_scale / yb_d on the same values, so the same bits.
+struct RicRowT {
+  double lam[3], E2[3], ap[3], s[3];
+  double W[3], id, c;
+  int k[3];
+};
+
+__device__ __noinline__ void ric_fill_tab(const OdePoint* ou, const double* __restrict__ wu, double xk, double h,
+                                          RicRowT* row, double* bt) {
+  const Radau R = radau_tableau();
+#pragma unroll 1
+  for (int j = 0; j < 3; ++j) {
+    const double cj = j == 0 ? R.c[0] : (j == 1 ? R.c[1] : R.c[2]);
+    const StageBase bs = ode_stage_base(*ou, wu, xk + cj * h);
+    row->lam[j] = bs.lam;
+    row->E2[j] = bs.E2;
+    row->ap[j] = bs.ap;
+    row->s[j] = bs.s;
+    row->k[j] = bs.k;
+    bt[j] = ou->gamma_w * bs.beta;
+  }
+  const double beta[3] = {bt[0], bt[1], bt[2]}, none[3] = {0.0, 0.0, 0.0};  // d is each lane's
+  const YbRec yr = yb_rec(radau_h(R, h), beta, none);
+  row->W[0] = yr.W[0];
+  row->W[1] = yr.W[1];
+  row->W[2] = yr.W[2];
+  row->id = yr.id;
+  row->c = yr.c;
 }
 
 // radau_step<false>'s transformed Newton iteration (newton_j) for ode_riccati_kernel: the same
@@ -891,14 +931,15 @@ __device__ __forceinline__ bool ric_step_ip(double h, const double (&hA2)[3], co
 // split-step code, each lane forming its own stages: two steps, so registers do not matter),
 // 2: the regular steps after it -- with its state handed on in OdeState; so the regular-step
 // kernels (0, 2) carry no split code.  A wave with no split in range runs in pass 0 alone.
-template <int kPhase>
-__global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) void ode_riccati_kernel(
-    const lzq_point* __restrict__ pts, const lzq_ode_params* __restrict__ ode, int64_t n,
-    const int32_t* __restrict__ tidx, const double* __restrict__ ws, int64_t max_steps, lzq_yield* __restrict__ out,
-    int32_t* __restrict__ status, int coop_on, int64_t k_lo, int64_t k_cnt, OdeState* __restrict__ state,
-    const int32_t* __restrict__ skip) {
-  __shared__ RicRow s_row[kOdeBlock / 64][64];
-  __shared__ YbCD s_rcd[kOdeBlock / 64][64];
+template <int kPhase, bool kTab = false>
+__global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : (kTab ? LZQ_RIC_TAB_MIN_WAVES : LZQ_RIC_MIN_WAVES)) void
+ode_riccati_kernel(const lzq_point* __restrict__ pts, const lzq_ode_params* __restrict__ ode, int64_t n,
+                   const int32_t* __restrict__ tidx, const double* __restrict__ ws, int64_t max_steps,
+                   lzq_yield* __restrict__ out, int32_t* __restrict__ status, int coop_on, int64_t k_lo, int64_t k_cnt,
+                   OdeState* __restrict__ state, const int32_t* __restrict__ skip) {
+  __shared__ RicRow s_row[kOdeBlock / 64][kTab ? 1 : 64];
+  __shared__ YbCD s_rcd[kOdeBlock / 64][kTab ? 1 : 64];
+  __shared__ RicRowT s_rowt[kOdeBlock / 64][kTab ? 64 : 1];
   __shared__ OdePoint s_pt[kOdeBlock / 64];
   __shared__ double s_beta[kOdeBlock / 64][64][3];  // the fill's beta_j (Gamma_wash * base)
 
@@ -929,7 +970,8 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
   const bool eq = same(o.m) && same(o.Tp) && same(o.B) && same(o.sig) && same(o.H0) && same(o.s0) && same(o.c_rel) &&
                   same(o.c_nr) && same(o.v0) && same(o.T_lo) && same(o.T_hi);
   if (!__all(eq)) return;                                                    // G < 64
-  if (!__all(same(__builtin_bit_cast(double, w)))) return;                   // tab_vary
+  if (__all(same(__builtin_bit_cast(double, w))) == kTab) return;            // tab_vary: the kTab kernel's
+  if (kTab && !LZQ_ODE_RICTAB) return;
   if (!__all(same(o.gamma_w))) return;                                       // !rec_shared
   if (LZQ_ODE_LINFAST && __all(o.sigmav == 0.0)) return;                     // lin_wave
   const int64_t N = (int64_t)steps;
@@ -1040,7 +1082,7 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
         OdeStage sg[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-          const StageBase b = ode_stage_base(ou, wu, xs + R.c[j] * hs);
+          const StageBase b = ode_stage_base(ou, kTab ? w : wu, xs + R.c[j] * hs);
           sg[j].alpha = Pf * b.a;
           sg[j].S = deplete ? sg[j].alpha : 0.0;
           sg[j].lam = sigmav * b.lam;
@@ -1076,6 +1118,8 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
 #pragma unroll
     for (int q = 0; q < 6; ++q) asm volatile("" : "+v"(pv[q]));
   }
+  int kc = -1;                             // kTab: the spline interval held in cc
+  double cc[4] = {0.0, 0.0, 0.0, 0.0};
   for (int64_t kb = pk_begin; kPhase != 1 && kb < pk_stop; kb += 64) {
     const int64_t kend = kb + 64 < pk_stop ? kb + 64 : pk_stop;
     uint64_t xok = 0;
@@ -1087,7 +1131,9 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
         xok = __ballot(kl < kend && xk + hu > xk);
       }
       if (kl < kend) {
-        if (LZQ_RIC_LEAN) {
+        if (kTab) {
+          ric_fill_tab(&s_pt[wv], wu, x0u + (double)kl * hu, hu, &s_rowt[wv][lane], s_beta[wv][lane]);
+        } else if (LZQ_RIC_LEAN) {
           ric_fill(&s_pt[wv], wu, x0u + (double)kl * hu, hu, &s_row[wv][lane], s_beta[wv][lane], &s_rcd[wv][lane]);
         } else {
         const double xk = x0u + (double)kl * hu;
@@ -1128,15 +1174,15 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
     // LZQ_RIC_V4: a uniform trip count, each lane's steps under !done (a lane whose Newton iteration
     // failed stops there, as in the loop below)
     const int nr = (int)(kend - kb);
-    if (LZQ_RIC_IP) {
+    if (LZQ_RIC_IP || kTab) {
       // the same steps with the loop-carried values written once each (ric_step_ip): the predictor
       // and block_guess fill g, the iterate lives in Zs, Y_B is committed only on success and the
       // status once after the loop (a lane done here failed here) -- the loop below copied Y_chi,
       // Y_B, the stages and the status between registers at every step's joins
       const bool done0 = done;
       for (int r = 0; r < nr; ++r) {
-        const RicRow row = s_row[wv][r];
-        const YbCD rc = s_rcd[wv][r];
+        const RicRow row = s_row[wv][kTab ? 0 : r];
+        const YbCD rc = s_rcd[wv][kTab ? 0 : r];
         if (done) continue;
         bool use_guess = false;
         double g[3] = {Zs[0], Zs[1], Zs[2]};  // Zs as it stands unless a guess replaces it
@@ -1156,13 +1202,37 @@ __global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : LZQ_RIC_MIN_WAVES) voi
         bool ok = true;
         if ((xok >> r) & 1) {
           double lam[3], E2[3], S[3];
+          double YBn;
+          if constexpr (kTab) {
+            // this lane's a_j from its own table at the row's (shared) spline location: the interval's
+            // four coefficients are reloaded only when k changes (wave-uniform; spline_at's
+            // operations on the same values), d from the row's W, id
+            const RicRowT& rw = s_rowt[wv][r];
+            double a[3];
 #pragma unroll
-          for (int j = 0; j < 3; ++j) {
-            S[j] = kDep ? (deplete ? Pf * row.a[j] : 0.0) : 0.0;
-            lam[j] = sigmav * row.lam[j];
-            E2[j] = row.E2[j];
+            for (int j = 0; j < 3; ++j) {
+              const int kj = __builtin_amdgcn_readfirstlane(rw.k[j]);
+              if (kj != kc) {
+                kc = kj;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) cc[q] = w[4 * kj + q];
+              }
+              a[j] = spline_cubic(cc, rw.s[j]) * rw.ap[j];
+              S[j] = kDep ? (deplete ? Pf * a[j] : 0.0) : 0.0;
+              lam[j] = sigmav * rw.lam[j];
+              E2[j] = rw.E2[j];
+            }
+            const double d = yb_d(YbW{{rw.W[0], rw.W[1], rw.W[2]}, rw.id}, a);
+            YBn = __builtin_fma(rw.c, YB, Pf * d);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+              S[j] = kDep ? (deplete ? Pf * row.a[j] : 0.0) : 0.0;
+              lam[j] = sigmav * row.lam[j];
+              E2[j] = row.E2[j];
+            }
+            YBn = __builtin_fma(rc.c, YB, Pf * rc.d);
           }
-          const double YBn = __builtin_fma(rc.c, YB, Pf * rc.d);
           if (riccati && r == rz) {
             OdeStage sg[3];
 #pragma unroll
@@ -1582,6 +1652,23 @@ int launch_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int
                            d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, lzq::g_ode_coop, k_lo,
                            k_cnt, st, d_skip);
         rc = hip_check(hipGetLastError(), fn);
+        if constexpr (LZQ_ODE_RICTAB) {  // the table-varying waves' three passes
+          if (rc != LZQ_OK) return rc;
+          hipLaunchKernelGGL((lzq::ode_riccati_kernel<0, true>), dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0,
+                             s, d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, lzq::g_ode_coop, k_lo,
+                             k_cnt, st, d_skip);
+          rc = hip_check(hipGetLastError(), fn);
+          if (rc != LZQ_OK) return rc;
+          hipLaunchKernelGGL((lzq::ode_riccati_kernel<1, true>), dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0,
+                             s, d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, lzq::g_ode_coop, k_lo,
+                             k_cnt, st, d_skip);
+          rc = hip_check(hipGetLastError(), fn);
+          if (rc != LZQ_OK) return rc;
+          hipLaunchKernelGGL((lzq::ode_riccati_kernel<2, true>), dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0,
+                             s, d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, lzq::g_ode_coop, k_lo,
+                             k_cnt, st, d_skip);
+          rc = hip_check(hipGetLastError(), fn);
+        }
       }
     }
     if constexpr (LZQ_ODE_LINFAST && LZQ_ODE_YBREC && !kChiOnly) {

@@ -605,6 +605,48 @@ def test_ode_cooperative_table_varying_bit_identical(gpu_engine):
                 assert rel_err(v, w) < 1e-10, (v, w)
 
 
+def test_ode_riccati_table_varying_bit_identical(gpu_engine):
+    """Whole waves whose points differ in the A/V kernel (I_p, v_w: a spline table each), P, flux,
+    sigma_v and deplete, with one Gamma_wash per wave: ode_riccati_kernel<., true> (LZQ_ODE_RICTAB)
+    steps them, each lane forming a and Y_B's d from its own table at the rows' shared spline
+    location.  The per-lane mode's bits, with a split step (m_chi = 40 crosses T = m/3 inside the
+    window: the kernel's three passes) and without (m_chi = 0.95), in one launch and as
+    continuation launches; and the C restatement's values."""
+    rng = np.random.default_rng(97)
+    cfgs = []
+    for m_chi in (0.95, 40.0):
+        for gw in (0.0, 0.5):
+            for _ in range(64):   # one whole wave (group_waves=False keeps the order)
+                c = full_cfg(BASE_CFG)
+                c.update(NARROW, m_chi_GeV=m_chi, I_p=float(rng.uniform(0.1, 1.0)), v_w=float(rng.uniform(0.1, 0.9)),
+                         P_chi_to_B=float(rng.uniform(0.05, 1.0)), incident_flux_scale=float(10 ** rng.uniform(-10, -8)),
+                         Gamma_wash_over_H=gw, sigma_v_chi_GeV_m2=float(rng.choice([1e-16, 1e-12])),
+                         deplete_DM_from_source=bool(rng.uniform() < 0.3))
+                cfgs.append(c)
+    p, o = recs(cfgs)
+    a, sa = gpu_engine.ode(p, o, group_waves=False)
+    assert bool((sa == 0).all())
+    prev = gpu_engine.tune_ode_coop(False)     # every wave per lane: the general variant's own stages
+    try:
+        b, sb = gpu_engine.ode(p, o, group_waves=False)
+    finally:
+        gpu_engine.tune_ode_coop(prev)
+    assert torch_equal(sa, sb) and torch_equal(a, b)
+    g, sg = gpu_engine.ode(p, o)               # regrouped for the launch, scattered back
+    assert torch_equal(a, g) and torch_equal(sa, sg)
+    prev = gpu_engine.tune_ode_launch_steps(11)
+    try:
+        c, sc = gpu_engine.ode(p, o, group_waves=False)
+    finally:
+        gpu_engine.tune_ode_launch_steps(prev)
+    assert torch_equal(a, c) and torch_equal(sa, sc)
+    ref, sr = O.ode_batch(cfgs[::16], nthreads=16)
+    for row, rr, s2 in zip(a.cpu().numpy()[::16], ref, sr):
+        assert s2 == 0
+        for v, w in zip(row[:5], rr[:5]):
+            assert rel_err(v, w) < 1e-10, (v, w)
+
+
 def test_ode_linear_waves_table_varying_bit_identical(gpu_engine):
     """Linear cooperative waves (sigma_v = 0, one Gamma_wash per segment) whose points each have
     their own A/V kernel (I_p): the tight loop forms a_j from each lane's table, reading the lane's

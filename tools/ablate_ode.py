@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Time the ODE fallback (Engine.ode, one chunk of up to 2^18 points) of every library variant under
 <package>/_build/variants/ in ONE process, interleaved rounds, on tools/bench_ode.py's
-narrow-window and stiff cases.  Variants must agree with the first one to 1e-11.
+narrow-window and stiff cases (ABLATE_GENERAL=1: also an I_p x v_w sweep, table-varying
+cooperative waves and per-lane waves -- the general variant's).  Variants must agree with the first one to 1e-11.
 
     python tools/ablate_ode.py [n_points] [rounds] [radau|quadrature]
 """
@@ -34,6 +35,11 @@ def main():
              "stiff_thermal": {"sigma_v_chi_GeV_m2": 1e-9, "regime": "thermal", "m_chi_GeV": 300.0,
                                "T_max_over_Tp": 1.3, "T_min_over_Tp": 0.2},
              "riccati_mchi_sv": {"T_max_over_Tp": 1.6, "T_min_over_Tp": 0.6}}
+    if os.environ.get("ABLATE_GENERAL"):
+        # the general variant's waves: an A/V-parameter sweep (I_p x v_w fastest: a spline table per
+        # point, cooperative table-varying waves) and the same points with every wave mixed (per lane)
+        cases["riccati_ipvw"] = {"T_max_over_Tp": 1.6, "T_min_over_Tp": 0.6, "sigma_v_chi_GeV_m2": 1e-12}
+        cases["riccati_ipvw_perlane"] = dict(cases["riccati_ipvw"])
     out = {}
     for cname, over in cases.items():
         cfgs = cfgs_for(over, n)
@@ -41,11 +47,16 @@ def main():
             for i, c in enumerate(cfgs):
                 c["m_chi_GeV"] = (0.95, 3.0, 10.0, 30.0)[i % 4]
                 c["sigma_v_chi_GeV_m2"] = 10.0 ** (-20 + ((i // 4) % 16) * 0.6)
+        if cname.startswith("riccati_ipvw"):
+            for i, c in enumerate(cfgs):
+                c["I_p"] = (0.1, 0.2, 0.4, 0.8)[i % 4]
+                c["v_w"] = (0.2, 0.4, 0.6, 0.8)[(i // 4) % 4]
+        kw = {"group_waves": False} if cname.endswith("_perlane") else {}
         pts = np.concatenate([cfgm.to_point(c) for c in cfgs])
         ods = np.concatenate([cfgm.to_ode_params(c) for c in cfgs])
         ref = None
         for k, e in engs.items():  # warm-up + agreement
-            t = e.ode(pts[:256], ods[:256], method=method)[0].cpu().numpy()
+            t = e.ode(pts[:256], ods[:256], method=method, **kw)[0].cpu().numpy()
             if ref is None:
                 ref = t
             if not os.environ.get("ABLATE_NOCHECK"):  # diagnostic variants that change results
@@ -56,7 +67,7 @@ def main():
             for k, e in engs.items():
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
-                last[k] = e.ode(pts, ods, chunk=1 << 18, method=method)[0]
+                last[k] = e.ode(pts, ods, chunk=1 << 18, method=method, **kw)[0]
                 torch.cuda.synchronize()
                 res[k].append(n / (time.perf_counter() - t0))
         out[cname] = {k: round(max(v)) for k, v in res.items()}

@@ -633,9 +633,11 @@ REUSE_MAX_BYTES = 16 << 30     # Engine.sweep(reuse=True): z-sum tables beyond t
 
 def wave_order(d_pts: torch.Tensor, d_ode: torch.Tensor, n: int):
     """A launch order (int64 permutation tensor, on the points' device) that makes points equal
-    in _native.ODE_COOP_KEY (and deplete) contiguous -- and within such a run, points equal in the
-    whole ODE_STAGE_KEY (same spline table) -- or None when the input is already grouped or has
-    no repeated keys.  d_pts / d_ode: the lzq_point / lzq_ode_params records as byte tensors.  A
+    in _native.ODE_COOP_KEY, deplete and Gamma_wash contiguous -- and within such a run, points
+    equal in the whole ODE_STAGE_KEY (same spline table) -- or None when the input is already
+    grouped or has no repeated keys.  Gamma_wash (round 6): a whole wave with one Gamma_wash shares
+    Y_B's step maps and runs the Riccati kernel, a wave that mixes several runs the general variant
+    (DESIGN §4.3).  d_pts / d_ode: the lzq_point / lzq_ode_params records as byte tensors.  A
     64-bit mix of the key fields' bits is sorted stably; a hash collision only puts unequal
     points in one wavefront, which the kernel detects and runs per lane."""
     if n <= 64:
@@ -654,6 +656,8 @@ def wave_order(d_pts: torch.Tensor, d_ode: torch.Tensor, n: int):
 
     h = mix(torch.zeros(n, dtype=torch.int64, device=d_pts.device), _native.ODE_COOP_KEY)
     h = (h * _MIX) ^ o32[:, _native.ODE_DTYPE.fields["deplete_DM_from_source"][1] // 4].to(torch.int64)
+    o64 = d_ode.view(n, _native.ODE_DTYPE.itemsize).view(torch.int64)
+    h = (h * _MIX) ^ o64[:, _native.ODE_DTYPE.fields["Gamma_wash_over_H"][1] // 8]
     breaks = int((h[1:] != h[:-1]).sum())
     if breaks == 0:
         return None

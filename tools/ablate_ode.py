@@ -40,6 +40,10 @@ def main():
         # point, cooperative table-varying waves) and the same points with every wave mixed (per lane)
         cases["riccati_ipvw"] = {"T_max_over_Tp": 1.6, "T_min_over_Tp": 0.6, "sigma_v_chi_GeV_m2": 1e-12}
         cases["riccati_ipvw_perlane"] = dict(cases["riccati_ipvw"])
+        # a Gamma_wash x sigma_v sweep (Gamma_wash fastest): grouped by the engine's wave order into
+        # one Gamma_wash per wave, and as given (every wave mixes four: the general variant)
+        cases["riccati_gw"] = {"T_max_over_Tp": 1.6, "T_min_over_Tp": 0.6}
+        cases["riccati_gw_perlane"] = dict(cases["riccati_gw"])
     out = {}
     for cname, over in cases.items():
         cfgs = cfgs_for(over, n)
@@ -51,6 +55,10 @@ def main():
             for i, c in enumerate(cfgs):
                 c["I_p"] = (0.1, 0.2, 0.4, 0.8)[i % 4]
                 c["v_w"] = (0.2, 0.4, 0.6, 0.8)[(i // 4) % 4]
+        if cname.startswith("riccati_gw"):
+            for i, c in enumerate(cfgs):
+                c["Gamma_wash_over_H"] = (0.1, 0.5, 2.0, 8.0)[i % 4]
+                c["sigma_v_chi_GeV_m2"] = 10.0 ** (-20 + ((i // 4) % 16) * 0.6)
         kw = {"group_waves": False} if cname.endswith("_perlane") else {}
         pts = np.concatenate([cfgm.to_point(c) for c in cfgs])
         ods = np.concatenate([cfgm.to_ode_params(c) for c in cfgs])

@@ -269,6 +269,13 @@ __global__ __launch_bounds__(64 * kSplWaves) void ode_spline_wave_kernel(const l
 // kLin: the variant for linear cooperative waves (see lin_wave below); every launch runs both
 // variants, each stepping only its own wavefronts (the other variant's return at once), so the
 // linear waves' tight loop does not share a register allocation with the Riccati Newton path.
+#ifndef LZQ_ODE_GEN_RICSTEP
+#define LZQ_ODE_GEN_RICSTEP 1  // the general variant's regular Riccati steps through ric_step (round 6)
+#endif
+template <bool kDep>
+__device__ bool ric_step(double h, const double (&hA2)[3], const double (&lam)[3], const double (&E2)[3],
+                         const double (&S)[3], const double (&pv)[6], double& Ychi, double (&Zs)[3], bool guess);
+
 template <bool kChiOnly, bool kLin = false, bool kNoSplit = false>
 __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_kernel(const lzq_point* __restrict__ pts,
                                                                   const lzq_ode_params* __restrict__ ode, int64_t n,
@@ -604,7 +611,21 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
               r = {yr.c, yr.d};
             }
             YB = __builtin_fma(r.c, YB, o.Pf * r.d);
-            ok = radau_step<false>(split ? radau_h(R, hs) : hA, sg, Ychi, YB, Zs, use_guess);
+            if (LZQ_ODE_GEN_RICSTEP && !split) {  // the same operations through ric_step (see there)
+              double lam[3], E2[3], S[3];
+#pragma unroll
+              for (int j = 0; j < 3; ++j) {
+                lam[j] = sg[j].lam;
+                E2[j] = sg[j].E2;
+                S[j] = sg[j].S;
+              }
+              const double hA2[3] = {hA.a[2][0], hA.a[2][1], hA.a[2][2]};
+              const double pv[6] = {kRadauAinvP[1], kRadauAinvP[2], kRadauAinvP[3],
+                                    kRadauAinvP[5], kRadauAinvP[6], kRadauAinvP[7]};
+              ok = ric_step<true>(h, hA2, lam, E2, S, pv, Ychi, Zs, use_guess);
+            } else {
+              ok = radau_step<false>(split ? radau_h(R, hs) : hA, sg, Ychi, YB, Zs, use_guess);
+            }
           } else {
             ok = radau_step<!kChiOnly>(split ? radau_h(R, hs) : hA, sg, Ychi, YB, Zs, use_guess);
           }

@@ -44,6 +44,8 @@ def main():
         # one Gamma_wash per wave, and as given (every wave mixes four: the general variant)
         cases["riccati_gw"] = {"T_max_over_Tp": 1.6, "T_min_over_Tp": 0.6}
         cases["riccati_gw_perlane"] = dict(cases["riccati_gw"])
+        # 16 points per m_chi (16 sigma_v each): 16-lane cooperative segments, the general variant
+        cases["riccati_g16"] = {"T_max_over_Tp": 1.6, "T_min_over_Tp": 0.6}
     out = {}
     for cname, over in cases.items():
         cfgs = cfgs_for(over, n)
@@ -55,6 +57,10 @@ def main():
             for i, c in enumerate(cfgs):
                 c["I_p"] = (0.1, 0.2, 0.4, 0.8)[i % 4]
                 c["v_w"] = (0.2, 0.4, 0.6, 0.8)[(i // 4) % 4]
+        if cname == "riccati_g16":
+            for i, c in enumerate(cfgs):
+                c["m_chi_GeV"] = 0.5 + 0.001 * (i // 16)
+                c["sigma_v_chi_GeV_m2"] = 10.0 ** (-20 + (i % 16) * 0.6)
         if cname.startswith("riccati_gw"):
             for i, c in enumerate(cfgs):
                 c["Gamma_wash_over_H"] = (0.1, 0.5, 2.0, 8.0)[i % 4]

@@ -1673,7 +1673,8 @@ int launch_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int
                            d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, lzq::g_ode_coop, k_lo,
                            k_cnt, st, d_skip);
         rc = hip_check(hipGetLastError(), fn);
-        if constexpr (LZQ_ODE_RICTAB) {  // the table-varying waves' three passes
+        // the table-varying waves' three passes (none for one point: its wave is clones of it)
+        if (LZQ_ODE_RICTAB && n > 1) {
           if (rc != LZQ_OK) return rc;
           hipLaunchKernelGGL((lzq::ode_riccati_kernel<0, true>), dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0,
                              s, d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, lzq::g_ode_coop, k_lo,

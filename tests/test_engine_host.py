@@ -87,6 +87,28 @@ def test_wave_order_groups_across_tables():
     assert set(pkg("_native").ODE_COOP_KEY) == set(pkg("_native").ODE_STAGE_KEY) - {"I_p", "v_w"}
 
 
+def test_wave_order_groups_gamma_wash():
+    """Gamma_wash is part of the order's key (round 6): a wave with one Gamma_wash shares Y_B's step
+    maps and runs the Riccati kernel.  A Gamma_wash x sigma_v sweep with Gamma_wash fastest -- one
+    cooperative group in the stage key alone, so the old key left it as given -- comes out in
+    contiguous Gamma_wash runs, each in its original relative order."""
+    rng = np.random.default_rng(12)
+    cfgs = []
+    for i in range(512):
+        c = full_cfg(BASE_CFG)
+        c.update(Gamma_wash_over_H=(0.1, 0.5, 2.0, 8.0)[i % 4], sigma_v_chi_GeV_m2=10.0 ** (-20 + (i // 4) % 16),
+                 P_chi_to_B=float(rng.uniform(0.1, 1.0)))
+        cfgs.append(c)
+    p, o = _recs(cfgs)
+    order = _order(p, o)
+    assert order is not None and sorted(order.tolist()) == list(range(len(cfgs)))
+    g = o["Gamma_wash_over_H"][order]
+    assert int(np.count_nonzero(g[1:] != g[:-1])) == 3          # four contiguous Gamma_wash runs
+    for val in (0.1, 0.5, 2.0, 8.0):
+        assert np.all(np.diff(order[g == val]) > 0)
+    assert _order(p[order], o[order]) is None                  # grouped input is left as it is
+
+
 def test_ode_step_counts_device_equals_host():
     """Engine.ode sizes its continuation launches from ode_step_counts_device (torch ops on the
     device records); it must give the numpy ode_step_counts' values exactly, edge cases included

@@ -342,8 +342,9 @@ class Engine:
             top = float(need_h.max()) + 64 if need_h.size else 0
         else:
             need = ode_step_counts_device(d_pts_all, n)   # same values as ode_step_counts, on the device
-            need = need[torch.isfinite(need)]
-            top = float(need.max()) + 64 if need.numel() else 0
+            # the largest finite count in one device reduction and one transfer (-inf: none finite)
+            top = float(torch.where(torch.isfinite(need), need, float("-inf")).max())
+            top = top + 64 if top != float("-inf") else 0
         longest = int(min(top, _native.ODE_MAX_LAUNCHES * per))
         max_steps = longest if max_steps is None else min(int(max_steps), longest)
         order = wave_order(d_pts_all, d_ode_all, n) if group_waves else None
@@ -658,10 +659,11 @@ def wave_order(d_pts: torch.Tensor, d_ode: torch.Tensor, n: int):
     h = (h * _MIX) ^ o32[:, _native.ODE_DTYPE.fields["deplete_DM_from_source"][1] // 4].to(torch.int64)
     o64 = d_ode.view(n, _native.ODE_DTYPE.itemsize).view(torch.int64)
     h = (h * _MIX) ^ o64[:, _native.ODE_DTYPE.fields["Gamma_wash_over_H"][1] // 8]
-    breaks = int((h[1:] != h[:-1]).sum())
+    # the key's breaks in input order and its distinct values (from one sort), in one transfer
+    hs = torch.sort(h).values
+    breaks, distinct = torch.stack([(h[1:] != h[:-1]).sum(), 1 + (hs[1:] != hs[:-1]).sum()]).tolist()
     if breaks == 0:
         return None
-    distinct = int(torch.unique(h).numel())
     if distinct == n or breaks <= 2 * (distinct - 1):
         return None
     ht = mix(torch.zeros(n, dtype=torch.int64, device=d_pts.device), ("I_p", "v_w"))

@@ -467,6 +467,11 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
       if (LZQ_ODE_RICVAR && !kChiOnly && G == 64 && (!tab_vary || LZQ_ODE_RICTAB) && rec_shared &&
           __all(k_split != -1))
         return;
+      // and split-free waves of narrower uniform segments, one table and one Gamma_wash each:
+      // ode_riccati_kernel<0, false, true> (LZQ_ODE_RICSEG)
+      if (LZQ_ODE_RICVAR && LZQ_ODE_RICSEG && kNoSplit && !kChiOnly && G > 0 && G < 64 && !tab_vary && rec_shared &&
+          __all(k_split != -1))
+        return;
     }
     const int64_t block = coop ? G : N;
     for (int64_t kb = k_begin; kb < k_stop; kb += block) {
@@ -952,8 +957,8 @@ __device__ __forceinline__ bool ric_step_ip(double h, const double (&hA2)[3], co
 // split-step code, each lane forming its own stages: two steps, so registers do not matter),
 // 2: the regular steps after it -- with its state handed on in OdeState; so the regular-step
 // kernels (0, 2) carry no split code.  A wave with no split in range runs in pass 0 alone.
-template <int kPhase, bool kTab = false>
-__global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : (kTab ? LZQ_RIC_TAB_MIN_WAVES : LZQ_RIC_MIN_WAVES)) void
+template <int kPhase, bool kTab = false, bool kSeg = false>
+__global__ __launch_bounds__(kOdeBlock, kPhase == 1 ? 1 : (kTab || kSeg ? LZQ_RIC_TAB_MIN_WAVES : LZQ_RIC_MIN_WAVES)) void
 ode_riccati_kernel(const lzq_point* __restrict__ pts, const lzq_ode_params* __restrict__ ode, int64_t n,
                    const int32_t* __restrict__ tidx, const double* __restrict__ ws, int64_t max_steps,
                    lzq_yield* __restrict__ out, int32_t* __restrict__ status, int coop_on, int64_t k_lo, int64_t k_cnt,
@@ -961,10 +966,12 @@ ode_riccati_kernel(const lzq_point* __restrict__ pts, const lzq_ode_params* __re
   __shared__ RicRow s_row[kOdeBlock / 64][kTab ? 1 : 64];
   __shared__ YbCD s_rcd[kOdeBlock / 64][kTab ? 1 : 64];
   __shared__ RicRowT s_rowt[kOdeBlock / 64][kTab ? 64 : 1];
-  __shared__ OdePoint s_pt[kOdeBlock / 64];
+  __shared__ OdePoint s_pt[kOdeBlock / 64][kSeg ? 64 / LZQ_ODE_MIN_GROUP : 1];  // kSeg: one per segment
   __shared__ double s_beta[kOdeBlock / 64][64][3];  // the fill's beta_j (Gamma_wash * base)
+  static_assert(!kSeg || (kPhase == 0 && !kTab), "segment waves run pass 0 only, on one table per segment");
 
   if (!LZQ_ODE_RICVAR || !LZQ_ODE_COOP || !coop_on) return;
+  if (kSeg && !LZQ_ODE_RICSEG) return;
   // --- the classification of ode_integrate_kernel<false, false, true>, on the same values ---
   const int64_t wave0 = (int64_t)blockIdx.x * kOdeBlock + (threadIdx.x & ~63);
   if (wave0 >= n) return;
@@ -987,10 +994,21 @@ ode_riccati_kernel(const lzq_point* __restrict__ pts, const lzq_ode_params* __re
   const double steps = ceil(fabs(x1 - x0) / max_step);
   if (!(steps <= (double)max_steps)) return;
   if (__ballot(1) != ~0ull) return;  // a lane returned above: not a whole cooperative wave
-  auto same = [](double v) { return __builtin_bit_cast(uint64_t, v) == __builtin_bit_cast(uint64_t, __shfl(v, 0, 64)); };
-  const bool eq = same(o.m) && same(o.Tp) && same(o.B) && same(o.sig) && same(o.H0) && same(o.s0) && same(o.c_rel) &&
-                  same(o.c_nr) && same(o.v0) && same(o.T_lo) && same(o.T_hi);
-  if (!__all(eq)) return;                                                    // G < 64
+  // G: the widest aligned segments (64, 32, 16, 8 lanes) that are each uniform in the stage key --
+  // ode_integrate_kernel's cooperative width, found the same way; this kernel takes G = 64 (kSeg
+  // false) or 8 <= G < 64 (kSeg), on one table and one Gamma_wash per segment
+  int G = 0;
+  for (int g = 64; g >= LZQ_ODE_MIN_GROUP && G == 0; g >>= 1) {
+    auto same_g = [g](double v) {
+      return __builtin_bit_cast(uint64_t, v) == __builtin_bit_cast(uint64_t, __shfl(v, 0, g));
+    };
+    const bool eq = same_g(o.m) && same_g(o.Tp) && same_g(o.B) && same_g(o.sig) && same_g(o.H0) && same_g(o.s0) &&
+                    same_g(o.c_rel) && same_g(o.c_nr) && same_g(o.v0) && same_g(o.T_lo) && same_g(o.T_hi);
+    if (__all(eq)) G = g;
+    if (!kSeg) break;  // only G = 64 is this variant's
+  }
+  if (kSeg ? !(G > 0 && G < 64) : G != 64) return;
+  auto same = [G](double v) { return __builtin_bit_cast(uint64_t, v) == __builtin_bit_cast(uint64_t, __shfl(v, 0, G)); };
   if (__all(same(__builtin_bit_cast(double, w))) == kTab) return;            // tab_vary: the kTab kernel's
   if (kTab && !LZQ_ODE_RICTAB) return;
   if (!__all(same(o.gamma_w))) return;                                       // !rec_shared
@@ -1020,6 +1038,10 @@ ode_riccati_kernel(const lzq_point* __restrict__ pts, const lzq_ode_params* __re
     }
   }
   if (!__all(k_split != -1)) return;  // x rounding comparable to h: the general variant's every-step test
+  if (kSeg) {  // no lane's split step in this launch's range (ode_integrate_kernel's lane_ns, all lanes)
+    const bool lane_ns = k_split == INT64_MAX || (k_split + 1 < k_begin || k_split >= k_stop);
+    if (!__all(lane_ns)) return;
+  }
   // the split step (xk < xb <= xk + h) of this wave: k_split, and k_split + 1 when a rounding splits
   // that one too (wave-uniform: x0, h and xb are); every other step is a regular one
   const int64_t ks = (int64_t)__builtin_bit_cast(uint64_t, ode_uniform(__builtin_bit_cast(double, k_split)));
@@ -1028,25 +1050,28 @@ ode_riccati_kernel(const lzq_point* __restrict__ pts, const lzq_ode_params* __re
   const bool in_range = ks != INT64_MAX && !(ks + 1 < k_begin || ks >= k_stop);
   if (kPhase > 0 && !in_range) return;
   const int64_t ks_lo = ks > k_begin ? ks : k_begin, ks_hi = ks + 2 < k_stop ? ks + 2 : k_stop;
-  const int64_t pk_begin = kPhase == 0 ? k_begin : (kPhase == 1 ? ks_lo : ks_hi);
-  const int64_t pk_stop = kPhase == 0 ? (in_range ? ks_lo : k_stop) : (kPhase == 1 ? ks_hi : k_stop);
+  const int64_t pk_begin = kSeg ? k_begin : kPhase == 0 ? k_begin : (kPhase == 1 ? ks_lo : ks_hi);
+  const int64_t pk_stop = kSeg ? k_stop : kPhase == 0 ? (in_range ? ks_lo : k_stop) : (kPhase == 1 ? ks_hi : k_stop);
   // --- this wave is ours: the wave-uniform point constants in the wave's LDS slot (read by the
   // fill phase only), the window, h, hA and the table pointer in SGPRs ---
+  // (kSeg: per segment -- the segment's point in its LDS slot; the window, h, hA and the table each
+  // lane's own, which equal its segment leader's bit for bit, in VGPRs)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (lane == 0) s_pt[wv] = o;
+  const int seg = kSeg ? (lane & ~(G - 1)) : 0;  // the segment's first lane: its rows are seg .. seg + G - 1
+  if (lane == seg) s_pt[wv][kSeg ? seg / G : 0] = o;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const OdePoint& ou = s_pt[wv];
-  const double* wu = reinterpret_cast<const double*>(
+  const OdePoint& ou = s_pt[wv][kSeg ? seg / G : 0];
+  const double* wu = kSeg ? w : reinterpret_cast<const double*>(
       (uintptr_t)__builtin_bit_cast(uint64_t, ode_uniform(__builtin_bit_cast(double, (uint64_t)(uintptr_t)w))));
-  const double x0u = ode_uniform(x0), hu = ode_uniform(h);
+  const double x0u = kSeg ? x0 : ode_uniform(x0), hu = kSeg ? h : ode_uniform(h);
   const Radau R = radau_tableau();
   RadauH hA = radau_h(R, hu);
 #pragma unroll
   for (int a = 0; a < 3; ++a)
 #pragma unroll
-    for (int b = 0; b < 3; ++b) hA.a[a][b] = ode_uniform(hA.a[a][b]);
+    for (int b = 0; b < 3; ++b) hA.a[a][b] = kSeg ? hA.a[a][b] : ode_uniform(hA.a[a][b]);
   // --- per-lane state (ode_integrate_kernel's) ---
   const double Pf = o.Pf, sigmav = o.sigmav;
   const int deplete = o.deplete;
@@ -1141,11 +1166,14 @@ ode_riccati_kernel(const lzq_point* __restrict__ pts, const lzq_ode_params* __re
   }
   int kc = -1;                             // kTab: the spline interval held in cc
   double cc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int64_t kb = pk_begin; kPhase != 1 && kb < pk_stop; kb += 64) {
-    const int64_t kend = kb + 64 < pk_stop ? kb + 64 : pk_stop;
+  // (kSeg: blocks of G steps; k_begin, hence kb, is the same on every lane, each segment's range
+  // ends at its own pk_stop -- a segment past it takes no steps while the others run on)
+  const int64_t blk = kSeg ? (int64_t)G : 64;
+  for (int64_t kb = pk_begin; kPhase != 1 && (kSeg ? __any(kb < pk_stop) : kb < pk_stop); kb += blk) {
+    const int64_t kend = kb + blk < pk_stop ? kb + blk : pk_stop;
     uint64_t xok = 0;
     {  // lane l: the stage ingredients and Y_B step map of step kb + l (the cooperative fill)
-      const int64_t kl = kb + lane;
+      const int64_t kl = kb + (lane - seg);
       if (LZQ_RIC_LEAN) {
         // the steps' x guard (xk + h > xk, wave-uniform per step) as one mask, from the fill's xk
         const double xk = x0u + (double)kl * hu;
@@ -1153,9 +1181,9 @@ ode_riccati_kernel(const lzq_point* __restrict__ pts, const lzq_ode_params* __re
       }
       if (kl < kend) {
         if (kTab) {
-          ric_fill_tab(&s_pt[wv], wu, x0u + (double)kl * hu, hu, &s_rowt[wv][lane], s_beta[wv][lane]);
+          ric_fill_tab(&ou, wu, x0u + (double)kl * hu, hu, &s_rowt[wv][lane], s_beta[wv][lane]);
         } else if (LZQ_RIC_LEAN) {
-          ric_fill(&s_pt[wv], wu, x0u + (double)kl * hu, hu, &s_row[wv][lane], s_beta[wv][lane], &s_rcd[wv][lane]);
+          ric_fill(&ou, wu, x0u + (double)kl * hu, hu, &s_row[wv][lane], s_beta[wv][lane], &s_rcd[wv][lane]);
         } else {
         const double xk = x0u + (double)kl * hu;
         RicRow& row = s_row[wv][lane];
@@ -1194,17 +1222,18 @@ ode_riccati_kernel(const lzq_point* __restrict__ pts, const lzq_ode_params* __re
     constexpr bool kDep = decltype(dep_tag)::value;
     // LZQ_RIC_V4: a uniform trip count, each lane's steps under !done (a lane whose Newton iteration
     // failed stops there, as in the loop below)
-    const int nr = (int)(kend - kb);
-    if (LZQ_RIC_IP || kTab) {
+    const int nr = kend > kb ? (int)(kend - kb) : 0;  // kSeg: this segment's steps in the block
+    if (LZQ_RIC_IP || kTab || kSeg) {
       // the same steps with the loop-carried values written once each (ric_step_ip): the predictor
       // and block_guess fill g, the iterate lives in Zs, Y_B is committed only on success and the
       // status once after the loop (a lane done here failed here) -- the loop below copied Y_chi,
       // Y_B, the stages and the status between registers at every step's joins
       const bool done0 = done;
-      for (int r = 0; r < nr; ++r) {
-        const RicRow row = s_row[wv][kTab ? 0 : r];
-        const YbCD rc = s_rcd[wv][kTab ? 0 : r];
-        if (done) continue;
+      const int nr_loop = kSeg ? G : nr;  // a uniform trip count (kSeg: a segment past its nr skips)
+      for (int r = 0; r < nr_loop; ++r) {
+        const RicRow row = s_row[wv][kTab ? 0 : seg + r];
+        const YbCD rc = s_rcd[wv][kTab ? 0 : seg + r];
+        if (done || (kSeg && r >= nr)) continue;
         bool use_guess = false;
         double g[3] = {Zs[0], Zs[1], Zs[2]};  // Zs as it stands unless a guess replaces it
         // a lane that is not done has taken steps 0 .. r - 1 of this block, so have = have || r > 0
@@ -1221,7 +1250,7 @@ ode_riccati_kernel(const lzq_point* __restrict__ pts, const lzq_ode_params* __re
         const double Ystart = Ychi;
         if (LZQ_RIC_IP >= 2) Yp = Ystart;  // the predictor has read the previous one
         bool ok = true;
-        if ((xok >> r) & 1) {
+        if ((xok >> (seg + r)) & 1) {
           double lam[3], E2[3], S[3];
           double YBn;
           if constexpr (kTab) {
@@ -1689,6 +1718,13 @@ int launch_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int
           hipLaunchKernelGGL((lzq::ode_riccati_kernel<2, true>), dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0,
                              s, d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, lzq::g_ode_coop, k_lo,
                              k_cnt, st, d_skip);
+          rc = hip_check(hipGetLastError(), fn);
+        }
+        if (LZQ_ODE_RICSEG && n > 1) {  // uniform 32/16/8-lane segments (a one-point wave is one whole segment)
+          if (rc != LZQ_OK) return rc;
+          hipLaunchKernelGGL((lzq::ode_riccati_kernel<0, false, true>), dim3((unsigned)ode_blocks(n)),
+                             dim3(lzq::kOdeBlock), 0, s, d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status,
+                             lzq::g_ode_coop, k_lo, k_cnt, st, d_skip);
           rc = hip_check(hipGetLastError(), fn);
         }
       }

@@ -548,6 +548,48 @@ def test_ode_cooperative_subgroups_bit_identical(gpu_engine):
         assert torch_equal(a, c) and torch_equal(sa, sc), method
 
 
+def test_ode_riccati_segments_bit_identical(gpu_engine):
+    """Waves of uniform 16- and 8-lane segments (fewer points per stage key than a wave), each
+    segment on one table with one Gamma_wash and no T = m/3 split in its window:
+    ode_riccati_kernel<0, false, true> (LZQ_ODE_RICSEG) steps them, every segment with its own
+    window, N and step size.  The per-lane mode's bits, in one launch and as continuation launches,
+    and the C restatement's values."""
+    rng = np.random.default_rng(79)
+    cfgs = []
+    for block, n_keys in ((16, 8), (8, 16)):
+        for kk in range(n_keys):
+            m_chi = float(10 ** rng.uniform(-0.5, 0.3))   # T > m/3 over the whole window: no split
+            win = dict(T_max_over_Tp=float(rng.uniform(1.3, 1.8)), T_min_over_Tp=float(rng.uniform(0.5, 0.7)))
+            gw = float(rng.choice([0.5, 2.0]))
+            for _ in range(block):
+                c = full_cfg(BASE_CFG)
+                c.update(win, m_chi_GeV=m_chi, P_chi_to_B=float(rng.uniform(0.05, 1.0)), Gamma_wash_over_H=gw,
+                         sigma_v_chi_GeV_m2=float(rng.choice([1e-16, 1e-12])),
+                         deplete_DM_from_source=bool(rng.uniform() < 0.3),
+                         regime=str(rng.choice(["thermal", "nonthermal"])))
+                cfgs.append(c)
+    p, o = recs(cfgs)
+    a, sa = gpu_engine.ode(p, o, group_waves=False)
+    assert bool((sa == 0).all())
+    prev = gpu_engine.tune_ode_coop(False)
+    try:
+        b, sb = gpu_engine.ode(p, o, group_waves=False)
+    finally:
+        gpu_engine.tune_ode_coop(prev)
+    assert torch_equal(sa, sb) and torch_equal(a, b)
+    prev = gpu_engine.tune_ode_launch_steps(11)
+    try:
+        c, sc = gpu_engine.ode(p, o, group_waves=False)
+    finally:
+        gpu_engine.tune_ode_launch_steps(prev)
+    assert torch_equal(a, c) and torch_equal(sa, sc)
+    ref, sr = O.ode_batch(cfgs[::16], nthreads=16)
+    for row, rr, s2 in zip(a.cpu().numpy()[::16], ref, sr):
+        assert s2 == 0
+        for v, w in zip(row[:5], rr[:5]):
+            assert rel_err(v, w) < 1e-10, (v, w)
+
+
 def test_ode_cooperative_table_varying_bit_identical(gpu_engine):
     """Cooperative segments whose points differ in the A/V kernel (I_p, v_w: a spline table each):
     the shared stage rows carry a / Av and the spline location, each lane forms a from its own

@@ -467,9 +467,9 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
       if (LZQ_ODE_RICVAR && !kChiOnly && G == 64 && (!tab_vary || LZQ_ODE_RICTAB) && rec_shared &&
           __all(k_split != -1))
         return;
-      // and split-free waves of narrower uniform segments, one table and one Gamma_wash each:
-      // ode_riccati_kernel<0, false, true> (LZQ_ODE_RICSEG)
-      if (LZQ_ODE_RICVAR && LZQ_ODE_RICSEG && kNoSplit && !kChiOnly && G > 0 && G < 64 && !tab_vary && rec_shared &&
+      // and waves of narrower uniform segments, one table and one Gamma_wash each:
+      // ode_riccati_kernel<., false, true> (LZQ_ODE_RICSEG)
+      if (LZQ_ODE_RICVAR && LZQ_ODE_RICSEG && !kChiOnly && G > 0 && G < 64 && !tab_vary && rec_shared &&
           __all(k_split != -1))
         return;
     }
@@ -968,7 +968,7 @@ ode_riccati_kernel(const lzq_point* __restrict__ pts, const lzq_ode_params* __re
   __shared__ RicRowT s_rowt[kOdeBlock / 64][kTab ? 64 : 1];
   __shared__ OdePoint s_pt[kOdeBlock / 64][kSeg ? 64 / LZQ_ODE_MIN_GROUP : 1];  // kSeg: one per segment
   __shared__ double s_beta[kOdeBlock / 64][64][3];  // the fill's beta_j (Gamma_wash * base)
-  static_assert(!kSeg || (kPhase == 0 && !kTab), "segment waves run pass 0 only, on one table per segment");
+  static_assert(!kSeg || !kTab, "segment waves: one table per segment");
 
   if (!LZQ_ODE_RICVAR || !LZQ_ODE_COOP || !coop_on) return;
   if (kSeg && !LZQ_ODE_RICSEG) return;
@@ -1038,20 +1038,18 @@ ode_riccati_kernel(const lzq_point* __restrict__ pts, const lzq_ode_params* __re
     }
   }
   if (!__all(k_split != -1)) return;  // x rounding comparable to h: the general variant's every-step test
-  if (kSeg) {  // no lane's split step in this launch's range (ode_integrate_kernel's lane_ns, all lanes)
-    const bool lane_ns = k_split == INT64_MAX || (k_split + 1 < k_begin || k_split >= k_stop);
-    if (!__all(lane_ns)) return;
-  }
   // the split step (xk < xb <= xk + h) of this wave: k_split, and k_split + 1 when a rounding splits
   // that one too (wave-uniform: x0, h and xb are); every other step is a regular one
-  const int64_t ks = (int64_t)__builtin_bit_cast(uint64_t, ode_uniform(__builtin_bit_cast(double, k_split)));
-  const double xbu = ode_uniform(xb), xb_below = nextafter(xbu, -INFINITY);
+  // (kSeg: the segment's own, per lane; so are the passes' ranges below, and a segment with no split
+  // step in range leaves passes 1 and 2 at once)
+  const int64_t ks = kSeg ? k_split : (int64_t)__builtin_bit_cast(uint64_t, ode_uniform(__builtin_bit_cast(double, k_split)));
+  const double xbu = kSeg ? xb : ode_uniform(xb), xb_below = nextafter(xbu, -INFINITY);
   // this pass's steps [pk_begin, pk_stop)
   const bool in_range = ks != INT64_MAX && !(ks + 1 < k_begin || ks >= k_stop);
   if (kPhase > 0 && !in_range) return;
   const int64_t ks_lo = ks > k_begin ? ks : k_begin, ks_hi = ks + 2 < k_stop ? ks + 2 : k_stop;
-  const int64_t pk_begin = kSeg ? k_begin : kPhase == 0 ? k_begin : (kPhase == 1 ? ks_lo : ks_hi);
-  const int64_t pk_stop = kSeg ? k_stop : kPhase == 0 ? (in_range ? ks_lo : k_stop) : (kPhase == 1 ? ks_hi : k_stop);
+  const int64_t pk_begin = kPhase == 0 ? k_begin : (kPhase == 1 ? ks_lo : ks_hi);
+  const int64_t pk_stop = kPhase == 0 ? (in_range ? ks_lo : k_stop) : (kPhase == 1 ? ks_hi : k_stop);
   // --- this wave is ours: the wave-uniform point constants in the wave's LDS slot (read by the
   // fill phase only), the window, h, hA and the table pointer in SGPRs ---
   // (kSeg: per segment -- the segment's point in its LDS slot; the window, h, hA and the table each
@@ -1723,6 +1721,16 @@ int launch_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int
         if (LZQ_ODE_RICSEG && n > 1) {  // uniform 32/16/8-lane segments (a one-point wave is one whole segment)
           if (rc != LZQ_OK) return rc;
           hipLaunchKernelGGL((lzq::ode_riccati_kernel<0, false, true>), dim3((unsigned)ode_blocks(n)),
+                             dim3(lzq::kOdeBlock), 0, s, d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status,
+                             lzq::g_ode_coop, k_lo, k_cnt, st, d_skip);
+          rc = hip_check(hipGetLastError(), fn);
+          if (rc != LZQ_OK) return rc;
+          hipLaunchKernelGGL((lzq::ode_riccati_kernel<1, false, true>), dim3((unsigned)ode_blocks(n)),
+                             dim3(lzq::kOdeBlock), 0, s, d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status,
+                             lzq::g_ode_coop, k_lo, k_cnt, st, d_skip);
+          rc = hip_check(hipGetLastError(), fn);
+          if (rc != LZQ_OK) return rc;
+          hipLaunchKernelGGL((lzq::ode_riccati_kernel<2, false, true>), dim3((unsigned)ode_blocks(n)),
                              dim3(lzq::kOdeBlock), 0, s, d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status,
                              lzq::g_ode_coop, k_lo, k_cnt, st, d_skip);
           rc = hip_check(hipGetLastError(), fn);

@@ -550,16 +550,21 @@ def test_ode_cooperative_subgroups_bit_identical(gpu_engine):
 
 def test_ode_riccati_segments_bit_identical(gpu_engine):
     """Waves of uniform 16- and 8-lane segments (fewer points per stage key than a wave), each
-    segment on one table with one Gamma_wash and no T = m/3 split in its window:
-    ode_riccati_kernel<0, false, true> (LZQ_ODE_RICSEG) steps them, every segment with its own
-    window, N and step size.  The per-lane mode's bits, in one launch and as continuation launches,
-    and the C restatement's values."""
+    segment on one table with one Gamma_wash: ode_riccati_kernel<., false, true> (LZQ_ODE_RICSEG)
+    steps them, every segment with its own window, N and step size -- without a T = m/3 split in
+    the window (pass 0 alone) and with one (m_chi ~ 40 on the narrow window: the three passes, each
+    segment's split at its own step).  The per-lane mode's bits, in one launch and as continuation
+    launches, and the C restatement's values."""
     rng = np.random.default_rng(79)
     cfgs = []
-    for block, n_keys in ((16, 8), (8, 16)):
+    for block, n_keys, split in ((16, 8, False), (8, 16, False), (16, 4, True), (8, 8, True)):
         for kk in range(n_keys):
-            m_chi = float(10 ** rng.uniform(-0.5, 0.3))   # T > m/3 over the whole window: no split
-            win = dict(T_max_over_Tp=float(rng.uniform(1.3, 1.8)), T_min_over_Tp=float(rng.uniform(0.5, 0.7)))
+            if split:
+                m_chi = 40.0 + 0.5 * kk
+                win = dict(NARROW)
+            else:
+                m_chi = float(10 ** rng.uniform(-0.5, 0.3))   # T > m/3 over the whole window: no split
+                win = dict(T_max_over_Tp=float(rng.uniform(1.3, 1.8)), T_min_over_Tp=float(rng.uniform(0.5, 0.7)))
             gw = float(rng.choice([0.5, 2.0]))
             for _ in range(block):
                 c = full_cfg(BASE_CFG)

@@ -46,6 +46,8 @@ def main():
         cases["riccati_gw_perlane"] = dict(cases["riccati_gw"])
         # 16 points per m_chi (16 sigma_v each): 16-lane cooperative segments, the general variant
         cases["riccati_g16"] = {"T_max_over_Tp": 1.6, "T_min_over_Tp": 0.6}
+        # the stiff thermal window (T = m/3 crossed: a split step per segment) with 16 points per m_chi
+        cases["stiff_g16"] = {"regime": "thermal", "T_max_over_Tp": 1.3, "T_min_over_Tp": 0.2}
     out = {}
     for cname, over in cases.items():
         cfgs = cfgs_for(over, n)
@@ -61,6 +63,10 @@ def main():
             for i, c in enumerate(cfgs):
                 c["m_chi_GeV"] = 0.5 + 0.001 * (i // 16)
                 c["sigma_v_chi_GeV_m2"] = 10.0 ** (-20 + (i % 16) * 0.6)
+        if cname == "stiff_g16":
+            for i, c in enumerate(cfgs):
+                c["m_chi_GeV"] = 300.0 + 0.01 * (i // 16)
+                c["sigma_v_chi_GeV_m2"] = 10.0 ** (-10 + (i % 16) * 0.1)
         if cname.startswith("riccati_gw"):
             for i, c in enumerate(cfgs):
                 c["Gamma_wash_over_H"] = (0.1, 0.5, 2.0, 8.0)[i % 4]

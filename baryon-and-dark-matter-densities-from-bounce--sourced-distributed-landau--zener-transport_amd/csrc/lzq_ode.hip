@@ -982,9 +982,19 @@ ode_riccati_kernel(const lzq_point* __restrict__ pts, const lzq_ode_params* __re
   const bool cont = state != nullptr, first = kPhase == 0 && (!cont || k_lo == 0);
   if (kPhase > 0 && !cont) return;  // passes 1 and 2 continue from pass 0's state
   if (cont && !first && state[i].status != kOdeInProgress) return;
+  const double* w = ws + (tidx ? (int64_t)tidx[i] : i) * (int64_t)kOdeWS;
+  // Two of the wave-uniform exits below, taken first (before the point's constants, ~40 us per
+  // 2.6e5 points in each of this kernel's launches): a linear wave (sigma_v = 0 on every lane:
+  // ode_integrate_kernel<kLin>'s) and, for whole waves, one of the other table class.  Evaluated on
+  // the lanes still here; with one missing the ballot below returns anyway, so neither exits a wave
+  // this kernel would step.
+  if (LZQ_ODE_LINFAST && __all(pymax(ode[i].sigma_v_chi_GeV_m2, 0.0) == 0.0)) return;
+  if (!kSeg) {
+    const uint64_t wb = (uint64_t)(uintptr_t)w;
+    if (__all(wb == __builtin_bit_cast(uint64_t, __shfl(__builtin_bit_cast(double, wb), 0, 64))) == kTab) return;
+  }
   const lzq_point pt = pts[i];
   const OdePoint o = ode_point(pt, ode[i]);
-  const double* w = ws + (tidx ? (int64_t)tidx[i] : i) * (int64_t)kOdeWS;
   if (!ode_grid_ok(o.T_lo, o.T_hi, o.stepT) || !ode_table_ok(w)) return;  // the general variant reports it
   const double m = o.m, T_p = o.Tp;
   const double x0 = m / o.T_hi, x1 = m / pymax(o.T_lo, 1e-30);

@@ -595,6 +595,34 @@ def test_ode_riccati_segments_bit_identical(gpu_engine):
             assert rel_err(v, w) < 1e-10, (v, w)
 
 
+def test_ode_partial_wave_of_segments(gpu_engine):
+    """A batch of 40 points in five 8-point stage keys: one partial wavefront whose lanes past the
+    batch clone its first point, so it splits into uniform 8-lane segments (the clones one more
+    segment of the first key) -- the segment Riccati kernel's wave.  Every point equals the
+    per-lane mode's and its own single-point run, bit for bit."""
+    rng = np.random.default_rng(83)
+    cfgs = []
+    for kk in range(5):
+        m_chi = float(10 ** rng.uniform(-0.5, 0.3))
+        for _ in range(8):
+            c = full_cfg(BASE_CFG)
+            c.update(NARROW, m_chi_GeV=m_chi, P_chi_to_B=float(rng.uniform(0.05, 1.0)), Gamma_wash_over_H=0.5,
+                     sigma_v_chi_GeV_m2=float(rng.choice([1e-16, 1e-12])))
+            cfgs.append(c)
+    p, o = recs(cfgs)
+    a, sa = gpu_engine.ode(p, o, group_waves=False)
+    assert bool((sa == 0).all())
+    prev = gpu_engine.tune_ode_coop(False)
+    try:
+        b, sb = gpu_engine.ode(p, o, group_waves=False)
+    finally:
+        gpu_engine.tune_ode_coop(prev)
+    assert torch_equal(sa, sb) and torch_equal(a, b)
+    for j in (0, 13, 39):
+        one, s1 = gpu_engine.ode(p[j:j + 1], o[j:j + 1], time_parallel=False)
+        assert torch_equal(one[0], a[j]) and torch_equal(s1[0], sa[j])
+
+
 def test_ode_cooperative_table_varying_bit_identical(gpu_engine):
     """Cooperative segments whose points differ in the A/V kernel (I_p, v_w: a spline table each):
     the shared stage rows carry a / Av and the spline location, each lane forms a from its own

@@ -123,7 +123,7 @@ EXPORTS = ("lzq_abi_version", "lzq_last_error", "lzq_init", "lzq_zgrid_init", "l
            "lzq_jchi_batch", "lzq_yields_batch", "lzq_sweep_grid", "lzq_sweep_grid_reuse_workspace",
            "lzq_sweep_grid_reuse", "lzq_sweep_grid_ztables", "lzq_sweep_grid_from_ztables",
            "lzq_yields_batch_reuse", "lzq_p_closed_form",
-           "lzq_lz_propagate", "lzq_lz_propagate_v", "lzq_ode_tables", "lzq_ode_integrate", "lzq_ode_integrate_shared", "lzq_ode_integrate_tp", "lzq_ode_quadrature", "lzq_ode_batch",
+           "lzq_lz_propagate", "lzq_lz_propagate_v", "lzq_ode_tables", "lzq_ode_integrate", "lzq_ode_integrate_shared", "lzq_ode_rows", "lzq_ode_integrate_rows", "lzq_ode_integrate_tp", "lzq_ode_quadrature", "lzq_ode_batch",
            "lzq_ode_aov_T", "lzq_ode_rhs", "lzq_profile_splines", "lzq_profile_crossings",
            "lzq_lz_propagate_profile")
 # the lzq_point fields an ODE spline table depends on (A/V kernel fpy:141-156 + window fpy:368-369)
@@ -187,6 +187,8 @@ def load(path: str | None = None):
     L.lzq_ode_tables.argtypes = [vp, i64, vp, vp, i32, i32, d, vp, vp, i64, vp, vp]
     L.lzq_ode_integrate.argtypes = [vp, vp, i64, vp, i64, i64, vp, vp, vp]
     L.lzq_ode_integrate_shared.argtypes = [vp, vp, i64, vp, i64, vp, i64, i64, vp, vp, vp]
+    L.lzq_ode_rows.argtypes = [vp, vp, i64, vp, i64, vp, i64, vp, vp, i64, i64, vp, i64, vp]
+    L.lzq_ode_integrate_rows.argtypes = [vp, vp, i64, vp, i64, vp, i64, i64, vp, vp, vp, i64, vp, i64, vp, vp, vp]
     L.lzq_ode_integrate_tp.argtypes = [vp, vp, i64, vp, i64, vp, i64, i64, vp, vp, vp, vp]
     L.lzq_ode_quadrature.argtypes = [vp, vp, i64, vp, i64, vp, i64, i64, vp, vp, vp]
     L.lzq_ode_batch.argtypes = [vp, vp, i64, i32, d, vp, vp, i64, i64, vp, vp, vp]

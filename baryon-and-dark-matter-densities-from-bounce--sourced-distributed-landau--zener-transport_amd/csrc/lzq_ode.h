@@ -600,6 +600,9 @@ __device__ __forceinline__ double fma_neg_s(double k, double a, double p) {
 #ifndef LZQ_ODE_RICSEG
 #define LZQ_ODE_RICSEG 1  // split-free waves of uniform 32/16/8-lane segments through ode_riccati_kernel<0, false, true>
 #endif
+#ifndef LZQ_ODE_ROWS
+#define LZQ_ODE_ROWS 1  // linear waves read their run's shared row table when given one (lzq_ode_integrate_rows)
+#endif
 #ifndef LZQ_ODE_PRED_BLOCK
 // The Radau5 predictor is not used on steps k = 0 (mod LZQ_ODE_PRED_BLOCK): every block of that
 // many steps starts its Newton iteration from Y_chi, so a block's end state is a function of its

@@ -276,6 +276,20 @@ template <bool kDep>
 __device__ bool ric_step(double h, const double (&hA2)[3], const double (&lam)[3], const double (&E2)[3],
                          const double (&S)[3], const double (&pv)[6], double& Ychi, double (&Zs)[3], bool guess);
 
+// Shared stage-row tables (round 6, lzq_ode_rows): Y_B's step maps (c, d) of every step of a
+// run -- points of the launch order equal in the cooperative fields, spline table and Gamma_wash
+// (engine.ode_runs) -- computed once per run by ode_rows_kernel instead of once per wavefront by
+// the cooperative fill.  ode_integrate_kernel<kLin> reads a run's rows for a wave only after
+// checking that the wave is that one run and that the run's representative point agrees with
+// every lane in all the fill reads (the cooperative fields, table, Gamma_wash, step count).
+struct OdeRows {
+  const int32_t* run_of;   // [n] each point's run, -1: none
+  const int64_t* run_rep;  // [n_runs] a point of each run
+  const int64_t* row_off;  // [n_runs + 1] the first row of each run (run r: row_off[r+1] - row_off[r] rows)
+  const YbCD* rows;        // nullptr: no row tables (every wave fills its own rows)
+  int64_t n_runs, cap;     // runs; rows the buffer holds
+};
+
 template <bool kChiOnly, bool kLin = false, bool kNoSplit = false>
 __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_kernel(const lzq_point* __restrict__ pts,
                                                                   const lzq_ode_params* __restrict__ ode, int64_t n,
@@ -285,7 +299,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
                                                                   int32_t* __restrict__ status, int coop_on,
                                                                   int64_t k_lo, int64_t k_cnt,
                                                                   OdeState* __restrict__ state,
-                                                                  const int32_t* __restrict__ skip) {
+                                                                  const int32_t* __restrict__ skip, OdeRows rws) {
   __shared__ StageBase s_base[kOdeBlock / 64][64][3];  // cooperative mode
   // shared Y_B step maps, (c, d) and the cofactor weights in separate arrays: the linear waves'
   // tight loop streams 16-B (c, d) rows
@@ -473,10 +487,40 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
           __all(k_split != -1))
         return;
     }
+    // Row tables (OdeRows): a whole linear wave of one run, no depletion (its rows would need the
+    // stage a_j too), whose run's representative agrees with every lane in the fill's inputs --
+    // the cooperative fields, table and Gamma_wash, bit for bit, and the step count -- reads the
+    // run's rows instead of filling its own (the same values: ode_rows_kernel's operations are the
+    // fill's).  Regular steps off the tight loop (after a split) then form their stages per lane.
+    const YbCD* rrow = nullptr;
+    if (kLin && LZQ_ODE_ROWS && rws.rows && G == 64) {
+      const int32_t ru = rws.run_of[i];
+      if (__all(ru >= 0 && (int64_t)ru < rws.n_runs && ru == __shfl(ru, 0, 64) && !o.deplete)) {
+        const int64_t rep = rws.run_rep[ru], r0 = rws.row_off[ru], r1 = rws.row_off[ru + 1];
+        bool ok = rep >= 0 && rep < n && r0 >= 0 && r1 - r0 == N && r1 <= rws.cap;
+        if (__all(ok)) {
+          const OdePoint q = ode_point(pts[rep], ode[rep]);
+          auto eqb = [](double a, double b) {
+            return __builtin_bit_cast(uint64_t, a) == __builtin_bit_cast(uint64_t, b);
+          };
+          ok = eqb(q.m, o.m) && eqb(q.Tp, o.Tp) && eqb(q.B, o.B) && eqb(q.sig, o.sig) && eqb(q.H0, o.H0) &&
+               eqb(q.s0, o.s0) && eqb(q.c_rel, o.c_rel) && eqb(q.c_nr, o.c_nr) && eqb(q.v0, o.v0) &&
+               eqb(q.T_lo, o.T_lo) && eqb(q.T_hi, o.T_hi) && eqb(q.gamma_w, o.gamma_w) &&
+               (tidx ? tidx[rep] == tidx[i] : rep == i);
+          if (__all(ok)) rrow = rws.rows + r0;
+        }
+      }
+    }
     const int64_t block = coop ? G : N;
     for (int64_t kb = k_begin; kb < k_stop; kb += block) {
       const int64_t kend = kb + block < k_stop ? kb + block : k_stop;
-      if (coop) {
+      if (kLin && LZQ_ODE_ROWS && rrow) {
+        const int64_t kl = kb + lane;
+        if (kl < kend) s_rcd[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][lane] = rrow[kl];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      } else if (coop) {
         const int64_t kl = kb + (lane - seg);
         if (kl < kend) {
           const double xk = x0 + (double)kl * h;
@@ -590,7 +634,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
         if (xa > xk) {
           const double hs = split ? xa - xk : h;
           OdeStage sg[3];
-          if (coop && !split) {
+          if (coop && !split && !(kLin && LZQ_ODE_ROWS && rrow)) {  // (row tables: no stage bases in LDS)
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
               StageBase b = s_base[wv][seg + (k - kb)][j];
@@ -694,6 +738,41 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
   if (!real) return;
   out[i] = r;
   if (status) status[i] = st;
+}
+
+// Row r of run q (lzq_ode_rows): Y_B's step map of step r of the run's representative point, with
+// the cooperative fill's operations (ode_integrate_kernel above: x_k, the stage bases, beta_j =
+// Gamma_wash * base, yb_rec with the step's hA; h from the run's step count as the integrator
+// forms it).  One lane per row; runs over blockIdx.y, grid-strided.
+__global__ __launch_bounds__(kOdeBlock) void ode_rows_kernel(const lzq_point* __restrict__ pts,
+                                                             const lzq_ode_params* __restrict__ ode, int64_t n,
+                                                             const int32_t* __restrict__ tidx,
+                                                             const double* __restrict__ ws,
+                                                             const int64_t* __restrict__ run_rep,
+                                                             const int64_t* __restrict__ row_off, int64_t n_runs,
+                                                             YbCD* __restrict__ rows, int64_t cap) {
+  const int64_t k = (int64_t)blockIdx.x * kOdeBlock + threadIdx.x;
+  for (int64_t q = blockIdx.y; q < n_runs; q += gridDim.y) {
+    const int64_t r0 = row_off[q], N = row_off[q + 1] - r0, i = run_rep[q];
+    if (k >= N || i < 0 || i >= n || r0 < 0 || r0 + k >= cap) continue;
+    const OdePoint o = ode_point(pts[i], ode[i]);
+    const double* w = ws + (tidx ? (int64_t)tidx[i] : i) * (int64_t)kOdeWS;
+    const double m = o.m;
+    const double x0 = m / o.T_hi, x1 = m / pymax(o.T_lo, 1e-30);
+    const double h = (x1 - x0) / (double)N;
+    const Radau R = radau_tableau();
+    const RadauH hA = radau_h(R, h);
+    const double xk = x0 + (double)k * h;
+    double beta[3], a[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const StageBase b = ode_stage_base(o, w, xk + R.c[j] * h);
+      beta[j] = o.gamma_w * b.beta;
+      a[j] = b.a;
+    }
+    const YbRec yr = yb_rec(hA, beta, a);
+    rows[r0 + k] = {yr.c, yr.d};
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1672,8 +1751,9 @@ int hip_check(hipError_t e, const char* what);
 template <bool kChiOnly>
 int launch_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, const int32_t* d_tidx,
                      const double* d_work, int64_t max_steps, lzq_yield* d_out, int32_t* d_status, hipStream_t s,
-                     const char* fn, const int32_t* d_skip = nullptr) {
+                     const char* fn, const int32_t* d_skip = nullptr, const lzq::OdeRows* rows = nullptr) {
   const int64_t per = (int64_t)1 << lzq::g_ode_launch_log2;
+  const lzq::OdeRows rw = rows ? *rows : lzq::OdeRows{nullptr, nullptr, nullptr, nullptr, 0, 0};
   const int64_t launches = max_steps <= per ? 1 : (max_steps + per - 1) / per;
   if (launches > 65536) {
     char buf[160];
@@ -1686,13 +1766,13 @@ int launch_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int
   auto launch = [&](int64_t k_lo, int64_t k_cnt, lzq::OdeState* st) {
     hipLaunchKernelGGL(lzq::ode_integrate_kernel<kChiOnly>, dim3((unsigned)ode_blocks(n)), dim3(lzq::kOdeBlock), 0, s,
                        d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status, lzq::g_ode_coop, k_lo, k_cnt,
-                       st, d_skip);
+                       st, d_skip, rw);
     int rc = hip_check(hipGetLastError(), fn);
     if constexpr (LZQ_ODE_NOSPLITVAR) {
       if (rc != LZQ_OK) return rc;
       hipLaunchKernelGGL((lzq::ode_integrate_kernel<kChiOnly, false, true>), dim3((unsigned)ode_blocks(n)),
                          dim3(lzq::kOdeBlock), 0, s, d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status,
-                         lzq::g_ode_coop, k_lo, k_cnt, st, d_skip);
+                         lzq::g_ode_coop, k_lo, k_cnt, st, d_skip, rw);
       rc = hip_check(hipGetLastError(), fn);
       if constexpr (LZQ_ODE_RICVAR && !kChiOnly) {  // the three passes (ode_riccati_kernel)
         if (rc != LZQ_OK) return rc;
@@ -1751,7 +1831,7 @@ int launch_integrate(const lzq_point* d_points, const lzq_ode_params* d_ode, int
       if (rc != LZQ_OK) return rc;
       hipLaunchKernelGGL((lzq::ode_integrate_kernel<kChiOnly, true>), dim3((unsigned)ode_blocks(n)),
                          dim3(lzq::kOdeBlock), 0, s, d_points, d_ode, n, d_tidx, d_work, max_steps, d_out, d_status,
-                         lzq::g_ode_coop, k_lo, k_cnt, st, d_skip);
+                         lzq::g_ode_coop, k_lo, k_cnt, st, d_skip, rw);
       rc = hip_check(hipGetLastError(), fn);
     }
     return rc;
@@ -1857,6 +1937,47 @@ int lzq_ode_integrate_shared(const lzq_point* d_points, const lzq_ode_params* d_
   if (n == 0) return LZQ_OK;
   return launch_integrate<false>(d_points, d_ode, n, d_table_index, d_work, max_steps, d_out, d_status,
                                  (hipStream_t)stream, "lzq_ode_integrate_shared");
+}
+
+int lzq_ode_rows(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, const int32_t* d_table_index,
+                 int64_t n_tables, const double* d_work, int64_t work_doubles, const int64_t* d_run_rep,
+                 const int64_t* d_row_off, int64_t n_runs, int64_t max_run_rows, double* d_rows,
+                 int64_t rows_doubles, void* stream) {
+  if (n < 0 || n_tables < 0 || n_runs < 0 || max_run_rows < 0 || rows_doubles < 0 ||
+      (n_runs > 0 && (!d_points || !d_ode || !d_run_rep || !d_row_off || !d_rows || n == 0)) ||
+      (d_table_index && n > 0 && n_tables == 0))
+    return lzq_set_error(LZQ_EINVAL, "lzq_ode_rows: bad arguments");
+  int rc = check_ws(d_table_index ? n_tables : n, d_work, work_doubles, "lzq_ode_rows");
+  if (rc) return rc;
+  if (n_runs == 0 || max_run_rows == 0) return LZQ_OK;
+  const int64_t bx = (max_run_rows + lzq::kOdeBlock - 1) / lzq::kOdeBlock;
+  if (bx > 2147483647LL) return lzq_set_error(LZQ_EINVAL, "lzq_ode_rows: max_run_rows too large");
+  const unsigned by = (unsigned)(n_runs < 65535 ? n_runs : 65535);  // runs beyond: grid-strided
+  hipLaunchKernelGGL(lzq::ode_rows_kernel, dim3((unsigned)bx, by), dim3(lzq::kOdeBlock), 0, (hipStream_t)stream,
+                     d_points, d_ode, n, d_table_index, d_work, d_run_rep, d_row_off, n_runs, (lzq::YbCD*)d_rows,
+                     rows_doubles / 2);
+  return hip_check(hipGetLastError(), "lzq_ode_rows");
+}
+
+int lzq_ode_integrate_rows(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n,
+                           const int32_t* d_table_index, int64_t n_tables, const double* d_work,
+                           int64_t work_doubles, int64_t max_steps, const int32_t* d_run_of,
+                           const int64_t* d_run_rep, const int64_t* d_row_off, int64_t n_runs,
+                           const double* d_rows, int64_t rows_doubles, lzq_yield* d_out, int32_t* d_status,
+                           void* stream) {
+  if (n < 0 || n_tables < 0 || n_runs < 0 || rows_doubles < 0 ||
+      (n > 0 && (!d_points || !d_ode || !d_out || !d_table_index || n_tables == 0)) ||
+      (n_runs > 0 && (!d_run_of || !d_run_rep || !d_row_off || !d_rows)))
+    return lzq_set_error(LZQ_EINVAL, "lzq_ode_integrate_rows: bad arguments");
+  int rc = check_ws(n_tables, d_work, work_doubles, "lzq_ode_integrate_rows");
+  if (rc) return rc;
+  if (max_steps < 0) return lzq_set_error(LZQ_EINVAL, "lzq_ode_integrate_rows: max_steps < 0");
+  if (ode_blocks(n) > 2147483647LL) return lzq_set_error(LZQ_EINVAL, "lzq_ode_integrate_rows: n too large");
+  if (n == 0) return LZQ_OK;
+  const lzq::OdeRows rows{d_run_of, d_run_rep, d_row_off, n_runs > 0 ? (const lzq::YbCD*)d_rows : nullptr, n_runs,
+                          rows_doubles / 2};
+  return launch_integrate<false>(d_points, d_ode, n, d_table_index, d_work, max_steps, d_out, d_status,
+                                 (hipStream_t)stream, "lzq_ode_integrate_rows", nullptr, &rows);
 }
 
 int lzq_ode_quadrature(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n,

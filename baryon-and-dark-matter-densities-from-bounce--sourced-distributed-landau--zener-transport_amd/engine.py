@@ -260,6 +260,11 @@ class Engine:
         return out
 
     # -- ODE fallback (fpy:200-219, 270-286, 385-417) ---------------------------------------
+    def ode_params_to_device(self, recs: np.ndarray) -> torch.Tensor:
+        """lzq_ode_params records (numpy ODE_DTYPE array) -> device byte tensor (Engine.ode's
+        device-resident input, with points_to_device)."""
+        return _to_device_bytes(np.ascontiguousarray(recs, dtype=_native.ODE_DTYPE), self.device)
+
     def ode_workspace(self, n: int, nt: int = _native.ODE_NT) -> torch.Tensor:
         return torch.empty(n * 4 * int(nt), dtype=torch.float64, device=self.device)
 
@@ -286,7 +291,8 @@ class Engine:
     def ode(self, points, ode_params, max_steps: Optional[int] = None, chunk: int = 1 << 18,
             share_tables: bool = True, method: str = "radau", group_waves: bool = True, nz: int = _native.LZQ_NZ,
             z_max: float = _native.LZQ_Z_MAX, aov=None, time_parallel: Optional[bool] = None) -> tuple:
-        """fpy:385-417 for n points (POINT_DTYPE records + ODE_DTYPE records): (n, 6) yields
+        """fpy:385-417 for n points (POINT_DTYPE records + ODE_DTYPE records, as numpy arrays or
+        as device byte tensors from points_to_device / ode_params_to_device): (n, 6) yields
         table and (n,) int32 status (enum lzq_ode_status), both on the device.  Points are
         processed in chunks so that the spline workspace stays <= chunk * 25.6 KB (6.7 GB at the
         default 2^18 points: 2 waves/SIMD on all 1024 SIMDs need >= 131072 points per launch).
@@ -318,24 +324,38 @@ class Engine:
         nz, z_max = _native.zgrid(nz, z_max)
         if method not in ("radau", "quadrature"):
             raise ValueError(f"method must be 'radau' or 'quadrature', got {method!r}")
-        pts = np.ascontiguousarray(points, dtype=_native.POINT_DTYPE).reshape(-1)
-        ods = np.ascontiguousarray(ode_params, dtype=_native.ODE_DTYPE).reshape(-1)
-        if pts.size != ods.size:
-            raise ValueError("points and ode_params must have the same length")
-        n = pts.size
+        if isinstance(points, torch.Tensor):   # device records (points_to_device / ode_params_to_device)
+            pts = None
+            rp_, ro_ = _native.POINT_DTYPE.itemsize, _native.ODE_DTYPE.itemsize
+            if not isinstance(ode_params, torch.Tensor) or points.dtype != torch.uint8 or \
+                    ode_params.dtype != torch.uint8 or points.device != self.device or \
+                    ode_params.device != self.device or points.numel() % rp_ or \
+                    points.numel() // rp_ != ode_params.numel() // ro_ or ode_params.numel() % ro_:
+                raise ValueError("device points / ode_params: uint8 record tensors of the same length on the "
+                                 "engine's device (points_to_device, ode_params_to_device)")
+            n = points.numel() // rp_
+        else:
+            pts = np.ascontiguousarray(points, dtype=_native.POINT_DTYPE).reshape(-1)
+            ods = np.ascontiguousarray(ode_params, dtype=_native.ODE_DTYPE).reshape(-1)
+            if pts.size != ods.size:
+                raise ValueError("points and ode_params must have the same length")
+            n = pts.size
         if time_parallel is None:
             time_parallel = n == 1
         time_parallel = bool(time_parallel) and method == "radau"
         tp_iters = torch.zeros(n, dtype=torch.int32, device=self.device) if time_parallel else None
-        d_pts_all = self.points_to_device(pts)
-        d_ode_all = _to_device_bytes(ods, self.device)
+        if pts is None:
+            d_pts_all, d_ode_all = points.contiguous().view(-1), ode_params.contiguous().view(-1)
+        else:
+            d_pts_all = self.points_to_device(pts)
+            d_ode_all = _to_device_bytes(ods, self.device)
         d_aov_all = self.aov_to_device(aov, n)
         if d_aov_all is not None:
             share_tables = False   # a table's key now includes the block (ODE_TABLE_KEY does not)
         # the launches cover the batch's own largest step count (or the cap, when a point needs more:
         # those points come back LZQ_ODE_TOO_MANY_STEPS), not the cap itself
         per = 1 << getattr(self, "_ode_launch_log2", 24)
-        if n <= 4096:
+        if n <= 4096 and pts is not None:
             # few points (the CLI's one): on the host, no device round trip (the same values)
             need_h = ode_step_counts(pts)
             need_h = need_h[np.isfinite(need_h)]
@@ -382,8 +402,14 @@ class Engine:
                         "table per point (an A/V z-sum table build each; the integration still shares stage rows "
                         "across tables) -- ~2.6x the cost per point of a shared-table sweep on a 20000-step "
                         "window (DESIGN §4.3)", c1 - c0, c1 - c0, ", ".join(_native.ODE_TABLE_KEY))
-            plan.append((c0, c1, d_pts, d_ode, d_rep, d_idx, n_tab, d_aov))
-            keep.append((d_pts, d_ode, d_rep, d_idx, d_aov))
+            runs = None
+            if (d_rep is not None and method == "radau" and not time_parallel and getattr(self, "ode_rows", True)):
+                runs = ode_runs(d_pts, d_ode, d_idx, c1 - c0)
+            if runs is not None:
+                runs = runs[:3] + (runs[3], torch.empty(2 * runs[4], dtype=torch.float64, device=self.device))
+                tables["row_runs"] = tables.get("row_runs", 0) + int(runs[1].numel())
+            plan.append((c0, c1, d_pts, d_ode, d_rep, d_idx, n_tab, d_aov, runs))
+            keep.append((d_pts, d_ode, d_rep, d_idx, d_aov) + (() if runs is None else (runs[0], runs[1], runs[2], runs[4])))
         # Two or more chunks: chunk c + 1's spline tables are built on a side stream into the other
         # of two workspaces while chunk c integrates (the table kernels fill the SIMDs the
         # integrator's tail leaves idle); events order each workspace's reuse.  One chunk: one stream.
@@ -403,7 +429,7 @@ class Engine:
         freed = [None] * len(works)
         nt = _native.ODE_NT
         with torch.cuda.device(self.device):
-            for ci, (c0, c1, d_pts, d_ode, d_rep, d_idx, n_tab, d_aov) in enumerate(plan):
+            for ci, (c0, c1, d_pts, d_ode, d_rep, d_idx, n_tab, d_aov, runs) in enumerate(plan):
                 b = ci % len(works)
                 work = works[b]
                 with torch.cuda.stream(side):
@@ -433,6 +459,17 @@ class Engine:
                     self._check(self.lib.lzq_ode_integrate(_vp(d_pts), _vp(d_ode), c1 - c0, _vp(work), work.numel(),
                                                            int(max_steps), _vp(out[c0:c1]), _vp(status[c0:c1]),
                                                            self._stream()))
+                elif runs is not None:   # linear runs read shared step rows (bit-identical)
+                    run_of, run_rep, row_off, max_rows, rows = runs
+                    nr = run_rep.numel()
+                    self._check(self.lib.lzq_ode_rows(_vp(d_pts), _vp(d_ode), c1 - c0, _vp(d_idx), n_tab, _vp(work),
+                                                      work.numel(), _vp(run_rep), _vp(row_off), nr, max_rows,
+                                                      _vp(rows), rows.numel(), self._stream()))
+                    self._check(self.lib.lzq_ode_integrate_rows(_vp(d_pts), _vp(d_ode), c1 - c0, _vp(d_idx), n_tab,
+                                                                _vp(work), work.numel(), int(max_steps), _vp(run_of),
+                                                                _vp(run_rep), _vp(row_off), nr, _vp(rows),
+                                                                rows.numel(), _vp(out[c0:c1]), _vp(status[c0:c1]),
+                                                                self._stream()))
                 else:
                     self._check(self.lib.lzq_ode_integrate_shared(_vp(d_pts), _vp(d_ode), c1 - c0, _vp(d_idx),
                                                                   n_tab, _vp(work), work.numel(), int(max_steps),
@@ -669,6 +706,60 @@ def wave_order(d_pts: torch.Tensor, d_ode: torch.Tensor, n: int):
     ht = mix(torch.zeros(n, dtype=torch.int64, device=d_pts.device), ("I_p", "v_w"))
     by_table = torch.argsort(ht, stable=True)
     return by_table[torch.argsort(h[by_table], stable=True)]
+
+
+ROWS_MAX_BYTES = 256 << 20     # Engine.ode: shared step-row tables per chunk (lzq_ode_rows) up to this
+ROWS_MIN_RUN = 64              # a run needs a whole wavefront to be read by one
+
+
+def ode_runs(d_pts: torch.Tensor, d_ode: torch.Tensor, d_idx: torch.Tensor, n: int,
+             max_bytes: int = ROWS_MAX_BYTES, min_run: int = ROWS_MIN_RUN):
+    """Runs for lzq_ode_rows / lzq_ode_integrate_rows (include/lzq.h): maximal stretches of the
+    launch order whose points agree in _native.ODE_COOP_KEY, Gamma_wash and the spline table
+    index d_idx, and are linear (sigma_v = 0) and not depleting -- the points whose whole
+    wavefronts share Y_B's step maps.  Returns (run_of int32 [n], run_rep int64 [R], row_off int64
+    [R + 1] on the device, max_rows, total_rows), or None when no run of >= min_run points fits.  Runs are
+    kept longest first while their rows (16 B per step of the run's step count, ode_step_counts)
+    fit in max_bytes.  A 64-bit mix of the key words decides the runs; the kernel compares every
+    lane with its run's representative, bit for bit, before it reads the rows, so a hash
+    collision only costs the sharing."""
+    if n < min_run:
+        return None
+    rp, ro = _native.POINT_DTYPE.itemsize, _native.ODE_DTYPE.itemsize
+    w64 = d_pts.view(n, rp).view(torch.int64)
+    w32 = d_pts.view(n, rp).view(torch.int32)
+    o64 = d_ode.view(n, ro).view(torch.int64)
+    o32 = d_ode.view(n, ro).view(torch.int32)
+    sv = o64[:, _native.ODE_DTYPE.fields["sigma_v_chi_GeV_m2"][1] // 8].view(torch.float64)
+    elig = (sv == 0.0) & (o32[:, _native.ODE_DTYPE.fields["deplete_DM_from_source"][1] // 4] == 0)
+    if int(elig.sum()) < min_run:   # no linear run possible (e.g. Riccati sweeps): one small reduction
+        return None
+    h = torch.zeros(n, dtype=torch.int64, device=d_pts.device)
+    for f in _native.ODE_COOP_KEY:
+        off = _native.POINT_DTYPE.fields[f][1]
+        col = w64[:, off // 8] if _native.POINT_DTYPE.fields[f][0].itemsize == 8 else w32[:, off // 4].to(torch.int64)
+        h = (h * _MIX) ^ col
+    h = (h * _MIX) ^ o64[:, _native.ODE_DTYPE.fields["Gamma_wash_over_H"][1] // 8]
+    h = (h * _MIX) ^ d_idx.to(torch.int64)
+    h = torch.where(elig, h, torch.full_like(h, -1))   # ineligible points: one key, never a run
+    _, inv, counts = torch.unique_consecutive(h, return_inverse=True, return_counts=True)
+    starts = torch.cumsum(counts, 0) - counts
+    steps = ode_step_counts_device(d_pts, n)[starts]
+    ok = (counts >= min_run) & elig[starts] & torch.isfinite(steps) & (steps > 0)
+    rows = torch.where(ok, steps, torch.zeros_like(steps)).to(torch.int64)
+    by_len = torch.argsort(counts * ok, descending=True, stable=True)
+    cap = max_bytes // 16
+    keep = torch.zeros_like(ok)
+    keep[by_len] = ok[by_len] & (torch.cumsum(rows[by_len], 0) <= cap)
+    n_runs, max_rows, total = torch.stack([keep.sum(), (rows * keep).max(), (rows * keep).sum()]).tolist()
+    if n_runs == 0:
+        return None
+    sel = torch.nonzero(keep).reshape(-1)               # kept runs in launch order
+    run_id = torch.full_like(counts, -1)
+    run_id[sel] = torch.arange(n_runs, dtype=torch.int64, device=d_pts.device)
+    row_off = torch.zeros(n_runs + 1, dtype=torch.int64, device=d_pts.device)
+    row_off[1:] = torch.cumsum(rows[sel], 0)
+    return run_id[inv].to(torch.int32), starts[sel].contiguous(), row_off, int(max_rows), int(total)
 
 
 _KEY_WORDS = [_native.POINT_DOUBLE_FIELDS.index(f) for f in _native.ODE_TABLE_KEY]  # 8-byte words of lzq_point

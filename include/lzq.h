@@ -322,6 +322,31 @@ int lzq_ode_integrate_shared(const lzq_point* d_points, const lzq_ode_params* d_
                              int64_t work_doubles, int64_t max_steps, lzq_yield* d_out, int32_t* d_status,
                              void* stream);
 
+/* Shared step-row tables for linear sweeps (sigma_v = 0, no depletion; round 6; no reference
+ * counterpart -- a re-use of fpy:270-286's per-step quantities across points).  A run is a set
+ * of points equal in everything Y_B's Radau step map reads but P and the flux: the stage fields
+ * of the A/V spline, m_chi, g_chi, g_star_s, source_shape_sigma_y, stats, the table and
+ * Gamma_wash.  lzq_ode_rows writes run q's N_q step maps (c, d: Y_B' = c Y_B + P flux d, 16 B a
+ * step) from its representative point d_run_rep[q] into d_rows (as doubles) from row
+ * d_row_off[q] on, N_q = d_row_off[q + 1] - d_row_off[q] = the point's step count (ceil(|x1 -
+ * x0| / max_step), fpy:403-404); max_run_rows >= every N_q; rows past rows_doubles / 2 are not
+ * written.  lzq_ode_integrate_rows is lzq_ode_integrate_shared whose linear wavefronts read their
+ * run's rows (d_run_of[i]: point i's run, -1 none) instead of forming their own -- only after
+ * checking, per wavefront, that it is one run whose representative equals each point in all the
+ * rows depend on, bit for bit, and whose row count is the point's step count (otherwise, and for
+ * every other wavefront, lzq_ode_integrate_shared's path).  Results are bit-identical to
+ * lzq_ode_integrate_shared. */
+int lzq_ode_rows(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n, const int32_t* d_table_index,
+                 int64_t n_tables, const double* d_work, int64_t work_doubles, const int64_t* d_run_rep,
+                 const int64_t* d_row_off, int64_t n_runs, int64_t max_run_rows, double* d_rows,
+                 int64_t rows_doubles, void* stream);
+int lzq_ode_integrate_rows(const lzq_point* d_points, const lzq_ode_params* d_ode, int64_t n,
+                           const int32_t* d_table_index, int64_t n_tables, const double* d_work,
+                           int64_t work_doubles, int64_t max_steps, const int32_t* d_run_of,
+                           const int64_t* d_run_rep, const int64_t* d_row_off, int64_t n_runs,
+                           const double* d_rows, int64_t rows_doubles, lzq_yield* d_out, int32_t* d_status,
+                           void* stream);
+
 /* lzq_ode_integrate / lzq_ode_integrate_shared (d_table_index NULL: table i for point i) for a
  * FEW points on long windows -- the CLI's single point -- integrated parallel in time: each
  * point's N fixed steps are cut into intervals of LZQ_TUNE_ODE_TP_INTERVAL steps, every interval

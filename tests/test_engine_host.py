@@ -197,3 +197,43 @@ def test_bounce_csv_reader_is_the_plugins(tmp_path):
     import pytest
     with pytest.raises(ValueError):
         B.read_bounce_csv(str(tmp_path / "q.csv"))
+
+
+def _runs(p, o, idx, **kw):
+    tp = torch.from_numpy(np.ascontiguousarray(p).view(np.uint8).copy())
+    to = torch.from_numpy(np.ascontiguousarray(o).view(np.uint8).copy())
+    return pkg("engine").ode_runs(tp, to, torch.as_tensor(idx, dtype=torch.int32), p.size, **kw)
+
+
+def test_ode_runs_linear_stretches():
+    """engine.ode_runs (the shared step-row tables of lzq_ode_integrate_rows): maximal stretches of
+    linear, non-depleting points equal in the cooperative key, Gamma_wash and table, of >= 64
+    points; each run's rows are its first point's step count (ode_step_counts); the rest -1."""
+    rng = np.random.default_rng(11)
+    cfgs = []
+    for blk, (m, gw, sv, dep, cnt) in enumerate([(0.95, 1.0, 0.0, False, 130), (0.95, 2.0, 0.0, False, 70),
+                                                 (0.95, 2.0, 1e-16, False, 100), (40.0, 1.0, 0.0, True, 80),
+                                                 (40.0, 1.0, 0.0, False, 30), (40.0, 0.5, 0.0, False, 64)]):
+        for _ in range(cnt):
+            c = full_cfg(BASE_CFG)
+            c.update(m_chi_GeV=m, Gamma_wash_over_H=gw, sigma_v_chi_GeV_m2=sv, deplete_DM_from_source=dep,
+                     P_chi_to_B=float(rng.uniform(0.1, 1.0)), T_max_over_Tp=1.6, T_min_over_Tp=0.6)
+            cfgs.append(c)
+    p, o = _recs(cfgs)
+    n = p.size
+    run_of, rep, off, max_rows, total = _runs(p, o, np.zeros(n))
+    run_of, rep, off = run_of.numpy(), rep.numpy(), off.numpy()
+    steps = pkg("engine").ode_step_counts(p)
+    assert rep.tolist() == [0, 130, 410]                       # blocks 0, 1 and 5 (>= 64 linear, no depletion)
+    assert run_of[:130].tolist() == [0] * 130 and run_of[130:200].tolist() == [1] * 70
+    assert (run_of[200:410] == -1).all() and run_of[410:].tolist() == [2] * 64
+    assert off.tolist() == [0, int(steps[0]), int(steps[0] + steps[130]), int(steps[0] + steps[130] + steps[410])]
+    assert max_rows == int(steps.max()) and total == off[-1]
+    # a different table index splits a run; under the byte cap only the longest runs stay
+    idx = np.zeros(n)
+    idx[70:130] = 1                                # 60 points: too short
+    run_of2 = _runs(p, o, idx)[0].numpy()
+    assert run_of2[:70].tolist() == [0] * 70 and (run_of2[70:130] == -1).all()
+    r3 = _runs(p, o, np.zeros(n), max_bytes=int(16 * steps[0]))
+    assert r3[1].tolist() == [0] and r3[0].numpy()[130:].max() == -1
+    assert _runs(p[:63], o[:63], np.zeros(63)) is None

@@ -337,6 +337,110 @@ def test_ode_linear_waves_bit_identical(gpu_engine):
             assert rel_err(v, w) < 1e-10, (v, w)
 
 
+def test_ode_row_tables_bit_identical(gpu_engine):
+    """Shared step-row tables (lzq_ode_rows + lzq_ode_integrate_rows, engine.ode_runs): linear,
+    non-depleting runs of one cooperative key, Gamma_wash and table read Y_B's step maps from one
+    table per run instead of filling them per wavefront.  The same bits as without the tables
+    (Engine.ode_rows = False) and as the per-lane mode: wash-out runs of 200 and 130 points (waves
+    straddling two runs fill their own), a window crossing T = m/3 (split steps), a depleting
+    group beside them (no tables), the batch shuffled (wave_order regroups it), and continuation
+    launches of 2^11 steps."""
+    rng = np.random.default_rng(53)
+    cfgs = []
+    for m_chi, gw, dep, cnt in ((0.95, 0.5, False, 200), (300.0, 2.0, False, 130), (0.95, 1.0, True, 70),
+                                (0.95, 1.0, False, 100)):
+        for _ in range(cnt):
+            c = full_cfg(BASE_CFG)
+            c.update(NARROW, m_chi_GeV=m_chi, P_chi_to_B=float(rng.uniform(0.05, 1.0)),
+                     incident_flux_scale=float(10 ** rng.uniform(-10, -8)), Gamma_wash_over_H=gw,
+                     sigma_v_chi_GeV_m2=0.0, deplete_DM_from_source=dep, regime=str(rng.choice(["thermal", "nonthermal"])))
+            cfgs.append(c)
+    perm = rng.permutation(len(cfgs))
+    p, o = recs([cfgs[i] for i in perm])
+    a, sa = gpu_engine.ode(p, o)
+    assert gpu_engine.last_ode_tables.get("row_runs", 0) == 3
+    gpu_engine.ode_rows = False
+    try:
+        b, sb = gpu_engine.ode(p, o)
+        assert "row_runs" not in gpu_engine.last_ode_tables
+        prev = gpu_engine.tune_ode_coop(False)
+        try:
+            c, sc = gpu_engine.ode(p, o)
+        finally:
+            gpu_engine.tune_ode_coop(prev)
+    finally:
+        gpu_engine.ode_rows = True
+    assert bool((sa == 0).all()) and torch_equal(sa, sb) and torch_equal(a, b)
+    assert torch_equal(sa, sc) and torch_equal(a, c)
+    prev = gpu_engine.tune_ode_launch_steps(11)
+    try:
+        d, sd = gpu_engine.ode(p, o)
+    finally:
+        gpu_engine.tune_ode_launch_steps(prev)
+    assert torch_equal(sa, sd) and torch_equal(a, d)
+    # device-resident records (points_to_device / ode_params_to_device): the same bits
+    e, se = gpu_engine.ode(gpu_engine.points_to_device(p), gpu_engine.ode_params_to_device(o))
+    assert torch_equal(sa, se) and torch_equal(a, e)
+    with pytest.raises(ValueError):
+        gpu_engine.ode(gpu_engine.points_to_device(p), gpu_engine.ode_params_to_device(o[:-1]))
+    sel =[int(np.nonzero(perm == j)[0][0]) for j in (0, 250, 340, 480)]
+    ref, _ = O.ode_batch([cfgs[perm[i]] for i in sel], nthreads=4)
+    for row, rr in zip(a.cpu().numpy()[sel], ref):
+        for v, w in zip(row[:5], rr[:5]):
+            assert rel_err(v, w) < 1e-10, (v, w)
+
+
+def test_ode_row_tables_raw_abi_guards(gpu_engine):
+    """lzq_ode_integrate_rows through the C ABI with run tables that must not be read: a row count
+    that is not the points' step count, and a representative that differs from its run (another
+    Gamma_wash).  Every wavefront then fills its own rows: the bits of lzq_ode_integrate_shared."""
+    eng, lib = gpu_engine, gpu_engine.lib
+    rng = np.random.default_rng(59)
+    cfgs = []
+    for _ in range(128):
+        c = full_cfg(BASE_CFG)
+        c.update(NARROW, m_chi_GeV=0.95, P_chi_to_B=float(rng.uniform(0.05, 1.0)), Gamma_wash_over_H=1.0,
+                 sigma_v_chi_GeV_m2=0.0, deplete_DM_from_source=False)
+        cfgs.append(c)
+    other = dict(cfgs[0], Gamma_wash_over_H=2.0)
+    p, o = recs(cfgs + [other])
+    n = len(cfgs)
+    E = pkg("engine")
+    vp = E._vp
+    d_pts, d_ode = eng.points_to_device(p), E._to_device_bytes(o, eng.device)
+    work = eng.ode_workspace(2)
+    idx = torch.zeros(n + 1, dtype=torch.int32, device=eng.device)
+    idx[n] = 1
+    rep_pts = d_pts.view(n + 1, -1)[[0, n]].contiguous()
+    st = torch.zeros(2, dtype=torch.int32, device=eng.device)
+    eng._check(lib.lzq_ode_tables(vp(rep_pts), 2, None, None, pkg("_native").ODE_NT, pkg("_native").LZQ_NZ,
+                                  pkg("_native").LZQ_Z_MAX, None, vp(work),
+                                  work.numel(), vp(st), eng._stream()))
+    N = int(E.ode_step_counts(p[:1])[0])
+    ms = N + 64
+    ref_out = torch.empty((n + 1, 6), dtype=torch.float64, device=eng.device)
+    ref_st = torch.zeros(n + 1, dtype=torch.int32, device=eng.device)
+    eng._check(lib.lzq_ode_integrate_shared(vp(d_pts), vp(d_ode), n + 1, vp(idx), 2, vp(work), work.numel(), ms,
+                                            vp(ref_out), vp(ref_st), eng._stream()))
+    run_of = torch.zeros(n + 1, dtype=torch.int32, device=eng.device)
+    run_of[n] = -1
+    for rep, nrows in ((0, N - 1), (n, N), (0, N)):
+        run_rep = torch.tensor([rep], dtype=torch.int64, device=eng.device)
+        row_off = torch.tensor([0, nrows], dtype=torch.int64, device=eng.device)
+        rows = torch.zeros(2 * N, dtype=torch.float64, device=eng.device)
+        eng._check(lib.lzq_ode_rows(vp(d_pts), vp(d_ode), n + 1, vp(idx), 2, vp(work), work.numel(), vp(run_rep),
+                                    vp(row_off), 1, nrows, vp(rows), rows.numel(), eng._stream()))
+        out = torch.empty((n + 1, 6), dtype=torch.float64, device=eng.device)
+        stt = torch.zeros(n + 1, dtype=torch.int32, device=eng.device)
+        eng._check(lib.lzq_ode_integrate_rows(vp(d_pts), vp(d_ode), n + 1, vp(idx), 2, vp(work), work.numel(), ms,
+                                              vp(run_of), vp(run_rep), vp(row_off), 1, vp(rows), rows.numel(),
+                                              vp(out), vp(stt), eng._stream()))
+        torch.cuda.synchronize()
+        assert torch_equal(stt, ref_st) and torch_equal(out, ref_out), (rep, nrows)
+    assert lib.lzq_ode_rows(vp(d_pts), vp(d_ode), -1, None, 0, vp(work), work.numel(), None, None, 0, 0, None, 0,
+                            None) < 0
+
+
 def test_ode_cooperative_waves_bit_identical(gpu_engine):
     """ode_integrate_kernel's cooperative mode (a full wavefront whose points differ only in P,
     flux, sigma_v, Gamma_wash, deplete and the initial state computes each step's stage

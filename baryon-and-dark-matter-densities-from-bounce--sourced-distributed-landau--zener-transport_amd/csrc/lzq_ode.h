@@ -603,6 +603,15 @@ __device__ __forceinline__ double fma_neg_s(double k, double a, double p) {
 #ifndef LZQ_ODE_ROWS
 #define LZQ_ODE_ROWS 1  // linear waves read their run's shared row table when given one (lzq_ode_integrate_rows)
 #endif
+#ifndef LZQ_ODE_ROWS_ASYNC
+#define LZQ_ODE_ROWS_ASYNC 0  // 1: row-table waves fetch the next block into LDS (global_load_lds) while a block steps (measured slower)
+#endif
+#ifndef LZQ_ODE_ROWS_COPY
+#define LZQ_ODE_ROWS_COPY 4  // row staging: loads in flight per lane (a divisor of LZQ_ODE_ROWS_BLOCK / 64)
+#endif
+#ifndef LZQ_ODE_ROWS_BLOCK
+#define LZQ_ODE_ROWS_BLOCK 256   // row-table waves stage 2x this many rows per block (LZQ_ODE_ROWS_ASYNC: two buffers of it)
+#endif
 #ifndef LZQ_ODE_PRED_BLOCK
 // The Radau5 predictor is not used on steps k = 0 (mod LZQ_ODE_PRED_BLOCK): every block of that
 // many steps starts its Newton iteration from Y_chi, so a block's end state is a function of its

@@ -511,15 +511,58 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
         }
       }
     }
-    const int64_t block = coop ? G : N;
+    // Row-table waves stage their run's rows in their wave's s_base slot (unused by them: their
+    // stages are per lane off the tight loop), kOdeRowBlk rows per block in two buffers: block
+    // i + 1's rows are fetched straight into LDS (global_load_lds, 16 B per lane, no registers)
+    // while block i steps, so the global latency is off the step chain.
+    // (LZQ_ODE_ROWS_ASYNC = 0: one buffer of twice the rows, staged through registers, 4 loads in flight)
+    constexpr int kOdeRowBlk = LZQ_ODE_ROWS_ASYNC ? LZQ_ODE_ROWS_BLOCK : 2 * LZQ_ODE_ROWS_BLOCK;
+    static_assert(sizeof(s_base[0]) >= (LZQ_ODE_ROWS_ASYNC ? 2 : 1) * kOdeRowBlk * sizeof(YbCD),
+                  "row buffers exceed the s_base slot");
+    static_assert(kOdeRowBlk % 64 == 0, "row blocks are whole wavefront fetches");
+    YbCD* const s_rows = reinterpret_cast<YbCD*>(&s_base[wv][0][0]);
+    const bool rowblk = kLin && LZQ_ODE_ROWS && rrow;
+    const int64_t block = rowblk ? kOdeRowBlk : (coop ? G : N);
+    // rows kf .. kf + kOdeRowBlk - 1 (those < k_stop) into dst; lane l's row of each 64 lands at dst + 64 j + l
+    auto fetch_rows = [&](int64_t kf, YbCD* dst) {
+#pragma unroll
+      for (int j = 0; j < kOdeRowBlk / 64; ++j)
+        if (kf + 64 * j + lane < k_stop)
+          __builtin_amdgcn_global_load_lds(rrow + kf + 64 * j + lane, dst + 64 * j, 16, 0, 0);
+    };
+    if (LZQ_ODE_ROWS_ASYNC && rowblk) fetch_rows(k_begin, s_rows);
+    YbCD* s_cur = s_rows;  // row-table waves: this block's buffer
     for (int64_t kb = k_begin; kb < k_stop; kb += block) {
       const int64_t kend = kb + block < k_stop ? kb + block : k_stop;
-      if (kLin && LZQ_ODE_ROWS && rrow) {
-        const int64_t kl = kb + lane;
-        if (kl < kend) s_rcd[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][lane] = rrow[kl];
+      if (rowblk && !LZQ_ODE_ROWS_ASYNC) {
+        // groups of LZQ_ODE_ROWS_COPY loads, all issued before the group's first store (the empty
+        // asm consumes the whole group; guarded per row, the compiler waited on each load before
+        // its store); rows past the run's end read its last row, into LDS slots no step reads
+#pragma unroll
+        for (int g = 0; g < kOdeRowBlk / 64; g += LZQ_ODE_ROWS_COPY) {
+          YbCD t[LZQ_ODE_ROWS_COPY];
+#pragma unroll
+          for (int j = 0; j < LZQ_ODE_ROWS_COPY; ++j) {
+            const int64_t kr = kb + lane + 64 * (g + j);
+            t[j] = rrow[kr < k_stop ? kr : k_stop - 1];
+          }
+#pragma unroll
+          for (int j = 0; j < LZQ_ODE_ROWS_COPY; ++j) asm volatile("" : "+v"(t[j].c), "+v"(t[j].d));
+#pragma unroll
+          for (int j = 0; j < LZQ_ODE_ROWS_COPY; ++j) s_rows[lane + 64 * (g + j)] = t[j];
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      } else if (rowblk) {
+        s_cur = s_rows + (((kb - k_begin) / kOdeRowBlk) & 1) * kOdeRowBlk;
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this block's rows have landed in LDS
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // the next block's rows into the other buffer (its last reader was the previous block, whose
+        // steps ended at that block's closing wave barrier)
+        if (kb + kOdeRowBlk < k_stop) fetch_rows(kb + kOdeRowBlk, s_rows + kOdeRowBlk - (s_cur - s_rows));
       } else if (coop) {
         const int64_t kl = kb + (lane - seg);
         if (kl < kend) {
@@ -554,7 +597,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
           const int nf = (int)(kg - k);
           if (nf > 0) {
             const int r0 = seg + (int)(k - kb);
-            const YbCD* rr = &s_rcd[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][r0];
+            const YbCD* rr = rowblk ? &s_cur[k - kb] : &s_rcd[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][r0];
             const YbW* rw = &s_rw[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][r0];
             if (tab_vary) {  // each step's a_j from this lane's table, then its own d
               // T falls with x, so the rows' spline intervals run from the first row's stage 0
@@ -592,7 +635,8 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
               }
             } else {
               // the rows in batches of 8: their LDS reads are independent of Y_B, so all eight are
-              // issued before the chain of fmas needs the first
+              // issued before the chain of fmas needs the first (reading the next batch ahead of
+              // the current one's fmas measured the same, profiles/round6/ablate_ode_lin_pipe.json)
               int jj = 0;
               for (; jj + 8 <= nf; jj += 8) {
                 YbCD q[8];
@@ -634,7 +678,7 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
         if (xa > xk) {
           const double hs = split ? xa - xk : h;
           OdeStage sg[3];
-          if (coop && !split && !(kLin && LZQ_ODE_ROWS && rrow)) {  // (row tables: no stage bases in LDS)
+          if (coop && !split && !rowblk) {  // (row tables: no stage bases in LDS)
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
               StageBase b = s_base[wv][seg + (k - kb)][j];
@@ -649,7 +693,9 @@ __global__ __launch_bounds__(kOdeBlock, LZQ_ODE_MIN_WAVES) void ode_integrate_ke
           if (riccati && !split && !pred_step(k)) use_guess = block_guess(R, hs, sg, Ychi, Zs);
           if (LZQ_ODE_YBREC && !kChiOnly) {  // Y_B by its step map, then Y_chi alone
             YbCD r;
-            if (rec_shared && !split) {
+            if (rowblk && !split) {
+              r = s_cur[k - kb];
+            } else if (rec_shared && !split) {
               r = s_rcd[LZQ_ODE_YBREC && !kChiOnly ? wv : 0][seg + (k - kb)];
               if (tab_vary) {
                 const double a[3] = {sg[0].a, sg[1].a, sg[2].a};

@@ -355,6 +355,7 @@ class Engine:
         # the launches cover the batch's own largest step count (or the cap, when a point needs more:
         # those points come back LZQ_ODE_TOO_MANY_STEPS), not the cap itself
         per = 1 << getattr(self, "_ode_launch_log2", 24)
+        need = None
         if n <= 4096 and pts is not None:
             # few points (the CLI's one): on the host, no device round trip (the same values)
             need_h = ode_step_counts(pts)
@@ -368,6 +369,8 @@ class Engine:
         longest = int(min(top, _native.ODE_MAX_LAUNCHES * per))
         max_steps = longest if max_steps is None else min(int(max_steps), longest)
         order = wave_order(d_pts_all, d_ode_all, n) if group_waves else None
+        if need is not None and order is not None:
+            need = need[order]
         if order is not None:
             d_pts_all = d_pts_all.view(n, -1)[order].contiguous().view(-1)
             d_ode_all = d_ode_all.view(n, -1)[order].contiguous().view(-1)
@@ -404,7 +407,7 @@ class Engine:
                         "window (DESIGN §4.3)", c1 - c0, c1 - c0, ", ".join(_native.ODE_TABLE_KEY))
             runs = None
             if (d_rep is not None and method == "radau" and not time_parallel and getattr(self, "ode_rows", True)):
-                runs = ode_runs(d_pts, d_ode, d_idx, c1 - c0)
+                runs = ode_runs(d_pts, d_ode, d_idx, c1 - c0, steps=None if need is None else need[c0:c1])
             if runs is not None:
                 runs = runs[:3] + (runs[3], torch.empty(2 * runs[4], dtype=torch.float64, device=self.device))
                 tables["row_runs"] = tables.get("row_runs", 0) + int(runs[1].numel())
@@ -665,7 +668,40 @@ class ProfileShapes:
         self.n_shapes, self.n_knots = int(knots.shape[0]), int(knots.shape[1])
 
 
-_MIX = -7046029254386353131  # 0x9E3779B97F4A7C15 as int64 (torch multiplies wrap)
+# fixed odd 64-bit weights of _key_hash (a wrapping weighted sum of the key words)
+_HASH_W = np.random.default_rng(0x6C7A71).integers(-2 ** 63, 2 ** 63 - 1, size=32, dtype=np.int64) | 1
+_hash_w_dev: dict = {}
+
+
+def _hash_weights(device, k: int) -> torch.Tensor:
+    w = _hash_w_dev.get(device)
+    if w is None:
+        w = _hash_w_dev[device] = torch.from_numpy(_HASH_W).to(device)
+    return w[:k]
+
+
+def _key_hash(d_pts: torch.Tensor, n: int, fields, d_ode: Optional[torch.Tensor] = None, ode_fields=(),
+              extra: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """A 64-bit hash of each point's key words (lzq_point fields, lzq_ode_params fields and an
+    optional extra int column): their bits times fixed odd 64-bit weights, summed with wrap-around
+    -- a few gathers and one reduction whatever the key length (the per-field multiply-xor chain
+    it replaces was ~3 kernels per field, a third of a 2.6e5-point linear ODE call's kernels).
+    Equal keys hash equally; the callers treat a collision of unequal keys as a lost grouping
+    only (the kernels and table_groups compare the words themselves)."""
+    cols = []
+    for rec, dt, fs in ((d_pts, _native.POINT_DTYPE, fields), (d_ode, _native.ODE_DTYPE, ode_fields)):
+        if not fs:
+            continue
+        i8 = [dt.fields[f][1] // 8 for f in fs if dt.fields[f][0].itemsize == 8]
+        i4 = [dt.fields[f][1] // 4 for f in fs if dt.fields[f][0].itemsize == 4]
+        if i8:
+            cols.append(rec.view(n, dt.itemsize).view(torch.int64)[:, i8])
+        if i4:
+            cols.append(rec.view(n, dt.itemsize).view(torch.int32)[:, i4].to(torch.int64))
+    if extra is not None:
+        cols.append(extra.to(torch.int64).view(n, 1))
+    c = torch.cat(cols, 1) if len(cols) > 1 else cols[0]
+    return (c * _hash_weights(c.device, c.shape[1])).sum(1)
 REUSE_MAX_BYTES = 16 << 30     # Engine.sweep(reuse=True): z-sum tables beyond this run dense
 
 
@@ -676,26 +712,11 @@ def wave_order(d_pts: torch.Tensor, d_ode: torch.Tensor, n: int):
     grouped or has no repeated keys.  Gamma_wash (round 6): a whole wave with one Gamma_wash shares
     Y_B's step maps and runs the Riccati kernel, a wave that mixes several runs the general variant
     (DESIGN §4.3).  d_pts / d_ode: the lzq_point / lzq_ode_params records as byte tensors.  A
-    64-bit mix of the key fields' bits is sorted stably; a hash collision only puts unequal
+    64-bit hash of the key fields' bits (_key_hash) is sorted stably; a hash collision only puts unequal
     points in one wavefront, which the kernel detects and runs per lane."""
     if n <= 64:
         return None
-    w64 = d_pts.view(n, _native.POINT_DTYPE.itemsize).view(torch.int64)
-    w32 = d_pts.view(n, _native.POINT_DTYPE.itemsize).view(torch.int32)
-    o32 = d_ode.view(n, _native.ODE_DTYPE.itemsize).view(torch.int32)
-
-    def mix(h, fields):
-        for f in fields:
-            off = _native.POINT_DTYPE.fields[f][1]
-            col = w64[:, off // 8] if _native.POINT_DTYPE.fields[f][0].itemsize == 8 else \
-                w32[:, off // 4].to(torch.int64)
-            h = (h * _MIX) ^ col
-        return h
-
-    h = mix(torch.zeros(n, dtype=torch.int64, device=d_pts.device), _native.ODE_COOP_KEY)
-    h = (h * _MIX) ^ o32[:, _native.ODE_DTYPE.fields["deplete_DM_from_source"][1] // 4].to(torch.int64)
-    o64 = d_ode.view(n, _native.ODE_DTYPE.itemsize).view(torch.int64)
-    h = (h * _MIX) ^ o64[:, _native.ODE_DTYPE.fields["Gamma_wash_over_H"][1] // 8]
+    h = _key_hash(d_pts, n, _native.ODE_COOP_KEY, d_ode, ("deplete_DM_from_source", "Gamma_wash_over_H"))
     # the key's breaks in input order and its distinct values (from one sort), in one transfer
     hs = torch.sort(h).values
     breaks, distinct = torch.stack([(h[1:] != h[:-1]).sum(), 1 + (hs[1:] != hs[:-1]).sum()]).tolist()
@@ -703,7 +724,7 @@ def wave_order(d_pts: torch.Tensor, d_ode: torch.Tensor, n: int):
         return None
     if distinct == n or breaks <= 2 * (distinct - 1):
         return None
-    ht = mix(torch.zeros(n, dtype=torch.int64, device=d_pts.device), ("I_p", "v_w"))
+    ht = _key_hash(d_pts, n, ("I_p", "v_w"))
     by_table = torch.argsort(ht, stable=True)
     return by_table[torch.argsort(h[by_table], stable=True)]
 
@@ -713,38 +734,31 @@ ROWS_MIN_RUN = 64              # a run needs a whole wavefront to be read by one
 
 
 def ode_runs(d_pts: torch.Tensor, d_ode: torch.Tensor, d_idx: torch.Tensor, n: int,
-             max_bytes: int = ROWS_MAX_BYTES, min_run: int = ROWS_MIN_RUN):
+             max_bytes: int = ROWS_MAX_BYTES, min_run: int = ROWS_MIN_RUN, steps: Optional[torch.Tensor] = None):
     """Runs for lzq_ode_rows / lzq_ode_integrate_rows (include/lzq.h): maximal stretches of the
     launch order whose points agree in _native.ODE_COOP_KEY, Gamma_wash and the spline table
     index d_idx, and are linear (sigma_v = 0) and not depleting -- the points whose whole
     wavefronts share Y_B's step maps.  Returns (run_of int32 [n], run_rep int64 [R], row_off int64
     [R + 1] on the device, max_rows, total_rows), or None when no run of >= min_run points fits.  Runs are
     kept longest first while their rows (16 B per step of the run's step count, ode_step_counts)
-    fit in max_bytes.  A 64-bit mix of the key words decides the runs; the kernel compares every
+    fit in max_bytes (steps: the points' ode_step_counts_device, when the caller has them).  A
+    64-bit hash of the key words (_key_hash) decides the runs; the kernel compares every
     lane with its run's representative, bit for bit, before it reads the rows, so a hash
     collision only costs the sharing."""
     if n < min_run:
         return None
-    rp, ro = _native.POINT_DTYPE.itemsize, _native.ODE_DTYPE.itemsize
-    w64 = d_pts.view(n, rp).view(torch.int64)
-    w32 = d_pts.view(n, rp).view(torch.int32)
+    ro = _native.ODE_DTYPE.itemsize
     o64 = d_ode.view(n, ro).view(torch.int64)
     o32 = d_ode.view(n, ro).view(torch.int32)
     sv = o64[:, _native.ODE_DTYPE.fields["sigma_v_chi_GeV_m2"][1] // 8].view(torch.float64)
     elig = (sv == 0.0) & (o32[:, _native.ODE_DTYPE.fields["deplete_DM_from_source"][1] // 4] == 0)
     if int(elig.sum()) < min_run:   # no linear run possible (e.g. Riccati sweeps): one small reduction
         return None
-    h = torch.zeros(n, dtype=torch.int64, device=d_pts.device)
-    for f in _native.ODE_COOP_KEY:
-        off = _native.POINT_DTYPE.fields[f][1]
-        col = w64[:, off // 8] if _native.POINT_DTYPE.fields[f][0].itemsize == 8 else w32[:, off // 4].to(torch.int64)
-        h = (h * _MIX) ^ col
-    h = (h * _MIX) ^ o64[:, _native.ODE_DTYPE.fields["Gamma_wash_over_H"][1] // 8]
-    h = (h * _MIX) ^ d_idx.to(torch.int64)
+    h = _key_hash(d_pts, n, _native.ODE_COOP_KEY, d_ode, ("Gamma_wash_over_H",), extra=d_idx)
     h = torch.where(elig, h, torch.full_like(h, -1))   # ineligible points: one key, never a run
     _, inv, counts = torch.unique_consecutive(h, return_inverse=True, return_counts=True)
     starts = torch.cumsum(counts, 0) - counts
-    steps = ode_step_counts_device(d_pts, n)[starts]
+    steps = (ode_step_counts_device(d_pts, n) if steps is None else steps)[starts]
     ok = (counts >= min_run) & elig[starts] & torch.isfinite(steps) & (steps > 0)
     rows = torch.where(ok, steps, torch.zeros_like(steps)).to(torch.int64)
     by_len = torch.argsort(counts * ok, descending=True, stable=True)
@@ -771,7 +785,7 @@ def table_groups(d_pts: torch.Tensor, n: int, words=None):
     bit, in _native.ODE_TABLE_KEY (or in the lzq_point words `words`: _ZSUM_WORDS for the
     quadrature's z-sum tables).  Returns (representative indices, per-point table index),
     both int64 device tensors, or None when sharing would not pay (more than half the points
-    distinct).  Index bookkeeping on the device: a 64-bit mix of the key words is deduplicated
+    distinct).  Index bookkeeping on the device: a 64-bit hash of the key words is deduplicated
     and every point's key is then compared with its representative's, so a hash collision only
     costs the sharing, never a wrong table."""
     if n < 2:
@@ -780,9 +794,7 @@ def table_groups(d_pts: torch.Tensor, n: int, words=None):
     if bool((key == key[0]).all()):
         z = torch.zeros(n, dtype=torch.int64, device=d_pts.device)
         return z[:1], z
-    h = key[:, 0].clone()
-    for j in range(1, key.shape[1]):
-        h = (h * _MIX) ^ key[:, j]
+    h = (key * _hash_weights(key.device, key.shape[1])).sum(1)
     u, inv = torch.unique(h, return_inverse=True)
     if u.numel() * 2 > n:
         return None

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--out", default=None)
     ap.add_argument("--profile", action="store_true")
+    ap.add_argument("--only", default=None, help="one mode: rows, no_rows, rows_resident, no_rows_resident "
+                    "(for a kernel trace of that mode alone)")
     a = ap.parse_args()
     from ode_pmc_run import CASES, case_points
     cfgm = importlib.import_module(PKG + ".config")
@@ -44,6 +46,8 @@ def main():
         for key in (("rows", True, False), ("no_rows", False, False), ("rows", True, True),
                     ("no_rows", False, True), ("rows", True, False)):
             tag, rows, resident = key[0] + ("_resident" if key[2] else ""), key[1], key[2]
+            if a.only and tag != a.only:
+                continue
             eng.ode_rows = rows
             args = d_in if resident else (pts, ods)
             eng.ode(*args)   # warm-up
@@ -57,15 +61,16 @@ def main():
                 best = d if best is None else min(best, d)
             res[tag] = min(best, res.get(tag, best))
             outs[tag] = (tab.clone(), st.clone(), dict(eng.last_ode_tables))
-        ref = outs["no_rows"]
+        ref = next(iter(outs.values()))
         same = all(bool(torch.equal(o[0].view(torch.int64), ref[0].view(torch.int64)) and torch.equal(o[1], ref[1]))
                    for o in outs.values())
-        rec = {"case": name, "points": a.points, "bit_identical": same, "row_runs": outs["rows"][2].get("row_runs", 0),
-               "all_ok": bool((ref[1] == 0).all())}
+        rec = {"case": name, "points": a.points, "bit_identical": same,
+               "row_runs": max(o[2].get("row_runs", 0) for o in outs.values()), "all_ok": bool((ref[1] == 0).all())}
         for tag, t in res.items():
             rec[tag + "_s"] = t
             rec[tag + "_points_per_s"] = a.points / t
-        rec["rows_speedup_resident"] = res["no_rows_resident"] / res["rows_resident"]
+        if "rows_resident" in res and "no_rows_resident" in res:
+            rec["rows_speedup_resident"] = res["no_rows_resident"] / res["rows_resident"]
         if a.profile:
             eng.ode_rows = True
             pr = cProfile.Profile()

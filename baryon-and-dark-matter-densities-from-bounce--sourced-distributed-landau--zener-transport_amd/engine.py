@@ -717,11 +717,13 @@ def wave_order(d_pts: torch.Tensor, d_ode: torch.Tensor, n: int):
     if n <= 64:
         return None
     h = _key_hash(d_pts, n, _native.ODE_COOP_KEY, d_ode, ("deplete_DM_from_source", "Gamma_wash_over_H"))
-    # the key's breaks in input order and its distinct values (from one sort), in one transfer
-    hs = torch.sort(h).values
-    breaks, distinct = torch.stack([(h[1:] != h[:-1]).sum(), 1 + (hs[1:] != hs[:-1]).sum()]).tolist()
+    # the key's breaks in input order (none: one key, the common sweep -- no sort needed), then its
+    # distinct values (from one sort)
+    breaks = int((h[1:] != h[:-1]).sum())
     if breaks == 0:
         return None
+    hs = torch.sort(h).values
+    distinct = 1 + int((hs[1:] != hs[:-1]).sum())
     if distinct == n or breaks <= 2 * (distinct - 1):
         return None
     ht = _key_hash(d_pts, n, ("I_p", "v_w"))
@@ -752,13 +754,24 @@ def ode_runs(d_pts: torch.Tensor, d_ode: torch.Tensor, d_idx: torch.Tensor, n: i
     o32 = d_ode.view(n, ro).view(torch.int32)
     sv = o64[:, _native.ODE_DTYPE.fields["sigma_v_chi_GeV_m2"][1] // 8].view(torch.float64)
     elig = (sv == 0.0) & (o32[:, _native.ODE_DTYPE.fields["deplete_DM_from_source"][1] // 4] == 0)
-    if int(elig.sum()) < min_run:   # no linear run possible (e.g. Riccati sweeps): one small reduction
-        return None
     h = _key_hash(d_pts, n, _native.ODE_COOP_KEY, d_ode, ("Gamma_wash_over_H",), extra=d_idx)
+    if steps is None:
+        steps = ode_step_counts_device(d_pts, n)
+    # one transfer: eligible points, points with the first point's key, the first point's step count
+    n_elig, n_same, s0 = torch.stack([elig.sum().to(torch.float64), (h == h[0]).sum().to(torch.float64),
+                                      steps[0]]).tolist()
+    if n_elig < min_run:   # no linear run possible (e.g. Riccati sweeps)
+        return None
+    if n_elig == n and n_same == n:   # one run (the common linear sweep): no grouping kernels
+        if not (np.isfinite(s0) and s0 > 0 and 16 * s0 <= max_bytes):
+            return None
+        dev = d_pts.device
+        return (torch.zeros(n, dtype=torch.int32, device=dev), torch.zeros(1, dtype=torch.int64, device=dev),
+                torch.tensor([0, int(s0)], dtype=torch.int64, device=dev), int(s0), int(s0))
     h = torch.where(elig, h, torch.full_like(h, -1))   # ineligible points: one key, never a run
     _, inv, counts = torch.unique_consecutive(h, return_inverse=True, return_counts=True)
     starts = torch.cumsum(counts, 0) - counts
-    steps = (ode_step_counts_device(d_pts, n) if steps is None else steps)[starts]
+    steps = steps[starts]
     ok = (counts >= min_run) & elig[starts] & torch.isfinite(steps) & (steps > 0)
     rows = torch.where(ok, steps, torch.zeros_like(steps)).to(torch.int64)
     by_len = torch.argsort(counts * ok, descending=True, stable=True)

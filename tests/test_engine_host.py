@@ -237,3 +237,26 @@ def test_ode_runs_linear_stretches():
     r3 = _runs(p, o, np.zeros(n), max_bytes=int(16 * steps[0]))
     assert r3[1].tolist() == [0] and r3[0].numpy()[130:].max() == -1
     assert _runs(p[:63], o[:63], np.zeros(63)) is None
+
+
+def test_ode_runs_single_run_fast_path():
+    """A chunk that is one linear run (the common wash-out sweep) comes back from the one-transfer
+    path: every point in run 0, represented by point 0, with point 0's step count of rows; one
+    depleting point among them sends the chunk through the general grouping instead."""
+    rng = np.random.default_rng(12)
+    cfgs = []
+    for _ in range(100):
+        c = full_cfg(BASE_CFG)
+        c.update(m_chi_GeV=0.95, Gamma_wash_over_H=1.0, sigma_v_chi_GeV_m2=0.0, deplete_DM_from_source=False,
+                 P_chi_to_B=float(rng.uniform(0.1, 1.0)), T_max_over_Tp=1.6, T_min_over_Tp=0.6)
+        cfgs.append(c)
+    p, o = _recs(cfgs)
+    steps = pkg("engine").ode_step_counts(p)
+    run_of, rep, off, max_rows, total = _runs(p, o, np.zeros(100))
+    assert run_of.tolist() == [0] * 100 and rep.tolist() == [0] and off.tolist() == [0, int(steps[0])]
+    assert max_rows == total == int(steps[0])
+    assert _runs(p, o, np.zeros(100), max_bytes=int(16 * steps[0]) - 1) is None
+    o2 = o.copy()
+    o2["deplete_DM_from_source"][99] = 1
+    run_of2, rep2, off2 = _runs(p, o2, np.zeros(100))[:3]
+    assert run_of2.tolist() == [0] * 99 + [-1] and rep2.tolist() == [0] and off2.tolist() == [0, int(steps[0])]

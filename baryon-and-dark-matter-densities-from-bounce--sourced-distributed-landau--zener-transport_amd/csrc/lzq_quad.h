@@ -58,6 +58,9 @@ constexpr int kWavesPerBlock = kBlock / kWaveSize;
 #ifndef LZQ_ACC_LDS
 #define LZQ_ACC_LDS 1
 #endif
+#ifndef LZQ_SPLIT_CLAMP
+#define LZQ_SPLIT_CLAMP 0  // clamped passes: the z-nodes no lane can clamp run clamp-free (zsum_dispatch)
+#endif
 constexpr int kKUnroll = LZQ_KUNROLL;  // z-nodes per scalar-load batch (must divide 1200)
 constexpr int kYB = LZQ_YB;            // y-nodes per lane per pass (independent chains)
 static_assert(kNZ % kKUnroll == 0, "z unroll must divide nz");
@@ -316,9 +319,12 @@ __device__ __forceinline__ double c2_scale() { return EXPV == kExpTable ? (doubl
 // N*1534 (no node can leave the clamp range); zsum_dispatch picks it per pass.
 template <int YB, int EXPV, bool CLAMP = true>
 __device__ __forceinline__ void zsum(const ZNode* __restrict__ zt, const double* tab, const double (&c2)[YB],
-                                     double (&F)[YB], int kend) {
+                                     double (&F)[YB], int kend, int kbeg = 0) {
+  // kbeg > 0: nodes kbeg.. continue F's running sums (LZQ_SPLIT_CLAMP), else F starts at 0
+  if (kbeg == 0) {
 #pragma unroll
-  for (int b = 0; b < YB; ++b) F[b] = 0.0;
+    for (int b = 0; b < YB; ++b) F[b] = 0.0;
+  }
   if constexpr (EXPV == kExpTable) {
     constexpr double kMagic = 0x1.8p52;
     constexpr double kTClamp = kMagic + (double)kTabKMin;  // exact
@@ -330,7 +336,7 @@ __device__ __forceinline__ void zsum(const ZNode* __restrict__ zt, const double*
     for (int i = 0; i < kPolyDeg; ++i) Bv[i] = TabPoly<kTabBits, kPolyDeg>::B[i];
     if constexpr (!kSqForm) Bv[0] = vgpr_const(Bv[0]);
     const char* tabb = reinterpret_cast<const char*>(tab);
-    for (int k = 0; k < kend; k += kKUnroll) {
+    for (int k = kbeg; k < kend; k += kKUnroll) {
       double g4[kKUnroll], om[kKUnroll];
 #pragma unroll
       for (int kk = 0; kk < kKUnroll; ++kk) {
@@ -440,10 +446,29 @@ __device__ __forceinline__ void zsum_dispatch(const ZNode* __restrict__ zt, int 
     }
     kend = (lo + kKUnroll - 1) / kKUnroll * kKUnroll;
   }
-  if (EXPV == kExpTable && __all(small))
+  if (EXPV == kExpTable && __all(small)) {
     zsum<YB, EXPV, false>(zt, tab, c2e, F, kend);
-  else
+  } else if (EXPV == kExpTable && LZQ_SPLIT_CLAMP) {
+    // LZQ_SPLIT_CLAMP: the nodes before the first one at which some lane's u = c2 g4 drops below
+    // KMIN + 1 (g4 non-decreasing -- build_ztable refuses other grids -- and c2 <= 0, so u only
+    // falls with k) cannot reach the clamp: they run clamp-free (max(t, M + KMIN) = t there, the
+    // same bits), the rest clamped, F summed in the same node order.  A wave-uniform binary search.
+    int lo = 0, hi = kend;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      const double g = zt[mid].g4;
+      bool low = false;
+#pragma unroll
+      for (int b = 0; b < YB; ++b) low = low || c2e[b] * g < (double)kTabKMin + 1.0;
+      if (__any(low)) hi = mid;
+      else lo = mid + 1;
+    }
+    const int ks = lo / kKUnroll * kKUnroll;
+    if (ks > 0) zsum<YB, EXPV, false>(zt, tab, c2e, F, ks);
+    zsum<YB, EXPV, true>(zt, tab, c2e, F, kend, ks);
+  } else {
     zsum<YB, EXPV, true>(zt, tab, c2e, F, kend);
+  }
 #pragma unroll
   for (int b = 0; b < YB; ++b) F[b] = dead[b] ? 0.0 : F[b];
 }

@@ -702,6 +702,8 @@ def _key_hash(d_pts: torch.Tensor, n: int, fields, d_ode: Optional[torch.Tensor]
         cols.append(extra.to(torch.int64).view(n, 1))
     c = torch.cat(cols, 1) if len(cols) > 1 else cols[0]
     return (c * _hash_weights(c.device, c.shape[1])).sum(1)
+
+
 REUSE_MAX_BYTES = 16 << 30     # Engine.sweep(reuse=True): z-sum tables beyond this run dense
 
 

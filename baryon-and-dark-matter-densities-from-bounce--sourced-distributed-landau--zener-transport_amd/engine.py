@@ -355,7 +355,7 @@ class Engine:
         # the launches cover the batch's own largest step count (or the cap, when a point needs more:
         # those points come back LZQ_ODE_TOO_MANY_STEPS), not the cap itself
         per = 1 << getattr(self, "_ode_launch_log2", 24)
-        need = None
+        need = h_coop = coop_breaks = tab_same = n_lin = None
         if n <= 4096 and pts is not None:
             # few points (the CLI's one): on the host, no device round trip (the same values)
             need_h = ode_step_counts(pts)
@@ -363,12 +363,32 @@ class Engine:
             top = float(need_h.max()) + 64 if need_h.size else 0
         else:
             need = ode_step_counts_device(d_pts_all, n)   # same values as ode_step_counts, on the device
-            # the largest finite count in one device reduction and one transfer (-inf: none finite)
-            top = float(torch.where(torch.isfinite(need), need, float("-inf")).max())
-            top = top + 64 if top != float("-inf") else 0
+            # one transfer for the largest finite count (-inf: none finite), the launch order's key
+            # breaks and whether every point has the first one's table key (wave_order, table_groups)
+            vals = [torch.where(torch.isfinite(need), need, float("-inf")).max()]
+            if group_waves and n > 64:
+                h_coop = _coop_hash(d_pts_all, d_ode_all, n)
+                vals.append((h_coop[1:] != h_coop[:-1]).sum().to(torch.float64))
+            rows_on = share_tables and method == "radau" and not time_parallel and getattr(self, "ode_rows", True)
+            if rows_on:   # points that could be in a row-table run (linear, not depleting): ode_runs' own test
+                o_ = d_ode_all.view(n, _native.ODE_DTYPE.itemsize)
+                sv_ = o_.view(torch.float64)[:, _native.ODE_DTYPE.fields["sigma_v_chi_GeV_m2"][1] // 8]
+                dep_ = o_.view(torch.int32)[:, _native.ODE_DTYPE.fields["deplete_DM_from_source"][1] // 4]
+                vals.append(((sv_ == 0.0) & (dep_ == 0)).sum().to(torch.float64))
+            if share_tables:
+                key = d_pts_all.view(n, _native.POINT_DTYPE.itemsize).view(torch.int64)[:, _KEY_WORDS]
+                vals.append((key == key[0]).all().to(torch.float64))
+            got = torch.stack(vals).tolist()
+            if rows_on:
+                n_lin = int(got[2 if group_waves and n > 64 else 1])
+            top = got[0] + 64 if got[0] != float("-inf") else 0
+            if group_waves and n > 64:
+                coop_breaks = int(got[1])
+            if share_tables:
+                tab_same = bool(got[-1])
         longest = int(min(top, _native.ODE_MAX_LAUNCHES * per))
         max_steps = longest if max_steps is None else min(int(max_steps), longest)
-        order = wave_order(d_pts_all, d_ode_all, n) if group_waves else None
+        order = wave_order(d_pts_all, d_ode_all, n, h=h_coop, breaks=coop_breaks) if group_waves else None
         if need is not None and order is not None:
             need = need[order]
         if order is not None:
@@ -389,7 +409,9 @@ class Engine:
             d_ode = d_ode_all[c0 * ro:c1 * ro]
             ra = _native.AOV_DTYPE.itemsize
             d_aov = None if d_aov_all is None else d_aov_all[c0 * ra:c1 * ra]
-            rep = table_groups(d_pts, c1 - c0) if share_tables else None
+            # (tab_same: whether every point of the batch has the first one's table key -- then every
+            # chunk's does; when not, a chunk's own grouping still finds a chunk of one key)
+            rep = table_groups(d_pts, c1 - c0, all_same=tab_same) if share_tables else None
             d_rep = d_idx = None
             if rep is not None:
                 d_rep = d_pts.view(c1 - c0, rp)[rep[0]].contiguous()
@@ -406,7 +428,8 @@ class Engine:
                         "across tables) -- ~2.6x the cost per point of a shared-table sweep on a 20000-step "
                         "window (DESIGN §4.3)", c1 - c0, c1 - c0, ", ".join(_native.ODE_TABLE_KEY))
             runs = None
-            if (d_rep is not None and method == "radau" and not time_parallel and getattr(self, "ode_rows", True)):
+            if (d_rep is not None and method == "radau" and not time_parallel and getattr(self, "ode_rows", True)
+                    and (n_lin is None or n_lin >= ROWS_MIN_RUN)):
                 runs = ode_runs(d_pts, d_ode, d_idx, c1 - c0, steps=None if need is None else need[c0:c1])
             if runs is not None:
                 runs = runs[:3] + (runs[3], torch.empty(2 * runs[4], dtype=torch.float64, device=self.device))
@@ -707,7 +730,13 @@ def _key_hash(d_pts: torch.Tensor, n: int, fields, d_ode: Optional[torch.Tensor]
 REUSE_MAX_BYTES = 16 << 30     # Engine.sweep(reuse=True): z-sum tables beyond this run dense
 
 
-def wave_order(d_pts: torch.Tensor, d_ode: torch.Tensor, n: int):
+def _coop_hash(d_pts: torch.Tensor, d_ode: torch.Tensor, n: int) -> torch.Tensor:
+    """wave_order's key: _native.ODE_COOP_KEY, deplete and Gamma_wash."""
+    return _key_hash(d_pts, n, _native.ODE_COOP_KEY, d_ode, ("deplete_DM_from_source", "Gamma_wash_over_H"))
+
+
+def wave_order(d_pts: torch.Tensor, d_ode: torch.Tensor, n: int, h: Optional[torch.Tensor] = None,
+               breaks: Optional[int] = None):
     """A launch order (int64 permutation tensor, on the points' device) that makes points equal
     in _native.ODE_COOP_KEY, deplete and Gamma_wash contiguous -- and within such a run, points
     equal in the whole ODE_STAGE_KEY (same spline table) -- or None when the input is already
@@ -715,13 +744,16 @@ def wave_order(d_pts: torch.Tensor, d_ode: torch.Tensor, n: int):
     Y_B's step maps and runs the Riccati kernel, a wave that mixes several runs the general variant
     (DESIGN §4.3).  d_pts / d_ode: the lzq_point / lzq_ode_params records as byte tensors.  A
     64-bit hash of the key fields' bits (_key_hash) is sorted stably; a hash collision only puts unequal
-    points in one wavefront, which the kernel detects and runs per lane."""
+    points in one wavefront, which the kernel detects and runs per lane.  h, breaks: _coop_hash
+    and its count of breaks in input order, when the caller has them (Engine.ode)."""
     if n <= 64:
         return None
-    h = _key_hash(d_pts, n, _native.ODE_COOP_KEY, d_ode, ("deplete_DM_from_source", "Gamma_wash_over_H"))
+    if h is None:
+        h = _coop_hash(d_pts, d_ode, n)
     # the key's breaks in input order (none: one key, the common sweep -- no sort needed), then its
     # distinct values (from one sort)
-    breaks = int((h[1:] != h[:-1]).sum())
+    if breaks is None:
+        breaks = int((h[1:] != h[:-1]).sum())
     if breaks == 0:
         return None
     hs = torch.sort(h).values
@@ -795,18 +827,22 @@ _KEY_WORDS = [_native.POINT_DOUBLE_FIELDS.index(f) for f in _native.ODE_TABLE_KE
 _ZSUM_WORDS = [_native.POINT_DOUBLE_FIELDS.index(f) for f in _native.ZSUM_KEY]
 
 
-def table_groups(d_pts: torch.Tensor, n: int, words=None):
+def table_groups(d_pts: torch.Tensor, n: int, words=None, all_same: Optional[bool] = None):
     """Points (device lzq_point records) that can share one ODE spline table: equal, bit for
     bit, in _native.ODE_TABLE_KEY (or in the lzq_point words `words`: _ZSUM_WORDS for the
     quadrature's z-sum tables).  Returns (representative indices, per-point table index),
     both int64 device tensors, or None when sharing would not pay (more than half the points
     distinct).  Index bookkeeping on the device: a 64-bit hash of the key words is deduplicated
     and every point's key is then compared with its representative's, so a hash collision only
-    costs the sharing, never a wrong table."""
+    costs the sharing, never a wrong table.  all_same: the caller already knows whether every
+    point has the first one's key (Engine.ode folds that test into one transfer)."""
     if n < 2:
         return None
+    if all_same:
+        z = torch.zeros(n, dtype=torch.int64, device=d_pts.device)
+        return z[:1], z
     key = d_pts.view(n, _native.POINT_DTYPE.itemsize).view(torch.int64)[:, _KEY_WORDS if words is None else words]
-    if bool((key == key[0]).all()):
+    if all_same is None and bool((key == key[0]).all()):
         z = torch.zeros(n, dtype=torch.int64, device=d_pts.device)
         return z[:1], z
     h = (key * _hash_weights(key.device, key.shape[1])).sum(1)

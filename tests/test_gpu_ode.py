@@ -383,6 +383,12 @@ def test_ode_row_tables_bit_identical(gpu_engine):
     assert torch_equal(sa, se) and torch_equal(a, e)
     with pytest.raises(ValueError):
         gpu_engine.ode(gpu_engine.points_to_device(p), gpu_engine.ode_params_to_device(o[:-1]))
+    # chunks of 128 (tables of chunk c + 1 built on the side stream while chunk c integrates, runs
+    # per chunk), from host and from resident records: the same bits
+    for args in ((p, o), (gpu_engine.points_to_device(p), gpu_engine.ode_params_to_device(o))):
+        f, sf = gpu_engine.ode(*args, chunk=128)
+        assert gpu_engine.last_ode_tables["chunks"] == 4 and gpu_engine.last_ode_tables.get("row_runs", 0) >= 3
+        assert torch_equal(sa, sf) and torch_equal(a, f)
     sel =[int(np.nonzero(perm == j)[0][0]) for j in (0, 250, 340, 480)]
     ref, _ = O.ode_batch([cfgs[perm[i]] for i in sel], nthreads=4)
     for row, rr in zip(a.cpu().numpy()[sel], ref):
